@@ -1,0 +1,229 @@
+/*
+ * mck.h -- C ABI of the MI355X block-checksum engine ("mck" = MI355X
+ * checksum kernels).
+ *
+ * This is the drop-in boundary for Speedb's per-block checksum path.  The
+ * reference has no plugin slot for block checksums (ChecksumType is a closed
+ * enum, include/rocksdb/table.h:69-75); its boundary is a set of internal C++
+ * functions, each of which is replaced below by an extern "C" entry point with
+ * plain pointers and sizes.  INTEGRATION.md shows the reference-side binding.
+ *
+ * Two families:
+ *   1. Scalar, signature-compatible shims (host pointers, synchronous).  The
+ *      u32 algebra (Mask/Unmask/Combine/context modifier) runs on the host;
+ *      every function that reads data bytes runs on the GPU.
+ *   2. Batched device API: many independent spans per call, device-resident
+ *      data, asynchronous on a HIP stream.  This is the hot path.
+ *
+ * Conventions (mirroring the reference):
+ *   - return 0 on success, a negative MCK_E* code on argument/HIP errors; a
+ *     checksum mismatch is data (an output), never an error;
+ *   - the caller owns every buffer; nothing is allocated per call on the
+ *     batched path;
+ *   - reentrant and thread-safe; one engine context per device, created
+ *     lazily on first use of that device;
+ *   - data spans may start at any byte address; device buffers must be
+ *     readable up to the next 16-byte boundary past each span (true of any
+ *     hipMalloc allocation).
+ */
+#ifndef SPEEDB_AMD_MCK_H_
+#define SPEEDB_AMD_MCK_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* A HIP stream (hipStream_t); NULL = the device's default stream. */
+typedef struct ihipStream_t* mck_stream_t;
+
+/* ---- error codes --------------------------------------------------------- */
+#define MCK_OK 0
+#define MCK_EINVAL (-1)   /* bad argument (NULL pointer, bad type, ...)     */
+#define MCK_EHIP (-2)     /* a HIP runtime call failed; see mck_last_error */
+#define MCK_ENODEV (-3)   /* no usable gfx950 device / device index       */
+#define MCK_ENOMEM (-4)   /* staging allocation failed                    */
+
+/* ---- checksum types: include/rocksdb/table.h:69-75 ChecksumType ---------- */
+#define MCK_kNoChecksum 0
+#define MCK_kCRC32c 1
+#define MCK_kxxHash 2
+#define MCK_kxxHash64 3
+#define MCK_kXXH3 4
+
+/* ---- WAL record types: db/log_format.h:22-45 ----------------------------- */
+#define MCK_WAL_kBlockSize 32768
+#define MCK_WAL_kHeaderSize 7
+#define MCK_WAL_kRecyclableHeaderSize 11
+
+/* Message of the last error on this thread ("" if none). */
+const char* mck_last_error(void);
+/* Engine version string. */
+const char* mck_version(void);
+/* Number of usable gfx950 devices (0 if none). */
+int mck_device_count(void);
+
+/* ========================================================================= */
+/* 1. Scalar shims                                                          */
+/* ========================================================================= */
+
+/* util/crc32c.h:44 Mask / :50 Unmask (host, pure u32 algebra) */
+uint32_t mck_crc32c_mask(uint32_t crc);
+uint32_t mck_crc32c_unmask(uint32_t masked_crc);
+/* util/crc32c.h:31 / util/crc32c.cc:1274 Crc32cCombine (host, O(log n)) */
+uint32_t mck_crc32c_combine(uint32_t crc1, uint32_t crc2, size_t crc2len);
+/* table/format.h:119 ChecksumModifierForContext (host) */
+uint32_t mck_context_modifier(uint32_t base_context_checksum, uint64_t offset);
+
+/* Data-reading shims.  Host pointers, synchronous; the bytes are staged to
+ * the calling thread's current device and hashed there.  They exist so that
+ * every reference call site can be re-pointed without a batching rewrite;
+ * batch-aware callers use family 2.  On error they return 0 and set
+ * mck_last_error(). */
+/* util/crc32c.h:26 Extend, :35 Value */
+uint32_t mck_crc32c_extend(uint32_t init_crc, const void* data, size_t n);
+uint32_t mck_crc32c_value(const void* data, size_t n);
+/* util/xxhash.h:5329 XXH3_64bits */
+uint64_t mck_xxh3_64(const void* data, size_t n);
+/* table/format.cc:578 ComputeBuiltinChecksum */
+uint32_t mck_builtin_checksum(int type, const void* data, size_t n);
+/* table/format.cc:604 ComputeBuiltinChecksumWithLastByte */
+uint32_t mck_builtin_checksum_with_last_byte(int type, const void* data,
+                                             size_t n, char last_byte);
+
+/* ========================================================================= */
+/* 2. Batched device API                                                    */
+/* ========================================================================= */
+
+/* A batch of independent byte spans in device memory.
+ *   span i = [base + off_i, base + off_i + len_i)
+ *   off_i  = offsets ? offsets[i] : i * stride
+ *   len_i  = lengths ? lengths[i] : length
+ * offsets/lengths, when given, are device arrays of `count` entries. */
+typedef struct mck_spans {
+  const void* base;
+  const uint64_t* offsets;
+  const uint32_t* lengths;
+  uint64_t stride;
+  uint32_t length;
+  uint32_t count;
+} mck_spans;
+
+/* flags for mck_crc32c_batch */
+#define MCK_F_MASK 1u /* store crc32c::Mask(crc) instead of crc */
+
+/* out[i] = Extend(init_crcs ? init_crcs[i] : 0, span i)   (util/crc32c.h:26)
+ * optionally masked.  out: device array [count]. */
+int mck_crc32c_batch(const mck_spans* spans, const uint32_t* init_crcs,
+                     uint32_t flags, uint32_t* out, mck_stream_t stream);
+
+/* out[i] = XXH3_64bits(span i)   (util/xxhash.h:5329) */
+int mck_xxh3_64_batch(const mck_spans* spans, uint64_t* out,
+                      mck_stream_t stream);
+
+/* out[i] = XXH32(span i, seed) / XXH64(span i, seed)  (legacy kxxHash /
+ * kxxHash64 block checksums) */
+int mck_xxh32_batch(const mck_spans* spans, uint32_t seed, uint32_t* out,
+                    mck_stream_t stream);
+int mck_xxh64_batch(const mck_spans* spans, uint64_t seed, uint64_t* out,
+                    mck_stream_t stream);
+
+/* out[i] = ComputeBuiltinChecksum(type, span i)                 if !last_bytes
+ *        = ComputeBuiltinChecksumWithLastByte(type, span i, last_bytes[i])
+ * (table/format.cc:578-645).  last_bytes: device array [count] or NULL. */
+int mck_builtin_checksum_batch(int type, const mck_spans* spans,
+                               const uint8_t* last_bytes, uint32_t* out,
+                               mck_stream_t stream);
+
+/* Write side of the SST trailer (table/block_based/block_based_table_builder.cc
+ * :1333-1348): for every block payload span,
+ *   out[i] = ComputeBuiltinChecksumWithLastByte(type, payload_i, comp_types[i])
+ *            + ChecksumModifierForContext(base_context_checksum, file_off_i)
+ * file_off_i = file_offsets ? file_offsets[i] : spans->offsets[i] (or
+ * i*stride).  The caller writes [comp_type][LE32 out[i]] after the payload. */
+int mck_sst_trailer_batch(int type, const mck_spans* payloads,
+                          const uint8_t* comp_types,
+                          const uint64_t* file_offsets,
+                          uint32_t base_context_checksum, uint32_t* out,
+                          mck_stream_t stream);
+
+/* Read side (table/block_based/reader_common.cc:26 VerifyBlockChecksum):
+ * every span is a block payload of len_i bytes followed in memory by its
+ * 5-byte trailer [type][LE32 stored].  For block i:
+ *   computed = ComputeBuiltinChecksum(type, payload_i || type_byte)
+ *   stored   = LE32 - ChecksumModifierForContext(base, file_off_i)
+ *   mismatch[i] = stored != computed
+ * Outputs (device arrays, each optional except mismatch):
+ *   mismatch[count] (uint8 0/1), computed[count], stored[count],
+ *   mismatch_count (one uint32, atomically incremented per mismatch; the
+ *   caller zeroes it). */
+int mck_sst_verify_batch(int type, const mck_spans* payloads,
+                         const uint64_t* file_offsets,
+                         uint32_t base_context_checksum, uint8_t* mismatch,
+                         uint32_t* computed, uint32_t* stored,
+                         uint32_t* mismatch_count, mck_stream_t stream);
+
+/* WAL record CRC, write side (db/log_writer.cc:263-311 EmitPhysicalRecord):
+ * out[i] = Mask(crc of [type_i][LE32 log_number if recyclable][payload_i]).
+ * types: device array [count].  recyclable = record type is 5..8 or 11. */
+int mck_wal_record_crc_batch(const mck_spans* payloads, const uint8_t* types,
+                             uint32_t log_number, uint32_t* out,
+                             mck_stream_t stream);
+
+/* Per-32KiB-block result of a WAL verify scan (db/log_reader.cc:450-584
+ * ReadPhysicalRecord, checksum on).  Records of block b are walked in order;
+ * the walk stops at the first record that the reference would not return. */
+typedef struct mck_wal_block_result {
+  uint32_t records_ok;   /* physical records that verified before the stop */
+  int32_t status;        /* MCK_WAL_OK or the MCK_WAL_* reason for the stop */
+  uint32_t stop_offset;  /* byte offset within the block of the stopping
+                            record's header (block size if none)           */
+  uint32_t bytes_ok;     /* header+payload bytes of the verified records   */
+} mck_wal_block_result;
+
+#define MCK_WAL_OK 0
+#define MCK_WAL_BAD_CHECKSUM 1   /* kBadRecordChecksum: drop rest of block */
+#define MCK_WAL_BAD_LENGTH 2     /* kBadRecordLen: header+length > block   */
+#define MCK_WAL_ZERO_RECORD 3    /* kZeroType with length 0 (kBadRecord)  */
+#define MCK_WAL_OLD_RECORD 4     /* recyclable record of another log      */
+#define MCK_WAL_BAD_HEADER 5     /* truncated header at end of input      */
+
+/* Verify every physical record of a WAL image of `nbytes` bytes (device
+ * memory, starting at a 32 KiB block boundary; the last block may be
+ * short).  results: device array [ceil(nbytes / 32768)]. */
+int mck_wal_verify_batch(const void* wal, uint64_t nbytes,
+                         uint32_t log_number, mck_wal_block_result* results,
+                         mck_stream_t stream);
+
+/* ========================================================================= */
+/* 3. Multi-GPU / host-resident input                                       */
+/* ========================================================================= */
+
+/* Split `count` spans with the given host-side lengths into `parts`
+ * contiguous ranges of near-equal byte totals: range p = [first[p],
+ * first[p+1]).  first: host array [parts + 1]. */
+int mck_partition_spans(const uint32_t* host_lengths, uint32_t count,
+                        uint32_t length, int parts, uint32_t* first);
+
+/* Host-resident batch: spans live in host memory (pinned or pageable; pinned
+ * gives full PCIe rate).  The batch is partitioned by bytes across devices
+ * [0, ndev) and streamed through each device in double-buffered chunks of
+ * `chunk_bytes` (H2D copy of chunk k+1 overlaps the kernel on chunk k); the
+ * per-span results come back to host memory.
+ * kind: MCK_kCRC32c (out32 = Value, masked if flags & MCK_F_MASK) or
+ *       MCK_kXXH3 (out64 = XXH3_64bits).
+ * host_offsets / host_lengths: host arrays (NULL => uniform as in mck_spans).
+ * Returns 0 on success.  *seconds (optional) = wall time of the call. */
+int mck_host_batch_checksum(int kind, const void* host_base,
+                            const uint64_t* host_offsets,
+                            const uint32_t* host_lengths, uint64_t stride,
+                            uint32_t length, uint32_t count, uint32_t flags,
+                            int ndev, size_t chunk_bytes, uint32_t* out32,
+                            uint64_t* out64, double* seconds);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SPEEDB_AMD_MCK_H_ */

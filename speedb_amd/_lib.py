@@ -1,0 +1,100 @@
+"""ctypes binding of the engine's C ABI (include/speedb_amd/mck.h).
+
+The shared library ``speedb_amd/libspeedb_amd.so`` is built in-tree by
+``__graft_entry__.build()`` (hipcc, gfx950).  There is no CPU fallback: if the
+library is missing, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libspeedb_amd.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"speedb_amd: native engine {LIB_PATH} is missing; run "
+        "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950). "
+        "There is no CPU fallback.")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+vp = ctypes.c_void_p
+
+
+class mck_spans(ctypes.Structure):
+    _fields_ = [
+        ("base", vp),
+        ("offsets", vp),
+        ("lengths", vp),
+        ("stride", ctypes.c_uint64),
+        ("length", ctypes.c_uint32),
+        ("count", ctypes.c_uint32),
+    ]
+
+
+class mck_wal_block_result(ctypes.Structure):
+    _fields_ = [
+        ("records_ok", ctypes.c_uint32),
+        ("status", ctypes.c_int32),
+        ("stop_offset", ctypes.c_uint32),
+        ("bytes_ok", ctypes.c_uint32),
+    ]
+
+
+# (name, restype, argtypes) for every symbol declared in mck.h
+SIGNATURES = [
+    ("mck_last_error", ctypes.c_char_p, []),
+    ("mck_version", ctypes.c_char_p, []),
+    ("mck_device_count", ctypes.c_int, []),
+    ("mck_crc32c_mask", ctypes.c_uint32, [ctypes.c_uint32]),
+    ("mck_crc32c_unmask", ctypes.c_uint32, [ctypes.c_uint32]),
+    ("mck_crc32c_combine", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_size_t]),
+    ("mck_context_modifier", ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64]),
+    ("mck_crc32c_extend", ctypes.c_uint32, [ctypes.c_uint32, vp, ctypes.c_size_t]),
+    ("mck_crc32c_value", ctypes.c_uint32, [vp, ctypes.c_size_t]),
+    ("mck_xxh3_64", ctypes.c_uint64, [vp, ctypes.c_size_t]),
+    ("mck_builtin_checksum", ctypes.c_uint32, [ctypes.c_int, vp, ctypes.c_size_t]),
+    ("mck_builtin_checksum_with_last_byte", ctypes.c_uint32,
+     [ctypes.c_int, vp, ctypes.c_size_t, ctypes.c_char]),
+    ("mck_crc32c_batch", ctypes.c_int,
+     [ctypes.POINTER(mck_spans), vp, ctypes.c_uint32, vp, vp]),
+    ("mck_xxh3_64_batch", ctypes.c_int, [ctypes.POINTER(mck_spans), vp, vp]),
+    ("mck_xxh32_batch", ctypes.c_int, [ctypes.POINTER(mck_spans), ctypes.c_uint32, vp, vp]),
+    ("mck_xxh64_batch", ctypes.c_int, [ctypes.POINTER(mck_spans), ctypes.c_uint64, vp, vp]),
+    ("mck_builtin_checksum_batch", ctypes.c_int,
+     [ctypes.c_int, ctypes.POINTER(mck_spans), vp, vp, vp]),
+    ("mck_sst_trailer_batch", ctypes.c_int,
+     [ctypes.c_int, ctypes.POINTER(mck_spans), vp, vp, ctypes.c_uint32, vp, vp]),
+    ("mck_sst_verify_batch", ctypes.c_int,
+     [ctypes.c_int, ctypes.POINTER(mck_spans), vp, ctypes.c_uint32, vp, vp, vp, vp, vp]),
+    ("mck_wal_record_crc_batch", ctypes.c_int,
+     [ctypes.POINTER(mck_spans), vp, ctypes.c_uint32, vp, vp]),
+    ("mck_wal_verify_batch", ctypes.c_int,
+     [vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp]),
+    ("mck_partition_spans", ctypes.c_int,
+     [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp]),
+    ("mck_host_batch_checksum", ctypes.c_int,
+     [ctypes.c_int, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+      ctypes.c_uint32, ctypes.c_int, ctypes.c_size_t, vp, vp,
+      ctypes.POINTER(ctypes.c_double)]),
+]
+
+for _name, _res, _args in SIGNATURES:
+    _f = getattr(lib, _name)
+    _f.restype = _res
+    _f.argtypes = _args
+
+
+class MckError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib.mck_last_error().decode(errors="replace")
+        raise MckError(f"{what} failed (rc={rc}): {msg}")

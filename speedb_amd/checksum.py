@@ -1,0 +1,345 @@
+"""Host-side mirror of the reference's block-checksum interface, over the
+engine's C ABI.
+
+Names, argument meaning and error behaviour follow the reference:
+
+* ``crc32c.Value / Extend / Mask / Unmask / Crc32cCombine``  -- util/crc32c.h:21-53
+* ``XXH3_64bits``                                            -- util/xxhash.h:5329
+* ``ChecksumType``                                           -- include/rocksdb/table.h:69-75
+* ``ComputeBuiltinChecksum[WithLastByte]``                   -- table/format.cc:578-645
+* ``ChecksumModifierForContext``                             -- table/format.h:119-146
+* ``VerifyBlockChecksum`` (returns a ``Status``)             -- table/block_based/reader_common.cc:26-63
+
+Scalar functions take host ``bytes`` and hash them on the GPU (synchronous);
+the ``*_batch`` functions take device-resident torch tensors and run
+asynchronously on the current HIP stream.  The u32 algebra (Mask, Unmask,
+Combine, context modifier) runs on the host, as in the reference.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from dataclasses import dataclass
+from typing import Optional
+
+from ._lib import check, lib, mck_spans, mck_wal_block_result
+
+# ---------------------------------------------------------------------------
+# enums / status
+# ---------------------------------------------------------------------------
+
+
+class ChecksumType(enum.IntEnum):
+    """include/rocksdb/table.h:69-75"""
+    kNoChecksum = 0
+    kCRC32c = 1
+    kxxHash = 2
+    kxxHash64 = 3
+    kXXH3 = 4
+
+
+class WalStatus(enum.IntEnum):
+    """Why a WAL block walk stopped (db/log_reader.h ReadPhysicalRecord codes)."""
+    kOk = 0
+    kBadRecordChecksum = 1
+    kBadRecordLen = 2
+    kBadRecord = 3        # kZeroType with length 0
+    kOldRecord = 4
+    kBadHeader = 5
+
+
+@dataclass(frozen=True)
+class Status:
+    """The slice of rocksdb::Status the checksum path produces."""
+    code: str = "OK"
+    message: str = ""
+
+    def ok(self) -> bool:
+        return self.code == "OK"
+
+    def IsCorruption(self) -> bool:
+        return self.code == "Corruption"
+
+    def ToString(self) -> str:
+        return "OK" if self.ok() else f"{self.code}: {self.message}"
+
+    @staticmethod
+    def OK() -> "Status":
+        return Status()
+
+    @staticmethod
+    def Corruption(msg: str) -> "Status":
+        return Status("Corruption", msg)
+
+
+@dataclass(frozen=True)
+class Footer:
+    """The two footer fields VerifyBlockChecksum reads (table/format.h)."""
+    checksum_type: ChecksumType = ChecksumType.kXXH3
+    base_context_checksum: int = 0
+
+
+def _buf(data):
+    if isinstance(data, str):
+        data = data.encode()
+    b = bytes(data)
+    return b, len(b)
+
+
+def _err():
+    return lib.mck_last_error().decode(errors="replace")
+
+
+def _checked(v):
+    e = _err()
+    if e:
+        raise RuntimeError(f"speedb_amd: {e}")
+    return v
+
+
+# ---------------------------------------------------------------------------
+# scalar API (util/crc32c.h, util/xxhash.h, table/format.cc)
+# ---------------------------------------------------------------------------
+
+
+class crc32c:  # noqa: N801 -- mirrors the reference's namespace
+    kMaskDelta = 0xA282EAD8
+
+    @staticmethod
+    def Extend(init_crc: int, data) -> int:
+        b, n = _buf(data)
+        return _checked(lib.mck_crc32c_extend(init_crc & 0xFFFFFFFF, b, n))
+
+    @staticmethod
+    def Value(data) -> int:
+        b, n = _buf(data)
+        return _checked(lib.mck_crc32c_value(b, n))
+
+    @staticmethod
+    def Mask(crc: int) -> int:
+        return lib.mck_crc32c_mask(crc & 0xFFFFFFFF)
+
+    @staticmethod
+    def Unmask(masked_crc: int) -> int:
+        return lib.mck_crc32c_unmask(masked_crc & 0xFFFFFFFF)
+
+    @staticmethod
+    def Crc32cCombine(crc1: int, crc2: int, crc2len: int) -> int:
+        return lib.mck_crc32c_combine(crc1 & 0xFFFFFFFF, crc2 & 0xFFFFFFFF, crc2len)
+
+
+def XXH3_64bits(data) -> int:
+    b, n = _buf(data)
+    return _checked(lib.mck_xxh3_64(b, n))
+
+
+def ComputeBuiltinChecksum(checksum_type: int, data) -> int:
+    b, n = _buf(data)
+    return _checked(lib.mck_builtin_checksum(int(checksum_type), b, n))
+
+
+def ComputeBuiltinChecksumWithLastByte(checksum_type: int, data, last_byte) -> int:
+    b, n = _buf(data)
+    if isinstance(last_byte, int):
+        last_byte = bytes([last_byte & 0xFF])
+    return _checked(lib.mck_builtin_checksum_with_last_byte(int(checksum_type), b, n, last_byte))
+
+
+def ChecksumModifierForContext(base_context_checksum: int, offset: int) -> int:
+    return lib.mck_context_modifier(base_context_checksum & 0xFFFFFFFF, offset)
+
+
+def _decode_fixed32(b: bytes, pos: int) -> int:
+    return int.from_bytes(b[pos:pos + 4], "little")
+
+
+def VerifyBlockChecksum(footer: Footer, data, block_size: int, file_name: str,
+                        offset: int) -> Status:
+    """table/block_based/reader_common.cc:26-63.  ``data`` holds the block
+    payload followed by its 5-byte trailer."""
+    b, _ = _buf(data)
+    ctype = ChecksumType(footer.checksum_type)
+    length = block_size + 1
+    stored = _decode_fixed32(b, length)
+    computed = ComputeBuiltinChecksum(ctype, b[:length])
+    modifier = ChecksumModifierForContext(footer.base_context_checksum, offset)
+    stored = (stored - modifier) & 0xFFFFFFFF
+    if stored == computed:
+        return Status.OK()
+    if ctype == ChecksumType.kCRC32c:
+        stored = crc32c.Unmask(stored)
+        computed = crc32c.Unmask(computed)
+    return Status.Corruption(
+        "block checksum mismatch: stored" + ("(context removed)" if modifier else "") +
+        f" = {stored}, computed = {computed}, type = {int(ctype)}  in {file_name} "
+        f"offset {offset} size {block_size}")
+
+
+# ---------------------------------------------------------------------------
+# batched device API (torch tensors on the GPU)
+# ---------------------------------------------------------------------------
+
+def _torch():
+    import torch
+    return torch
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream) -> Optional[int]:
+    torch = _torch()
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return stream.cuda_stream
+
+
+@dataclass
+class Spans:
+    """mck_spans over a device byte tensor.  span i = base[off_i : off_i+len_i]
+    with off_i = offsets[i] (int64 tensor) or i*stride and len_i = lengths[i]
+    (int32 tensor) or ``length``."""
+    base: object
+    count: int
+    offsets: object = None
+    lengths: object = None
+    stride: int = 0
+    length: int = 0
+
+    def c(self) -> mck_spans:
+        for t in (self.offsets, self.lengths):
+            if t is not None and not t.is_contiguous():
+                raise ValueError("offsets/lengths must be contiguous")
+        return mck_spans(self.base.data_ptr(), _ptr(self.offsets), _ptr(self.lengths),
+                         self.stride, self.length, self.count)
+
+    @staticmethod
+    def uniform(base, block: int, count: Optional[int] = None) -> "Spans":
+        if count is None:
+            count = base.numel() // block
+        return Spans(base, count, stride=block, length=block)
+
+
+def _empty(count, dtype, device):
+    return _torch().empty(count, dtype=dtype, device=device)
+
+
+def crc32c_batch(spans: Spans, init_crcs=None, mask: bool = False, out=None, stream=None):
+    """out[i] = crc32c::Extend(init_crcs[i] or 0, span i) (Mask()ed if mask).
+    Returns an int32 tensor holding the u32 bit patterns."""
+    torch = _torch()
+    if out is None:
+        out = _empty(spans.count, torch.int32, spans.base.device)
+    s = spans.c()
+    check(lib.mck_crc32c_batch(ctypes.byref(s), _ptr(init_crcs), 1 if mask else 0,
+                               out.data_ptr(), _stream(stream)), "mck_crc32c_batch")
+    return out
+
+
+def xxh3_64_batch(spans: Spans, out=None, stream=None):
+    torch = _torch()
+    if out is None:
+        out = _empty(spans.count, torch.int64, spans.base.device)
+    s = spans.c()
+    check(lib.mck_xxh3_64_batch(ctypes.byref(s), out.data_ptr(), _stream(stream)),
+          "mck_xxh3_64_batch")
+    return out
+
+
+def xxh32_batch(spans: Spans, seed: int = 0, out=None, stream=None):
+    torch = _torch()
+    if out is None:
+        out = _empty(spans.count, torch.int32, spans.base.device)
+    s = spans.c()
+    check(lib.mck_xxh32_batch(ctypes.byref(s), seed, out.data_ptr(), _stream(stream)),
+          "mck_xxh32_batch")
+    return out
+
+
+def xxh64_batch(spans: Spans, seed: int = 0, out=None, stream=None):
+    torch = _torch()
+    if out is None:
+        out = _empty(spans.count, torch.int64, spans.base.device)
+    s = spans.c()
+    check(lib.mck_xxh64_batch(ctypes.byref(s), seed, out.data_ptr(), _stream(stream)),
+          "mck_xxh64_batch")
+    return out
+
+
+def builtin_checksum_batch(checksum_type: int, spans: Spans, last_bytes=None, out=None,
+                           stream=None):
+    torch = _torch()
+    if out is None:
+        out = _empty(spans.count, torch.int32, spans.base.device)
+    s = spans.c()
+    check(lib.mck_builtin_checksum_batch(int(checksum_type), ctypes.byref(s), _ptr(last_bytes),
+                                         out.data_ptr(), _stream(stream)),
+          "mck_builtin_checksum_batch")
+    return out
+
+
+def sst_trailer_batch(checksum_type: int, payloads: Spans, comp_types, file_offsets=None,
+                      base_context_checksum: int = 0, out=None, stream=None):
+    torch = _torch()
+    if out is None:
+        out = _empty(payloads.count, torch.int32, payloads.base.device)
+    s = payloads.c()
+    check(lib.mck_sst_trailer_batch(int(checksum_type), ctypes.byref(s), _ptr(comp_types),
+                                    _ptr(file_offsets), base_context_checksum & 0xFFFFFFFF,
+                                    out.data_ptr(), _stream(stream)), "mck_sst_trailer_batch")
+    return out
+
+
+def sst_verify_batch(checksum_type: int, payloads: Spans, file_offsets=None,
+                     base_context_checksum: int = 0, stream=None):
+    """Returns (mismatch uint8, computed int32, stored int32, mismatch_count int32[1])."""
+    torch = _torch()
+    dev = payloads.base.device
+    mismatch = _empty(payloads.count, torch.uint8, dev)
+    computed = _empty(payloads.count, torch.int32, dev)
+    stored = _empty(payloads.count, torch.int32, dev)
+    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = payloads.c()
+    check(lib.mck_sst_verify_batch(int(checksum_type), ctypes.byref(s), _ptr(file_offsets),
+                                   base_context_checksum & 0xFFFFFFFF, mismatch.data_ptr(),
+                                   computed.data_ptr(), stored.data_ptr(), count.data_ptr(),
+                                   _stream(stream)), "mck_sst_verify_batch")
+    return mismatch, computed, stored, count
+
+
+def wal_record_crc_batch(payloads: Spans, types, log_number: int = 0, out=None, stream=None):
+    torch = _torch()
+    if out is None:
+        out = _empty(payloads.count, torch.int32, payloads.base.device)
+    s = payloads.c()
+    check(lib.mck_wal_record_crc_batch(ctypes.byref(s), types.data_ptr(), log_number & 0xFFFFFFFF,
+                                       out.data_ptr(), _stream(stream)),
+          "mck_wal_record_crc_batch")
+    return out
+
+
+def wal_verify_batch(wal, nbytes: Optional[int] = None, log_number: int = 0, stream=None):
+    """Returns an int32 tensor [nblocks, 4]: records_ok, status, stop_offset, bytes_ok."""
+    torch = _torch()
+    if nbytes is None:
+        nbytes = wal.numel()
+    nblocks = (nbytes + 32767) // 32768
+    res = torch.empty((nblocks, 4), dtype=torch.int32, device=wal.device)
+    check(lib.mck_wal_verify_batch(wal.data_ptr(), nbytes, log_number & 0xFFFFFFFF,
+                                   res.data_ptr(), _stream(stream)), "mck_wal_verify_batch")
+    return res
+
+
+def device_count() -> int:
+    return lib.mck_device_count()
+
+
+__all__ = [
+    "ChecksumType", "WalStatus", "Status", "Footer", "crc32c", "XXH3_64bits",
+    "ComputeBuiltinChecksum", "ComputeBuiltinChecksumWithLastByte",
+    "ChecksumModifierForContext", "VerifyBlockChecksum", "Spans", "crc32c_batch",
+    "xxh3_64_batch", "xxh32_batch", "xxh64_batch", "builtin_checksum_batch",
+    "sst_trailer_batch", "sst_verify_batch", "wal_record_crc_batch", "wal_verify_batch",
+    "device_count", "mck_wal_block_result",
+]

@@ -1,0 +1,648 @@
+// mck_engine.hip -- C ABI of the MI355X block-checksum engine: per-device
+// context, launch geometry, the batched device entry points, the scalar
+// shims and the host-resident multi-GPU pipeline.  See include/speedb_amd/
+// mck.h for the contract of every function.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "../../include/speedb_amd/mck.h"
+#include "mck_kernels.hpp"
+
+namespace mck {
+
+__device__ CrcTables g_crc_tables;
+
+namespace {
+
+thread_local char t_err[512] = "";
+
+void set_err(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(t_err, sizeof t_err, fmt, ap);
+  va_end(ap);
+}
+
+#define MCK_HIP(call)                                                                \
+  do {                                                                               \
+    hipError_t e_ = (call);                                                          \
+    if (e_ != hipSuccess) {                                                          \
+      set_err("%s failed: %s (%s:%d)", #call, hipGetErrorString(e_), __FILE__, __LINE__); \
+      return MCK_EHIP;                                                               \
+    }                                                                                \
+  } while (0)
+
+constexpr int kMaxDev = 64;
+
+struct DevCtx {
+  std::once_flag once;
+  int status = MCK_ENODEV;
+  int ncu = 0;
+};
+DevCtx g_dev[kMaxDev];
+
+const CrcTables& host_tables() {
+  static CrcTables* t = [] {
+    CrcTables* x = new CrcTables;
+    build_crc_tables(x);
+    return x;
+  }();
+  return *t;
+}
+
+// Set the dynamic-LDS limit of a CRC kernel instantiation (once per device).
+template <class K>
+int ensure_lds(K kern, int dev) {
+  static std::atomic<uint64_t> done{0};
+  const uint64_t bit = 1ull << dev;
+  if (done.load(std::memory_order_acquire) & bit) return MCK_OK;
+  MCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)kCrcLdsBytes));
+  done.fetch_or(bit, std::memory_order_acq_rel);
+  return MCK_OK;
+}
+
+// Initialise the current device: check it is gfx950 and upload the tables.
+int current_device(int* dev_out, int* ncu_out) {
+  int dev = 0;
+  MCK_HIP(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDev) {
+    set_err("device index %d out of range", dev);
+    return MCK_ENODEV;
+  }
+  DevCtx& d = g_dev[dev];
+  std::call_once(d.once, [&] {
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+      d.status = MCK_EHIP;
+      return;
+    }
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+      set_err("device %d is %s; this engine is built for gfx950 only", dev, prop.gcnArchName);
+      d.status = MCK_ENODEV;
+      return;
+    }
+    d.ncu = prop.multiProcessorCount;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_crc_tables), &host_tables(), sizeof(CrcTables)) != hipSuccess ||
+        hipDeviceSynchronize() != hipSuccess) {
+      d.status = MCK_EHIP;
+      return;
+    }
+    d.status = MCK_OK;
+  });
+  if (d.status != MCK_OK) {
+    if (!t_err[0]) set_err("device %d initialisation failed", dev);
+    return d.status;
+  }
+  if (dev_out) *dev_out = dev;
+  if (ncu_out) *ncu_out = d.ncu;
+  return MCK_OK;
+}
+
+int check_spans(const mck_spans* s) {
+  if (!s) {
+    set_err("spans is NULL");
+    return MCK_EINVAL;
+  }
+  if (s->count && !s->base) {
+    set_err("spans->base is NULL");
+    return MCK_EINVAL;
+  }
+  return MCK_OK;
+}
+
+SpanSrc to_src(const mck_spans* s) {
+  return SpanSrc{static_cast<const uint8_t*>(s->base), s->offsets, s->lengths, s->stride, s->length};
+}
+
+// ---- launchers -------------------------------------------------------------
+template <class Op>
+int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
+  if (!count) return MCK_OK;
+  int dev, ncu;
+  int rc = current_device(&dev, &ncu);
+  if (rc) return rc;
+  rc = ensure_lds(k_crc<Op>, dev);
+  if (rc) return rc;
+  // persistent: one 16-wave workgroup per CU (105 KiB of LDS each)
+  const uint32_t grid = std::min<uint32_t>(ncu, (count + 15) / 16);
+  hipLaunchKernelGGL(k_crc<Op>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, count);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+template <class Op>
+int launch_xxh3(const Op& op, uint32_t count, hipStream_t st) {
+  if (!count) return MCK_OK;
+  int ncu;
+  int rc = current_device(nullptr, &ncu);
+  if (rc) return rc;
+  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 3) / 4);
+  hipLaunchKernelGGL(k_xxh3<Op>, dim3(grid), dim3(256), 0, st, op, count);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+template <class Op>
+int launch_legacy(const Op& op, uint32_t count, hipStream_t st) {
+  if (!count) return MCK_OK;
+  int ncu;
+  int rc = current_device(nullptr, &ncu);
+  if (rc) return rc;
+  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 255) / 256);
+  hipLaunchKernelGGL(k_legacy<Op>, dim3(grid), dim3(256), 0, st, op, count);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+template <int MODE>
+int launch_block(int type, const BlockArgs& a, uint32_t count, hipStream_t st) {
+  switch (type) {
+    case MCK_kCRC32c:
+      return launch_crc(OpCrcBlock<MODE>{a}, count, st);
+    case MCK_kXXH3:
+      return launch_xxh3(OpX3Block<MODE>{a}, count, st);
+    case MCK_kxxHash:
+      return launch_legacy(OpLegacyBlock<false, MODE>{a}, count, st);
+    case MCK_kxxHash64:
+      return launch_legacy(OpLegacyBlock<true, MODE>{a}, count, st);
+    case MCK_kNoChecksum:
+      return launch_legacy(OpNoneBlock<MODE>{a}, count, st);
+    default:
+      set_err("unknown checksum type %d", type);
+      return MCK_EINVAL;
+  }
+}
+
+// Value(type byte [+ LE32 log number]) for every record type, db/log_writer.cc
+// :48-51 (type_crc_) and :281-291 (recyclable log number).
+WalTypeCrcs wal_type_crcs(uint32_t log_number) {
+  WalTypeCrcs t;
+  for (int ty = 0; ty < 16; ty++) {
+    uint32_t s = ~0u;
+    auto feed = [&](uint8_t b) {
+      s ^= b;
+      for (int k = 0; k < 8; k++) s = gf_mulx(s);
+    };
+    feed((uint8_t)ty);
+    const bool recyclable = (ty >= 5 && ty <= 8) || ty == 11;
+    if (recyclable)
+      for (int k = 0; k < 4; k++) feed((uint8_t)(log_number >> (8 * k)));
+    t.v[ty] = ~s;
+  }
+  return t;
+}
+
+// ---- per-thread staging for the synchronous scalar shims ------------------
+struct Staging {
+  int dev = -1;
+  void* d_buf = nullptr;
+  size_t cap = 0;
+  ~Staging() {
+    if (d_buf) (void)hipFree(d_buf);
+  }
+};
+thread_local Staging t_stage;
+
+int stage_in(const void* data, size_t n, uint8_t** d_data, void** d_out) {
+  int dev;
+  int rc = current_device(&dev, nullptr);
+  if (rc) return rc;
+  const size_t need = 64 + ((n + 64 + 255) & ~size_t(255));
+  if (t_stage.dev != dev || t_stage.cap < need) {
+    if (t_stage.d_buf) (void)hipFree(t_stage.d_buf);
+    t_stage.d_buf = nullptr;
+    t_stage.cap = 0;
+    const size_t cap = std::max<size_t>(need, 1 << 20);
+    MCK_HIP(hipMalloc(&t_stage.d_buf, cap));
+    t_stage.cap = cap;
+    t_stage.dev = dev;
+  }
+  *d_out = t_stage.d_buf;  // 64 bytes of results
+  *d_data = static_cast<uint8_t*>(t_stage.d_buf) + 64;
+  if (n) MCK_HIP(hipMemcpy(*d_data, data, n, hipMemcpyHostToDevice));
+  return MCK_OK;
+}
+
+}  // namespace
+}  // namespace mck
+
+using namespace mck;
+
+// ============================================================================
+extern "C" {
+
+const char* mck_last_error(void) { return t_err; }
+const char* mck_version(void) { return "speedb_amd mck 0.1 (gfx950)"; }
+
+int mck_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  int good = 0;
+  for (int i = 0; i < n; i++) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, i) == hipSuccess && strncmp(p.gcnArchName, "gfx950", 6) == 0) good++;
+  }
+  return good;
+}
+
+// ---- scalar u32 algebra (host) ------------------------------------------
+uint32_t mck_crc32c_mask(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + 0xa282ead8u; }
+uint32_t mck_crc32c_unmask(uint32_t m) {
+  const uint32_t rot = m - 0xa282ead8u;
+  return (rot >> 17) | (rot << 15);
+}
+// Value(A||B) = zshift(Value(A), |B|) ^ Value(B): util/crc32c.cc:1221-1289
+uint32_t mck_crc32c_combine(uint32_t crc1, uint32_t crc2, size_t crc2len) {
+  return gf_zshift(crc1, crc2len) ^ crc2;
+}
+uint32_t mck_context_modifier(uint32_t base, uint64_t offset) {
+  const uint32_t all_or_nothing = 0u - (uint32_t)(base != 0);
+  return (base ^ ((uint32_t)offset + (uint32_t)(offset >> 32))) & all_or_nothing;
+}
+
+// ---- batched device API ----------------------------------------------------
+int mck_crc32c_batch(const mck_spans* spans, const uint32_t* init_crcs, uint32_t flags, uint32_t* out,
+                     mck_stream_t stream) {
+  t_err[0] = 0;
+  if (int rc = check_spans(spans)) return rc;
+  if (spans->count && !out) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  return launch_crc(OpCrcValue{to_src(spans), init_crcs, flags & MCK_F_MASK, out}, spans->count,
+                    reinterpret_cast<hipStream_t>(stream));
+}
+
+int mck_xxh3_64_batch(const mck_spans* spans, uint64_t* out, mck_stream_t stream) {
+  t_err[0] = 0;
+  if (int rc = check_spans(spans)) return rc;
+  if (spans->count && !out) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  return launch_xxh3(OpX3Value{to_src(spans), out}, spans->count, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mck_xxh32_batch(const mck_spans* spans, uint32_t seed, uint32_t* out, mck_stream_t stream) {
+  t_err[0] = 0;
+  if (int rc = check_spans(spans)) return rc;
+  if (spans->count && !out) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  return launch_legacy(OpLegacyValue<false>{to_src(spans), seed, out}, spans->count,
+                       reinterpret_cast<hipStream_t>(stream));
+}
+
+int mck_xxh64_batch(const mck_spans* spans, uint64_t seed, uint64_t* out, mck_stream_t stream) {
+  t_err[0] = 0;
+  if (int rc = check_spans(spans)) return rc;
+  if (spans->count && !out) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  return launch_legacy(OpLegacyValue<true>{to_src(spans), seed, out}, spans->count,
+                       reinterpret_cast<hipStream_t>(stream));
+}
+
+int mck_builtin_checksum_batch(int type, const mck_spans* spans, const uint8_t* last_bytes, uint32_t* out,
+                               mck_stream_t stream) {
+  t_err[0] = 0;
+  if (int rc = check_spans(spans)) return rc;
+  if (spans->count && !out) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  BlockArgs a{to_src(spans), last_bytes, nullptr, 0, out, nullptr, nullptr, nullptr};
+  return launch_block<kModeBuiltin>(type, a, spans->count, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mck_sst_trailer_batch(int type, const mck_spans* payloads, const uint8_t* comp_types,
+                          const uint64_t* file_offsets, uint32_t base_context_checksum, uint32_t* out,
+                          mck_stream_t stream) {
+  t_err[0] = 0;
+  if (int rc = check_spans(payloads)) return rc;
+  if (payloads->count && (!out || !comp_types)) {
+    set_err("out / comp_types is NULL");
+    return MCK_EINVAL;
+  }
+  BlockArgs a{to_src(payloads), comp_types, file_offsets, base_context_checksum, out, nullptr, nullptr, nullptr};
+  return launch_block<kModeTrailer>(type, a, payloads->count, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mck_sst_verify_batch(int type, const mck_spans* payloads, const uint64_t* file_offsets,
+                         uint32_t base_context_checksum, uint8_t* mismatch, uint32_t* computed, uint32_t* stored,
+                         uint32_t* mismatch_count, mck_stream_t stream) {
+  t_err[0] = 0;
+  if (int rc = check_spans(payloads)) return rc;
+  if (payloads->count && !mismatch) {
+    set_err("mismatch is NULL");
+    return MCK_EINVAL;
+  }
+  BlockArgs a{to_src(payloads), nullptr, file_offsets, base_context_checksum, computed, mismatch, stored,
+              mismatch_count};
+  return launch_block<kModeVerify>(type, a, payloads->count, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mck_wal_record_crc_batch(const mck_spans* payloads, const uint8_t* types, uint32_t log_number, uint32_t* out,
+                             mck_stream_t stream) {
+  t_err[0] = 0;
+  if (int rc = check_spans(payloads)) return rc;
+  if (payloads->count && (!out || !types)) {
+    set_err("out / types is NULL");
+    return MCK_EINVAL;
+  }
+  return launch_crc(OpCrcWal{to_src(payloads), types, wal_type_crcs(log_number), out}, payloads->count,
+                    reinterpret_cast<hipStream_t>(stream));
+}
+
+int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, mck_wal_block_result* results,
+                         mck_stream_t stream) {
+  t_err[0] = 0;
+  static_assert(sizeof(mck_wal_block_result) == sizeof(WalResult), "layout");
+  if (!nbytes) return MCK_OK;
+  if (!wal || !results) {
+    set_err("wal / results is NULL");
+    return MCK_EINVAL;
+  }
+  const uint64_t nb64 = (nbytes + 32767) / 32768;
+  if (nb64 > 0xFFFFFFFFull) {
+    set_err("WAL image too large");
+    return MCK_EINVAL;
+  }
+  int dev, ncu;
+  if (int rc = current_device(&dev, &ncu)) return rc;
+  if (int rc = ensure_lds(k_wal_verify, dev)) return rc;
+  const uint32_t nblocks = (uint32_t)nb64;
+  const uint32_t grid = std::min<uint32_t>(ncu, (nblocks + 15) / 16);
+  hipLaunchKernelGGL(k_wal_verify, dim3(grid), dim3(1024), kCrcLdsBytes, reinterpret_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(wal), nbytes, log_number, reinterpret_cast<WalResult*>(results),
+                     nblocks);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+// ---- scalar data shims (GPU, synchronous) ----------------------------------
+static uint32_t scalar_u32(int kind, uint32_t init, const void* data, size_t n, int type, int has_last,
+                           char last) {
+  t_err[0] = 0;
+  if (!data && n) {
+    set_err("data is NULL");
+    return 0;
+  }
+  if (n > 0xFFFFFFFFull) {
+    set_err("span too long for the scalar shim");
+    return 0;
+  }
+  uint8_t* d_data;
+  void* d_out;
+  if (stage_in(data, n, &d_data, &d_out)) return 0;
+  uint8_t* d_last = static_cast<uint8_t*>(d_out) + 32;
+  if (has_last && hipMemcpy(d_last, &last, 1, hipMemcpyHostToDevice) != hipSuccess) {
+    set_err("hipMemcpy failed");
+    return 0;
+  }
+  const mck_spans s{d_data, nullptr, nullptr, 0, (uint32_t)n, 1};
+  uint32_t* d_init = static_cast<uint32_t*>(d_out) + 4;
+  int rc;
+  if (kind == 0) {
+    if (hipMemcpy(d_init, &init, 4, hipMemcpyHostToDevice) != hipSuccess) {
+      set_err("hipMemcpy failed");
+      return 0;
+    }
+    rc = mck_crc32c_batch(&s, d_init, 0, static_cast<uint32_t*>(d_out), nullptr);
+  } else {
+    rc = mck_builtin_checksum_batch(type, &s, has_last ? d_last : nullptr, static_cast<uint32_t*>(d_out), nullptr);
+  }
+  uint32_t v = 0;
+  if (rc == 0 && hipMemcpy(&v, d_out, 4, hipMemcpyDeviceToHost) != hipSuccess) set_err("hipMemcpy failed");
+  return v;
+}
+
+uint32_t mck_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
+  return scalar_u32(0, init_crc, data, n, 0, 0, 0);
+}
+uint32_t mck_crc32c_value(const void* data, size_t n) { return scalar_u32(0, 0, data, n, 0, 0, 0); }
+uint32_t mck_builtin_checksum(int type, const void* data, size_t n) {
+  return scalar_u32(1, 0, data, n, type, 0, 0);
+}
+uint32_t mck_builtin_checksum_with_last_byte(int type, const void* data, size_t n, char last_byte) {
+  return scalar_u32(1, 0, data, n, type, 1, last_byte);
+}
+uint64_t mck_xxh3_64(const void* data, size_t n) {
+  t_err[0] = 0;
+  if (!data && n) {
+    set_err("data is NULL");
+    return 0;
+  }
+  if (n > 0xFFFFFFFFull) {
+    set_err("span too long for the scalar shim");
+    return 0;
+  }
+  uint8_t* d_data;
+  void* d_out;
+  if (stage_in(data, n, &d_data, &d_out)) return 0;
+  const mck_spans s{d_data, nullptr, nullptr, 0, (uint32_t)n, 1};
+  uint64_t v = 0;
+  if (mck_xxh3_64_batch(&s, static_cast<uint64_t*>(d_out), nullptr) == 0 &&
+      hipMemcpy(&v, d_out, 8, hipMemcpyDeviceToHost) != hipSuccess)
+    set_err("hipMemcpy failed");
+  return v;
+}
+
+// ---- partitioning + host-resident multi-GPU pipeline -----------------------
+int mck_partition_spans(const uint32_t* host_lengths, uint32_t count, uint32_t length, int parts, uint32_t* first) {
+  t_err[0] = 0;
+  if (parts <= 0 || !first) {
+    set_err("bad parts/first");
+    return MCK_EINVAL;
+  }
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < count; i++) total += host_lengths ? host_lengths[i] : length;
+  first[0] = 0;
+  uint64_t acc = 0;
+  uint32_t i = 0;
+  for (int p = 1; p < parts; p++) {
+    const uint64_t target = (total * (uint64_t)p + parts / 2) / (uint64_t)parts;
+    while (i < count && acc + (host_lengths ? host_lengths[i] : length) / 2 < target) {
+      acc += host_lengths ? host_lengths[i] : length;
+      i++;
+    }
+    first[p] = i;
+  }
+  first[parts] = count;
+  return MCK_OK;
+}
+
+namespace {
+
+struct HostJob {
+  int kind;
+  const uint8_t* base;
+  const uint64_t* offs;
+  const uint32_t* lens;
+  uint64_t stride;
+  uint32_t length;
+  uint32_t flags;
+  size_t chunk_bytes;
+  uint32_t* out32;
+  uint64_t* out64;
+  uint64_t off(uint32_t i) const { return offs ? offs[i] : (uint64_t)i * stride; }
+  uint32_t len(uint32_t i) const { return lens ? lens[i] : length; }
+};
+
+// One device's share [lo, hi): spans must be sorted by offset.  Chunks of
+// spans are staged through two device buffers on two streams, so the H2D
+// copy of one chunk overlaps the kernel of the other.
+int run_device_share(int dev, const HostJob& J, uint32_t lo, uint32_t hi) {
+  MCK_HIP(hipSetDevice(dev));
+  if (lo >= hi) return MCK_OK;
+  int rc = current_device(nullptr, nullptr);
+  if (rc) return rc;
+  // longest span bounds the chunk
+  size_t cap = J.chunk_bytes;
+  for (uint32_t i = lo; i < hi; i++) cap = std::max<size_t>(cap, J.len(i) + 32);
+  const uint32_t max_spans = (uint32_t)std::min<uint64_t>(hi - lo, 1u << 20);
+  struct Slot {
+    hipStream_t st = nullptr;
+    uint8_t* d_data = nullptr;
+    uint64_t* d_off = nullptr;
+    uint32_t* d_len = nullptr;
+    void* d_res = nullptr;
+    uint64_t* h_off = nullptr;
+    uint32_t* h_len = nullptr;
+    void* h_res = nullptr;
+    uint32_t first = 0, n = 0;
+  } slot[2];
+  const size_t res_sz = J.kind == MCK_kXXH3 ? 8 : 4;
+  for (auto& s : slot) {
+    MCK_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
+    MCK_HIP(hipMalloc(&s.d_data, cap + 64));
+    MCK_HIP(hipMalloc(&s.d_off, (size_t)max_spans * 8));
+    MCK_HIP(hipMalloc(&s.d_len, (size_t)max_spans * 4));
+    MCK_HIP(hipMalloc(&s.d_res, (size_t)max_spans * res_sz));
+    MCK_HIP(hipHostMalloc(&s.h_off, (size_t)max_spans * 8, hipHostMallocDefault));
+    MCK_HIP(hipHostMalloc(&s.h_len, (size_t)max_spans * 4, hipHostMallocDefault));
+    MCK_HIP(hipHostMalloc(&s.h_res, (size_t)max_spans * res_sz, hipHostMallocDefault));
+  }
+  auto drain = [&](Slot& s) -> int {
+    if (!s.n) return MCK_OK;
+    MCK_HIP(hipStreamSynchronize(s.st));
+    if (J.kind == MCK_kXXH3)
+      memcpy(J.out64 + s.first, s.h_res, (size_t)s.n * 8);
+    else
+      memcpy(J.out32 + s.first, s.h_res, (size_t)s.n * 4);
+    s.n = 0;
+    return MCK_OK;
+  };
+  uint32_t i = lo;
+  int k = 0;
+  while (i < hi) {
+    Slot& s = slot[k & 1];
+    if ((rc = drain(s))) return rc;
+    // gather spans [i, j) whose covering byte range fits the chunk
+    const uint64_t start = J.off(i);
+    uint32_t j = i;
+    uint64_t endb = start;
+    while (j < hi && j - i < max_spans) {
+      const uint64_t e = J.off(j) + J.len(j);
+      if (j > i && e - start > cap) break;
+      endb = std::max(endb, e);
+      s.h_off[j - i] = J.off(j) - start;
+      s.h_len[j - i] = J.len(j);
+      j++;
+    }
+    s.first = i;
+    s.n = j - i;
+    MCK_HIP(hipMemcpyAsync(s.d_data, J.base + start, endb - start, hipMemcpyHostToDevice, s.st));
+    MCK_HIP(hipMemcpyAsync(s.d_off, s.h_off, (size_t)s.n * 8, hipMemcpyHostToDevice, s.st));
+    MCK_HIP(hipMemcpyAsync(s.d_len, s.h_len, (size_t)s.n * 4, hipMemcpyHostToDevice, s.st));
+    const mck_spans sp{s.d_data, s.d_off, s.d_len, 0, 0, s.n};
+    rc = J.kind == MCK_kXXH3
+             ? mck_xxh3_64_batch(&sp, static_cast<uint64_t*>(s.d_res), reinterpret_cast<mck_stream_t>(s.st))
+             : mck_crc32c_batch(&sp, nullptr, J.flags, static_cast<uint32_t*>(s.d_res),
+                                reinterpret_cast<mck_stream_t>(s.st));
+    if (rc) return rc;
+    MCK_HIP(hipMemcpyAsync(s.h_res, s.d_res, (size_t)s.n * res_sz, hipMemcpyDeviceToHost, s.st));
+    i = j;
+    k++;
+  }
+  for (auto& s : slot)
+    if ((rc = drain(s))) return rc;
+  for (auto& s : slot) {
+    (void)hipStreamDestroy(s.st);
+    (void)hipFree(s.d_data);
+    (void)hipFree(s.d_off);
+    (void)hipFree(s.d_len);
+    (void)hipFree(s.d_res);
+    (void)hipHostFree(s.h_off);
+    (void)hipHostFree(s.h_len);
+    (void)hipHostFree(s.h_res);
+  }
+  return MCK_OK;
+}
+
+}  // namespace
+
+int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* host_offsets,
+                            const uint32_t* host_lengths, uint64_t stride, uint32_t length, uint32_t count,
+                            uint32_t flags, int ndev, size_t chunk_bytes, uint32_t* out32, uint64_t* out64,
+                            double* seconds) {
+  t_err[0] = 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (kind != MCK_kCRC32c && kind != MCK_kXXH3) {
+    set_err("kind must be MCK_kCRC32c or MCK_kXXH3");
+    return MCK_EINVAL;
+  }
+  if (count && (!host_base || (kind == MCK_kCRC32c ? !out32 : !out64))) {
+    set_err("NULL base/out");
+    return MCK_EINVAL;
+  }
+  int have = 0;
+  if (hipGetDeviceCount(&have) != hipSuccess || have <= 0) {
+    set_err("no HIP device");
+    return MCK_ENODEV;
+  }
+  if (ndev <= 0 || ndev > have) ndev = have;
+  if (!chunk_bytes) chunk_bytes = 256u << 20;
+  for (uint32_t i = 1; host_offsets && i < count; i++)
+    if (host_offsets[i] < host_offsets[i - 1]) {
+      set_err("host_offsets must be non-decreasing");
+      return MCK_EINVAL;
+    }
+  std::vector<uint32_t> first(ndev + 1);
+  mck_partition_spans(host_lengths, count, length, ndev, first.data());
+  HostJob J{kind, static_cast<const uint8_t*>(host_base), host_offsets, host_lengths, stride, length,
+            flags & MCK_F_MASK, chunk_bytes, out32, out64};
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  std::vector<int> rcs(ndev, 0);
+  std::vector<std::string> errs(ndev);
+  std::vector<std::thread> th;
+  for (int d = 0; d < ndev; d++)
+    th.emplace_back([&, d] {
+      rcs[d] = run_device_share(d, J, first[d], first[d + 1]);
+      if (rcs[d]) errs[d] = t_err;
+    });
+  for (auto& t : th) t.join();
+  (void)hipSetDevice(prev);
+  for (int d = 0; d < ndev; d++)
+    if (rcs[d]) {
+      set_err("device %d: %s", d, errs[d].c_str());
+      return rcs[d];
+    }
+  if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  return MCK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,301 @@
+// mck_kernels.hpp -- kernel templates and the per-call "ops" that bind the
+// generic CRC32C / XXH3 / XXH32 / XXH64 span engines to the reference's
+// call-site semantics (table/format.cc:578-645, block_based_table_builder.cc
+// :1333-1348, reader_common.cc:26-63, log_writer.cc:263-311).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mck_crc.hpp"
+#include "mck_xxh.hpp"
+
+namespace mck {
+
+extern __device__ CrcTables g_crc_tables;
+
+constexpr uint32_t kRandomPrime = 0x6b9083d9u;  // table/format.cc:573
+
+// ---- span source: the mck_spans descriptor --------------------------------
+struct SpanSrc {
+  const uint8_t* base;
+  const uint64_t* offsets;
+  const uint32_t* lengths;
+  uint64_t stride;
+  uint32_t length;
+  __device__ __forceinline__ uint64_t off(uint32_t i) const { return offsets ? offsets[i] : (uint64_t)i * stride; }
+  __device__ __forceinline__ uint64_t len(uint32_t i) const { return lengths ? lengths[i] : length; }
+  __device__ __forceinline__ const uint8_t* ptr(uint32_t i) const { return base + off(i); }
+};
+
+// table/format.h:119-146 ChecksumModifierForContext
+__device__ __forceinline__ uint32_t context_modifier(uint32_t base, uint64_t offset) {
+  const uint32_t all_or_nothing = 0u - (uint32_t)(base != 0);
+  return (base ^ ((uint32_t)offset + (uint32_t)(offset >> 32))) & all_or_nothing;
+}
+
+__device__ __forceinline__ uint32_t rd32_bytes(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// What a block op does with a block's builtin checksum.
+enum BlockMode : int {
+  kModeBuiltin = 0,  // out[i] = builtin(span, last?)
+  kModeTrailer = 1,  // out[i] = builtin(span, comp[i]) + modifier(file offset)
+  kModeVerify = 2,   // span+type byte vs stored LE32 (context removed)
+};
+
+struct BlockArgs {
+  SpanSrc s;
+  const uint8_t* last;     // builtin: optional last bytes; trailer: comp types
+  const uint64_t* foff;    // trailer/verify: file offsets (NULL = s.off)
+  uint32_t base_ctx;       // base_context_checksum
+  uint32_t* out;           // builtin/trailer result; verify: computed (opt)
+  uint8_t* mismatch;       // verify
+  uint32_t* stored;        // verify (opt)
+  uint32_t* mismatch_count;  // verify (opt)
+};
+
+// Verify / trailer epilogue shared by every hash kind.  `v` = builtin value.
+template <int MODE>
+__device__ __forceinline__ void block_epilogue(const BlockArgs& a, uint32_t i, uint32_t v) {
+  if (MODE == kModeBuiltin) {
+    a.out[i] = v;
+  } else if (MODE == kModeTrailer) {
+    a.out[i] = v + context_modifier(a.base_ctx, a.foff ? a.foff[i] : a.s.off(i));
+  } else {
+    const uint8_t* p = a.s.ptr(i) + a.s.len(i) + 1;
+    const uint32_t stored = rd32_bytes(p) - context_modifier(a.base_ctx, a.foff ? a.foff[i] : a.s.off(i));
+    const bool bad = stored != v;
+    a.mismatch[i] = bad;
+    if (a.out) a.out[i] = v;
+    if (a.stored) a.stored[i] = stored;
+    if (bad && a.mismatch_count) atomicAdd(a.mismatch_count, 1u);
+  }
+}
+
+// ============================ CRC32C ======================================
+struct OpCrcValue {
+  SpanSrc s;
+  const uint32_t* init;
+  uint32_t flags;
+  uint32_t* out;
+  __device__ const uint8_t* ptr(uint32_t i) const { return s.ptr(i); }
+  __device__ uint64_t len(uint32_t i) const { return s.len(i); }
+  __device__ uint32_t init_crc(uint32_t i) const { return init ? init[i] : 0u; }
+  __device__ void finish(uint32_t i, uint32_t crc, const uint8_t*) const {
+    if ((threadIdx.x & 63) == 0) out[i] = (flags & 1u) ? crc_mask(crc) : crc;
+  }
+};
+
+// WAL write side: init = Value(type byte [+ LE32 log number])
+struct WalTypeCrcs {
+  uint32_t v[16];
+};
+struct OpCrcWal {
+  SpanSrc s;
+  const uint8_t* types;
+  WalTypeCrcs tc;
+  uint32_t* out;
+  __device__ const uint8_t* ptr(uint32_t i) const { return s.ptr(i); }
+  __device__ uint64_t len(uint32_t i) const { return s.len(i); }
+  __device__ uint32_t init_crc(uint32_t i) const { return tc.v[types[i] & 15]; }
+  __device__ void finish(uint32_t i, uint32_t crc, const uint8_t*) const {
+    if ((threadIdx.x & 63) == 0) out[i] = crc_mask(crc);
+  }
+};
+
+template <int MODE>
+struct OpCrcBlock {
+  BlockArgs a;
+  __device__ const uint8_t* ptr(uint32_t i) const { return a.s.ptr(i); }
+  __device__ uint64_t len(uint32_t i) const { return a.s.len(i) + (MODE == kModeVerify ? 1 : 0); }
+  __device__ uint32_t init_crc(uint32_t) const { return 0u; }
+  __device__ void finish(uint32_t i, uint32_t crc, const uint8_t* lds) const {
+    if (MODE == kModeTrailer || (MODE == kModeBuiltin && a.last)) crc = crc_extend_byte(lds, crc, a.last[i]);
+    if ((threadIdx.x & 63) == 0) block_epilogue<MODE>(a, i, crc_mask(crc));
+  }
+};
+
+template <class Op>
+__global__ __launch_bounds__(1024) void k_crc(Op op, uint32_t count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  crc_spans_driver(op, count, lds, &g_crc_tables);
+}
+
+// ============================ XXH3 ========================================
+// wave per span; grid-stride over spans
+template <class Op>
+__global__ __launch_bounds__(256) void k_xxh3(Op op, uint32_t count) {
+  const XxhLane X = xxh_lane();
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t nw = gridDim.x * wpb;
+  for (uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)); i < count; i += nw)
+    op.run(i, X);
+}
+
+struct OpX3Value {
+  SpanSrc s;
+  uint64_t* out;
+  __device__ void run(uint32_t i, const XxhLane& X) const {
+    const uint64_t h = xxh3_wave(s.ptr(i), s.len(i), X);
+    if (X.lane == 0) out[i] = h;
+  }
+};
+
+template <int MODE>
+struct OpX3Block {
+  BlockArgs a;
+  __device__ void run(uint32_t i, const XxhLane& X) const {
+    const uint8_t* p = a.s.ptr(i);
+    const uint64_t n = a.s.len(i);
+    uint32_t v;
+    if (MODE == kModeVerify) {
+      // checksummed = payload || type byte: XXH3(payload) ^ type * prime
+      v = (uint32_t)xxh3_wave(p, n, X) ^ (uint32_t)p[n] * kRandomPrime;
+    } else if (MODE == kModeTrailer || a.last) {
+      v = (uint32_t)xxh3_wave(p, n, X) ^ (uint32_t)a.last[i] * kRandomPrime;
+    } else {
+      v = n == 0 ? 0u : (uint32_t)xxh3_wave(p, n - 1, X) ^ (uint32_t)p[n - 1] * kRandomPrime;
+    }
+    if (X.lane == 0) block_epilogue<MODE>(a, i, v);
+  }
+};
+
+// ===================== legacy XXH32 / XXH64 ===============================
+template <class Op>
+__global__ __launch_bounds__(256) void k_legacy(Op op, uint32_t count) {
+  const uint32_t nt = gridDim.x * blockDim.x;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < count; i += nt) op.run(i);
+}
+
+template <bool IS64>
+struct OpLegacyValue {
+  SpanSrc s;
+  uint64_t seed;
+  void* out;
+  __device__ void run(uint32_t i) const {
+    const VBytes b{s.ptr(i), s.len(i), false, 0};
+    if (IS64)
+      static_cast<uint64_t*>(out)[i] = xxh64_lane(b, seed);
+    else
+      static_cast<uint32_t*>(out)[i] = xxh32_lane(b, (uint32_t)seed);
+  }
+};
+
+template <bool IS64, int MODE>
+struct OpLegacyBlock {
+  BlockArgs a;
+  __device__ void run(uint32_t i) const {
+    const uint8_t* p = a.s.ptr(i);
+    const uint64_t n = a.s.len(i);
+    VBytes b{p, n, false, 0};
+    if (MODE == kModeVerify) b.n = n + 1;
+    if (MODE == kModeTrailer || (MODE == kModeBuiltin && a.last)) {
+      b.has_extra = true;
+      b.extra = a.last[i];
+    }
+    const uint32_t v = IS64 ? (uint32_t)xxh64_lane(b, 0) : xxh32_lane(b, 0);
+    block_epilogue<MODE>(a, i, v);
+  }
+};
+
+// kNoChecksum: builtin value 0 (table/format.cc:599-601)
+template <int MODE>
+struct OpNoneBlock {
+  BlockArgs a;
+  __device__ void run(uint32_t i) const { block_epilogue<MODE>(a, i, 0u); }
+};
+
+// ============================ WAL verify ==================================
+// db/log_reader.cc:450-584 ReadPhysicalRecord with checksum_ = true, applied
+// to every 32 KiB block independently; one wave per block.
+struct WalResult {
+  uint32_t records_ok;
+  int32_t status;
+  uint32_t stop_offset;
+  uint32_t bytes_ok;
+};
+
+__device__ __forceinline__ uint32_t crc_span_wave(const uint8_t* lds, const uint8_t* p, uint64_t n, uint32_t init,
+                                                  const CrcLane& L) {
+  const CrcSpan sp = crc_span(p, n, init);
+  uint32_t s = 0;
+  Chunk cur = crc_load_chunk(sp, sp.rounds - 1, L);
+  for (int r = sp.rounds - 1; r >= 0; r--) {
+    Chunk nxt;
+    if (r > 0) nxt = crc_load_chunk(sp, r - 1, L);
+    s = crc_round(lds, s, cur, sp, r, L);
+    cur = nxt;
+  }
+  return crc_finish(lds, s, sp, L);
+}
+
+__global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_t nbytes, uint32_t log_number,
+                                                     WalResult* res, uint32_t nblocks) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  crc_fill_lds(lds, &g_crc_tables);
+  __syncthreads();
+  const CrcLane L = crc_lane();
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t nw = gridDim.x * wpb;
+  for (uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)); b < nblocks; b += nw) {
+    const uint8_t* blk = wal + (uint64_t)b * 32768;
+    const uint64_t rem = nbytes - (uint64_t)b * 32768;
+    const uint32_t size = rem < 32768 ? (uint32_t)rem : 32768u;
+    const bool last_block = rem <= 32768;  // reader reaches EOF inside it
+    uint32_t pos = 0, ok = 0, bytes_ok = 0;
+    int32_t status = 0;
+    for (;;) {
+      const uint32_t left = size - pos;
+      if (left < 7) {
+        // fewer than kHeaderSize bytes: block trailer (skip), or at EOF a
+        // truncated header (db/log_reader.cc:432-440)
+        if (last_block && left > 0) status = 5;  // MCK_WAL_BAD_HEADER
+        break;
+      }
+      const uint8_t* h = blk + pos;
+      const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
+      const uint32_t type = h[6];
+      uint32_t hsize = 7;
+      if ((type >= 5 && type <= 8) || type == 11) {
+        hsize = 11;
+        if (left < 11) {
+          if (last_block) status = 5;
+          break;
+        }
+        if (rd32_bytes(h + 7) != log_number) {
+          status = 4;  // kOldRecord
+          break;
+        }
+      }
+      if (hsize + length > left) {
+        status = 2;  // kBadRecordLen
+        break;
+      }
+      if (type == 0 && length == 0) {
+        status = 3;  // kZeroType, length 0: buffer cleared
+        break;
+      }
+      const uint32_t stored = rd32_bytes(h);
+      const uint32_t actual = crc_span_wave(lds, h + 6, length + hsize - 6, 0u, L);
+      // Unmask(stored) == actual  <=>  stored == Mask(actual)
+      if (crc_mask(actual) != stored) {
+        status = 1;  // kBadRecordChecksum
+        break;
+      }
+      ok++;
+      pos += hsize + length;
+      bytes_ok += hsize + length;
+    }
+    if ((threadIdx.x & 63) == 0) {
+      WalResult r;
+      r.records_ok = ok;
+      r.status = status;
+      r.stop_offset = status ? pos : size;
+      r.bytes_ok = bytes_ok;
+      res[b] = r;
+    }
+  }
+}
+
+}  // namespace mck

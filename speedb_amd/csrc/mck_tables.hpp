@@ -1,0 +1,81 @@
+// mck_tables.hpp -- GF(2) constant tables for the CRC32C kernels.
+//
+// CRC-32C is linear over GF(2): the "pure" state (init 0, no final
+// inversion -- the algebra of util/crc32c.cc:1221-1266) after appending d
+// zero bytes is zshift(s, d) = s * x^(8d) mod P, P the reflected Castagnoli
+// polynomial 0x82f63b78 (util/crc32c.cc:1193).  Every table here is a byte-
+// or nibble-wise decomposition of one such linear map, so a map costs 4 byte
+// lookups or 8 nibble lookups.  Tables are generated on the host once per
+// process and uploaded to each device (mck_engine.cpp).
+#pragma once
+#include <stdint.h>
+
+namespace mck {
+
+constexpr uint32_t kCrc32cPoly = 0x82f63b78u;  // reflected
+
+// Lanes cover 64-byte chunks; a wave covers one 4 KiB "round" of a span.
+constexpr int kChunkBytes = 64;
+constexpr int kRoundBytes = 64 * kChunkBytes;                   // 4096
+constexpr int kGapBytes = kRoundBytes - kChunkBytes;            // 4032
+constexpr int kMaxUnshift = 16;                                 // k in [0,16)
+
+struct CrcTables {
+  uint32_t step[4][256];          // zshift(v << 8t, 4): the 4-byte step
+  uint32_t lane_final[8][16][64]; // zshift(v << 4n, 64*(63-lane))
+  uint32_t gap[8][16];            // zshift(v << 4n, kGapBytes)
+  uint32_t ext1[8][16];           // zshift(v << 4n, 1)
+  uint32_t unshift[kMaxUnshift][8][16];  // zshift^-1(v << 4n, k)
+};
+
+// ---- host-side GF(2) helpers (also used by the host shims) ----------------
+inline uint32_t gf_mulx(uint32_t a) { return (a >> 1) ^ ((a & 1u) ? kCrc32cPoly : 0u); }
+// inverse of gf_mulx: bit 31 of P is set, so bit 31 of mulx(a) = a & 1.
+inline uint32_t gf_unmulx(uint32_t b) {
+  uint32_t lo = b >> 31;
+  return ((b ^ (lo ? kCrc32cPoly : 0u)) << 1) | lo;
+}
+inline uint32_t gf_mul(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+  for (int j = 0; j < 32; j++) {
+    if (b & (0x80000000u >> j)) p ^= a;
+    a = gf_mulx(a);
+  }
+  return p;
+}
+inline uint32_t gf_xpow8n(uint64_t nbytes) {
+  uint32_t r = 0x80000000u, sq = 0x00800000u;  // x^0, x^8
+  while (nbytes) {
+    if (nbytes & 1) r = gf_mul(r, sq);
+    sq = gf_mul(sq, sq);
+    nbytes >>= 1;
+  }
+  return r;
+}
+inline uint32_t gf_zshift(uint32_t s, uint64_t nbytes) { return gf_mul(s, gf_xpow8n(nbytes)); }
+
+inline void build_crc_tables(CrcTables* t) {
+  const uint32_t k4 = gf_xpow8n(4);
+  for (int b = 0; b < 4; b++)
+    for (int v = 0; v < 256; v++) t->step[b][v] = gf_mul((uint32_t)v << (8 * b), k4);
+  for (int l = 0; l < 64; l++) {
+    const uint32_t k = gf_xpow8n((uint64_t)kChunkBytes * (63 - l));
+    for (int n = 0; n < 8; n++)
+      for (int v = 0; v < 16; v++) t->lane_final[n][v][l] = gf_mul((uint32_t)v << (4 * n), k);
+  }
+  const uint32_t kg = gf_xpow8n(kGapBytes), k1 = gf_xpow8n(1);
+  for (int n = 0; n < 8; n++)
+    for (int v = 0; v < 16; v++) {
+      t->gap[n][v] = gf_mul((uint32_t)v << (4 * n), kg);
+      t->ext1[n][v] = gf_mul((uint32_t)v << (4 * n), k1);
+    }
+  for (int k = 0; k < kMaxUnshift; k++)
+    for (int n = 0; n < 8; n++)
+      for (int v = 0; v < 16; v++) {
+        uint32_t x = (uint32_t)v << (4 * n);
+        for (int i = 0; i < 8 * k; i++) x = gf_unmulx(x);
+        t->unshift[k][n][v] = x;
+      }
+}
+
+}  // namespace mck

@@ -1,0 +1,109 @@
+"""CPU-side checks of the drop-in boundary: the C-ABI library loads, exports
+every symbol include/speedb_amd/mck.h declares, its host-side u32 algebra
+matches the oracle, and the product path never touches oracle/."""
+import ctypes
+import os
+import random
+import re
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(REPO, "include", "speedb_amd", "mck.h")
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mck_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    from speedb_amd import _lib
+    syms = declared_symbols()
+    assert len(syms) >= 20
+    for s in syms:
+        assert hasattr(_lib.lib, s), f"{s} declared in mck.h but not exported"
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    assert set(syms) == bound, set(syms) ^ bound
+
+
+def test_version_and_no_device_here():
+    from speedb_amd import _lib
+    assert b"gfx950" in _lib.lib.mck_version()
+    assert _lib.lib.mck_device_count() >= 0
+
+
+def test_host_algebra_matches_oracle(oracle):
+    from speedb_amd import _lib
+    L = _lib.lib
+    rnd = random.Random(11)
+    for _ in range(2000):
+        v = rnd.getrandbits(32)
+        assert L.mck_crc32c_mask(v) == oracle.Mask(v)
+        assert L.mck_crc32c_unmask(v) == oracle.Unmask(v)
+        a, b = rnd.getrandbits(32), rnd.getrandbits(32)
+        n = rnd.choice([0, 1, 2, 3, 4, 7, 4096, rnd.getrandbits(20), rnd.getrandbits(40)])
+        assert L.mck_crc32c_combine(a, b, n) == oracle.Combine(a, b, n)
+        base = rnd.choice([0, rnd.getrandbits(32)])
+        off = rnd.getrandbits(64)
+        assert L.mck_context_modifier(base, off) == oracle.ContextModifier(base, off)
+
+
+def test_host_algebra_vs_golden(golden):
+    from speedb_amd import _lib
+    for c in golden["combine"]:
+        assert _lib.lib.mck_crc32c_combine(c["crc1"], c["crc2"], c["len2"]) == c["out"]
+    for c in golden["context_modifier"]:
+        assert _lib.lib.mck_context_modifier(c["base"], c["offset"]) == c["out"]
+
+
+def test_partition_spans():
+    from speedb_amd import _lib
+    rnd = random.Random(5)
+    for parts in (1, 2, 3, 4, 8):
+        n = 1000
+        lens = (ctypes.c_uint32 * n)(*[rnd.choice([4096, 16384, 65536]) for _ in range(n)])
+        first = (ctypes.c_uint32 * (parts + 1))()
+        assert _lib.lib.mck_partition_spans(lens, n, 0, parts, first) == 0
+        f = list(first)
+        assert f[0] == 0 and f[-1] == n and f == sorted(f)
+        tot = sum(lens)
+        shares = [sum(lens[f[p]:f[p + 1]]) for p in range(parts)]
+        assert max(shares) - min(shares) <= 2 * 65536, shares
+        assert sum(shares) == tot
+    first = (ctypes.c_uint32 * 9)()
+    assert _lib.lib.mck_partition_spans(None, 80, 4096, 8, first) == 0
+    assert list(first) == [10 * i for i in range(9)]
+
+
+def test_data_shims_fail_cleanly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from speedb_amd import _lib
+    assert _lib.lib.mck_crc32c_value(b"abc", 3) == 0
+    assert _lib.lib.mck_last_error() != b""
+
+
+def test_product_does_not_use_oracle():
+    """Only tests/, smoke() and bench.py's cpu_baseline may touch oracle/."""
+    pkg = os.path.join(REPO, "speedb_amd")
+    for root, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith((".py", ".hip", ".hpp", ".cpp", ".h")):
+                txt = open(os.path.join(root, fn)).read()
+                assert "oracle" not in txt.lower(), fn
+
+
+def test_python_mirror_exports():
+    import speedb_amd as S
+    for name in ("crc32c", "XXH3_64bits", "ComputeBuiltinChecksum",
+                 "ComputeBuiltinChecksumWithLastByte", "ChecksumModifierForContext",
+                 "VerifyBlockChecksum", "ChecksumType", "Status", "crc32c_batch",
+                 "xxh3_64_batch", "sst_verify_batch", "sst_trailer_batch", "wal_verify_batch",
+                 "wal_record_crc_batch", "builtin_checksum_batch"):
+        assert hasattr(S, name), name
+    assert [int(t) for t in S.ChecksumType] == [0, 1, 2, 3, 4]
+    assert S.crc32c.kMaskDelta == 0xA282EAD8
+    assert S.crc32c.Unmask(S.crc32c.Mask(0x12345678)) == 0x12345678

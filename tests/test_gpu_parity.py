@@ -1,0 +1,331 @@
+"""GPU parity: every batched entry point of the C ABI against the CPU oracle,
+bit-exact, on seeded inputs -- ragged and unaligned spans, every length class
+of XXH3, multi-round CRC spans, empty and tiny spans, and the reference's own
+known-answer vectors pushed through the device path."""
+import random
+import struct
+
+import numpy as np
+import pytest
+
+from formats import WalWriter, folly_buffer, sst_blocks, splitmix_bytes, wal_expected_blocks
+
+pytestmark = pytest.mark.gpu
+
+LENGTHS = (list(range(0, 70)) + [127, 128, 129, 239, 240, 241, 255, 256, 257, 1023, 1024, 1025,
+                                 1087, 1088, 2048, 4032, 4095, 4096, 4097, 4111, 8191, 8192, 8193,
+                                 16383, 16384, 16385, 32761, 32762, 65535, 65536, 65537, 100003,
+                                 262144, 300001])
+
+
+def u32(t):
+    return t.cpu().numpy().view(np.uint32).astype(np.uint64).tolist()
+
+
+def u64(t):
+    return t.cpu().numpy().view(np.uint64).tolist()
+
+
+def make_batch(torch, seed, lengths, align_mix=True, pad=4096):
+    """Pack spans back to back with random 0..63 byte gaps (so starts are at
+    every alignment); returns (host bytes, device tensor, offsets, lengths)."""
+    rnd = random.Random(seed)
+    offs, pos = [], 0
+    for n in lengths:
+        pos += rnd.randrange(0, 64) if align_mix else 0
+        offs.append(pos)
+        pos += n
+    total = pos + pad
+    host = splitmix_bytes(seed, total)
+    dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda")
+    return host, dev, offs, list(lengths)
+
+
+def spans(torch, S, dev, offs, lens):
+    o = torch.tensor(offs, dtype=torch.int64, device="cuda")
+    l_ = torch.tensor(lens, dtype=torch.int32, device="cuda")
+    return S.Spans(dev, len(offs), offsets=o, lengths=l_)
+
+
+def test_crc32c_batch_ragged(gpu, oracle):
+    import speedb_amd as S
+    torch = gpu
+    lens = LENGTHS * 3
+    random.Random(1).shuffle(lens)
+    host, dev, offs, lens = make_batch(torch, 1, lens)
+    sp = spans(torch, S, dev, offs, lens)
+    got = u32(S.crc32c_batch(sp))
+    torch.cuda.synchronize()
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert got[i] == oracle.Value(host[o:o + n]), (i, o, n)
+    gotm = u32(S.crc32c_batch(sp, mask=True))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert gotm[i] == oracle.Mask(oracle.Value(host[o:o + n]))
+    rnd = random.Random(2)
+    inits = [rnd.getrandbits(32) for _ in lens]
+    it = torch.tensor(np.array(inits, dtype=np.uint32).view(np.int32), device="cuda")
+    gote = u32(S.crc32c_batch(sp, init_crcs=it))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert gote[i] == oracle.Extend(inits[i], host[o:o + n]), (i, n)
+
+
+def test_crc32c_uniform_blocks(gpu, oracle):
+    import speedb_amd as S
+    torch = gpu
+    for block in (4096, 16384, 65536, 32768, 4100, 1000):
+        count = max(1, (8 << 20) // block)
+        host = splitmix_bytes(block, block * count)
+        dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda")
+        got = u32(S.crc32c_batch(S.Spans.uniform(dev, block, count)))
+        for i in list(range(0, count, max(1, count // 97))) + [count - 1]:
+            assert got[i] == oracle.Value(host[i * block:(i + 1) * block]), (block, i)
+
+
+def test_crc32c_known_answers_on_device(gpu, golden):
+    import speedb_amd as S
+    torch = gpu
+    kat = golden["kat"]
+    buf = folly_buffer(kat["folly_buffer_bytes"])
+    dev = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to("cuda")
+    offs = [o for o, _, _ in kat["folly"]]
+    lens = [n for _, n, _ in kat["folly"]]
+    got = u32(S.crc32c_batch(spans(torch, S, dev, offs, lens)))
+    for g, (_, _, exp) in zip(got, kat["folly"]):
+        assert g == (~exp) & 0xFFFFFFFF
+    rfc = {r["pattern"]: int(r["crc"], 16) for r in kat["rfc3720"]}
+    assert S.crc32c.Value(bytes(32)) == rfc["zeros32"]
+    assert S.crc32c.Value(b"\xff" * 32) == rfc["ff32"]
+    assert S.crc32c.Value(bytes(range(32))) == rfc["inc32"]
+    assert S.crc32c.Value(bytes(31 - i for i in range(32))) == rfc["dec32"]
+    assert S.crc32c.Value(bytes.fromhex(kat["iscsi48"])) == rfc["iscsi48"]
+
+
+def test_scalar_shims(gpu, oracle, golden):
+    import speedb_amd as S
+    blob = golden["blob"]
+    for c in golden["cases"]:
+        d = blob[c["off"]:c["off"] + c["len"]]
+        assert S.crc32c.Value(d) == c["crc32c"]
+        assert S.crc32c.Extend(c["extend_init"], d) == c["crc32c_extend"]
+        assert S.XXH3_64bits(d) == c["xxh3"]
+        for t, v in c["builtin"].items():
+            assert S.ComputeBuiltinChecksum(int(t), d) == v, (t, c["len"])
+            if d:
+                assert S.ComputeBuiltinChecksumWithLastByte(int(t), d[:-1], d[-1]) == v
+    # util/crc32c_test.cc:113-126
+    assert S.crc32c.Value(b"hello world") == S.crc32c.Extend(S.crc32c.Value(b"hello "), b"world")
+    assert S.crc32c.Crc32cCombine(S.crc32c.Value(b"hello "), S.crc32c.Value(b"world"), 5) == \
+        S.crc32c.Value(b"hello world")
+
+
+def test_checksum_schemas_on_device(gpu, golden):
+    """table/table_test.cc:2286-2403 through the device path."""
+    import speedb_amd as S
+    si = golden["kat"]["schemas_inputs"]
+    b2 = (si["b2_repeat"] * si["b2_times"] + si["b2_suffix"]).encode()
+    cts = [si["compression_last_bytes"][k] for k in ("ct1", "ct2", "ct3")]
+    for t, exp in golden["kat"]["schemas"].items():
+        t = int(t)
+        assert struct.pack("<I", S.ComputeBuiltinChecksum(t, b"")).hex().upper() == exp["empty"]
+        for name, data in (("b0", si["b0"].encode()), ("b1", si["b1"].encode()), ("b2", b2)):
+            for ct, want in zip(cts, exp[name]):
+                d = data[:-1] + bytes([ct])
+                got = S.ComputeBuiltinChecksum(t, d)
+                assert struct.pack("<I", got).hex().upper() == want, (t, name, ct)
+
+
+def test_xxh3_batch_all_length_classes(gpu, oracle):
+    import speedb_amd as S
+    torch = gpu
+    lens = LENGTHS + list(range(230, 260)) + [1024 * k + d for k in (1, 2, 3, 4, 5, 8)
+                                              for d in (-65, -64, -63, -1, 0, 1, 63, 64, 65)]
+    host, dev, offs, lens = make_batch(torch, 3, lens)
+    got = u64(S.xxh3_64_batch(spans(torch, S, dev, offs, lens)))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert got[i] == oracle.XXH3(host[o:o + n]), (i, n, o % 16)
+
+
+def test_legacy_xxh_batch(gpu, oracle):
+    import speedb_amd as S
+    torch = gpu
+    host, dev, offs, lens = make_batch(torch, 4, LENGTHS)
+    sp = spans(torch, S, dev, offs, lens)
+    g32 = u32(S.xxh32_batch(sp, seed=7))
+    g64 = u64(S.xxh64_batch(sp, seed=9))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        d = host[o:o + n]
+        assert g32[i] == oracle.XXH32(d, 7), n
+        assert g64[i] == oracle.XXH64(d, 9), n
+
+
+@pytest.mark.parametrize("ctype", [0, 1, 2, 3, 4])
+def test_builtin_checksum_batch(gpu, oracle, ctype):
+    import speedb_amd as S
+    torch = gpu
+    host, dev, offs, lens = make_batch(torch, 10 + ctype, LENGTHS)
+    sp = spans(torch, S, dev, offs, lens)
+    got = u32(S.builtin_checksum_batch(ctype, sp))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert got[i] == oracle.Builtin(ctype, host[o:o + n]), (ctype, n)
+    rnd = random.Random(ctype)
+    last = [rnd.choice([0, 1, 7, 0x40, 255]) for _ in lens]
+    lt = torch.tensor(last, dtype=torch.uint8, device="cuda")
+    got = u32(S.builtin_checksum_batch(ctype, sp, last_bytes=lt))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert got[i] == oracle.BuiltinLast(ctype, host[o:o + n], last[i]), (ctype, n)
+
+
+@pytest.mark.parametrize("ctype", [1, 2, 3, 4])
+@pytest.mark.parametrize("base_ctx", [0, 0x9E3779B9])
+def test_sst_trailer_and_verify(gpu, oracle, ctype, base_ctx):
+    """Write side (trailer compute) and read side (VerifyBlockChecksum) over a
+    compaction-shaped run of 4/16/64 KiB blocks with jitter, format_version 6
+    context checksums, then one flipped byte in some blocks."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(ctype * 1000 + base_ctx % 7)
+    sizes = [rnd.choice([4096] * 6 + [16384] * 3 + [65536]) + rnd.randrange(0, 256) for _ in range(120)]
+    sizes += [0, 1, 2, 3, 4, 5]
+    payloads = [splitmix_bytes(1000 + i, n) for i, n in enumerate(sizes)]
+    comps = [rnd.choice([0, 1, 7]) for _ in sizes]
+    file_start = 1 << 33  # offsets above 4 GiB exercise the upper-32 fold
+    img, offs, lens = sst_blocks(oracle, payloads, ctype, comps, base_ctx, file_start)
+    dev = torch.frombuffer(bytearray(img + bytes(64)), dtype=torch.uint8).to("cuda")
+    sp = spans(torch, S, dev, offs, lens)
+    foff = torch.tensor([file_start + o for o in offs], dtype=torch.int64, device="cuda")
+    # write side
+    ct = torch.tensor(comps, dtype=torch.uint8, device="cuda")
+    tr = u32(S.sst_trailer_batch(ctype, sp, ct, file_offsets=foff, base_context_checksum=base_ctx))
+    for i, o in enumerate(offs):
+        assert tr[i] == struct.unpack_from("<I", img, o + lens[i] + 1)[0], (i, lens[i])
+    # read side, clean
+    mm, comp, stored, cnt = S.sst_verify_batch(ctype, sp, file_offsets=foff,
+                                               base_context_checksum=base_ctx)
+    assert int(cnt.item()) == 0 and int(mm.sum().item()) == 0
+    comp_l = u32(comp)
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert comp_l[i] == oracle.Builtin(ctype, img[o:o + n + 1])
+    # corrupt: flip one byte (payload, type byte or stored checksum) in 10 blocks
+    bad = sorted(rnd.sample(range(len(sizes)), 10))
+    cor = bytearray(img)
+    for i in bad:
+        pos = offs[i] + rnd.randrange(0, lens[i] + 5)
+        cor[pos] ^= 1 << rnd.randrange(8)
+    dev2 = torch.frombuffer(bytes(cor) + bytes(64), dtype=torch.uint8).to("cuda")
+    sp2 = spans(torch, S, dev2, offs, lens)
+    mm, comp, stored, cnt = S.sst_verify_batch(ctype, sp2, file_offsets=foff,
+                                               base_context_checksum=base_ctx)
+    flagged = [i for i, v in enumerate(mm.cpu().tolist()) if v]
+    assert flagged == bad
+    assert int(cnt.item()) == len(bad)
+    st = u32(stored)
+    for i in bad:
+        o, n = offs[i], lens[i]
+        exp_stored = (struct.unpack_from("<I", cor, o + n + 1)[0] -
+                      oracle.ContextModifier(base_ctx, file_start + o)) & 0xFFFFFFFF
+        assert st[i] == exp_stored
+
+
+def test_verify_block_checksum_status(gpu, oracle):
+    """VerifyBlockChecksum's Status and message (reader_common.cc:46-61)."""
+    import speedb_amd as S
+    payload = b"This is a long block!" * 50
+    for t, base in ((1, 0), (4, 0), (1, 0x1234), (4, 0x77)):
+        img, offs, lens = sst_blocks(oracle, [payload], t, [1], base, 4096)
+        f = S.Footer(S.ChecksumType(t), base)
+        assert S.VerifyBlockChecksum(f, img, len(payload), "000012.sst", 4096).ok()
+        cor = bytearray(img)
+        cor[10] ^= 0x20
+        st = S.VerifyBlockChecksum(f, bytes(cor), len(payload), "000012.sst", 4096)
+        assert st.IsCorruption()
+        m = st.ToString()
+        assert m.startswith("Corruption: block checksum mismatch: stored")
+        assert ("(context removed)" in m) == bool(base)
+        assert m.endswith(f", type = {t}  in 000012.sst offset 4096 size {len(payload)}")
+
+
+def test_wal_record_crc_batch(gpu, oracle, golden):
+    import speedb_amd as S
+    torch = gpu
+    blob = golden["blob"]
+    recs = golden["wal_records"]
+    for ln in sorted({r["log_number"] for r in recs}):
+        sub = [r for r in recs if r["log_number"] == ln]
+        dev = torch.frombuffer(bytearray(blob + bytes(64)), dtype=torch.uint8).to("cuda")
+        sp = spans(torch, S, dev, [r["off"] for r in sub], [r["len"] for r in sub])
+        types = torch.tensor([r["type"] for r in sub], dtype=torch.uint8, device="cuda")
+        got = u32(S.wal_record_crc_batch(sp, types, ln))
+        assert got == [r["crc"] for r in sub]
+
+
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_verify_batch(gpu, oracle, recycle):
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(42 + recycle)
+    w = WalWriter(oracle, log_number=123, recycle=recycle)
+    for _ in range(300):
+        n = rnd.choice([0, 1, 10, 100, 1000, 5000, 32761, 40000, rnd.randrange(0, 100000)])
+        w.add_record(splitmix_bytes(rnd.getrandbits(32), n))
+    data = bytes(w.buf)
+    dev = torch.frombuffer(bytearray(data + bytes(64)), dtype=torch.uint8).to("cuda")
+    res = S.wal_verify_batch(dev, len(data), 123).cpu().tolist()
+    exp = wal_expected_blocks(data, 123, oracle)
+    assert [tuple(r) for r in res] == exp
+    assert all(r[1] == 0 for r in res)
+    # corruption: flip bytes in 5 blocks, plus a wrong log number
+    cor = bytearray(data)
+    nb = len(res)
+    for b in rnd.sample(range(nb), min(5, nb)):
+        lo = b * 32768
+        cor[lo + rnd.randrange(0, min(32768, len(data) - lo))] ^= 0x10
+    dev2 = torch.frombuffer(bytearray(bytes(cor) + bytes(64)), dtype=torch.uint8).to("cuda")
+    res2 = [tuple(r) for r in S.wal_verify_batch(dev2, len(cor), 123).cpu().tolist()]
+    assert res2 == wal_expected_blocks(bytes(cor), 123, oracle)
+    res3 = [tuple(r) for r in S.wal_verify_batch(dev, len(data), 124).cpu().tolist()]
+    assert res3 == wal_expected_blocks(data, 124, oracle)
+
+
+def test_empty_and_zero_inputs(gpu, oracle):
+    import speedb_amd as S
+    torch = gpu
+    dev = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    out = S.crc32c_batch(S.Spans(dev, 0, stride=0, length=0))
+    assert out.numel() == 0
+    # ChecksumZeroInputs (table_test.cc:2405-2440): zero buffers never give 0
+    lens = list(range(0, 2000)) + list(range(2000, 20000, 37))
+    sp = spans(torch, S, dev, [0] * len(lens), lens)
+    for t in (1, 2, 3, 4):
+        got = u32(S.builtin_checksum_batch(t, sp))
+        for n, v in zip(lens, got):
+            assert v == oracle.Builtin(t, bytes(n))
+            assert v != 0 or (t == 4 and n == 0)
+
+
+def test_full_size_properties(gpu, oracle):
+    """1M x 4 KiB (the bench workload): sampled blocks bit-exact, uniform vs
+    explicit descriptors identical, and per-block CRCs combine to the CRC of
+    the whole buffer (checksum of checksums via Crc32cCombine)."""
+    import speedb_amd as S
+    torch = gpu
+    count, block = 1 << 20, 4096
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234)
+    dev = torch.randint(0, 256, (count * block,), dtype=torch.uint8, device="cuda", generator=g)
+    got = S.crc32c_batch(S.Spans.uniform(dev, block, count))
+    offs = torch.arange(count, dtype=torch.int64, device="cuda") * block
+    lens = torch.full((count,), block, dtype=torch.int32, device="cuda")
+    got2 = S.crc32c_batch(S.Spans(dev, count, offsets=offs, lengths=lens))
+    assert torch.equal(got, got2)
+    g_l = u32(got)
+    rnd = random.Random(5)
+    for i in rnd.sample(range(count), 200) + [0, count - 1]:
+        blk = dev[i * block:(i + 1) * block].cpu().numpy().tobytes()
+        assert g_l[i] == oracle.Value(blk)
+    # whole-buffer CRC of a 64 MiB prefix two ways: one span vs combine of blocks
+    n = 16384
+    whole = u32(S.crc32c_batch(S.Spans(dev, 1, stride=0, length=n * block)))[0]
+    acc = 0
+    for i in range(n):
+        acc = S.crc32c.Crc32cCombine(acc, g_l[i], block)
+    assert acc == whole
