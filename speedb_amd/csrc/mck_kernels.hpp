@@ -79,7 +79,8 @@ struct OpCrcValue {
   const uint32_t* init;
   uint32_t flags;
   uint32_t* out;
-  __device__ const uint8_t* ptr(uint32_t i) const { return s.ptr(i); }
+  __device__ const uint8_t* base() const { return s.base; }
+  __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return init ? init[i] : 0u; }
   __device__ void finish(uint32_t i, uint32_t crc, const uint8_t*) const {
@@ -96,7 +97,8 @@ struct OpCrcWal {
   const uint8_t* types;
   WalTypeCrcs tc;
   uint32_t* out;
-  __device__ const uint8_t* ptr(uint32_t i) const { return s.ptr(i); }
+  __device__ const uint8_t* base() const { return s.base; }
+  __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return tc.v[types[i] & 15]; }
   __device__ void finish(uint32_t i, uint32_t crc, const uint8_t*) const {
@@ -107,7 +109,8 @@ struct OpCrcWal {
 template <int MODE>
 struct OpCrcBlock {
   BlockArgs a;
-  __device__ const uint8_t* ptr(uint32_t i) const { return a.s.ptr(i); }
+  __device__ const uint8_t* base() const { return a.s.base; }
+  __device__ uint64_t off(uint32_t i) const { return a.s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return a.s.len(i) + (MODE == kModeVerify ? 1 : 0); }
   __device__ uint32_t init_crc(uint32_t) const { return 0u; }
   __device__ void finish(uint32_t i, uint32_t crc, const uint8_t* lds) const {
@@ -218,7 +221,7 @@ struct WalResult {
 
 __device__ __forceinline__ uint32_t crc_span_wave(const uint8_t* lds, const uint8_t* p, uint64_t n, uint32_t init,
                                                   const CrcLane& L) {
-  const CrcSpan sp = crc_span(p, n, init);
+  const CrcSpan sp = crc_span(lds, p, n, init);
   uint32_t s = 0;
   Chunk cur = crc_load_chunk(sp, sp.rounds - 1, L);
   for (int r = sp.rounds - 1; r >= 0; r--) {
