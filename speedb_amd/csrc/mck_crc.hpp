@@ -9,30 +9,35 @@
 //
 // Why it is exact (the algebra of util/crc32c.cc:1221-1266):
 //   * pure CRC (init 0, no inversion) is linear, and leading zero bytes do
-//     not change it, so bytes before the span are loaded as zeros;
+//     not change it;
 //   * Value/Extend's init state (~init_crc) sits at the span's first byte;
-//     it is injected into the owning lane's state at the enclosing 16-byte
-//     piece boundary, pre-un-shifted by the (ptr mod 16) bytes in between;
+//     it is injected into the "owner" lane's state at the start of its
+//     first-round chunk, pre-un-shifted by the hb < 64 bytes in between,
+//     which that lane zeroes; lanes whose first chunk lies wholly before the
+//     span drop their state after the first round;
 //   * bytes after the span (up to the aligned end) are zeros appended: the
-//     result is un-shifted by those k < 16 bytes with an inverse table;
+//     result is un-shifted by those kt < 16 bytes;
 //   * between a lane's chunks in consecutive rounds lie 4032 bytes owned by
 //     other lanes: the lane's state is advanced by zshift(., 4032).
-// A 16-byte-aligned span therefore runs with no masking and no divergence.
+// A span whose start is on the 64-byte grid and whose end is 16-aligned runs
+// with no masking and no divergence.
 //
-// LDS image (128 KiB per workgroup, filled once per persistent workgroup):
+// LDS image (160 KiB per workgroup, filled once per persistent workgroup):
 //   [0, 32K)       per-lane final shift, nibble tables [8][16][64 lanes];
 //   [32K, +512)    gap shift (4032 B), nibble tables [8][16];
 //   [+512, +512)   1-byte extend, nibble tables;
-//   [33K, 41K)     un-shift by k bytes, nibble tables [16][8][16];
 //   [64K, 128K)    4-byte-step byte tables, 16 interleaved copies: entry
 //                  (table t, byte v, copy c) at 64K | v<<8 | t<<6 | c<<2;
 //                  lane l reads copy l%16, so the address is ONE v_perm_b32
-//                  of the state and a per-lane constant, and lanes l, l+16
-//                  are the only possible bank sharers (<=2-way).
-// Nibble tables sit below 64 KiB so their offsets fold into ds_read
-// immediates; 16 entries in 16 distinct banks never conflict.
+//                  of the state and per-lane constants; with the per-lane
+//                  table rotation (crc_lane) every lookup is conflict-free;
+//   [128K, 160K)   un-shift by k < 64 bytes, nibble tables [64][8][16]
+//                  (k is wave-uniform: the base goes in an SGPR).
+// Fixed-offset nibble tables sit below 64 KiB so their offsets fold into
+// ds_read immediates; 16 entries in 16 distinct banks never conflict.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "mck_tables.hpp"
@@ -42,10 +47,13 @@ namespace mck {
 constexpr uint32_t kLdsFinal = 0;
 constexpr uint32_t kLdsGap = kLdsFinal + 32768;
 constexpr uint32_t kLdsExt1 = kLdsGap + 512;
-constexpr uint32_t kLdsUnshift = kLdsExt1 + 512;
-constexpr uint32_t kLdsNibEnd = kLdsUnshift + kMaxUnshift * 512;  // 41984
+constexpr uint32_t kLdsLowEnd = kLdsExt1 + 512;  // 33792
 constexpr uint32_t kLdsStep = 65536;
-constexpr uint32_t kCrcLdsBytes = kLdsStep + 65536;  // 131072
+constexpr uint32_t kLdsUnshift = 131072;
+constexpr uint32_t kCrcLdsBytes = kLdsUnshift + kMaxUnshift * 512;  // 163840
+
+static_assert(offsetof(CrcTables, gap) - offsetof(CrcTables, lane_final) == kLdsGap - kLdsFinal, "layout");
+static_assert(offsetof(CrcTables, unshift) - offsetof(CrcTables, lane_final) == kLdsLowEnd - kLdsFinal, "layout");
 
 struct alignas(16) Chunk {
   uint4 v[4];
@@ -55,7 +63,7 @@ struct alignas(16) Chunk {
 // at LDS address 0 and table addresses are absolute: reading through an
 // address_space(3) pointer built from the integer avoids re-adding the base.
 typedef __attribute__((address_space(3))) const uint32_t lds_word_t;
-__device__ __forceinline__ uint32_t lds_u32(const uint8_t*, uint32_t off) {
+__device__ __forceinline__ uint32_t lds_u32(uint32_t off) {
   return *reinterpret_cast<lds_word_t*>(static_cast<size_t>(off));
 }
 
@@ -75,97 +83,117 @@ __device__ __forceinline__ void crc_fill_lds(uint8_t* lds, const CrcTables* __re
   for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
     // 16-byte slot i covers word indices 4i..4i+3 = copies c..c+3 of
     // (t = (i >> 2) & 3, v = i >> 4)
-    uint32_t x = g->step[(i >> 2) & 3][i >> 4];
+    const uint32_t x = g->step[(i >> 2) & 3][i >> 4];
     l4[i] = make_uint4(x, x, x, x);
   }
-  const uint4* src = reinterpret_cast<const uint4*>(&g->lane_final[0][0][0]);
-  uint4* dst = reinterpret_cast<uint4*>(lds + kLdsFinal);
-  constexpr int n16 = (kLdsNibEnd - kLdsFinal) / 16;
-  static_assert(sizeof(CrcTables) - sizeof(CrcTables::step) == kLdsNibEnd - kLdsFinal, "layout");
-  for (int i = threadIdx.x; i < n16; i += blockDim.x) dst[i] = src[i];
+  const uint4* lo = reinterpret_cast<const uint4*>(&g->lane_final[0][0][0]);
+  uint4* dlo = reinterpret_cast<uint4*>(lds + kLdsFinal);
+  for (int i = threadIdx.x; i < (int)(kLdsLowEnd - kLdsFinal) / 16; i += blockDim.x) dlo[i] = lo[i];
+  const uint4* us = reinterpret_cast<const uint4*>(&g->unshift[0][0][0]);
+  uint4* dus = reinterpret_cast<uint4*>(lds + kLdsUnshift);
+  for (int i = threadIdx.x; i < kMaxUnshift * 512 / 16; i += blockDim.x) dus[i] = us[i];
 }
 
-// Per-lane constants for the v_perm address formation.
+// Per-lane constants for the v_perm address formation.  Lookup k of a step
+// reads table t = (k + h) & 3 with h = bit 4 of the lane id: within each
+// 32-lane LDS group, lanes 0-15 and 16-31 then always hit opposite halves
+// of the 32 banks (bank = (t & 1) * 16 + lane % 16), so all 32 lanes of the
+// group are on distinct banks -- conflict-free with only 16 table copies.
+// The v_perm selector (byte1 <- state byte t) is therefore per lane.
 struct CrcLane {
-  uint32_t pc[4];
-  uint32_t lane4;  // lane * 4
+  uint32_t pc[4];   // 64K | t << 6 | copy << 2
+  uint32_t sel[4];  // v_perm selector for table t
+  uint32_t lane4;   // lane * 4
   int lane;
 };
 __device__ __forceinline__ CrcLane crc_lane() {
   CrcLane L;
   L.lane = threadIdx.x & 63;
-  const uint32_t c = (uint32_t)(L.lane & 15);
+  const uint32_t c = (uint32_t)(L.lane & 15), h = (uint32_t)(L.lane >> 4) & 1u;
 #pragma unroll
-  for (int t = 0; t < 4; t++) L.pc[t] = kLdsStep | ((uint32_t)t << 6) | (c << 2);
+  for (int k = 0; k < 4; k++) {
+    const uint32_t t = ((uint32_t)k + h) & 3u;
+    L.pc[k] = kLdsStep | (t << 6) | (c << 2);
+    // byte0 <- pc.b0, byte1 <- state byte t, byte2 <- pc.b2 (=1), byte3 <- 0
+    L.sel[k] = 0x0C020000u | ((4u + t) << 8);
+  }
   L.lane4 = (uint32_t)L.lane << 2;
   return L;
 }
 
-// s' = zshift(s, 4): 4 byte-table lookups; address byte1 = state byte t,
-// byte0 = per-lane (table, copy) slot, byte2 = 1 (the 64 KiB region).
-__device__ __forceinline__ uint32_t crc_step4(const uint8_t* lds, uint32_t s, const CrcLane& L) {
-  const uint32_t a0 = __builtin_amdgcn_perm(s, L.pc[0], 0x0C020400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(s, L.pc[1], 0x0C020500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(s, L.pc[2], 0x0C020600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(s, L.pc[3], 0x0C020700u);
-  return lds_u32(lds, a0) ^ lds_u32(lds, a1) ^ lds_u32(lds, a2) ^ lds_u32(lds, a3);
+// s' = zshift(s, 4): 4 byte-table lookups, one v_perm_b32 address each.
+__device__ __forceinline__ uint32_t crc_step4(uint32_t s, const CrcLane& L) {
+  const uint32_t a0 = __builtin_amdgcn_perm(s, L.pc[0], L.sel[0]);
+  const uint32_t a1 = __builtin_amdgcn_perm(s, L.pc[1], L.sel[1]);
+  const uint32_t a2 = __builtin_amdgcn_perm(s, L.pc[2], L.sel[2]);
+  const uint32_t a3 = __builtin_amdgcn_perm(s, L.pc[3], L.sel[3]);
+  return lds_u32(a0) ^ lds_u32(a1) ^ lds_u32(a2) ^ lds_u32(a3);
 }
 
 // A linear map given as 8 nibble tables [8][16] at LDS offset `off`.
-__device__ __forceinline__ uint32_t crc_nibmap(const uint8_t* lds, uint32_t off, uint32_t s) {
-  uint32_t r = 0;
+__device__ __forceinline__ uint32_t crc_nibmap(uint32_t off, uint32_t s) {
+  uint32_t x[8];
 #pragma unroll
-  for (int n = 0; n < 8; n++) r ^= lds_u32(lds, off + n * 64 + (((s >> (4 * n)) & 15u) << 2));
-  return r;
+  for (int n = 0; n < 8; n++) x[n] = lds_u32(off + n * 64 + (((s >> (4 * n)) & 15u) << 2));
+  return (x[0] ^ x[1]) ^ (x[2] ^ x[3]) ^ ((x[4] ^ x[5]) ^ (x[6] ^ x[7]));
 }
 
 // zshift(s, 64*(63-lane)) with the per-lane tables.
-__device__ __forceinline__ uint32_t crc_lane_final(const uint8_t* lds, uint32_t s, const CrcLane& L) {
-  uint32_t r = 0;
+__device__ __forceinline__ uint32_t crc_lane_final(uint32_t s, const CrcLane& L) {
+  uint32_t x[8];
 #pragma unroll
-  for (int n = 0; n < 8; n++)
-    r ^= lds_u32(lds, kLdsFinal + n * 4096 + ((((s >> (4 * n)) & 15u) << 8) | L.lane4));
-  return r;
+  for (int n = 0; n < 8; n++) x[n] = lds_u32(kLdsFinal + n * 4096 + ((((s >> (4 * n)) & 15u) << 8) | L.lane4));
+  return (x[0] ^ x[1]) ^ (x[2] ^ x[3]) ^ ((x[4] ^ x[5]) ^ (x[6] ^ x[7]));
 }
 
+// XOR over the 64 lanes, returned wave-uniform: DPP butterfly inside each
+// 16-lane row (xor 1, xor 2, half-mirror, mirror), then the 4 row totals are
+// read out with v_readlane.  No LDS traffic.
 __device__ __forceinline__ uint32_t wave_xor32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v ^= __shfl_xor(v, o, 64);
-  return v;
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 16) ^
+         (uint32_t)__builtin_amdgcn_readlane((int)v, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
 
-// Un-shift by a wave-uniform k in [0, 16) bytes.
-__device__ __forceinline__ uint32_t crc_unshift(const uint8_t* lds, uint32_t k, uint32_t s) {
-  return crc_nibmap(lds, kLdsUnshift + k * 512, s);
+// Un-shift by a wave-uniform k in [0, 64) bytes.
+__device__ __forceinline__ uint32_t crc_unshift(uint32_t k, uint32_t s) {
+  return crc_nibmap(kLdsUnshift + k * 512, s);
 }
 
 // Geometry of one span under the end-anchored round grid.
 struct CrcSpan {
   uint64_t ptr;    // first byte
   uint64_t end;    // one past last byte
-  uint64_t a0;     // ptr rounded down to 16
+  uint64_t a0;     // ptr rounded down to 16 (lowest address ever loaded)
   uint64_t a1;     // end rounded up to 16
-  int32_t rounds;  // number of 4 KiB rounds covering [a0, a1)
-  uint32_t head;   // ptr - a0: leading bytes of the first piece to zero
+  int32_t rounds;  // 4 KiB rounds covering [ptr, a1)
+  int32_t owner;   // lane whose first-round chunk holds ptr
+  uint32_t hb;     // ptr - owner's chunk start: bytes the owner zeroes
   uint32_t kt;     // a1 - end: trailing zero bytes to un-shift
-  uint32_t inj;    // init state, un-shifted to the piece boundary a0
+  uint32_t inj;    // init state, un-shifted by hb bytes
   uint32_t init_crc;
   bool empty;      // n == 0: Extend(init, "") = init
 };
 
-__device__ __forceinline__ CrcSpan crc_span(const uint8_t* lds, const uint8_t* p, uint64_t n, uint32_t init_crc) {
+__device__ __forceinline__ CrcSpan crc_span(const uint8_t* p, uint64_t n, uint32_t init_crc) {
   CrcSpan s;
   s.ptr = reinterpret_cast<uint64_t>(p);
   s.end = s.ptr + n;
   s.a0 = s.ptr & ~15ull;
   s.a1 = (s.end + 15) & ~15ull;
   s.empty = n == 0;
-  s.rounds = s.empty ? 1 : (int32_t)((s.a1 - s.a0 + kRoundBytes - 1) / kRoundBytes);
-  s.head = (uint32_t)(s.ptr - s.a0);
+  const uint64_t cover = s.a1 - s.ptr;  // > 0 unless empty
+  s.rounds = s.empty ? 1 : (int32_t)((cover + kRoundBytes - 1) / kRoundBytes);
+  const uint32_t lead = (uint32_t)((uint64_t)kRoundBytes * s.rounds - cover);  // base0 .. ptr
+  s.owner = s.empty ? 64 : (int32_t)(lead >> 6);
+  s.hb = lead & 63u;
   s.kt = (uint32_t)(s.a1 - s.end);
   s.init_crc = init_crc;
   s.inj = ~init_crc;
-  if (s.head) s.inj = crc_unshift(lds, s.head, s.inj);  // wave-uniform branch
+  if (s.hb) s.inj = crc_unshift(s.hb, s.inj);  // wave-uniform branch
   return s;
 }
 
@@ -173,87 +201,98 @@ __device__ __forceinline__ uint64_t crc_chunk_base(const CrcSpan& sp, int r, con
   return sp.a1 - (uint64_t)kRoundBytes * (r + 1) + (uint64_t)L.lane * kChunkBytes;
 }
 
-// Branch-free so the compiler can count outstanding loads (a load under an
-// exec-masked branch makes every later wait a vmcnt(0) and kills the
-// prefetch): pieces wholly before the span load from a0 instead and are
-// zeroed by a select.
+// Loads stay outside branches so the compiler can count them (a load under
+// an exec-masked branch turns later waits into vmcnt(0) and kills the
+// prefetch).  In the first round, pieces below a0 read a0 instead (their
+// data is discarded); only the address computation is branched, uniformly.
 __device__ __forceinline__ Chunk crc_load_chunk(const CrcSpan& sp, int r, const CrcLane& L) {
-  Chunk c;
   const uint64_t cb = crc_chunk_base(sp, r, L);
+  uint64_t pa[4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    const uint64_t pa = cb + 16 * j;
-    const bool ok = !sp.empty && pa >= sp.a0;
-    const uint4 v = gload16(ok ? pa : sp.a0);
-    c.v[j] = ok ? v : make_uint4(0, 0, 0, 0);
+  for (int j = 0; j < 4; j++) pa[j] = cb + 16 * j;
+  if (r == sp.rounds - 1 && (sp.owner > 0 || sp.hb >= 16 || sp.empty)) {
+#pragma unroll
+    for (int j = 0; j < 4; j++) pa[j] = pa[j] < sp.a0 ? sp.a0 : pa[j];
   }
+  Chunk c;
+#pragma unroll
+  for (int j = 0; j < 4; j++) c.v[j] = gload16(pa[j]);
   return c;
 }
 
-// keep bytes [lo, hi) of a 16-byte piece, zero the rest
-__device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int k, int lo, int hi) {
-  const int a = lo - 4 * k, b = hi - 4 * k;  // keep [a, b) of this word
-  uint64_t m = 0xFFFFFFFFull;
-  if (a > 0) m = a >= 4 ? 0 : (m << (8 * a)) & 0xFFFFFFFFull;
-  if (b < 4) m = b <= 0 ? 0 : m & (0xFFFFFFFFull >> (8 * (4 - b)));
-  return w & (uint32_t)m;
+// zero bytes [0, hb) of a chunk (hb < 64): the owner lane's bytes before ptr
+__device__ __forceinline__ void crc_zero_head(Chunk& c, uint32_t hb) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&c.v[j]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int b = 16 * j + 4 * q;  // first byte of this word
+      const int z = (int)hb - b;     // bytes of this word to zero
+      w[q] = z <= 0 ? w[q] : z >= 4 ? 0u : w[q] & (0xFFFFFFFFu << (8 * z));
+    }
+  }
 }
-__device__ __forceinline__ void keep_piece(uint4& v, int lo, int hi) {
-  v.x = keep_bytes(v.x, 0, lo, hi);
-  v.y = keep_bytes(v.y, 1, lo, hi);
-  v.z = keep_bytes(v.z, 2, lo, hi);
-  v.w = keep_bytes(v.w, 3, lo, hi);
+// keep the first `keep` (1..15) bytes of a 16-byte piece
+__device__ __forceinline__ void crc_keep_head_bytes(uint4& v, uint32_t keep) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int k = (int)keep - 4 * q;
+    w[q] = k >= 4 ? w[q] : k <= 0 ? 0u : w[q] & (0xFFFFFFFFu >> (8 * (4 - k)));
+  }
 }
 
-__device__ __forceinline__ uint32_t crc_piece(const uint8_t* lds, uint32_t s, const uint4& v, const CrcLane& L) {
+__device__ __forceinline__ uint32_t crc_piece(uint32_t s, const uint4& v, const CrcLane& L) {
   s ^= v.x;
-  s = crc_step4(lds, s, L);
+  s = crc_step4(s, L);
   s ^= v.y;
-  s = crc_step4(lds, s, L);
+  s = crc_step4(s, L);
   s ^= v.z;
-  s = crc_step4(lds, s, L);
+  s = crc_step4(s, L);
   s ^= v.w;
-  s = crc_step4(lds, s, L);
+  s = crc_step4(s, L);
   return s;
 }
 
 // Advance one lane over its chunk of round r.
-__device__ __forceinline__ uint32_t crc_round(const uint8_t* lds, uint32_t s, Chunk c, const CrcSpan& sp, int r,
-                                              const CrcLane& L) {
-  if (r != sp.rounds - 1) s = crc_nibmap(lds, kLdsGap, s);  // wave-uniform
-  const uint64_t cb = crc_chunk_base(sp, r, L);
-  // piece (0..3) of this chunk that starts at a0, or out of range
-  const int64_t jh = (int64_t)(sp.a0 - cb) >> 4;
-  if (sp.head && jh >= 0 && jh < 4) {  // unaligned start: one lane, once
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      if (j == jh) keep_piece(c.v[j], (int)sp.head, 16);
+__device__ __forceinline__ uint32_t crc_round(uint32_t s, Chunk c, const CrcSpan& sp, int r, const CrcLane& L) {
+  const bool first = r == sp.rounds - 1;  // wave-uniform
+  if (first) {
+    s = L.lane == sp.owner ? sp.inj : 0u;
+    if (sp.hb && L.lane == sp.owner) crc_zero_head(c, sp.hb);  // one lane, unaligned starts
+  } else {
+    s = crc_nibmap(kLdsGap, s);
   }
-  if (sp.kt && r == 0 && L.lane == 63) keep_piece(c.v[3], 0, 16 - (int)sp.kt);  // unaligned end
-  const uint32_t inj = sp.empty ? 0u : sp.inj;
+  if (sp.kt && r == 0 && L.lane == 63) crc_keep_head_bytes(c.v[3], 16 - sp.kt);  // unaligned end
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    s ^= jh == j ? inj : 0u;
-    s = crc_piece(lds, s, c.v[j], L);
-  }
+  for (int j = 0; j < 4; j++) s = crc_piece(s, c.v[j], L);
+  if (first) s = L.lane < sp.owner ? 0u : s;  // chunks wholly before the span
   return s;
 }
 
 // Combine the lanes' states into the span's CRC (Extend semantics).  Every
 // lane returns the same value.
-__device__ __forceinline__ uint32_t crc_finish(const uint8_t* lds, uint32_t s, const CrcSpan& sp,
-                                               const CrcLane& L) {
-  uint32_t p = wave_xor32(crc_lane_final(lds, s, L));
-  if (sp.kt) p = crc_unshift(lds, sp.kt, p);
+__device__ __forceinline__ uint32_t crc_finish(uint32_t s, const CrcSpan& sp, const CrcLane& L) {
+  uint32_t p = wave_xor32(crc_lane_final(s, L));
+  if (sp.kt) p = crc_unshift(sp.kt, p);
   return sp.empty ? sp.init_crc : ~p;
 }
 
 // CRC Extend by one byte on a finished CRC value (all lanes identical).
-__device__ __forceinline__ uint32_t crc_extend_byte(const uint8_t* lds, uint32_t crc, uint8_t b) {
-  return ~crc_nibmap(lds, kLdsExt1, ~crc ^ (uint32_t)b);
+__device__ __forceinline__ uint32_t crc_extend_byte(uint32_t crc, uint8_t b) {
+  return ~crc_nibmap(kLdsExt1, ~crc ^ (uint32_t)b);
 }
 
 __device__ __forceinline__ uint32_t crc_mask(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
+
+// v_readlane returns int: widen through uint32_t, never sign-extend.
+__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, uint32_t k) {
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));
+}
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t k) {
+  return ((uint64_t)readlane_u32((uint32_t)(v >> 32), k) << 32) | (uint64_t)readlane_u32((uint32_t)v, k);
+}
 
 // Persistent, software-pipelined driver: each wave walks (span, round) pairs
 // of spans wave_id, wave_id + nwaves, ...; the next pair's chunk is loaded
@@ -263,7 +302,7 @@ __device__ __forceinline__ uint32_t crc_mask(uint32_t c) { return ((c >> 15) | (
 // Op supplies the spans and consumes the results:
 //   const uint8_t* Op::base(), uint64_t Op::off(i), uint64_t Op::len(i),
 //   uint32_t Op::init_crc(i)                    (per lane, i < count)
-//   void Op::finish(i, crc, lds)   (all lanes call it; lane 0 writes)
+//   void Op::finish(i, crc)   (all lanes call it; lane 0 writes)
 struct SpanDesc {
   uint64_t off;
   uint64_t len;
@@ -281,13 +320,6 @@ __device__ __forceinline__ SpanDesc crc_desc_fetch(const Op& op, uint32_t first,
     d.init = op.init_crc((uint32_t)i);
   }
   return d;
-}
-// v_readlane returns int: widen through uint32_t, never sign-extend.
-__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, uint32_t k) {
-  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));
-}
-__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t k) {
-  return ((uint64_t)readlane_u32((uint32_t)(v >> 32), k) << 32) | (uint64_t)readlane_u32((uint32_t)v, k);
 }
 __device__ __forceinline__ SpanDesc crc_desc_pick(const SpanDesc& d, uint32_t k) {
   SpanDesc r;
@@ -312,7 +344,7 @@ __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, u
   uint32_t k = 0;     // its slot in the descriptor batch
   SpanDesc db = crc_desc_fetch(op, i, nwaves, count, L);
   SpanDesc d = crc_desc_pick(db, 0);
-  CrcSpan sp = crc_span(lds, reinterpret_cast<const uint8_t*>(base + d.off), d.len, d.init);
+  CrcSpan sp = crc_span(reinterpret_cast<const uint8_t*>(base + d.off), d.len, d.init);
   int r = sp.rounds - 1;
   Chunk cur = crc_load_chunk(sp, r, L);
   uint32_t s = 0;
@@ -331,18 +363,15 @@ __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, u
           nk = 0;
         }
         const SpanDesc nd = crc_desc_pick(db, nk);
-        nsp = crc_span(lds, reinterpret_cast<const uint8_t*>(base + nd.off), nd.len, nd.init);
+        nsp = crc_span(reinterpret_cast<const uint8_t*>(base + nd.off), nd.len, nd.init);
         nr = nsp.rounds - 1;
       }
     }
     // unconditional (see crc_load_chunk); after the last round it re-reads
     // the current chunk, which is never used
     const Chunk nxt = crc_load_chunk(more ? nsp : sp, more ? nr : r, L);
-    s = crc_round(lds, s, cur, sp, r, L);
-    if (r == 0) {
-      op.finish(i, crc_finish(lds, s, sp, L), lds);
-      s = 0;
-    }
+    s = crc_round(s, cur, sp, r, L);
+    if (r == 0) op.finish(i, crc_finish(s, sp, L));
     if (!more) break;
     i = ni;
     k = nk;

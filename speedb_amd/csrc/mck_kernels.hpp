@@ -83,7 +83,7 @@ struct OpCrcValue {
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return init ? init[i] : 0u; }
-  __device__ void finish(uint32_t i, uint32_t crc, const uint8_t*) const {
+  __device__ void finish(uint32_t i, uint32_t crc) const {
     if ((threadIdx.x & 63) == 0) out[i] = (flags & 1u) ? crc_mask(crc) : crc;
   }
 };
@@ -101,7 +101,7 @@ struct OpCrcWal {
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return tc.v[types[i] & 15]; }
-  __device__ void finish(uint32_t i, uint32_t crc, const uint8_t*) const {
+  __device__ void finish(uint32_t i, uint32_t crc) const {
     if ((threadIdx.x & 63) == 0) out[i] = crc_mask(crc);
   }
 };
@@ -113,8 +113,8 @@ struct OpCrcBlock {
   __device__ uint64_t off(uint32_t i) const { return a.s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return a.s.len(i) + (MODE == kModeVerify ? 1 : 0); }
   __device__ uint32_t init_crc(uint32_t) const { return 0u; }
-  __device__ void finish(uint32_t i, uint32_t crc, const uint8_t* lds) const {
-    if (MODE == kModeTrailer || (MODE == kModeBuiltin && a.last)) crc = crc_extend_byte(lds, crc, a.last[i]);
+  __device__ void finish(uint32_t i, uint32_t crc) const {
+    if (MODE == kModeTrailer || (MODE == kModeBuiltin && a.last)) crc = crc_extend_byte(crc, a.last[i]);
     if ((threadIdx.x & 63) == 0) block_epilogue<MODE>(a, i, crc_mask(crc));
   }
 };
@@ -219,18 +219,16 @@ struct WalResult {
   uint32_t bytes_ok;
 };
 
-__device__ __forceinline__ uint32_t crc_span_wave(const uint8_t* lds, const uint8_t* p, uint64_t n, uint32_t init,
-                                                  const CrcLane& L) {
-  const CrcSpan sp = crc_span(lds, p, n, init);
+__device__ __forceinline__ uint32_t crc_span_wave(const uint8_t* p, uint64_t n, uint32_t init, const CrcLane& L) {
+  const CrcSpan sp = crc_span(p, n, init);
   uint32_t s = 0;
   Chunk cur = crc_load_chunk(sp, sp.rounds - 1, L);
   for (int r = sp.rounds - 1; r >= 0; r--) {
-    Chunk nxt;
-    if (r > 0) nxt = crc_load_chunk(sp, r - 1, L);
-    s = crc_round(lds, s, cur, sp, r, L);
+    const Chunk nxt = crc_load_chunk(sp, r > 0 ? r - 1 : 0, L);
+    s = crc_round(s, cur, sp, r, L);
     cur = nxt;
   }
-  return crc_finish(lds, s, sp, L);
+  return crc_finish(s, sp, L);
 }
 
 __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_t nbytes, uint32_t log_number,
@@ -280,7 +278,7 @@ __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_
         break;
       }
       const uint32_t stored = rd32_bytes(h);
-      const uint32_t actual = crc_span_wave(lds, h + 6, length + hsize - 6, 0u, L);
+      const uint32_t actual = crc_span_wave(h + 6, length + hsize - 6, 0u, L);
       // Unmask(stored) == actual  <=>  stored == Mask(actual)
       if (crc_mask(actual) != stored) {
         status = 1;  // kBadRecordChecksum

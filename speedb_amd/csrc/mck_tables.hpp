@@ -18,7 +18,7 @@ constexpr uint32_t kCrc32cPoly = 0x82f63b78u;  // reflected
 constexpr int kChunkBytes = 64;
 constexpr int kRoundBytes = 64 * kChunkBytes;                   // 4096
 constexpr int kGapBytes = kRoundBytes - kChunkBytes;            // 4032
-constexpr int kMaxUnshift = 16;                                 // k in [0,16)
+constexpr int kMaxUnshift = 64;                                 // k in [0,64)
 
 struct CrcTables {
   uint32_t step[4][256];          // zshift(v << 8t, 4): the 4-byte step
