@@ -1,0 +1,264 @@
+// checksum.hpp -- C++ host-side mirror of the reference's block-checksum
+// interface, implemented over the engine's C ABI (mck.h).
+//
+// A Speedb/RocksDB build re-points its call sites at these names (see
+// INTEGRATION.md); signatures, argument meaning and error behaviour follow
+// the reference:
+//   crc32c::Value / Extend / Mask / Unmask / Crc32cCombine  util/crc32c.h:21-53
+//   XXH3_64bits                                             util/xxhash.h:5329
+//   ChecksumType                                            include/rocksdb/table.h:69-75
+//   ComputeBuiltinChecksum[WithLastByte]                    table/format.cc:578-645
+//   ChecksumModifierForContext                              table/format.h:119-146
+//   VerifyBlockChecksum                                     table/block_based/reader_common.cc:26-63
+//   log::EmitPhysicalRecord's header CRC                    db/log_writer.cc:263-311
+// plus the batched entry points the reference lacks (VerifyBlockChecksums
+// for RetrieveMultipleBlocks / VerifyChecksumInBlocks, block trailer
+// generation for a run of blocks, whole-WAL verification).
+//
+// Header-only; link against speedb_amd/libspeedb_amd.so.
+#pragma once
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "mck.h"
+
+namespace speedb_amd {
+
+// include/rocksdb/table.h:69-75
+enum ChecksumType : char {
+  kNoChecksum = 0x0,
+  kCRC32c = 0x1,
+  kxxHash = 0x2,
+  kxxHash64 = 0x3,
+  kXXH3 = 0x4,
+};
+
+// The slice of rocksdb::Status this path produces.
+class Status {
+ public:
+  Status() = default;
+  static Status OK() { return Status(); }
+  static Status Corruption(const std::string& msg) { return Status(kCorruption, msg); }
+  static Status InvalidArgument(const std::string& msg) { return Status(kInvalidArgument, msg); }
+  static Status IOError(const std::string& msg) { return Status(kIOError, msg); }
+  bool ok() const { return code_ == kOk; }
+  bool IsCorruption() const { return code_ == kCorruption; }
+  bool IsInvalidArgument() const { return code_ == kInvalidArgument; }
+  std::string ToString() const {
+    switch (code_) {
+      case kOk:
+        return "OK";
+      case kCorruption:
+        return "Corruption: " + msg_;
+      case kInvalidArgument:
+        return "Invalid argument: " + msg_;
+      default:
+        return "IO error: " + msg_;
+    }
+  }
+
+ private:
+  enum Code { kOk, kCorruption, kInvalidArgument, kIOError };
+  Status(Code c, const std::string& m) : code_(c), msg_(m) {}
+  Code code_ = kOk;
+  std::string msg_;
+};
+
+inline Status FromRc(int rc, const char* what) {
+  if (rc == MCK_OK) return Status::OK();
+  std::string m = std::string(what) + ": " + mck_last_error();
+  return rc == MCK_EINVAL ? Status::InvalidArgument(m) : Status::IOError(m);
+}
+
+namespace crc32c {
+static const uint32_t kMaskDelta = 0xa282ead8ul;
+inline uint32_t Extend(uint32_t init_crc, const char* data, size_t n) { return mck_crc32c_extend(init_crc, data, n); }
+inline uint32_t Value(const char* data, size_t n) { return mck_crc32c_value(data, n); }
+inline uint32_t Mask(uint32_t crc) { return mck_crc32c_mask(crc); }
+inline uint32_t Unmask(uint32_t masked_crc) { return mck_crc32c_unmask(masked_crc); }
+inline uint32_t Crc32cCombine(uint32_t crc1, uint32_t crc2, size_t crc2len) {
+  return mck_crc32c_combine(crc1, crc2, crc2len);
+}
+}  // namespace crc32c
+
+inline uint64_t XXH3_64bits(const void* data, size_t n) { return mck_xxh3_64(data, n); }
+
+inline uint32_t ComputeBuiltinChecksum(ChecksumType type, const char* data, size_t data_size) {
+  return mck_builtin_checksum(type, data, data_size);
+}
+inline uint32_t ComputeBuiltinChecksumWithLastByte(ChecksumType type, const char* data, size_t data_size,
+                                                   char last_byte) {
+  return mck_builtin_checksum_with_last_byte(type, data, data_size, last_byte);
+}
+inline uint32_t ChecksumModifierForContext(uint32_t base_context_checksum, uint64_t offset) {
+  return mck_context_modifier(base_context_checksum, offset);
+}
+
+inline uint32_t DecodeFixed32(const char* p) {
+  const unsigned char* u = reinterpret_cast<const unsigned char*>(p);
+  return (uint32_t)u[0] | ((uint32_t)u[1] << 8) | ((uint32_t)u[2] << 16) | ((uint32_t)u[3] << 24);
+}
+
+// The two footer fields VerifyBlockChecksum reads (table/format.h Footer).
+struct Footer {
+  ChecksumType checksum_type = kXXH3;
+  uint32_t base_context_checksum = 0;
+};
+
+inline Status BlockChecksumMismatch(ChecksumType type, uint32_t stored, uint32_t computed, bool context,
+                                    const std::string& file_name, uint64_t offset, size_t block_size) {
+  if (type == kCRC32c) {  // reader_common.cc:51-55: unmask for people
+    stored = crc32c::Unmask(stored);
+    computed = crc32c::Unmask(computed);
+  }
+  return Status::Corruption("block checksum mismatch: stored" + std::string(context ? "(context removed)" : "") +
+                            " = " + std::to_string(stored) + ", computed = " + std::to_string(computed) +
+                            ", type = " + std::to_string((int)type) + "  in " + file_name + " offset " +
+                            std::to_string(offset) + " size " + std::to_string(block_size));
+}
+
+// table/block_based/reader_common.cc:26-63.  data = block payload followed by
+// its 5-byte trailer, host memory.
+inline Status VerifyBlockChecksum(const Footer& footer, const char* data, size_t block_size,
+                                  const std::string& file_name, uint64_t offset) {
+  const ChecksumType type = footer.checksum_type;
+  const size_t len = block_size + 1;
+  uint32_t stored = DecodeFixed32(data + len);
+  const uint32_t computed = ComputeBuiltinChecksum(type, data, len);
+  const uint32_t modifier = ChecksumModifierForContext(footer.base_context_checksum, offset);
+  stored -= modifier;
+  if (stored == computed) return Status::OK();
+  return BlockChecksumMismatch(type, stored, computed, modifier != 0, file_name, offset, block_size);
+}
+
+// A block handle (table/format.h BlockHandle): payload offset and size.
+struct BlockHandle {
+  uint64_t offset;
+  uint64_t size;
+};
+
+// Batched read-side verify: the caller has the blocks' bytes (payload +
+// trailer, at handle.offset - file_base) in device memory, e.g. the buffer a
+// MultiRead filled (table/block_based/block_based_table_reader_sync_and_async.h
+// :217-228 verifies these one by one).  Writes one Status per block; returns
+// the first non-OK status (or OK).
+inline Status VerifyBlockChecksums(const Footer& footer, const void* dev_image, uint64_t file_base,
+                                   const std::vector<BlockHandle>& handles, const std::string& file_name,
+                                   std::vector<Status>* per_block, mck_stream_t stream = nullptr);
+
+namespace log {
+// db/log_format.h:22-45
+enum RecordType {
+  kZeroType = 0,
+  kFullType = 1,
+  kFirstType = 2,
+  kMiddleType = 3,
+  kLastType = 4,
+  kRecyclableFullType = 5,
+  kRecyclableFirstType = 6,
+  kRecyclableMiddleType = 7,
+  kRecyclableLastType = 8,
+  kSetCompressionType = 9,
+  kUserDefinedTimestampSizeType = 10,
+  kRecyclableUserDefinedTimestampSizeType = 11,
+};
+constexpr unsigned int kBlockSize = MCK_WAL_kBlockSize;
+constexpr int kHeaderSize = MCK_WAL_kHeaderSize;
+constexpr int kRecyclableHeaderSize = MCK_WAL_kRecyclableHeaderSize;
+
+inline bool IsRecyclable(unsigned t) {
+  return (t >= kRecyclableFullType && t <= kRecyclableLastType) || t == kRecyclableUserDefinedTimestampSizeType;
+}
+
+// db/log_writer.cc:281-298: the masked header CRC of one physical record.
+inline uint32_t PhysicalRecordCrc(RecordType t, const char* payload, size_t n, uint64_t log_number) {
+  const char type_byte = static_cast<char>(t);
+  uint32_t crc = crc32c::Value(&type_byte, 1);
+  if (IsRecyclable(t)) {
+    char buf[4];
+    const uint32_t ln = static_cast<uint32_t>(log_number);
+    for (int i = 0; i < 4; i++) buf[i] = static_cast<char>(ln >> (8 * i));
+    crc = crc32c::Extend(crc, buf, 4);
+  }
+  const uint32_t payload_crc = crc32c::Value(payload, n);
+  crc = crc32c::Crc32cCombine(crc, payload_crc, n);
+  return crc32c::Mask(crc);
+}
+}  // namespace log
+
+// ---------------------------------------------------------------------------
+// inline definitions of the batched helpers (need HIP for device buffers)
+// ---------------------------------------------------------------------------
+}  // namespace speedb_amd
+
+#include <hip/hip_runtime_api.h>
+
+namespace speedb_amd {
+
+inline Status VerifyBlockChecksums(const Footer& footer, const void* dev_image, uint64_t file_base,
+                                   const std::vector<BlockHandle>& handles, const std::string& file_name,
+                                   std::vector<Status>* per_block, mck_stream_t stream) {
+  const uint32_t n = static_cast<uint32_t>(handles.size());
+  if (per_block) per_block->assign(n, Status::OK());
+  if (!n) return Status::OK();
+  std::vector<uint64_t> offs(n), foffs(n);
+  std::vector<uint32_t> lens(n);
+  for (uint32_t i = 0; i < n; i++) {
+    offs[i] = handles[i].offset - file_base;
+    foffs[i] = handles[i].offset;
+    lens[i] = static_cast<uint32_t>(handles[i].size);
+  }
+  uint64_t *d_off = nullptr, *d_foff = nullptr;
+  uint32_t *d_len = nullptr, *d_comp = nullptr, *d_stored = nullptr, *d_cnt = nullptr;
+  uint8_t* d_mm = nullptr;
+  auto cleanup = [&] {
+    (void)hipFree(d_off);
+    (void)hipFree(d_foff);
+    (void)hipFree(d_len);
+    (void)hipFree(d_comp);
+    (void)hipFree(d_stored);
+    (void)hipFree(d_cnt);
+    (void)hipFree(d_mm);
+  };
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMalloc(&d_off, n * 8) != hipSuccess || hipMalloc(&d_foff, n * 8) != hipSuccess ||
+      hipMalloc(&d_len, n * 4) != hipSuccess || hipMalloc(&d_comp, n * 4) != hipSuccess ||
+      hipMalloc(&d_stored, n * 4) != hipSuccess || hipMalloc(&d_cnt, 4) != hipSuccess ||
+      hipMalloc(&d_mm, n) != hipSuccess) {
+    cleanup();
+    return Status::IOError("hipMalloc failed");
+  }
+  (void)hipMemcpyAsync(d_off, offs.data(), n * 8, hipMemcpyHostToDevice, st);
+  (void)hipMemcpyAsync(d_foff, foffs.data(), n * 8, hipMemcpyHostToDevice, st);
+  (void)hipMemcpyAsync(d_len, lens.data(), n * 4, hipMemcpyHostToDevice, st);
+  (void)hipMemsetAsync(d_cnt, 0, 4, st);
+  const mck_spans sp{dev_image, d_off, d_len, 0, 0, n};
+  int rc = mck_sst_verify_batch(footer.checksum_type, &sp, d_foff, footer.base_context_checksum, d_mm, d_comp,
+                                d_stored, d_cnt, stream);
+  if (rc) {
+    cleanup();
+    return FromRc(rc, "mck_sst_verify_batch");
+  }
+  std::vector<uint8_t> mm(n);
+  std::vector<uint32_t> comp(n), stored(n);
+  (void)hipMemcpyAsync(mm.data(), d_mm, n, hipMemcpyDeviceToHost, st);
+  (void)hipMemcpyAsync(comp.data(), d_comp, n * 4, hipMemcpyDeviceToHost, st);
+  (void)hipMemcpyAsync(stored.data(), d_stored, n * 4, hipMemcpyDeviceToHost, st);
+  const hipError_t e = hipStreamSynchronize(st);
+  cleanup();
+  if (e != hipSuccess) return Status::IOError(hipGetErrorString(e));
+  Status first;
+  for (uint32_t i = 0; i < n; i++) {
+    if (!mm[i]) continue;
+    const bool ctx = ChecksumModifierForContext(footer.base_context_checksum, handles[i].offset) != 0;
+    Status s = BlockChecksumMismatch(footer.checksum_type, stored[i], comp[i], ctx, file_name, handles[i].offset,
+                                     handles[i].size);
+    if (first.ok()) first = s;
+    if (per_block) (*per_block)[i] = s;
+  }
+  return first;
+}
+
+}  // namespace speedb_amd

@@ -208,6 +208,7 @@ static void report(const char* name, double ms, size_t bytes) {
   fflush(stdout);
 }
 
+#ifndef MB_NO_MAIN
 int main(int argc, char** argv) {
   size_t nblk = argc > 1 ? strtoull(argv[1], 0, 10) : (1u << 20);
   int reps = argc > 2 ? atoi(argv[2]) : 10;
@@ -294,3 +295,4 @@ int main(int argc, char** argv) {
   printf("fails=%d\n", fails);
   return fails ? 1 : 0;
 }
+#endif

@@ -26,6 +26,8 @@
 //   [0, 32K)       per-lane final shift, nibble tables [8][16][64 lanes];
 //   [32K, +512)    gap shift (4032 B), nibble tables [8][16];
 //   [+512, +512)   1-byte extend, nibble tables;
+//   [+512, +512)   32-byte shift, nibble tables (joins a lane's chains);
+//   [+512, +512)   16-byte shift, nibble tables;
 //   [64K, 128K)    4-byte-step byte tables, 16 interleaved copies: entry
 //                  (table t, byte v, copy c) at 64K | v<<8 | t<<6 | c<<2;
 //                  lane l reads copy l%16, so the address is ONE v_perm_b32
@@ -47,7 +49,16 @@ namespace mck {
 constexpr uint32_t kLdsFinal = 0;
 constexpr uint32_t kLdsGap = kLdsFinal + 32768;
 constexpr uint32_t kLdsExt1 = kLdsGap + 512;
-constexpr uint32_t kLdsLowEnd = kLdsExt1 + 512;  // 33792
+constexpr uint32_t kLdsHalf = kLdsExt1 + 512;
+constexpr uint32_t kLdsQuarter = kLdsHalf + 512;
+constexpr uint32_t kLdsLowEnd = kLdsQuarter + 512;  // 34816
+
+// Independent lookup chains per lane and round (1, 2 or 4); see crc_round.
+#ifndef MCK_CRC_CHAINS
+#define MCK_CRC_CHAINS 2
+#endif
+constexpr int kCrcChains = MCK_CRC_CHAINS;
+static_assert(kCrcChains == 1 || kCrcChains == 2 || kCrcChains == 4, "chains");
 constexpr uint32_t kLdsStep = 65536;
 constexpr uint32_t kLdsUnshift = 131072;
 constexpr uint32_t kCrcLdsBytes = kLdsUnshift + kMaxUnshift * 512;  // 163840
@@ -243,30 +254,41 @@ __device__ __forceinline__ void crc_keep_head_bytes(uint4& v, uint32_t keep) {
   }
 }
 
-__device__ __forceinline__ uint32_t crc_piece(uint32_t s, const uint4& v, const CrcLane& L) {
-  s ^= v.x;
-  s = crc_step4(s, L);
-  s ^= v.y;
-  s = crc_step4(s, L);
-  s ^= v.z;
-  s = crc_step4(s, L);
-  s ^= v.w;
-  s = crc_step4(s, L);
-  return s;
-}
-
-// Advance one lane over its chunk of round r.
+// Advance one lane over its chunk of round r.  The chunk is hashed as
+// kCrcChains interleaved chains over consecutive 64/kCrcChains-byte parts,
+// so each lane keeps that many independent LDS lookup chains in flight (the
+// per-lane work is latency-bound on the chain), joined at the end of the
+// round by zshift(part state, bytes after the part) and XOR.
 __device__ __forceinline__ uint32_t crc_round(uint32_t s, Chunk c, const CrcSpan& sp, int r, const CrcLane& L) {
   const bool first = r == sp.rounds - 1;  // wave-uniform
+  uint32_t x[kCrcChains];
   if (first) {
-    s = L.lane == sp.owner ? sp.inj : 0u;
+    x[0] = L.lane == sp.owner ? sp.inj : 0u;
     if (sp.hb && L.lane == sp.owner) crc_zero_head(c, sp.hb);  // one lane, unaligned starts
   } else {
-    s = crc_nibmap(kLdsGap, s);
+    x[0] = crc_nibmap(kLdsGap, s);
   }
   if (sp.kt && r == 0 && L.lane == 63) crc_keep_head_bytes(c.v[3], 16 - sp.kt);  // unaligned end
 #pragma unroll
-  for (int j = 0; j < 4; j++) s = crc_piece(s, c.v[j], L);
+  for (int q = 1; q < kCrcChains; q++) x[q] = 0;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&c.v[0]);
+  constexpr int kWords = 16 / kCrcChains;  // words per chain
+#pragma unroll
+  for (int i = 0; i < kWords; i++) {
+#pragma unroll
+    for (int q = 0; q < kCrcChains; q++) x[q] ^= w[q * kWords + i];
+#pragma unroll
+    for (int q = 0; q < kCrcChains; q++) x[q] = crc_step4(x[q], L);
+  }
+  if (kCrcChains == 1) {
+    s = x[0];
+  } else if (kCrcChains == 2) {
+    s = crc_nibmap(kLdsHalf, x[0]) ^ x[1];
+  } else {
+    const uint32_t t0 = crc_nibmap(kLdsQuarter, x[0]) ^ x[1];
+    const uint32_t t1 = crc_nibmap(kLdsQuarter, x[2]) ^ x[3];
+    s = crc_nibmap(kLdsHalf, t0) ^ t1;
+  }
   if (first) s = L.lane < sp.owner ? 0u : s;  // chunks wholly before the span
   return s;
 }
@@ -375,6 +397,75 @@ __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, u
     if (!more) break;
     i = ni;
     k = nk;
+    r = nr;
+    sp = nsp;
+    cur = nxt;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Uniform batches: every span has the same 16-byte-multiple length and a
+// 16-byte-aligned start (base + i * stride).  All span geometry is then
+// batch-constant and precomputed on the host; FULL = length is a multiple of
+// the 4 KiB round (owner 0, nothing to zero or clamp).
+struct CrcUniform {
+  uint64_t stride;
+  uint32_t length;
+  int32_t rounds;
+  int32_t owner;
+  uint32_t hb;
+  uint32_t inj;  // unshift(~0, hb): Value's init state at the owner's chunk start
+};
+
+template <bool FULL>
+__device__ __forceinline__ CrcSpan crc_uniform_span(uint64_t base, uint32_t i, const CrcUniform& U) {
+  CrcSpan sp;
+  sp.ptr = base + (uint64_t)i * U.stride;
+  sp.a0 = sp.ptr;
+  sp.a1 = sp.ptr + U.length;
+  sp.end = sp.a1;
+  sp.rounds = U.rounds;
+  sp.owner = FULL ? 0 : U.owner;
+  sp.hb = FULL ? 0u : U.hb;
+  sp.kt = 0;
+  sp.inj = FULL ? 0xFFFFFFFFu : U.inj;
+  sp.init_crc = 0;
+  sp.empty = false;
+  return sp;
+}
+
+template <class Op, bool FULL>
+__device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUniform& U, uint32_t count, uint8_t* lds,
+                                                   const CrcTables* __restrict__ g) {
+  crc_fill_lds(lds, g);
+  __syncthreads();
+  const CrcLane L = crc_lane();
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * wpb;
+  if (wave >= count) return;
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  uint32_t i = wave;
+  CrcSpan sp = crc_uniform_span<FULL>(base, i, U);
+  int r = sp.rounds - 1;
+  Chunk cur = crc_load_chunk(sp, r, L);
+  uint32_t s = 0;
+  for (;;) {
+    uint32_t ni = i;
+    int nr = r - 1;
+    CrcSpan nsp = sp;
+    bool more = true;
+    if (nr < 0) {
+      ni = i + nwaves;
+      more = ni < count;
+      nsp = crc_uniform_span<FULL>(base, more ? ni : i, U);
+      nr = U.rounds - 1;
+    }
+    const Chunk nxt = crc_load_chunk(more ? nsp : sp, more ? nr : r, L);
+    s = crc_round(s, cur, sp, r, L);
+    if (r == 0) op.finish(i, crc_finish(s, sp, L));
+    if (!more) break;
+    i = ni;
     r = nr;
     sp = nsp;
     cur = nxt;

@@ -140,6 +140,43 @@ int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
   return MCK_OK;
 }
 
+// Uniform batch fast path: geometry precomputed here (crc_uniform_driver).
+template <class Op>
+int launch_crc_uniform(const Op& op, const mck_spans* sp, hipStream_t st) {
+  const uint32_t count = sp->count;
+  if (!count) return MCK_OK;
+  int dev, ncu;
+  int rc = current_device(&dev, &ncu);
+  if (rc) return rc;
+  CrcUniform U;
+  U.stride = sp->stride;
+  U.length = sp->length;
+  U.rounds = (int32_t)((sp->length + kRoundBytes - 1) / kRoundBytes);
+  const uint32_t lead = (uint32_t)U.rounds * kRoundBytes - sp->length;
+  U.owner = (int32_t)(lead >> 6);
+  U.hb = lead & 63u;
+  uint32_t inj = 0xFFFFFFFFu;
+  for (uint32_t b = 0; b < 8 * U.hb; b++) inj = gf_unmulx(inj);
+  U.inj = inj;
+  const uint32_t grid = std::min<uint32_t>(ncu, (count + 15) / 16);
+  if (U.owner == 0 && U.hb == 0) {
+    rc = ensure_lds(k_crc_uniform<Op, true>, dev);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_crc_uniform<Op, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, U, count);
+  } else {
+    rc = ensure_lds(k_crc_uniform<Op, false>, dev);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_crc_uniform<Op, false>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, U, count);
+  }
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+bool is_uniform_aligned(const mck_spans* s) {
+  return !s->offsets && !s->lengths && s->length > 0 && (s->length & 15u) == 0 && (s->stride & 15u) == 0 &&
+         (reinterpret_cast<uintptr_t>(s->base) & 15u) == 0;
+}
+
 template <class Op>
 int launch_xxh3(const Op& op, uint32_t count, hipStream_t st) {
   if (!count) return MCK_OK;
@@ -279,8 +316,10 @@ int mck_crc32c_batch(const mck_spans* spans, const uint32_t* init_crcs, uint32_t
     set_err("out is NULL");
     return MCK_EINVAL;
   }
-  return launch_crc(OpCrcValue{to_src(spans), init_crcs, flags & MCK_F_MASK, out}, spans->count,
-                    reinterpret_cast<hipStream_t>(stream));
+  const OpCrcValue op{to_src(spans), init_crcs, flags & MCK_F_MASK, out};
+  if (!init_crcs && is_uniform_aligned(spans))
+    return launch_crc_uniform(op, spans, reinterpret_cast<hipStream_t>(stream));
+  return launch_crc(op, spans->count, reinterpret_cast<hipStream_t>(stream));
 }
 
 int mck_xxh3_64_batch(const mck_spans* spans, uint64_t* out, mck_stream_t stream) {

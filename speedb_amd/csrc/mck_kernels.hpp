@@ -125,6 +125,13 @@ __global__ __launch_bounds__(1024) void k_crc(Op op, uint32_t count) {
   crc_spans_driver(op, count, lds, &g_crc_tables);
 }
 
+// uniform batches (see CrcUniform)
+template <class Op, bool FULL>
+__global__ __launch_bounds__(1024) void k_crc_uniform(Op op, CrcUniform U, uint32_t count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  crc_uniform_driver<Op, FULL>(op, U, count, lds, &g_crc_tables);
+}
+
 // ============================ XXH3 ========================================
 // wave per span; grid-stride over spans
 template <class Op>

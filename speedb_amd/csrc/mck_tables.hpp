@@ -25,6 +25,8 @@ struct CrcTables {
   uint32_t lane_final[8][16][64]; // zshift(v << 4n, 64*(63-lane))
   uint32_t gap[8][16];            // zshift(v << 4n, kGapBytes)
   uint32_t ext1[8][16];           // zshift(v << 4n, 1)
+  uint32_t half[8][16];           // zshift(v << 4n, 32): joins a lane's chains
+  uint32_t quarter[8][16];        // zshift(v << 4n, 16)
   uint32_t unshift[kMaxUnshift][8][16];  // zshift^-1(v << 4n, k)
 };
 
@@ -63,11 +65,14 @@ inline void build_crc_tables(CrcTables* t) {
     for (int n = 0; n < 8; n++)
       for (int v = 0; v < 16; v++) t->lane_final[n][v][l] = gf_mul((uint32_t)v << (4 * n), k);
   }
-  const uint32_t kg = gf_xpow8n(kGapBytes), k1 = gf_xpow8n(1);
+  const uint32_t kg = gf_xpow8n(kGapBytes), k1 = gf_xpow8n(1), k32 = gf_xpow8n(kChunkBytes / 2),
+                 k16 = gf_xpow8n(kChunkBytes / 4);
   for (int n = 0; n < 8; n++)
     for (int v = 0; v < 16; v++) {
       t->gap[n][v] = gf_mul((uint32_t)v << (4 * n), kg);
       t->ext1[n][v] = gf_mul((uint32_t)v << (4 * n), k1);
+      t->half[n][v] = gf_mul((uint32_t)v << (4 * n), k32);
+      t->quarter[n][v] = gf_mul((uint32_t)v << (4 * n), k16);
     }
   for (int k = 0; k < kMaxUnshift; k++)
     for (int n = 0; n < 8; n++)

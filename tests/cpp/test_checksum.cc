@@ -1,0 +1,244 @@
+// test_checksum.cc -- the reference's checksum tests, restated against the
+// C++ host mirror (include/speedb_amd/checksum.hpp) and so against the GPU
+// engine.  Expected values are the reference's own (util/crc32c_test.cc,
+// table/table_test.cc); test names follow theirs.  Needs a GPU; built and
+// run by tests/test_cpp_mirror.py.
+#include <hip/hip_runtime_api.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <random>
+#include <string>
+#include <vector>
+
+#include "speedb_amd/checksum.hpp"
+
+using namespace speedb_amd;
+
+static int g_fail = 0, g_checks = 0;
+#define EXPECT_EQ(a, b)                                                                       \
+  do {                                                                                        \
+    g_checks++;                                                                               \
+    auto va_ = (a);                                                                           \
+    auto vb_ = (b);                                                                           \
+    if (!(va_ == vb_)) {                                                                      \
+      g_fail++;                                                                               \
+      fprintf(stderr, "%s:%d: EXPECT_EQ(%s, %s) failed\n", __FILE__, __LINE__, #a, #b);       \
+    }                                                                                         \
+  } while (0)
+#define EXPECT_NE(a, b) EXPECT_EQ(!((a) == (b)), true)
+#define EXPECT_TRUE(a) EXPECT_EQ(!!(a), true)
+#define TEST(s, n) static void s##_##n()
+#define RUN(s, n)                         \
+  do {                                    \
+    int before = g_fail;                  \
+    s##_##n();                            \
+    printf("[%s] %s.%s\n", g_fail == before ? "  OK  " : " FAIL ", #s, #n); \
+  } while (0)
+
+// util/crc32c_test.cc:70-94
+TEST(CRC, StandardResults) {
+  char buf[32];
+  memset(buf, 0, sizeof(buf));
+  EXPECT_EQ(0x8a9136aaU, crc32c::Value(buf, sizeof(buf)));
+  memset(buf, 0xff, sizeof(buf));
+  EXPECT_EQ(0x62a8ab43U, crc32c::Value(buf, sizeof(buf)));
+  for (int i = 0; i < 32; i++) buf[i] = static_cast<char>(i);
+  EXPECT_EQ(0x46dd794eU, crc32c::Value(buf, sizeof(buf)));
+  for (int i = 0; i < 32; i++) buf[i] = static_cast<char>(31 - i);
+  EXPECT_EQ(0x113fdb5cU, crc32c::Value(buf, sizeof(buf)));
+  unsigned char data[48] = {
+      0x01, 0xc0, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00,
+      0x14, 0x00, 0x00, 0x00, 0x00, 0x00, 0x04, 0x00, 0x00, 0x00, 0x00, 0x14, 0x00, 0x00, 0x00, 0x18,
+      0x28, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x02, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00, 0x00,
+  };
+  EXPECT_EQ(0xd9963a56U, crc32c::Value(reinterpret_cast<char*>(data), sizeof(data)));
+}
+
+TEST(CRC, Values) { EXPECT_NE(crc32c::Value("a", 1), crc32c::Value("foo", 3)); }
+
+TEST(CRC, Extend) {
+  EXPECT_EQ(crc32c::Value("hello world", 11), crc32c::Extend(crc32c::Value("hello ", 6), "world", 5));
+}
+
+TEST(CRC, Mask) {
+  uint32_t crc = crc32c::Value("foo", 3);
+  EXPECT_NE(crc, crc32c::Mask(crc));
+  EXPECT_NE(crc, crc32c::Mask(crc32c::Mask(crc)));
+  EXPECT_EQ(crc, crc32c::Unmask(crc32c::Mask(crc)));
+  EXPECT_EQ(crc, crc32c::Unmask(crc32c::Unmask(crc32c::Mask(crc32c::Mask(crc)))));
+}
+
+TEST(CRC, Crc32cCombineBasicTest) {
+  uint32_t crc1 = crc32c::Value("hello ", 6), crc2 = crc32c::Value("world", 5);
+  EXPECT_EQ(crc32c::Value("hello world", 11), crc32c::Crc32cCombine(crc1, crc2, 5));
+}
+
+TEST(CRC, Crc32cCombineOrderMattersTest) {
+  uint32_t crc1 = crc32c::Value("hello ", 6), crc2 = crc32c::Value("world", 5);
+  EXPECT_NE(crc32c::Value("hello world", 11), crc32c::Crc32cCombine(crc2, crc1, 6));
+}
+
+// util/crc32c_test.cc:144-158, scaled from 4096 to 257 sizes (each is a
+// synchronous GPU round trip here)
+TEST(CRC, Crc32cCombineFullCoverTest) {
+  std::mt19937_64 rnd(301);
+  std::string s1(1 << 20, 0);
+  for (auto& c : s1) c = static_cast<char>(rnd());
+  const uint32_t crc1 = crc32c::Value(s1.data(), s1.size());
+  for (int size2 = 0; size2 < 4096; size2 += 16) {
+    std::string s2(size2, 0);
+    for (auto& c : s2) c = static_cast<char>(rnd());
+    const uint32_t crc2 = crc32c::Value(s2.data(), s2.size());
+    EXPECT_EQ(crc32c::Extend(crc1, s2.data(), s2.size()), crc32c::Crc32cCombine(crc1, crc2, s2.size()));
+  }
+}
+
+static std::string Hex(uint32_t v) {
+  char b[9];
+  const unsigned char* u = reinterpret_cast<const unsigned char*>(&v);  // little endian as in file
+  snprintf(b, sizeof b, "%02X%02X%02X%02X", u[0], u[1], u[2], u[3]);
+  return b;
+}
+static std::string ChecksumAsString(const std::string& data, ChecksumType t) {
+  uint32_t v = ComputeBuiltinChecksum(t, data.data(), data.size());
+  if (data.size() >= 1)
+    EXPECT_EQ(v, ComputeBuiltinChecksumWithLastByte(t, data.data(), data.size() - 1, data.back()));
+  return Hex(v);
+}
+static std::string ChecksumAsString(std::string* data, char new_last_byte, ChecksumType t) {
+  data->back() = new_last_byte;
+  return ChecksumAsString(*data, t);
+}
+
+// table/table_test.cc:2325-2403 BuiltinChecksumTest.ChecksumSchemas
+TEST(BuiltinChecksumTest, ChecksumSchemas) {
+  std::string b0 = "x";
+  std::string b1 = "This is a short block!x";
+  std::string b2;
+  for (int i = 0; i < 100; ++i) b2.append("This is a long block!");
+  b2.append("x");
+  std::string empty;
+  const char ct1 = 0, ct2 = 1, ct3 = 7;  // kNoCompression, kSnappyCompression, kZSTD
+  const char* want[5][10] = {
+      {"00000000", "00000000", "00000000", "00000000", "00000000", "00000000", "00000000", "00000000",
+       "00000000", "00000000"},
+      {"D8EA82A2", "D28F2549", "052B2843", "46F8F711", "583F0355", "2F9B0A57", "ECE7DA1D", "943EF0AB",
+       "43A2EDB1", "00E53D63"},
+      {"055DCC02", "3EB065CF", "31F79238", "320D2E00", "4A2E5FB0", "0BD9F652", "B4107E50", "20F4D4BA",
+       "8F1A1F99", "A191A338"},
+      {"99E9D851", "682705DB", "30E7211B", "B7BB58E8", "B74655EF", "B6C8BBBE", "AED9E3B4", "0D4999FE",
+       "F5932423", "6B31BAB1"},
+      {"00000000", "C294D338", "1B174353", "2D0E20C8", "B37FB5E6", "6AFC258D", "5CE54616", "FA2D482E",
+       "23AED845", "15B7BBDE"},
+  };
+  for (int t = 0; t < 5; t++) {
+    const ChecksumType ct = static_cast<ChecksumType>(t);
+    EXPECT_EQ(ChecksumAsString(empty, ct), std::string(want[t][0]));
+    EXPECT_EQ(ChecksumAsString(&b0, ct1, ct), std::string(want[t][1]));
+    EXPECT_EQ(ChecksumAsString(&b0, ct2, ct), std::string(want[t][2]));
+    EXPECT_EQ(ChecksumAsString(&b0, ct3, ct), std::string(want[t][3]));
+    EXPECT_EQ(ChecksumAsString(&b1, ct1, ct), std::string(want[t][4]));
+    EXPECT_EQ(ChecksumAsString(&b1, ct2, ct), std::string(want[t][5]));
+    EXPECT_EQ(ChecksumAsString(&b1, ct3, ct), std::string(want[t][6]));
+    EXPECT_EQ(ChecksumAsString(&b2, ct1, ct), std::string(want[t][7]));
+    EXPECT_EQ(ChecksumAsString(&b2, ct2, ct), std::string(want[t][8]));
+    EXPECT_EQ(ChecksumAsString(&b2, ct3, ct), std::string(want[t][9]));
+  }
+}
+
+// reader_common.cc:26-63 through the scalar mirror, and the batched verify
+// over a run of blocks with one corrupted byte in some of them.
+TEST(BlockChecksum, VerifyScalarAndBatched) {
+  std::mt19937_64 rnd(7);
+  for (ChecksumType t : {kCRC32c, kXXH3, kxxHash, kxxHash64}) {
+    for (uint32_t base : {0u, 0x9e3779b9u}) {
+      // build a run of blocks [payload][type][LE32 checksum + modifier]
+      std::string img;
+      std::vector<BlockHandle> handles;
+      const uint64_t file_base = 1ull << 32;
+      for (int b = 0; b < 64; b++) {
+        const size_t n = (b % 3 == 0 ? 4096 : b % 3 == 1 ? 16384 : 65536) + rnd() % 256;
+        std::string payload(n, 0);
+        for (auto& c : payload) c = static_cast<char>(rnd());
+        const char comp = static_cast<char>(b % 2 ? 1 : 0);
+        const uint64_t off = file_base + img.size();
+        uint32_t ck = ComputeBuiltinChecksumWithLastByte(t, payload.data(), n, comp);
+        ck += ChecksumModifierForContext(base, off);
+        handles.push_back({off, n});
+        img += payload;
+        img.push_back(comp);
+        for (int i = 0; i < 4; i++) img.push_back(static_cast<char>(ck >> (8 * i)));
+      }
+      Footer f{t, base};
+      // scalar
+      EXPECT_TRUE(VerifyBlockChecksum(f, img.data() + (handles[3].offset - file_base), handles[3].size, "x.sst",
+                                      handles[3].offset).ok());
+      // batched, clean then corrupted
+      std::string bad = img;
+      const int corrupt[3] = {5, 17, 40};
+      for (int b : corrupt) bad[handles[b].offset - file_base + 100] ^= 0x04;
+      for (int pass = 0; pass < 2; pass++) {
+        const std::string& src = pass ? bad : img;
+        void* d = nullptr;
+        if (hipMalloc(&d, src.size() + 64) != hipSuccess) {
+          g_fail++;
+          return;
+        }
+        (void)hipMemcpy(d, src.data(), src.size(), hipMemcpyHostToDevice);
+        std::vector<Status> per;
+        Status s = VerifyBlockChecksums(f, d, file_base, handles, "000042.sst", &per);
+        (void)hipFree(d);
+        EXPECT_EQ(s.ok(), pass == 0);
+        int nbad = 0;
+        for (size_t i = 0; i < per.size(); i++) nbad += !per[i].ok();
+        EXPECT_EQ(nbad, pass ? 3 : 0);
+        if (pass) {
+          EXPECT_TRUE(per[5].IsCorruption() && per[17].IsCorruption() && per[40].IsCorruption());
+          // the batched message equals the scalar VerifyBlockChecksum message
+          const Status one = VerifyBlockChecksum(f, bad.data() + (handles[17].offset - file_base),
+                                                 handles[17].size, "000042.sst", handles[17].offset);
+          EXPECT_EQ(one.ToString(), per[17].ToString());
+          EXPECT_EQ(per[17].ToString().rfind("Corruption: block checksum mismatch: stored", 0), 0u);
+        }
+      }
+    }
+  }
+}
+
+// db/log_writer.cc:48-51 type_crc_ and the record CRC algebra
+TEST(Log, PhysicalRecordCrc) {
+  const uint32_t type_crc[5] = {0xa016d052u, 0xb34623a6u, 0x412da0a5u, 0x95e7c44eu, 0x678c474du};
+  for (int t = 1; t <= 5; t++) {
+    const char c = static_cast<char>(t);
+    EXPECT_EQ(crc32c::Value(&c, 1), type_crc[t - 1]);
+  }
+  std::string payload = "a physical record payload";
+  for (int t = 1; t <= 8; t++) {
+    std::string hdr_and_payload(1, static_cast<char>(t));
+    if (log::IsRecyclable(t)) hdr_and_payload += std::string("\x7b\x00\x00\x00", 4);  // log 123
+    hdr_and_payload += payload;
+    const uint32_t direct = crc32c::Mask(crc32c::Value(hdr_and_payload.data(), hdr_and_payload.size()));
+    EXPECT_EQ(log::PhysicalRecordCrc(static_cast<log::RecordType>(t), payload.data(), payload.size(), 123),
+              direct);
+  }
+}
+
+int main() {
+  if (mck_device_count() < 1) {
+    fprintf(stderr, "no gfx950 device\n");
+    return 2;
+  }
+  RUN(CRC, StandardResults);
+  RUN(CRC, Values);
+  RUN(CRC, Extend);
+  RUN(CRC, Mask);
+  RUN(CRC, Crc32cCombineBasicTest);
+  RUN(CRC, Crc32cCombineOrderMattersTest);
+  RUN(CRC, Crc32cCombineFullCoverTest);
+  RUN(BuiltinChecksumTest, ChecksumSchemas);
+  RUN(BlockChecksum, VerifyScalarAndBatched);
+  RUN(Log, PhysicalRecordCrc);
+  printf("%d checks, %d failures\n", g_checks, g_fail);
+  return g_fail ? 1 : 0;
+}

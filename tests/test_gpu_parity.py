@@ -72,7 +72,8 @@ def test_crc32c_batch_ragged(gpu, oracle):
 def test_crc32c_uniform_blocks(gpu, oracle):
     import speedb_amd as S
     torch = gpu
-    for block in (4096, 16384, 65536, 32768, 4100, 1000):
+    # 16-byte multiples take the uniform fast path (full 4 KiB rounds or not)
+    for block in (4096, 16384, 65536, 32768, 16, 48, 1008, 4112, 5008, 4100, 1000):
         count = max(1, (8 << 20) // block)
         host = splitmix_bytes(block, block * count)
         dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda")
