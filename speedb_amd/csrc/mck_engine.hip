@@ -183,7 +183,8 @@ int launch_xxh3(const Op& op, uint32_t count, hipStream_t st) {
   int ncu;
   int rc = current_device(nullptr, &ncu);
   if (rc) return rc;
-  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 3) / 4);
+  // 16 rows (spans) per 256-thread workgroup
+  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 15) / 16);
   hipLaunchKernelGGL(k_xxh3<Op>, dim3(grid), dim3(256), 0, st, op, count);
   MCK_HIP(hipGetLastError());
   return MCK_OK;

@@ -133,41 +133,46 @@ __global__ __launch_bounds__(1024) void k_crc_uniform(Op op, CrcUniform U, uint3
 }
 
 // ============================ XXH3 ========================================
-// wave per span; grid-stride over spans
+// one span per 16-lane row (see xxh3_rows_driver)
 template <class Op>
 __global__ __launch_bounds__(256) void k_xxh3(Op op, uint32_t count) {
-  const XxhLane X = xxh_lane();
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint32_t nw = gridDim.x * wpb;
-  for (uint32_t i = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)); i < count; i += nw)
-    op.run(i, X);
+  xxh3_rows_driver(op, count);
 }
 
 struct OpX3Value {
   SpanSrc s;
   uint64_t* out;
-  __device__ void run(uint32_t i, const XxhLane& X) const {
-    const uint64_t h = xxh3_wave(s.ptr(i), s.len(i), X);
-    if (X.lane == 0) out[i] = h;
-  }
+  __device__ const uint8_t* base() const { return s.base; }
+  __device__ uint64_t off(uint32_t i) const { return s.off(i); }
+  __device__ uint64_t hlen(uint32_t i) const { return s.len(i); }
+  __device__ void finish(uint32_t i, uint64_t h) const { out[i] = h; }
 };
 
+// kXXH3 block checksum (table/format.cc:569-597): lo32(XXH3 of all but the
+// last checksummed byte) ^ last byte * kRandomPrime; 0 for empty input.
 template <int MODE>
 struct OpX3Block {
   BlockArgs a;
-  __device__ void run(uint32_t i, const XxhLane& X) const {
+  __device__ const uint8_t* base() const { return a.s.base; }
+  __device__ uint64_t off(uint32_t i) const { return a.s.off(i); }
+  __device__ uint64_t hlen(uint32_t i) const {
+    const uint64_t n = a.s.len(i);
+    // verify: payload || type byte -> hash the payload; trailer / explicit
+    // last byte: hash the span; builtin: all but the span's last byte
+    if (MODE == kModeVerify || MODE == kModeTrailer || a.last) return n;
+    return n ? n - 1 : 0;
+  }
+  __device__ void finish(uint32_t i, uint64_t h) const {
     const uint8_t* p = a.s.ptr(i);
     const uint64_t n = a.s.len(i);
     uint32_t v;
-    if (MODE == kModeVerify) {
-      // checksummed = payload || type byte: XXH3(payload) ^ type * prime
-      v = (uint32_t)xxh3_wave(p, n, X) ^ (uint32_t)p[n] * kRandomPrime;
-    } else if (MODE == kModeTrailer || a.last) {
-      v = (uint32_t)xxh3_wave(p, n, X) ^ (uint32_t)a.last[i] * kRandomPrime;
-    } else {
-      v = n == 0 ? 0u : (uint32_t)xxh3_wave(p, n - 1, X) ^ (uint32_t)p[n - 1] * kRandomPrime;
-    }
-    if (X.lane == 0) block_epilogue<MODE>(a, i, v);
+    if (MODE == kModeVerify)
+      v = (uint32_t)h ^ (uint32_t)p[n] * kRandomPrime;
+    else if (MODE == kModeTrailer || a.last)
+      v = (uint32_t)h ^ (uint32_t)a.last[i] * kRandomPrime;
+    else
+      v = n == 0 ? 0u : (uint32_t)h ^ (uint32_t)p[n - 1] * kRandomPrime;
+    block_epilogue<MODE>(a, i, v);
   }
 };
 

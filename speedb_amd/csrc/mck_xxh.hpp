@@ -1,13 +1,19 @@
-// mck_xxh.hpp -- device XXH3-64 (wave per span) and legacy XXH32/XXH64
+// mck_xxh.hpp -- device XXH3-64 (16-lane row per span) and legacy XXH32/XXH64
 // (lane per span), xxHash v0.8.1 as vendored at util/xxhash.h.
 //
 // XXH3 long inputs (n > 240, util/xxhash.h:5141-5227): 8 u64 accumulators;
-// each 1 KiB segment = 16 stripes x 64 B; within a segment the 128
-// (stripe, accumulator-lane) terms are independent sums mod 2^64, so the
-// wave computes them in parallel: lane l owns stripe l>>2 and accumulator
-// pair q = l&3 (16 contiguous bytes per lane => one coalesced 1 KiB load per
-// segment).  The per-segment sums are reduced across the 16 stripe lanes and
-// then applied in order with the (nonlinear, sequential) scramble.
+// each 1 KiB segment = 16 stripes x 64 B, and within a segment the 128
+// (stripe, accumulator-lane) terms are independent sums mod 2^64; only the
+// scramble between segments is sequential.
+//
+// Layout: every 16-lane row of a wave owns one span.  Lane j of a row owns
+// accumulator pair q = j & 3 (accumulators 2q, 2q+1) and the four stripes
+// st4, st4+4, st4+8, st4+12 (st4 = j >> 2): per segment it issues four
+// 16-byte loads (the row's 16 lanes read 256 contiguous bytes per load) and
+// folds its four stripes locally, so the per-segment reduction is only 2
+// in-row DPP steps (over st4) and the scramble chain never leaves the row.
+// Rows walk their own spans (statically strided), so ragged batches keep all
+// rows busy; the wave loops while any row has work.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -138,45 +144,23 @@ __device__ __noinline__ uint64_t xxh3_short(const uint8_t* in, uint64_t len) {
   return xxh3_avalanche(acc + acc_end);
 }
 
-// Per-lane secret words for the long path.
-struct XxhLane {
-  uint64_t k0, k1;    // stripe secret for accumulators 2q, 2q+1 of stripe st
-  uint64_t ks0, ks1;  // scramble secret (offset 128)
-  uint64_t kl0, kl1;  // last-stripe secret (offset 121)
-  uint64_t km0, km1;  // merge secret (offset 11)
-  uint64_t i0, i1;    // XXH3_INIT_ACC for 2q, 2q+1
-  int lane, st, q;
-};
-__device__ __forceinline__ XxhLane xxh_lane() {
-  XxhLane X;
-  X.lane = threadIdx.x & 63;
-  X.st = X.lane >> 2;
-  X.q = X.lane & 3;
-  X.k0 = sec64(8 * X.st + 16 * X.q);
-  X.k1 = sec64(8 * X.st + 16 * X.q + 8);
-  X.ks0 = sec64(128 + 16 * X.q);
-  X.ks1 = sec64(136 + 16 * X.q);
-  X.kl0 = sec64(121 + 16 * X.q);
-  X.kl1 = sec64(129 + 16 * X.q);
-  X.km0 = sec64(11 + 16 * X.q);
-  X.km1 = sec64(19 + 16 * X.q);
-  // INIT_ACC = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1}
-  const uint64_t init[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
-  X.i0 = X.q == 0 ? init[0] : X.q == 1 ? init[2] : X.q == 2 ? init[4] : init[6];
-  X.i1 = X.q == 0 ? init[1] : X.q == 1 ? init[3] : X.q == 2 ? init[5] : init[7];
-  return X;
-}
-
-__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int o) {
-  const uint32_t lo = __shfl_xor((uint32_t)v, o, 64), hi = __shfl_xor((uint32_t)(v >> 32), o, 64);
+// 64-bit DPP move (both halves with the same control)
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
   return ((uint64_t)hi << 32) | lo;
 }
-// sum over the 16 stripe lanes sharing q (lane bits 2..5)
-__device__ __forceinline__ uint64_t sum_stripes(uint64_t v) {
-  v += shfl_xor64(v, 4);
-  v += shfl_xor64(v, 8);
-  v += shfl_xor64(v, 16);
-  v += shfl_xor64(v, 32);
+// sum over the 4 lanes of a row with the same (lane & 3): row_ror 4, 8
+__device__ __forceinline__ uint64_t row_sum_st4(uint64_t v) {
+  v += dpp64<0x124>(v);
+  v += dpp64<0x128>(v);
+  return v;
+}
+// sum over the 4 lanes of a quad: quad_perm [1,0,3,2], [2,3,0,1]
+__device__ __forceinline__ uint64_t quad_sum(uint64_t v) {
+  v += dpp64<0xB1>(v);
+  v += dpp64<0x4E>(v);
   return v;
 }
 __device__ __forceinline__ uint64_t xxh3_scramble(uint64_t a, uint64_t k) {
@@ -185,62 +169,132 @@ __device__ __forceinline__ uint64_t xxh3_scramble(uint64_t a, uint64_t k) {
   return a * P32_1;
 }
 
-// XXH3_64bits of [in, in+len), len > 240; all lanes of the wave call it and
-// all return the hash.
-__device__ __forceinline__ uint64_t xxh3_long_wave(const uint8_t* in, uint64_t len, const XxhLane& X) {
-  uint64_t a0 = X.i0, a1 = X.i1;
-  const uint64_t nb = (len - 1) / 1024;                          // full segments
-  const int nstripes = (int)(((len - 1) - 1024 * nb) / 64);      // in the last one
-  for (uint64_t g0 = 0; g0 <= nb; g0 += 4) {
-    uint4 d[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint64_t g = g0 + j;
-      const bool act = g < nb || (g == nb && X.st < nstripes);
-      d[j] = act ? *reinterpret_cast<const uint4*>(in + 1024 * g + 16 * X.lane) : make_uint4(0, 0, 0, 0);
-    }
-    uint64_t c0[4], c1[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint64_t g = g0 + j;
-      const bool act = g < nb || (g == nb && X.st < nstripes);
-      const uint64_t d0 = ((uint64_t)d[j].y << 32) | d[j].x, d1 = ((uint64_t)d[j].w << 32) | d[j].z;
-      c0[j] = act ? d1 + mul32to64(d0 ^ X.k0) : 0;
-      c1[j] = act ? d0 + mul32to64(d1 ^ X.k1) : 0;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      c0[j] = sum_stripes(c0[j]);
-      c1[j] = sum_stripes(c1[j]);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint64_t g = g0 + j;
-      if (g <= nb) {
-        a0 += c0[j];
-        a1 += c1[j];
-        if (g < nb) {
-          a0 = xxh3_scramble(a0, X.ks0);
-          a1 = xxh3_scramble(a1, X.ks1);
-        }
-      }
-    }
-  }
-  {  // last stripe at in + len - 64, secret + 121
-    const uint8_t* p = in + len - 64 + 16 * X.q;
-    const uint64_t d0 = rd64(p), d1 = rd64(p + 8);
-    a0 += d1 + mul32to64(d0 ^ X.kl0);
-    a1 += d0 + mul32to64(d1 ^ X.kl1);
-  }
-  uint64_t m = mul128_fold64(a0 ^ X.km0, a1 ^ X.km1);
-  m += shfl_xor64(m, 1);
-  m += shfl_xor64(m, 2);
-  return xxh3_avalanche(len * P64_1 + m);
+typedef unsigned int xu32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const xu32x4 xgbl_u32x4_t;
+// 16-byte global load at any byte address (the hardware splits misaligned
+// accesses; full rate at 4-byte alignment)
+__device__ __forceinline__ uint4 gload16u(uint64_t addr) {
+  const xu32x4 v = *reinterpret_cast<xgbl_u32x4_t*>(addr);
+  return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-__device__ __forceinline__ uint64_t xxh3_wave(const uint8_t* in, uint64_t len, const XxhLane& X) {
-  if (len <= 240) return __shfl(X.lane == 0 ? xxh3_short(in, len) : 0ull, 0, 64);
-  return xxh3_long_wave(in, len, X);
+// Per-lane constants of the row layout.
+struct X3Row {
+  uint64_t k0[4], k1[4];  // stripe secrets for accumulators 2q, 2q+1 of stripe st4+4k
+  uint64_t ks0, ks1;      // scramble secret (offset 128)
+  uint64_t kl0, kl1;      // last-stripe secret (offset 121)
+  uint64_t km0, km1;      // merge secret (offset 11)
+  uint64_t i0, i1;        // XXH3_INIT_ACC
+  int lane, row, j, q, st4;
+};
+__device__ __forceinline__ X3Row x3_row() {
+  X3Row X;
+  X.lane = threadIdx.x & 63;
+  X.row = X.lane >> 4;
+  X.j = X.lane & 15;
+  X.q = X.j & 3;
+  X.st4 = X.j >> 2;
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const int st = X.st4 + 4 * k;
+    X.k0[k] = sec64(8 * st + 16 * X.q);
+    X.k1[k] = sec64(8 * st + 16 * X.q + 8);
+  }
+  X.ks0 = sec64(128 + 16 * X.q);
+  X.ks1 = sec64(136 + 16 * X.q);
+  X.kl0 = sec64(121 + 16 * X.q);
+  X.kl1 = sec64(129 + 16 * X.q);
+  X.km0 = sec64(11 + 16 * X.q);
+  X.km1 = sec64(19 + 16 * X.q);
+  // INIT_ACC = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1}
+  X.i0 = X.q == 0 ? (uint64_t)P32_3 : X.q == 1 ? P64_2 : X.q == 2 ? P64_4 : P64_5;
+  X.i1 = X.q == 0 ? P64_1 : X.q == 1 ? P64_3 : X.q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+  return X;
+}
+
+// One row's span in progress.
+struct X3Span {
+  uint64_t ptr, len;
+  uint32_t nb;   // full segments: (len - 1) / 1024
+  uint32_t nst;  // stripes in the last, partial segment
+  uint32_t g;    // segment being processed
+  uint32_t i;    // span index
+};
+
+// Advance the row to its next long span (hashing short ones -- n <= 240 --
+// on the row's first lane on the way).  Op: base(), off(i), hlen(i),
+// finish(i, h) (called by lane j == 0 of the row).  Returns false when the
+// row has no spans left.
+template <class Op>
+__device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t count, uint32_t stride,
+                                             const X3Row& X, X3Span& rs) {
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  for (; i < count; i += stride) {
+    const uint64_t len = op.hlen(i);
+    const uint64_t ptr = base + op.off(i);
+    if (len > 240) {
+      rs.ptr = ptr;
+      rs.len = len;
+      rs.nb = (uint32_t)((len - 1) / 1024);
+      rs.nst = (uint32_t)(((len - 1) - 1024ull * rs.nb) / 64);
+      rs.g = 0;
+      rs.i = i;
+      return true;
+    }
+    if (X.j == 0) op.finish(i, xxh3_short(reinterpret_cast<const uint8_t*>(ptr), len));
+  }
+  return false;
+}
+
+template <class Op>
+__device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count) {
+  const X3Row X = x3_row();
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t stride = gridDim.x * wpb * 4;  // rows in the grid
+  const uint32_t first = (blockIdx.x * wpb + (threadIdx.x >> 6)) * 4 + X.row;
+  // idle rows keep loading from a valid address: the batch's base
+  X3Span rs{reinterpret_cast<uint64_t>(op.base()), 0, 0, 0, 0, 0};
+  bool act = x3_next_long(op, first, count, stride, X, rs);
+  uint64_t a0 = X.i0, a1 = X.i1;
+  while (__any(act)) {
+    // loads first and unconditional (clamped when a stripe is not part of
+    // the segment, or the row is idle), so they are counted and in flight
+    const uint64_t seg = rs.ptr + 1024ull * rs.g;
+    const bool full = rs.g < rs.nb;
+    uint4 d[4];
+    bool ok[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t st = (uint32_t)(X.st4 + 4 * k);
+      ok[k] = act && (full || st < rs.nst);
+      d[k] = gload16u(ok[k] ? seg + 64 * st + 16 * X.q : rs.ptr);
+    }
+    const uint4 dl = gload16u(act ? rs.ptr + rs.len - 64 + 16 * X.q : rs.ptr);
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint64_t d0 = ((uint64_t)d[k].y << 32) | d[k].x, d1 = ((uint64_t)d[k].w << 32) | d[k].z;
+      c0 += ok[k] ? d1 + mul32to64(d0 ^ X.k0[k]) : 0;
+      c1 += ok[k] ? d0 + mul32to64(d1 ^ X.k1[k]) : 0;
+    }
+    a0 += row_sum_st4(c0);
+    a1 += row_sum_st4(c1);
+    if (full) {
+      a0 = xxh3_scramble(a0, X.ks0);
+      a1 = xxh3_scramble(a1, X.ks1);
+      rs.g++;
+    } else if (act) {  // last, partial segment done: last stripe, merge, next span
+      const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
+      a0 += l1 + mul32to64(l0 ^ X.kl0);
+      a1 += l0 + mul32to64(l1 ^ X.kl1);
+      const uint64_t m = quad_sum(mul128_fold64(a0 ^ X.km0, a1 ^ X.km1));
+      const uint64_t h = xxh3_avalanche(rs.len * P64_1 + m);
+      if (X.j == 0) op.finish(rs.i, h);
+      act = x3_next_long(op, rs.i + stride, count, stride, X, rs);
+      a0 = X.i0;
+      a1 = X.i1;
+    }
+  }
 }
 
 // ---- legacy XXH32 / XXH64, one lane per span ----------------------------
