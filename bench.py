@@ -1,19 +1,33 @@
 #!/usr/bin/env python3
-"""Headline benchmark: CRC32C over 1M x 4 KiB random blocks, device-resident
-(BASELINE.json configs[1]); metric "GiB/s checksummed (device-resident)".
+"""Benchmarks of the block-checksum hot path (BASELINE.json).
 
-One step = one mck_crc32c_batch launch over the rank's whole batch.  With
-N > 1 (torchrun, one process per GPU) every rank checksums its own 1M-block
+Default workload (the headline, BASELINE.json configs[1]): CRC32C over
+1M x 4 KiB random blocks per GPU, device-resident; metric "GiB/s checksummed
+(device-resident)".  Other configs via --workload:
+
+  crc32c   configs[1]  CRC32C, N x B uniform blocks (default 1M x 4 KiB)
+  xxh3     configs[1]  same data, XXH3-64
+  sst      configs[2]  compaction-shaped 4/16/64 KiB (+0..255 B) SST blocks
+                       with 5-byte trailers, format_version 6 context
+                       checksums; VerifyBlockChecksum of every block, one
+                       kCRC32c image and one kXXH3 image per step
+  wal      configs[3]  WAL replay: 32 KiB blocks, one kFullType record each,
+                       ReadPhysicalRecord CRC verify of every record
+  host     configs[4]  host-resident (pinned) 4.2 KiB SST-sized blocks,
+                       H2D + CRC32C + D2H double-buffered through the GPU
+
+One step = one pass of the workload's kernel(s) over the rank's whole batch.
+With N > 1 (torchrun, one process per GPU) every rank checksums its own
 shard -- blocks are independent, so there is no data-path collective
 (scaling "weak"); the only collectives are the timing barrier and the
 max-over-ranks of the elapsed time.
 
-Printed JSON (rank 0): value = total bytes of all ranks / max-over-ranks wall
-time of the K timed steps, in GiB/s; roofline = the CRC kernel's algorithmic
-bytes per launch / its average launch time from HIP events on the launch
-stream, against the 8 TB/s HBM3E peak; cpu_baseline = the reference's own
-crc32c (oracle/_ref, compiled from util/crc32c.cc) on the host cores, rank 0
-at N=1 only, on a bounded DRAM-resident sample.
+Printed JSON (rank 0): value = checksummed bytes of all ranks / max-over-ranks
+wall time of the K timed steps, in GiB/s; roofline = the dominant kernel's
+algorithmic bytes per launch / its average launch time (HIP events on the
+launch stream) against the 8 TB/s HBM3E peak; cpu_baseline = the reference's
+own crc32c / XXH3 (oracle/_ref, compiled from util/crc32c.cc + util/xxhash.cc)
+on 16 host threads, rank 0 at N=1 only, on a bounded DRAM-resident sample.
 """
 import argparse
 import ctypes
@@ -34,9 +48,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
-    p.add_argument("--kind", choices=["crc32c", "xxh3"], default="crc32c")
+    p.add_argument("--sst-bytes", type=int, default=2 << 30, help="per SST image (sst)")
+    p.add_argument("--wal-blocks", type=int, default=1 << 16, help="32 KiB blocks (wal)")
+    p.add_argument("--host-bytes", type=int, default=4 << 30, help="pinned source bytes (host)")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="approximate CPU-baseline budget (0 disables)")
     p.add_argument("--cpu-threads", type=int, default=16)
@@ -44,15 +61,17 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(args, seconds):
+def cpu_baseline(args, kind, block, sample, gpu_lo32_sum):
     """The reference's crc32c::Value (util/crc32c.cc crc32c_3way, SSE4.2 +
-    PCLMUL) / XXH3_64bits, one block per call, blocks strided across threads,
-    over a DRAM-resident 1 GiB sample of distinct random blocks."""
+    PCLMUL) or XXH3_64bits, one block per call (tools/db_bench_tool.cc
+    :4392-4412), blocks strided across threads, over a DRAM-resident host copy
+    of the first 1 GiB of the GPU's own blocks.  The first (calibration) pass
+    also cross-checks the GPU: the reference's sum of lo32(checksum) over the
+    sample must equal the sum over the GPU's outputs for the same blocks."""
     import numpy as np
     flags = open("/proc/cpuinfo").read()
     name = "libspdb_ref_v4.so" if " avx512f " in flags else "libspdb_ref.so"
     path = os.path.join(REPO, "oracle", "_ref", name)
-    kind = "reference"
     if not os.path.exists(path):
         return None
     lib = ctypes.CDLL(path)
@@ -60,32 +79,163 @@ def cpu_baseline(args, seconds):
     lib.ref_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                               ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                               ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
-    block = args.block_bytes
-    nblocks = (1 << 30) // block
-    buf = np.random.default_rng(7).integers(0, 256, nblocks * block, dtype=np.uint8)
+    buf = np.ascontiguousarray(sample)
+    nblocks = buf.size // block
     threads = args.cpu_threads
-    k = 0 if args.kind == "crc32c" else 1
-    secs = ctypes.c_double()
-    sink = ctypes.c_uint32()
-    # calibrate with one pass, then size the run to ~`seconds`
-    tot = lib.ref_bench(k, 1, threads, block, 0, buf.ctypes.data, nblocks, 1, ctypes.byref(secs),
-                        ctypes.byref(sink))
-    passes = max(1, int(seconds / max(secs.value, 1e-6)))
+    k = 0 if kind == "crc32c" else 1
+    secs, sink = ctypes.c_double(), ctypes.c_uint32()
+    lib.ref_bench(k, 1, threads, block, 0, buf.ctypes.data, nblocks, 1, ctypes.byref(secs),
+                  ctypes.byref(sink))  # calibration pass
+    agrees = int(sink.value) == gpu_lo32_sum
+    passes = max(1, int(args.cpu_seconds / max(secs.value, 1e-6)))
     tot = lib.ref_bench(k, 1, threads, block, 0, buf.ctypes.data, nblocks, passes,
                         ctypes.byref(secs), ctypes.byref(sink))
-    model = ""
-    for line in flags.splitlines():
-        if line.startswith("model name"):
-            model = line.split(":", 1)[1].strip()
-            break
+    model = next((ln.split(":", 1)[1].strip() for ln in flags.splitlines()
+                  if ln.startswith("model name")), "")
     return {
         "value": round(tot / secs.value / 2**30, 2), "unit": "GiB/s", "cores": threads,
-        "kind": kind,
-        "sample": (f"{args.kind} via oracle/_ref/{name} (reference util/crc32c.cc + "
-                   f"util/xxhash.cc), {passes} pass(es) over {nblocks} distinct random "
-                   f"{block}-B blocks (1 GiB, DRAM-resident), one block per call, blocks "
-                   f"strided over {threads} threads, {secs.value:.1f} s; host {model}"),
+        "kind": "reference",
+        "sample": (f"{kind} via oracle/_ref/{name} (reference util/crc32c.cc + util/xxhash.cc), "
+                   f"{passes} pass(es) over the GPU workload's first {nblocks} {block}-B blocks "
+                   f"({nblocks * block >> 20} MiB host copy, DRAM-resident), one block per call, "
+                   f"blocks strided over {threads} threads, {secs.value:.1f} s; host {model}"),
+        "agrees_with_gpu": agrees,
     }
+
+
+class Workload:
+    """step() runs one pass; span_bytes = checksummed bytes per step;
+    alg_bytes = algorithmic HBM bytes per launch of the dominant kernel;
+    check() -> bool verifies results (bit-exact spot checks)."""
+
+
+def make_workload(args, dev, rank):
+    import numpy as np
+    import torch
+
+    import speedb_amd as S
+    from speedb_amd import workloads as W
+
+    stream = torch.cuda.current_stream(dev)
+    w = Workload()
+    w.launches = 1
+    if args.workload in ("crc32c", "xxh3"):
+        count, block = args.blocks, args.block_bytes
+        data, spans = W.uniform_blocks(count, block, dev, seed=1000 + rank)
+        out32 = torch.empty(count, dtype=torch.int32, device=dev)
+        out64 = torch.empty(count, dtype=torch.int64, device=dev)
+        if args.workload == "crc32c":
+            w.step = lambda: S.crc32c_batch(spans, out=out32, stream=stream)
+            w.kernel = "mck::k_crc_uniform<OpCrcValue>"
+            w.alg_bytes = count * (block + 4)
+        else:
+            w.step = lambda: S.xxh3_64_batch(spans, out=out64, stream=stream)
+            w.kernel = "mck::k_xxh3<OpX3Value>"
+            w.alg_bytes = count * (block + 8)
+        w.span_bytes = count * block
+        w.desc = (f"{args.workload} over {count} x {block} B random blocks per GPU, device-resident "
+                  "(BASELINE.json configs[1])")
+        w.cfg = {"blocks_per_gpu": count, "block_bytes": block}
+
+        def check():
+            # the bytes and outputs the CPU-baseline leg cross-checks
+            n = min(count, (1 << 30) // block)
+            res = out32 if args.workload == "crc32c" else out64
+            lo = res[:n].cpu().numpy().astype(np.uint64) & 0xFFFFFFFF
+            w.sample = data[:n * block].cpu().numpy()
+            w.lo32_sum = int(lo.sum()) & 0xFFFFFFFF
+            return None
+        w.check = check
+    elif args.workload == "sst":
+        imgs = [W.SstImage(args.sst_bytes, t, dev, seed=100 + 2 * rank + k)
+                for k, t in enumerate((S.ChecksumType.kCRC32c, S.ChecksumType.kXXH3))]
+        res = {}
+
+        def step():
+            for im in imgs:
+                res[im.checksum_type] = im.verify(stream=stream)
+        w.step = step
+        w.launches = 2
+        w.kernel = "mck::k_crc<OpCrcBlock<kModeVerify>> + mck::k_xxh3<OpX3Block<kModeVerify>>"
+        w.span_bytes = sum(im.payload_bytes + im.count for im in imgs)  # payload + type byte
+        # per launch: span bytes + 4 B stored + 8 B offset + 4 B length + 8 B
+        # file offset in, 1 B flag + 4 + 4 B out
+        w.alg_bytes = sum(im.payload_bytes + im.count * (1 + 4 + 8 + 4 + 8 + 1 + 4 + 4)
+                          for im in imgs) / 2
+        w.desc = ("VerifyBlockChecksum over a compaction-shaped run of 4/16/64 KiB (+0..255 B) SST "
+                  f"blocks, {args.sst_bytes >> 20} MiB per image, format_version 6 context "
+                  "checksums; one kCRC32c + one kXXH3 image per step (BASELINE.json configs[2])")
+        w.cfg = {"blocks_per_gpu": sum(im.count for im in imgs), "image_bytes": args.sst_bytes,
+                 "checksum_types": ["kCRC32c", "kXXH3"]}
+
+        def check():
+            # every block the write-side kernel sealed verifies, and injected
+            # corruption is flagged exactly
+            import random
+            ok = True
+            for im in imgs:
+                mm, _, _, cnt = im.verify(stream=stream, with_count=True)
+                ok &= int(cnt.item()) == 0 and int(mm.sum().item()) == 0
+                bad = sorted(random.Random(rank).sample(range(im.count), 8))
+                im.corrupt(bad)
+                mm, _, _, cnt = im.verify(stream=stream, with_count=True)
+                flagged = torch.nonzero(mm).flatten().cpu().tolist()
+                im.corrupt(bad)  # restore
+                ok &= flagged == bad and int(cnt.item()) == 8
+            return ok
+        w.check = check
+    elif args.workload == "wal":
+        im = W.WalImage(args.wal_blocks, dev, seed=300 + rank)
+        res = {}
+
+        def step():
+            res["r"] = im.verify(stream=stream)
+        w.step = step
+        w.kernel = "mck::k_wal_verify"
+        w.span_bytes = im.nblocks * (W.WalImage.PAYLOAD + 1)  # CRC span: type + payload
+        w.alg_bytes = im.nbytes + im.nblocks * 16
+        w.desc = (f"WAL replay: {im.nblocks} x 32 KiB blocks per GPU, one kFullType 32761-B record "
+                  "each, ReadPhysicalRecord CRC32C verify (BASELINE.json configs[3])")
+        w.cfg = {"blocks_per_gpu": im.nblocks, "block_bytes": 32768}
+
+        def check():
+            step()
+            r = res["r"].cpu()
+            return bool((r[:, 0] == 1).all() and (r[:, 1] == 0).all())
+        w.check = check
+    else:  # host
+        import numpy as np
+        from speedb_amd import _lib
+        block = 4300  # 4 x (16 B key + 1000 B value) + block overhead, FlushBlockBySizePolicy
+        count = args.host_bytes // block
+        hbuf = torch.empty(count * block + 64, dtype=torch.uint8, pin_memory=True)
+        hbuf.copy_(torch.randint(0, 256, hbuf.shape, dtype=torch.uint8,
+                                 generator=torch.Generator().manual_seed(5)))
+        out = np.empty(count, dtype=np.uint32)
+        secs = ctypes.c_double()
+
+        def step():
+            _lib.check(_lib.lib.mck_host_batch_checksum(
+                1, hbuf.data_ptr(), None, None, block, block, count, 0, 0, 256 << 20,
+                out.ctypes.data, None, ctypes.byref(secs)), "mck_host_batch_checksum")
+        w.step = step
+        w.kernel = "mck::k_crc<OpCrcValue> (H2D/D2H overlapped)"
+        w.span_bytes = count * block
+        w.alg_bytes = count * (block + 4 + 8 + 4)
+        w.desc = (f"host-resident pinned {count} x {block} B blocks (SST-sized, 80M-key/1KB-value "
+                  "README shape) -> H2D + CRC32C + D2H, 256 MiB double-buffered chunks, "
+                  "copy-inclusive (BASELINE.json configs[4])")
+        w.cfg = {"blocks_per_gpu": count, "block_bytes": block, "pcie_inclusive": True}
+
+        def check():
+            # host-pipeline results == the device-resident kernel's on a sample
+            import random
+            idx = sorted(random.Random(rank).sample(range(count), 256))
+            smp = torch.stack([hbuf[i * block:(i + 1) * block] for i in idx]).to(dev).flatten()
+            want = S.crc32c_batch(S.Spans.uniform(smp, block, len(idx))).cpu().numpy()
+            return bool((want.view(np.uint32) == out[idx]).all())
+        w.check = check
+    return w
 
 
 def main():
@@ -101,25 +251,10 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    import speedb_amd as S
-
-    count, block = args.blocks, args.block_bytes
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + rank)
-    data = torch.randint(0, 256, (count * block + 64,), dtype=torch.uint8, device=dev, generator=g)
-    spans = S.Spans.uniform(data, block, count)
-    out32 = torch.empty(count, dtype=torch.int32, device=dev)
-    out64 = torch.empty(count, dtype=torch.int64, device=dev)
+    w = make_workload(args, dev, rank)
     stream = torch.cuda.current_stream(dev)
-
-    def step():
-        if args.kind == "crc32c":
-            S.crc32c_batch(spans, out=out32, stream=stream)
-        else:
-            S.xxh3_64_batch(spans, out=out64, stream=stream)
-
     for _ in range(args.warmup):
-        step()
+        w.step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -129,77 +264,59 @@ def main():
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
-        step()
+        w.step()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step
+    kern_ms = ev0.elapsed_time(ev1) / (args.steps * w.launches)
     if world > 1:
         t = torch.tensor([wall], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         wall = float(t.item())
 
-    verified = None
-    if not args.no_verify:
-        # bit-exact spot check of 64 random blocks against the CPU oracle
-        import random
+    verified = None if args.no_verify else w.check()
+    if verified is False:
+        print("bench: RESULT CHECK FAILED", file=sys.stderr)
 
-        import numpy as np
-        orc = ctypes.CDLL(os.path.join(REPO, "oracle", "liboracle.so"))
-        orc.orc_crc32c_value.restype = ctypes.c_uint32
-        orc.orc_crc32c_value.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
-        orc.orc_xxh3_64.restype = ctypes.c_uint64
-        orc.orc_xxh3_64.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
-        res = (out32.cpu().numpy().view(np.uint32) if args.kind == "crc32c"
-               else out64.cpu().numpy().view(np.uint64))
-        verified = True
-        for i in random.Random(rank).sample(range(count), 64):
-            b = data[i * block:(i + 1) * block].cpu().numpy().tobytes()
-            want = orc.orc_crc32c_value(b, block) if args.kind == "crc32c" else orc.orc_xxh3_64(b, block)
-            verified &= int(res[i]) == want
-        if not verified:
-            print("bench: RESULT MISMATCH vs oracle", file=sys.stderr)
-
-    total_bytes = count * block * world * args.steps
-    value = total_bytes / wall / 2**30
-    out_bytes = 4 if args.kind == "crc32c" else 8
-    alg_bytes = count * (block + out_bytes)  # per launch: spans read + results written
-    achieved = alg_bytes / (kern_ms * 1e-3)
-    roof = {
-        "bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
-        "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
-        "kernel": "mck::k_crc<OpCrcValue>" if args.kind == "crc32c" else "mck::k_xxh3<OpX3Value>",
-        "kernel_avg_ms": round(kern_ms, 4), "alg_bytes_per_launch": alg_bytes,
-    }
-    traffic_file = os.path.join(REPO, "profiles", f"traffic_{args.kind}_{block}.json")
-    if os.path.exists(traffic_file):
-        with open(traffic_file) as f:
-            tr = json.load(f)
-        if tr.get("blocks") == count:
-            roof["traffic"] = tr["hbm_bytes_per_launch"]
-            roof["traffic_source"] = os.path.relpath(traffic_file, REPO)
-
+    value = w.span_bytes * world * args.steps / wall / 2**30
+    roof = None
+    if args.workload != "host":
+        achieved = w.alg_bytes / (kern_ms * 1e-3)
+        roof = {
+            "bound": "hbm", "achieved": round(achieved / 1e9, 1), "peak": HBM_PEAK / 1e9,
+            "unit": "GB/s", "frac": round(achieved / HBM_PEAK, 4), "traffic": None,
+            "kernel": w.kernel, "kernel_avg_ms": round(kern_ms, 4),
+            "alg_bytes_per_launch": int(w.alg_bytes),
+        }
+        tf = os.path.join(REPO, "profiles", f"traffic_{args.workload}.json")
+        if os.path.exists(tf):
+            with open(tf) as f:
+                tr = json.load(f)
+            if tr.get("config") == w.cfg:
+                roof["traffic"] = tr["hbm_bytes_per_launch"]
+                roof["traffic_source"] = os.path.relpath(tf, REPO)
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(args, args.cpu_seconds)
-
+    if (rank == 0 and world == 1 and args.cpu_seconds > 0 and not args.no_verify
+            and args.workload in ("crc32c", "xxh3")):
+        cpu = cpu_baseline(args, args.workload, args.block_bytes, w.sample, w.lo32_sum)
+        if cpu is not None:
+            verified = cpu["agrees_with_gpu"]
+            if not verified:
+                print("bench: GPU checksums disagree with the reference", file=sys.stderr)
     if rank == 0:
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": "synthetic: torch.randint random bytes generated on-device (device-resident)",
-            "config": {
-                "workload": (f"{args.kind} over {count} x {block} B random blocks per GPU, "
-                             "device-resident (BASELINE.json configs[1])"),
-                "blocks_per_gpu": count, "block_bytes": block,
-                "parallelism": f"partitioned x{world} (no collective)",
-            },
-            "roofline": roof, "cpu_baseline": cpu, "verified_vs_oracle": verified,
+            "data": "synthetic: random bytes generated on-device (device-resident)"
+                    if args.workload != "host" else "synthetic: random bytes in pinned host memory",
+            "config": dict({"workload": w.desc, "parallelism": f"partitioned x{world} (no collective)"},
+                           **w.cfg),
+            "roofline": roof, "cpu_baseline": cpu, "verified": verified,
         }
         print(json.dumps(line))
     if world > 1:

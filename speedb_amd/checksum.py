@@ -292,18 +292,20 @@ def sst_trailer_batch(checksum_type: int, payloads: Spans, comp_types, file_offs
 
 
 def sst_verify_batch(checksum_type: int, payloads: Spans, file_offsets=None,
-                     base_context_checksum: int = 0, stream=None):
-    """Returns (mismatch uint8, computed int32, stored int32, mismatch_count int32[1])."""
+                     base_context_checksum: int = 0, stream=None, outs=None, with_count=True):
+    """Returns (mismatch uint8, computed int32, stored int32, mismatch_count
+    int32[1] or None).  ``outs`` = preallocated (mismatch, computed, stored)."""
     torch = _torch()
     dev = payloads.base.device
-    mismatch = _empty(payloads.count, torch.uint8, dev)
-    computed = _empty(payloads.count, torch.int32, dev)
-    stored = _empty(payloads.count, torch.int32, dev)
-    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    if outs is None:
+        outs = (_empty(payloads.count, torch.uint8, dev), _empty(payloads.count, torch.int32, dev),
+                _empty(payloads.count, torch.int32, dev))
+    mismatch, computed, stored = outs
+    count = torch.zeros(1, dtype=torch.int32, device=dev) if with_count else None
     s = payloads.c()
     check(lib.mck_sst_verify_batch(int(checksum_type), ctypes.byref(s), _ptr(file_offsets),
                                    base_context_checksum & 0xFFFFFFFF, mismatch.data_ptr(),
-                                   computed.data_ptr(), stored.data_ptr(), count.data_ptr(),
+                                   _ptr(computed), _ptr(stored), _ptr(count),
                                    _stream(stream)), "mck_sst_verify_batch")
     return mismatch, computed, stored, count
 
@@ -319,13 +321,14 @@ def wal_record_crc_batch(payloads: Spans, types, log_number: int = 0, out=None, 
     return out
 
 
-def wal_verify_batch(wal, nbytes: Optional[int] = None, log_number: int = 0, stream=None):
+def wal_verify_batch(wal, nbytes: Optional[int] = None, log_number: int = 0, stream=None,
+                     out=None):
     """Returns an int32 tensor [nblocks, 4]: records_ok, status, stop_offset, bytes_ok."""
     torch = _torch()
     if nbytes is None:
         nbytes = wal.numel()
     nblocks = (nbytes + 32767) // 32768
-    res = torch.empty((nblocks, 4), dtype=torch.int32, device=wal.device)
+    res = out if out is not None else torch.empty((nblocks, 4), dtype=torch.int32, device=wal.device)
     check(lib.mck_wal_verify_batch(wal.data_ptr(), nbytes, log_number & 0xFFFFFFFF,
                                    res.data_ptr(), _stream(stream)), "mck_wal_verify_batch")
     return res

@@ -653,7 +653,17 @@ int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* hos
     set_err("no HIP device");
     return MCK_ENODEV;
   }
-  if (ndev <= 0 || ndev > have) ndev = have;
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  // ndev <= 0: only the calling thread's current device (one process per
+  // GPU); otherwise devices [0, ndev)
+  std::vector<int> devs;
+  if (ndev <= 0) {
+    devs.push_back(prev);
+  } else {
+    for (int d = 0; d < std::min(ndev, have); d++) devs.push_back(d);
+  }
+  ndev = (int)devs.size();
   if (!chunk_bytes) chunk_bytes = 256u << 20;
   for (uint32_t i = 1; host_offsets && i < count; i++)
     if (host_offsets[i] < host_offsets[i - 1]) {
@@ -664,14 +674,12 @@ int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* hos
   mck_partition_spans(host_lengths, count, length, ndev, first.data());
   HostJob J{kind, static_cast<const uint8_t*>(host_base), host_offsets, host_lengths, stride, length,
             flags & MCK_F_MASK, chunk_bytes, out32, out64};
-  int prev = 0;
-  (void)hipGetDevice(&prev);
   std::vector<int> rcs(ndev, 0);
   std::vector<std::string> errs(ndev);
   std::vector<std::thread> th;
   for (int d = 0; d < ndev; d++)
     th.emplace_back([&, d] {
-      rcs[d] = run_device_share(d, J, first[d], first[d + 1]);
+      rcs[d] = run_device_share(devs[d], J, first[d], first[d + 1]);
       if (rcs[d]) errs[d] = t_err;
     });
   for (auto& t : th) t.join();
