@@ -51,8 +51,8 @@ def parse():
     p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
-    p.add_argument("--sst-bytes", type=int, default=2 << 30, help="per SST image (sst)")
-    p.add_argument("--wal-blocks", type=int, default=1 << 16, help="32 KiB blocks (wal)")
+    p.add_argument("--sst-bytes", type=int, default=1 << 30, help="per SST image (sst); 2 images")
+    p.add_argument("--wal-blocks", type=int, default=1 << 18, help="32 KiB blocks per GPU (wal)")
     p.add_argument("--host-bytes", type=int, default=4 << 30, help="pinned source bytes (host)")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="approximate CPU-baseline budget (0 disables)")
@@ -126,11 +126,11 @@ def make_workload(args, dev, rank):
         out64 = torch.empty(count, dtype=torch.int64, device=dev)
         if args.workload == "crc32c":
             w.step = lambda: S.crc32c_batch(spans, out=out32, stream=stream)
-            w.kernel = "mck::k_crc_uniform<OpCrcValue>"
+            w.kernel = "mck::k_crc_uniform<mck::OpCrcValue, true>"
             w.alg_bytes = count * (block + 4)
         else:
             w.step = lambda: S.xxh3_64_batch(spans, out=out64, stream=stream)
-            w.kernel = "mck::k_xxh3<OpX3Value>"
+            w.kernel = "mck::k_xxh3<mck::OpX3Value>"
             w.alg_bytes = count * (block + 8)
         w.span_bytes = count * block
         w.desc = (f"{args.workload} over {count} x {block} B random blocks per GPU, device-resident "
@@ -156,7 +156,7 @@ def make_workload(args, dev, rank):
                 res[im.checksum_type] = im.verify(stream=stream)
         w.step = step
         w.launches = 2
-        w.kernel = "mck::k_crc<OpCrcBlock<kModeVerify>> + mck::k_xxh3<OpX3Block<kModeVerify>>"
+        w.kernel = "mck::k_crc<mck::OpCrcBlock<2> > + mck::k_xxh3<mck::OpX3Block<2> >"
         w.span_bytes = sum(im.payload_bytes + im.count for im in imgs)  # payload + type byte
         # per launch: span bytes + 4 B stored + 8 B offset + 4 B length + 8 B
         # file offset in, 1 B flag + 4 + 4 B out
@@ -176,12 +176,12 @@ def make_workload(args, dev, rank):
             for im in imgs:
                 mm, _, _, cnt = im.verify(stream=stream, with_count=True)
                 ok &= int(cnt.item()) == 0 and int(mm.sum().item()) == 0
-                bad = sorted(random.Random(rank).sample(range(im.count), 8))
+                bad = sorted(random.Random(rank).sample(range(im.count), max(1, im.count // 1000)))
                 im.corrupt(bad)
                 mm, _, _, cnt = im.verify(stream=stream, with_count=True)
                 flagged = torch.nonzero(mm).flatten().cpu().tolist()
                 im.corrupt(bad)  # restore
-                ok &= flagged == bad and int(cnt.item()) == 8
+                ok &= flagged == bad and int(cnt.item()) == len(bad)
             return ok
         w.check = check
     elif args.workload == "wal":
@@ -219,7 +219,7 @@ def make_workload(args, dev, rank):
                 1, hbuf.data_ptr(), None, None, block, block, count, 0, 0, 256 << 20,
                 out.ctypes.data, None, ctypes.byref(secs)), "mck_host_batch_checksum")
         w.step = step
-        w.kernel = "mck::k_crc<OpCrcValue> (H2D/D2H overlapped)"
+        w.kernel = "mck::k_crc_uniform<mck::OpCrcValue, false> (H2D/D2H overlapped)"
         w.span_bytes = count * block
         w.alg_bytes = count * (block + 4 + 8 + 4)
         w.desc = (f"host-resident pinned {count} x {block} B blocks (SST-sized, 80M-key/1KB-value "
@@ -295,7 +295,7 @@ def main():
         if os.path.exists(tf):
             with open(tf) as f:
                 tr = json.load(f)
-            if tr.get("config") == w.cfg:
+            if tr.get("config") == w.cfg and tr.get("kernel") == w.kernel:
                 roof["traffic"] = tr["hbm_bytes_per_launch"]
                 roof["traffic_source"] = os.path.relpath(tf, REPO)
     cpu = None

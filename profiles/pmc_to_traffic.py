@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Turn a run_profile.sh output directory into the per-launch HBM traffic
+figure bench.py reports as roofline.traffic.
+
+  python profiles/pmc_to_traffic.py gpurun_out/prof_<tag> <workload>
+
+Reads the bench JSON line of the trace pass (kernel names + config), the
+kernel-trace stats (average duration of those kernels), and the FETCH_SIZE /
+WRITE_SIZE passes.  Corrections per MI355X_MICROARCH.md (HBM/rocprofv3):
+FETCH_SIZE and WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the
+bytes of a 16-B/lane streaming read, so it is doubled; WRITE_SIZE is exact.
+Writes profiles/traffic_<workload>.json and prints a summary.
+"""
+import csv
+import json
+import os
+import sys
+
+
+def bench_line(path):
+    with open(path) as f:
+        for ln in f:
+            if ln.startswith("{"):
+                return json.loads(ln)
+    raise SystemExit(f"no bench JSON line in {path}")
+
+
+def per_launch(path, names, counter):
+    vals = []
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if r["Counter_Name"] == counter and any(n in r["Kernel_Name"] for n in names):
+                vals.append(float(r["Counter_Value"]))
+    return vals
+
+
+def main():
+    d, workload = sys.argv[1], sys.argv[2]
+    line = bench_line(os.path.join(d, "bench_trace.txt"))
+    kernel = line["roofline"]["kernel"]
+    names = [k.strip() for k in kernel.split(" + ")]
+    cfg = {k: v for k, v in line["config"].items() if k not in ("workload", "parallelism")}
+    stats = {}
+    with open(os.path.join(d, "trace", "trace_kernel_stats.csv")) as f:
+        for r in csv.DictReader(f):
+            stats[r["Name"]] = r
+    avg_ns, calls = 0.0, 0
+    for name, r in stats.items():
+        if any(n in name for n in names):
+            avg_ns += float(r["TotalDurationNs"])
+            calls += int(r["Calls"])
+    fetch = per_launch(os.path.join(d, "pmc_fetch", "pmc_counter_collection.csv"), names, "FETCH_SIZE")
+    write = per_launch(os.path.join(d, "pmc_write", "pmc_counter_collection.csv"), names, "WRITE_SIZE")
+    if not fetch or not write:
+        raise SystemExit("no counter rows for " + kernel)
+    rd = 2 * 1024 * sum(fetch) / len(fetch)
+    wr = 1024 * sum(write) / len(write)
+    alg = line["roofline"]["alg_bytes_per_launch"]
+    out = {
+        "workload": workload, "kernel": kernel, "config": cfg,
+        "hbm_bytes_per_launch": int(rd + wr),
+        "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
+        "alg_bytes_per_launch": alg, "traffic_over_alg": round((rd + wr) / alg, 4),
+        "rocprof_avg_kernel_ns": round(avg_ns / max(calls, 1), 1), "rocprof_calls": calls,
+        "bench_kernel_avg_ms": line["roofline"]["kernel_avg_ms"],
+        "source": os.path.relpath(d),
+        "method": "FETCH_SIZE(KiB)*1024*2 (gfx950 16B/lane read correction) + WRITE_SIZE(KiB)*1024, "
+                  "averaged over the dominant kernel's dispatches; separate --pmc passes with "
+                  "--kernel-trace only",
+    }
+    dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"traffic_{workload}.json")
+    with open(dst, "w") as f:
+        json.dump(out, f, indent=1)
+        f.write("\n")
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
