@@ -400,6 +400,145 @@ uint64_t orc_xxh3_64(const void* data, size_t n) {
 }
 
 /* ------------------------------------------------------------------ */
+/* XXPH3 -- the XXH3 *preview* (v0.7.2) behind Hash64 / NPHash64        */
+/* (util/xxph3.h, util/hash.cc:81-88).  Same default secret as XXH3     */
+/* (util/xxph3.h:924), but its own length classes, avalanche constant, */
+/* non-swapping accumulate and block/last-stripe rules.                */
+/* ------------------------------------------------------------------ */
+
+/* primes P32_* / P64_* as above (util/xxph3.h:568-650, same values) */
+
+/* util/xxph3.h:1073 XXPH3_avalanche */
+static uint64_t xxph3_avalanche(uint64_t h) {
+  h ^= h >> 37;
+  h *= P64_3;
+  return h ^ (h >> 32);
+}
+
+/* util/xxph3.h:1086-1147 XXPH3_len_0to16_64b (incl. the RocksDB change for
+ * len 0 at 1139-1142) */
+static uint64_t xxph3_0to16(const uint8_t* in, size_t len, const uint8_t* sec, uint64_t seed) {
+  if (len > 8) {
+    uint64_t lo = rd64(in) ^ (rd64(sec) + seed);
+    uint64_t hi = rd64(in + len - 8) ^ (rd64(sec + 8) - seed);
+    return xxph3_avalanche(len + (lo + hi) + mul128_fold64(lo, hi));
+  }
+  if (len >= 4) {
+    uint64_t in64 = (uint64_t)rd32(in) | ((uint64_t)rd32(in + len - 4) << 32);
+    uint64_t keyed = in64 ^ (rd64(sec) + seed);
+    uint64_t mix = len + ((keyed ^ (keyed >> 51)) * P32_1);
+    return xxph3_avalanche((mix ^ (mix >> 47)) * P64_2);
+  }
+  if (len) {
+    uint32_t comb = (uint32_t)in[0] | ((uint32_t)in[len >> 1] << 8) | ((uint32_t)in[len - 1] << 16) |
+                    ((uint32_t)len << 24);
+    uint64_t keyed = (uint64_t)comb ^ ((uint64_t)rd32(sec) + seed);
+    return xxph3_avalanche(keyed * P64_1);
+  }
+  return mul128_fold64(seed + rd64(sec), P64_2);
+}
+
+/* util/xxph3.h:1644 XXPH3_mix16B */
+static uint64_t xxph3_mix16(const uint8_t* in, const uint8_t* sec, uint64_t seed) {
+  return mul128_fold64(rd64(in) ^ (rd64(sec) + seed), rd64(in + 8) ^ (rd64(sec + 8) - seed));
+}
+
+/* util/xxph3.h:1655 XXPH3_len_17to128_64b */
+static uint64_t xxph3_17to128(const uint8_t* in, size_t len, uint64_t seed) {
+  uint64_t acc = len * P64_1;
+  if (len > 32) {
+    if (len > 64) {
+      if (len > 96) {
+        acc += xxph3_mix16(in + 48, kSecret + 96, seed);
+        acc += xxph3_mix16(in + len - 64, kSecret + 112, seed);
+      }
+      acc += xxph3_mix16(in + 32, kSecret + 64, seed);
+      acc += xxph3_mix16(in + len - 48, kSecret + 80, seed);
+    }
+    acc += xxph3_mix16(in + 16, kSecret + 32, seed);
+    acc += xxph3_mix16(in + len - 32, kSecret + 48, seed);
+  }
+  acc += xxph3_mix16(in, kSecret, seed);
+  acc += xxph3_mix16(in + len - 16, kSecret + 16, seed);
+  return xxph3_avalanche(acc);
+}
+
+/* util/xxph3.h:1685 XXPH3_len_129to240_64b */
+static uint64_t xxph3_129to240(const uint8_t* in, size_t len, uint64_t seed) {
+  uint64_t acc = len * P64_1;
+  int rounds = (int)len / 16, i;
+  for (i = 0; i < 8; i++) acc += xxph3_mix16(in + 16 * i, kSecret + 16 * i, seed);
+  acc = xxph3_avalanche(acc);
+  for (i = 8; i < rounds; i++) acc += xxph3_mix16(in + 16 * i, kSecret + 16 * (i - 8) + 3, seed);
+  acc += xxph3_mix16(in + len - 16, kSecret + 136 - 17, seed);
+  return xxph3_avalanche(acc);
+}
+
+/* util/xxph3.h:1330-1344 scalar accumulate_512, XXPH3_acc_64bits (no lane
+ * swap) */
+static void xxph3_acc512(uint64_t acc[8], const uint8_t* in, const uint8_t* sec) {
+  for (int i = 0; i < 8; i++) {
+    uint64_t d = rd64(in + 8 * i), k = d ^ rd64(sec + 8 * i);
+    acc[i] += d;
+    acc[i] += (k & 0xFFFFFFFFu) * (k >> 32);
+  }
+}
+
+/* util/xxph3.h:1516-1543 hashLong_internal_loop + 1574-1587 merge, over a
+ * 192-byte secret */
+static uint64_t xxph3_long(const uint8_t* in, size_t len, const uint8_t* sec) {
+  uint64_t acc[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+  const size_t block = 1024, nb = len / block;
+  size_t n, s;
+  for (n = 0; n < nb; n++) {
+    for (s = 0; s < 16; s++) xxph3_acc512(acc, in + n * block + 64 * s, sec + 8 * s);
+    scramble(acc, sec + 128);
+  }
+  size_t stripes = (len - nb * block) / 64;
+  for (s = 0; s < stripes; s++) xxph3_acc512(acc, in + nb * block + 64 * s, sec + 8 * s);
+  if (len & 63) xxph3_acc512(acc, in + len - 64, sec + 192 - 64 - 7);
+  uint64_t r = len * P64_1;
+  for (int i = 0; i < 4; i++) r += mul128_fold64(acc[2 * i] ^ rd64(sec + 11 + 16 * i),
+                                                 acc[2 * i + 1] ^ rd64(sec + 19 + 16 * i));
+  return xxph3_avalanche(r);
+}
+
+/* util/xxph3.h:1737-1744 XXPH3_64bits_withSeed (long inputs with a seed use
+ * the custom secret of XXPH3_initCustomSecret, 1613-1624) */
+uint64_t orc_hash64(const void* data, size_t n, uint64_t seed) {
+  const uint8_t* in = (const uint8_t*)data;
+  if (n <= 16) return xxph3_0to16(in, n, kSecret, seed);
+  if (n <= 128) return xxph3_17to128(in, n, seed);
+  if (n <= 240) return xxph3_129to240(in, n, seed);
+  if (seed == 0) return xxph3_long(in, n, kSecret);
+  uint8_t sec[192];
+  for (int i = 0; i < 12; i++) {
+    uint64_t a = rd64(kSecret + 16 * i) + seed, b = rd64(kSecret + 16 * i + 8) - seed;
+    memcpy(sec + 16 * i, &a, 8);
+    memcpy(sec + 16 * i + 8, &b, 8);
+  }
+  return xxph3_long(in, n, sec);
+}
+
+/* db/kv_checksum.h:84-88 seeds; ProtectKV 324-331, ProtectKVO 296-306,
+ * ProtectS 456-462, ProtectC 432-438.  Fields hashed with NPHash64 and
+ * XORed; op type is 1 byte, the seqno 8 bytes LE, the CF id 4 bytes LE. */
+uint64_t orc_kv_protect(int mode, const void* key, size_t kn, const void* value, size_t vn,
+                        uint8_t op, uint64_t extra) {
+  uint64_t v = orc_hash64(key, kn, 0) ^ orc_hash64(value, vn, 0xD28AAD72F49BD50BULL);
+  if (mode >= 1) v ^= orc_hash64(&op, 1, 0xA5155AE5E937AA16ULL);
+  if (mode == 2) {
+    uint8_t b[8];
+    memcpy(b, &extra, 8);
+    v ^= orc_hash64(b, 8, 0x77A00858DDD37F21ULL);
+  } else if (mode == 3) {
+    uint32_t cf = (uint32_t)extra;
+    v ^= orc_hash64(&cf, 4, 0x4A2AB5CBD26F542CULL);
+  }
+  return v;
+}
+
+/* ------------------------------------------------------------------ */
 /* Block trailer / WAL record semantics                                */
 /* ------------------------------------------------------------------ */
 

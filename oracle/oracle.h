@@ -62,6 +62,16 @@ int orc_verify_block(int type, const void* block, size_t payload_len,
 uint32_t orc_wal_record_crc(uint8_t type, const void* payload, size_t n,
                             int recyclable, uint32_t log_number);
 
+/* util/hash.cc:81 Hash64 == util/hash.h:45 NPHash64 == XXPH3_64bits_withSeed
+ * (util/xxph3.h:1737), the preview XXH3 -- NOT XXH3_64bits. */
+uint64_t orc_hash64(const void* data, size_t n, uint64_t seed);
+
+/* db/kv_checksum.h per-KV protection (ProtectionInfo64), value as the
+ * Encode(8) bytes read LE.  mode 0 ProtectKV; 1 ProtectKVO(op); 2 KVO then
+ * ProtectS(seqno = extra); 3 KVO then ProtectC(cf = (uint32)extra). */
+uint64_t orc_kv_protect(int mode, const void* key, size_t kn, const void* value,
+                        size_t vn, uint8_t op, uint64_t extra);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,7 +1,8 @@
 // ref_shim.cc -- C-ABI wrapper over the REFERENCE's own checksum primitives.
 //
 // TEST INFRASTRUCTURE ONLY.  oracle/Makefile compiles this file together with
-// the reference's util/crc32c.cc and util/xxhash.cc, read in place from
+// the reference's util/crc32c.cc, util/xxhash.cc and util/hash.cc (and the
+// header-only db/kv_checksum.h), read in place from
 // /root/reference, into oracle/_ref/libspdb_ref.so (git-ignored).  Nothing is
 // copied into this repository.  It is used (a) to pin oracle.c, (b) to make
 // the golden fixtures under tests/golden/, and (c) as bench.py's
@@ -19,7 +20,9 @@
 #include <string>
 #include <vector>
 
+#include "db/kv_checksum.h"
 #include "util/crc32c.h"
+#include "util/hash.h"
 #include "util/xxhash.h"
 
 namespace c = ROCKSDB_NAMESPACE::crc32c;
@@ -43,6 +46,44 @@ uint32_t ref_xxh32(const void* p, size_t n, uint32_t seed) {
 }
 uint64_t ref_xxh64(const void* p, size_t n, uint64_t seed) {
   return XXH64(p, n, seed);
+}
+
+// util/hash.cc:81-88 Hash64 (= NPHash64, util/hash.h:45-64) -> XXPH3.
+uint64_t ref_hash64(const void* p, size_t n, uint64_t seed) {
+  return ROCKSDB_NAMESPACE::Hash64(static_cast<const char*>(p), n, seed);
+}
+
+// db/kv_checksum.h, the reference's own templates, read back through the
+// public Encode(8, ...):  mode 0 ProtectKV(key, value); 1 ProtectKVO(key,
+// value, op); 2 ProtectKVO(...).ProtectS(seq = extra); 3 ProtectKVO(...)
+// .ProtectC(cf = (uint32)extra).
+uint64_t ref_kv_protect(int mode, const void* key, size_t kn, const void* value,
+                        size_t vn, uint8_t op, uint64_t extra) {
+  namespace R = ROCKSDB_NAMESPACE;
+  const R::Slice k(static_cast<const char*>(key), kn);
+  const R::Slice v(static_cast<const char*>(value), vn);
+  const R::ValueType t = static_cast<R::ValueType>(op);
+  char buf[8];
+  switch (mode) {
+    case 0:
+      R::ProtectionInfo64().ProtectKV(k, v).Encode(8, buf);
+      break;
+    case 1:
+      R::ProtectionInfo64().ProtectKVO(k, v, t).Encode(8, buf);
+      break;
+    case 2:
+      R::ProtectionInfo64().ProtectKVO(k, v, t).ProtectS(extra).Encode(8, buf);
+      break;
+    default:
+      R::ProtectionInfo64()
+          .ProtectKVO(k, v, t)
+          .ProtectC(static_cast<uint32_t>(extra))
+          .Encode(8, buf);
+      break;
+  }
+  uint64_t r;
+  memcpy(&r, buf, 8);  // EncodeFixed64 is little-endian
+  return r;
 }
 
 // table/format.cc:578-602 over the reference primitives.

@@ -3,7 +3,8 @@
 * ``oracle``  -- ctypes handle on oracle/liboracle.so, the CPU restatement of
   the reference checksum path (TEST INFRASTRUCTURE; built on demand with make).
 * ``ref``     -- ctypes handle on oracle/_ref/libspdb_ref.so (the reference's
-  own util/crc32c.cc + util/xxhash.cc), or None when it was not built.
+  own util/crc32c.cc + util/xxhash.cc + util/hash.cc), or None when it was
+  not built.
 * ``golden``  -- tests/golden/vectors.json + blob.bin + kat.json.
 
 Tests that need a GPU carry ``@pytest.mark.gpu``.
@@ -48,6 +49,11 @@ def _bind(lib, prefix):
             "verify_block": (c.c_int, [c.c_int, c.c_char_p, c.c_size_t, c.c_uint32, c.c_uint64,
                                        ctypes.POINTER(c.c_uint32), ctypes.POINTER(c.c_uint32)]),
         })
+    sig.update({
+        "hash64": (c.c_uint64, [c.c_char_p, c.c_size_t, c.c_uint64]),
+        "kv_protect": (c.c_uint64, [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p, c.c_size_t,
+                                    c.c_uint8, c.c_uint64]),
+    })
     for name, (res, args) in sig.items():
         f = getattr(lib, f"{prefix}_{name}")
         f.restype, f.argtypes = res, args
@@ -92,6 +98,12 @@ class _Oracle:
 
     def ContextModifier(self, base, off):
         return self.lib.orc_context_modifier(base, off)
+
+    def Hash64(self, b, seed=0):
+        return self.lib.orc_hash64(b, len(b), seed)
+
+    def KvProtect(self, mode, key, value, op=0, extra=0):
+        return self.lib.orc_kv_protect(mode, key, len(key), value, len(value), op, extra)
 
     def WalRecordCrc(self, t, payload, recyclable, log_number):
         return self.lib.orc_wal_record_crc(t, payload, len(payload), 1 if recyclable else 0,

@@ -57,6 +57,9 @@ def load_ref():
         "ref_builtin_checksum": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
         "ref_wal_record_crc": (ctypes.c_uint32, [ctypes.c_uint8, ctypes.c_char_p, ctypes.c_size_t,
                                                  ctypes.c_int, ctypes.c_uint32]),
+        "ref_hash64": (ctypes.c_uint64, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64]),
+        "ref_kv_protect": (ctypes.c_uint64, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                             ctypes.c_size_t, ctypes.c_uint8, ctypes.c_uint64]),
     }
     for k, (res, args) in sig.items():
         f = getattr(r, k)
@@ -116,11 +119,32 @@ def main():
         wal.append({"type": t, "off": off, "len": n, "recyclable": recyclable, "log_number": ln,
                     "crc": ref.ref_wal_record_crc(t, blob[off:off + n], n, recyclable, ln)})
     type_crc = [ref.ref_crc32c_value(bytes([t]), 1) for t in range(12)]
+    # per-KV protection (db/kv_checksum.h): Hash64 = XXPH3 with the field seeds
+    rng2 = random.Random(20261016)
+    seeds = [0, 0xD28AAD72F49BD50B, 0xA5155AE5E937AA16, 0x77A00858DDD37F21, 0x4A2AB5CBD26F542C]
+    hash64 = []
+    for n in (list(range(0, 260)) + [511, 512, 513, 1000, 1023, 1024, 1025, 1088, 2047, 2048, 2049,
+                                     3071, 3072, 4096, 4100, 8191, 16384]
+              + [rng2.randrange(0, 20000) for _ in range(24)]):
+        off = rng2.randrange(0, BLOB_BYTES - n)
+        seed = seeds[n % 5] if n % 7 else rng2.getrandbits(64)
+        hash64.append({"off": off, "len": n, "seed": seed,
+                       "out": ref.ref_hash64(blob[off:off + n], n, seed)})
+    kv = []
+    for i in range(200):
+        kn = rng2.choice([0, 1, 8, 16, 24, rng2.randrange(0, 300)])
+        vn = rng2.choice([0, 1, 100, 240, 241, 1000, 1024, rng2.randrange(0, 5000)])
+        ko, vo = rng2.randrange(0, BLOB_BYTES - kn), rng2.randrange(0, BLOB_BYTES - vn)
+        mode, op, extra = i % 4, rng2.randrange(0, 256), rng2.getrandbits(64)
+        kv.append({"mode": mode, "koff": ko, "klen": kn, "voff": vo, "vlen": vn, "op": op, "extra": extra,
+                   "out": ref.ref_kv_protect(mode, blob[ko:ko + kn], kn, blob[vo:vo + vn], vn, op, extra)})
     out = {"blob_seed": BLOB_SEED, "blob_bytes": BLOB_BYTES, "cases": cases, "combine": combine,
-           "context_modifier": ctx, "wal_records": wal, "wal_type_crc": type_crc}
+           "context_modifier": ctx, "wal_records": wal, "wal_type_crc": type_crc,
+           "hash64": hash64, "kv_protect": kv}
     with open(os.path.join(HERE, "vectors.json"), "w") as f:
         json.dump(out, f, indent=0)
-    print(f"wrote {len(cases)} cases, {len(combine)} combine, {len(ctx)} ctx, {len(wal)} wal")
+    print(f"wrote {len(cases)} cases, {len(combine)} combine, {len(ctx)} ctx, {len(wal)} wal, "
+          f"{len(hash64)} hash64, {len(kv)} kv_protect")
 
 
 if __name__ == "__main__":

@@ -123,6 +123,34 @@ def test_vectors_from_reference(oracle, golden):
         assert oracle.Value(bytes([t])) == v
 
 
+def test_hash64_small_value_schema(oracle, golden):
+    """util/hash_test.cc:162-228: Hash64 (XXPH3, seed 0) of short strings."""
+    for h, v in golden["kat"]["hash64_small"]:
+        assert oracle.Hash64(bytes.fromhex(h)) == int(v), h
+
+
+def test_hash64_large_value_schema(oracle, golden):
+    """util/hash_test.cc:216-279: the mod-61 descriptor of Hash64 over every
+    prefix length < 430 of a repeated string (covers all XXPH3 length classes
+    up to the long loop)."""
+    enc = "abcdefghijklmnopqrstuvwxyz123456789ABCDEFGHIJKLMNOPQRSTUVWXYZ"
+    for rep, want in golden["kat"]["hash64_descriptors"].items():
+        inp = (rep * 430)[:430].encode()
+        got = "".join(enc[oracle.Hash64(inp[:i]) % 61] for i in range(430))
+        assert got == want, rep
+
+
+def test_hash64_and_kv_protect_vectors(oracle, golden):
+    blob = golden["blob"]
+    for c in golden["hash64"]:
+        d = blob[c["off"]:c["off"] + c["len"]]
+        assert oracle.Hash64(d, c["seed"]) == c["out"], (c["len"], c["seed"])
+    for c in golden["kv_protect"]:
+        k = blob[c["koff"]:c["koff"] + c["klen"]]
+        v = blob[c["voff"]:c["voff"] + c["vlen"]]
+        assert oracle.KvProtect(c["mode"], k, v, c["op"], c["extra"]) == c["out"]
+
+
 def test_oracle_vs_live_reference(oracle, ref):
     if ref is None:
         pytest.skip("oracle/_ref not built")
@@ -137,6 +165,8 @@ def test_oracle_vs_live_reference(oracle, ref):
         assert oracle.XXH64(d, 9) == ref.ref_xxh64(d, n, 9)
         for t in range(5):
             assert oracle.Builtin(t, d) == ref.ref_builtin_checksum(t, d, n)
+        seed = rnd.choice([0, rnd.getrandbits(64)])
+        assert oracle.Hash64(d, seed) == ref.ref_hash64(d, n, seed)
 
 
 def test_wal_writer_layout(oracle):
