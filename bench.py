@@ -15,6 +15,8 @@ Default workload (the headline, BASELINE.json configs[1]): CRC32C over
                        ReadPhysicalRecord CRC verify of every record
   host     configs[4]  host-resident (pinned) 4.2 KiB SST-sized blocks,
                        H2D + CRC32C + D2H double-buffered through the GPU
+  kv       (row a12)   per-KV protection of memtable inserts, README shape
+                       (16 B key, 1000 B value): ProtectKVO(...).ProtectS(seq)
 
 One step = one pass of the workload's kernel(s) over the rank's whole batch.
 With N > 1 (torchrun, one process per GPU) every rank checksums its own
@@ -48,11 +50,12 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host"], default="crc32c")
+    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
     p.add_argument("--sst-bytes", type=int, default=1 << 30, help="per SST image (sst); 2 images")
     p.add_argument("--wal-blocks", type=int, default=1 << 18, help="32 KiB blocks per GPU (wal)")
+    p.add_argument("--kvs", type=int, default=1 << 22, help="KVs per GPU (kv)")
     p.add_argument("--host-bytes", type=int, default=4 << 30, help="pinned source bytes (host)")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="approximate CPU-baseline budget (0 disables)")
@@ -109,7 +112,7 @@ class Workload:
     check() -> bool verifies results (bit-exact spot checks)."""
 
 
-def make_workload(args, dev, rank):
+def make_workload(args, dev, rank, world):
     import numpy as np
     import torch
 
@@ -120,7 +123,12 @@ def make_workload(args, dev, rank):
     w = Workload()
     w.launches = 1
     if args.workload in ("crc32c", "xxh3"):
-        count, block = args.blocks, args.block_bytes
+        from speedb_amd import shard
+        block = args.block_bytes
+        # global batch = blocks x world (weak scaling); this rank's contiguous
+        # byte-balanced shard of it
+        b, e = shard.rank_range(None, args.blocks * world, world, rank, length=block)
+        count = e - b
         data, spans = W.uniform_blocks(count, block, dev, seed=1000 + rank)
         out32 = torch.empty(count, dtype=torch.int32, device=dev)
         out64 = torch.empty(count, dtype=torch.int64, device=dev)
@@ -203,6 +211,40 @@ def make_workload(args, dev, rank):
             r = res["r"].cpu()
             return bool((r[:, 0] == 1).all() and (r[:, 1] == 0).all())
         w.check = check
+    elif args.workload == "kv":
+        count, kb, vb = args.kvs, 16, 1000
+        keys = W.rand_bytes(count * kb + 64, dev, 400 + rank)
+        vals = W.rand_bytes(count * vb + 64, dev, 401 + rank)
+        ks, vs = S.Spans.uniform(keys, kb, count), S.Spans.uniform(vals, vb, count)
+        ops = W.rand_bytes(count, dev, 402 + rank)
+        seqs = torch.arange(count, dtype=torch.int64, device=dev) + (rank << 40)
+        out = torch.empty(count, dtype=torch.int64, device=dev)
+        w.step = lambda: S.kv_protect_batch(S.ProtectionKind.KVOS, ks, vs, ops, seqs, out=out, stream=stream)
+        w.kernel = "mck::k_xph3<mck::OpKvProtect<false> >"
+        w.span_bytes = count * (kb + vb)
+        w.alg_bytes = count * (kb + vb + 1 + 8 + 8)
+        w.desc = (f"per-KV protection ProtectKVO(key, value, op).ProtectS(seqno) (db/kv_checksum.h) of "
+                  f"{count} KVs per GPU, {kb} B keys + {vb} B values (README 80M-key/1KB-value shape)")
+        w.cfg = {"kvs_per_gpu": count, "key_bytes": kb, "value_bytes": vb}
+
+        def check():
+            # the batched kernel == ProtectionInfo64 composed from scalar
+            # NPHash64 field hashes (both on the GPU, different code paths)
+            import random
+            res = out.cpu().numpy().view(np.uint64)
+            kh = keys.cpu().numpy()
+            vh = vals.cpu().numpy()
+            oh = ops.cpu().numpy()
+            ok = True
+            for i in random.Random(rank).sample(range(count), 16):
+                k = kh[i * kb:(i + 1) * kb].tobytes()
+                v = vh[i * vb:(i + 1) * vb].tobytes()
+                want = (S.NPHash64(k, 0) ^ S.NPHash64(v, 0xD28AAD72F49BD50B)
+                        ^ S.NPHash64(bytes([int(oh[i])]), 0xA5155AE5E937AA16)
+                        ^ S.NPHash64(int(i + (rank << 40)).to_bytes(8, "little"), 0x77A00858DDD37F21))
+                ok &= int(res[i]) == want
+            return ok
+        w.check = check
     else:  # host
         import numpy as np
         from speedb_amd import _lib
@@ -251,13 +293,13 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    w = make_workload(args, dev, rank)
+    from speedb_amd import shard
+    w = make_workload(args, dev, rank, world)
     stream = torch.cuda.current_stream(dev)
     for _ in range(args.warmup):
         w.step()
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    shard.barrier(dev)
     torch.cuda.synchronize(dev)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -267,21 +309,16 @@ def main():
         w.step()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    shard.barrier(dev)
     torch.cuda.synchronize(dev)
-    wall = time.perf_counter() - t0
+    wall = shard.reduce_max(time.perf_counter() - t0, dev)
     kern_ms = ev0.elapsed_time(ev1) / (args.steps * w.launches)
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
 
     verified = None if args.no_verify else w.check()
     if verified is False:
         print("bench: RESULT CHECK FAILED", file=sys.stderr)
 
-    value = w.span_bytes * world * args.steps / wall / 2**30
+    value = shard.reduce_sum(int(w.span_bytes), dev) * args.steps / wall / 2**30
     roof = None
     if args.workload != "host":
         achieved = w.alg_bytes / (kern_ms * 1e-3)

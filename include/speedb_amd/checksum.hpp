@@ -188,6 +188,61 @@ inline uint32_t PhysicalRecordCrc(RecordType t, const char* payload, size_t n, u
 }
 }  // namespace log
 
+// util/hash.h:45 NPHash64 / util/hash.cc:81 Hash64 -- XXPH3 on the GPU.
+inline uint64_t NPHash64(const char* data, size_t n, uint64_t seed = 0) { return mck_np_hash64(data, n, seed); }
+inline uint64_t Hash64(const char* data, size_t n, uint64_t seed = 0) { return mck_np_hash64(data, n, seed); }
+
+// db/kv_checksum.h ProtectionInfo64, flattened: one value type whose Protect*
+// / Strip* / Update* steps XOR in the NPHash64 of a field with that field's
+// seed (:84-88), exactly as the reference's template chain does.
+class ProtectionInfo64 {
+ public:
+  static constexpr uint64_t kSeedK = 0, kSeedV = 0xD28AAD72F49BD50Bull, kSeedO = 0xA5155AE5E937AA16ull,
+                            kSeedS = 0x77A00858DDD37F21ull, kSeedC = 0x4A2AB5CBD26F542Cull;
+  ProtectionInfo64() = default;
+  explicit ProtectionInfo64(uint64_t v) : val_(v) {}
+  uint64_t GetVal() const { return val_; }
+  // ProtectKV (:324) / ProtectKVO (:296) / StripKVO (:400)
+  ProtectionInfo64 ProtectKV(const std::string& key, const std::string& value) const {
+    return ProtectionInfo64(val_ ^ NPHash64(key.data(), key.size(), kSeedK) ^
+                            NPHash64(value.data(), value.size(), kSeedV));
+  }
+  ProtectionInfo64 ProtectKVO(const std::string& key, const std::string& value, uint8_t op_type) const {
+    const char t = static_cast<char>(op_type);
+    return ProtectionInfo64(ProtectKV(key, value).val_ ^ NPHash64(&t, 1, kSeedO));
+  }
+  ProtectionInfo64 StripKVO(const std::string& key, const std::string& value, uint8_t op_type) const {
+    return ProtectKVO(key, value, op_type);  // XOR is its own inverse
+  }
+  // ProtectS (:456) / StripS (:466), ProtectC (:432) / StripC (:442)
+  ProtectionInfo64 ProtectS(uint64_t seqno) const {
+    char b[8];
+    for (int i = 0; i < 8; i++) b[i] = static_cast<char>(seqno >> (8 * i));
+    return ProtectionInfo64(val_ ^ NPHash64(b, 8, kSeedS));
+  }
+  ProtectionInfo64 StripS(uint64_t seqno) const { return ProtectS(seqno); }
+  ProtectionInfo64 ProtectC(uint32_t cf) const {
+    char b[4];
+    for (int i = 0; i < 4; i++) b[i] = static_cast<char>(cf >> (8 * i));
+    return ProtectionInfo64(val_ ^ NPHash64(b, 4, kSeedC));
+  }
+  ProtectionInfo64 StripC(uint32_t cf) const { return ProtectC(cf); }
+  // Encode / Verify (:80-121): the low `len` bytes, little-endian
+  void Encode(uint8_t len, char* dst) const {
+    for (int i = 0; i < len; i++) dst[i] = static_cast<char>(val_ >> (8 * i));
+  }
+  bool Verify(uint8_t len, const char* p) const {
+    for (int i = 0; i < len; i++)
+      if (static_cast<uint8_t>(p[i]) != static_cast<uint8_t>(val_ >> (8 * i))) return false;
+    return true;
+  }
+  // GetStatus (:286-292)
+  Status GetStatus() const { return val_ ? Status::Corruption("ProtectionInfo mismatch") : Status::OK(); }
+
+ private:
+  uint64_t val_ = 0;
+};
+
 // ---------------------------------------------------------------------------
 // inline definitions of the batched helpers (need HIP for device buffers)
 // ---------------------------------------------------------------------------

@@ -89,6 +89,8 @@ uint32_t mck_crc32c_value(const void* data, size_t n);
 uint64_t mck_xxh3_64(const void* data, size_t n);
 /* table/format.cc:578 ComputeBuiltinChecksum */
 uint32_t mck_builtin_checksum(int type, const void* data, size_t n);
+/* util/hash.h:45 NPHash64 / util/hash.cc:81 Hash64 (XXPH3, seeded) */
+uint64_t mck_np_hash64(const void* data, size_t n, uint64_t seed);
 /* table/format.cc:604 ComputeBuiltinChecksumWithLastByte */
 uint32_t mck_builtin_checksum_with_last_byte(int type, const void* data,
                                              size_t n, char last_byte);
@@ -196,6 +198,44 @@ typedef struct mck_wal_block_result {
 int mck_wal_verify_batch(const void* wal, uint64_t nbytes,
                          uint32_t log_number, mck_wal_block_result* results,
                          mck_stream_t stream);
+
+/* ---- per-KV protection ----------------------------- */
+
+/* util/hash.h:45 NPHash64 == util/hash.cc:81 Hash64 == XXPH3_64bits_withSeed
+ * (util/xxph3.h:1737), the XXH3 *preview* -- not XXH3_64bits.
+ * out[i] = NPHash64(span i, seed). */
+int mck_np_hash64_batch(const mck_spans* spans, uint64_t seed, uint64_t* out,
+                        mck_stream_t stream);
+
+/* db/kv_checksum.h ProtectionInfo64 of a batch of KVs (key span i, value
+ * span i, same count):
+ *   MCK_KV_PROTECT_KV    ProtectKV(key, value)                (:324)
+ *   MCK_KV_PROTECT_KVO   ProtectKVO(key, value, op_types[i])  (:296)
+ *   MCK_KV_PROTECT_KVOS  ProtectKVO(...).ProtectS(extras[i])  (:456; seqno)
+ *   MCK_KV_PROTECT_KVOC  ProtectKVO(...).ProtectC(extras[i])  (:432; CF id)
+ * out[i] = the u64 protection value; its Encode(len) form
+ * (db/kv_checksum.h:80-98) is the low `len` bytes, little-endian.
+ * op_types: device [count] (NULL = 0); extras: device [count] u64. */
+#define MCK_KV_PROTECT_KV 0
+#define MCK_KV_PROTECT_KVO 1
+#define MCK_KV_PROTECT_KVOS 2
+#define MCK_KV_PROTECT_KVOC 3
+int mck_kv_protect_batch(int kind, const mck_spans* keys,
+                         const mck_spans* values, const uint8_t* op_types,
+                         const uint64_t* extras, uint64_t* out,
+                         mck_stream_t stream);
+
+/* ProtectionInfo::Verify(prot_bytes, stored + i*prot_bytes) (db/kv_checksum.h
+ * :100-121) for every KV: mismatch[i] = 0/1; mismatch_count (optional,
+ * caller-zeroed) counts mismatches; computed (optional) gets the u64 values.
+ * prot_bytes: 1, 2, 4 or 8. */
+int mck_kv_protect_verify_batch(int kind, const mck_spans* keys,
+                                const mck_spans* values,
+                                const uint8_t* op_types,
+                                const uint64_t* extras, const uint8_t* stored,
+                                uint32_t prot_bytes, uint8_t* mismatch,
+                                uint32_t* mismatch_count, uint64_t* computed,
+                                mck_stream_t stream);
 
 /* ========================================================================= */
 /* 3. Multi-GPU / host-resident input                                       */

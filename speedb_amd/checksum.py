@@ -145,6 +145,16 @@ def ComputeBuiltinChecksumWithLastByte(checksum_type: int, data, last_byte) -> i
     return _checked(lib.mck_builtin_checksum_with_last_byte(int(checksum_type), b, n, last_byte))
 
 
+def NPHash64(data, seed: int = 0) -> int:
+    """util/hash.h:45 NPHash64 == util/hash.cc:81 Hash64: XXPH3 (the XXH3
+    preview), seeded -- computed on the GPU."""
+    b, n = _buf(data)
+    return _checked(lib.mck_np_hash64(b, n, seed & 0xFFFFFFFFFFFFFFFF))
+
+
+Hash64 = NPHash64
+
+
 def ChecksumModifierForContext(base_context_checksum: int, offset: int) -> int:
     return lib.mck_context_modifier(base_context_checksum & 0xFFFFFFFF, offset)
 
@@ -334,6 +344,56 @@ def wal_verify_batch(wal, nbytes: Optional[int] = None, log_number: int = 0, str
     return res
 
 
+def np_hash64_batch(spans: Spans, seed: int = 0, out=None, stream=None):
+    """out[i] = NPHash64(span i, seed) (int64 tensor of the u64 bit patterns)."""
+    torch = _torch()
+    if out is None:
+        out = _empty(spans.count, torch.int64, spans.base.device)
+    s = spans.c()
+    check(lib.mck_np_hash64_batch(ctypes.byref(s), seed & 0xFFFFFFFFFFFFFFFF, out.data_ptr(),
+                                  _stream(stream)), "mck_np_hash64_batch")
+    return out
+
+
+class ProtectionKind(enum.IntEnum):
+    """Which db/kv_checksum.h ProtectionInfo64 value a batch computes."""
+    KV = 0    # ProtectKV(key, value)
+    KVO = 1   # ProtectKVO(key, value, op_type)
+    KVOS = 2  # ProtectKVO(...).ProtectS(seqno)
+    KVOC = 3  # ProtectKVO(...).ProtectC(column_family_id)
+
+
+def kv_protect_batch(kind: int, keys: Spans, values: Spans, op_types=None, extras=None, out=None,
+                     stream=None):
+    """Per-KV protection values (u64 bit patterns in an int64 tensor)."""
+    torch = _torch()
+    if out is None:
+        out = _empty(values.count, torch.int64, values.base.device)
+    k, v = keys.c(), values.c()
+    check(lib.mck_kv_protect_batch(int(kind), ctypes.byref(k), ctypes.byref(v), _ptr(op_types),
+                                   _ptr(extras), out.data_ptr(), _stream(stream)),
+          "mck_kv_protect_batch")
+    return out
+
+
+def kv_protect_verify_batch(kind: int, keys: Spans, values: Spans, stored, prot_bytes: int,
+                            op_types=None, extras=None, stream=None):
+    """ProtectionInfo::Verify for every KV against ``stored`` (uint8 tensor of
+    count*prot_bytes).  Returns (mismatch uint8, mismatch_count int32[1],
+    computed int64)."""
+    torch = _torch()
+    dev = values.base.device
+    mismatch = _empty(values.count, torch.uint8, dev)
+    computed = _empty(values.count, torch.int64, dev)
+    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    k, v = keys.c(), values.c()
+    check(lib.mck_kv_protect_verify_batch(int(kind), ctypes.byref(k), ctypes.byref(v), _ptr(op_types),
+                                          _ptr(extras), stored.data_ptr(), prot_bytes,
+                                          mismatch.data_ptr(), count.data_ptr(), computed.data_ptr(),
+                                          _stream(stream)), "mck_kv_protect_verify_batch")
+    return mismatch, count, computed
+
+
 def device_count() -> int:
     return lib.mck_device_count()
 
@@ -344,5 +404,6 @@ __all__ = [
     "ChecksumModifierForContext", "VerifyBlockChecksum", "Spans", "crc32c_batch",
     "xxh3_64_batch", "xxh32_batch", "xxh64_batch", "builtin_checksum_batch",
     "sst_trailer_batch", "sst_verify_batch", "wal_record_crc_batch", "wal_verify_batch",
-    "device_count", "mck_wal_block_result",
+    "device_count", "mck_wal_block_result", "NPHash64", "Hash64", "np_hash64_batch",
+    "ProtectionKind", "kv_protect_batch", "kv_protect_verify_batch",
 ]

@@ -133,10 +133,13 @@ __global__ __launch_bounds__(1024) void k_crc_uniform(Op op, CrcUniform U, uint3
 }
 
 // ============================ XXH3 ========================================
-// one span per 16-lane row (see xxh3_rows_driver)
-template <class Op>
+// one span per 16-lane row (xxh3_rows_driver) or per wave (xxh3_wave_driver)
+template <class Op, bool WAVE = false>
 __global__ __launch_bounds__(256) void k_xxh3(Op op, uint32_t count) {
-  xxh3_rows_driver(op, count);
+  if (WAVE)
+    xxh3_wave_driver<Op, false>(op, count, 0);
+  else
+    xxh3_rows_driver(op, count);
 }
 
 struct OpX3Value {
@@ -173,6 +176,68 @@ struct OpX3Block {
     else
       v = n == 0 ? 0u : (uint32_t)h ^ (uint32_t)p[n - 1] * kRandomPrime;
     block_epilogue<MODE>(a, i, v);
+  }
+};
+
+// ===================== XXPH3: Hash64 / per-KV protection =================
+// Same row driver as XXH3, preview rules (util/xxph3.h), seeded.
+template <class Op>
+__global__ __launch_bounds__(256) void k_xph3(Op op, uint32_t count, uint64_t seed) {
+  xxh3_rows_driver<Op, true>(op, count, seed);
+}
+
+// util/hash.h:45 NPHash64(data, n, seed) == util/hash.cc:81 Hash64
+struct OpXpValue {
+  SpanSrc s;
+  uint64_t* out;
+  __device__ const uint8_t* base() const { return s.base; }
+  __device__ uint64_t off(uint32_t i) const { return s.off(i); }
+  __device__ uint64_t hlen(uint32_t i) const { return s.len(i); }
+  __device__ void finish(uint32_t i, uint64_t h) const { out[i] = h; }
+};
+
+// db/kv_checksum.h:84-88 field seeds
+constexpr uint64_t kSeedK = 0, kSeedV = 0xD28AAD72F49BD50Bull, kSeedO = 0xA5155AE5E937AA16ull,
+                   kSeedS = 0x77A00858DDD37F21ull, kSeedC = 0x4A2AB5CBD26F542Cull;
+
+// ProtectionInfo64 of one KV (db/kv_checksum.h): the row driver hashes the
+// VALUE (seed kSeedV); finish() XORs in the key (seed 0), and per kind the op
+// type (1 byte), seqno (8 bytes LE) or CF id (4 bytes LE).
+//   kind 0 ProtectKV (:324), 1 ProtectKVO (:296), 2 ProtectKVO.ProtectS
+//   (:456), 3 ProtectKVO.ProtectC (:432)
+// VERIFY: ProtectionInfo::Verify(len, stored) (:103-121): the low
+// `prot_bytes` bytes of the value against stored[i*prot_bytes ..].
+template <bool VERIFY>
+struct OpKvProtect {
+  SpanSrc keys, values;
+  const uint8_t* ops;
+  const uint64_t* extras;
+  int kind;
+  uint64_t* out;
+  const uint8_t* stored;
+  uint32_t prot_bytes;
+  uint8_t* mismatch;
+  uint32_t* mismatch_count;
+  __device__ const uint8_t* base() const { return values.base; }
+  __device__ uint64_t off(uint32_t i) const { return values.off(i); }
+  __device__ uint64_t hlen(uint32_t i) const { return values.len(i); }
+  __device__ void finish(uint32_t i, uint64_t hv) const {
+    uint64_t v = hv ^ xxph3_any(keys.ptr(i), keys.len(i), kSeedK);
+    if (kind >= 1) v ^= xxph3_u8(ops ? ops[i] : 0u, kSeedO);
+    if (kind == 2) v ^= xxph3_u64(extras[i], kSeedS);
+    if (kind == 3) v ^= xxph3_u32((uint32_t)extras[i], kSeedC);
+    if (!VERIFY) {
+      out[i] = v;
+      return;
+    }
+    const uint8_t* st = stored + (uint64_t)i * prot_bytes;
+    uint64_t sv = 0;
+    for (uint32_t b = 0; b < prot_bytes; b++) sv |= (uint64_t)st[b] << (8 * b);
+    const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
+    const bool bad = sv != (v & keep);
+    mismatch[i] = bad;
+    if (out) out[i] = v;
+    if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
   }
 };
 

@@ -1,5 +1,7 @@
 // mck_xxh.hpp -- device XXH3-64 (16-lane row per span) and legacy XXH32/XXH64
-// (lane per span), xxHash v0.8.1 as vendored at util/xxhash.h.
+// (lane per span), xxHash v0.8.1 as vendored at util/xxhash.h; and XXPH3,
+// the XXH3 preview (v0.7.2, util/xxph3.h) behind Hash64 / NPHash64, which
+// runs on the same row driver (template flag PREVIEW).
 //
 // XXH3 long inputs (n > 240, util/xxhash.h:5141-5227): 8 u64 accumulators;
 // each 1 KiB segment = 16 stripes x 64 B, and within a segment the 128
@@ -54,6 +56,18 @@ __device__ __forceinline__ uint32_t sec32(int off) {
   for (int b = 3; b >= 0; b--) v = (v << 8) | kXxh3Secret[off + b];
   return v;
 }
+// 8 bytes at byte offset `off` of the seeded secret of
+// XXPH3_initCustomSecret (util/xxph3.h:1613-1624): 8-byte word w of the
+// default secret gets +seed (w even) or -seed (w odd).  seed 0 = the default
+// secret, so XXH3 v0.8.1 uses the same accessor.
+__device__ __forceinline__ uint64_t csec64(int off, uint64_t seed) {
+  const int w = off >> 3, sh = (off & 7) * 8;
+  const uint64_t lo = sec64(8 * w) + ((w & 1) ? 0 - seed : seed);
+  if (sh == 0) return lo;
+  const uint64_t hi = sec64(8 * w + 8) + (((w + 1) & 1) ? 0 - seed : seed);
+  return (lo >> sh) | (hi << (64 - sh));
+}
+
 // unaligned little-endian reads from device memory
 __device__ __forceinline__ uint64_t rd64(const uint8_t* p) {
   uint64_t v;
@@ -144,6 +158,109 @@ __device__ __noinline__ uint64_t xxh3_short(const uint8_t* in, uint64_t len) {
   return xxh3_avalanche(acc + acc_end);
 }
 
+// ---- XXPH3 (the XXH3 preview v0.7.2 behind Hash64/NPHash64) ---------------
+// util/xxph3.h; util/hash.cc:81-88.  Differs from v0.8.1 in the short
+// length classes, the avalanche constant (PRIME64_3), the non-swapping
+// accumulate and the block/last-stripe rules of the long loop.
+__device__ __forceinline__ uint64_t xxph3_avalanche(uint64_t h) {  // :1073
+  h ^= h >> 37;
+  h *= P64_3;
+  return h ^ (h >> 32);
+}
+__device__ __forceinline__ uint64_t xxph3_mix16(const uint8_t* in, int s, uint64_t seed) {  // :1644
+  return mul128_fold64(rd64(in) ^ (sec64(s) + seed), rd64(in + 8) ^ (sec64(s + 8) - seed));
+}
+// :1102 len 4..8 on the two (possibly overlapping) 4-byte words
+__device__ __forceinline__ uint64_t xxph3_4to8(uint32_t lo, uint32_t hi, uint64_t len, uint64_t seed) {
+  const uint64_t keyed = ((uint64_t)lo | ((uint64_t)hi << 32)) ^ (sec64(0) + seed);
+  const uint64_t mix = len + ((keyed ^ (keyed >> 51)) * P32_1);
+  return xxph3_avalanche((mix ^ (mix >> 47)) * P64_2);
+}
+// :1086 len 1..3
+__device__ __forceinline__ uint64_t xxph3_1to3(uint32_t c1, uint32_t c2, uint32_t c3, uint64_t len,
+                                               uint64_t seed) {
+  const uint32_t comb = c1 | (c2 << 8) | (c3 << 16) | ((uint32_t)len << 24);
+  return xxph3_avalanche(((uint64_t)comb ^ ((uint64_t)sec32(0) + seed)) * P64_1);
+}
+// Hash64 of a register value: 1-byte op type, 4-byte CF id, 8-byte seqno
+// (db/kv_checksum.h hashes them through their in-memory LE bytes)
+__device__ __forceinline__ uint64_t xxph3_u8(uint32_t b, uint64_t seed) { return xxph3_1to3(b, b, b, 1, seed); }
+__device__ __forceinline__ uint64_t xxph3_u32(uint32_t x, uint64_t seed) { return xxph3_4to8(x, x, 4, seed); }
+__device__ __forceinline__ uint64_t xxph3_u64(uint64_t x, uint64_t seed) {
+  return xxph3_4to8((uint32_t)x, (uint32_t)(x >> 32), 8, seed);
+}
+
+// XXPH3_64bits_withSeed for n <= 240 (:1086-1147 incl. the RocksDB len-0
+// rule, :1655, :1685), one lane.
+__device__ __noinline__ uint64_t xxph3_short(const uint8_t* in, uint64_t len, uint64_t seed) {
+  if (len <= 16) {
+    if (len > 8) {
+      const uint64_t lo = rd64(in) ^ (sec64(0) + seed), hi = rd64(in + len - 8) ^ (sec64(8) - seed);
+      return xxph3_avalanche(len + (lo + hi) + mul128_fold64(lo, hi));
+    }
+    if (len >= 4) return xxph3_4to8(rd32(in), rd32(in + len - 4), len, seed);
+    if (len) return xxph3_1to3(in[0], in[len >> 1], in[len - 1], len, seed);
+    return mul128_fold64(seed + sec64(0), P64_2);
+  }
+  uint64_t acc = len * P64_1;
+  if (len <= 128) {
+    if (len > 32) {
+      if (len > 64) {
+        if (len > 96) {
+          acc += xxph3_mix16(in + 48, 96, seed);
+          acc += xxph3_mix16(in + len - 64, 112, seed);
+        }
+        acc += xxph3_mix16(in + 32, 64, seed);
+        acc += xxph3_mix16(in + len - 48, 80, seed);
+      }
+      acc += xxph3_mix16(in + 16, 32, seed);
+      acc += xxph3_mix16(in + len - 32, 48, seed);
+    }
+    acc += xxph3_mix16(in, 0, seed);
+    acc += xxph3_mix16(in + len - 16, 16, seed);
+    return xxph3_avalanche(acc);
+  }
+  for (int i = 0; i < 8; i++) acc += xxph3_mix16(in + 16 * i, 16 * i, seed);
+  acc = xxph3_avalanche(acc);
+  const int rounds = (int)len / 16;
+  for (int i = 8; i < rounds; i++) acc += xxph3_mix16(in + 16 * i, 16 * (i - 8) + 3, seed);
+  acc += xxph3_mix16(in + len - 16, 136 - 17, seed);
+  return xxph3_avalanche(acc);
+}
+
+// XXPH3 long loop on ONE lane (:1516-1587 with the seeded secret), for the
+// rare long key; values go through the row driver.
+__device__ __noinline__ uint64_t xxph3_long_lane(const uint8_t* in, uint64_t len, uint64_t seed) {
+  uint64_t acc[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+  const uint64_t nb = len / 1024;
+  auto stripe = [&](const uint8_t* p, int soff) {
+    for (int l = 0; l < 8; l++) {
+      const uint64_t d = rd64(p + 8 * l), k = d ^ csec64(soff + 8 * l, seed);
+      acc[l] += d + mul32to64(k);
+    }
+  };
+  for (uint64_t b = 0; b < nb; b++) {
+    for (int s2 = 0; s2 < 16; s2++) stripe(in + 1024 * b + 64 * s2, 8 * s2);
+    for (int l = 0; l < 8; l++) {
+      uint64_t a = acc[l];
+      a ^= a >> 47;
+      a ^= csec64(128 + 8 * l, seed);
+      acc[l] = a * P32_1;
+    }
+  }
+  const int nst = (int)((len - 1024 * nb) / 64);
+  for (int s2 = 0; s2 < nst; s2++) stripe(in + 1024 * nb + 64 * s2, 8 * s2);
+  if (len & 63) stripe(in + len - 64, 121);
+  uint64_t r = len * P64_1;
+  for (int l = 0; l < 4; l++)
+    r += mul128_fold64(acc[2 * l] ^ csec64(11 + 16 * l, seed), acc[2 * l + 1] ^ csec64(19 + 16 * l, seed));
+  return xxph3_avalanche(r);
+}
+
+__device__ __forceinline__ uint64_t xxph3_any(const uint8_t* in, uint64_t len, uint64_t seed) {
+  return len <= 240 ? xxph3_short(in, len, seed) : xxph3_long_lane(in, len, seed);
+}
+
 // 64-bit DPP move (both halves with the same control)
 template <int CTRL>
 __device__ __forceinline__ uint64_t dpp64(uint64_t v) {
@@ -185,9 +302,10 @@ struct X3Row {
   uint64_t kl0, kl1;      // last-stripe secret (offset 121)
   uint64_t km0, km1;      // merge secret (offset 11)
   uint64_t i0, i1;        // XXH3_INIT_ACC
+  uint64_t seed;          // XXPH3 seed (0 for XXH3)
   int lane, row, j, q, st4;
 };
-__device__ __forceinline__ X3Row x3_row() {
+__device__ __forceinline__ X3Row x3_row(uint64_t seed) {
   X3Row X;
   X.lane = threadIdx.x & 63;
   X.row = X.lane >> 4;
@@ -197,15 +315,16 @@ __device__ __forceinline__ X3Row x3_row() {
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const int st = X.st4 + 4 * k;
-    X.k0[k] = sec64(8 * st + 16 * X.q);
-    X.k1[k] = sec64(8 * st + 16 * X.q + 8);
+    X.k0[k] = csec64(8 * st + 16 * X.q, seed);
+    X.k1[k] = csec64(8 * st + 16 * X.q + 8, seed);
   }
-  X.ks0 = sec64(128 + 16 * X.q);
-  X.ks1 = sec64(136 + 16 * X.q);
-  X.kl0 = sec64(121 + 16 * X.q);
-  X.kl1 = sec64(129 + 16 * X.q);
-  X.km0 = sec64(11 + 16 * X.q);
-  X.km1 = sec64(19 + 16 * X.q);
+  X.ks0 = csec64(128 + 16 * X.q, seed);
+  X.ks1 = csec64(136 + 16 * X.q, seed);
+  X.kl0 = csec64(121 + 16 * X.q, seed);
+  X.kl1 = csec64(129 + 16 * X.q, seed);
+  X.km0 = csec64(11 + 16 * X.q, seed);
+  X.km1 = csec64(19 + 16 * X.q, seed);
+  X.seed = seed;
   // INIT_ACC = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1}
   X.i0 = X.q == 0 ? (uint64_t)P32_3 : X.q == 1 ? P64_2 : X.q == 2 ? P64_4 : P64_5;
   X.i1 = X.q == 0 ? P64_1 : X.q == 1 ? P64_3 : X.q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
@@ -215,17 +334,18 @@ __device__ __forceinline__ X3Row x3_row() {
 // One row's span in progress.
 struct X3Span {
   uint64_t ptr, len;
-  uint32_t nb;   // full segments: (len - 1) / 1024
+  uint32_t nb;   // full segments: (len - 1) / 1024 (XXPH3: len / 1024)
   uint32_t nst;  // stripes in the last, partial segment
   uint32_t g;    // segment being processed
   uint32_t i;    // span index
+  bool tail;     // last stripe at len - 64 (XXPH3: only if len % 64)
 };
 
 // Advance the row to its next long span (hashing short ones -- n <= 240 --
 // on the row's first lane on the way).  Op: base(), off(i), hlen(i),
 // finish(i, h) (called by lane j == 0 of the row).  Returns false when the
 // row has no spans left.
-template <class Op>
+template <class Op, bool PREVIEW>
 __device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t count, uint32_t stride,
                                              const X3Row& X, X3Span& rs) {
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
@@ -235,26 +355,33 @@ __device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t 
     if (len > 240) {
       rs.ptr = ptr;
       rs.len = len;
-      rs.nb = (uint32_t)((len - 1) / 1024);
-      rs.nst = (uint32_t)(((len - 1) - 1024ull * rs.nb) / 64);
+      // XXH3 util/xxhash.h:5141-5171; XXPH3 util/xxph3.h:1516-1543
+      const uint64_t body = PREVIEW ? len : len - 1;
+      rs.nb = (uint32_t)(body / 1024);
+      rs.nst = (uint32_t)((body - 1024ull * rs.nb) / 64);
+      rs.tail = PREVIEW ? (len & 63) != 0 : true;
       rs.g = 0;
       rs.i = i;
       return true;
     }
-    if (X.j == 0) op.finish(i, xxh3_short(reinterpret_cast<const uint8_t*>(ptr), len));
+    if (X.j == 0) {
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr);
+      op.finish(i, PREVIEW ? xxph3_short(p, len, X.seed) : xxh3_short(p, len));
+    }
   }
   return false;
 }
 
-template <class Op>
-__device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count) {
-  const X3Row X = x3_row();
+// PREVIEW = XXPH3 (Hash64 with `seed`), else XXH3_64bits v0.8.1 (seed 0).
+template <class Op, bool PREVIEW = false>
+__device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, uint64_t seed = 0) {
+  const X3Row X = x3_row(seed);
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t stride = gridDim.x * wpb * 4;  // rows in the grid
   const uint32_t first = (blockIdx.x * wpb + (threadIdx.x >> 6)) * 4 + X.row;
   // idle rows keep loading from a valid address: the batch's base
-  X3Span rs{reinterpret_cast<uint64_t>(op.base()), 0, 0, 0, 0, 0};
-  bool act = x3_next_long(op, first, count, stride, X, rs);
+  X3Span rs{reinterpret_cast<uint64_t>(op.base()), 0, 0, 0, 0, 0, false};
+  bool act = x3_next_long<Op, PREVIEW>(op, first, count, stride, X, rs);
   uint64_t a0 = X.i0, a1 = X.i1;
   while (__any(act)) {
     // loads first and unconditional (clamped when a stripe is not part of
@@ -274,8 +401,10 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count) {
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint64_t d0 = ((uint64_t)d[k].y << 32) | d[k].x, d1 = ((uint64_t)d[k].w << 32) | d[k].z;
-      c0 += ok[k] ? d1 + mul32to64(d0 ^ X.k0[k]) : 0;
-      c1 += ok[k] ? d0 + mul32to64(d1 ^ X.k1[k]) : 0;
+      // v0.8.1 adds the data word to the neighbouring accumulator
+      // (acc[l ^ 1]); the preview adds it to its own (acc_64bits)
+      c0 += ok[k] ? (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.k0[k]) : 0;
+      c1 += ok[k] ? (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.k1[k]) : 0;
     }
     a0 += row_sum_st4(c0);
     a1 += row_sum_st4(c1);
@@ -285,15 +414,104 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count) {
       rs.g++;
     } else if (act) {  // last, partial segment done: last stripe, merge, next span
       const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
-      a0 += l1 + mul32to64(l0 ^ X.kl0);
-      a1 += l0 + mul32to64(l1 ^ X.kl1);
+      if (rs.tail) {
+        a0 += (PREVIEW ? l0 : l1) + mul32to64(l0 ^ X.kl0);
+        a1 += (PREVIEW ? l1 : l0) + mul32to64(l1 ^ X.kl1);
+      }
       const uint64_t m = quad_sum(mul128_fold64(a0 ^ X.km0, a1 ^ X.km1));
-      const uint64_t h = xxh3_avalanche(rs.len * P64_1 + m);
+      const uint64_t h = PREVIEW ? xxph3_avalanche(rs.len * P64_1 + m) : xxh3_avalanche(rs.len * P64_1 + m);
       if (X.j == 0) op.finish(rs.i, h);
-      act = x3_next_long(op, rs.i + stride, count, stride, X, rs);
+      act = x3_next_long<Op, PREVIEW>(op, rs.i + stride, count, stride, X, rs);
       a0 = X.i0;
       a1 = X.i1;
     }
+  }
+}
+
+// ---- XXH3 / XXPH3, one WAVE per span ---------------------------------------
+// For batches of KiB-sized blocks (SST): spans are dealt to waves like the
+// CRC engine, so a long span is not serialised on one 16-lane row and a
+// ragged batch balances over 4x fewer, 4x faster workers.
+// Round k: row r folds segment g = 4k + r (4 x 16-byte loads per lane: the
+// wave reads 4 KiB contiguous).  A segment's stripe sums C_g do not depend
+// on the accumulators -- only the scramble between segments is sequential --
+// so after the in-row reduction every lane gathers the four rows' C_g for its
+// accumulator pair q (ds_bpermute) and runs acc = scramble(acc + C_g) over
+// the round's segments; segment nb is the partial one (no scramble), then
+// the last stripe and the merge.
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src_lane) {
+  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)v);
+  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)(v >> 32));
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+template <class Op, bool PREVIEW>
+__device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, uint64_t seed) {
+  const X3Row X = x3_row(seed);
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+  const uint32_t nwaves = gridDim.x * wpb;
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  for (uint32_t i = wave; i < count; i += nwaves) {
+    const uint64_t len = op.hlen(i);
+    const uint64_t ptr = base + op.off(i);
+    if (len <= 240) {
+      if (X.lane == 0) {
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr);
+        op.finish(i, PREVIEW ? xxph3_short(p, len, X.seed) : xxh3_short(p, len));
+      }
+      continue;
+    }
+    // XXH3 util/xxhash.h:5141-5171; XXPH3 util/xxph3.h:1516-1543
+    const uint64_t body = PREVIEW ? len : len - 1;
+    const uint32_t nb = (uint32_t)(body / 1024);
+    const uint32_t nst = (uint32_t)((body - 1024ull * nb) / 64);
+    const bool tail = PREVIEW ? (len & 63) != 0 : true;
+    const uint32_t rounds = nb / 4 + 1;
+    uint64_t a0 = X.i0, a1 = X.i1;
+    for (uint32_t k = 0; k < rounds; k++) {
+      const uint32_t g = 4 * k + X.row;
+      const uint64_t seg = ptr + 1024ull * g;
+      const bool full = g < nb;
+      uint4 d[4];
+      bool ok[4];
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const uint32_t st = (uint32_t)(X.st4 + 4 * m);
+        ok[m] = full || (g == nb && st < nst);
+        d[m] = gload16u(ok[m] ? seg + 64 * st + 16 * X.q : ptr);
+      }
+      uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const uint64_t d0 = ((uint64_t)d[m].y << 32) | d[m].x, d1 = ((uint64_t)d[m].w << 32) | d[m].z;
+        c0 += ok[m] ? (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.k0[m]) : 0;
+        c1 += ok[m] ? (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.k1[m]) : 0;
+      }
+      c0 = row_sum_st4(c0);
+      c1 = row_sum_st4(c1);
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const uint32_t gr = 4 * k + r;
+        if (gr > nb) break;  // wave-uniform
+        const uint64_t C0 = shfl64(c0, 16 * r + X.q), C1 = shfl64(c1, 16 * r + X.q);
+        a0 += C0;
+        a1 += C1;
+        if (gr < nb) {
+          a0 = xxh3_scramble(a0, X.ks0);
+          a1 = xxh3_scramble(a1, X.ks1);
+        }
+      }
+    }
+    const uint4 dl = gload16u(ptr + len - 64 + 16 * X.q);
+    const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
+    if (tail) {
+      a0 += (PREVIEW ? l0 : l1) + mul32to64(l0 ^ X.kl0);
+      a1 += (PREVIEW ? l1 : l0) + mul32to64(l1 ^ X.kl1);
+    }
+    const uint64_t m = quad_sum(mul128_fold64(a0 ^ X.km0, a1 ^ X.km1));
+    const uint64_t h = PREVIEW ? xxph3_avalanche(len * P64_1 + m) : xxh3_avalanche(len * P64_1 + m);
+    if (X.lane == 0) op.finish(i, h);
   }
 }
 

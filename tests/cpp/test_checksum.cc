@@ -224,6 +224,74 @@ TEST(Log, PhysicalRecordCrc) {
   }
 }
 
+// util/hash_test.cc:162-228 (a sample of Hash64SmallValueSchema)
+TEST(HashTest, Hash64SmallValueSchema) {
+  EXPECT_EQ(Hash64("", 0, 0), uint64_t{5999572062939766020u});
+  EXPECT_EQ(Hash64("\x08", 1, 0), uint64_t{583283813901344696u});
+  EXPECT_EQ(Hash64("\x4d\x76", 2, 0), uint64_t{6859542833406258115u});
+  EXPECT_EQ(Hash64("\x67\x53\x81\x1c", 4, 0), uint64_t{9010661983527562386u});
+  EXPECT_EQ(Hash64("\x31\x1b\x98\x75\x96\x22\xd3\x9a", 8, 0), uint64_t{9844314944338447628u});
+  EXPECT_EQ(Hash64("\xbd\x2c\x63\x38\xbf\xe9\x78\xb7\xbf\x15", 10, 0), uint64_t{10551812464348219044u});
+}
+
+// db/kv_checksum.h: the scalar template chain == the batched kernel, and
+// Protect/Strip round trips to 0 (GetStatus OK)
+TEST(KvChecksum, ScalarChainEqualsBatch) {
+  std::mt19937_64 rnd(11);
+  const int n = 64;
+  std::vector<std::string> keys(n), vals(n);
+  std::vector<uint8_t> ops(n);
+  std::vector<uint64_t> seqs(n);
+  std::string kimg, vimg;
+  std::vector<uint64_t> koff(n), voff(n);
+  std::vector<uint32_t> klen(n), vlen(n);
+  for (int i = 0; i < n; i++) {
+    keys[i].resize(i % 5 == 0 ? 300 : 8 + rnd() % 40);
+    vals[i].resize(i % 7 == 0 ? 0 : rnd() % 3000);
+    for (auto& c : keys[i]) c = static_cast<char>(rnd());
+    for (auto& c : vals[i]) c = static_cast<char>(rnd());
+    ops[i] = static_cast<uint8_t>(rnd());
+    seqs[i] = rnd();
+    koff[i] = kimg.size();
+    klen[i] = static_cast<uint32_t>(keys[i].size());
+    kimg += keys[i];
+    voff[i] = vimg.size();
+    vlen[i] = static_cast<uint32_t>(vals[i].size());
+    vimg += vals[i];
+  }
+  void *dk, *dv, *dko, *dvo, *dkl, *dvl, *dops, *dseq, *dout;
+  if (hipMalloc(&dk, kimg.size() + 64) || hipMalloc(&dv, vimg.size() + 64) || hipMalloc(&dko, 8 * n) ||
+      hipMalloc(&dvo, 8 * n) || hipMalloc(&dkl, 4 * n) || hipMalloc(&dvl, 4 * n) || hipMalloc(&dops, n) ||
+      hipMalloc(&dseq, 8 * n) || hipMalloc(&dout, 8 * n)) {
+    g_fail++;
+    return;
+  }
+  (void)hipMemcpy(dk, kimg.data(), kimg.size(), hipMemcpyHostToDevice);
+  (void)hipMemcpy(dv, vimg.data(), vimg.size(), hipMemcpyHostToDevice);
+  (void)hipMemcpy(dko, koff.data(), 8 * n, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dvo, voff.data(), 8 * n, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dkl, klen.data(), 4 * n, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dvl, vlen.data(), 4 * n, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dops, ops.data(), n, hipMemcpyHostToDevice);
+  (void)hipMemcpy(dseq, seqs.data(), 8 * n, hipMemcpyHostToDevice);
+  const mck_spans ks{dk, static_cast<uint64_t*>(dko), static_cast<uint32_t*>(dkl), 0, 0, (uint32_t)n};
+  const mck_spans vs{dv, static_cast<uint64_t*>(dvo), static_cast<uint32_t*>(dvl), 0, 0, (uint32_t)n};
+  EXPECT_EQ(mck_kv_protect_batch(MCK_KV_PROTECT_KVOS, &ks, &vs, static_cast<uint8_t*>(dops),
+                                 static_cast<uint64_t*>(dseq), static_cast<uint64_t*>(dout), nullptr),
+            0);
+  std::vector<uint64_t> out(n);
+  (void)hipMemcpy(out.data(), dout, 8 * n, hipMemcpyDeviceToHost);
+  for (void* p : {dk, dv, dko, dvo, dkl, dvl, dops, dseq, dout}) (void)hipFree(p);
+  for (int i = 0; i < n; i++) {
+    const ProtectionInfo64 kvos = ProtectionInfo64().ProtectKVO(keys[i], vals[i], ops[i]).ProtectS(seqs[i]);
+    EXPECT_EQ(kvos.GetVal(), out[i]);
+    EXPECT_TRUE(kvos.StripS(seqs[i]).StripKVO(keys[i], vals[i], ops[i]).GetStatus().ok());
+    char enc[8];
+    kvos.Encode(4, enc);
+    EXPECT_TRUE(kvos.Verify(4, enc));
+  }
+}
+
 int main() {
   if (mck_device_count() < 1) {
     fprintf(stderr, "no gfx950 device\n");
@@ -239,6 +307,8 @@ int main() {
   RUN(BuiltinChecksumTest, ChecksumSchemas);
   RUN(BlockChecksum, VerifyScalarAndBatched);
   RUN(Log, PhysicalRecordCrc);
+  RUN(HashTest, Hash64SmallValueSchema);
+  RUN(KvChecksum, ScalarChainEqualsBatch);
   printf("%d checks, %d failures\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }
