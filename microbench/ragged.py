@@ -23,6 +23,9 @@ DISTS = {
     "u65536_gap5": ([65536], [1.0], 0, 5),
     "mixed_nojit_a16": ([4096, 16384, 65536], [.6, .3, .1], 0, 16),
     "mixed_sst": ([4096, 16384, 65536], [.6, .3, .1], 256, 5),
+    # same multiset, but span i's size depends only on i // 4096, so the
+    # static round-robin over 4096 waves gives every wave identical work
+    "mixed_wavebal_a16": ("wavebal", None, 0, 16),
 }
 
 
@@ -38,8 +41,12 @@ def main():
     for name, (sizes, p, jit, gap) in DISTS.items():
         rng = np.random.default_rng(1)
         lens, offs, pos = [], [], 0
+        pattern = rng.permutation([4096] * 6 + [16384] * 3 + [65536])
         while pos < total:
-            n = int(rng.choice(sizes, p=p) + (rng.integers(0, jit) if jit else 0))
+            if sizes == "wavebal":
+                n = int(pattern[(len(lens) // 4096) % len(pattern)])
+            else:
+                n = int(rng.choice(sizes, p=p) + (rng.integers(0, jit) if jit else 0))
             if gap == 16:
                 pos = (pos + 15) & ~15
             offs.append(pos)
@@ -62,7 +69,7 @@ def main():
             e1.record(st)
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / args.iters
-            res.append(f"{kind} {nbytes / ms / 1e9:7.0f} GB/s ({ms * 1e3:6.1f} us)")
+            res.append(f"{kind} {nbytes / (ms * 1e-3) / 1e12:5.2f} TB/s ({ms * 1e3:6.1f} us)")
         print(f"{name:18s} n={len(lens):7d}  " + "  ".join(res), flush=True)
 
 

@@ -42,6 +42,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include "mck_common.hpp"
 #include "mck_tables.hpp"
 
 namespace mck {
@@ -187,7 +188,18 @@ struct CrcSpan {
   uint32_t inj;    // init state, un-shifted by hb bytes
   uint32_t init_crc;
   bool empty;      // n == 0: Extend(init, "") = init
+  // Head mini-round (mini = 1): the first <= 1 KiB of the span, when that is
+  // all a first 4 KiB round would hold, is hashed with 16-byte chunks per
+  // lane instead (a quarter of the step work) and reduced to one state that
+  // the first full round injects at lane 0.  The mini round is round
+  // rounds-1; full rounds are rounds-1-mini .. 0.
+  int32_t mini;
+  int32_t owner_m;  // lane whose 16-byte mini chunk holds ptr
+  uint32_t hb_m;    // ptr - that chunk's start (< 16)
+  uint32_t inj_m;   // init state, un-shifted by hb_m bytes
 };
+
+constexpr uint32_t kMiniBytes = 1024;  // 64 lanes x 16 bytes
 
 __device__ __forceinline__ CrcSpan crc_span(const uint8_t* p, uint64_t n, uint32_t init_crc) {
   CrcSpan s;
@@ -196,13 +208,32 @@ __device__ __forceinline__ CrcSpan crc_span(const uint8_t* p, uint64_t n, uint32
   s.a0 = s.ptr & ~15ull;
   s.a1 = (s.end + 15) & ~15ull;
   s.empty = n == 0;
+  s.kt = (uint32_t)(s.a1 - s.end);
+  s.init_crc = init_crc;
   const uint64_t cover = s.a1 - s.ptr;  // > 0 unless empty
+  const uint32_t head = (uint32_t)(cover % kRoundBytes);
+  s.mini = !s.empty && head != 0 && head <= kMiniBytes;
+  if (s.mini) {
+    const int32_t full = (int32_t)(cover / kRoundBytes);
+    s.rounds = full + 1;
+    const uint32_t lead = kMiniBytes - head;  // mini base .. ptr
+    s.owner_m = (int32_t)(lead >> 4);
+    s.hb_m = lead & 15u;
+    s.inj_m = ~init_crc;
+    if (s.hb_m) s.inj_m = crc_unshift(s.hb_m, s.inj_m);  // wave-uniform branch
+    // the first full round starts exactly at the mini round's end
+    s.owner = 0;
+    s.hb = 0;
+    s.inj = 0;
+    return s;
+  }
+  s.owner_m = 64;
+  s.hb_m = 0;
+  s.inj_m = 0;
   s.rounds = s.empty ? 1 : (int32_t)((cover + kRoundBytes - 1) / kRoundBytes);
   const uint32_t lead = (uint32_t)((uint64_t)kRoundBytes * s.rounds - cover);  // base0 .. ptr
   s.owner = s.empty ? 64 : (int32_t)(lead >> 6);
   s.hb = lead & 63u;
-  s.kt = (uint32_t)(s.a1 - s.end);
-  s.init_crc = init_crc;
   s.inj = ~init_crc;
   if (s.hb) s.inj = crc_unshift(s.hb, s.inj);  // wave-uniform branch
   return s;
@@ -221,7 +252,14 @@ __device__ __forceinline__ Chunk crc_load_chunk(const CrcSpan& sp, int r, const 
   uint64_t pa[4];
 #pragma unroll
   for (int j = 0; j < 4; j++) pa[j] = cb + 16 * j;
-  if (r == sp.rounds - 1 && (sp.owner > 0 || sp.hb >= 16 || sp.empty)) {
+  if (sp.mini && r == sp.rounds - 1) {
+    // mini round: lane l's 16 bytes at a1 - 4 KiB * (rounds-1) - 1 KiB + 16 l
+    // (all four loads read it: the load count stays fixed for vmcnt)
+    uint64_t a = sp.a1 - (uint64_t)kRoundBytes * (sp.rounds - 1) - kMiniBytes + 16ull * L.lane;
+    a = a < sp.a0 ? sp.a0 : a;
+#pragma unroll
+    for (int j = 0; j < 4; j++) pa[j] = a;
+  } else if (r == sp.rounds - 1 && (sp.owner > 0 || sp.hb >= 16 || sp.empty)) {
 #pragma unroll
     for (int j = 0; j < 4; j++) pa[j] = pa[j] < sp.a0 ? sp.a0 : pa[j];
   }
@@ -259,10 +297,48 @@ __device__ __forceinline__ void crc_keep_head_bytes(uint4& v, uint32_t keep) {
 // so each lane keeps that many independent LDS lookup chains in flight (the
 // per-lane work is latency-bound on the chain), joined at the end of the
 // round by zshift(part state, bytes after the part) and XOR.
+// zshift(s, 16 * (63 - lane)): 64-byte part by the final-shift tables of
+// lane 63 - (63 - lane) / 4, the remaining 0..48 bytes by the 16/32-byte maps.
+__device__ __forceinline__ uint32_t crc_lane_final16(uint32_t s, const CrcLane& L) {
+  const uint32_t d = 63u - (uint32_t)L.lane;
+  const uint32_t l4 = (63u - (d >> 2)) << 2;
+  uint32_t x[8];
+#pragma unroll
+  for (int n = 0; n < 8; n++) x[n] = lds_u32(kLdsFinal + n * 4096 + ((((s >> (4 * n)) & 15u) << 8) | l4));
+  s = (x[0] ^ x[1]) ^ (x[2] ^ x[3]) ^ ((x[4] ^ x[5]) ^ (x[6] ^ x[7]));
+  const uint32_t q = crc_nibmap(kLdsQuarter, s);
+  s = (d & 1u) ? q : s;
+  const uint32_t h = crc_nibmap(kLdsHalf, s);
+  return (d & 2u) ? h : s;
+}
+
+// The head mini-round: every lane folds its 16-byte chunk (the first word of
+// c); returns the pure state at the mini round's end, wave-uniform.
+__device__ __forceinline__ uint32_t crc_mini_round(Chunk c, const CrcSpan& sp, const CrcLane& L) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(&c.v[0]);
+  if (sp.hb_m && L.lane == sp.owner_m) {  // zero the owner's bytes before ptr
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int z = (int)sp.hb_m - 4 * q;
+      w[q] = z <= 0 ? w[q] : z >= 4 ? 0u : w[q] & (0xFFFFFFFFu << (8 * z));
+    }
+  }
+  if (sp.rounds == 1 && sp.kt && L.lane == 63) crc_keep_head_bytes(c.v[0], 16 - sp.kt);  // span ends here
+  uint32_t x = L.lane == sp.owner_m ? sp.inj_m : 0u;
+#pragma unroll
+  for (int q = 0; q < 4; q++) x = crc_step4(x ^ w[q], L);
+  x = L.lane < sp.owner_m ? 0u : x;
+  if (sp.owner_m == 63) return readlane_u32(x, 63);  // one chunk: already at the end
+  return wave_xor32(crc_lane_final16(x, L));
+}
+
 __device__ __forceinline__ uint32_t crc_round(uint32_t s, Chunk c, const CrcSpan& sp, int r, const CrcLane& L) {
-  const bool first = r == sp.rounds - 1;  // wave-uniform
+  if (sp.mini && r == sp.rounds - 1) return crc_mini_round(c, sp, L);  // wave-uniform
+  const bool first = r == sp.rounds - 1 - sp.mini;                       // wave-uniform
   uint32_t x[kCrcChains];
-  if (first) {
+  if (first && sp.mini) {
+    x[0] = L.lane == 0 ? s : 0u;  // the mini round's state, at lane 0's chunk start
+  } else if (first) {
     x[0] = L.lane == sp.owner ? sp.inj : 0u;
     if (sp.hb && L.lane == sp.owner) crc_zero_head(c, sp.hb);  // one lane, unaligned starts
   } else {
@@ -289,14 +365,15 @@ __device__ __forceinline__ uint32_t crc_round(uint32_t s, Chunk c, const CrcSpan
     const uint32_t t1 = crc_nibmap(kLdsQuarter, x[2]) ^ x[3];
     s = crc_nibmap(kLdsHalf, t0) ^ t1;
   }
-  if (first) s = L.lane < sp.owner ? 0u : s;  // chunks wholly before the span
+  if (first && !sp.mini) s = L.lane < sp.owner ? 0u : s;  // chunks wholly before the span
   return s;
 }
 
 // Combine the lanes' states into the span's CRC (Extend semantics).  Every
 // lane returns the same value.
 __device__ __forceinline__ uint32_t crc_finish(uint32_t s, const CrcSpan& sp, const CrcLane& L) {
-  uint32_t p = wave_xor32(crc_lane_final(s, L));
+  // a span that was only a mini round is already reduced
+  uint32_t p = (sp.mini && sp.rounds == 1) ? s : wave_xor32(crc_lane_final(s, L));
   if (sp.kt) p = crc_unshift(sp.kt, p);
   return sp.empty ? sp.init_crc : ~p;
 }
@@ -308,23 +385,7 @@ __device__ __forceinline__ uint32_t crc_extend_byte(uint32_t crc, uint8_t b) {
 
 __device__ __forceinline__ uint32_t crc_mask(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
 
-// v_readlane returns int: widen through uint32_t, never sign-extend.
-__device__ __forceinline__ uint32_t readlane_u32(uint32_t v, uint32_t k) {
-  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));
-}
-__device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t k) {
-  return ((uint64_t)readlane_u32((uint32_t)(v >> 32), k) << 32) | (uint64_t)readlane_u32((uint32_t)v, k);
-}
 
-// Persistent, software-pipelined driver: each wave walks (span, round) pairs
-// of spans wave_id, wave_id + nwaves, ...; the next pair's chunk is loaded
-// before the current one is hashed.  Span descriptors are fetched 64 spans at
-// a time (lane l loads the descriptor of the wave's l-th next span) and read
-// back with v_readlane, so a descriptor costs no memory latency per span.
-// Op supplies the spans and consumes the results:
-//   const uint8_t* Op::base(), uint64_t Op::off(i), uint64_t Op::len(i),
-//   uint32_t Op::init_crc(i)                    (per lane, i < count)
-//   void Op::finish(i, crc)   (all lanes call it; lane 0 writes)
 struct SpanDesc {
   uint64_t off;
   uint64_t len;
@@ -332,11 +393,11 @@ struct SpanDesc {
 };
 
 template <class Op>
-__device__ __forceinline__ SpanDesc crc_desc_fetch(const Op& op, uint32_t first, uint32_t nwaves, uint32_t count,
+__device__ __forceinline__ SpanDesc crc_desc_fetch(const Op& op, uint32_t first, uint32_t stride, uint32_t end,
                                                    const CrcLane& L) {
   SpanDesc d{0, 0, 0};
-  const uint64_t i = (uint64_t)first + (uint64_t)L.lane * nwaves;
-  if (i < count) {
+  const uint64_t i = (uint64_t)first + (uint64_t)L.lane * stride;
+  if (i < end) {
     d.off = op.off((uint32_t)i);
     d.len = op.len((uint32_t)i);
     d.init = op.init_crc((uint32_t)i);
@@ -351,40 +412,103 @@ __device__ __forceinline__ SpanDesc crc_desc_pick(const SpanDesc& d, uint32_t k)
   return r;
 }
 
+// ---- span feeds: which span a wave hashes next ----------------------------
+// Static: spans wave_id, wave_id + nwaves, ... over the whole grid; span
+// descriptors are fetched 64 at a time (lane l loads the wave's l-th next
+// descriptor) and read back with v_readlane.
 template <class Op>
-__device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, uint8_t* lds,
-                                                 const CrcTables* __restrict__ g) {
-  crc_fill_lds(lds, g);
-  __syncthreads();
-  const CrcLane L = crc_lane();
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-  const uint32_t nwaves = gridDim.x * wpb;
-  if (wave >= count) return;
+struct FeedStatic {
+  uint32_t i, k, nwaves, count;
+  SpanDesc db;
+  __device__ bool first(const Op& op, const CrcLane& L, uint32_t* span, SpanDesc* d) {
+    const uint32_t wpb = blockDim.x >> 6;
+    i = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+    nwaves = gridDim.x * wpb;
+    if (i >= count) return false;
+    k = 0;
+    db = crc_desc_fetch(op, i, nwaves, count, L);
+    *d = crc_desc_pick(db, 0);
+    *span = i;
+    return true;
+  }
+  __device__ bool next(const Op& op, const CrcLane& L, uint32_t* span, SpanDesc* d) {
+    const uint32_t ni = i + nwaves;
+    if (ni >= count) return false;
+    if (++k == 64) {
+      db = crc_desc_fetch(op, ni, nwaves, count, L);
+      k = 0;
+    }
+    *d = crc_desc_pick(db, k);
+    *span = i = ni;
+    return true;
+  }
+};
+
+// Dynamic: workgroup b owns spans b, b + G, b + 2G, ... (interleaved, so
+// runs of similar spans spread over all CUs); their descriptors are staged
+// in LDS once, and each wave takes the next one with an LDS ticket when it
+// frees up -- ragged batches stay balanced inside the CU.  Used when a
+// workgroup's share fits the LDS descriptor cache.
+constexpr uint32_t kDescCache = 1536;
+constexpr uint32_t kLdsDescOff = kLdsLowEnd;                     // u64 [1536]
+constexpr uint32_t kLdsDescLen = kLdsDescOff + 8 * kDescCache;   // u32 [1536]
+constexpr uint32_t kLdsDescInit = kLdsDescLen + 4 * kDescCache;  // u32 [1536]
+constexpr uint32_t kLdsTicket = kLdsDescInit + 4 * kDescCache;   // u32
+static_assert(kLdsTicket + 4 <= kLdsStep, "descriptor cache must fit below the step tables");
+
+typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
+typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
+__device__ __forceinline__ lds_u32_t* lds_p32(uint32_t off) { return reinterpret_cast<lds_u32_t*>(static_cast<size_t>(off)); }
+__device__ __forceinline__ lds_u64_t* lds_p64(uint32_t off) { return reinterpret_cast<lds_u64_t*>(static_cast<size_t>(off)); }
+
+template <class Op>
+__device__ __forceinline__ void feed_lds_stage(const Op& op, uint32_t count) {
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t n = (count - b + G - 1) / G;
+  for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+    const uint32_t i = b + G * t;
+    *lds_p64(kLdsDescOff + 8 * t) = op.off(i);
+    *lds_p32(kLdsDescLen + 4 * t) = (uint32_t)op.len(i);
+    *lds_p32(kLdsDescInit + 4 * t) = op.init_crc(i);
+  }
+  if (threadIdx.x == 0) *lds_p32(kLdsTicket) = 0;
+}
+
+template <class Op>
+struct FeedLds {
+  uint32_t n;
+  __device__ bool take(uint32_t* span, SpanDesc* d) {
+    const uint32_t t = __builtin_amdgcn_readfirstlane(lds_ticket(lds_p32(kLdsTicket)));
+    if (t >= n) return false;
+    *span = blockIdx.x + gridDim.x * t;
+    d->off = *lds_p64(kLdsDescOff + 8 * t);
+    d->len = *lds_p32(kLdsDescLen + 4 * t);
+    d->init = *lds_p32(kLdsDescInit + 4 * t);
+    return true;
+  }
+  __device__ bool first(const Op&, const CrcLane&, uint32_t* span, SpanDesc* d) { return take(span, d); }
+  __device__ bool next(const Op&, const CrcLane&, uint32_t* span, SpanDesc* d) { return take(span, d); }
+};
+
+template <class Op, class Feed>
+__device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& L) {
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  uint32_t i = wave;  // current span
-  uint32_t k = 0;     // its slot in the descriptor batch
-  SpanDesc db = crc_desc_fetch(op, i, nwaves, count, L);
-  SpanDesc d = crc_desc_pick(db, 0);
+  uint32_t i;
+  SpanDesc d;
+  if (!f.first(op, L, &i, &d)) return;
   CrcSpan sp = crc_span(reinterpret_cast<const uint8_t*>(base + d.off), d.len, d.init);
   int r = sp.rounds - 1;
   Chunk cur = crc_load_chunk(sp, r, L);
   uint32_t s = 0;
   for (;;) {
-    uint32_t ni = i, nk = k;
+    uint32_t ni = i;
     int nr = r - 1;
     CrcSpan nsp = sp;
     bool more = true;
     if (nr < 0) {
-      ni = i + nwaves;
-      more = ni < count;
+      SpanDesc nd;
+      more = f.next(op, L, &ni, &nd);
       if (more) {
-        nk = k + 1;
-        if (nk == 64) {
-          db = crc_desc_fetch(op, ni, nwaves, count, L);
-          nk = 0;
-        }
-        const SpanDesc nd = crc_desc_pick(db, nk);
         nsp = crc_span(reinterpret_cast<const uint8_t*>(base + nd.off), nd.len, nd.init);
         nr = nsp.rounds - 1;
       }
@@ -396,10 +520,35 @@ __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, u
     if (r == 0) op.finish(i, crc_finish(s, sp, L));
     if (!more) break;
     i = ni;
-    k = nk;
     r = nr;
     sp = nsp;
     cur = nxt;
+  }
+}
+
+// Persistent, software-pipelined driver: each wave walks (span, round) pairs
+// of the spans its feed hands it; the next pair's chunk is loaded before the
+// current one is hashed.
+// Op supplies the spans and consumes the results:
+//   const uint8_t* Op::base(), uint64_t Op::off(i), uint64_t Op::len(i),
+//   uint32_t Op::init_crc(i)                    (per lane, i < count)
+//   void Op::finish(i, crc)   (all lanes call it; lane 0 writes)
+template <class Op>
+__device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, uint8_t* lds,
+                                                 const CrcTables* __restrict__ g) {
+  crc_fill_lds(lds, g);
+  const uint32_t share = (count + gridDim.x - 1) / gridDim.x;  // largest workgroup share
+  const bool dyn = share <= kDescCache;                       // grid-uniform
+  if (dyn) feed_lds_stage(op, count);
+  __syncthreads();
+  const CrcLane L = crc_lane();
+  if (dyn) {
+    FeedLds<Op> f{(count - blockIdx.x + gridDim.x - 1) / gridDim.x};
+    crc_drive(op, f, L);
+  } else {
+    FeedStatic<Op> f;
+    f.count = count;
+    crc_drive(op, f, L);
   }
 }
 
@@ -431,6 +580,10 @@ __device__ __forceinline__ CrcSpan crc_uniform_span(uint64_t base, uint32_t i, c
   sp.inj = FULL ? 0xFFFFFFFFu : U.inj;
   sp.init_crc = 0;
   sp.empty = false;
+  sp.mini = 0;
+  sp.owner_m = 64;
+  sp.hb_m = 0;
+  sp.inj_m = 0;
   return sp;
 }
 

@@ -194,12 +194,13 @@ int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform) {
   }();
   const bool wave = force ? force == 2 : !uniform;
   if (wave) {
-    const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 3) / 4);
-    hipLaunchKernelGGL((k_xxh3<Op, true>), dim3(grid), dim3(256), 0, st, op, count);
+    // one 16-wave workgroup per CU, spans dealt by LDS tickets
+    const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + 15) / 16);
+    hipLaunchKernelGGL((k_xxh3_wave<Op>), dim3(grid), dim3(1024), 0, st, op, count);
   } else {
     // 16 rows (spans) per 256-thread workgroup
     const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 15) / 16);
-    hipLaunchKernelGGL((k_xxh3<Op, false>), dim3(grid), dim3(256), 0, st, op, count);
+    hipLaunchKernelGGL((k_xxh3<Op>), dim3(grid), dim3(256), 0, st, op, count);
   }
   MCK_HIP(hipGetLastError());
   return MCK_OK;

@@ -134,12 +134,13 @@ __global__ __launch_bounds__(1024) void k_crc_uniform(Op op, CrcUniform U, uint3
 
 // ============================ XXH3 ========================================
 // one span per 16-lane row (xxh3_rows_driver) or per wave (xxh3_wave_driver)
-template <class Op, bool WAVE = false>
+template <class Op>
 __global__ __launch_bounds__(256) void k_xxh3(Op op, uint32_t count) {
-  if (WAVE)
-    xxh3_wave_driver<Op, false>(op, count, 0);
-  else
-    xxh3_rows_driver(op, count);
+  xxh3_rows_driver(op, count);
+}
+template <class Op>
+__global__ __launch_bounds__(1024) void k_xxh3_wave(Op op, uint32_t count) {
+  xxh3_wave_driver<Op, false>(op, count, 0);
 }
 
 struct OpX3Value {

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "mck_common.hpp"
+
 namespace mck {
 
 constexpr uint64_t P64_1 = 0x9E3779B185EBCA87ull, P64_2 = 0xC2B2AE3D27D4EB4Full,
@@ -302,6 +304,7 @@ struct X3Row {
   uint64_t kl0, kl1;      // last-stripe secret (offset 121)
   uint64_t km0, km1;      // merge secret (offset 11)
   uint64_t i0, i1;        // XXH3_INIT_ACC
+  uint64_t ko0, ko1;      // wave layout, lone partial segment: stripe lane>>2, pair q
   uint64_t seed;          // XXPH3 seed (0 for XXH3)
   int lane, row, j, q, st4;
 };
@@ -324,6 +327,8 @@ __device__ __forceinline__ X3Row x3_row(uint64_t seed) {
   X.kl1 = csec64(129 + 16 * X.q, seed);
   X.km0 = csec64(11 + 16 * X.q, seed);
   X.km1 = csec64(19 + 16 * X.q, seed);
+  X.ko0 = csec64(8 * (X.lane >> 2) + 16 * X.q, seed);
+  X.ko1 = csec64(8 * (X.lane >> 2) + 16 * X.q + 8, seed);
   X.seed = seed;
   // INIT_ACC = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1}
   X.i0 = X.q == 0 ? (uint64_t)P32_3 : X.q == 1 ? P64_2 : X.q == 2 ? P64_4 : P64_5;
@@ -435,26 +440,61 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
 // Round k: row r folds segment g = 4k + r (4 x 16-byte loads per lane: the
 // wave reads 4 KiB contiguous).  A segment's stripe sums C_g do not depend
 // on the accumulators -- only the scramble between segments is sequential --
-// so after the in-row reduction every lane gathers the four rows' C_g for its
-// accumulator pair q (ds_bpermute) and runs acc = scramble(acc + C_g) over
-// the round's segments; segment nb is the partial one (no scramble), then
-// the last stripe and the merge.
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, int src_lane) {
-  const int lo = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)v);
-  const int hi = __builtin_amdgcn_ds_bpermute(src_lane << 2, (int)(uint32_t)(v >> 32));
-  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+// so after the in-row reduction row 0 gathers the four rows' C_g for its
+// accumulator pair q (v_permlane16/32_swap) and runs acc = scramble(acc +
+// C_g) over the round's segments; segment nb is the partial one (no
+// scramble).  When it would be alone in a round it is spread over all 64
+// lanes (stripe = lane / 4) instead.  Then the last stripe and the merge.
+// value of lane ^ 16 / lane ^ 32 (gfx950 v_permlane16/32_swap: with both
+// operands = v, one result is v itself and the other the partner row's value)
+__device__ __forceinline__ uint32_t xl16(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+  return r[0] ^ r[1] ^ v;
 }
+__device__ __forceinline__ uint32_t xl32(uint32_t v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  return r[0] ^ r[1] ^ v;
+}
+__device__ __forceinline__ uint64_t xl16_64(uint64_t v) {
+  return ((uint64_t)xl16((uint32_t)(v >> 32)) << 32) | xl16((uint32_t)v);
+}
+__device__ __forceinline__ uint64_t xl32_64(uint64_t v) {
+  return ((uint64_t)xl32((uint32_t)(v >> 32)) << 32) | xl32((uint32_t)v);
+}
+
+// Workgroup b (1024 threads) owns spans b, b + G, ... (interleaved over the
+// batch).  When its share fits, the descriptors are staged in LDS and each
+// wave takes the next span with an LDS ticket as it frees up (balanced
+// inside the CU); otherwise the waves walk the share round-robin.
+constexpr uint32_t kX3DescCache = 1536;
 
 template <class Op, bool PREVIEW>
 __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, uint64_t seed) {
   const X3Row X = x3_row(seed);
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-  const uint32_t nwaves = gridDim.x * wpb;
+  __shared__ uint64_t s_off[kX3DescCache];
+  __shared__ uint32_t s_len[kX3DescCache];
+  __shared__ uint32_t s_ctr;
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t n = (count - b + G - 1) / G;
+  const bool dyn = (count + G - 1) / G <= kX3DescCache;  // grid-uniform
+  if (dyn) {
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+      s_off[t] = op.off(b + G * t);
+      s_len[t] = (uint32_t)op.hlen(b + G * t);
+    }
+    if (threadIdx.x == 0) s_ctr = 0;
+  }
+  __syncthreads();
+  const uint32_t wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  for (uint32_t i = wave; i < count; i += nwaves) {
-    const uint64_t len = op.hlen(i);
-    const uint64_t ptr = base + op.off(i);
+  uint32_t t = wid;  // static walk: this wave's next position in the share
+  for (;;) {
+    if (dyn) t = __builtin_amdgcn_readfirstlane(lds_ticket(&s_ctr));
+    if (t >= n) break;
+    const uint32_t i = b + G * t;
+    const uint64_t len = dyn ? (uint64_t)s_len[t] : op.hlen(i);
+    const uint64_t ptr = base + (dyn ? s_off[t] : op.off(i));
+    if (!dyn) t += wpb;
     if (len <= 240) {
       if (X.lane == 0) {
         const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr);
@@ -467,7 +507,10 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
     const uint32_t nb = (uint32_t)(body / 1024);
     const uint32_t nst = (uint32_t)((body - 1024ull * nb) / 64);
     const bool tail = PREVIEW ? (len & 63) != 0 : true;
-    const uint32_t rounds = nb / 4 + 1;
+    // rounds of four segments; when the last round would hold only the
+    // partial segment nb, it is spread over the whole wave instead
+    const bool lone = (nb & 3) == 0;
+    const uint32_t rounds = nb / 4 + (lone ? 0 : 1);
     uint64_t a0 = X.i0, a1 = X.i1;
     for (uint32_t k = 0; k < rounds; k++) {
       const uint32_t g = 4 * k + X.row;
@@ -490,18 +533,37 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
       }
       c0 = row_sum_st4(c0);
       c1 = row_sum_st4(c1);
+      // row 0 gathers the four rows' sums in segment order: rows 0, 1
+      // (lane ^ 16), 2 (lane ^ 32), 3 (lane ^ 48); only row 0's
+      // accumulators are used
+      const uint64_t e0 = xl16_64(c0), e1 = xl16_64(c1);
+      uint64_t C0[4] = {c0, e0, xl32_64(c0), xl32_64(e0)};
+      uint64_t C1[4] = {c1, e1, xl32_64(c1), xl32_64(e1)};
 #pragma unroll
       for (int r = 0; r < 4; r++) {
         const uint32_t gr = 4 * k + r;
         if (gr > nb) break;  // wave-uniform
-        const uint64_t C0 = shfl64(c0, 16 * r + X.q), C1 = shfl64(c1, 16 * r + X.q);
-        a0 += C0;
-        a1 += C1;
+        a0 += C0[r];
+        a1 += C1[r];
         if (gr < nb) {
           a0 = xxh3_scramble(a0, X.ks0);
           a1 = xxh3_scramble(a1, X.ks1);
         }
       }
+    }
+    if (lone) {  // segment nb alone: lane = stripe * 4 + pair
+      const uint32_t st = X.lane >> 2;
+      const bool okl = st < nst;
+      const uint4 v = gload16u(okl ? ptr + 1024ull * nb + 64 * st + 16 * X.q : ptr);
+      const uint64_t d0 = ((uint64_t)v.y << 32) | v.x, d1 = ((uint64_t)v.w << 32) | v.z;
+      uint64_t c0 = okl ? (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.ko0) : 0;
+      uint64_t c1 = okl ? (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.ko1) : 0;
+      c0 = row_sum_st4(c0);
+      c1 = row_sum_st4(c1);
+      c0 += xl16_64(c0);
+      c1 += xl16_64(c1);
+      a0 += c0 + xl32_64(c0);
+      a1 += c1 + xl32_64(c1);
     }
     const uint4 dl = gload16u(ptr + len - 64 + 16 * X.q);
     const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
