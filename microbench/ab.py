@@ -29,14 +29,21 @@ def main():
     ap.add_argument("--block", type=int, default=4096)
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--kind", default="crc32c")
+    ap.add_argument("--kind", default="crc32c", help="crc32c | xxh3 | wal")
     ap.add_argument("--mixed", action="store_true",
                     help="compaction-shaped 4/16/64 KiB (+0..255) spans at odd offsets")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     g.manual_seed(1)
-    if a.mixed:
+    if a.kind == "wal":
+        # a.blocks WAL blocks of 32 KiB, one kFullType record each; record
+        # CRCs written by the first library
+        count = a.blocks
+        data = torch.randint(0, 256, (count * 32768 + 64,), dtype=torch.uint8, device=dev, generator=g)
+        pay = Spans(data.data_ptr() + 7, None, None, 32768, 32761, count)
+        span_bytes = count * 32768
+    elif a.mixed:
         import random
         rnd = random.Random(3)
         lens, offs, pos = [], [], 0
@@ -64,11 +71,29 @@ def main():
         L.mck_crc32c_batch.argtypes = [ctypes.POINTER(Spans), ctypes.c_void_p, ctypes.c_uint32,
                                        ctypes.c_void_p, ctypes.c_void_p]
         L.mck_xxh3_64_batch.argtypes = [ctypes.POINTER(Spans), ctypes.c_void_p, ctypes.c_void_p]
+        L.mck_wal_record_crc_batch.argtypes = [ctypes.POINTER(Spans), ctypes.c_void_p, ctypes.c_uint32,
+                                               ctypes.c_void_p, ctypes.c_void_p]
+        L.mck_wal_verify_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                           ctypes.c_void_p, ctypes.c_void_p]
         libs.append(L)
+    if a.kind == "wal":
+        types = torch.ones(count, dtype=torch.uint8, device=dev)
+        crc = torch.empty(count, dtype=torch.int32, device=dev)
+        assert libs[0].mck_wal_record_crc_batch(ctypes.byref(pay), types.data_ptr(), 7, crc.data_ptr(), None) == 0
+        blocks = data[:count * 32768].view(count, 32768)
+        blocks[:, 0:4] = crc.view(torch.uint8).view(count, 4)
+        blocks[:, 4] = 32761 & 0xFF
+        blocks[:, 5] = 32761 >> 8
+        blocks[:, 6] = 1
+        torch.cuda.synchronize()
     stream = torch.cuda.current_stream(dev)
     outs = []
     for L in libs:
-        if a.kind == "crc32c":
+        if a.kind == "wal":
+            out = torch.zeros((count, 4), dtype=torch.int32, device=dev)
+            f = (lambda L=L, out=out: L.mck_wal_verify_batch(data.data_ptr(), count * 32768, 7, out.data_ptr(),
+                                                             stream.cuda_stream))
+        elif a.kind == "crc32c":
             out = torch.zeros(count, dtype=torch.int32, device=dev)
             f = (lambda L=L, out=out: L.mck_crc32c_batch(ctypes.byref(sp), None, 0, out.data_ptr(),
                                                          stream.cuda_stream))

@@ -450,3 +450,31 @@ def test_kv_protect_verify(gpu, oracle, prot_bytes):
     assert int(cnt.item()) == sum(exp)
     if prot_bytes >= 4:
         assert sorted(i for i, e in enumerate(exp) if e) == sorted(bad)
+
+
+def test_large_ragged_batches_static_and_dynamic_feeds(gpu, oracle):
+    """Ragged batches above and below the per-workgroup LDS descriptor cache
+    (1536 spans per workgroup share): the static round-robin feed and the
+    LDS-ticket feed must give identical, oracle-exact results."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(77)
+    for count in (60_000, 450_000):
+        lens = [rnd.choice([0, 1, 7, 64, 100, 240, 241, 700, 1023, 1500, rnd.randrange(0, 2000)])
+                for _ in range(count)]
+        offs, pos = [], 0
+        for n in lens:
+            pos += rnd.randrange(0, 8)
+            offs.append(pos)
+            pos += n
+        dev = torch.randint(0, 256, (pos + 4096,), dtype=torch.uint8, device="cuda",
+                            generator=torch.Generator(device="cuda").manual_seed(count))
+        sp = spans(torch, S, dev, offs, lens)
+        crc = u32(S.crc32c_batch(sp))
+        x3 = u64(S.xxh3_64_batch(sp))
+        host = dev.cpu().numpy().tobytes()
+        idx = rnd.sample(range(count), 2500) + list(range(50)) + list(range(count - 50, count))
+        for i in idx:
+            b = host[offs[i]:offs[i] + lens[i]]
+            assert crc[i] == oracle.Value(b), (count, i, lens[i])
+            assert x3[i] == oracle.XXH3(b), (count, i, lens[i])
