@@ -49,6 +49,17 @@ def main():
         if any(n in name for n in names):
             avg_ns += float(r["TotalDurationNs"])
             calls += int(r["Calls"])
+    # the bench's timed window = the last steps x launches dispatches of the
+    # dominant kernel(s) (the warmup launches come first)
+    timed_ns = None
+    kt = os.path.join(d, "trace", "trace_kernel_trace.csv")
+    if os.path.exists(kt):
+        with open(kt) as f:
+            durs = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(f)
+                    if any(n in r["Kernel_Name"] for n in names)]
+        k = line["steps"] * len(names)
+        if len(durs) >= k:
+            timed_ns = sum(durs[-k:]) / k
     fetch = per_launch(os.path.join(d, "pmc_fetch", "pmc_counter_collection.csv"), names, "FETCH_SIZE")
     write = per_launch(os.path.join(d, "pmc_write", "pmc_counter_collection.csv"), names, "WRITE_SIZE")
     if not fetch or not write:
@@ -62,6 +73,7 @@ def main():
         "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
         "alg_bytes_per_launch": alg, "traffic_over_alg": round((rd + wr) / alg, 4),
         "rocprof_avg_kernel_ns": round(avg_ns / max(calls, 1), 1), "rocprof_calls": calls,
+        "rocprof_timed_window_avg_kernel_ns": None if timed_ns is None else round(timed_ns, 1),
         "bench_kernel_avg_ms": line["roofline"]["kernel_avg_ms"],
         "source": os.path.relpath(d),
         "method": "FETCH_SIZE(KiB)*1024*2 (gfx950 16B/lane read correction) + WRITE_SIZE(KiB)*1024, "

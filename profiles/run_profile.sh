@@ -13,7 +13,7 @@ shift 2 || true
 out=gpurun_out/prof_${tag}_${wl}
 mkdir -p "$out"
 export TMPDIR=/tmp
-args="--workload $wl --steps 10 --warmup 2 --cpu-seconds 0 --no-verify $*"
+args="--workload $wl --cpu-seconds 0 --no-verify $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/trace" -o trace --output-format csv -- python3 bench.py $args > "$out/bench_trace.txt" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$out/pmc_fetch" -o pmc --output-format csv -- python3 bench.py $args > "$out/bench_fetch.txt" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$out/pmc_write" -o pmc --output-format csv -- python3 bench.py $args > "$out/bench_write.txt" 2>&1

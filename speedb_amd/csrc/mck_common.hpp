@@ -6,6 +6,29 @@
 
 namespace mck {
 
+typedef unsigned int span_u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const span_u32x4 span_gbl_u32x4_t;
+// 16-byte load through a global (address_space(1)) pointer: a global_load
+// (vmcnt-ordered), not a flat_load; any byte address (the hardware splits
+// misaligned accesses).
+//
+// NT = non-temporal ("nt" bit): every span byte is read exactly once.  It
+// pays only when each load INSTRUCTION reads contiguous bytes (the XXH3 row
+// layout: +3-4 % at 4 KiB, same-process A/B); the CRC layout, where one
+// instruction touches 16 B of every 64 B and the next three instructions
+// the rest of the same lines, drops from 5.66 to 3.77 TB/s with nt (the
+// lines are not kept for the sibling loads), so CRC loads use the default
+// policy.
+template <bool NT>
+__device__ __forceinline__ uint4 span_load16(uint64_t addr) {
+  span_u32x4 v;
+  if (NT)
+    v = __builtin_nontemporal_load(reinterpret_cast<span_gbl_u32x4_t*>(addr));
+  else
+    v = *reinterpret_cast<span_gbl_u32x4_t*>(addr);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 // v_readlane returns int: widen through uint32_t, never sign-extend.
 __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, uint32_t k) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));

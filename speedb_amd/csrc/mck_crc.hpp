@@ -79,31 +79,70 @@ __device__ __forceinline__ uint32_t lds_u32(uint32_t off) {
   return *reinterpret_cast<lds_word_t*>(static_cast<size_t>(off));
 }
 
-// 16-byte load through a global (address_space(1)) pointer: keeps the load a
-// global_load (vmcnt-ordered) rather than a flat_load.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const u32x4 gbl_u32x4_t;
-__device__ __forceinline__ uint4 gload16(uint64_t addr) {
-  const u32x4 v = *reinterpret_cast<gbl_u32x4_t*>(addr);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
+__device__ __forceinline__ uint4 gload16(uint64_t addr) { return span_load16<false>(addr); }
 
-// Fill the LDS image from the device-global tables.  All threads call it,
-// followed by __syncthreads().
-__device__ __forceinline__ void crc_fill_lds(uint8_t* lds, const CrcTables* __restrict__ g) {
-  uint4* l4 = reinterpret_cast<uint4*>(lds + kLdsStep);
-  for (int i = threadIdx.x; i < 4096; i += blockDim.x) {
+// Fill the LDS image from the device-global tables, in two halves so that
+// the table loads of all threads are in flight together (one memory round
+// trip instead of one per loop trip) and the caller can issue its first
+// span loads in between: crc_fill_load(), [span loads], crc_fill_store(),
+// __syncthreads().  Every CRC kernel runs kCrcBlock threads per workgroup.
+// UNSHIFT = false skips the un-shift tables (uniform FULL batches never
+// un-shift).
+constexpr int kCrcBlock = 1024;
+constexpr int kFillLow = (int)(kLdsLowEnd - kLdsFinal) / 16;  // 2176 slots
+constexpr int kFillUnshift = kMaxUnshift * 512 / 16;          // 2048 slots
+struct CrcFill {
+  uint32_t step[4096 / kCrcBlock];
+  uint4 low[(kFillLow + kCrcBlock - 1) / kCrcBlock];
+  uint4 un[kFillUnshift / kCrcBlock];
+};
+template <bool UNSHIFT>
+__device__ __forceinline__ void crc_fill_load(CrcFill& f, const CrcTables* __restrict__ g) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 4096 / kCrcBlock; k++) {
     // 16-byte slot i covers word indices 4i..4i+3 = copies c..c+3 of
     // (t = (i >> 2) & 3, v = i >> 4)
-    const uint32_t x = g->step[(i >> 2) & 3][i >> 4];
-    l4[i] = make_uint4(x, x, x, x);
+    const int i = t + kCrcBlock * k;
+    f.step[k] = g->step[(i >> 2) & 3][i >> 4];
   }
   const uint4* lo = reinterpret_cast<const uint4*>(&g->lane_final[0][0][0]);
+#pragma unroll
+  for (int k = 0; k < (kFillLow + kCrcBlock - 1) / kCrcBlock; k++) {
+    const int i = t + kCrcBlock * k;
+    f.low[k] = lo[i < kFillLow ? i : 0];
+  }
+  if (UNSHIFT) {
+    const uint4* us = reinterpret_cast<const uint4*>(&g->unshift[0][0][0]);
+#pragma unroll
+    for (int k = 0; k < kFillUnshift / kCrcBlock; k++) f.un[k] = us[t + kCrcBlock * k];
+  }
+}
+template <bool UNSHIFT>
+__device__ __forceinline__ void crc_fill_store(const CrcFill& f, uint8_t* lds) {
+  const int t = threadIdx.x;
+  uint4* l4 = reinterpret_cast<uint4*>(lds + kLdsStep);
+#pragma unroll
+  for (int k = 0; k < 4096 / kCrcBlock; k++) {
+    const uint32_t x = f.step[k];
+    l4[t + kCrcBlock * k] = make_uint4(x, x, x, x);
+  }
   uint4* dlo = reinterpret_cast<uint4*>(lds + kLdsFinal);
-  for (int i = threadIdx.x; i < (int)(kLdsLowEnd - kLdsFinal) / 16; i += blockDim.x) dlo[i] = lo[i];
-  const uint4* us = reinterpret_cast<const uint4*>(&g->unshift[0][0][0]);
-  uint4* dus = reinterpret_cast<uint4*>(lds + kLdsUnshift);
-  for (int i = threadIdx.x; i < kMaxUnshift * 512 / 16; i += blockDim.x) dus[i] = us[i];
+#pragma unroll
+  for (int k = 0; k < (kFillLow + kCrcBlock - 1) / kCrcBlock; k++) {
+    const int i = t + kCrcBlock * k;
+    if (i < kFillLow) dlo[i] = f.low[k];
+  }
+  if (UNSHIFT) {
+    uint4* dus = reinterpret_cast<uint4*>(lds + kLdsUnshift);
+#pragma unroll
+    for (int k = 0; k < kFillUnshift / kCrcBlock; k++) dus[t + kCrcBlock * k] = f.un[k];
+  }
+}
+__device__ __forceinline__ void crc_fill_lds(uint8_t* lds, const CrcTables* __restrict__ g) {
+  CrcFill f;
+  crc_fill_load<true>(f, g);
+  crc_fill_store<true>(f, lds);
 }
 
 // Per-lane constants for the v_perm address formation.  Lookup k of a step
@@ -590,18 +629,23 @@ __device__ __forceinline__ CrcSpan crc_uniform_span(uint64_t base, uint32_t i, c
 template <class Op, bool FULL>
 __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUniform& U, uint32_t count, uint8_t* lds,
                                                    const CrcTables* __restrict__ g) {
-  crc_fill_lds(lds, g);
-  __syncthreads();
+  // table loads, then this wave's first span loads, then the LDS stores:
+  // the first round's HBM latency overlaps the fill (uniform spans never
+  // un-shift, so those tables are not loaded)
+  CrcFill fill;
+  crc_fill_load<false>(fill, g);
   const CrcLane L = crc_lane();
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * wpb;
-  if (wave >= count) return;
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  uint32_t i = wave;
+  uint32_t i = wave < count ? wave : 0;
   CrcSpan sp = crc_uniform_span<FULL>(base, i, U);
   int r = sp.rounds - 1;
   Chunk cur = crc_load_chunk(sp, r, L);
+  crc_fill_store<false>(fill, lds);
+  __syncthreads();
+  if (wave >= count) return;
   uint32_t s = 0;
   for (;;) {
     uint32_t ni = i;

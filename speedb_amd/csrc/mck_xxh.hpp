@@ -288,14 +288,8 @@ __device__ __forceinline__ uint64_t xxh3_scramble(uint64_t a, uint64_t k) {
   return a * P32_1;
 }
 
-typedef unsigned int xu32x4 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const xu32x4 xgbl_u32x4_t;
-// 16-byte global load at any byte address (the hardware splits misaligned
-// accesses; full rate at 4-byte alignment)
-__device__ __forceinline__ uint4 gload16u(uint64_t addr) {
-  const xu32x4 v = *reinterpret_cast<xgbl_u32x4_t*>(addr);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
+// 16-byte global load at any byte address (full rate at 4-byte alignment)
+__device__ __forceinline__ uint4 gload16u(uint64_t addr) { return span_load16<true>(addr); }
 
 // Per-lane constants of the row layout.
 struct X3Row {
