@@ -19,6 +19,7 @@
 #pragma once
 #include <stdint.h>
 
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -244,6 +245,66 @@ class ProtectionInfo64 {
 };
 
 // ---------------------------------------------------------------------------
+// Whole-file checksums: include/rocksdb/file_checksum.h:23-90,
+// util/file_checksum_helper.h:22-72.
+constexpr char kUnknownFileChecksum[] = "";
+constexpr char kUnknownFileChecksumFuncName[] = "Unknown";
+constexpr char kStandardDbFileChecksumFuncName[] = "FileChecksumCrc32c";
+
+struct FileChecksumGenContext {
+  std::string file_name;
+  std::string requested_checksum_func_name;
+};
+
+class FileChecksumGenerator {
+ public:
+  virtual ~FileChecksumGenerator() {}
+  virtual void Update(const char* data, size_t n) = 0;
+  virtual void Finalize() = 0;
+  virtual std::string GetChecksum() const = 0;
+  virtual const char* Name() const = 0;
+};
+
+// checksum_ = crc32c::Extend over every Update, from 0; Finalize stores it as
+// 4 big-endian bytes.  Update() takes host bytes (inputs over 1 MiB go
+// through the engine's long-span path); UpdateDevice() takes bytes already
+// in device memory (mck_crc32c_long, no host copy).
+class FileChecksumGenCrc32c : public FileChecksumGenerator {
+ public:
+  explicit FileChecksumGenCrc32c(const FileChecksumGenContext& /*context*/) {}
+  ~FileChecksumGenCrc32c() override;
+  void Update(const char* data, size_t n) override { checksum_ = crc32c::Extend(checksum_, data, n); }
+  // Returns false (checksum unchanged, mck_last_error() set) on a HIP error;
+  // exceptions never escape (include/rocksdb/file_checksum.h:47-49).
+  bool UpdateDevice(const void* dev_data, uint64_t n, mck_stream_t stream = nullptr);
+  void Finalize() override {
+    char b[4];
+    for (int i = 0; i < 4; i++) b[i] = static_cast<char>(checksum_ >> (24 - 8 * i));
+    checksum_str_.assign(b, 4);
+  }
+  std::string GetChecksum() const override { return checksum_str_; }
+  const char* Name() const override { return "FileChecksumCrc32c"; }
+
+ private:
+  uint32_t checksum_ = 0;
+  std::string checksum_str_;
+  uint32_t* d_scratch_ = nullptr;  // device: long-span piece CRCs + result
+  uint64_t scratch_words_ = 0;
+};
+
+class FileChecksumGenCrc32cFactory {
+ public:
+  std::unique_ptr<FileChecksumGenerator> CreateFileChecksumGenerator(const FileChecksumGenContext& context) {
+    if (context.requested_checksum_func_name.empty() ||
+        context.requested_checksum_func_name == "FileChecksumCrc32c")
+      return std::unique_ptr<FileChecksumGenerator>(new FileChecksumGenCrc32c(context));
+    return nullptr;
+  }
+  static const char* kClassName() { return "FileChecksumGenCrc32cFactory"; }
+  const char* Name() const { return kClassName(); }
+};
+
+// ---------------------------------------------------------------------------
 // inline definitions of the batched helpers (need HIP for device buffers)
 // ---------------------------------------------------------------------------
 }  // namespace speedb_amd
@@ -314,6 +375,29 @@ inline Status VerifyBlockChecksums(const Footer& footer, const void* dev_image, 
     if (per_block) (*per_block)[i] = s;
   }
   return first;
+}
+
+inline FileChecksumGenCrc32c::~FileChecksumGenCrc32c() {
+  if (d_scratch_) (void)hipFree(d_scratch_);
+}
+
+inline bool FileChecksumGenCrc32c::UpdateDevice(const void* dev_data, uint64_t n, mck_stream_t stream) {
+  const uint64_t need = mck_crc32c_long_scratch_words(n) + 1;  // + result word
+  if (need > scratch_words_) {
+    if (d_scratch_) (void)hipFree(d_scratch_);
+    d_scratch_ = nullptr;
+    scratch_words_ = 0;
+    if (hipMalloc(&d_scratch_, need * 4) != hipSuccess) return false;
+    scratch_words_ = need;
+  }
+  if (mck_crc32c_long(dev_data, n, checksum_, d_scratch_ + 1, d_scratch_, stream) != MCK_OK) return false;
+  uint32_t v = 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemcpyAsync(&v, d_scratch_, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return false;
+  checksum_ = v;
+  return true;
 }
 
 }  // namespace speedb_amd

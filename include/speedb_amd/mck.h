@@ -199,6 +199,26 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes,
                          uint32_t log_number, mck_wal_block_result* results,
                          mck_stream_t stream);
 
+/* ---- long spans / whole files ----------------------- */
+
+/* Piece size of mck_crc32c_long (a multiple of the 4 KiB kernel round). */
+#define MCK_LONG_PIECE_BYTES 65536u
+
+/* uint32 scratch words mck_crc32c_long needs for an n-byte span. */
+uint64_t mck_crc32c_long_scratch_words(uint64_t n);
+
+/* *out = crc32c::Extend(init_crc, data, n) for ONE long device-resident span,
+ * e.g. a whole SST/blob file image: util/file_checksum_helper.h:22-60
+ * FileChecksumGenCrc32c (Extend over every Update, checksum_ starting at 0),
+ * file/writable_file_writer.cc:100-131 (buffer CRC handoff).  The span is cut
+ * into MCK_LONG_PIECE_BYTES pieces hashed in parallel by the batch kernel and
+ * joined on the device with the Crc32cCombine algebra (util/crc32c.cc
+ * :1221-1289).  data: any alignment; scratch: device array of
+ * mck_crc32c_long_scratch_words(n) uint32; out: device pointer to one uint32.
+ * Asynchronous on `stream`. */
+int mck_crc32c_long(const void* data, uint64_t n, uint32_t init_crc,
+                    uint32_t* scratch, uint32_t* out, mck_stream_t stream);
+
 /* ---- per-KV protection ----------------------------- */
 
 /* util/hash.h:45 NPHash64 == util/hash.cc:81 Hash64 == XXPH3_64bits_withSeed

@@ -635,3 +635,12 @@ uint32_t orc_wal_record_crc(uint8_t type, const void* payload, size_t n,
   crc = orc_crc32c_combine(crc, orc_crc32c_value(payload, n), n);
   return orc_crc32c_mask(crc);
 }
+
+/* util/file_checksum_helper.h:22-46 FileChecksumGenCrc32c */
+void orc_file_checksum_crc32c(const void* data, size_t n, uint8_t out[4]) {
+  const uint32_t c = orc_crc32c_extend(0, data, n);
+  out[0] = (uint8_t)(c >> 24);
+  out[1] = (uint8_t)(c >> 16);
+  out[2] = (uint8_t)(c >> 8);
+  out[3] = (uint8_t)c;
+}

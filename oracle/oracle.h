@@ -33,6 +33,11 @@ uint32_t orc_crc32c_combine(uint32_t crc1, uint32_t crc2, size_t crc2len);
  * behind util/crc32c.cc:1199 Crc32AppendZeroes) */
 uint32_t orc_crc32c_zshift(uint32_t state, uint64_t nbytes);
 
+/* util/file_checksum_helper.h:22-46 FileChecksumGenCrc32c: Update() =
+ * crc32c::Extend from checksum_ = 0, Finalize() = PutFixed32 of
+ * EndianSwapValue(checksum_), i.e. the 4 big-endian bytes of Value(file). */
+void orc_file_checksum_crc32c(const void* data, size_t n, uint8_t out[4]);
+
 /* util/xxhash.h:5329 XXH3_64bits (seed 0, default secret) */
 uint64_t orc_xxh3_64(const void* data, size_t n);
 /* util/xxhash.h XXH32 / XXH64 with a seed (kxxHash / kxxHash64) */

@@ -76,6 +76,9 @@ SIGNATURES = [
      [ctypes.POINTER(mck_spans), vp, ctypes.c_uint32, vp, vp]),
     ("mck_wal_verify_batch", ctypes.c_int,
      [vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp]),
+    ("mck_crc32c_long_scratch_words", ctypes.c_uint64, [ctypes.c_uint64]),
+    ("mck_crc32c_long", ctypes.c_int,
+     [vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp, vp]),
     ("mck_np_hash64", ctypes.c_uint64, [vp, ctypes.c_size_t, ctypes.c_uint64]),
     ("mck_np_hash64_batch", ctypes.c_int, [ctypes.POINTER(mck_spans), ctypes.c_uint64, vp, vp]),
     ("mck_kv_protect_batch", ctypes.c_int,

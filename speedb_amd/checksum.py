@@ -394,6 +394,102 @@ def kv_protect_verify_batch(kind: int, keys: Spans, values: Spans, stored, prot_
     return mismatch, count, computed
 
 
+def crc32c_long(data, nbytes: Optional[int] = None, init_crc: int = 0, offset: int = 0,
+                scratch=None, out=None, stream=None):
+    """crc32c::Extend(init_crc, data[offset : offset+nbytes]) of ONE long
+    device-resident span (a whole file image), computed as 64 KiB pieces in
+    parallel + the Crc32cCombine algebra on the device (mck_crc32c_long).
+    Returns a 1-element int32 tensor (u32 bit pattern), asynchronously."""
+    torch = _torch()
+    if nbytes is None:
+        nbytes = data.numel() - offset
+    words = int(lib.mck_crc32c_long_scratch_words(nbytes))
+    if scratch is None:
+        scratch = _empty(max(words, 1), torch.int32, data.device)
+    if scratch.numel() < words:
+        raise ValueError(f"scratch needs {words} int32 words")
+    if out is None:
+        out = _empty(1, torch.int32, data.device)
+    check(lib.mck_crc32c_long(data.data_ptr() + offset, nbytes, init_crc & 0xFFFFFFFF,
+                              scratch.data_ptr(), out.data_ptr(), _stream(stream)), "mck_crc32c_long")
+    return out
+
+
+# ---------------------------------------------------------------------------
+# whole-file checksums: include/rocksdb/file_checksum.h:50-90,
+# util/file_checksum_helper.h:22-60
+# ---------------------------------------------------------------------------
+
+kUnknownFileChecksum = ""
+kUnknownFileChecksumFuncName = "Unknown"
+kStandardDbFileChecksumFuncName = "FileChecksumCrc32c"
+
+
+@dataclass
+class FileChecksumGenContext:
+    """include/rocksdb/file_checksum.h:31-38"""
+    file_name: str = ""
+    requested_checksum_func_name: str = ""
+
+
+class FileChecksumGenCrc32c:
+    """util/file_checksum_helper.h:22-52: checksum_ = crc32c::Extend over every
+    Update (starting at 0); Finalize stores it as 4 big-endian bytes.
+
+    Update() takes host bytes (one synchronous device call; inputs over 1 MiB
+    go through the long-span path).  UpdateDevice() takes a device-resident
+    tensor region and runs mck_crc32c_long on it -- the file-writer handoff
+    when the file's bytes are already in HBM."""
+
+    def __init__(self, context: Optional[FileChecksumGenContext] = None):
+        self._checksum = 0
+        self._str: Optional[bytes] = None
+
+    def Update(self, data) -> None:
+        assert self._str is None, "Update after Finalize"
+        self._checksum = crc32c.Extend(self._checksum, data)
+
+    def UpdateDevice(self, data, nbytes: Optional[int] = None, offset: int = 0, stream=None) -> None:
+        assert self._str is None, "Update after Finalize"
+        out = crc32c_long(data, nbytes, self._checksum, offset=offset, stream=stream)
+        self._checksum = int(out.cpu().item()) & 0xFFFFFFFF
+
+    def Finalize(self) -> None:
+        assert self._str is None
+        self._str = self._checksum.to_bytes(4, "big")  # PutFixed32(EndianSwapValue)
+
+    def GetChecksum(self) -> bytes:
+        assert self._str is not None
+        return self._str
+
+    def Name(self) -> str:
+        return "FileChecksumCrc32c"
+
+
+class FileChecksumGenCrc32cFactory:
+    """util/file_checksum_helper.h:54-72"""
+
+    def CreateFileChecksumGenerator(self, context: FileChecksumGenContext):
+        if context.requested_checksum_func_name in ("", "FileChecksumCrc32c"):
+            return FileChecksumGenCrc32c(context)
+        return None
+
+    @staticmethod
+    def kClassName() -> str:
+        return "FileChecksumGenCrc32cFactory"
+
+    def Name(self) -> str:
+        return self.kClassName()
+
+
+def GetFileChecksumGenCrc32cFactory() -> FileChecksumGenCrc32cFactory:
+    """util/file_checksum_helper.cc GetFileChecksumGenCrc32cFactory()"""
+    return _DEFAULT_FACTORY
+
+
+_DEFAULT_FACTORY = FileChecksumGenCrc32cFactory()
+
+
 def device_count() -> int:
     return lib.mck_device_count()
 
@@ -405,5 +501,8 @@ __all__ = [
     "xxh3_64_batch", "xxh32_batch", "xxh64_batch", "builtin_checksum_batch",
     "sst_trailer_batch", "sst_verify_batch", "wal_record_crc_batch", "wal_verify_batch",
     "device_count", "mck_wal_block_result", "NPHash64", "Hash64", "np_hash64_batch",
-    "ProtectionKind", "kv_protect_batch", "kv_protect_verify_batch",
+    "ProtectionKind", "kv_protect_batch", "kv_protect_verify_batch", "crc32c_long",
+    "FileChecksumGenContext", "FileChecksumGenCrc32c", "FileChecksumGenCrc32cFactory",
+    "GetFileChecksumGenCrc32cFactory", "kStandardDbFileChecksumFuncName",
+    "kUnknownFileChecksum", "kUnknownFileChecksumFuncName",
 ]

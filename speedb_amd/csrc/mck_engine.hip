@@ -279,11 +279,14 @@ struct Staging {
 };
 thread_local Staging t_stage;
 
-int stage_in(const void* data, size_t n, uint8_t** d_data, void** d_out) {
+// d_buf = [64 B of results][data, n bytes][scratch, `extra` bytes]
+int stage_in(const void* data, size_t n, uint8_t** d_data, void** d_out, size_t extra = 0,
+             uint32_t** d_scratch = nullptr) {
   int dev;
   int rc = current_device(&dev, nullptr);
   if (rc) return rc;
-  const size_t need = 64 + ((n + 64 + 255) & ~size_t(255));
+  const size_t data_sz = (n + 64 + 255) & ~size_t(255);
+  const size_t need = 64 + data_sz + extra;
   if (t_stage.dev != dev || t_stage.cap < need) {
     if (t_stage.d_buf) (void)hipFree(t_stage.d_buf);
     t_stage.d_buf = nullptr;
@@ -295,6 +298,7 @@ int stage_in(const void* data, size_t n, uint8_t** d_data, void** d_out) {
   }
   *d_out = t_stage.d_buf;  // 64 bytes of results
   *d_data = static_cast<uint8_t*>(t_stage.d_buf) + 64;
+  if (d_scratch) *d_scratch = reinterpret_cast<uint32_t*>(*d_data + data_sz);
   if (n) MCK_HIP(hipMemcpy(*d_data, data, n, hipMemcpyHostToDevice));
   return MCK_OK;
 }
@@ -461,7 +465,57 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, 
   return MCK_OK;
 }
 
+// ---- long spans ------------------------------------------------------------
+uint64_t mck_crc32c_long_scratch_words(uint64_t n) {
+  return (n + MCK_LONG_PIECE_BYTES - 1) / MCK_LONG_PIECE_BYTES;
+}
+
+int mck_crc32c_long(const void* data, uint64_t n, uint32_t init_crc, uint32_t* scratch, uint32_t* out,
+                    mck_stream_t stream) {
+  t_err[0] = 0;
+  if (!out || (n && (!data || !scratch))) {
+    set_err("data / scratch / out is NULL");
+    return MCK_EINVAL;
+  }
+  const uint64_t P = MCK_LONG_PIECE_BYTES;
+  const uint64_t full = n / P, tail = n % P, npieces = full + (tail ? 1 : 0);
+  if (npieces > 0xFFFFFFFFull) {
+    set_err("span too long (%llu pieces)", (unsigned long long)npieces);
+    return MCK_EINVAL;
+  }
+  int dev, ncu;
+  if (int rc = current_device(&dev, &ncu)) return rc;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  // seed: ~zshift(~init, n); n == 0 leaves init_crc (Extend(c, "") = c)
+  MCK_HIP(hipMemsetD32Async(out, (int)~gf_zshift(~init_crc, n), 1, st));
+  if (!n) return MCK_OK;
+  if (full) {
+    const mck_spans s{data, nullptr, nullptr, P, (uint32_t)P, (uint32_t)full};
+    if (int rc = mck_crc32c_batch(&s, nullptr, 0, scratch, stream)) return rc;
+  }
+  if (tail) {
+    const mck_spans s{static_cast<const uint8_t*>(data) + full * P, nullptr, nullptr, 0, (uint32_t)tail, 1};
+    if (int rc = mck_crc32c_batch(&s, nullptr, 0, scratch + full, stream)) return rc;
+  }
+  static const CrcPowers pw = [] {
+    CrcPowers p;
+    for (int k = 0; k < 64; k++) p.x8[k] = gf_xpow8n(1ull << k);
+    return p;
+  }();
+  static const uint32_t c_full = gf_zshift(0xFFFFFFFFu, P);
+  const uint32_t c_tail = gf_zshift(0xFFFFFFFFu, tail);
+  const uint32_t grid = (uint32_t)((npieces + 255) / 256);
+  hipLaunchKernelGGL(k_crc_combine, dim3(grid), dim3(256), 0, st, scratch, (uint32_t)npieces, P, n, c_full, c_tail,
+                     pw, out);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
 // ---- scalar data shims (GPU, synchronous) ----------------------------------
+// Extend over more than this many bytes goes through the long-span path
+// (pieces hashed in parallel + device combine) instead of one span.
+constexpr size_t kShimLongBytes = 1u << 20;
+
 static uint32_t scalar_u32(int kind, uint32_t init, const void* data, size_t n, int type, int has_last,
                            char last) {
   t_err[0] = 0;
@@ -469,12 +523,21 @@ static uint32_t scalar_u32(int kind, uint32_t init, const void* data, size_t n, 
     set_err("data is NULL");
     return 0;
   }
+  uint8_t* d_data;
+  void* d_out;
+  if (kind == 0 && n > kShimLongBytes) {
+    uint32_t* d_scratch;
+    if (stage_in(data, n, &d_data, &d_out, 4 * mck_crc32c_long_scratch_words(n), &d_scratch)) return 0;
+    uint32_t v = 0;
+    if (mck_crc32c_long(d_data, n, init, d_scratch, static_cast<uint32_t*>(d_out), nullptr) == 0 &&
+        hipMemcpy(&v, d_out, 4, hipMemcpyDeviceToHost) != hipSuccess)
+      set_err("hipMemcpy failed");
+    return v;
+  }
   if (n > 0xFFFFFFFFull) {
     set_err("span too long for the scalar shim");
     return 0;
   }
-  uint8_t* d_data;
-  void* d_out;
   if (stage_in(data, n, &d_data, &d_out)) return 0;
   uint8_t* d_last = static_cast<uint8_t*>(d_out) + 32;
   if (has_last && hipMemcpy(d_last, &last, 1, hipMemcpyHostToDevice) != hipSuccess) {

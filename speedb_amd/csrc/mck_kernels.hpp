@@ -287,6 +287,50 @@ struct OpNoneBlock {
   __device__ void run(uint32_t i) const { block_epilogue<MODE>(a, i, 0u); }
 };
 
+// ===================== long spans: pieces + combine =======================
+// util/crc32c.cc:1221-1289 Crc32cCombine, applied to every piece of a long
+// span at once.  Pieces i were hashed by the batch kernels (v[i] = Value of
+// piece i); with pure(.) the init-0, no-inversion CRC,
+//   Extend(init, span) = ~( zshift(~init, n) ^ XOR_i zshift(pure_i, after_i) )
+//   pure_i = ~v[i] ^ zshift(~0, len_i)      (Value's init state, removed)
+// after_i = bytes of the span behind piece i.  The caller seeds *out with
+// ~zshift(~init, n); every wave XORs in its pieces' terms atomically (XOR
+// commutes: the result does not depend on the order).
+__device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
+  uint32_t p = 0;
+#pragma unroll 8
+  for (int j = 0; j < 32; j++) {
+    p ^= (b & (0x80000000u >> j)) ? a : 0u;
+    a = (a >> 1) ^ ((a & 1u) ? kCrc32cPoly : 0u);
+  }
+  return p;
+}
+
+struct CrcPowers {
+  uint32_t x8[64];  // x^(8 * 2^k) mod P, k < 64 (util/crc32c.cc crc32c_powers)
+};
+
+__device__ __forceinline__ uint32_t gf_zshift_dev(uint32_t s, uint64_t nbytes, const CrcPowers& pw) {
+  for (int k = 0; nbytes; k++, nbytes >>= 1)
+    if (nbytes & 1) s = gf_mul_dev(s, pw.x8[k]);
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_crc_combine(const uint32_t* __restrict__ v, uint32_t npieces,
+                                                     uint64_t piece, uint64_t n, uint32_t c_full,
+                                                     uint32_t c_tail, CrcPowers pw, uint32_t* out) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t term = 0;
+  if (i < npieces) {
+    const uint64_t start = (uint64_t)i * piece;
+    const uint64_t len = n - start < piece ? n - start : piece;
+    const uint32_t pure = ~v[i] ^ (len == piece ? c_full : c_tail);
+    term = gf_zshift_dev(pure, n - start - len, pw);
+  }
+  term = wave_xor32(term);
+  if ((threadIdx.x & 63) == 0 && term) atomicXor(out, term);
+}
+
 // ============================ WAL verify ==================================
 // db/log_reader.cc:450-584 ReadPhysicalRecord with checksum_ = true, applied
 // to every 32 KiB block independently; one wave per block.

@@ -46,6 +46,7 @@ def _bind(lib, prefix):
             "builtin_checksum_with_last_byte": (c.c_uint32, [c.c_int, c.c_char_p, c.c_size_t,
                                                              c.c_uint8]),
             "context_modifier": (c.c_uint32, [c.c_uint32, c.c_uint64]),
+            "file_checksum_crc32c": (None, [c.c_char_p, c.c_size_t, c.c_char_p]),
             "verify_block": (c.c_int, [c.c_int, c.c_char_p, c.c_size_t, c.c_uint32, c.c_uint64,
                                        ctypes.POINTER(c.c_uint32), ctypes.POINTER(c.c_uint32)]),
         })
@@ -98,6 +99,11 @@ class _Oracle:
 
     def ContextModifier(self, base, off):
         return self.lib.orc_context_modifier(base, off)
+
+    def FileChecksumCrc32c(self, b):
+        out = ctypes.create_string_buffer(4)
+        self.lib.orc_file_checksum_crc32c(b, len(b), out)
+        return out.raw
 
     def Hash64(self, b, seed=0):
         return self.lib.orc_hash64(b, len(b), seed)

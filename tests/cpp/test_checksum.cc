@@ -292,6 +292,55 @@ TEST(KvChecksum, ScalarChainEqualsBatch) {
   }
 }
 
+// util/file_checksum_helper.h:22-72: FileChecksumCrc32c = big-endian
+// crc32c::Value of the whole file, however the Updates are cut; host Update
+// (incl. the > 1 MiB long-span path), device UpdateDevice and the factory's
+// name matching.
+TEST(FileChecksum, Crc32cGenerator) {
+  FileChecksumGenCrc32cFactory factory;
+  FileChecksumGenContext ctx;
+  EXPECT_TRUE(factory.CreateFileChecksumGenerator(ctx) != nullptr);
+  ctx.requested_checksum_func_name = "FileChecksumCrc32c";
+  auto g0 = factory.CreateFileChecksumGenerator(ctx);
+  EXPECT_TRUE(g0 != nullptr);
+  ctx.requested_checksum_func_name = "SomethingElse";
+  EXPECT_TRUE(factory.CreateFileChecksumGenerator(ctx) == nullptr);
+  EXPECT_EQ(std::string(g0->Name()), std::string(kStandardDbFileChecksumFuncName));
+  g0->Update("1234", 4);
+  g0->Update("56789", 5);
+  g0->Finalize();
+  EXPECT_EQ(g0->GetChecksum(), std::string("\xe3\x06\x92\x83", 4));  // crc32c_test.cc:81 "123456789"
+
+  std::mt19937_64 rng(4546);
+  std::string file((3u << 20) + 17, '\0');
+  for (auto& c : file) c = static_cast<char>(rng());
+  FileChecksumGenCrc32c whole(ctx), pieces(ctx), dev(ctx);
+  whole.Update(file.data(), file.size());
+  size_t pos = 0, step = 1;
+  while (pos < file.size()) {
+    const size_t n = std::min(step, file.size() - pos);
+    pieces.Update(file.data() + pos, n);
+    pos += n;
+    step = step * 7 + 3;
+  }
+  void* d = nullptr;
+  EXPECT_EQ(hipMalloc(&d, file.size() + 64), hipSuccess);
+  EXPECT_EQ(hipMemcpy(d, file.data(), file.size(), hipMemcpyHostToDevice), hipSuccess);
+  // device Updates at odd offsets: 5 bytes, then (1 MiB + 3), then the rest
+  EXPECT_TRUE(dev.UpdateDevice(d, 5));
+  EXPECT_TRUE(dev.UpdateDevice(static_cast<char*>(d) + 5, (1u << 20) + 3));
+  EXPECT_TRUE(dev.UpdateDevice(static_cast<char*>(d) + (1u << 20) + 8, file.size() - (1u << 20) - 8));
+  (void)hipFree(d);
+  for (auto* g : {&whole, &pieces, &dev}) g->Finalize();
+  EXPECT_EQ(pieces.GetChecksum(), whole.GetChecksum());
+  EXPECT_EQ(dev.GetChecksum(), whole.GetChecksum());
+  const uint32_t v = crc32c::Value(file.data(), file.size());
+  const std::string& w = whole.GetChecksum();
+  EXPECT_EQ(((uint32_t)(uint8_t)w[0] << 24) | ((uint32_t)(uint8_t)w[1] << 16) | ((uint32_t)(uint8_t)w[2] << 8) |
+                (uint32_t)(uint8_t)w[3],
+            v);
+}
+
 int main() {
   if (mck_device_count() < 1) {
     fprintf(stderr, "no gfx950 device\n");
@@ -309,6 +358,7 @@ int main() {
   RUN(Log, PhysicalRecordCrc);
   RUN(HashTest, Hash64SmallValueSchema);
   RUN(KvChecksum, ScalarChainEqualsBatch);
+  RUN(FileChecksum, Crc32cGenerator);
   printf("%d checks, %d failures\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }

@@ -478,3 +478,78 @@ def test_large_ragged_batches_static_and_dynamic_feeds(gpu, oracle):
             b = host[offs[i]:offs[i] + lens[i]]
             assert crc[i] == oracle.Value(b), (count, i, lens[i])
             assert x3[i] == oracle.XXH3(b), (count, i, lens[i])
+
+
+# ---- long spans / whole-file checksum -----------------
+
+LONG_SIZES = [0, 1, 15, 16, 4095, 4096, 65535, 65536, 65537, 131072, 3 * 65536 + 5,
+              (1 << 20) + 3, (5 << 20) + 4097]
+
+
+def test_crc32c_long_vs_oracle(gpu, oracle):
+    """mck_crc32c_long == crc32c::Extend over the whole span, at piece-boundary
+    sizes, every start alignment and random init values."""
+    import speedb_amd as S
+    torch = gpu
+    host = splitmix_bytes(77, (6 << 20) + 256)
+    dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda")
+    rnd = random.Random(78)
+    for n in LONG_SIZES:
+        for off in (0, 1, 7, 16, 63):
+            init = rnd.choice([0, 0xFFFFFFFF, rnd.getrandbits(32)])
+            got = int(S.crc32c_long(dev, n, init, offset=off).cpu().numpy().view(np.uint32)[0])
+            assert got == oracle.Extend(init, host[off:off + n]), (n, off, init)
+
+
+def test_file_checksum_generator(gpu, oracle):
+    """FileChecksumGenCrc32c (util/file_checksum_helper.h:22-72): the same
+    big-endian checksum whether the file arrives as host Updates of any
+    cut, or as device-resident regions (UpdateDevice)."""
+    import speedb_amd as S
+    torch = gpu
+    data = splitmix_bytes(4546, (3 << 20) + 17)
+    want = oracle.FileChecksumCrc32c(data)
+    fac = S.GetFileChecksumGenCrc32cFactory()
+    assert fac.Name() == "FileChecksumGenCrc32cFactory"
+    assert fac.CreateFileChecksumGenerator(S.FileChecksumGenContext("f", "Other")) is None
+    g_host = fac.CreateFileChecksumGenerator(S.FileChecksumGenContext("f", ""))
+    g_dev = fac.CreateFileChecksumGenerator(S.FileChecksumGenContext("f", "FileChecksumCrc32c"))
+    pos, step = 0, 1
+    while pos < len(data):
+        g_host.Update(data[pos:pos + step])
+        pos += step
+        step = step * 5 + 1
+    dev = torch.frombuffer(bytearray(data + bytes(64)), dtype=torch.uint8).to("cuda")
+    cuts = [0, 3, 70000, (1 << 20) + 9, len(data)]
+    for a, b in zip(cuts, cuts[1:]):
+        g_dev.UpdateDevice(dev, b - a, offset=a)
+    for g in (g_host, g_dev):
+        g.Finalize()
+        assert g.GetChecksum() == want
+        assert g.Name() == S.kStandardDbFileChecksumFuncName
+    g0 = S.FileChecksumGenCrc32c()
+    g0.Update(b"123456789")  # util/crc32c_test.cc:81
+    g0.Finalize()
+    assert g0.GetChecksum() == bytes.fromhex("e3069283")
+
+
+def test_crc32c_long_full_size_combine(gpu, oracle):
+    """At full size (1 GiB + odd tail) the long-span CRC equals the host
+    Crc32cCombine fold of the uniform batch kernel's per-4 KiB CRCs -- two
+    device paths and the host algebra agree (a size-independent property)."""
+    import speedb_amd as S
+    torch = gpu
+    n_blocks, tail = 1 << 18, 12345
+    g = torch.Generator(device="cuda")
+    g.manual_seed(9)
+    dev = torch.randint(0, 256, (n_blocks * 4096 + tail + 64,), dtype=torch.uint8, device="cuda",
+                        generator=g)
+    per = S.crc32c_batch(S.Spans.uniform(dev, 4096, n_blocks)).cpu().numpy().view(np.uint32)
+    tail_crc = int(S.crc32c_batch(S.Spans(dev[n_blocks * 4096:], 1, stride=0, length=tail))
+                   .cpu().numpy().view(np.uint32)[0])
+    acc = 0
+    for v in per.tolist():
+        acc = oracle.Combine(acc, int(v), 4096)
+    acc = oracle.Combine(acc, tail_crc, tail)
+    got = int(S.crc32c_long(dev, n_blocks * 4096 + tail).cpu().numpy().view(np.uint32)[0])
+    assert got == acc

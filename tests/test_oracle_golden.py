@@ -184,3 +184,17 @@ def test_wal_writer_layout(oracle):
         exp = wal_expected_blocks(data, 123, oracle)
         assert all(s == 0 for _, s, _, _ in exp), exp
         assert sum(r for r, _, _, _ in exp) == len(w.records)
+
+
+def test_oracle_file_checksum_crc32c(oracle, ref):
+    """FileChecksumGenCrc32c restatement: big-endian Value of the whole file
+    (util/file_checksum_helper.h:22-46), pinned to the crc32c_test.cc:81
+    vector and to the reference's crc32c::Value on random files."""
+    import random
+    assert oracle.FileChecksumCrc32c(b"123456789") == bytes.fromhex("e3069283")
+    assert oracle.FileChecksumCrc32c(b"") == bytes(4)
+    rnd = random.Random(5)
+    for n in (1, 4096, 65537, 300001):
+        b = bytes(rnd.getrandbits(8) for _ in range(n))
+        want = ref.ref_crc32c_value(b, n) if ref is not None else oracle.Value(b)
+        assert oracle.FileChecksumCrc32c(b) == want.to_bytes(4, "big")
