@@ -15,6 +15,11 @@ Default workload (the headline, BASELINE.json configs[1]): CRC32C over
                        ReadPhysicalRecord CRC verify of every record
   host     configs[4]  host-resident (pinned) 4.2 KiB SST-sized blocks,
                        H2D + CRC32C + D2H double-buffered through the GPU
+  file     (8f row 2)  whole-file CRC32C (FileChecksumGenCrc32c) of one 4 GiB
+                       device-resident file image: 64 KiB pieces + device
+                       Crc32cCombine fold; at N > 1 each rank hashes its
+                       contiguous slice and the ranks' (crc, length) pairs
+                       are all-gathered and folded (8 bytes per rank)
   kv       (row a12)   per-KV protection of memtable inserts, README shape
                        (16 B key, 1000 B value): ProtectKVO(...).ProtectS(seq)
 
@@ -54,11 +59,12 @@ def parse():
     # 0.77 -> 0.90 -> 0.76 ms per launch at 1M x 4 KiB); the default warmup
     # covers that transient
     p.add_argument("--warmup", type=int, default=100)
-    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv"], default="crc32c")
+    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
     p.add_argument("--sst-bytes", type=int, default=1 << 30, help="per SST image (sst); 2 images")
     p.add_argument("--wal-blocks", type=int, default=1 << 18, help="32 KiB blocks per GPU (wal)")
+    p.add_argument("--file-bytes", type=int, default=4 << 30, help="file image bytes per GPU (file)")
     p.add_argument("--kvs", type=int, default=1 << 22, help="KVs per GPU (kv)")
     p.add_argument("--host-bytes", type=int, default=4 << 30, help="pinned source bytes (host)")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -214,6 +220,39 @@ def make_workload(args, dev, rank, world):
             step()
             r = res["r"].cpu()
             return bool((r[:, 0] == 1).all() and (r[:, 1] == 0).all())
+        w.check = check
+    elif args.workload == "file":
+        from speedb_amd import shard
+        nbytes = args.file_bytes + 4093  # an odd tail: one partial piece
+        data = W.rand_bytes(nbytes + 64, dev, 500 + rank)
+        scratch = torch.empty(int(S._lib.lib.mck_crc32c_long_scratch_words(nbytes)), dtype=torch.int32,
+                              device=dev)
+        out = torch.empty(1, dtype=torch.int32, device=dev)
+        res = {}
+
+        def step():
+            S.crc32c_long(data, nbytes, 0, scratch=scratch, out=out, stream=stream)
+            if world > 1:  # the one real exchange: (crc, length) per rank
+                res["crc"] = shard.combine_span_crcs(out, nbytes, dev)
+        w.step = step
+        w.kernel = "mck::k_crc_uniform<mck::OpCrcValue, true>"
+        w.span_bytes = nbytes
+        w.alg_bytes = (nbytes // 65536) * (65536 + 4)
+        w.desc = (f"whole-file CRC32C (FileChecksumGenCrc32c, util/file_checksum_helper.h) of a "
+                  f"{nbytes}-byte device-resident file image per GPU: 64 KiB pieces + device "
+                  "Crc32cCombine fold (SURVEY.md 8f row 2)")
+        w.cfg = {"file_bytes_per_gpu": nbytes, "piece_bytes": 65536}
+
+        def check():
+            # the long-span result == the host Crc32cCombine fold of the piece
+            # CRCs the batch kernel wrote into scratch (two paths agree)
+            pieces = scratch.cpu().numpy().view(np.uint32).tolist()
+            acc, left = 0, nbytes
+            for v in pieces:
+                ln = min(65536, left)
+                acc = S.crc32c.Crc32cCombine(acc, v, ln)
+                left -= ln
+            return acc == int(out.cpu().numpy().view(np.uint32)[0])
         w.check = check
     elif args.workload == "kv":
         count, kb, vb = args.kvs, 16, 1000

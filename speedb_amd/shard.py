@@ -83,6 +83,32 @@ def reduce_sum(value: int, device=None) -> int:
     return int(t.item())
 
 
+def combine_span_crcs(local_crc, local_len: int, device=None) -> int:
+    """One span split contiguously across ranks (rank r holds bytes
+    [off_r, off_r + len_r)): each rank has the CRC32C of its slice (rank 0's
+    may carry an init via Extend); the whole span's CRC is the
+    util/crc32c.cc:1274 Crc32cCombine fold of the (crc, length) pairs in rank
+    order -- the only data exchanged is 8 bytes per rank.
+    ``local_crc``: int or a 1-element int32 tensor on ``device``."""
+    import torch
+    if not isinstance(local_crc, int):
+        t = local_crc.reshape(1).to(torch.int64) & 0xFFFFFFFF
+    else:
+        t = torch.tensor([local_crc & 0xFFFFFFFF], dtype=torch.int64, device=device or "cpu")
+    pair = torch.cat([t, torch.tensor([int(local_len)], dtype=torch.int64, device=t.device)])
+    dist = _dist()
+    if dist is None:
+        parts = [pair]
+    else:
+        parts = [torch.empty_like(pair) for _ in range(dist.get_world_size())]
+        dist.all_gather(parts, pair)
+    acc = 0
+    for p in parts:
+        crc, ln = (int(x) for x in p.cpu().tolist())
+        acc = int(lib.mck_crc32c_combine(acc, crc, ln))
+    return acc
+
+
 def timed_steps(step, steps: int, sync=None, device=None) -> float:
     """Barrier + sync, run ``steps`` calls of ``step``, sync + barrier; the
     max over ranks of the wall time (seconds)."""
@@ -102,4 +128,5 @@ def timed_steps(step, steps: int, sync=None, device=None) -> float:
     return reduce_max(time.perf_counter() - t0, device)
 
 
-__all__ = ["partition_spans", "rank_range", "barrier", "reduce_max", "reduce_sum", "timed_steps"]
+__all__ = ["partition_spans", "rank_range", "barrier", "reduce_max", "reduce_sum", "timed_steps",
+           "combine_span_crcs"]

@@ -67,3 +67,41 @@ def test_partition_edge_cases():
     assert list(f) == list(range(8))
     with pytest.raises(Exception):
         shard.partition_spans([1, 2], 3, 2)
+
+
+def _long_worker(rank, world, port, data, out_dir):
+    import ctypes
+
+    import torch.distributed as dist
+
+    from speedb_amd import shard
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # this rank's contiguous slice of ONE span; its CRC from the CPU
+        # oracle (test infrastructure: no GPU here), rank 0 with an init
+        orc = ctypes.CDLL(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                       "oracle", "liboracle.so"))
+        orc.orc_crc32c_extend.restype = ctypes.c_uint32
+        orc.orc_crc32c_extend.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+        cuts = [len(data) * r // world for r in range(world + 1)]
+        part = data[cuts[rank]:cuts[rank + 1]]
+        init = 0x1234ABCD if rank == 0 else 0
+        crc = orc.orc_crc32c_extend(init, part, len(part))
+        whole = shard.combine_span_crcs(int(crc), len(part))
+        np.save(os.path.join(out_dir, f"l{rank}.npy"), np.array([whole], dtype=np.uint64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_long_span_split_across_ranks_gloo(tmp_path, world, oracle):
+    """one long span split across ranks; the (crc, length)
+    pairs are all-gathered (8 B per rank) and folded with Crc32cCombine --
+    every rank ends with crc32c::Extend(init, whole span)."""
+    rnd = random.Random(40 + world)
+    data = bytes(rnd.getrandbits(8) for _ in range(200003))
+    mp.spawn(_long_worker, args=(world, _free_port(), data, str(tmp_path)), nprocs=world, join=True)
+    want = oracle.Extend(0x1234ABCD, data)
+    for r in range(world):
+        assert int(np.load(tmp_path / f"l{r}.npy")[0]) == want
