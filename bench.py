@@ -174,7 +174,7 @@ def make_workload(args, dev, rank, world):
                 res[im.checksum_type] = im.verify(stream=stream)
         w.step = step
         w.launches = 2
-        w.kernel = "mck::k_crc<mck::OpCrcBlock<2> > + mck::k_xxh3<mck::OpX3Block<2> >"
+        w.kernel = "mck::k_crc<mck::OpCrcBlock<2> > + mck::k_xxh3_wave<mck::OpX3Block<2> >"
         w.span_bytes = sum(im.payload_bytes + im.count for im in imgs)  # payload + type byte
         # per launch: span bytes + 4 B stored + 8 B offset + 4 B length + 8 B
         # file offset in, 1 B flag + 4 + 4 B out

@@ -37,6 +37,11 @@ __device__ __forceinline__ uint64_t readlane_u64(uint64_t v, uint32_t k) {
   return ((uint64_t)readlane_u32((uint32_t)(v >> 32), k) << 32) | (uint64_t)readlane_u32((uint32_t)v, k);
 }
 
+__device__ __forceinline__ uint64_t readfirstlane_u64(uint64_t v) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+}
+
 // Span tickets: lane 0 takes the next ticket from a workgroup-local LDS
 // counter; the value is spread with ds_bpermute, so the compiler treats it
 // as per-lane and loads the span's descriptor with VECTOR loads (counted in

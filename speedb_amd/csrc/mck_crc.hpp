@@ -538,6 +538,8 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
   CrcSpan sp = crc_span(reinterpret_cast<const uint8_t*>(base + d.off), d.len, d.init);
   int r = sp.rounds - 1;
   Chunk cur = crc_load_chunk(sp, r, L);
+  // the epilogue inputs of the span being loaded travel with its chunks
+  typename Op::Pre pcur = op.pre(i, sp.ptr, sp.end - sp.ptr);
   uint32_t s = 0;
   for (;;) {
     uint32_t ni = i;
@@ -554,14 +556,17 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
     }
     // unconditional (see crc_load_chunk); after the last round it re-reads
     // the current chunk, which is never used
-    const Chunk nxt = crc_load_chunk(more ? nsp : sp, more ? nr : r, L);
+    const CrcSpan& lsp = more ? nsp : sp;
+    const Chunk nxt = crc_load_chunk(lsp, more ? nr : r, L);
+    const typename Op::Pre pnxt = op.pre(more ? ni : i, lsp.ptr, lsp.end - lsp.ptr);
     s = crc_round(s, cur, sp, r, L);
-    if (r == 0) op.finish(i, crc_finish(s, sp, L));
+    if (r == 0) op.finish(i, crc_finish(s, sp, L), pcur);
     if (!more) break;
     i = ni;
     r = nr;
     sp = nsp;
     cur = nxt;
+    pcur = pnxt;
   }
 }
 
@@ -571,7 +576,8 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
 // Op supplies the spans and consumes the results:
 //   const uint8_t* Op::base(), uint64_t Op::off(i), uint64_t Op::len(i),
 //   uint32_t Op::init_crc(i)                    (per lane, i < count)
-//   void Op::finish(i, crc)   (all lanes call it; lane 0 writes)
+//   Op::Pre Op::pre(i, ptr, len)   epilogue inputs, loaded with the chunks
+//   void Op::finish(i, crc, pre)   (all lanes call it; lane 0 writes)
 template <class Op>
 __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, uint8_t* lds,
                                                  const CrcTables* __restrict__ g) {

@@ -55,16 +55,49 @@ struct BlockArgs {
   uint32_t* mismatch_count;  // verify (opt)
 };
 
+// Epilogue inputs of a block op, loaded by the driver together with the
+// span's data (software-pipelined drivers issue them before folding the
+// current unit), so the epilogue never issues a dependent load that would
+// wait behind the next unit's prefetch (vmcnt retires in order):
+//   at = address of the byte after the hashed span (verify: type byte, then
+//        the stored LE32; XXH3 builtin: the last checksummed byte)
+//   two aligned dwords around it, the file offset, last[i].
+struct BlockPre {
+  uint32_t w0, w1;
+  uint32_t sh;  // (at & 3) * 8
+  uint32_t last;
+  uint64_t foff;
+  __device__ __forceinline__ uint64_t bytes() const { return (((uint64_t)w1 << 32) | w0) >> sh; }
+};
+typedef __attribute__((address_space(1))) const uint32_t gbl_u32_t;
+typedef __attribute__((address_space(1))) const uint64_t gbl_u64_t;
+typedef __attribute__((address_space(1))) const uint8_t gbl_u8_t;
+// at: device address; off = the span's offset from the batch base.  Verify
+// reads the 8 bytes at floor4(at) (type byte + stored LE32 lie inside them:
+// never past the 4-byte word holding the trailer's last byte); the other
+// modes read only the dword holding byte `at` where they need it.
+template <int MODE>
+__device__ __forceinline__ BlockPre block_pre(const BlockArgs& a, uint32_t i, uint64_t at, uint64_t off,
+                                              bool need_at) {
+  BlockPre e;
+  const uint64_t a4 = at & ~3ull;
+  e.sh = (uint32_t)(at & 3) * 8;
+  e.w0 = need_at ? *reinterpret_cast<gbl_u32_t*>(a4) : 0u;
+  e.w1 = MODE == kModeVerify ? *reinterpret_cast<gbl_u32_t*>(a4 + 4) : 0u;
+  e.last = (MODE == kModeTrailer || (MODE == kModeBuiltin && a.last)) ? *reinterpret_cast<gbl_u8_t*>(reinterpret_cast<uint64_t>(a.last + i)) : 0u;
+  e.foff = MODE == kModeBuiltin ? 0 : a.foff ? *reinterpret_cast<gbl_u64_t*>(reinterpret_cast<uint64_t>(a.foff + i)) : off;
+  return e;
+}
+
 // Verify / trailer epilogue shared by every hash kind.  `v` = builtin value.
 template <int MODE>
-__device__ __forceinline__ void block_epilogue(const BlockArgs& a, uint32_t i, uint32_t v) {
+__device__ __forceinline__ void block_epilogue(const BlockArgs& a, uint32_t i, uint32_t v, const BlockPre& e) {
   if (MODE == kModeBuiltin) {
     a.out[i] = v;
   } else if (MODE == kModeTrailer) {
-    a.out[i] = v + context_modifier(a.base_ctx, a.foff ? a.foff[i] : a.s.off(i));
+    a.out[i] = v + context_modifier(a.base_ctx, e.foff);
   } else {
-    const uint8_t* p = a.s.ptr(i) + a.s.len(i) + 1;
-    const uint32_t stored = rd32_bytes(p) - context_modifier(a.base_ctx, a.foff ? a.foff[i] : a.s.off(i));
+    const uint32_t stored = (uint32_t)(e.bytes() >> 8) - context_modifier(a.base_ctx, e.foff);
     const bool bad = stored != v;
     a.mismatch[i] = bad;
     if (a.out) a.out[i] = v;
@@ -72,18 +105,32 @@ __device__ __forceinline__ void block_epilogue(const BlockArgs& a, uint32_t i, u
     if (bad && a.mismatch_count) atomicAdd(a.mismatch_count, 1u);
   }
 }
+// Same, with the inputs loaded here (drivers without epilogue prefetch).
+template <int MODE>
+__device__ __forceinline__ void block_epilogue(const BlockArgs& a, uint32_t i, uint32_t v) {
+  const uint64_t off = a.s.off(i);
+  block_epilogue<MODE>(a, i, v,
+                       block_pre<MODE>(a, i, reinterpret_cast<uint64_t>(a.s.base) + off + a.s.len(i), off,
+                                       MODE == kModeVerify));
+}
+
+struct NoPre {};
 
 // ============================ CRC32C ======================================
+// CRC ops: the generic driver calls pre(i, ptr, len) with the span's
+// last-round loads and finish(i, crc, pre) after its last round.
 struct OpCrcValue {
   SpanSrc s;
   const uint32_t* init;
   uint32_t flags;
   uint32_t* out;
+  typedef NoPre Pre;
   __device__ const uint8_t* base() const { return s.base; }
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return init ? init[i] : 0u; }
-  __device__ void finish(uint32_t i, uint32_t crc) const {
+  __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre& = Pre{}) const {
     if ((threadIdx.x & 63) == 0) out[i] = (flags & 1u) ? crc_mask(crc) : crc;
   }
 };
@@ -97,25 +144,35 @@ struct OpCrcWal {
   const uint8_t* types;
   WalTypeCrcs tc;
   uint32_t* out;
+  typedef NoPre Pre;
   __device__ const uint8_t* base() const { return s.base; }
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return tc.v[types[i] & 15]; }
-  __device__ void finish(uint32_t i, uint32_t crc) const {
+  __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre& = Pre{}) const {
     if ((threadIdx.x & 63) == 0) out[i] = crc_mask(crc);
   }
 };
 
+// verify: the CRC span is payload || type byte (len = payload + 1); the
+// stored LE32 follows it
 template <int MODE>
 struct OpCrcBlock {
   BlockArgs a;
+  typedef BlockPre Pre;
   __device__ const uint8_t* base() const { return a.s.base; }
   __device__ uint64_t off(uint32_t i) const { return a.s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return a.s.len(i) + (MODE == kModeVerify ? 1 : 0); }
   __device__ uint32_t init_crc(uint32_t) const { return 0u; }
-  __device__ void finish(uint32_t i, uint32_t crc) const {
-    if (MODE == kModeTrailer || (MODE == kModeBuiltin && a.last)) crc = crc_extend_byte(crc, a.last[i]);
-    if ((threadIdx.x & 63) == 0) block_epilogue<MODE>(a, i, crc_mask(crc));
+  __device__ Pre pre(uint32_t i, uint64_t ptr, uint64_t len) const {
+    // verify: bytes from the type byte (ptr + len - 1) on
+    return block_pre<MODE>(a, i, ptr + len - (MODE == kModeVerify ? 1 : 0),
+                           ptr - reinterpret_cast<uint64_t>(a.s.base), MODE == kModeVerify);
+  }
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre& e) const {
+    if (MODE == kModeTrailer || (MODE == kModeBuiltin && a.last)) crc = crc_extend_byte(crc, (uint8_t)e.last);
+    if ((threadIdx.x & 63) == 0) block_epilogue<MODE>(a, i, crc_mask(crc), e);
   }
 };
 
@@ -138,18 +195,27 @@ template <class Op>
 __global__ __launch_bounds__(256) void k_xxh3(Op op, uint32_t count) {
   xxh3_rows_driver(op, count);
 }
+// Wave driver workgroup: 16 waves, one workgroup per CU.
+#ifndef MCK_X3W_THREADS
+#define MCK_X3W_THREADS 1024
+#endif
+constexpr int kX3WaveThreads = MCK_X3W_THREADS;
 template <class Op>
-__global__ __launch_bounds__(1024) void k_xxh3_wave(Op op, uint32_t count) {
+__global__ __launch_bounds__(kX3WaveThreads) void k_xxh3_wave(Op op, uint32_t count) {
   xxh3_wave_driver<Op, false>(op, count, 0);
 }
 
+// XXH3 ops.  The wave driver calls pre(i, ptr, hlen) with the span's last
+// unit and finish(i, h, pre); the row driver calls finish(i, h).
 struct OpX3Value {
   SpanSrc s;
   uint64_t* out;
+  typedef NoPre Pre;
   __device__ const uint8_t* base() const { return s.base; }
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t hlen(uint32_t i) const { return s.len(i); }
-  __device__ void finish(uint32_t i, uint64_t h) const { out[i] = h; }
+  __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
+  __device__ void finish(uint32_t i, uint64_t h, const Pre& = Pre{}) const { out[i] = h; }
 };
 
 // kXXH3 block checksum (table/format.cc:569-597): lo32(XXH3 of all but the
@@ -157,6 +223,7 @@ struct OpX3Value {
 template <int MODE>
 struct OpX3Block {
   BlockArgs a;
+  typedef BlockPre Pre;
   __device__ const uint8_t* base() const { return a.s.base; }
   __device__ uint64_t off(uint32_t i) const { return a.s.off(i); }
   __device__ uint64_t hlen(uint32_t i) const {
@@ -166,17 +233,30 @@ struct OpX3Block {
     if (MODE == kModeVerify || MODE == kModeTrailer || a.last) return n;
     return n ? n - 1 : 0;
   }
-  __device__ void finish(uint32_t i, uint64_t h) const {
-    const uint8_t* p = a.s.ptr(i);
-    const uint64_t n = a.s.len(i);
+  // the byte after the hashed part: verify -- the type byte (then the
+  // stored LE32); builtin without last bytes -- the span's last byte
+  __device__ Pre pre(uint32_t i, uint64_t ptr, uint64_t hlen) const {
+    const bool need = MODE == kModeVerify || (MODE == kModeBuiltin && !a.last);
+    return block_pre<MODE>(a, i, ptr + hlen, ptr - reinterpret_cast<uint64_t>(a.s.base), need);
+  }
+  // (the wave driver hashes only spans > 240 bytes here, never empty ones)
+  __device__ void finish(uint32_t i, uint64_t h, const Pre& e) const {
     uint32_t v;
-    if (MODE == kModeVerify)
-      v = (uint32_t)h ^ (uint32_t)p[n] * kRandomPrime;
-    else if (MODE == kModeTrailer || a.last)
-      v = (uint32_t)h ^ (uint32_t)a.last[i] * kRandomPrime;
+    if (MODE == kModeVerify || (MODE == kModeBuiltin && !a.last))
+      v = (uint32_t)h ^ (uint32_t)(e.bytes() & 0xFF) * kRandomPrime;
     else
-      v = n == 0 ? 0u : (uint32_t)h ^ (uint32_t)p[n - 1] * kRandomPrime;
-    block_epilogue<MODE>(a, i, v);
+      v = (uint32_t)h ^ e.last * kRandomPrime;
+    block_epilogue<MODE>(a, i, v, e);
+  }
+  // row driver and short spans: inputs loaded here; an empty builtin span
+  // is 0 (table/format.cc:588) and reads nothing
+  __device__ void finish(uint32_t i, uint64_t h) const {
+    const uint64_t ptr = reinterpret_cast<uint64_t>(a.s.ptr(i));
+    if (MODE == kModeBuiltin && !a.last && a.s.len(i) == 0) {
+      block_epilogue<MODE>(a, i, 0u, block_pre<MODE>(a, i, ptr, 0, false));
+      return;
+    }
+    finish(i, h, pre(i, ptr, hlen(i)));
   }
 };
 

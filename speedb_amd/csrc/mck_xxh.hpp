@@ -462,6 +462,205 @@ __device__ __forceinline__ uint64_t xl32_64(uint64_t v) {
 // inside the CU); otherwise the waves walk the share round-robin.
 constexpr uint32_t kX3DescCache = 1536;
 
+// One span on the wave, cut into "units": unit k < rounds is round k (four
+// segments, one per row); the last unit (k = units - 1) also carries the
+// lone partial segment (spread over the wave) and the last stripe.  Every
+// unit issues the same six 16-byte loads per lane (clamped to the span's
+// first bytes where a load has no work), so the driver can keep the NEXT
+// unit's loads -- of this span or of the next one -- in flight while it
+// folds the current unit: one HBM round trip per unit is hidden behind the
+// previous unit's compute.
+struct X3WSpan {
+  uint64_t ptr, len;
+  uint32_t i;       // span index
+  uint32_t nb;      // full segments
+  uint32_t nst;     // stripes in the partial segment nb
+  uint32_t rounds;  // four-segment rounds
+  uint32_t units;   // max(rounds, 1)
+  bool lone;        // segment nb is folded by the whole wave in the last unit
+  bool tail;        // last stripe at len - 64
+};
+template <bool PREVIEW>
+__device__ __forceinline__ X3WSpan x3w_span(uint64_t ptr, uint64_t len, uint32_t i) {
+  X3WSpan sp;
+  sp.ptr = ptr;
+  sp.len = len;
+  sp.i = i;
+  // XXH3 util/xxhash.h:5141-5171; XXPH3 util/xxph3.h:1516-1543
+  const uint64_t body = PREVIEW ? len : len - 1;
+  sp.nb = (uint32_t)(body / 1024);
+  sp.nst = (uint32_t)((body - 1024ull * sp.nb) / 64);
+  sp.tail = PREVIEW ? (len & 63) != 0 : true;
+  // when the last round would hold only the partial segment nb, it is
+  // spread over the whole wave instead
+  sp.lone = (sp.nb & 3) == 0;
+  sp.rounds = sp.nb / 4 + (sp.lone ? 0 : 1);
+  sp.units = sp.rounds ? sp.rounds : 1;
+  return sp;
+}
+struct X3WLoads {
+  uint4 d[4];  // round part: stripes st4 + 4m of segment 4k + row, pair q
+  uint4 v;     // lone partial segment: stripe lane / 4, pair q
+  uint4 dl;    // last stripe (len - 64), pair q
+};
+__device__ __forceinline__ bool x3w_ok(const X3WSpan& sp, uint32_t k, uint32_t g, uint32_t st) {
+  return k < sp.rounds && (g < sp.nb || (g == sp.nb && st < sp.nst));
+}
+__device__ __forceinline__ X3WLoads x3w_load(const X3WSpan& sp, uint32_t k, const X3Row& X) {
+  X3WLoads L;
+  const uint32_t g = 4 * k + X.row;
+  const uint64_t seg = sp.ptr + 1024ull * g;
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const uint32_t st = (uint32_t)(X.st4 + 4 * m);
+    L.d[m] = gload16u(x3w_ok(sp, k, g, st) ? seg + 64 * st + 16 * X.q : sp.ptr);
+  }
+  const bool last = k + 1 == sp.units;
+  const bool okl = last && sp.lone && (uint32_t)(X.lane >> 2) < sp.nst;
+  L.v = gload16u(okl ? sp.ptr + 1024ull * sp.nb + 64 * (X.lane >> 2) + 16 * X.q : sp.ptr);
+  L.dl = gload16u(last ? sp.ptr + sp.len - 64 + 16 * X.q : sp.ptr);
+  return L;
+}
+
+// Fold unit k of the span into (a0, a1); after the last unit, merge, finish
+// and reset the accumulators.
+template <class Op, bool PREVIEW>
+__device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32_t k, const X3WLoads& L,
+                                         const X3Row& X, uint64_t& a0, uint64_t& a1, const typename Op::Pre& e) {
+  if (k < sp.rounds) {  // wave-uniform
+    const uint32_t g = 4 * k + X.row;
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (int m = 0; m < 4; m++) {
+      const bool ok = x3w_ok(sp, k, g, (uint32_t)(X.st4 + 4 * m));
+      const uint64_t d0 = ((uint64_t)L.d[m].y << 32) | L.d[m].x, d1 = ((uint64_t)L.d[m].w << 32) | L.d[m].z;
+      // v0.8.1 adds the data word to the neighbouring accumulator
+      // (acc[l ^ 1]); the preview adds it to its own (acc_64bits)
+      c0 += ok ? (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.k0[m]) : 0;
+      c1 += ok ? (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.k1[m]) : 0;
+    }
+    c0 = row_sum_st4(c0);
+    c1 = row_sum_st4(c1);
+    // row 0 gathers the four rows' sums in segment order: rows 0, 1
+    // (lane ^ 16), 2 (lane ^ 32), 3 (lane ^ 48); only row 0's accumulators
+    // are used
+    const uint64_t e0 = xl16_64(c0), e1 = xl16_64(c1);
+    const uint64_t C0[4] = {c0, e0, xl32_64(c0), xl32_64(e0)};
+    const uint64_t C1[4] = {c1, e1, xl32_64(c1), xl32_64(e1)};
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const uint32_t gr = 4 * k + r;
+      if (gr > sp.nb) break;  // wave-uniform
+      a0 += C0[r];
+      a1 += C1[r];
+      if (gr < sp.nb) {
+        a0 = xxh3_scramble(a0, X.ks0);
+        a1 = xxh3_scramble(a1, X.ks1);
+      }
+    }
+  }
+  if (k + 1 < sp.units) return;  // wave-uniform
+  if (sp.lone) {  // segment nb alone: lane = stripe * 4 + pair
+    const bool okl = (uint32_t)(X.lane >> 2) < sp.nst;
+    const uint64_t d0 = ((uint64_t)L.v.y << 32) | L.v.x, d1 = ((uint64_t)L.v.w << 32) | L.v.z;
+    uint64_t c0 = okl ? (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.ko0) : 0;
+    uint64_t c1 = okl ? (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.ko1) : 0;
+    c0 = row_sum_st4(c0);
+    c1 = row_sum_st4(c1);
+    c0 += xl16_64(c0);
+    c1 += xl16_64(c1);
+    a0 += c0 + xl32_64(c0);
+    a1 += c1 + xl32_64(c1);
+  }
+  const uint64_t l0 = ((uint64_t)L.dl.y << 32) | L.dl.x, l1 = ((uint64_t)L.dl.w << 32) | L.dl.z;
+  if (sp.tail) {
+    a0 += (PREVIEW ? l0 : l1) + mul32to64(l0 ^ X.kl0);
+    a1 += (PREVIEW ? l1 : l0) + mul32to64(l1 ^ X.kl1);
+  }
+  const uint64_t m = quad_sum(mul128_fold64(a0 ^ X.km0, a1 ^ X.km1));
+  const uint64_t h = PREVIEW ? xxph3_avalanche(sp.len * P64_1 + m) : xxh3_avalanche(sp.len * P64_1 + m);
+  if (X.lane == 0) op.finish(sp.i, h, e);
+  a0 = X.i0;
+  a1 = X.i1;
+}
+
+// Span feeds of the wave driver (compile-time variants, so the dynamic feed
+// has no global load that the in-order vmcnt would make wait behind the
+// prefetched unit):
+//   X3FeedLds    -- the workgroup's share is staged in LDS; waves take spans
+//                   with an LDS ticket as they free up (balanced in the CU);
+//   X3FeedStatic -- share too large for LDS: the wave walks positions
+//                   wid, wid + wpb, ... and fetches 64 descriptors at a time
+//                   (lane l: the l-th next), read back with v_readlane.
+// Both skip short spans (done before the loop).
+struct X3FeedLds {
+  const uint64_t* off;  // LDS
+  const uint32_t* len;  // LDS
+  uint32_t* ctr;        // LDS
+  uint32_t n, b, G;
+  uint64_t base;
+  template <class Op, bool PREVIEW>
+  __device__ __forceinline__ bool next(const Op&, X3WSpan& sp) {
+    for (;;) {
+      const uint32_t t = __builtin_amdgcn_readfirstlane(lds_ticket(ctr));
+      if (t >= n) return false;
+      const uint64_t n_t = readfirstlane_u64((uint64_t)len[t]);
+      if (n_t > 240) {
+        sp = x3w_span<PREVIEW>(readfirstlane_u64(base + off[t]), n_t, b + G * t);
+        return true;
+      }
+    }
+  }
+};
+struct X3FeedStatic {
+  uint32_t t, k, n, b, G, wpb;
+  uint64_t base;
+  uint64_t d_off;  // per lane: descriptor of position t + lane * wpb
+  uint32_t d_len;
+  template <class Op, bool PREVIEW>
+  __device__ __forceinline__ bool next(const Op& op, X3WSpan& sp) {
+    for (;;) {
+      if (k == 64) {  // refill: the wave's next 64 positions
+        const uint32_t tl = t + (uint32_t)(threadIdx.x & 63) * wpb;
+        d_off = tl < n ? op.off(b + G * tl) : 0;
+        d_len = tl < n ? (uint32_t)op.hlen(b + G * tl) : 0;
+        k = 0;
+      }
+      if (t >= n) return false;
+      const uint64_t len = readlane_u32(d_len, k);
+      const uint64_t off = readlane_u64(d_off, k);
+      const uint32_t i = b + G * t;
+      t += wpb;
+      k++;
+      if (len > 240) {
+        sp = x3w_span<PREVIEW>(base + off, len, i);
+        return true;
+      }
+    }
+  }
+};
+
+// Every unit issues all its loads -- the four round loads, the lone partial
+// segment, the last stripe and the epilogue inputs -- before any is used, so
+// a span of up to 4 KiB + 1 segment costs ONE memory round trip (the
+// unpipelined loads of round, lone segment, last stripe and the epilogue's
+// dependent descriptor/trailer reads were four).  Latency across units is
+// hidden by the other waves (16 per CU); prefetching the next unit in
+// registers as well needs ~150 VGPRs, and at 3 waves per SIMD measured
+// slower (4.07 vs 4.91 TB/s on the SST-shaped mix).
+template <class Op, bool PREVIEW, class Feed>
+__device__ __forceinline__ void xxh3_wave_loop(const Op& op, Feed& f, const X3Row& X) {
+  X3WSpan cur;
+  while (f.template next<Op, PREVIEW>(op, cur)) {
+    uint64_t a0 = X.i0, a1 = X.i1;
+    for (uint32_t k = 0; k < cur.units; k++) {
+      const X3WLoads L = x3w_load(cur, k, X);
+      const typename Op::Pre e = op.pre(cur.i, cur.ptr, cur.len);
+      x3w_fold<Op, PREVIEW>(op, cur, k, L, X, a0, a1, e);
+    }
+  }
+}
+
 template <class Op, bool PREVIEW>
 __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, uint64_t seed) {
   const X3Row X = x3_row(seed);
@@ -481,93 +680,22 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
   __syncthreads();
   const uint32_t wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  uint32_t t = wid;  // static walk: this wave's next position in the share
-  for (;;) {
-    if (dyn) t = __builtin_amdgcn_readfirstlane(lds_ticket(&s_ctr));
-    if (t >= n) break;
-    const uint32_t i = b + G * t;
-    const uint64_t len = dyn ? (uint64_t)s_len[t] : op.hlen(i);
-    const uint64_t ptr = base + (dyn ? s_off[t] : op.off(i));
-    if (!dyn) t += wpb;
+  // short spans (n <= 240: the three small-input classes) first, one per
+  // lane -- outside the pipelined loop
+  for (uint32_t tt = threadIdx.x; tt < n; tt += blockDim.x) {
+    const uint32_t i = b + G * tt;
+    const uint64_t len = dyn ? (uint64_t)s_len[tt] : op.hlen(i);
     if (len <= 240) {
-      if (X.lane == 0) {
-        const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr);
-        op.finish(i, PREVIEW ? xxph3_short(p, len, X.seed) : xxh3_short(p, len));
-      }
-      continue;
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(base + (dyn ? s_off[tt] : op.off(i)));
+      op.finish(i, PREVIEW ? xxph3_short(p, len, seed) : xxh3_short(p, len));
     }
-    // XXH3 util/xxhash.h:5141-5171; XXPH3 util/xxph3.h:1516-1543
-    const uint64_t body = PREVIEW ? len : len - 1;
-    const uint32_t nb = (uint32_t)(body / 1024);
-    const uint32_t nst = (uint32_t)((body - 1024ull * nb) / 64);
-    const bool tail = PREVIEW ? (len & 63) != 0 : true;
-    // rounds of four segments; when the last round would hold only the
-    // partial segment nb, it is spread over the whole wave instead
-    const bool lone = (nb & 3) == 0;
-    const uint32_t rounds = nb / 4 + (lone ? 0 : 1);
-    uint64_t a0 = X.i0, a1 = X.i1;
-    for (uint32_t k = 0; k < rounds; k++) {
-      const uint32_t g = 4 * k + X.row;
-      const uint64_t seg = ptr + 1024ull * g;
-      const bool full = g < nb;
-      uint4 d[4];
-      bool ok[4];
-#pragma unroll
-      for (int m = 0; m < 4; m++) {
-        const uint32_t st = (uint32_t)(X.st4 + 4 * m);
-        ok[m] = full || (g == nb && st < nst);
-        d[m] = gload16u(ok[m] ? seg + 64 * st + 16 * X.q : ptr);
-      }
-      uint64_t c0 = 0, c1 = 0;
-#pragma unroll
-      for (int m = 0; m < 4; m++) {
-        const uint64_t d0 = ((uint64_t)d[m].y << 32) | d[m].x, d1 = ((uint64_t)d[m].w << 32) | d[m].z;
-        c0 += ok[m] ? (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.k0[m]) : 0;
-        c1 += ok[m] ? (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.k1[m]) : 0;
-      }
-      c0 = row_sum_st4(c0);
-      c1 = row_sum_st4(c1);
-      // row 0 gathers the four rows' sums in segment order: rows 0, 1
-      // (lane ^ 16), 2 (lane ^ 32), 3 (lane ^ 48); only row 0's
-      // accumulators are used
-      const uint64_t e0 = xl16_64(c0), e1 = xl16_64(c1);
-      uint64_t C0[4] = {c0, e0, xl32_64(c0), xl32_64(e0)};
-      uint64_t C1[4] = {c1, e1, xl32_64(c1), xl32_64(e1)};
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const uint32_t gr = 4 * k + r;
-        if (gr > nb) break;  // wave-uniform
-        a0 += C0[r];
-        a1 += C1[r];
-        if (gr < nb) {
-          a0 = xxh3_scramble(a0, X.ks0);
-          a1 = xxh3_scramble(a1, X.ks1);
-        }
-      }
-    }
-    if (lone) {  // segment nb alone: lane = stripe * 4 + pair
-      const uint32_t st = X.lane >> 2;
-      const bool okl = st < nst;
-      const uint4 v = gload16u(okl ? ptr + 1024ull * nb + 64 * st + 16 * X.q : ptr);
-      const uint64_t d0 = ((uint64_t)v.y << 32) | v.x, d1 = ((uint64_t)v.w << 32) | v.z;
-      uint64_t c0 = okl ? (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.ko0) : 0;
-      uint64_t c1 = okl ? (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.ko1) : 0;
-      c0 = row_sum_st4(c0);
-      c1 = row_sum_st4(c1);
-      c0 += xl16_64(c0);
-      c1 += xl16_64(c1);
-      a0 += c0 + xl32_64(c0);
-      a1 += c1 + xl32_64(c1);
-    }
-    const uint4 dl = gload16u(ptr + len - 64 + 16 * X.q);
-    const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
-    if (tail) {
-      a0 += (PREVIEW ? l0 : l1) + mul32to64(l0 ^ X.kl0);
-      a1 += (PREVIEW ? l1 : l0) + mul32to64(l1 ^ X.kl1);
-    }
-    const uint64_t m = quad_sum(mul128_fold64(a0 ^ X.km0, a1 ^ X.km1));
-    const uint64_t h = PREVIEW ? xxph3_avalanche(len * P64_1 + m) : xxh3_avalanche(len * P64_1 + m);
-    if (X.lane == 0) op.finish(i, h);
+  }
+  if (dyn) {
+    X3FeedLds f{s_off, s_len, &s_ctr, n, b, G, base};
+    xxh3_wave_loop<Op, PREVIEW>(op, f, X);
+  } else {
+    X3FeedStatic f{wid, 64, n, b, G, wpb, base, 0, 0};
+    xxh3_wave_loop<Op, PREVIEW>(op, f, X);
   }
 }
 
