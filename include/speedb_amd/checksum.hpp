@@ -44,9 +44,11 @@ class Status {
   static Status Corruption(const std::string& msg) { return Status(kCorruption, msg); }
   static Status InvalidArgument(const std::string& msg) { return Status(kInvalidArgument, msg); }
   static Status IOError(const std::string& msg) { return Status(kIOError, msg); }
+  static Status NotSupported(const std::string& msg) { return Status(kNotSupported, msg); }
   bool ok() const { return code_ == kOk; }
   bool IsCorruption() const { return code_ == kCorruption; }
   bool IsInvalidArgument() const { return code_ == kInvalidArgument; }
+  bool IsNotSupported() const { return code_ == kNotSupported; }
   std::string ToString() const {
     switch (code_) {
       case kOk:
@@ -55,13 +57,15 @@ class Status {
         return "Corruption: " + msg_;
       case kInvalidArgument:
         return "Invalid argument: " + msg_;
+      case kNotSupported:
+        return "Not implemented: " + msg_;
       default:
         return "IO error: " + msg_;
     }
   }
 
  private:
-  enum Code { kOk, kCorruption, kInvalidArgument, kIOError };
+  enum Code { kOk, kCorruption, kInvalidArgument, kIOError, kNotSupported };
   Status(Code c, const std::string& m) : code_(c), msg_(m) {}
   Code code_ = kOk;
   std::string msg_;
@@ -69,6 +73,8 @@ class Status {
 
 inline Status FromRc(int rc, const char* what) {
   if (rc == MCK_OK) return Status::OK();
+  if (rc == MCK_ECORRUPT) return Status::Corruption(mck_last_error());
+  if (rc == MCK_ENOTSUP) return Status::NotSupported(mck_last_error());
   std::string m = std::string(what) + ": " + mck_last_error();
   return rc == MCK_EINVAL ? Status::InvalidArgument(m) : Status::IOError(m);
 }
@@ -148,6 +154,15 @@ struct BlockHandle {
 inline Status VerifyBlockChecksums(const Footer& footer, const void* dev_image, uint64_t file_base,
                                    const std::vector<BlockHandle>& handles, const std::string& file_name,
                                    std::vector<Status>* per_block, mck_stream_t stream = nullptr);
+
+// table/block_based/block_based_table_reader.cc:2336-2500
+// BlockBasedTable::VerifyChecksum of a whole SST image in host memory: the
+// footer / metaindex / properties / index are read on the host
+// (mck_sst_list_blocks), the format_version 6 footer checksum is checked, and
+// every block is verified on the GPU in one batch.  Returns the first
+// failure (Footer::DecodeFrom's or VerifyBlockChecksum's message).
+inline Status VerifySstFile(const std::string& file_name, const char* image, uint64_t size,
+                            std::vector<mck_sst_block>* blocks_out = nullptr, mck_stream_t stream = nullptr);
 
 namespace log {
 // db/log_format.h:22-45
@@ -398,6 +413,35 @@ inline bool FileChecksumGenCrc32c::UpdateDevice(const void* dev_data, uint64_t n
     return false;
   checksum_ = v;
   return true;
+}
+
+inline Status VerifySstFile(const std::string& file_name, const char* image, uint64_t size,
+                            std::vector<mck_sst_block>* blocks_out, mck_stream_t stream) {
+  mck_sst_footer f;
+  uint64_t n = 0;
+  int rc = mck_sst_list_blocks(image, size, &f, nullptr, 0, &n);
+  if (rc) return FromRc(rc, "mck_sst_list_blocks");
+  std::vector<mck_sst_block> blocks(n);
+  rc = mck_sst_list_blocks(image, size, &f, blocks.data(), n, &n);
+  if (rc) return FromRc(rc, "mck_sst_list_blocks");
+  rc = mck_sst_verify_footer(image + f.footer_offset, &f);
+  if (rc) return FromRc(rc, "mck_sst_verify_footer");
+  if (blocks_out) *blocks_out = blocks;
+  void* d = nullptr;
+  if (hipMalloc(&d, size + 64) != hipSuccess) return Status::IOError("hipMalloc failed");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (hipMemcpyAsync(d, image, size, hipMemcpyHostToDevice, st) != hipSuccess) {
+    (void)hipFree(d);
+    return Status::IOError("hipMemcpyAsync failed");
+  }
+  std::vector<BlockHandle> handles(n);
+  for (uint64_t i = 0; i < n; i++) handles[i] = BlockHandle{blocks[i].offset, blocks[i].size};
+  Footer footer;
+  footer.checksum_type = static_cast<ChecksumType>(f.checksum_type);
+  footer.base_context_checksum = f.base_context_checksum;
+  Status s = VerifyBlockChecksums(footer, d, 0, handles, file_name, nullptr, stream);
+  (void)hipFree(d);
+  return s;
 }
 
 }  // namespace speedb_amd

@@ -45,6 +45,8 @@ typedef struct ihipStream_t* mck_stream_t;
 #define MCK_EHIP (-2)     /* a HIP runtime call failed; see mck_last_error */
 #define MCK_ENODEV (-3)   /* no usable gfx950 device / device index       */
 #define MCK_ENOMEM (-4)   /* staging allocation failed                    */
+#define MCK_ECORRUPT (-5) /* corrupt SST structure (footer, handles ...)  */
+#define MCK_ENOTSUP (-6)  /* valid but unsupported here (e.g. compressed index) */
 
 /* ---- checksum types: include/rocksdb/table.h:69-75 ChecksumType ---------- */
 #define MCK_kNoChecksum 0
@@ -256,6 +258,72 @@ int mck_kv_protect_verify_batch(int kind, const mck_spans* keys,
                                 uint32_t prot_bytes, uint8_t* mismatch,
                                 uint32_t* mismatch_count, uint64_t* computed,
                                 mck_stream_t stream);
+
+/* ---- SST files: whole-file verification ------------- */
+
+/* Footer of a block-based table (table/format.h Footer). */
+typedef struct mck_sst_footer {
+  uint64_t magic;                  /* table magic (legacy magic upconverted) */
+  uint32_t format_version;
+  int32_t checksum_type;           /* MCK_k* */
+  uint32_t base_context_checksum;  /* format_version >= 6, else 0          */
+  uint32_t footer_checksum;        /* format_version >= 6: stored value    */
+  uint32_t block_trailer_size;     /* 5                                     */
+  uint32_t has_index_handle;       /* 0 until the metaindex supplied it (v6) */
+  uint64_t footer_offset;
+  uint64_t metaindex_offset, metaindex_size;
+  uint64_t index_offset, index_size;
+  uint32_t index_type;             /* BlockBasedTableOptions::IndexType     */
+  uint32_t index_value_is_delta_encoded;
+} mck_sst_footer;
+
+/* Block kinds (table/block_based/block_type.h, meta block names of
+ * table/meta_blocks.cc:29-35, block_based_table_builder.cc:2096-2100). */
+#define MCK_SST_BLOCK_DATA 0
+#define MCK_SST_BLOCK_INDEX 1
+#define MCK_SST_BLOCK_INDEX_PARTITION 2
+#define MCK_SST_BLOCK_METAINDEX 3
+#define MCK_SST_BLOCK_PROPERTIES 4
+#define MCK_SST_BLOCK_FILTER 5
+#define MCK_SST_BLOCK_FILTER_PARTITION_INDEX 6
+#define MCK_SST_BLOCK_FILTER_PARTITION 7
+#define MCK_SST_BLOCK_RANGE_DEL 8
+#define MCK_SST_BLOCK_COMPRESSION_DICT 9
+#define MCK_SST_BLOCK_OTHER_META 10
+
+/* One checksummed block: payload [offset, offset + size), then its 5-byte
+ * trailer [compression type][LE32 checksum + context modifier]. */
+typedef struct mck_sst_block {
+  uint64_t offset;
+  uint64_t size;
+  int32_t kind;
+  uint32_t reserved;
+} mck_sst_block;
+
+/* table/format.cc:348-470 Footer::DecodeFrom on the last tail_len bytes of a
+ * file (tail_offset = their file offset; tail_len >= 48, normally 53).
+ * Host memory, no device work; the v6 footer checksum is checked by
+ * mck_sst_verify_footer.  MCK_ECORRUPT / MCK_ENOTSUP with the reference's
+ * message in mck_last_error(). */
+int mck_sst_decode_footer(const void* tail, uint64_t tail_len,
+                          uint64_t tail_offset, mck_sst_footer* footer);
+
+/* Every checksummed block of an SST image held in HOST memory, in the order
+ * BlockBasedTable::VerifyChecksum visits them (table/block_based/
+ * block_based_table_reader.cc:2336-2500): metaindex, meta blocks, index (and
+ * its partitions for kTwoLevelIndexSearch), data blocks, filter partitions.
+ * Reads the footer, metaindex, properties (index type, value delta
+ * encoding) and index blocks on the host.  blocks = NULL queries the count
+ * (*nblocks).  Compressed index/meta blocks: MCK_ENOTSUP. */
+int mck_sst_list_blocks(const void* file, uint64_t file_size,
+                        mck_sst_footer* footer, mck_sst_block* blocks,
+                        uint64_t cap, uint64_t* nblocks);
+
+/* table/format.cc:405-440: check the format_version 6 footer checksum of the
+ * 53 footer bytes (host memory); 0 for older formats / kNoChecksum.  The
+ * blocks themselves are verified with ONE mck_sst_verify_batch over the
+ * listed handles (file image in device memory, offsets = handle offsets). */
+int mck_sst_verify_footer(const void* footer53, const mck_sst_footer* footer);
 
 /* ========================================================================= */
 /* 3. Multi-GPU / host-resident input                                       */

@@ -9,6 +9,7 @@ raises ImportError: there is no CPU fallback.
 from . import _lib  # noqa: F401  (fails loudly if the engine is not built)
 from .checksum import *  # noqa: F401,F403
 from .checksum import __all__ as _checksum_all
+from . import sst  # noqa: F401  (whole-SST-file verification)
 
 __all__ = list(_checksum_all)
 __version__ = "0.1.0"

@@ -86,6 +86,9 @@ SIGNATURES = [
     ("mck_kv_protect_verify_batch", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.POINTER(mck_spans), vp, vp, vp,
       ctypes.c_uint32, vp, vp, vp, vp]),
+    ("mck_sst_decode_footer", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
+    ("mck_sst_list_blocks", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
+    ("mck_sst_verify_footer", ctypes.c_int, [vp, vp]),
     ("mck_partition_spans", ctypes.c_int,
      [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp]),
     ("mck_host_batch_checksum", ctypes.c_int,

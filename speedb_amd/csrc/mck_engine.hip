@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../../include/speedb_amd/mck.h"
+#include "mck_internal.h"
 #include "mck_kernels.hpp"
 
 namespace mck {
@@ -313,6 +314,7 @@ using namespace mck;
 extern "C" {
 
 const char* mck_last_error(void) { return t_err; }
+void mck_internal_set_error(const char* msg) { snprintf(t_err, sizeof t_err, "%s", msg); }
 const char* mck_version(void) { return "speedb_amd mck 0.1 (gfx950)"; }
 
 int mck_device_count(void) {

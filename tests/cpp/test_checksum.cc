@@ -5,6 +5,7 @@
 // run by tests/test_cpp_mirror.py.
 #include <hip/hip_runtime_api.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <random>
@@ -341,11 +342,43 @@ TEST(FileChecksum, Crc32cGenerator) {
             v);
 }
 
-int main() {
+// BlockBasedTable::VerifyChecksum of an SST image written by the test-side
+// writer (tests/sst_format.py): clean -> OK; with one payload byte flipped at
+// `bad_off` -> Corruption naming the block.
+static int VerifySstFileCase(const char* path, long bad_off) {
+  FILE* fp = fopen(path, "rb");
+  if (!fp) return 2;
+  std::string img;
+  char buf[1 << 16];
+  size_t k;
+  while ((k = fread(buf, 1, sizeof buf, fp)) > 0) img.append(buf, k);
+  fclose(fp);
+  std::vector<mck_sst_block> blocks;
+  Status s = VerifySstFile("000042.sst", img.data(), img.size(), &blocks);
+  printf("clean: %s (%zu blocks)\n", s.ToString().c_str(), blocks.size());
+  EXPECT_TRUE(s.ok());
+  EXPECT_TRUE(blocks.size() > 3);
+  img[bad_off] ^= 0x08;
+  s = VerifySstFile("000042.sst", img.data(), img.size());
+  printf("corrupt: %s\n", s.ToString().c_str());
+  EXPECT_TRUE(s.IsCorruption());
+  EXPECT_TRUE(s.ToString().find("block checksum mismatch") != std::string::npos);
+  EXPECT_TRUE(s.ToString().find("in 000042.sst offset") != std::string::npos);
+  img[bad_off] ^= 0x08;
+  img[img.size() - 1] ^= 0x01;  // magic
+  s = VerifySstFile("000042.sst", img.data(), img.size());
+  EXPECT_TRUE(s.IsCorruption());
+  EXPECT_TRUE(s.ToString().find("Bad table magic number") != std::string::npos);
+  printf("%d checks, %d failures\n", g_checks, g_fail);
+  return g_fail ? 1 : 0;
+}
+
+int main(int argc, char** argv) {
   if (mck_device_count() < 1) {
     fprintf(stderr, "no gfx950 device\n");
     return 2;
   }
+  if (argc == 4 && !strcmp(argv[1], "--sst")) return VerifySstFileCase(argv[2], atol(argv[3]));
   RUN(CRC, StandardResults);
   RUN(CRC, Values);
   RUN(CRC, Extend);

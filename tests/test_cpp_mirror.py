@@ -35,3 +35,21 @@ def test_cpp_mirror_reference_cases(gpu):
     print(out.stderr)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "0 failures" in out.stdout
+
+
+@pytest.mark.gpu
+def test_cpp_verify_sst_file(gpu, oracle, tmp_path):
+    """speedb_amd::VerifySstFile (C++ mirror of BlockBasedTable::
+    VerifyChecksum) on a format_version 6 image from the test writer."""
+    from sst_format import write_sst
+    img, layout = write_sst(oracle, format_version=6, checksum_type=1, index_type=2, n_data=30,
+                            meta=("partitioned_filter", "range_del"))
+    path = tmp_path / "000042.sst"
+    path.write_bytes(img)
+    data = [b for b in layout.blocks if b[2] == "data"]
+    bad = data[len(data) // 2][0] + 11
+    out = subprocess.run([build(), "--sst", str(path), str(bad)], capture_output=True, text=True, timeout=120)
+    print(out.stdout)
+    print(out.stderr)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 failures" in out.stdout

@@ -1,0 +1,137 @@
+"""Whole-SST-file verification: the engine's host SST
+reader (mck_sst_list_blocks) lists exactly the blocks the test-side writer
+put into block-based-table images of every footer version / index type, and
+the reference's footer errors are reported; on the GPU every block of the
+image verifies in one batch and injected corruption is flagged at exactly
+the corrupted block (with VerifyBlockChecksum's message)."""
+import random
+import struct
+
+import pytest
+
+from sst_format import write_sst
+
+CASES = [
+    # (format_version, checksum type, index type, delta, meta blocks)
+    (0, 1, 0, False, ("filter",)),
+    (2, 1, 0, False, ("filter", "range_del")),
+    (3, 4, 1, False, ("range_del",)),
+    (4, 1, 0, True, ("filter", "compression_dict")),
+    (5, 4, 2, True, ("partitioned_filter", "range_del")),
+    (5, 1, 3, True, ()),
+    (6, 4, 0, True, ("filter", "range_del")),
+    (6, 1, 2, True, ("partitioned_filter",)),
+    (6, 4, 3, False, ("filter",)),
+    (5, 2, 0, True, ("filter",)),   # kxxHash
+    (5, 3, 0, True, ()),            # kxxHash64
+    (5, 0, 0, True, ("filter",)),   # kNoChecksum
+]
+
+
+def _kinds(blocks):
+    return sorted((b.offset, b.size, b.kind) for b in blocks)
+
+
+@pytest.mark.parametrize("fv,ct,it,delta,meta", CASES)
+def test_list_blocks_matches_writer(oracle, fv, ct, it, delta, meta):
+    from speedb_amd import sst
+    if fv == 0 and ct != 1:
+        pytest.skip("format_version 0 implies kCRC32c")
+    img, layout = write_sst(oracle, seed=fv * 31 + it, checksum_type=ct, format_version=fv, index_type=it,
+                            delta=delta, meta=meta, n_data=37)
+    f, blocks = sst.list_blocks(img)
+    assert f.format_version == fv and f.checksum_type == ct
+    assert f.index_type == it and bool(f.index_value_is_delta_encoded) == delta
+    assert f.footer_offset == layout.footer_offset
+    if fv >= 6:
+        assert f.base_context_checksum == 0x5EED1234
+    assert _kinds(blocks) == sorted(layout.blocks)
+    # VerifyChecksum order: metaindex first, data blocks after the index
+    assert blocks[0].kind == "metaindex"
+    assert [b.offset for b in blocks if b.kind == "data"] == sorted(
+        o for o, _, k in layout.blocks if k == "data")
+
+
+def test_footer_errors(oracle):
+    """Footer::DecodeFrom's corruption messages (table/format.cc:348-470)."""
+    from speedb_amd import sst
+    img, _ = write_sst(oracle, format_version=6, n_data=4)
+    bad = bytearray(img)
+    bad[-1] ^= 0xFF
+    with pytest.raises(sst.SstError, match="Bad table magic number"):
+        sst.list_blocks(bytes(bad))
+    bad = bytearray(img)
+    bad[-12:-8] = struct.pack("<I", 7)
+    with pytest.raises(sst.SstError, match="Corrupt or unsupported format_version: 7"):
+        sst.list_blocks(bytes(bad))
+    bad = bytearray(img)
+    bad[-53] = 9
+    with pytest.raises(sst.SstError, match="Corrupt or unsupported checksum type: 9"):
+        sst.list_blocks(bytes(bad))
+    bad = bytearray(img)
+    bad[-52] ^= 1
+    with pytest.raises(sst.SstError, match="Bad extended magic number"):
+        sst.list_blocks(bytes(bad))
+    bad = bytearray(img)
+    bad[-13] = 1  # checked reserved padding
+    with pytest.raises(sst.SstError, match="future feature"):
+        sst.list_blocks(bytes(bad))
+    with pytest.raises(sst.SstError, match="too short"):
+        sst.list_blocks(b"x" * 20)
+
+
+def test_structure_errors(oracle):
+    """A handle past the end of the file, a compressed index block."""
+    from speedb_amd import sst
+    img, layout = write_sst(oracle, format_version=5, n_data=6)
+    f, blocks = sst.list_blocks(img)
+    idx = next(b for b in blocks if b.kind == "index")
+    bad = bytearray(img)
+    bad[idx.offset + idx.size] = 1  # trailer type byte: compressed
+    with pytest.raises(sst.SstError, match="compressed"):
+        sst.list_blocks(bytes(bad))
+    # truncate the file just before the footer: the metaindex handle dangles
+    short = img[:idx.offset] + img[-53:]
+    with pytest.raises(sst.SstError):
+        sst.list_blocks(short)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fv,ct,it,delta,meta", CASES)
+def test_verify_sst_image(gpu, oracle, fv, ct, it, delta, meta):
+    from speedb_amd import sst
+    img, layout = write_sst(oracle, seed=fv * 7 + it, checksum_type=ct, format_version=fv, index_type=it,
+                            delta=delta, meta=meta, n_data=53)
+    per = []
+    st = sst.VerifyChecksum(img, "000042.sst", per_block=per)
+    assert st.ok(), st.ToString()
+    assert len(per) == len(layout.blocks)
+    if ct == 0:
+        return  # kNoChecksum: nothing to corrupt
+    # flip one byte in three blocks of different kinds: exactly those fail
+    f, blocks = sst.list_blocks(img)
+    rnd = random.Random(fv)
+    victims = [rnd.choice([b for b in blocks if b.kind == "data"]),
+               next(b for b in blocks if b.kind == "properties")]
+    bad = bytearray(img)
+    for b in victims:
+        bad[b.offset + b.size // 2] ^= 0x10
+    per = []
+    st = sst.VerifyChecksum(bytes(bad), "000042.sst", per_block=per)
+    assert st.IsCorruption()
+    assert "block checksum mismatch" in st.message and "in 000042.sst offset" in st.message
+    failed = sorted(b.offset for b, s in per if not s.ok())
+    assert failed == sorted(b.offset for b in victims)
+
+
+@pytest.mark.gpu
+def test_verify_sst_footer_checksum(gpu, oracle):
+    """format_version 6: a flipped bit in the footer's reserved (unchecked)
+    padding is caught by the footer checksum (table/format.cc:419-426)."""
+    from speedb_amd import sst
+    img, _ = write_sst(oracle, format_version=6, n_data=5, checksum_type=4)
+    assert sst.VerifyChecksum(img).ok()
+    bad = bytearray(img)
+    bad[-53 + 1 + 16 + 3] ^= 0x40  # inside the 16 unchecked reserved bytes
+    st = sst.VerifyChecksum(bytes(bad))
+    assert st.IsCorruption() and "checksum mismatch" in st.message and "Footer at" in st.message
