@@ -176,6 +176,41 @@ int mck_wal_record_crc_batch(const mck_spans* payloads, const uint8_t* types,
                              uint32_t log_number, uint32_t* out,
                              mck_stream_t stream);
 
+/* ---- device WAL writer ------------------------------ */
+
+/* One physical record of the write plan. */
+typedef struct mck_wal_fragment {
+  uint64_t src_off;  /* payload offset in the source buffer                */
+  uint64_t dst_off;  /* header offset in the output stream                 */
+  uint32_t length;   /* payload bytes (<= kBlockSize - header size)         */
+  uint8_t type;      /* record type (db/log_format.h)                       */
+  uint8_t pad;       /* zero bytes written just before the header (the
+                        previous block's trailer, < header size)           */
+  uint16_t reserved;
+} mck_wal_fragment;
+
+/* Host: log::Writer::AddRecord's fragmentation (db/log_writer.cc:79-175, no
+ * WAL compression) of `count` logical records of host_lengths[r] bytes at
+ * source offsets host_src_offsets[r], appended to a log whose current block
+ * holds block_offset bytes.  Writes the fragments (frags = NULL queries the
+ * count), the number of bytes the records add to the log (*out_bytes, incl.
+ * block-trailer padding) and the writer's block_offset_ afterwards. */
+int mck_wal_plan(const uint64_t* host_src_offsets, const uint32_t* host_lengths,
+                 uint32_t count, uint32_t block_offset, int recycle,
+                 mck_wal_fragment* frags, uint64_t cap, uint64_t* nfrags,
+                 uint64_t* out_bytes, uint32_t* new_block_offset);
+
+/* Device: write the planned physical records into `out` (device; byte
+ * offsets of the plan relative to out) exactly as log::Writer appends them
+ * (db/log_writer.cc:263-311 EmitPhysicalRecord): trailer zero padding,
+ * [masked CRC LE32][length LE16][type][log number LE32 if recyclable],
+ * payload.  frags: device array [nfrags]; crc_scratch: device u32 [nfrags]
+ * (the masked fragment CRCs, computed first in one batch); out must be
+ * 16-byte aligned (any hipMalloc allocation is). */
+int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags,
+                        uint32_t nfrags, uint32_t log_number,
+                        uint32_t* crc_scratch, void* out, mck_stream_t stream);
+
 /* Per-32KiB-block result of a WAL verify scan (db/log_reader.cc:450-584
  * ReadPhysicalRecord, checksum on).  Records of block b are walked in order;
  * the walk stops at the first record that the reference would not return. */
@@ -324,6 +359,60 @@ int mck_sst_list_blocks(const void* file, uint64_t file_size,
  * blocks themselves are verified with ONE mck_sst_verify_batch over the
  * listed handles (file image in device memory, offsets = handle offsets). */
 int mck_sst_verify_footer(const void* footer53, const mck_sst_footer* footer);
+
+/* ---- blob files: db/blob/blob_log_format.{h,cc} ------ */
+
+#define MCK_BLOB_kHeaderSize 30        /* BlobLogHeader::kSize        */
+#define MCK_BLOB_kFooterSize 32        /* BlobLogFooter::kSize        */
+#define MCK_BLOB_kRecordHeaderSize 32  /* BlobLogRecord::kHeaderSize  */
+#define MCK_BLOB_kMagicNumber 2395959u
+
+/* Blob file header/footer fields (BlobLogHeader / BlobLogFooter). */
+typedef struct mck_blob_file_info {
+  uint32_t version;
+  uint32_t column_family_id;
+  uint8_t has_ttl;
+  uint8_t compression;
+  uint8_t has_footer;   /* the last 32 bytes start with the magic number */
+  uint8_t reserved;
+  uint64_t expiration_first, expiration_second;
+  uint64_t footer_blob_count;
+  uint32_t footer_crc;  /* stored; = Mask(Value(footer[0..28))) if intact */
+  uint32_t reserved2;
+} mck_blob_file_info;
+
+/* One record: header at `offset`, then key_size + value_size blob bytes. */
+typedef struct mck_blob_record {
+  uint64_t offset;
+  uint64_t key_size;
+  uint64_t value_size;
+} mck_blob_record;
+
+/* Walk a blob file image in HOST memory (BlobLogSequentialReader order):
+ * decode the header (BlobLogHeader::DecodeFrom), list every record by its
+ * header's sizes, and decode the footer when the last 32 bytes start with
+ * the magic number (its CRC -- footer_crc -- is for the caller to check on
+ * the device, BlobLogFooter::DecodeFrom).  Host only, no device work.
+ * records = NULL queries the count.  MCK_ECORRUPT with the
+ * reference's message (e.g. "Error while decoding blob log header: Magic
+ * number mismatch") on a structural error. */
+int mck_blob_list_records(const void* file, uint64_t file_size,
+                          mck_blob_file_info* info, mck_blob_record* records,
+                          uint64_t cap, uint64_t* nrecords);
+
+/* Every record of a device-resident blob file image in one batch
+ * (BlobLogRecord::DecodeHeaderFrom + CheckBlobCRC, blob_log_format.cc
+ * :103-135):
+ *   write == 0: status[i] = (header CRC mismatch) | (blob CRC mismatch) << 1,
+ *               mismatch_count (optional, caller-zeroed) += records with any;
+ *   write != 0: BlobLogRecord::EncodeHeaderTo's CRC fields -- header_crc and
+ *               blob_crc are computed and stored into each record header.
+ * record_offsets: device u64 [count] (header offsets), blob_lengths: device
+ * u32 [count] (key_size + value_size). */
+int mck_blob_record_batch(int write, void* file, const uint64_t* record_offsets,
+                          const uint32_t* blob_lengths, uint32_t count,
+                          uint8_t* status, uint32_t* mismatch_count,
+                          mck_stream_t stream);
 
 /* ========================================================================= */
 /* 3. Multi-GPU / host-resident input                                       */

@@ -10,6 +10,7 @@ from . import _lib  # noqa: F401  (fails loudly if the engine is not built)
 from .checksum import *  # noqa: F401,F403
 from .checksum import __all__ as _checksum_all
 from . import sst  # noqa: F401  (whole-SST-file verification)
+from . import blob  # noqa: F401  (blob file records)
 
 __all__ = list(_checksum_all)
 __version__ = "0.1.0"

@@ -89,6 +89,13 @@ SIGNATURES = [
     ("mck_sst_decode_footer", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
     ("mck_sst_list_blocks", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
     ("mck_sst_verify_footer", ctypes.c_int, [vp, vp]),
+    ("mck_wal_plan", ctypes.c_int,
+     [vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp, ctypes.c_uint64, vp, vp, vp]),
+    ("mck_wal_write_batch", ctypes.c_int,
+     [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]),
+    ("mck_blob_list_records", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
+    ("mck_blob_record_batch", ctypes.c_int,
+     [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, vp, vp, vp]),
     ("mck_partition_spans", ctypes.c_int,
      [vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp]),
     ("mck_host_batch_checksum", ctypes.c_int,

@@ -506,3 +506,62 @@ __all__ = [
     "GetFileChecksumGenCrc32cFactory", "kStandardDbFileChecksumFuncName",
     "kUnknownFileChecksum", "kUnknownFileChecksumFuncName",
 ]
+
+
+# ---------------------------------------------------------------------------
+# device WAL writer (db/log_writer.cc:79-175 AddRecord + :263-311
+# EmitPhysicalRecord, as one group-commit batch)
+# ---------------------------------------------------------------------------
+
+class mck_wal_fragment(ctypes.Structure):
+    _fields_ = [("src_off", ctypes.c_uint64), ("dst_off", ctypes.c_uint64), ("length", ctypes.c_uint32),
+                ("type", ctypes.c_uint8), ("pad", ctypes.c_uint8), ("reserved", ctypes.c_uint16)]
+
+
+def wal_plan(src_offsets, lengths, block_offset: int = 0, recycle: bool = False):
+    """log::Writer::AddRecord's fragmentation of records (host sizes).
+    Returns (fragments ctypes array, output bytes, new block_offset)."""
+    import numpy as np
+    offs = np.ascontiguousarray(np.asarray(src_offsets, dtype=np.uint64))
+    lens = np.ascontiguousarray(np.asarray(lengths, dtype=np.uint32))
+    n = ctypes.c_uint64()
+    out_bytes = ctypes.c_uint64()
+    nbo = ctypes.c_uint32()
+    check(lib.mck_wal_plan(offs.ctypes.data, lens.ctypes.data, len(lens), block_offset, 1 if recycle else 0,
+                           None, 0, ctypes.addressof(n), ctypes.addressof(out_bytes), ctypes.addressof(nbo)),
+          "mck_wal_plan")
+    frags = (mck_wal_fragment * max(n.value, 1))()
+    check(lib.mck_wal_plan(offs.ctypes.data, lens.ctypes.data, len(lens), block_offset, 1 if recycle else 0,
+                           ctypes.addressof(frags), n.value, ctypes.addressof(n), ctypes.addressof(out_bytes),
+                           ctypes.addressof(nbo)), "mck_wal_plan")
+    return frags, n.value, out_bytes.value, nbo.value
+
+
+class WalBatchWriter:
+    """log::Writer for group commits on the device: AddRecords() appends a
+    batch of logical records (a device byte tensor + host offsets/lengths)
+    to a device-resident log image, fragmented, framed and CRC'd exactly as
+    AddRecord/EmitPhysicalRecord would."""
+
+    def __init__(self, log_number: int = 0, recycle_log_files: bool = False, block_offset: int = 0):
+        self.log_number = log_number & 0xFFFFFFFF
+        self.recycle = recycle_log_files
+        self.block_offset = block_offset
+
+    def AddRecords(self, src, src_offsets, lengths, stream=None):
+        """Returns the device uint8 tensor of the bytes the records append."""
+        torch = _torch()
+        frags, n, nbytes, nbo = wal_plan(src_offsets, lengths, self.block_offset, self.recycle)
+        dev = src.device
+        d_frags = torch.frombuffer(bytearray(bytes(frags)[:n * ctypes.sizeof(mck_wal_fragment)]),
+                                   dtype=torch.uint8).to(dev) if n else torch.empty(0, dtype=torch.uint8,
+                                                                                     device=dev)
+        crc = _empty(max(n, 1), torch.int32, dev)
+        out = torch.zeros(nbytes + 16, dtype=torch.uint8, device=dev)
+        check(lib.mck_wal_write_batch(src.data_ptr(), d_frags.data_ptr(), n, self.log_number, crc.data_ptr(),
+                                      out.data_ptr(), _stream(stream)), "mck_wal_write_batch")
+        self.block_offset = nbo
+        return out[:nbytes]
+
+
+__all__ += ["wal_plan", "WalBatchWriter", "mck_wal_fragment"]

@@ -468,6 +468,48 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, 
   return MCK_OK;
 }
 
+// ---- device WAL writer -------------------------------------------------------
+int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t nfrags, uint32_t log_number,
+                        uint32_t* crc_scratch, void* out, mck_stream_t stream) {
+  t_err[0] = 0;
+  static_assert(sizeof(mck_wal_fragment) == sizeof(WalFrag), "layout");
+  if (!nfrags) return MCK_OK;
+  if (!src || !frags || !crc_scratch || !out) {
+    set_err("src / frags / crc_scratch / out is NULL");
+    return MCK_EINVAL;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const WalFrag* f = reinterpret_cast<const WalFrag*>(frags);
+  if (int rc = launch_crc(OpWalFragCrc{static_cast<const uint8_t*>(src), f, wal_type_crcs(log_number), crc_scratch},
+                          nfrags, st))
+    return rc;
+  int ncu;
+  if (int rc = current_device(nullptr, &ncu)) return rc;
+  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (nfrags + 3) / 4);
+  hipLaunchKernelGGL(k_wal_write, dim3(grid), dim3(256), 0, st, static_cast<const uint8_t*>(src), f, nfrags,
+                     log_number, crc_scratch, static_cast<uint8_t*>(out));
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+// ---- blob log records --------------------------------------------------------
+int mck_blob_record_batch(int write, void* file, const uint64_t* record_offsets, const uint32_t* blob_lengths,
+                          uint32_t count, uint8_t* status, uint32_t* mismatch_count, mck_stream_t stream) {
+  t_err[0] = 0;
+  if (count && (!file || !record_offsets || !blob_lengths || (!write && !status))) {
+    set_err("file / record_offsets / blob_lengths / status is NULL");
+    return MCK_EINVAL;
+  }
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (write)
+    return launch_crc(OpBlobRecord<true>{static_cast<const uint8_t*>(file), record_offsets, blob_lengths, nullptr,
+                                         nullptr},
+                      count, st);
+  return launch_crc(OpBlobRecord<false>{static_cast<const uint8_t*>(file), record_offsets, blob_lengths, status,
+                                        mismatch_count},
+                    count, st);
+}
+
 // ---- long spans ------------------------------------------------------------
 uint64_t mck_crc32c_long_scratch_words(uint64_t n) {
   return (n + MCK_LONG_PIECE_BYTES - 1) / MCK_LONG_PIECE_BYTES;

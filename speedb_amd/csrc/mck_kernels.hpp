@@ -367,6 +367,146 @@ struct OpNoneBlock {
   __device__ void run(uint32_t i) const { block_epilogue<MODE>(a, i, 0u); }
 };
 
+// ===================== device WAL writer ==================================
+// Fragment CRCs: span = the fragment's payload in the source, init =
+// Value(type [+ LE32 log number]) (db/log_writer.cc:48-51, 281-298).
+struct WalFrag {  // = mck_wal_fragment
+  uint64_t src_off, dst_off;
+  uint32_t length;
+  uint8_t type, pad;
+  uint16_t reserved;
+};
+struct OpWalFragCrc {
+  const uint8_t* src;
+  const WalFrag* frags;
+  WalTypeCrcs tc;
+  uint32_t* out;
+  typedef NoPre Pre;
+  __device__ const uint8_t* base() const { return src; }
+  __device__ uint64_t off(uint32_t i) const { return frags[i].src_off; }
+  __device__ uint64_t len(uint32_t i) const { return frags[i].length; }
+  __device__ uint32_t init_crc(uint32_t i) const { return tc.v[frags[i].type & 15]; }
+  __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre& = Pre{}) const {
+    if ((threadIdx.x & 63) == 0) out[i] = crc_mask(crc);
+  }
+};
+
+// The physical record image: [pad zeros][crc LE32][len LE16][type]
+// [log number LE32 if recyclable][payload].  One wave per fragment; the
+// body is written as aligned 16-byte stores assembled from aligned source
+// dwords (v_alignbyte), the head (padding + header + the first payload
+// bytes up to a 16-byte boundary) and the tail byte-wise.
+__device__ __forceinline__ uint8_t wal_out_byte(const WalFrag& f, uint32_t crc, uint32_t log_number, uint32_t hs,
+                                                const uint8_t* src, uint64_t a) {
+  // a: output offset within [dst_off - pad, dst_off + hs + length)
+  if (a < f.dst_off) return 0;  // block trailer padding
+  const uint64_t h = a - f.dst_off;
+  if (h < 4) return (uint8_t)(crc >> (8 * h));
+  if (h < 6) return (uint8_t)(f.length >> (8 * (h - 4)));
+  if (h == 6) return f.type;
+  if (h < hs) return (uint8_t)(log_number >> (8 * (h - 7)));
+  return src[f.src_off + (h - hs)];
+}
+
+__global__ __launch_bounds__(256) void k_wal_write(const uint8_t* __restrict__ src, const WalFrag* __restrict__ frags,
+                                                   uint32_t nfrags, uint32_t log_number,
+                                                   const uint32_t* __restrict__ crcs, uint8_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t nw = gridDim.x * wpb;
+  for (uint32_t fi = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)); fi < nfrags; fi += nw) {
+    const WalFrag f = frags[fi];
+    const uint32_t crc = crcs[fi];
+    const uint32_t hs = (f.type >= 5 && f.type <= 8) || f.type == 11 ? 11u : 7u;
+    const uint64_t start = f.dst_off - f.pad;
+    const uint64_t end = f.dst_off + hs + f.length;
+    const uint64_t pay = f.dst_off + hs;              // output offset of payload byte 0
+    const uint64_t body0 = (pay + 15) & ~15ull;       // first 16-aligned chunk of payload
+    const uint64_t body1 = end & ~15ull;              // end of the last full chunk
+    // head: [start, body0) byte-wise -- or the whole record when it has no
+    // full 16-byte payload chunk
+    const uint64_t head_end = body0 < body1 ? body0 : end;
+    for (uint64_t a = start + lane; a < head_end; a += 64) out[a] = wal_out_byte(f, crc, log_number, hs, src, a);
+    if (body0 < body1) {
+      // body: 16-byte chunks; chunk c covers payload bytes [c - pay, +16) of
+      // the fragment = source bytes s = f.src_off + (c - pay) ...
+      for (uint64_t c = body0 + 16ull * lane; c < body1; c += 16ull * 64) {
+        const uint64_t s = f.src_off + (c - pay);
+        const uint64_t s4 = s & ~3ull;
+        const uint32_t sh = (uint32_t)(s & 3);
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(src + s4);
+        // aligned source dwords; with sh == 0 the fifth is not needed (and
+        // could lie past the payload's last dword): re-read the fourth
+        uint32_t x[5];
+#pragma unroll
+        for (int k = 0; k < 4; k++) x[k] = w[k];
+        x[4] = w[sh ? 4 : 3];
+        uint4 v;
+        v.x = __builtin_amdgcn_alignbyte(x[1], x[0], sh);
+        v.y = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
+        v.z = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
+        v.w = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
+        *reinterpret_cast<uint4*>(out + c) = v;
+      }
+      // tail: [body1, end) byte-wise
+      for (uint64_t a = body1 + lane; a < end; a += 64) out[a] = wal_out_byte(f, crc, log_number, hs, src, a);
+    }
+  }
+}
+
+// ===================== blob log records ===================================
+// db/blob/blob_log_format.cc:97-135 BlobLogRecord: a 32-byte header
+// [key_size u64][value_size u64][expiration u64][header_crc u32][blob_crc
+// u32], then key and value.  header_crc = Mask(Value(header[0..24))),
+// blob_crc = Mask(Extend(Value(key), value)) = Mask(Value(key || value)).
+// The CRC span is key || value; the header travels as the epilogue input.
+struct BlobPre {
+  uint4 h0, h1;  // header bytes [0, 16), [16, 32)
+};
+// crc32c::Value of the 24 header bytes on every lane (6 table steps).
+__device__ __forceinline__ uint32_t blob_header_crc(const BlobPre& e) {
+  const CrcLane L = crc_lane();
+  const uint32_t w[6] = {e.h0.x, e.h0.y, e.h0.z, e.h0.w, e.h1.x, e.h1.y};
+  uint32_t s = 0xFFFFFFFFu;
+#pragma unroll
+  for (int k = 0; k < 6; k++) s = crc_step4(s ^ w[k], L);
+  return ~s;
+}
+template <bool WRITE>
+struct OpBlobRecord {
+  const uint8_t* file;
+  const uint64_t* rec_off;   // record header offsets in the file
+  const uint32_t* blob_len;  // key_size + value_size
+  uint8_t* status;           // verify: bit 0 header CRC bad, bit 1 blob CRC bad
+  uint32_t* mismatch_count;  // verify (opt): records with any bad CRC
+  typedef BlobPre Pre;
+  __device__ const uint8_t* base() const { return file; }
+  __device__ uint64_t off(uint32_t i) const { return rec_off[i] + 32; }
+  __device__ uint64_t len(uint32_t i) const { return blob_len[i]; }
+  __device__ uint32_t init_crc(uint32_t) const { return 0u; }
+  __device__ Pre pre(uint32_t, uint64_t ptr, uint64_t) const {
+    return Pre{span_load16<false>(ptr - 32), span_load16<false>(ptr - 16)};
+  }
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre& e) const {
+    const uint32_t hcrc = crc_mask(blob_header_crc(e));
+    const uint32_t bcrc = crc_mask(crc);
+    if ((threadIdx.x & 63) != 0) return;
+    if (WRITE) {  // BlobLogRecord::EncodeHeaderTo: the two CRC fields, LE
+      uint8_t* h = const_cast<uint8_t*>(file) + rec_off[i] + 24;
+#pragma unroll
+      for (int b = 0; b < 4; b++) {
+        h[b] = (uint8_t)(hcrc >> (8 * b));
+        h[4 + b] = (uint8_t)(bcrc >> (8 * b));
+      }
+    } else {  // DecodeHeaderFrom + CheckBlobCRC
+      const uint8_t st = (uint8_t)((hcrc != e.h1.z ? 1u : 0u) | (bcrc != e.h1.w ? 2u : 0u));
+      status[i] = st;
+      if (st && mismatch_count) atomicAdd(mismatch_count, 1u);
+    }
+  }
+};
+
 // ===================== long spans: pieces + combine =======================
 // util/crc32c.cc:1221-1289 Crc32cCombine, applied to every piece of a long
 // span at once.  Pieces i were hashed by the batch kernels (v[i] = Value of

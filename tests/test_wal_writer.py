@@ -1,0 +1,69 @@
+"""Device WAL writer: the host plan fragments records
+exactly as log::Writer::AddRecord does (compared with the test-side Python
+restatement of db/log_writer.cc, tests/formats.py WalWriter), and the device
+writes the same bytes -- legacy and recyclable headers, records spanning
+blocks, empty records, block-trailer padding, an initial block offset."""
+import random
+
+import numpy as np
+import pytest
+
+from formats import WalWriter
+
+
+def _records(seed, n, big=False):
+    rnd = random.Random(seed)
+    sizes = [0, 1, 7, 11, 32761, 32762, 32768, 70000] + [rnd.choice(
+        [rnd.randrange(0, 100), rnd.randrange(0, 5000), rnd.randrange(30000, 100000 if big else 40000)])
+        for _ in range(n)]
+    rnd.shuffle(sizes)
+    return [bytes(rnd.getrandbits(8) for _ in range(s)) for s in sizes]
+
+
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_plan_matches_writer(oracle, recycle):
+    import speedb_amd as S
+    recs = _records(1, 60)
+    w = WalWriter(oracle, log_number=123, recycle=recycle)
+    # start mid-block like a log that already holds data
+    pre = bytes(32768 - 9)
+    w.add_record(pre[:32768 - 9 - (11 if recycle else 7)])
+    start = len(w.buf)
+    for r in recs:
+        w.add_record(r)
+    offs = np.cumsum([0] + [len(r) for r in recs[:-1]])
+    frags, n, nbytes, nbo = S.wal_plan(offs, [len(r) for r in recs], start % 32768, recycle)
+    assert nbytes == len(w.buf) - start
+    assert nbo == w.block_offset
+    got = [(f.dst_off + start, f.type, f.length) for f in frags[:n]]
+    assert got == [r for r in w.records if r[0] >= start]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_write_batch_bit_exact(gpu, oracle, recycle):
+    import torch
+
+    import speedb_amd as S
+    recs = _records(2, 300, big=True)
+    w = WalWriter(oracle, log_number=77, recycle=recycle)
+    w.add_record(b"x" * 1000)  # the log already holds one record
+    start = len(w.buf)
+    for r in recs:
+        w.add_record(r)
+    src = b"".join(recs)
+    offs = np.cumsum([0] + [len(r) for r in recs[:-1]])
+    dev = torch.frombuffer(bytearray(src + bytes(64)), dtype=torch.uint8).to("cuda")
+    wr = S.WalBatchWriter(log_number=77, recycle_log_files=recycle, block_offset=start)
+    out = wr.AddRecords(dev, offs, [len(r) for r in recs])
+    got, want = bytes(out.cpu().numpy().tobytes()), bytes(w.buf[start:])
+    if got != want:
+        i = next(k for k in range(min(len(got), len(want))) if got[k] != want[k])
+        fr = [r for r in w.records if r[0] <= i + start][-1]
+        raise AssertionError(f"first difference at stream offset {i + start}: fragment {fr}")
+    assert len(got) == len(want)
+    assert wr.block_offset == w.block_offset
+    # the device reader accepts every record of the full image
+    full = torch.frombuffer(bytearray(bytes(w.buf) + bytes(64)), dtype=torch.uint8).to("cuda")
+    res = S.wal_verify_batch(full, len(w.buf), 77).cpu().numpy()
+    assert (res[:, 1] == 0).all()
