@@ -675,63 +675,4 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
   }
 }
 
-// Ping-pong variant: two chunk buffers A and B, the loop unrolled by two, a
-// buffer refilled right after it was folded.  While round k is folded,
-// round k+1 is in flight; while the wave waits for round k+1, round k+2 is
-// already in flight too -- two rounds (8 KiB) per wave in the memory system
-// instead of one, and no register copies at the loop latch (a copy of the
-// prefetched chunk waits for its loads before the next prefetch is issued).
-// Units past the wave's last one re-read a valid chunk (never folded).
-template <class Op, bool FULL>
-__device__ __forceinline__ void crc_uniform_driver_pp(const Op& op, const CrcUniform& U, uint32_t count, uint8_t* lds,
-                                                      const CrcTables* __restrict__ g) {
-  CrcFill fill;
-  crc_fill_load<false>(fill, g);
-  const CrcLane L = crc_lane();
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-  const uint32_t nwaves = gridDim.x * wpb;
-  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  const int R = U.rounds;
-  // unit = (span i, round r): rounds R-1 .. 0 of span i, then span i + nwaves
-  auto adv = [&](uint32_t& i, int& r) {
-    if (--r < 0) {
-      r = R - 1;
-      i += nwaves;
-    }
-  };
-  auto load = [&](uint32_t i, int r) {
-    const uint32_t ic = i < count ? i : (wave < count ? wave : 0u);
-    return crc_load_chunk(crc_uniform_span<FULL>(base, ic, U), r, L);
-  };
-  uint32_t li = wave;  // load cursor
-  int lr = R - 1;
-  Chunk A = load(li, lr);
-  adv(li, lr);
-  Chunk B = load(li, lr);
-  adv(li, lr);
-  crc_fill_store<false>(fill, lds);
-  __syncthreads();
-  if (wave >= count) return;
-  uint32_t ci = wave;  // fold cursor
-  int cr = R - 1;
-  uint32_t s = 0;
-  for (;;) {
-    CrcSpan sp = crc_uniform_span<FULL>(base, ci, U);
-    s = crc_round(s, A, sp, cr, L);
-    if (cr == 0) op.finish(ci, crc_finish(s, sp, L));
-    adv(ci, cr);
-    if (ci >= count) break;
-    A = load(li, lr);
-    adv(li, lr);
-    sp = crc_uniform_span<FULL>(base, ci, U);
-    s = crc_round(s, B, sp, cr, L);
-    if (cr == 0) op.finish(ci, crc_finish(s, sp, L));
-    adv(ci, cr);
-    if (ci >= count) break;
-    B = load(li, lr);
-    adv(li, lr);
-  }
-}
-
 }  // namespace mck

@@ -186,11 +186,7 @@ __global__ __launch_bounds__(1024) void k_crc(Op op, uint32_t count) {
 template <class Op, bool FULL>
 __global__ __launch_bounds__(1024) void k_crc_uniform(Op op, CrcUniform U, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-#if MCK_CRC_PINGPONG
-  crc_uniform_driver_pp<Op, FULL>(op, U, count, lds, &g_crc_tables);
-#else
   crc_uniform_driver<Op, FULL>(op, U, count, lds, &g_crc_tables);
-#endif
 }
 
 // ============================ XXH3 ========================================
