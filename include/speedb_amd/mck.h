@@ -211,6 +211,34 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags,
                         uint32_t nfrags, uint32_t log_number,
                         uint32_t* crc_scratch, void* out, mck_stream_t stream);
 
+/* ---- WAL recovery: logical records ----------------- */
+
+/* Host: log::Reader::ReadRecord's reassembly (db/log_reader.cc:69-321) over a
+ * WAL image in host memory: every logical record as the list of its
+ * fragments' payloads (src_off = offset in the WAL image, dst_off = offset in
+ * one contiguous record buffer, length, type) and the records themselves as
+ * (rec_offsets[r], rec_lengths[r]) in that buffer.  Physical records are
+ * walked as ReadPhysicalRecord does (32 KiB blocks, trailers, legacy and
+ * recyclable headers, kZeroType padding); a bad length drops the rest of its
+ * block, a record of another log (recycled file) or a truncated header ends
+ * the walk; partial records are dropped as ReadRecord drops them.  CRCs are
+ * NOT checked here (mck_wal_verify_batch does that on the device).  Any
+ * output pointer may be NULL to query counts; *records_bytes = size of the
+ * contiguous buffer. */
+int mck_wal_list_records(const void* wal, uint64_t nbytes, uint32_t log_number,
+                         mck_wal_fragment* frags, uint64_t frag_cap,
+                         uint64_t* nfrags, uint64_t* rec_offsets,
+                         uint32_t* rec_lengths, uint64_t rec_cap,
+                         uint64_t* nrecords, uint64_t* records_bytes);
+
+/* Device: copy every fragment's payload (wal + src_off, length bytes) to
+ * out + dst_off -- reassembles the logical records of mck_wal_list_records
+ * into one buffer, whose records' XXH3_64bits (ReadRecord's record_checksum,
+ * db/log_reader.cc:107-158) are then one mck_xxh3_64_batch.  out: 16-byte
+ * aligned device buffer. */
+int mck_wal_gather_batch(const void* wal, const mck_wal_fragment* frags,
+                         uint32_t nfrags, void* out, mck_stream_t stream);
+
 /* Per-32KiB-block result of a WAL verify scan (db/log_reader.cc:450-584
  * ReadPhysicalRecord, checksum on).  Records of block b are walked in order;
  * the walk stops at the first record that the reference would not return. */

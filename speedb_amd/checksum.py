@@ -564,4 +564,47 @@ class WalBatchWriter:
         return out[:nbytes]
 
 
-__all__ += ["wal_plan", "WalBatchWriter", "mck_wal_fragment"]
+def wal_list_records(wal: bytes, log_number: int = 0):
+    """log::Reader::ReadRecord's reassembly plan of a host WAL image:
+    (fragments ctypes array, nfrags, record offsets, record lengths,
+    buffer bytes)."""
+    import numpy as np
+    buf = bytes(wal)
+    nf, nr, nb = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    check(lib.mck_wal_list_records(buf, len(buf), log_number & 0xFFFFFFFF, None, 0, ctypes.addressof(nf),
+                                   None, None, 0, ctypes.addressof(nr), ctypes.addressof(nb)),
+          "mck_wal_list_records")
+    frags = (mck_wal_fragment * max(nf.value, 1))()
+    offs = np.zeros(max(nr.value, 1), dtype=np.uint64)
+    lens = np.zeros(max(nr.value, 1), dtype=np.uint32)
+    check(lib.mck_wal_list_records(buf, len(buf), log_number & 0xFFFFFFFF, ctypes.addressof(frags), nf.value,
+                                   ctypes.addressof(nf), offs.ctypes.data, lens.ctypes.data, nr.value,
+                                   ctypes.addressof(nr), ctypes.addressof(nb)), "mck_wal_list_records")
+    return frags, nf.value, offs[:nr.value], lens[:nr.value], nb.value
+
+
+def WalReadRecords(wal: bytes, log_number: int = 0, device=None, stream=None):
+    """Recovery on the device: every logical record of a WAL image
+    reassembled into one device buffer (mck_wal_gather_batch) and its
+    XXH3_64bits record checksum (ReadRecord's record_checksum) in one batch;
+    the physical records' CRCs per 32 KiB block (mck_wal_verify_batch).
+    Returns (records uint8 tensor, offsets, lengths, xxh3 uint64 numpy,
+    per-block verify results)."""
+    import numpy as np
+    torch = _torch()
+    dev = torch.device("cuda") if device is None else device
+    frags, nf, offs, lens, nbytes = wal_list_records(wal, log_number)
+    img = torch.frombuffer(bytearray(bytes(wal) + bytes(64)), dtype=torch.uint8).to(dev)
+    out = torch.zeros(nbytes + 64, dtype=torch.uint8, device=dev)
+    d_frags = torch.frombuffer(bytearray(bytes(frags)[:nf * ctypes.sizeof(mck_wal_fragment)] or b"\0"),
+                               dtype=torch.uint8).to(dev)
+    check(lib.mck_wal_gather_batch(img.data_ptr(), d_frags.data_ptr(), nf, out.data_ptr(), _stream(stream)),
+          "mck_wal_gather_batch")
+    sp = Spans(out, len(offs), offsets=torch.from_numpy(offs.astype(np.int64)).to(dev),
+               lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
+    x3 = xxh3_64_batch(sp, stream=stream).cpu().numpy().view(np.uint64) if len(offs) else np.zeros(0, np.uint64)
+    blocks = wal_verify_batch(img, len(wal), log_number, stream=stream) if len(wal) else None
+    return out[:nbytes], offs, lens, x3, blocks
+
+
+__all__ += ["wal_plan", "WalBatchWriter", "mck_wal_fragment", "wal_list_records", "WalReadRecords"]

@@ -486,8 +486,26 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   int ncu;
   if (int rc = current_device(nullptr, &ncu)) return rc;
   const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (nfrags + 3) / 4);
-  hipLaunchKernelGGL(k_wal_write, dim3(grid), dim3(256), 0, st, static_cast<const uint8_t*>(src), f, nfrags,
+  hipLaunchKernelGGL(k_wal_copy<false>, dim3(grid), dim3(256), 0, st, static_cast<const uint8_t*>(src), f, nfrags,
                      log_number, crc_scratch, static_cast<uint8_t*>(out));
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+int mck_wal_gather_batch(const void* wal, const mck_wal_fragment* frags, uint32_t nfrags, void* out,
+                         mck_stream_t stream) {
+  t_err[0] = 0;
+  if (!nfrags) return MCK_OK;
+  if (!wal || !frags || !out) {
+    set_err("wal / frags / out is NULL");
+    return MCK_EINVAL;
+  }
+  int ncu;
+  if (int rc = current_device(nullptr, &ncu)) return rc;
+  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (nfrags + 3) / 4);
+  hipLaunchKernelGGL(k_wal_copy<true>, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(wal), reinterpret_cast<const WalFrag*>(frags), nfrags, 0u,
+                     static_cast<const uint32_t*>(nullptr), static_cast<uint8_t*>(out));
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }

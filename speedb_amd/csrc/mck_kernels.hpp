@@ -409,17 +409,21 @@ __device__ __forceinline__ uint8_t wal_out_byte(const WalFrag& f, uint32_t crc, 
   return src[f.src_off + (h - hs)];
 }
 
-__global__ __launch_bounds__(256) void k_wal_write(const uint8_t* __restrict__ src, const WalFrag* __restrict__ frags,
-                                                   uint32_t nfrags, uint32_t log_number,
-                                                   const uint32_t* __restrict__ crcs, uint8_t* __restrict__ out) {
+// GATHER: the reverse direction for recovery -- copy each fragment's
+// payload (no header, no padding) to out + dst_off, reassembling logical
+// records (mck_wal_gather_batch).
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_wal_copy(const uint8_t* __restrict__ src, const WalFrag* __restrict__ frags,
+                                                  uint32_t nfrags, uint32_t log_number,
+                                                  const uint32_t* __restrict__ crcs, uint8_t* __restrict__ out) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t nw = gridDim.x * wpb;
   for (uint32_t fi = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)); fi < nfrags; fi += nw) {
     const WalFrag f = frags[fi];
-    const uint32_t crc = crcs[fi];
-    const uint32_t hs = (f.type >= 5 && f.type <= 8) || f.type == 11 ? 11u : 7u;
-    const uint64_t start = f.dst_off - f.pad;
+    const uint32_t crc = GATHER ? 0u : crcs[fi];
+    const uint32_t hs = GATHER ? 0u : (f.type >= 5 && f.type <= 8) || f.type == 11 ? 11u : 7u;
+    const uint64_t start = f.dst_off - (GATHER ? 0u : f.pad);
     const uint64_t end = f.dst_off + hs + f.length;
     const uint64_t pay = f.dst_off + hs;              // output offset of payload byte 0
     const uint64_t body0 = (pay + 15) & ~15ull;       // first 16-aligned chunk of payload
@@ -427,7 +431,8 @@ __global__ __launch_bounds__(256) void k_wal_write(const uint8_t* __restrict__ s
     // head: [start, body0) byte-wise -- or the whole record when it has no
     // full 16-byte payload chunk
     const uint64_t head_end = body0 < body1 ? body0 : end;
-    for (uint64_t a = start + lane; a < head_end; a += 64) out[a] = wal_out_byte(f, crc, log_number, hs, src, a);
+    for (uint64_t a = start + lane; a < head_end; a += 64)
+      out[a] = GATHER ? src[f.src_off + (a - pay)] : wal_out_byte(f, crc, log_number, hs, src, a);
     if (body0 < body1) {
       // body: 16-byte chunks; chunk c covers payload bytes [c - pay, +16) of
       // the fragment = source bytes s = f.src_off + (c - pay) ...
@@ -450,7 +455,8 @@ __global__ __launch_bounds__(256) void k_wal_write(const uint8_t* __restrict__ s
         *reinterpret_cast<uint4*>(out + c) = v;
       }
       // tail: [body1, end) byte-wise
-      for (uint64_t a = body1 + lane; a < end; a += 64) out[a] = wal_out_byte(f, crc, log_number, hs, src, a);
+      for (uint64_t a = body1 + lane; a < end; a += 64)
+        out[a] = GATHER ? src[f.src_off + (a - pay)] : wal_out_byte(f, crc, log_number, hs, src, a);
     }
   }
 }

@@ -67,3 +67,61 @@ def test_wal_write_batch_bit_exact(gpu, oracle, recycle):
     full = torch.frombuffer(bytearray(bytes(w.buf) + bytes(64)), dtype=torch.uint8).to("cuda")
     res = S.wal_verify_batch(full, len(w.buf), 77).cpu().numpy()
     assert (res[:, 1] == 0).all()
+
+
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_list_records_reassembly_plan(oracle, recycle):
+    """log::Reader::ReadRecord's reassembly on the host: the logical records
+    the writer produced, in order, with their fragments."""
+    import speedb_amd as S
+    recs = _records(3, 80)
+    w = WalWriter(oracle, log_number=9, recycle=recycle)
+    for r in recs:
+        w.add_record(r)
+    frags, nf, offs, lens, nbytes = S.wal_list_records(bytes(w.buf), 9)
+    assert list(lens) == [len(r) for r in recs]
+    assert nbytes == sum(len(r) for r in recs)
+    assert nf == len(w.records)
+    img = bytes(w.buf)
+    buf = bytearray(nbytes)
+    for f in frags[:nf]:
+        buf[f.dst_off:f.dst_off + f.length] = img[f.src_off:f.src_off + f.length]
+    for r, o, n in zip(recs, offs, lens):
+        assert bytes(buf[o:o + n]) == r
+    if recycle:  # a recycled log's records of another log number end the walk
+        _, _, offs2, _, _ = S.wal_list_records(img, 10)
+        assert len(offs2) == 0
+
+
+def test_wal_list_records_drops_partial(oracle):
+    """A record whose Last fragment is missing (the WAL ends mid-record) is
+    dropped; a bad length drops the rest of its block."""
+    import speedb_amd as S
+    recs = [b"a" * 100, b"b" * 70000, b"c" * 50]
+    w = WalWriter(oracle, log_number=1)
+    for r in recs:
+        w.add_record(r)
+    img = bytes(w.buf)
+    # cut inside the second record's Middle fragment: only record 0 survives
+    cut = w.records[2][0] + 100
+    _, _, offs, lens, _ = S.wal_list_records(img[:cut], 1)
+    assert list(lens) == [100]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_read_records_xxh3(gpu, oracle, recycle):
+    """Recovery on the device: reassembled records bit-exact, their
+    XXH3_64bits (record_checksum) equal to the oracle's, every block's CRCs
+    verified."""
+    import speedb_amd as S
+    recs = _records(4, 200, big=True)
+    w = WalWriter(oracle, log_number=5, recycle=recycle)
+    for r in recs:
+        w.add_record(r)
+    out, offs, lens, x3, blocks = S.WalReadRecords(bytes(w.buf), 5)
+    host = bytes(out.cpu().numpy().tobytes())
+    for r, o, n, h in zip(recs, offs, lens, x3):
+        assert host[o:o + n] == r
+        assert int(h) == oracle.XXH3(r)
+    assert (blocks.cpu().numpy()[:, 1] == 0).all()
