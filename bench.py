@@ -20,6 +20,11 @@ Default workload (the headline, BASELINE.json configs[1]): CRC32C over
                        Crc32cCombine fold; at N > 1 each rank hashes its
                        contiguous slice and the ranks' (crc, length) pairs
                        are all-gathered and folded (8 bytes per rank)
+  walwrite (8f row 3)  device WAL writer: a group commit of 2M records of
+                       1000-1100 B (README 1 KB values) fragmented, framed
+                       and CRC'd into the log byte stream (mck_wal_write_batch)
+  blob     (8f row 3)  blob file verify: 1M records (16 B key, 4 KiB value),
+                       header + blob CRC of every record (mck_blob_record_batch)
   kv       (row a12)   per-KV protection of memtable inserts, README shape
                        (16 B key, 1000 B value): ProtectKVO(...).ProtectS(seq)
 
@@ -59,12 +64,14 @@ def parse():
     # 0.77 -> 0.90 -> 0.76 ms per launch at 1M x 4 KiB); the default warmup
     # covers that transient
     p.add_argument("--warmup", type=int, default=100)
-    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file"], default="crc32c")
+    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file", "walwrite", "blob"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
     p.add_argument("--sst-bytes", type=int, default=1 << 30, help="per SST image (sst); 2 images")
     p.add_argument("--wal-blocks", type=int, default=1 << 18, help="32 KiB blocks per GPU (wal)")
     p.add_argument("--file-bytes", type=int, default=4 << 30, help="file image bytes per GPU (file)")
+    p.add_argument("--wal-records", type=int, default=2 << 20, help="logical records per GPU (walwrite)")
+    p.add_argument("--blob-records", type=int, default=1 << 20, help="blob records per GPU (blob)")
     p.add_argument("--kvs", type=int, default=1 << 22, help="KVs per GPU (kv)")
     p.add_argument("--host-bytes", type=int, default=4 << 30, help="pinned source bytes (host)")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -253,6 +260,68 @@ def make_workload(args, dev, rank, world):
                 acc = S.crc32c.Crc32cCombine(acc, v, ln)
                 left -= ln
             return acc == int(out.cpu().numpy().view(np.uint32)[0])
+        w.check = check
+    elif args.workload == "walwrite":
+        rng = np.random.default_rng(600 + rank)
+        lens = rng.integers(1000, 1101, size=args.wal_records).astype(np.uint32)
+        offs = np.zeros(len(lens), dtype=np.uint64)
+        offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        src = W.rand_bytes(int(lens.sum()) + 64, dev, 601 + rank)
+        frags, nf, nbytes, _ = S.wal_plan(offs, lens, 0, False)
+        d_frags = torch.frombuffer(bytearray(bytes(frags)), dtype=torch.uint8).to(dev)
+        crc = torch.empty(nf, dtype=torch.int32, device=dev)
+        out = torch.zeros(nbytes + 64, dtype=torch.uint8, device=dev)
+        from speedb_amd import _lib
+
+        def step():
+            _lib.check(_lib.lib.mck_wal_write_batch(src.data_ptr(), d_frags.data_ptr(), nf, 7, crc.data_ptr(),
+                                                    out.data_ptr(), stream.cuda_stream), "mck_wal_write_batch")
+        w.step = step
+        w.launches = 2
+        w.kernel = "mck::k_crc<mck::OpWalFragCrc> + mck::k_wal_copy<false>"
+        w.span_bytes = int(lens.sum())
+        # per launch (avg of the two): CRC reads the payload + 24 B descriptor
+        # + 4 B out per fragment; the writer reads the payload + descriptor +
+        # crc and writes the stream
+        w.alg_bytes = (2 * int(lens.sum()) + nbytes + nf * (24 + 4 + 24 + 4)) / 2
+        w.desc = (f"device WAL writer: group commit of {len(lens)} records of 1000-1100 B per GPU "
+                  f"(README 1 KB values) -> {nf} physical records, {nbytes} B of log stream "
+                  "(log::Writer::AddRecord + EmitPhysicalRecord, SURVEY.md 8f row 3)")
+        w.cfg = {"records_per_gpu": len(lens), "fragments": nf, "stream_bytes": nbytes}
+
+        def check():
+            # the device's log stream walks back to the same records, and
+            # every physical record's CRC verifies on the device reader
+            step()
+            res = S.wal_verify_batch(out, nbytes, 7).cpu().numpy()
+            return bool((res[:, 1] == 0).all() and int(res[:, 0].sum()) == nf)
+        w.check = check
+    elif args.workload == "blob":
+        n, kb, vb = args.blob_records, 16, 4096
+        rec = 32 + kb + vb
+        nbytes = 30 + n * rec
+        img = W.rand_bytes(nbytes + 64, dev, 700 + rank)
+        recs = img[30:30 + n * rec].view(n, rec)
+        recs[:, 0:8] = torch.tensor(list(kb.to_bytes(8, "little")), dtype=torch.uint8, device=dev)
+        recs[:, 8:16] = torch.tensor(list(vb.to_bytes(8, "little")), dtype=torch.uint8, device=dev)
+        offs = 30 + torch.arange(n, dtype=torch.int64, device=dev) * rec
+        lens = torch.full((n,), kb + vb, dtype=torch.int32, device=dev)
+        S.blob.WriteRecordCrcs(img, offs, lens)  # BlobLogRecord::EncodeHeaderTo on the device
+        status = torch.empty(n, dtype=torch.uint8, device=dev)
+
+        def step():
+            S.blob.record_batch(False, img, offs, lens, status=status, stream=stream)
+        w.step = step
+        w.kernel = "mck::k_crc<mck::OpBlobRecord<false> >"
+        w.span_bytes = n * rec
+        w.alg_bytes = n * (rec + 8 + 4 + 1)
+        w.desc = (f"blob file verify: {n} records per GPU ({kb} B key, {vb} B value), header CRC + blob CRC "
+                  "of every record (BlobLogRecord::DecodeHeaderFrom + CheckBlobCRC, SURVEY.md 8f row 3)")
+        w.cfg = {"records_per_gpu": n, "key_bytes": kb, "value_bytes": vb}
+
+        def check():
+            step()
+            return int(status.sum().item()) == 0
         w.check = check
     elif args.workload == "kv":
         count, kb, vb = args.kvs, 16, 1000

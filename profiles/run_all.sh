@@ -5,7 +5,7 @@
 set -euo pipefail
 tag=${1:-run}
 shift || true
-wls=${WORKLOADS:-"crc32c xxh3 sst wal file kv host"}
+wls=${WORKLOADS:-"crc32c xxh3 sst wal file kv walwrite blob host"}
 mkdir -p gpurun_out/bench_$tag
 for wl in $wls; do
   cpu=0
