@@ -271,10 +271,12 @@ __global__ __launch_bounds__(256) void k_xph3(Op op, uint32_t count, uint64_t se
 struct OpXpValue {
   SpanSrc s;
   uint64_t* out;
+  typedef NoPre Pre;
   __device__ const uint8_t* base() const { return s.base; }
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t hlen(uint32_t i) const { return s.len(i); }
-  __device__ void finish(uint32_t i, uint64_t h) const { out[i] = h; }
+  __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
+  __device__ void finish(uint32_t i, uint64_t h, const Pre& = Pre{}) const { out[i] = h; }
 };
 
 // db/kv_checksum.h:84-88 field seeds
@@ -288,6 +290,37 @@ constexpr uint64_t kSeedK = 0, kSeedV = 0xD28AAD72F49BD50Bull, kSeedO = 0xA5155A
 //   (:456), 3 ProtectKVO.ProtectC (:432)
 // VERIFY: ProtectionInfo::Verify(len, stored) (:103-121): the low
 // `prot_bytes` bytes of the value against stored[i*prot_bytes ..].
+// The row driver issues pre() with the value's loads, so the key bytes (up
+// to 16: the first and last 8), op type, seqno / CF id and stored bytes are
+// in registers when the value's hash completes (no dependent loads behind
+// the next segment's); keys longer than 16 bytes are read in finish().
+__device__ const uint64_t g_zero16[2] = {0, 0};
+struct KvPre {
+  // len >= 8: key bytes [0, 8) and [len - 8, len); len 1..7: the aligned
+  // qwords holding the first and the last key byte (no read leaves the
+  // pages the key occupies), joined in finish()
+  uint64_t k0, k1;
+  uint64_t klen;
+  uint32_t sh;  // len 1..7: key start & 7
+  uint64_t extra;
+  uint64_t stored;  // verify: the stored protection bytes, LE
+  uint32_t op;
+};
+// XXPH3 of a key of len <= 16 from its first and last 8 bytes
+// (xxph3_short's 0 / 1-3 / 4-8 / 9-16 classes, util/xxph3.h:1390-1445)
+__device__ __forceinline__ uint64_t xxph3_le16(uint64_t a, uint64_t b, uint64_t len, uint64_t seed) {
+  if (len > 8) {
+    const uint64_t lo = a ^ (sec64(0) + seed), hi = b ^ (sec64(8) - seed);
+    return xxph3_avalanche(len + (lo + hi) + mul128_fold64(lo, hi));
+  }
+  if (len >= 4) return xxph3_4to8((uint32_t)a, (uint32_t)(a >> (8 * (len - 4))), len, seed);
+  if (len) {
+    return xxph3_1to3((uint32_t)(a & 0xFF), (uint32_t)((a >> (8 * (len >> 1))) & 0xFF),
+                      (uint32_t)((a >> (8 * (len - 1))) & 0xFF), len, seed);
+  }
+  return mul128_fold64(seed + sec64(0), P64_2);
+}
+typedef __attribute__((address_space(1))) const uint64_t gbl_u64u_t;
 template <bool VERIFY>
 struct OpKvProtect {
   SpanSrc keys, values;
@@ -299,27 +332,50 @@ struct OpKvProtect {
   uint32_t prot_bytes;
   uint8_t* mismatch;
   uint32_t* mismatch_count;
+  typedef KvPre Pre;
   __device__ const uint8_t* base() const { return values.base; }
   __device__ uint64_t off(uint32_t i) const { return values.off(i); }
   __device__ uint64_t hlen(uint32_t i) const { return values.len(i); }
-  __device__ void finish(uint32_t i, uint64_t hv) const {
-    uint64_t v = hv ^ xxph3_any(keys.ptr(i), keys.len(i), kSeedK);
-    if (kind >= 1) v ^= xxph3_u8(ops ? ops[i] : 0u, kSeedO);
-    if (kind == 2) v ^= xxph3_u64(extras[i], kSeedS);
-    if (kind == 3) v ^= xxph3_u32((uint32_t)extras[i], kSeedC);
+  __device__ Pre pre(uint32_t i, uint64_t, uint64_t) const {
+    KvPre e;
+    e.klen = keys.len(i);
+    const uint64_t kp = reinterpret_cast<uint64_t>(keys.ptr(i));
+    // an empty key reads nothing of its own: a zero word instead
+    const uint64_t z = reinterpret_cast<uint64_t>(&g_zero16[0]);
+    const bool wide = e.klen >= 8;
+    const uint64_t a0 = wide ? kp : e.klen ? kp & ~7ull : z;
+    const uint64_t a1 = wide ? kp + e.klen - 8 : e.klen ? (kp + e.klen - 1) & ~7ull : z;
+    e.k0 = *reinterpret_cast<gbl_u64u_t*>(a0);  // any byte alignment (unaligned global loads)
+    e.k1 = *reinterpret_cast<gbl_u64u_t*>(a1);
+    e.sh = (uint32_t)(kp & 7);
+    e.op = ops ? *reinterpret_cast<gbl_u8_t*>(reinterpret_cast<uint64_t>(ops + i)) : 0u;
+    e.extra = kind >= 2 ? *reinterpret_cast<gbl_u64_t*>(reinterpret_cast<uint64_t>(extras + i)) : 0;
+    e.stored = 0;
+    if (VERIFY) {
+      const uint64_t st = reinterpret_cast<uint64_t>(stored) + (uint64_t)i * prot_bytes;
+      for (uint32_t b = 0; b < prot_bytes; b++) e.stored |= (uint64_t)*reinterpret_cast<gbl_u8_t*>(st + b) << (8 * b);
+    }
+    return e;
+  }
+  __device__ void finish(uint32_t i, uint64_t hv, const Pre& e) const {
+    const uint64_t k0 = e.klen >= 8 || e.sh == 0 ? e.k0 : (e.k0 >> (8 * e.sh)) | (e.k1 << (64 - 8 * e.sh));
+    uint64_t v = hv ^ (e.klen <= 16 ? xxph3_le16(k0, e.k1, e.klen, kSeedK)
+                                    : xxph3_any(keys.ptr(i), e.klen, kSeedK));
+    if (kind >= 1) v ^= xxph3_u8(e.op, kSeedO);
+    if (kind == 2) v ^= xxph3_u64(e.extra, kSeedS);
+    if (kind == 3) v ^= xxph3_u32((uint32_t)e.extra, kSeedC);
     if (!VERIFY) {
       out[i] = v;
       return;
     }
-    const uint8_t* st = stored + (uint64_t)i * prot_bytes;
-    uint64_t sv = 0;
-    for (uint32_t b = 0; b < prot_bytes; b++) sv |= (uint64_t)st[b] << (8 * b);
+    const uint64_t sv = e.stored;
     const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
     const bool bad = sv != (v & keep);
     mismatch[i] = bad;
     if (out) out[i] = v;
     if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
   }
+  __device__ void finish(uint32_t i, uint64_t hv) const { finish(i, hv, pre(i, 0, 0)); }
 };
 
 // ===================== legacy XXH32 / XXH64 ===============================

@@ -396,6 +396,8 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
       d[k] = gload16u(ok[k] ? seg + 64 * st + 16 * X.q : rs.ptr);
     }
     const uint4 dl = gload16u(act ? rs.ptr + rs.len - 64 + 16 * X.q : rs.ptr);
+    // the span's epilogue inputs travel with its data (see BlockPre / KvPre)
+    const typename Op::Pre e = op.pre(rs.i, rs.ptr, rs.len);
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -419,7 +421,7 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
       }
       const uint64_t m = quad_sum(mul128_fold64(a0 ^ X.km0, a1 ^ X.km1));
       const uint64_t h = PREVIEW ? xxph3_avalanche(rs.len * P64_1 + m) : xxh3_avalanche(rs.len * P64_1 + m);
-      if (X.j == 0) op.finish(rs.i, h);
+      if (X.j == 0) op.finish(rs.i, h, e);
       act = x3_next_long<Op, PREVIEW>(op, rs.i + stride, count, stride, X, rs);
       a0 = X.i0;
       a1 = X.i1;

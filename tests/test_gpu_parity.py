@@ -418,6 +418,28 @@ def test_kv_protect_batch(gpu, oracle, golden):
             assert got[i] == want, (mode, i, kl[i], vl[i])
 
 
+def test_kv_protect_key_classes(gpu, oracle):
+    """Keys of every length 0..40 (the 0 / 1-3 / 4-8 / 9-16 / 17+ XXPH3
+    classes; keys <= 16 bytes are hashed from the two prefetched words) at
+    every byte alignment."""
+    import speedb_amd as S
+    torch = gpu
+    klen = [n for n in range(41) for _ in range(8)]
+    vlen = [(37 * i) % 1500 for i in range(len(klen))]
+    kh, kd, ko, _ = make_batch(torch, 77, klen)
+    vh, vd, vo, _ = make_batch(torch, 78, vlen)
+    ops = [(5 * i) % 256 for i in range(len(klen))]
+    ex = [(0x9E3779B97F4A7C15 * (i + 1)) & (2 ** 64 - 1) for i in range(len(klen))]
+    ks, vs = spans(torch, S, kd, ko, klen), spans(torch, S, vd, vo, vlen)
+    dops = torch.tensor(ops, dtype=torch.uint8, device="cuda")
+    dex = torch.tensor(np.array(ex, dtype=np.uint64).view(np.int64), device="cuda")
+    for mode in range(4):
+        got = u64(S.kv_protect_batch(mode, ks, vs, dops, dex))
+        for i in range(len(klen)):
+            want = oracle.KvProtect(mode, kh[ko[i]:ko[i] + klen[i]], vh[vo[i]:vo[i] + vlen[i]], ops[i], ex[i])
+            assert got[i] == want, (mode, i, klen[i], vlen[i])
+
+
 @pytest.mark.parametrize("prot_bytes", [1, 2, 4, 8])
 def test_kv_protect_verify(gpu, oracle, prot_bytes):
     """ProtectionInfo::Verify(len, ptr): stored = Encode(len) of the right
