@@ -32,6 +32,9 @@ def main():
     ap.add_argument("--kind", default="crc32c", help="crc32c | xxh3 | wal")
     ap.add_argument("--mixed", action="store_true",
                     help="compaction-shaped 4/16/64 KiB (+0..255) spans at odd offsets")
+    ap.add_argument("--align", type=int, default=1,
+                    help="--mixed: round every span start up to this many bytes")
+    ap.add_argument("--nojitter", action="store_true", help="--mixed: no +0..255 length jitter")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
@@ -50,6 +53,9 @@ def main():
         total = a.blocks * a.block
         while pos < total:
             n = rnd.choice([4096] * 6 + [16384] * 3 + [65536]) + rnd.randrange(0, 256)
+            if a.nojitter:
+                n &= ~255
+            pos = (pos + a.align - 1) // a.align * a.align
             offs.append(pos)
             lens.append(n)
             pos += n + 5

@@ -291,6 +291,50 @@ __device__ __forceinline__ uint64_t xxh3_scramble(uint64_t a, uint64_t k) {
 // 16-byte global load at any byte address (full rate at 4-byte alignment)
 __device__ __forceinline__ uint4 gload16u(uint64_t addr) { return span_load16<true>(addr); }
 
+// ---- byte-misaligned spans -------------------------------------------------
+// A 16-byte load at a byte-misaligned address runs far below rate (SST-shaped
+// mix, XXH3: 4.27 TB/s with block starts at any byte, 5.24 at 4-byte-aligned
+// starts; uniform 4097-byte stride 3.92 vs 4112-byte 5.13).  So every lane
+// loads DWORD-aligned: for the window [a, a + 16) with s = a & 3 (s = 4 when
+// a is dword-aligned), U = the 16 bytes at a - s + 4 and D0 = the dword at
+// a - s, which is the previous window's U.w -- the neighbouring lane's, taken
+// with DPP -- or, at the start of a contiguous run, one extra dword load.
+// Then window dword d = bytes s..s+3 of (U[d] : U[d-1]) (v_perm_b32).  Every
+// address read lies in the dwords that hold the window's bytes.
+typedef __attribute__((address_space(1))) const uint32_t gbl_u32c_t;
+__device__ __forceinline__ uint32_t gload4(uint64_t addr) { return *reinterpret_cast<gbl_u32c_t*>(addr); }
+__device__ __forceinline__ uint32_t rd_shift(uint64_t ptr) {
+  const uint32_t b = (uint32_t)ptr & 3u;
+  return b ? b : 4u;
+}
+__device__ __forceinline__ uint32_t rd_sel(uint32_t s) { return 0x03020100u + s * 0x01010101u; }
+__device__ __forceinline__ uint64_t floor4(uint64_t a) { return a & ~3ull; }
+__device__ __forceinline__ uint4 rd_fix(const uint4& u, uint32_t d0, uint32_t sel) {
+  return make_uint4(__builtin_amdgcn_perm(u.x, d0, sel), __builtin_amdgcn_perm(u.y, u.x, sel),
+                    __builtin_amdgcn_perm(u.z, u.y, sel), __builtin_amdgcn_perm(u.w, u.z, sel));
+}
+// (take DPP results into a variable before any ?: -- clang lowers ?: with
+// call operands to branches, and the move would then read masked lanes)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+constexpr int kDppRowRor1 = 0x121;   // lane j of a row <- lane j - 1 (mod 16)
+constexpr int kDppWaveShr1 = 0x138;  // lane l <- lane l - 1
+constexpr int kDppQuadShr1 = 0x90;   // quad_perm [0,0,1,2]: lane q <- lane q - 1
+
+// The row layout (lane j of a 16-lane row reads bytes 16 j of each 256-byte
+// chunk k = 0..3 of a 1 KiB segment): previous dword of window (k, j) is
+// the U.w of (k, j - 1), of (k - 1, 15) for j = 0, and e0 (the dword before
+// the segment) for (0, 0).
+__device__ __forceinline__ void rd_fix_row(uint4 (&d)[4], uint32_t e0, int j, uint32_t sel) {
+  uint32_t r[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) r[k] = dpp32<kDppRowRor1>(d[k].w);
+#pragma unroll
+  for (int k = 0; k < 4; k++) d[k] = rd_fix(d[k], j ? r[k] : k ? r[k - 1] : e0, sel);
+}
+
 // Per-lane constants of the row layout.
 struct X3Row {
   uint64_t k0[4], k1[4];  // stripe secrets for accumulators 2q, 2q+1 of stripe st4+4k
@@ -387,17 +431,28 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
     // the segment, or the row is idle), so they are counted and in flight
     const uint64_t seg = rs.ptr + 1024ull * rs.g;
     const bool full = rs.g < rs.nb;
+    // dword-aligned loads (see rd_fix); lanes without work read the span's
+    // first dwords
+    const uint32_t sh = rd_shift(rs.ptr), sel = rd_sel(sh);
+    const uint64_t idle = floor4(rs.ptr);
     uint4 d[4];
     bool ok[4];
 #pragma unroll
     for (int k = 0; k < 4; k++) {
       const uint32_t st = (uint32_t)(X.st4 + 4 * k);
       ok[k] = act && (full || st < rs.nst);
-      d[k] = gload16u(ok[k] ? seg + 64 * st + 16 * X.q : rs.ptr);
+      d[k] = gload16u(ok[k] ? seg + 64 * st + 16 * X.q - sh + 4 : idle);
     }
-    const uint4 dl = gload16u(act ? rs.ptr + rs.len - 64 + 16 * X.q : rs.ptr);
+    const uint64_t lst = rs.ptr + rs.len - 64;  // last stripe: its own byte offset
+    const uint32_t shl = rd_shift(lst);
+    uint4 dl = gload16u(act ? lst + 16 * X.q - shl + 4 : idle);
+    const uint32_t e0 = gload4(act && seg - sh >= idle ? seg - sh : idle);
+    const uint32_t el = gload4(act ? lst - shl : idle);
     // the span's epilogue inputs travel with its data (see BlockPre / KvPre)
     const typename Op::Pre e = op.pre(rs.i, rs.ptr, rs.len);
+    rd_fix_row(d, e0, X.j, sel);
+    const uint32_t pl = dpp32<kDppQuadShr1>(dl.w);  // unconditional: see x3w_fold
+    dl = rd_fix(dl, X.q ? pl : el, rd_sel(shl));
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
@@ -504,33 +559,45 @@ struct X3WLoads {
   uint4 d[4];  // round part: stripes st4 + 4m of segment 4k + row, pair q
   uint4 v;     // lone partial segment: stripe lane / 4, pair q
   uint4 dl;    // last stripe (len - 64), pair q
+  uint32_t e0, ev, el;  // the dwords before the row's segment, the lone segment, the last stripe
 };
 __device__ __forceinline__ bool x3w_ok(const X3WSpan& sp, uint32_t k, uint32_t g, uint32_t st) {
   return k < sp.rounds && (g < sp.nb || (g == sp.nb && st < sp.nst));
 }
+// (dword-aligned loads, realigned in x3w_fold: see rd_fix; loads without
+// work read the span's first dwords)
 __device__ __forceinline__ X3WLoads x3w_load(const X3WSpan& sp, uint32_t k, const X3Row& X) {
   X3WLoads L;
   const uint32_t g = 4 * k + X.row;
   const uint64_t seg = sp.ptr + 1024ull * g;
+  const uint32_t sh = rd_shift(sp.ptr);
+  const uint64_t idle = floor4(sp.ptr);
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const uint32_t st = (uint32_t)(X.st4 + 4 * m);
-    L.d[m] = gload16u(x3w_ok(sp, k, g, st) ? seg + 64 * st + 16 * X.q : sp.ptr);
+    L.d[m] = gload16u(x3w_ok(sp, k, g, st) ? seg + 64 * st + 16 * X.q - sh + 4 : idle);
   }
   const bool last = k + 1 == sp.units;
   const bool okl = last && sp.lone && (uint32_t)(X.lane >> 2) < sp.nst;
-  L.v = gload16u(okl ? sp.ptr + 1024ull * sp.nb + 64 * (X.lane >> 2) + 16 * X.q : sp.ptr);
-  L.dl = gload16u(last ? sp.ptr + sp.len - 64 + 16 * X.q : sp.ptr);
+  const uint64_t lone = sp.ptr + 1024ull * sp.nb, lst = sp.ptr + sp.len - 64;
+  L.v = gload16u(okl ? lone + 16 * X.lane - sh + 4 : idle);
+  const uint32_t shl = rd_shift(lst);  // the last stripe's own byte offset
+  L.dl = gload16u(last ? lst + 16 * X.q - shl + 4 : idle);
+  L.e0 = gload4(x3w_ok(sp, k, g, 0) && g ? seg - sh : idle);
+  L.ev = gload4(okl && sp.nb ? lone - sh : idle);
+  L.el = gload4(last ? lst - shl : idle);
   return L;
 }
 
 // Fold unit k of the span into (a0, a1); after the last unit, merge, finish
 // and reset the accumulators.
 template <class Op, bool PREVIEW>
-__device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32_t k, const X3WLoads& L,
+__device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32_t k, X3WLoads L,
                                          const X3Row& X, uint64_t& a0, uint64_t& a1, const typename Op::Pre& e) {
+  const uint32_t sel = rd_sel(rd_shift(sp.ptr));
   if (k < sp.rounds) {  // wave-uniform
     const uint32_t g = 4 * k + X.row;
+    rd_fix_row(L.d, L.e0, X.j, sel);
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll
     for (int m = 0; m < 4; m++) {
@@ -564,7 +631,11 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
   if (k + 1 < sp.units) return;  // wave-uniform
   if (sp.lone) {  // segment nb alone: lane = stripe * 4 + pair
     const bool okl = (uint32_t)(X.lane >> 2) < sp.nst;
-    const uint64_t d0 = ((uint64_t)L.v.y << 32) | L.v.x, d1 = ((uint64_t)L.v.w << 32) | L.v.z;
+    // (DPP results taken unconditionally: inside ?: they would run with
+    // the source lanes masked off)
+    const uint32_t pv = dpp32<kDppWaveShr1>(L.v.w);
+    const uint4 v = rd_fix(L.v, X.lane ? pv : L.ev, sel);
+    const uint64_t d0 = ((uint64_t)v.y << 32) | v.x, d1 = ((uint64_t)v.w << 32) | v.z;
     uint64_t c0 = okl ? (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.ko0) : 0;
     uint64_t c1 = okl ? (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.ko1) : 0;
     c0 = row_sum_st4(c0);
@@ -574,7 +645,9 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
     a0 += c0 + xl32_64(c0);
     a1 += c1 + xl32_64(c1);
   }
-  const uint64_t l0 = ((uint64_t)L.dl.y << 32) | L.dl.x, l1 = ((uint64_t)L.dl.w << 32) | L.dl.z;
+  const uint32_t pl = dpp32<kDppQuadShr1>(L.dl.w);
+  const uint4 dl = rd_fix(L.dl, X.q ? pl : L.el, rd_sel(rd_shift(sp.ptr + sp.len - 64)));
+  const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
   if (sp.tail) {
     a0 += (PREVIEW ? l0 : l1) + mul32to64(l0 ^ X.kl0);
     a1 += (PREVIEW ? l1 : l0) + mul32to64(l1 ^ X.kl1);
