@@ -632,15 +632,66 @@ __device__ __forceinline__ CrcSpan crc_uniform_span(uint64_t base, uint32_t i, c
   return sp;
 }
 
-template <class Op, bool FULL>
+// ---- transposed loads (uniform FULL batches) ---------------------------
+// The chunk layout makes every load instruction touch 16 B of each of the
+// 64 chunks (64 lines); a streaming probe (microbench/layout_probe.hip,
+// 4 GiB, 16 waves/CU, one round prefetched) reads 6.05 TB/s that way,
+// 6.13 TB/s when each instruction reads 1 KiB contiguous, and 6.90 TB/s
+// contiguous with non-temporal loads (the chunk layout with nt: 3.82).  So
+// lane l = 4a + q loads the 16 B at 1024 j + 16 l of the round (j = 0..3,
+// nt), and a 4 x 4 transpose of 16-byte pieces inside each lane quad (two
+// DPP xor-steps) hands lane l the 64-byte chunk 16 q + a.  The CRC algebra
+// is unchanged, under that "virtual lane" (crc_lane_t).
+__device__ __forceinline__ Chunk crc_load_chunk_t(const CrcSpan& sp, int r, int plane) {
+  const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 16ull * plane;
+  Chunk c;
+#pragma unroll
+  for (int j = 0; j < 4; j++) c.v[j] = span_load16<true>(b + 1024ull * j);
+  return c;
+}
+// one xor-step of the quad transpose on one 32-bit component: register j
+// takes register j ^ M of lane q ^ M where bit M of q differs from bit M of j
+template <int M, int CTRL>
+__device__ __forceinline__ void quad_xstep(uint32_t (&w)[4], int q) {
+  uint32_t x[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) x[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[j ^ M], CTRL, 0xF, 0xF, false);
+#pragma unroll
+  for (int j = 0; j < 4; j++) w[j] = ((q ^ j) & M) ? x[j] : w[j];
+}
+__device__ __forceinline__ void quad_transpose(Chunk& c, int q) {
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) w[j] = reinterpret_cast<const uint32_t*>(&c.v[j])[d];
+    quad_xstep<2, 0x4E>(w, q);  // quad_perm [2,3,0,1]
+    quad_xstep<1, 0xB1>(w, q);  // quad_perm [1,0,3,2]
+#pragma unroll
+    for (int j = 0; j < 4; j++) reinterpret_cast<uint32_t*>(&c.v[j])[d] = w[j];
+  }
+}
+// CrcLane for the transposed layout: table copies by the physical lane (the
+// bank pattern), positions by the virtual lane 16 (l & 3) + (l >> 2).
+__device__ __forceinline__ CrcLane crc_lane_t() {
+  CrcLane L = crc_lane();
+  L.lane = 16 * (L.lane & 3) + (L.lane >> 2);
+  L.lane4 = (uint32_t)L.lane << 2;
+  return L;
+}
+
+// TLAYOUT: transposed loads (FULL batches only).
+template <class Op, bool FULL, bool TLAYOUT = false>
 __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUniform& U, uint32_t count, uint8_t* lds,
                                                    const CrcTables* __restrict__ g) {
+  static_assert(FULL || !TLAYOUT, "transposed loads need whole rounds");
   // table loads, then this wave's first span loads, then the LDS stores:
   // the first round's HBM latency overlaps the fill (uniform spans never
   // un-shift, so those tables are not loaded)
   CrcFill fill;
   crc_fill_load<false>(fill, g);
-  const CrcLane L = crc_lane();
+  const CrcLane L = TLAYOUT ? crc_lane_t() : crc_lane();
+  const int plane = (int)(threadIdx.x & 63);
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
   const uint32_t nwaves = gridDim.x * wpb;
@@ -648,7 +699,7 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
   uint32_t i = wave < count ? wave : 0;
   CrcSpan sp = crc_uniform_span<FULL>(base, i, U);
   int r = sp.rounds - 1;
-  Chunk cur = crc_load_chunk(sp, r, L);
+  Chunk cur = TLAYOUT ? crc_load_chunk_t(sp, r, plane) : crc_load_chunk(sp, r, L);
   crc_fill_store<false>(fill, lds);
   __syncthreads();
   if (wave >= count) return;
@@ -664,7 +715,9 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
       nsp = crc_uniform_span<FULL>(base, more ? ni : i, U);
       nr = U.rounds - 1;
     }
-    const Chunk nxt = crc_load_chunk(more ? nsp : sp, more ? nr : r, L);
+    const Chunk nxt = TLAYOUT ? crc_load_chunk_t(more ? nsp : sp, more ? nr : r, plane)
+                              : crc_load_chunk(more ? nsp : sp, more ? nr : r, L);
+    if (TLAYOUT) quad_transpose(cur, plane & 3);
     s = crc_round(s, cur, sp, r, L);
     if (r == 0) op.finish(i, crc_finish(s, sp, L));
     if (!more) break;

@@ -160,7 +160,16 @@ int launch_crc_uniform(const Op& op, const mck_spans* sp, hipStream_t st) {
   for (uint32_t b = 0; b < 8 * U.hb; b++) inj = gf_unmulx(inj);
   U.inj = inj;
   const uint32_t grid = std::min<uint32_t>(ncu, (count + 15) / 16);
-  if (U.owner == 0 && U.hb == 0) {
+  // MCK_CRC_LAYOUT=0 selects the chunk-layout loads for whole-round spans (A/B)
+  static const bool tlayout = [] {
+    const char* e = getenv("MCK_CRC_LAYOUT");
+    return !e || strcmp(e, "0") != 0;
+  }();
+  if (U.owner == 0 && U.hb == 0 && tlayout) {
+    rc = ensure_lds(k_crc_uniform<Op, true, true>, dev);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_crc_uniform<Op, true, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, U, count);
+  } else if (U.owner == 0 && U.hb == 0) {
     rc = ensure_lds(k_crc_uniform<Op, true>, dev);
     if (rc) return rc;
     hipLaunchKernelGGL((k_crc_uniform<Op, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, U, count);

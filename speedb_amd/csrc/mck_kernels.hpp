@@ -183,10 +183,10 @@ __global__ __launch_bounds__(1024) void k_crc(Op op, uint32_t count) {
 }
 
 // uniform batches (see CrcUniform)
-template <class Op, bool FULL>
+template <class Op, bool FULL, bool TLAYOUT = false>
 __global__ __launch_bounds__(1024) void k_crc_uniform(Op op, CrcUniform U, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_uniform_driver<Op, FULL>(op, U, count, lds, &g_crc_tables);
+  crc_uniform_driver<Op, FULL, TLAYOUT>(op, U, count, lds, &g_crc_tables);
 }
 
 // ============================ XXH3 ========================================
