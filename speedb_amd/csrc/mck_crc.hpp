@@ -155,7 +155,8 @@ struct CrcLane {
   uint32_t pc[4];   // 64K | t << 6 | copy << 2
   uint32_t sel[4];  // v_perm selector for table t
   uint32_t lane4;   // lane * 4
-  int lane;
+  int lane;         // chunk position (the virtual lane under transposed loads)
+  int plane;        // physical lane (16-byte mini-round pieces, descriptor slots)
 };
 __device__ __forceinline__ CrcLane crc_lane() {
   CrcLane L;
@@ -169,6 +170,7 @@ __device__ __forceinline__ CrcLane crc_lane() {
     L.sel[k] = 0x0C020000u | ((4u + t) << 8);
   }
   L.lane4 = (uint32_t)L.lane << 2;
+  L.plane = L.lane;
   return L;
 }
 
@@ -278,6 +280,54 @@ __device__ __forceinline__ CrcSpan crc_span(const uint8_t* p, uint64_t n, uint32
   return s;
 }
 
+// ---- transposed loads -------------------------------------------------------
+// The chunk layout makes every load instruction touch 16 B of each of the
+// 64 chunks (64 lines); a streaming probe (microbench/layout_probe.hip,
+// 4 GiB, 16 waves/CU, one round prefetched) reads 6.05 TB/s that way,
+// 6.13 TB/s when each instruction reads 1 KiB contiguous, and 6.90 TB/s
+// contiguous with non-temporal loads (the chunk layout with nt: 3.82).  So
+// lane l = 4a + q loads the 16 B at 1024 j + 16 l of the round (j = 0..3,
+// nt), and a 4 x 4 transpose of 16-byte pieces inside each lane quad (two
+// DPP xor-steps) hands lane l the 64-byte chunk 16 q + a.  The CRC algebra
+// is unchanged, under that "virtual lane" (crc_lane_t).
+__device__ __forceinline__ Chunk crc_load_chunk_t(const CrcSpan& sp, int r, int plane) {
+  const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 16ull * plane;
+  Chunk c;
+#pragma unroll
+  for (int j = 0; j < 4; j++) c.v[j] = span_load16<true>(b + 1024ull * j);
+  return c;
+}
+// one xor-step of the quad transpose on one 32-bit component: register j
+// takes register j ^ M of lane q ^ M where bit M of q differs from bit M of j
+template <int M, int CTRL>
+__device__ __forceinline__ void quad_xstep(uint32_t (&w)[4], int q) {
+  uint32_t x[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) x[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[j ^ M], CTRL, 0xF, 0xF, false);
+#pragma unroll
+  for (int j = 0; j < 4; j++) w[j] = ((q ^ j) & M) ? x[j] : w[j];
+}
+__device__ __forceinline__ void quad_transpose(Chunk& c, int q) {
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) w[j] = reinterpret_cast<const uint32_t*>(&c.v[j])[d];
+    quad_xstep<2, 0x4E>(w, q);  // quad_perm [2,3,0,1]
+    quad_xstep<1, 0xB1>(w, q);  // quad_perm [1,0,3,2]
+#pragma unroll
+    for (int j = 0; j < 4; j++) reinterpret_cast<uint32_t*>(&c.v[j])[d] = w[j];
+  }
+}
+// CrcLane for the transposed layout: table copies by the physical lane (the
+// bank pattern), positions by the virtual lane 16 (l & 3) + (l >> 2).
+__device__ __forceinline__ CrcLane crc_lane_t() {
+  CrcLane L = crc_lane();
+  L.lane = 16 * (L.lane & 3) + (L.lane >> 2);
+  L.lane4 = (uint32_t)L.lane << 2;
+  return L;
+}
+
 __device__ __forceinline__ uint64_t crc_chunk_base(const CrcSpan& sp, int r, const CrcLane& L) {
   return sp.a1 - (uint64_t)kRoundBytes * (r + 1) + (uint64_t)L.lane * kChunkBytes;
 }
@@ -286,15 +336,25 @@ __device__ __forceinline__ uint64_t crc_chunk_base(const CrcSpan& sp, int r, con
 // an exec-masked branch turns later waits into vmcnt(0) and kills the
 // prefetch).  In the first round, pieces below a0 read a0 instead (their
 // data is discarded); only the address computation is branched, uniformly.
+// T = transposed loads (see crc_load_chunk_t): full rounds read 1 KiB
+// contiguous per instruction, non-temporal; quad_transpose() before
+// crc_round turns them into chunks.
+template <bool T = false>
 __device__ __forceinline__ Chunk crc_load_chunk(const CrcSpan& sp, int r, const CrcLane& L) {
-  const uint64_t cb = crc_chunk_base(sp, r, L);
   uint64_t pa[4];
+  if (T) {
+    const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 16ull * L.plane;
 #pragma unroll
-  for (int j = 0; j < 4; j++) pa[j] = cb + 16 * j;
+    for (int j = 0; j < 4; j++) pa[j] = b + 1024ull * j;
+  } else {
+    const uint64_t cb = crc_chunk_base(sp, r, L);
+#pragma unroll
+    for (int j = 0; j < 4; j++) pa[j] = cb + 16 * j;
+  }
   if (sp.mini && r == sp.rounds - 1) {
     // mini round: lane l's 16 bytes at a1 - 4 KiB * (rounds-1) - 1 KiB + 16 l
     // (all four loads read it: the load count stays fixed for vmcnt)
-    uint64_t a = sp.a1 - (uint64_t)kRoundBytes * (sp.rounds - 1) - kMiniBytes + 16ull * L.lane;
+    uint64_t a = sp.a1 - (uint64_t)kRoundBytes * (sp.rounds - 1) - kMiniBytes + 16ull * L.plane;
     a = a < sp.a0 ? sp.a0 : a;
 #pragma unroll
     for (int j = 0; j < 4; j++) pa[j] = a;
@@ -304,7 +364,7 @@ __device__ __forceinline__ Chunk crc_load_chunk(const CrcSpan& sp, int r, const 
   }
   Chunk c;
 #pragma unroll
-  for (int j = 0; j < 4; j++) c.v[j] = gload16(pa[j]);
+  for (int j = 0; j < 4; j++) c.v[j] = span_load16<T>(pa[j]);
   return c;
 }
 
@@ -339,7 +399,7 @@ __device__ __forceinline__ void crc_keep_head_bytes(uint4& v, uint32_t keep) {
 // zshift(s, 16 * (63 - lane)): 64-byte part by the final-shift tables of
 // lane 63 - (63 - lane) / 4, the remaining 0..48 bytes by the 16/32-byte maps.
 __device__ __forceinline__ uint32_t crc_lane_final16(uint32_t s, const CrcLane& L) {
-  const uint32_t d = 63u - (uint32_t)L.lane;
+  const uint32_t d = 63u - (uint32_t)L.plane;  // (mini rounds: physical pieces)
   const uint32_t l4 = (63u - (d >> 2)) << 2;
   uint32_t x[8];
 #pragma unroll
@@ -355,18 +415,18 @@ __device__ __forceinline__ uint32_t crc_lane_final16(uint32_t s, const CrcLane& 
 // c); returns the pure state at the mini round's end, wave-uniform.
 __device__ __forceinline__ uint32_t crc_mini_round(Chunk c, const CrcSpan& sp, const CrcLane& L) {
   uint32_t* w = reinterpret_cast<uint32_t*>(&c.v[0]);
-  if (sp.hb_m && L.lane == sp.owner_m) {  // zero the owner's bytes before ptr
+  if (sp.hb_m && L.plane == sp.owner_m) {  // zero the owner's bytes before ptr
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int z = (int)sp.hb_m - 4 * q;
       w[q] = z <= 0 ? w[q] : z >= 4 ? 0u : w[q] & (0xFFFFFFFFu << (8 * z));
     }
   }
-  if (sp.rounds == 1 && sp.kt && L.lane == 63) crc_keep_head_bytes(c.v[0], 16 - sp.kt);  // span ends here
-  uint32_t x = L.lane == sp.owner_m ? sp.inj_m : 0u;
+  if (sp.rounds == 1 && sp.kt && L.plane == 63) crc_keep_head_bytes(c.v[0], 16 - sp.kt);  // span ends here
+  uint32_t x = L.plane == sp.owner_m ? sp.inj_m : 0u;
 #pragma unroll
   for (int q = 0; q < 4; q++) x = crc_step4(x ^ w[q], L);
-  x = L.lane < sp.owner_m ? 0u : x;
+  x = L.plane < sp.owner_m ? 0u : x;
   if (sp.owner_m == 63) return readlane_u32(x, 63);  // one chunk: already at the end
   return wave_xor32(crc_lane_final16(x, L));
 }
@@ -435,7 +495,7 @@ template <class Op>
 __device__ __forceinline__ SpanDesc crc_desc_fetch(const Op& op, uint32_t first, uint32_t stride, uint32_t end,
                                                    const CrcLane& L) {
   SpanDesc d{0, 0, 0};
-  const uint64_t i = (uint64_t)first + (uint64_t)L.lane * stride;
+  const uint64_t i = (uint64_t)first + (uint64_t)L.plane * stride;
   if (i < end) {
     d.off = op.off((uint32_t)i);
     d.len = op.len((uint32_t)i);
@@ -529,7 +589,7 @@ struct FeedLds {
   __device__ bool next(const Op&, const CrcLane&, uint32_t* span, SpanDesc* d) { return take(span, d); }
 };
 
-template <class Op, class Feed>
+template <class Op, class Feed, bool T = false>
 __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& L) {
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   uint32_t i;
@@ -537,7 +597,7 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
   if (!f.first(op, L, &i, &d)) return;
   CrcSpan sp = crc_span(reinterpret_cast<const uint8_t*>(base + d.off), d.len, d.init);
   int r = sp.rounds - 1;
-  Chunk cur = crc_load_chunk(sp, r, L);
+  Chunk cur = crc_load_chunk<T>(sp, r, L);
   // the epilogue inputs of the span being loaded travel with its chunks
   typename Op::Pre pcur = op.pre(i, sp.ptr, sp.end - sp.ptr);
   uint32_t s = 0;
@@ -557,8 +617,9 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
     // unconditional (see crc_load_chunk); after the last round it re-reads
     // the current chunk, which is never used
     const CrcSpan& lsp = more ? nsp : sp;
-    const Chunk nxt = crc_load_chunk(lsp, more ? nr : r, L);
+    const Chunk nxt = crc_load_chunk<T>(lsp, more ? nr : r, L);
     const typename Op::Pre pnxt = op.pre(more ? ni : i, lsp.ptr, lsp.end - lsp.ptr);
+    if (T && !(sp.mini && r == sp.rounds - 1)) quad_transpose(cur, L.plane & 3);  // wave-uniform
     s = crc_round(s, cur, sp, r, L);
     if (r == 0) op.finish(i, crc_finish(s, sp, L), pcur);
     if (!more) break;
@@ -578,7 +639,8 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
 //   uint32_t Op::init_crc(i)                    (per lane, i < count)
 //   Op::Pre Op::pre(i, ptr, len)   epilogue inputs, loaded with the chunks
 //   void Op::finish(i, crc, pre)   (all lanes call it; lane 0 writes)
-template <class Op>
+// T: transposed loads (crc_load_chunk<true>).
+template <class Op, bool T = false>
 __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, uint8_t* lds,
                                                  const CrcTables* __restrict__ g) {
   crc_fill_lds(lds, g);
@@ -586,14 +648,14 @@ __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, u
   const bool dyn = share <= kDescCache;                       // grid-uniform
   if (dyn) feed_lds_stage(op, count);
   __syncthreads();
-  const CrcLane L = crc_lane();
+  const CrcLane L = T ? crc_lane_t() : crc_lane();
   if (dyn) {
     FeedLds<Op> f{(count - blockIdx.x + gridDim.x - 1) / gridDim.x};
-    crc_drive(op, f, L);
+    crc_drive<Op, FeedLds<Op>, T>(op, f, L);
   } else {
     FeedStatic<Op> f;
     f.count = count;
-    crc_drive(op, f, L);
+    crc_drive<Op, FeedStatic<Op>, T>(op, f, L);
   }
 }
 
@@ -630,54 +692,6 @@ __device__ __forceinline__ CrcSpan crc_uniform_span(uint64_t base, uint32_t i, c
   sp.hb_m = 0;
   sp.inj_m = 0;
   return sp;
-}
-
-// ---- transposed loads (uniform FULL batches) ---------------------------
-// The chunk layout makes every load instruction touch 16 B of each of the
-// 64 chunks (64 lines); a streaming probe (microbench/layout_probe.hip,
-// 4 GiB, 16 waves/CU, one round prefetched) reads 6.05 TB/s that way,
-// 6.13 TB/s when each instruction reads 1 KiB contiguous, and 6.90 TB/s
-// contiguous with non-temporal loads (the chunk layout with nt: 3.82).  So
-// lane l = 4a + q loads the 16 B at 1024 j + 16 l of the round (j = 0..3,
-// nt), and a 4 x 4 transpose of 16-byte pieces inside each lane quad (two
-// DPP xor-steps) hands lane l the 64-byte chunk 16 q + a.  The CRC algebra
-// is unchanged, under that "virtual lane" (crc_lane_t).
-__device__ __forceinline__ Chunk crc_load_chunk_t(const CrcSpan& sp, int r, int plane) {
-  const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 16ull * plane;
-  Chunk c;
-#pragma unroll
-  for (int j = 0; j < 4; j++) c.v[j] = span_load16<true>(b + 1024ull * j);
-  return c;
-}
-// one xor-step of the quad transpose on one 32-bit component: register j
-// takes register j ^ M of lane q ^ M where bit M of q differs from bit M of j
-template <int M, int CTRL>
-__device__ __forceinline__ void quad_xstep(uint32_t (&w)[4], int q) {
-  uint32_t x[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) x[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[j ^ M], CTRL, 0xF, 0xF, false);
-#pragma unroll
-  for (int j = 0; j < 4; j++) w[j] = ((q ^ j) & M) ? x[j] : w[j];
-}
-__device__ __forceinline__ void quad_transpose(Chunk& c, int q) {
-#pragma unroll
-  for (int d = 0; d < 4; d++) {
-    uint32_t w[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) w[j] = reinterpret_cast<const uint32_t*>(&c.v[j])[d];
-    quad_xstep<2, 0x4E>(w, q);  // quad_perm [2,3,0,1]
-    quad_xstep<1, 0xB1>(w, q);  // quad_perm [1,0,3,2]
-#pragma unroll
-    for (int j = 0; j < 4; j++) reinterpret_cast<uint32_t*>(&c.v[j])[d] = w[j];
-  }
-}
-// CrcLane for the transposed layout: table copies by the physical lane (the
-// bank pattern), positions by the virtual lane 16 (l & 3) + (l >> 2).
-__device__ __forceinline__ CrcLane crc_lane_t() {
-  CrcLane L = crc_lane();
-  L.lane = 16 * (L.lane & 3) + (L.lane >> 2);
-  L.lane4 = (uint32_t)L.lane << 2;
-  return L;
 }
 
 // TLAYOUT: transposed loads (FULL batches only).

@@ -176,10 +176,10 @@ struct OpCrcBlock {
   }
 };
 
-template <class Op>
+template <class Op, bool T = false>
 __global__ __launch_bounds__(1024) void k_crc(Op op, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_spans_driver(op, count, lds, &g_crc_tables);
+  crc_spans_driver<Op, T>(op, count, lds, &g_crc_tables);
 }
 
 // uniform batches (see CrcUniform)
