@@ -81,6 +81,11 @@ def parse():
     return p.parse_args()
 
 
+# whole-round uniform CRC kernel: transposed loads unless MCK_CRC_LAYOUT=0
+CRC_UNIFORM_FULL = ("mck::k_crc_uniform<mck::OpCrcValue, true, false>" if os.environ.get("MCK_CRC_LAYOUT") == "0"
+                    else "mck::k_crc_uniform<mck::OpCrcValue, true, true>")
+
+
 def cpu_baseline(args, kind, block, sample, gpu_lo32_sum):
     """The reference's crc32c::Value (util/crc32c.cc crc32c_3way, SSE4.2 +
     PCLMUL) or XXH3_64bits, one block per call (tools/db_bench_tool.cc
@@ -151,7 +156,7 @@ def make_workload(args, dev, rank, world):
         out64 = torch.empty(count, dtype=torch.int64, device=dev)
         if args.workload == "crc32c":
             w.step = lambda: S.crc32c_batch(spans, out=out32, stream=stream)
-            w.kernel = "mck::k_crc_uniform<mck::OpCrcValue, true>"
+            w.kernel = CRC_UNIFORM_FULL
             w.alg_bytes = count * (block + 4)
         else:
             w.step = lambda: S.xxh3_64_batch(spans, out=out64, stream=stream)
@@ -181,7 +186,7 @@ def make_workload(args, dev, rank, world):
                 res[im.checksum_type] = im.verify(stream=stream)
         w.step = step
         w.launches = 2
-        w.kernel = "mck::k_crc<mck::OpCrcBlock<2> > + mck::k_xxh3_wave<mck::OpX3Block<2> >"
+        w.kernel = "mck::k_crc<mck::OpCrcBlock<2>, false> + mck::k_xxh3_wave<mck::OpX3Block<2> >"
         w.span_bytes = sum(im.payload_bytes + im.count for im in imgs)  # payload + type byte
         # per launch: span bytes + 4 B stored + 8 B offset + 4 B length + 8 B
         # file offset in, 1 B flag + 4 + 4 B out
@@ -242,7 +247,7 @@ def make_workload(args, dev, rank, world):
             if world > 1:  # the one real exchange: (crc, length) per rank
                 res["crc"] = shard.combine_span_crcs(out, nbytes, dev)
         w.step = step
-        w.kernel = "mck::k_crc_uniform<mck::OpCrcValue, true>"
+        w.kernel = CRC_UNIFORM_FULL
         w.span_bytes = nbytes
         w.alg_bytes = (nbytes // 65536) * (65536 + 4)
         w.desc = (f"whole-file CRC32C (FileChecksumGenCrc32c, util/file_checksum_helper.h) of a "
@@ -278,7 +283,7 @@ def make_workload(args, dev, rank, world):
                                                     out.data_ptr(), stream.cuda_stream), "mck_wal_write_batch")
         w.step = step
         w.launches = 2
-        w.kernel = "mck::k_crc<mck::OpWalFragCrc> + mck::k_wal_copy<false>"
+        w.kernel = "mck::k_crc<mck::OpWalFragCrc, false> + mck::k_wal_copy<false>"
         w.span_bytes = int(lens.sum())
         # per launch (avg of the two): CRC reads the payload + 24 B descriptor
         # + 4 B out per fragment; the writer reads the payload + descriptor +
@@ -312,7 +317,7 @@ def make_workload(args, dev, rank, world):
         def step():
             S.blob.record_batch(False, img, offs, lens, status=status, stream=stream)
         w.step = step
-        w.kernel = "mck::k_crc<mck::OpBlobRecord<false> >"
+        w.kernel = "mck::k_crc<mck::OpBlobRecord<false>, false>"
         w.span_bytes = n * rec
         w.alg_bytes = n * (rec + 8 + 4 + 1)
         w.desc = (f"blob file verify: {n} records per GPU ({kb} B key, {vb} B value), header CRC + blob CRC "
@@ -373,7 +378,7 @@ def make_workload(args, dev, rank, world):
                 1, hbuf.data_ptr(), None, None, block, block, count, 0, 0, 256 << 20,
                 out.ctypes.data, None, ctypes.byref(secs)), "mck_host_batch_checksum")
         w.step = step
-        w.kernel = "mck::k_crc_uniform<mck::OpCrcValue, false> (H2D/D2H overlapped)"
+        w.kernel = "mck::k_crc_uniform<mck::OpCrcValue, false, false> (H2D/D2H overlapped)"
         w.span_bytes = count * block
         w.alg_bytes = count * (block + 4 + 8 + 4)
         w.desc = (f"host-resident pinned {count} x {block} B blocks (SST-sized, 80M-key/1KB-value "
