@@ -11,7 +11,8 @@ ol.orc_crc32c_value.restype = ctypes.c_uint32
 ol.orc_crc32c_value.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
 mask = lambda c: ((((c >> 15) | (c << 17)) & 0xFFFFFFFF) + 0xa282ead8) & 0xFFFFFFFF
 dev = torch.device("cuda", 0)
-n, kb, vb = int(sys.argv[1]) if len(sys.argv) > 1 else 200000, 16, 4096
+n, kb = int(sys.argv[1]) if len(sys.argv) > 1 else 200000, 16
+vb = int(sys.argv[2]) if len(sys.argv) > 2 else 4096
 rec = 32 + kb + vb
 img = W.rand_bytes(30 + n * rec + 64, dev, 700)
 recs = img[30:30 + n * rec].view(n, rec)

@@ -29,6 +29,16 @@ __device__ __forceinline__ uint4 span_load16(uint64_t addr) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+// 16 bytes at ANY byte address through a vector load, also when the address
+// is wave-uniform: for a uniform address the compiler may pick s_load, and
+// scalar loads are dword-granular (they drop the low two address bits) --
+// a misaligned uniform 16-byte load then reads the wrong bytes.  The empty
+// asm makes the address a VGPR value.
+__device__ __forceinline__ uint4 vload16_any(uint64_t addr) {
+  asm volatile("" : "+v"(addr));
+  return span_load16<false>(addr);
+}
+
 // v_readlane returns int: widen through uint32_t, never sign-extend.
 __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, uint32_t k) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));

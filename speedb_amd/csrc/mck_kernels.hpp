@@ -548,7 +548,8 @@ struct OpBlobRecord {
   __device__ uint64_t len(uint32_t i) const { return blob_len[i]; }
   __device__ uint32_t init_crc(uint32_t) const { return 0u; }
   __device__ Pre pre(uint32_t, uint64_t ptr, uint64_t) const {
-    return Pre{span_load16<false>(ptr - 32), span_load16<false>(ptr - 16)};
+    // (record headers sit at any byte offset: vload16_any, never s_load)
+    return Pre{vload16_any(ptr - 32), vload16_any(ptr - 16)};
   }
   __device__ void finish(uint32_t i, uint32_t crc, const Pre& e) const {
     const uint32_t hcrc = crc_mask(blob_header_crc(e));

@@ -81,3 +81,36 @@ def test_write_record_crcs(gpu, oracle):
     dev, offs, lens = blob._device_records(bytes(blank), got, torch.device("cuda"))
     blob.WriteRecordCrcs(dev, offs, lens)
     assert bytes(dev[:len(img)].cpu().numpy().tobytes()) == img
+
+
+@pytest.mark.gpu
+def test_record_batch_large_static_feed(gpu, oracle):
+    """More records than a workgroup's LDS descriptor cache (> 393,216 on 256
+    CUs: the static feed, whose first span per wave has a wave-uniform
+    address) with headers at odd byte offsets and one-round blobs: the
+    header fields must be read with vector loads (a scalar 16-byte load drops
+    the low address bits).  Write side vs the oracle, then verify."""
+    import numpy as np
+    import torch
+    from speedb_amd import blob
+    n, kb, vb = 420_000, 16, 200
+    rec = 32 + kb + vb
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    img = torch.randint(0, 256, (30 + n * rec + 64,), dtype=torch.uint8, device="cuda", generator=g)
+    recs = img[30:30 + n * rec].view(n, rec)
+    recs[:, 0:8] = torch.tensor(list(kb.to_bytes(8, "little")), dtype=torch.uint8, device="cuda")
+    recs[:, 8:16] = torch.tensor(list(vb.to_bytes(8, "little")), dtype=torch.uint8, device="cuda")
+    offs = 30 + torch.arange(n, dtype=torch.int64, device="cuda") * rec
+    lens = torch.full((n,), kb + vb, dtype=torch.int32, device="cuda")
+    blob.WriteRecordCrcs(img, offs, lens)
+    h = img.cpu().numpy().tobytes()
+    for i in list(range(0, 8192)) + list(range(8192, n, 101)) + [n - 1]:
+        o = 30 + i * rec
+        assert struct.unpack_from("<I", h, o + 24)[0] == oracle.Mask(oracle.Value(h[o:o + 24])), i
+        assert struct.unpack_from("<I", h, o + 28)[0] == oracle.Mask(oracle.Value(h[o + 32:o + rec])), i
+    st = blob.record_batch(False, img, offs, lens)
+    assert int(st.sum().item()) == 0
+    img[30 + 5 * rec + 40] ^= 1  # one blob byte of record 5
+    st = blob.record_batch(False, img, offs, lens).cpu().numpy()
+    assert np.nonzero(st)[0].tolist() == [5] and st[5] == 2
