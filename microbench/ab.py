@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--align", type=int, default=1,
                     help="--mixed: round every span start up to this many bytes")
     ap.add_argument("--nojitter", action="store_true", help="--mixed: no +0..255 length jitter")
+    ap.add_argument("--ragged", action="store_true",
+                    help="uniform blocks passed with explicit offsets/lengths (the generic driver)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
@@ -70,6 +72,10 @@ def main():
         count = a.blocks
         data = torch.randint(0, 256, (count * a.block + 64,), dtype=torch.uint8, device=dev, generator=g)
         sp = Spans(data.data_ptr(), None, None, a.block, a.block, count)
+        if a.ragged:
+            o = torch.arange(count, dtype=torch.int64, device=dev) * a.block
+            l_ = torch.full((count,), a.block, dtype=torch.int32, device=dev)
+            sp = Spans(data.data_ptr(), o.data_ptr(), l_.data_ptr(), 0, 0, count)
         span_bytes = count * a.block
     libs = []
     for p in a.libs:
