@@ -205,8 +205,10 @@ __global__ __launch_bounds__(kX3WaveThreads) void k_xxh3_wave(Op op, uint32_t co
   xxh3_wave_driver<Op, false>(op, count, 0);
 }
 
-// XXH3 ops.  The wave driver calls pre(i, ptr, hlen) with the span's last
-// unit and finish(i, h, pre); the row driver calls finish(i, h).
+// XXH3 ops.  Both drivers call pre(i, ptr, hlen) with the span's loads (the
+// wave driver with every unit, the row driver with every segment) and
+// finish(i, h, pre); spans <= 240 bytes (hashed on one lane) call
+// finish(i, h).
 struct OpX3Value {
   SpanSrc s;
   uint64_t* out;

@@ -522,11 +522,10 @@ constexpr uint32_t kX3DescCache = 1536;
 // One span on the wave, cut into "units": unit k < rounds is round k (four
 // segments, one per row); the last unit (k = units - 1) also carries the
 // lone partial segment (spread over the wave) and the last stripe.  Every
-// unit issues the same six 16-byte loads per lane (clamped to the span's
-// first bytes where a load has no work), so the driver can keep the NEXT
-// unit's loads -- of this span or of the next one -- in flight while it
-// folds the current unit: one HBM round trip per unit is hidden behind the
-// previous unit's compute.
+// unit issues the same loads per lane -- six dword-aligned 16-byte loads and
+// three dwords for the realignment (rd_fix), clamped to the span's first
+// dwords where a load has no work -- all before any is used, so a unit costs
+// one HBM round trip (see xxh3_wave_loop; the next unit is not prefetched).
 struct X3WSpan {
   uint64_t ptr, len;
   uint32_t i;       // span index
