@@ -319,6 +319,48 @@ __device__ __forceinline__ void quad_transpose(Chunk& c, int q) {
     for (int j = 0; j < 4; j++) reinterpret_cast<uint32_t*>(&c.v[j])[d] = w[j];
   }
 }
+// Row variant (MCK_CRC_ROWT, the default): lane l = 16 k + c loads the 16 B
+// at 1024 j + 64 c + 16 k -- each instruction still reads the round's 1 KiB
+// j whole, in a permuted lane order -- and a 4 x 4 transpose over (row k,
+// register j) made of two v_permlane16_swap and two v_permlane32_swap per
+// 32-bit component (4 instructions, each moving two registers, instead of
+// 16 DPP moves and selects) leaves lane l holding the 64-byte chunk l: the
+// chunk layout itself, no virtual lanes.
+#ifndef MCK_CRC_ROWT
+#define MCK_CRC_ROWT 1
+#endif
+constexpr bool kCrcRowT = MCK_CRC_ROWT;
+__device__ __forceinline__ Chunk crc_load_chunk_rt(const CrcSpan& sp, int r, int plane) {
+  const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 64ull * (plane & 15) + 16ull * (plane >> 4);
+  Chunk c;
+#pragma unroll
+  for (int j = 0; j < 4; j++) c.v[j] = span_load16<true>(b + 1024ull * j);
+  return c;
+}
+__device__ __forceinline__ void row_transpose(Chunk& c) {
+#pragma unroll
+  for (int d = 0; d < 4; d++) {
+    uint32_t w[4];
+#pragma unroll
+    for (int j = 0; j < 4; j++) w[j] = reinterpret_cast<const uint32_t*>(&c.v[j])[d];
+    // row bit 0 <-> register bit 0: a's odd rows swap with b's even rows
+    auto p = __builtin_amdgcn_permlane16_swap(w[0], w[1], false, false);
+    w[0] = p[0];
+    w[1] = p[1];
+    p = __builtin_amdgcn_permlane16_swap(w[2], w[3], false, false);
+    w[2] = p[0];
+    w[3] = p[1];
+    // row bit 1 <-> register bit 1: a's rows 2-3 swap with b's rows 0-1
+    p = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+    w[0] = p[0];
+    w[2] = p[1];
+    p = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+    w[1] = p[0];
+    w[3] = p[1];
+#pragma unroll
+    for (int j = 0; j < 4; j++) reinterpret_cast<uint32_t*>(&c.v[j])[d] = w[j];
+  }
+}
 // CrcLane for the transposed layout: table copies by the physical lane (the
 // bank pattern), positions by the virtual lane 16 (l & 3) + (l >> 2).
 __device__ __forceinline__ CrcLane crc_lane_t() {
@@ -704,7 +746,7 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
   // un-shift, so those tables are not loaded)
   CrcFill fill;
   crc_fill_load<false>(fill, g);
-  const CrcLane L = TLAYOUT ? crc_lane_t() : crc_lane();
+  const CrcLane L = TLAYOUT && !kCrcRowT ? crc_lane_t() : crc_lane();
   const int plane = (int)(threadIdx.x & 63);
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
@@ -713,7 +755,8 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
   uint32_t i = wave < count ? wave : 0;
   CrcSpan sp = crc_uniform_span<FULL>(base, i, U);
   int r = sp.rounds - 1;
-  Chunk cur = TLAYOUT ? crc_load_chunk_t(sp, r, plane) : crc_load_chunk(sp, r, L);
+  Chunk cur = !TLAYOUT ? crc_load_chunk(sp, r, L) : kCrcRowT ? crc_load_chunk_rt(sp, r, plane)
+                                                             : crc_load_chunk_t(sp, r, plane);
   crc_fill_store<false>(fill, lds);
   __syncthreads();
   if (wave >= count) return;
@@ -729,9 +772,11 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
       nsp = crc_uniform_span<FULL>(base, more ? ni : i, U);
       nr = U.rounds - 1;
     }
-    const Chunk nxt = TLAYOUT ? crc_load_chunk_t(more ? nsp : sp, more ? nr : r, plane)
-                              : crc_load_chunk(more ? nsp : sp, more ? nr : r, L);
-    if (TLAYOUT) quad_transpose(cur, plane & 3);
+    const Chunk nxt = !TLAYOUT  ? crc_load_chunk(more ? nsp : sp, more ? nr : r, L)
+                      : kCrcRowT ? crc_load_chunk_rt(more ? nsp : sp, more ? nr : r, plane)
+                                 : crc_load_chunk_t(more ? nsp : sp, more ? nr : r, plane);
+    if (TLAYOUT && kCrcRowT) row_transpose(cur);
+    if (TLAYOUT && !kCrcRowT) quad_transpose(cur, plane & 3);
     s = crc_round(s, cur, sp, r, L);
     if (r == 0) op.finish(i, crc_finish(s, sp, L));
     if (!more) break;
