@@ -384,8 +384,8 @@ __device__ __forceinline__ uint64_t crc_chunk_base(const CrcSpan& sp, int r, con
 template <bool T = false>
 __device__ __forceinline__ Chunk crc_load_chunk(const CrcSpan& sp, int r, const CrcLane& L) {
   uint64_t pa[4];
-  if (T) {
-    const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 16ull * L.plane;
+  if (T) {  // the row-transpose layout (crc_load_chunk_rt; row_transpose before crc_round)
+    const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 64ull * (L.plane & 15) + 16ull * (L.plane >> 4);
 #pragma unroll
     for (int j = 0; j < 4; j++) pa[j] = b + 1024ull * j;
   } else {
@@ -661,7 +661,7 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
     const CrcSpan& lsp = more ? nsp : sp;
     const Chunk nxt = crc_load_chunk<T>(lsp, more ? nr : r, L);
     const typename Op::Pre pnxt = op.pre(more ? ni : i, lsp.ptr, lsp.end - lsp.ptr);
-    if (T && !(sp.mini && r == sp.rounds - 1)) quad_transpose(cur, L.plane & 3);  // wave-uniform
+    if (T && !(sp.mini && r == sp.rounds - 1)) row_transpose(cur);  // wave-uniform
     s = crc_round(s, cur, sp, r, L);
     if (r == 0) op.finish(i, crc_finish(s, sp, L), pcur);
     if (!more) break;
@@ -681,7 +681,7 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
 //   uint32_t Op::init_crc(i)                    (per lane, i < count)
 //   Op::Pre Op::pre(i, ptr, len)   epilogue inputs, loaded with the chunks
 //   void Op::finish(i, crc, pre)   (all lanes call it; lane 0 writes)
-// T: transposed loads (crc_load_chunk<true>).
+// T: row-transposed loads (crc_load_chunk<true>, row_transpose).
 template <class Op, bool T = false>
 __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, uint8_t* lds,
                                                  const CrcTables* __restrict__ g) {
@@ -690,7 +690,7 @@ __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, u
   const bool dyn = share <= kDescCache;                       // grid-uniform
   if (dyn) feed_lds_stage(op, count);
   __syncthreads();
-  const CrcLane L = T ? crc_lane_t() : crc_lane();
+  const CrcLane L = crc_lane();
   if (dyn) {
     FeedLds<Op> f{(count - blockIdx.x + gridDim.x - 1) / gridDim.x};
     crc_drive<Op, FeedLds<Op>, T>(op, f, L);

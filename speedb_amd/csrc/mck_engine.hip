@@ -135,6 +135,22 @@ bool crc_tlayout() {
   return t;
 }
 
+// Generic CRC driver load layout per op: row-transposed, non-temporal loads
+// (k_crc<Op, true>: SST mix 63.0 -> 66.4 %, ragged 4 KiB 65.0 -> 69.3 %,
+// 64 KiB 74.7 -> 83.4 %) except for the ~1 KiB WAL-writer fragments, where
+// the chunk layout measured 0.285 vs 0.276.  -DMCK_CRC_GENERIC_T=0 turns it off.
+#ifndef MCK_CRC_GENERIC_T
+#define MCK_CRC_GENERIC_T 1
+#endif
+template <class Op>
+struct CrcRowT {
+  static constexpr bool value = MCK_CRC_GENERIC_T;
+};
+template <>
+struct CrcRowT<OpWalFragCrc> {
+  static constexpr bool value = false;
+};
+
 // ---- launchers -------------------------------------------------------------
 template <class Op>
 int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
@@ -142,13 +158,13 @@ int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
   int dev, ncu;
   int rc = current_device(&dev, &ncu);
   if (rc) return rc;
-  // persistent: one 16-wave workgroup per CU (160 KiB of LDS each).  Chunk
-  // layout: transposed loads (k_crc<Op, true>) measured no gain here (SST
-  // mix 0.622 vs 0.627, WAL writer 0.269 vs 0.287), unlike the uniform path.
-  rc = ensure_lds(k_crc<Op>, dev);
+  // persistent: one 16-wave workgroup per CU (160 KiB of LDS each), with
+  // row-transposed loads (CrcRowT)
+  constexpr bool T = CrcRowT<Op>::value;
+  rc = ensure_lds(k_crc<Op, T>, dev);
   if (rc) return rc;
   const uint32_t grid = std::min<uint32_t>(ncu, (count + 15) / 16);
-  hipLaunchKernelGGL(k_crc<Op>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, count);
+  hipLaunchKernelGGL((k_crc<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, count);
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }
@@ -474,12 +490,15 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, 
   }
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
-  if (int rc = ensure_lds(k_wal_verify, dev)) return rc;
+#ifndef MCK_WAL_T
+#define MCK_WAL_T 1
+#endif
+  if (int rc = ensure_lds(k_wal_verify<MCK_WAL_T>, dev)) return rc;
   const uint32_t nblocks = (uint32_t)nb64;
   const uint32_t grid = std::min<uint32_t>(ncu, (nblocks + 15) / 16);
-  hipLaunchKernelGGL(k_wal_verify, dim3(grid), dim3(1024), kCrcLdsBytes, reinterpret_cast<hipStream_t>(stream),
-                     static_cast<const uint8_t*>(wal), nbytes, log_number, reinterpret_cast<WalResult*>(results),
-                     nblocks);
+  hipLaunchKernelGGL(k_wal_verify<MCK_WAL_T>, dim3(grid), dim3(1024), kCrcLdsBytes,
+                     reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(wal), nbytes, log_number,
+                     reinterpret_cast<WalResult*>(results), nblocks);
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }

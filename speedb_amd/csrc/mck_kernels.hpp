@@ -626,18 +626,22 @@ struct WalResult {
   uint32_t bytes_ok;
 };
 
+// T: row-transposed loads for the full rounds (crc_load_chunk<true>).
+template <bool T>
 __device__ __forceinline__ uint32_t crc_span_wave(const uint8_t* p, uint64_t n, uint32_t init, const CrcLane& L) {
   const CrcSpan sp = crc_span(p, n, init);
   uint32_t s = 0;
-  Chunk cur = crc_load_chunk(sp, sp.rounds - 1, L);
+  Chunk cur = crc_load_chunk<T>(sp, sp.rounds - 1, L);
   for (int r = sp.rounds - 1; r >= 0; r--) {
-    const Chunk nxt = crc_load_chunk(sp, r > 0 ? r - 1 : 0, L);
+    const Chunk nxt = crc_load_chunk<T>(sp, r > 0 ? r - 1 : 0, L);
+    if (T && !(sp.mini && r == sp.rounds - 1)) row_transpose(cur);  // wave-uniform
     s = crc_round(s, cur, sp, r, L);
     cur = nxt;
   }
   return crc_finish(s, sp, L);
 }
 
+template <bool T>
 __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_t nbytes, uint32_t log_number,
                                                      WalResult* res, uint32_t nblocks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -685,7 +689,7 @@ __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_
         break;
       }
       const uint32_t stored = rd32_bytes(h);
-      const uint32_t actual = crc_span_wave(h + 6, length + hsize - 6, 0u, L);
+      const uint32_t actual = crc_span_wave<T>(h + 6, length + hsize - 6, 0u, L);
       // Unmask(stored) == actual  <=>  stored == Mask(actual)
       if (crc_mask(actual) != stored) {
         status = 1;  // kBadRecordChecksum
