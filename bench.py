@@ -186,7 +186,7 @@ def make_workload(args, dev, rank, world):
                 res[im.checksum_type] = im.verify(stream=stream)
         w.step = step
         w.launches = 2
-        w.kernel = "mck::k_crc<mck::OpCrcBlock<2>, false> + mck::k_xxh3_wave<mck::OpX3Block<2> >"
+        w.kernel = "mck::k_crc<mck::OpCrcBlock<2>, true> + mck::k_xxh3_wave<mck::OpX3Block<2> >"
         w.span_bytes = sum(im.payload_bytes + im.count for im in imgs)  # payload + type byte
         # per launch: span bytes + 4 B stored + 8 B offset + 4 B length + 8 B
         # file offset in, 1 B flag + 4 + 4 B out
@@ -317,7 +317,7 @@ def make_workload(args, dev, rank, world):
         def step():
             S.blob.record_batch(False, img, offs, lens, status=status, stream=stream)
         w.step = step
-        w.kernel = "mck::k_crc<mck::OpBlobRecord<false>, false>"
+        w.kernel = "mck::k_crc<mck::OpBlobRecord<false>, true>"
         w.span_bytes = n * rec
         w.alg_bytes = n * (rec + 8 + 4 + 1)
         w.desc = (f"blob file verify: {n} records per GPU ({kb} B key, {vb} B value), header CRC + blob CRC "
