@@ -575,3 +575,42 @@ def test_crc32c_long_full_size_combine(gpu, oracle):
     acc = oracle.Combine(acc, tail_crc, tail)
     got = int(S.crc32c_long(dev, n_blocks * 4096 + tail).cpu().numpy().view(np.uint32)[0])
     assert got == acc
+
+
+@pytest.mark.parametrize("ctype", [1, 4])
+def test_sst_verify_large_static_feed(gpu, oracle, ctype):
+    """More blocks than the per-workgroup LDS descriptor caches (the static
+    feeds of the CRC and XXH3 drivers, whose first span per wave has a
+    wave-uniform address): small blocks at odd offsets, trailers computed on
+    the device and checked against the oracle on a sample that includes the
+    first blocks of every wave, then one flipped byte per corrupted block."""
+    import speedb_amd as S
+    torch = gpu
+    n = 420_000
+    rng = np.random.default_rng(ctype)
+    lens = rng.integers(50, 300, n)
+    offs = np.concatenate([[3], 3 + np.cumsum(lens + 5)[:-1]])
+    total = int(offs[-1] + lens[-1] + 5)
+    host = bytearray(rng.integers(0, 256, total + 64, dtype=np.uint8).tobytes())
+    comps = rng.integers(0, 2, n).astype(np.uint8)
+    dev = torch.frombuffer(bytes(host), dtype=torch.uint8).to("cuda")
+    sp = spans(torch, S, dev, offs.tolist(), lens.tolist())
+    ct = torch.tensor(comps, device="cuda")
+    tr = np.array(u32(S.sst_trailer_batch(ctype, sp, ct)), dtype=np.uint32)
+    for i in list(range(0, 5000)) + list(range(5000, n, 211)) + [n - 1]:
+        o, ln = int(offs[i]), int(lens[i])
+        assert tr[i] == oracle.BuiltinLast(ctype, bytes(host[o:o + ln]), int(comps[i])), i
+    arr = np.frombuffer(host, dtype=np.uint8).copy()
+    arr[offs + lens] = comps
+    trb = tr.view(np.uint8).reshape(n, 4)
+    for k in range(4):
+        arr[offs + lens + 1 + k] = trb[:, k]
+    bad = sorted(set([0, 1, 17, 4095, 4096, 9000] + rng.integers(0, n, 20).tolist()))
+    for i in bad:
+        arr[offs[i] + rng.integers(0, lens[i])] ^= 0x10
+    dev2 = torch.from_numpy(arr).to("cuda")
+    sp2 = spans(torch, S, dev2, offs.tolist(), lens.tolist())
+    mm, comp, stored, cnt = S.sst_verify_batch(ctype, sp2)
+    flagged = np.nonzero(mm.cpu().numpy())[0].tolist()
+    assert flagged == bad
+    assert int(cnt.item()) == len(bad)
