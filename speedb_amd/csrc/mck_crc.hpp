@@ -55,8 +55,12 @@ constexpr uint32_t kLdsQuarter = kLdsHalf + 512;
 constexpr uint32_t kLdsLowEnd = kLdsQuarter + 512;  // 34816
 
 // Independent lookup chains per lane and round (1, 2 or 4); see crc_round.
+// One chain since the row-transposed loads made the kernels VALU-bound:
+// the join of two chains (a 32-byte nibble map per round) costs more than
+// the latency it hides (headline 0.786 vs 0.774, SST 0.657 vs 0.648, WAL
+// 0.711 vs 0.700; four chains: 73.1 vs 76.5 %).
 #ifndef MCK_CRC_CHAINS
-#define MCK_CRC_CHAINS 2
+#define MCK_CRC_CHAINS 1
 #endif
 constexpr int kCrcChains = MCK_CRC_CHAINS;
 static_assert(kCrcChains == 1 || kCrcChains == 2 || kCrcChains == 4, "chains");
