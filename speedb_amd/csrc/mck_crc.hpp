@@ -178,21 +178,31 @@ __device__ __forceinline__ CrcLane crc_lane() {
   return L;
 }
 
-// s' = zshift(s, 4): 4 byte-table lookups, one v_perm_b32 address each.
-__device__ __forceinline__ uint32_t crc_step4(uint32_t s, const CrcLane& L) {
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); the kernels are
+// VALU-bound, and the XOR trees of the table steps are most of their VALU.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// zshift(s, 4) ^ w: 4 byte-table lookups, one v_perm_b32 address each; w is
+// the next data word, folded in by the same two bitop3 that join the
+// lookups (a step costs 4 perm + 2 bitop3 instead of 4 perm + 4 xor).
+__device__ __forceinline__ uint32_t crc_step4x(uint32_t s, const CrcLane& L, uint32_t w) {
   const uint32_t a0 = __builtin_amdgcn_perm(s, L.pc[0], L.sel[0]);
   const uint32_t a1 = __builtin_amdgcn_perm(s, L.pc[1], L.sel[1]);
   const uint32_t a2 = __builtin_amdgcn_perm(s, L.pc[2], L.sel[2]);
   const uint32_t a3 = __builtin_amdgcn_perm(s, L.pc[3], L.sel[3]);
-  return lds_u32(a0) ^ lds_u32(a1) ^ lds_u32(a2) ^ lds_u32(a3);
+  return xor3(xor3(lds_u32(a0), lds_u32(a1), lds_u32(a2)), lds_u32(a3), w);
 }
+// s' = zshift(s, 4)
+__device__ __forceinline__ uint32_t crc_step4(uint32_t s, const CrcLane& L) { return crc_step4x(s, L, 0u); }
 
 // A linear map given as 8 nibble tables [8][16] at LDS offset `off`.
 __device__ __forceinline__ uint32_t crc_nibmap(uint32_t off, uint32_t s) {
   uint32_t x[8];
 #pragma unroll
   for (int n = 0; n < 8; n++) x[n] = lds_u32(off + n * 64 + (((s >> (4 * n)) & 15u) << 2));
-  return (x[0] ^ x[1]) ^ (x[2] ^ x[3]) ^ ((x[4] ^ x[5]) ^ (x[6] ^ x[7]));
+  return xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], x[5]), x[6] ^ x[7]);
 }
 
 // zshift(s, 64*(63-lane)) with the per-lane tables.
@@ -200,7 +210,7 @@ __device__ __forceinline__ uint32_t crc_lane_final(uint32_t s, const CrcLane& L)
   uint32_t x[8];
 #pragma unroll
   for (int n = 0; n < 8; n++) x[n] = lds_u32(kLdsFinal + n * 4096 + ((((s >> (4 * n)) & 15u) << 8) | L.lane4));
-  return (x[0] ^ x[1]) ^ (x[2] ^ x[3]) ^ ((x[4] ^ x[5]) ^ (x[6] ^ x[7]));
+  return xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], x[5]), x[6] ^ x[7]);
 }
 
 // XOR over the 64 lanes, returned wave-uniform: DPP butterfly inside each
@@ -450,7 +460,7 @@ __device__ __forceinline__ uint32_t crc_lane_final16(uint32_t s, const CrcLane& 
   uint32_t x[8];
 #pragma unroll
   for (int n = 0; n < 8; n++) x[n] = lds_u32(kLdsFinal + n * 4096 + ((((s >> (4 * n)) & 15u) << 8) | l4));
-  s = (x[0] ^ x[1]) ^ (x[2] ^ x[3]) ^ ((x[4] ^ x[5]) ^ (x[6] ^ x[7]));
+  s = xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], x[5]), x[6] ^ x[7]);
   const uint32_t q = crc_nibmap(kLdsQuarter, s);
   s = (d & 1u) ? q : s;
   const uint32_t h = crc_nibmap(kLdsHalf, s);
@@ -470,8 +480,9 @@ __device__ __forceinline__ uint32_t crc_mini_round(Chunk c, const CrcSpan& sp, c
   }
   if (sp.rounds == 1 && sp.kt && L.plane == 63) crc_keep_head_bytes(c.v[0], 16 - sp.kt);  // span ends here
   uint32_t x = L.plane == sp.owner_m ? sp.inj_m : 0u;
+  x ^= w[0];
 #pragma unroll
-  for (int q = 0; q < 4; q++) x = crc_step4(x ^ w[q], L);
+  for (int q = 0; q < 4; q++) x = crc_step4x(x, L, q < 3 ? w[q + 1] : 0u);
   x = L.plane < sp.owner_m ? 0u : x;
   if (sp.owner_m == 63) return readlane_u32(x, 63);  // one chunk: already at the end
   return wave_xor32(crc_lane_final16(x, L));
@@ -495,11 +506,11 @@ __device__ __forceinline__ uint32_t crc_round(uint32_t s, Chunk c, const CrcSpan
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&c.v[0]);
   constexpr int kWords = 16 / kCrcChains;  // words per chain
 #pragma unroll
+  for (int q = 0; q < kCrcChains; q++) x[q] ^= w[q * kWords];
+#pragma unroll
   for (int i = 0; i < kWords; i++) {
 #pragma unroll
-    for (int q = 0; q < kCrcChains; q++) x[q] ^= w[q * kWords + i];
-#pragma unroll
-    for (int q = 0; q < kCrcChains; q++) x[q] = crc_step4(x[q], L);
+    for (int q = 0; q < kCrcChains; q++) x[q] = crc_step4x(x[q], L, i + 1 < kWords ? w[q * kWords + i + 1] : 0u);
   }
   if (kCrcChains == 1) {
     s = x[0];

@@ -532,9 +532,9 @@ struct BlobPre {
 __device__ __forceinline__ uint32_t blob_header_crc(const BlobPre& e) {
   const CrcLane L = crc_lane();
   const uint32_t w[6] = {e.h0.x, e.h0.y, e.h0.z, e.h0.w, e.h1.x, e.h1.y};
-  uint32_t s = 0xFFFFFFFFu;
+  uint32_t s = 0xFFFFFFFFu ^ w[0];
 #pragma unroll
-  for (int k = 0; k < 6; k++) s = crc_step4(s ^ w[k], L);
+  for (int k = 0; k < 6; k++) s = crc_step4x(s, L, k < 5 ? w[k + 1] : 0u);
   return ~s;
 }
 template <bool WRITE>
