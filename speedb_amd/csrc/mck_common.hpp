@@ -39,6 +39,16 @@ __device__ __forceinline__ uint4 vload16_any(uint64_t addr) {
   return span_load16<false>(addr);
 }
 
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96): the checksum
+// kernels are VALU-bound, and XOR trees are a large part of their VALU.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint64_t xor3_64(uint64_t a, uint64_t b, uint64_t c) {
+  return ((uint64_t)xor3((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32)) << 32) |
+         xor3((uint32_t)a, (uint32_t)b, (uint32_t)c);
+}
+
 // v_readlane returns int: widen through uint32_t, never sign-extend.
 __device__ __forceinline__ uint32_t readlane_u32(uint32_t v, uint32_t k) {
   return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));

@@ -178,12 +178,6 @@ __device__ __forceinline__ CrcLane crc_lane() {
   return L;
 }
 
-// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); the kernels are
-// VALU-bound, and the XOR trees of the table steps are most of their VALU.
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
 // zshift(s, 4) ^ w: 4 byte-table lookups, one v_perm_b32 address each; w is
 // the next data word, folded in by the same two bitop3 that join the
 // lookups (a step costs 4 perm + 2 bitop3 instead of 4 perm + 4 xor).

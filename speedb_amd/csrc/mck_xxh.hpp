@@ -500,11 +500,11 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
 // operands = v, one result is v itself and the other the partner row's value)
 __device__ __forceinline__ uint32_t xl16(uint32_t v) {
   const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
-  return r[0] ^ r[1] ^ v;
+  return xor3(r[0], r[1], v);
 }
 __device__ __forceinline__ uint32_t xl32(uint32_t v) {
   const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
-  return r[0] ^ r[1] ^ v;
+  return xor3(r[0], r[1], v);
 }
 __device__ __forceinline__ uint64_t xl16_64(uint64_t v) {
   return ((uint64_t)xl16((uint32_t)(v >> 32)) << 32) | xl16((uint32_t)v);
@@ -596,7 +596,7 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
   const uint32_t sel = rd_sel(rd_shift(sp.ptr));
   if (k < sp.rounds) {  // wave-uniform
     const uint32_t g = 4 * k + X.row;
-    rd_fix_row(L.d, L.e0, X.j, sel);
+    if (sp.ptr & 3) rd_fix_row(L.d, L.e0, X.j, sel);  // wave-uniform: dword-aligned spans need no fix
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll
     for (int m = 0; m < 4; m++) {
@@ -630,10 +630,13 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
   if (k + 1 < sp.units) return;  // wave-uniform
   if (sp.lone) {  // segment nb alone: lane = stripe * 4 + pair
     const bool okl = (uint32_t)(X.lane >> 2) < sp.nst;
-    // (DPP results taken unconditionally: inside ?: they would run with
-    // the source lanes masked off)
-    const uint32_t pv = dpp32<kDppWaveShr1>(L.v.w);
-    const uint4 v = rd_fix(L.v, X.lane ? pv : L.ev, sel);
+    uint4 v = L.v;
+    if (sp.ptr & 3) {  // wave-uniform
+      // (DPP result taken before the ?: -- inside it the move would run
+      // with the source lanes masked off)
+      const uint32_t pv = dpp32<kDppWaveShr1>(L.v.w);
+      v = rd_fix(L.v, X.lane ? pv : L.ev, sel);
+    }
     const uint64_t d0 = ((uint64_t)v.y << 32) | v.x, d1 = ((uint64_t)v.w << 32) | v.z;
     uint64_t c0 = okl ? (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.ko0) : 0;
     uint64_t c1 = okl ? (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.ko1) : 0;
@@ -644,8 +647,11 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
     a0 += c0 + xl32_64(c0);
     a1 += c1 + xl32_64(c1);
   }
-  const uint32_t pl = dpp32<kDppQuadShr1>(L.dl.w);
-  const uint4 dl = rd_fix(L.dl, X.q ? pl : L.el, rd_sel(rd_shift(sp.ptr + sp.len - 64)));
+  uint4 dl = L.dl;
+  if ((sp.ptr + sp.len) & 3) {  // wave-uniform: the last stripe's own alignment
+    const uint32_t pl = dpp32<kDppQuadShr1>(L.dl.w);
+    dl = rd_fix(L.dl, X.q ? pl : L.el, rd_sel(rd_shift(sp.ptr + sp.len - 64)));
+  }
   const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
   if (sp.tail) {
     a0 += (PREVIEW ? l0 : l1) + mul32to64(l0 ^ X.kl0);
