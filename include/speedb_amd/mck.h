@@ -205,8 +205,11 @@ int mck_wal_plan(const uint64_t* host_src_offsets, const uint32_t* host_lengths,
  * (db/log_writer.cc:263-311 EmitPhysicalRecord): trailer zero padding,
  * [masked CRC LE32][length LE16][type][log number LE32 if recyclable],
  * payload.  frags: device array [nfrags]; crc_scratch: device u32 [nfrags]
- * (the masked fragment CRCs, computed first in one batch); out must be
- * 16-byte aligned (any hipMalloc allocation is). */
+ * (the masked fragment CRCs); out must be 16-byte aligned (any hipMalloc
+ * allocation is).  Large batches run in pieces whose copies overlap the next
+ * piece's CRCs on an engine-owned side stream (per host thread and device),
+ * joined back into `stream` before the call returns: work queued on
+ * `stream` afterwards sees the whole log stream written. */
 int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags,
                         uint32_t nfrags, uint32_t log_number,
                         uint32_t* crc_scratch, void* out, mck_stream_t stream);

@@ -504,6 +504,50 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, 
 }
 
 // ---- device WAL writer -------------------------------------------------------
+// The writer is two dependent kernels: the fragment CRCs (k_crc, one
+// 16-wave workgroup per CU holding the 160 KiB LDS tables, latency-bound on
+// ~1 KiB spans) and the header + payload copy (k_wal_copy, no LDS).  The
+// fragment list is cut into pieces; the copy of piece k runs on a side
+// stream while the CRC of piece k+1 runs on the caller's stream, so the copy
+// waves fill the wave slots the CRC workgroup leaves free on every CU.
+// MCK_WAL_PIECES=n (A/B switch, default 8; 1 = one CRC launch then one copy
+// on the caller's stream).
+uint32_t wal_pieces() {
+  static const uint32_t n = [] {
+    const char* e = getenv("MCK_WAL_PIECES");
+    const int v = e ? atoi(e) : 8;
+    return (uint32_t)(v < 1 ? 1 : v > 16 ? 16 : v);
+  }();
+  return n;
+}
+
+// Side stream and fork/join events, per host thread and device (an event
+// re-recorded by another thread between record and wait would join the
+// wrong work).
+struct WalSide {
+  hipStream_t st = nullptr;
+  hipEvent_t ev[17] = {};
+};
+
+int wal_side(int dev, WalSide** out) {
+  thread_local WalSide side[kMaxDev];
+  WalSide& w = side[dev];
+  if (!w.st) {
+    MCK_HIP(hipStreamCreateWithFlags(&w.st, hipStreamNonBlocking));
+    for (hipEvent_t& e : w.ev) MCK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  *out = &w;
+  return MCK_OK;
+}
+
+int launch_wal_copy(const uint8_t* src, const WalFrag* f, uint32_t n, uint32_t log_number, const uint32_t* crcs,
+                    uint8_t* out, int ncu, hipStream_t st) {
+  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (n + 3) / 4);
+  hipLaunchKernelGGL(k_wal_copy<false>, dim3(grid), dim3(256), 0, st, src, f, n, log_number, crcs, out);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
 int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t nfrags, uint32_t log_number,
                         uint32_t* crc_scratch, void* out, mck_stream_t stream) {
   t_err[0] = 0;
@@ -515,15 +559,34 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const WalFrag* f = reinterpret_cast<const WalFrag*>(frags);
-  if (int rc = launch_crc(OpWalFragCrc{static_cast<const uint8_t*>(src), f, wal_type_crcs(log_number), crc_scratch},
-                          nfrags, st))
-    return rc;
-  int ncu;
-  if (int rc = current_device(nullptr, &ncu)) return rc;
-  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (nfrags + 3) / 4);
-  hipLaunchKernelGGL(k_wal_copy<false>, dim3(grid), dim3(256), 0, st, static_cast<const uint8_t*>(src), f, nfrags,
-                     log_number, crc_scratch, static_cast<uint8_t*>(out));
-  MCK_HIP(hipGetLastError());
+  const uint8_t* s8 = static_cast<const uint8_t*>(src);
+  uint8_t* o8 = static_cast<uint8_t*>(out);
+  const WalTypeCrcs tc = wal_type_crcs(log_number);
+  int dev, ncu;
+  if (int rc = current_device(&dev, &ncu)) return rc;
+  // pieces of at least 16 fragments per CU (one CRC grid's worth of spans)
+  uint32_t pieces = wal_pieces();
+  while (pieces > 1 && nfrags / pieces < 16u * (uint32_t)ncu) pieces--;
+  if (pieces == 1) {
+    if (int rc = launch_crc(OpWalFragCrc{s8, f, tc, crc_scratch}, nfrags, st)) return rc;
+    return launch_wal_copy(s8, f, nfrags, log_number, crc_scratch, o8, ncu, st);
+  }
+  WalSide* w;
+  if (int rc = wal_side(dev, &w)) return rc;
+  // the side stream starts after the caller's prior work (inputs ready)
+  MCK_HIP(hipEventRecord(w->ev[16], st));
+  MCK_HIP(hipStreamWaitEvent(w->st, w->ev[16], 0));
+  for (uint32_t k = 0; k < pieces; k++) {
+    const uint32_t lo = (uint32_t)((uint64_t)nfrags * k / pieces);
+    const uint32_t hi = (uint32_t)((uint64_t)nfrags * (k + 1) / pieces);
+    if (int rc = launch_crc(OpWalFragCrc{s8, f + lo, tc, crc_scratch + lo}, hi - lo, st)) return rc;
+    MCK_HIP(hipEventRecord(w->ev[k], st));
+    MCK_HIP(hipStreamWaitEvent(w->st, w->ev[k], 0));
+    if (int rc = launch_wal_copy(s8, f + lo, hi - lo, log_number, crc_scratch + lo, o8, ncu, w->st)) return rc;
+  }
+  // join: the caller's stream continues after the last copy
+  MCK_HIP(hipEventRecord(w->ev[16], w->st));
+  MCK_HIP(hipStreamWaitEvent(st, w->ev[16], 0));
   return MCK_OK;
 }
 

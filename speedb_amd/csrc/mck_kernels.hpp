@@ -467,6 +467,119 @@ __device__ __forceinline__ uint8_t wal_out_byte(const WalFrag& f, uint32_t crc, 
   return src[f.src_off + (h - hs)];
 }
 
+#ifndef MCK_WAL_COPY_PIPE
+#define MCK_WAL_COPY_PIPE 1
+#endif
+#if MCK_WAL_COPY_PIPE
+// One fragment's pass in k_wal_copy: every load of the fragment's first
+// 1 KiB (head bytes, first 16-byte body chunk of each lane, tail bytes) is
+// issued before any of its stores, and the next fragment's descriptor is
+// loaded before them -- a wave waits one memory round trip per typical
+// (1 KB) fragment instead of one per head / body / tail loop.  Bytes beyond
+// the first pass (long fragments, a head > 64 bytes from an odd pad) run in
+// wal_copy_rest.  Measured (walwrite bench, 2.16M fragments): 1.038 vs
+// 1.143 ms; with non-temporal body loads 1.100; with two fragments' loads
+// issued before either's stores 1.354 (1.388 with nt loads).
+struct WalCopyPass {
+  uint64_t pay, body0, body1, end, head_end;
+  uint64_t ha, ca, ta;  // this lane's head byte, body chunk, tail byte (output offsets)
+  bool hv, cv, tv;
+  uint8_t hb, tb;
+  uint4 v;
+};
+
+// 16 output bytes at payload-relative source offset s: one 16-byte load at
+// the dword below s (dword-aligned: a byte-misaligned 16-byte load runs far
+// below rate) plus the next dword when s is not dword-aligned.
+__device__ __forceinline__ uint4 wal_chunk_load(const uint8_t* src, uint64_t s) {
+  const uint64_t s4 = s & ~3ull;
+  const uint32_t sh = (uint32_t)(s & 3);
+  const uint4 a = span_load16<false>(reinterpret_cast<uint64_t>(src + s4));
+  // with sh == 0 the fifth dword is not needed (and could lie past the
+  // payload's last dword): re-read the fourth
+  const uint32_t e = reinterpret_cast<const uint32_t*>(src + s4)[sh ? 4 : 3];
+  uint4 v;
+  v.x = __builtin_amdgcn_alignbyte(a.y, a.x, sh);
+  v.y = __builtin_amdgcn_alignbyte(a.z, a.y, sh);
+  v.z = __builtin_amdgcn_alignbyte(a.w, a.z, sh);
+  v.w = __builtin_amdgcn_alignbyte(e, a.w, sh);
+  return v;
+}
+
+template <bool GATHER>
+__device__ __forceinline__ void wal_copy_issue(WalCopyPass& p, const WalFrag& f, uint32_t crc, uint32_t log_number,
+                                               const uint8_t* __restrict__ src, uint32_t lane) {
+  const uint32_t hs = GATHER ? 0u : (f.type >= 5 && f.type <= 8) || f.type == 11 ? 11u : 7u;
+  const uint64_t start = f.dst_off - (GATHER ? 0u : f.pad);
+  p.end = f.dst_off + hs + f.length;
+  p.pay = f.dst_off + hs;                // output offset of payload byte 0
+  p.body0 = (p.pay + 15) & ~15ull;       // first 16-aligned chunk of payload
+  p.body1 = p.end & ~15ull;              // end of the last full chunk
+  const bool body = p.body0 < p.body1;
+  // head: [start, body0) byte-wise -- or the whole record when it has no
+  // full 16-byte payload chunk; tail: [body1, end) byte-wise (< 16 bytes)
+  p.head_end = body ? p.body0 : p.end;
+  p.ha = start + lane;
+  p.hv = p.ha < p.head_end;
+  p.ca = p.body0 + 16ull * lane;
+  p.cv = body && p.ca < p.body1;
+  p.ta = p.body1 + lane;
+  p.tv = body && p.ta < p.end;
+  p.hb = p.tb = 0;
+  if (p.hv) p.hb = GATHER ? src[f.src_off + (p.ha - p.pay)] : wal_out_byte(f, crc, log_number, hs, src, p.ha);
+  if (p.tv) p.tb = GATHER ? src[f.src_off + (p.ta - p.pay)] : wal_out_byte(f, crc, log_number, hs, src, p.ta);
+  if (p.cv) p.v = wal_chunk_load(src, f.src_off + (p.ca - p.pay));
+}
+
+__device__ __forceinline__ void wal_copy_store(const WalCopyPass& p, uint8_t* __restrict__ out) {
+  if (p.hv) out[p.ha] = p.hb;
+  if (p.cv) *reinterpret_cast<uint4*>(out + p.ca) = p.v;
+  if (p.tv) out[p.ta] = p.tb;
+}
+
+template <bool GATHER>
+__device__ __forceinline__ void wal_copy_rest(const WalCopyPass& p, const WalFrag& f, uint32_t crc,
+                                              uint32_t log_number, const uint8_t* __restrict__ src,
+                                              uint8_t* __restrict__ out) {
+  const uint32_t hs = GATHER ? 0u : (f.type >= 5 && f.type <= 8) || f.type == 11 ? 11u : 7u;
+  for (uint64_t a = p.ha + 64; a < p.head_end; a += 64)
+    out[a] = GATHER ? src[f.src_off + (a - p.pay)] : wal_out_byte(f, crc, log_number, hs, src, a);
+  for (uint64_t c = p.ca + 16ull * 64; c < p.body1; c += 16ull * 64)
+    *reinterpret_cast<uint4*>(out + c) = wal_chunk_load(src, f.src_off + (c - p.pay));
+}
+
+// GATHER: the reverse direction for recovery -- copy each fragment's
+// payload (no header, no padding) to out + dst_off, reassembling logical
+// records (mck_wal_gather_batch).
+template <bool GATHER>
+__global__ __launch_bounds__(256) void k_wal_copy(const uint8_t* __restrict__ src, const WalFrag* __restrict__ frags,
+                                                  uint32_t nfrags, uint32_t log_number,
+                                                  const uint32_t* __restrict__ crcs, uint8_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t nw = gridDim.x * wpb;
+  uint32_t fi = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+  if (fi >= nfrags) return;
+  WalFrag f = frags[fi];
+  uint32_t crc = GATHER ? 0u : crcs[fi];
+  for (;;) {
+    WalCopyPass p;
+    wal_copy_issue<GATHER>(p, f, crc, log_number, src, lane);
+    const uint32_t fn = fi + nw;
+    const bool more = fn < nfrags;
+    const uint32_t nx = more ? fn : fi;
+    const WalFrag f2 = frags[nx];
+    const uint32_t crc2 = GATHER ? 0u : crcs[nx];
+    wal_copy_store(p, out);
+    wal_copy_rest<GATHER>(p, f, crc, log_number, src, out);
+    if (!more) break;
+    fi = fn;
+    f = f2;
+    crc = crc2;
+  }
+}
+
+#else
 // GATHER: the reverse direction for recovery -- copy each fragment's
 // payload (no header, no padding) to out + dst_off, reassembling logical
 // records (mck_wal_gather_batch).
@@ -518,6 +631,8 @@ __global__ __launch_bounds__(256) void k_wal_copy(const uint8_t* __restrict__ sr
     }
   }
 }
+
+#endif
 
 // ===================== blob log records ===================================
 // db/blob/blob_log_format.cc:97-135 BlobLogRecord: a 32-byte header
