@@ -38,7 +38,11 @@ def main():
     d, workload = sys.argv[1], sys.argv[2]
     line = bench_line(os.path.join(d, "bench_trace.txt"))
     kernel = line["roofline"]["kernel"]
-    names = [k.strip() for k in kernel.split(" + ")]
+    # "(overlapped step)": the bench times a whole step whose kernels run
+    # concurrently in pieces (the device WAL writer); traffic is then per
+    # step = per-launch average x launches per step
+    overlapped = kernel.endswith("(overlapped step)")
+    names = [k.strip() for k in kernel.replace("(overlapped step)", "").split(" + ")]
     cfg = {k: v for k, v in line["config"].items() if k not in ("workload", "parallelism")}
     stats = {}
     with open(os.path.join(d, "trace", "trace_kernel_stats.csv")) as f:
@@ -66,6 +70,10 @@ def main():
         raise SystemExit("no counter rows for " + kernel)
     rd = 2 * 1024 * sum(fetch) / len(fetch)
     wr = 1024 * sum(write) / len(write)
+    if overlapped:
+        per_step = calls / (line["warmup"] + line["steps"])
+        rd, wr = rd * per_step, wr * per_step
+        timed_ns = None
     alg = line["roofline"]["alg_bytes_per_launch"]
     out = {
         "workload": workload, "kernel": kernel, "config": cfg,
