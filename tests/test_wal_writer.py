@@ -69,6 +69,37 @@ def test_wal_write_batch_bit_exact(gpu, oracle, recycle):
     assert (res[:, 1] == 0).all()
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_write_batch_pieces_bit_exact(gpu, oracle, recycle):
+    """A group commit large enough that mck_wal_write_batch runs in pieces
+    (>= 2 x 16 fragments per CU): the copy of each piece overlaps the next
+    piece's CRCs on the engine's side stream; the stream must still be
+    log::Writer's, byte for byte, and complete when the call's stream is."""
+    import torch
+
+    import speedb_amd as S
+    rng = np.random.default_rng(5)
+    lens = rng.integers(0, 700, size=24000)
+    lens[rng.integers(0, len(lens), size=40)] = rng.integers(30000, 70000, size=40)  # block-spanning ones
+    src = rng.integers(0, 256, size=int(lens.sum()), dtype=np.uint8).tobytes()
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])])
+    w = WalWriter(oracle, log_number=91, recycle=recycle)
+    w.add_record(b"y" * 333)
+    start = len(w.buf)
+    for o, n in zip(offs, lens):
+        w.add_record(src[o:o + n])
+    dev = torch.frombuffer(bytearray(src + bytes(64)), dtype=torch.uint8).to("cuda")
+    wr = S.WalBatchWriter(log_number=91, recycle_log_files=recycle, block_offset=start)
+    out = wr.AddRecords(dev, offs, [int(n) for n in lens])
+    got = out.cpu().numpy().tobytes()  # the caller's stream: joined after the side stream's copies
+    want = bytes(w.buf[start:])
+    assert len(got) == len(want)
+    if got != want:
+        i = next(k for k in range(len(got)) if got[k] != want[k])
+        raise AssertionError(f"first difference at stream offset {i + start}")
+
+
 @pytest.mark.parametrize("recycle", [False, True])
 def test_wal_list_records_reassembly_plan(oracle, recycle):
     """log::Reader::ReadRecord's reassembly on the host: the logical records
