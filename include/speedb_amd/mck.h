@@ -80,10 +80,19 @@ uint32_t mck_crc32c_combine(uint32_t crc1, uint32_t crc2, size_t crc2len);
 uint32_t mck_context_modifier(uint32_t base_context_checksum, uint64_t offset);
 
 /* Data-reading shims.  Host pointers, synchronous; the bytes are staged to
- * the calling thread's current device and hashed there.  They exist so that
- * every reference call site can be re-pointed without a batching rewrite;
- * batch-aware callers use family 2.  On error they return 0 and set
- * mck_last_error(). */
+ * the calling thread's current device and hashed there (one H2D copy, one
+ * launch, one D2H copy per call: tens of microseconds -- see DESIGN.md
+ * "Scalar shims" for the measured latency).  They exist so that a reference
+ * call site CAN be re-pointed without a batching rewrite; they are not the
+ * fast path.  INTEGRATION.md keeps the reference's CPU crc32c::Extend for
+ * small synchronous calls and routes only batch-shaped callers to family 2.
+ *
+ * Error behaviour: the reference functions have no failure channel
+ * (util/crc32c.h:26, include/rocksdb/file_checksum.h:47-49), so the plain
+ * shims return 0 on ANY error and set mck_last_error() -- in particular
+ * when mck_device_count() == 0 or a HIP call fails.  A caller that must not
+ * mistake an error for a checksum uses the *_r variants, which return 0 /
+ * MCK_E* and write the result through `out`. */
 /* util/crc32c.h:26 Extend, :35 Value */
 uint32_t mck_crc32c_extend(uint32_t init_crc, const void* data, size_t n);
 uint32_t mck_crc32c_value(const void* data, size_t n);
@@ -96,6 +105,21 @@ uint64_t mck_np_hash64(const void* data, size_t n, uint64_t seed);
 /* table/format.cc:604 ComputeBuiltinChecksumWithLastByte */
 uint32_t mck_builtin_checksum_with_last_byte(int type, const void* data,
                                              size_t n, char last_byte);
+
+/* Error-returning variants of the shims above: 0 on success with the result
+ * in *out, MCK_EINVAL / MCK_EHIP / MCK_ENODEV / MCK_ENOMEM otherwise (*out
+ * = 0 then). */
+int mck_crc32c_extend_r(uint32_t init_crc, const void* data, size_t n,
+                        uint32_t* out);
+int mck_crc32c_value_r(const void* data, size_t n, uint32_t* out);
+int mck_xxh3_64_r(const void* data, size_t n, uint64_t* out);
+int mck_builtin_checksum_r(int type, const void* data, size_t n,
+                           uint32_t* out);
+int mck_builtin_checksum_with_last_byte_r(int type, const void* data,
+                                          size_t n, char last_byte,
+                                          uint32_t* out);
+int mck_np_hash64_r(const void* data, size_t n, uint64_t seed,
+                    uint64_t* out);
 
 /* ========================================================================= */
 /* 2. Batched device API                                                    */
@@ -213,6 +237,15 @@ int mck_wal_plan(const uint64_t* host_src_offsets, const uint32_t* host_lengths,
 int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags,
                         uint32_t nfrags, uint32_t log_number,
                         uint32_t* crc_scratch, void* out, mck_stream_t stream);
+/* The number of overlapped pieces mck_wal_write_batch uses for `nfrags`
+ * fragments on the current device (1 = one CRC launch then one copy on the
+ * caller's stream), or a negative MCK_E* code.  Pieces hold >= 16 fragments
+ * per CU; at most MCK_WAL_PIECES (env, default 8). */
+int mck_wal_write_pieces(uint32_t nfrags);
+/* The side streams come from a per-device pool (one side per concurrently
+ * running call, created on first need: a stream + 17 events); this destroys
+ * the idle ones. */
+void mck_wal_side_release(void);
 
 /* ---- WAL recovery: logical records ----------------- */
 
@@ -465,6 +498,12 @@ int mck_partition_spans(const uint32_t* host_lengths, uint32_t count,
  * kind: MCK_kCRC32c (out32 = Value, masked if flags & MCK_F_MASK) or
  *       MCK_kXXH3 (out64 = XXH3_64bits).
  * host_offsets / host_lengths: host arrays (NULL => uniform as in mck_spans).
+ * The per-device staging (two slots, each a stream, a device chunk buffer
+ * of max(chunk_bytes, longest span + 32) bytes, and device + pinned
+ * descriptor/result arrays) is allocated on a device's first call and reused
+ * by later ones (grown when a call needs more); calls on one device are
+ * serialised.  On any error every copy already queued has completed before
+ * the call returns, and a failed allocation leaves nothing allocated.
  * Returns 0 on success.  *seconds (optional) = wall time of the call. */
 int mck_host_batch_checksum(int kind, const void* host_base,
                             const uint64_t* host_offsets,
@@ -472,6 +511,8 @@ int mck_host_batch_checksum(int kind, const void* host_base,
                             uint32_t length, uint32_t count, uint32_t flags,
                             int ndev, size_t chunk_bytes, uint32_t* out32,
                             uint64_t* out64, double* seconds);
+/* Free the host pipeline's cached staging on every device. */
+void mck_host_pipeline_release(void);
 
 #ifdef __cplusplus
 }

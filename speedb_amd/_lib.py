@@ -61,6 +61,13 @@ SIGNATURES = [
     ("mck_builtin_checksum", ctypes.c_uint32, [ctypes.c_int, vp, ctypes.c_size_t]),
     ("mck_builtin_checksum_with_last_byte", ctypes.c_uint32,
      [ctypes.c_int, vp, ctypes.c_size_t, ctypes.c_char]),
+    ("mck_crc32c_extend_r", ctypes.c_int, [ctypes.c_uint32, vp, ctypes.c_size_t, u32p]),
+    ("mck_crc32c_value_r", ctypes.c_int, [vp, ctypes.c_size_t, u32p]),
+    ("mck_xxh3_64_r", ctypes.c_int, [vp, ctypes.c_size_t, u64p]),
+    ("mck_builtin_checksum_r", ctypes.c_int, [ctypes.c_int, vp, ctypes.c_size_t, u32p]),
+    ("mck_builtin_checksum_with_last_byte_r", ctypes.c_int,
+     [ctypes.c_int, vp, ctypes.c_size_t, ctypes.c_char, u32p]),
+    ("mck_np_hash64_r", ctypes.c_int, [vp, ctypes.c_size_t, ctypes.c_uint64, u64p]),
     ("mck_crc32c_batch", ctypes.c_int,
      [ctypes.POINTER(mck_spans), vp, ctypes.c_uint32, vp, vp]),
     ("mck_xxh3_64_batch", ctypes.c_int, [ctypes.POINTER(mck_spans), vp, vp]),
@@ -93,6 +100,8 @@ SIGNATURES = [
      [vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp, ctypes.c_uint64, vp, vp, vp]),
     ("mck_wal_write_batch", ctypes.c_int,
      [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]),
+    ("mck_wal_write_pieces", ctypes.c_int, [ctypes.c_uint32]),
+    ("mck_wal_side_release", None, []),
     ("mck_wal_list_records", ctypes.c_int,
      [vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint64, vp, vp, vp, ctypes.c_uint64, vp, vp]),
     ("mck_wal_gather_batch", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp]),
@@ -105,6 +114,7 @@ SIGNATURES = [
      [ctypes.c_int, vp, vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
       ctypes.c_uint32, ctypes.c_int, ctypes.c_size_t, vp, vp,
       ctypes.POINTER(ctypes.c_double)]),
+    ("mck_host_pipeline_release", None, []),
 ]
 
 for _name, _res, _args in SIGNATURES:

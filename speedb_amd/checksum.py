@@ -608,3 +608,39 @@ def WalReadRecords(wal: bytes, log_number: int = 0, device=None, stream=None):
 
 
 __all__ += ["wal_plan", "WalBatchWriter", "mck_wal_fragment", "wal_list_records", "WalReadRecords"]
+
+
+# ---------------------------------------------------------------------------
+# host-resident batches (mck_host_batch_checksum): the copy-inclusive path
+# ---------------------------------------------------------------------------
+
+def host_batch_checksum(kind: int, host, offsets=None, lengths=None, stride: int = 0, length: int = 0,
+                        count: Optional[int] = None, mask: bool = False, ndev: int = 0,
+                        chunk_bytes: int = 0):
+    """Checksum spans that live in HOST memory (pinned gives the full PCIe
+    rate): H2D in double-buffered chunks, CRC32C (``kind`` =
+    ChecksumType.kCRC32c, optionally masked) or XXH3_64bits (kXXH3) on the
+    device, results back to the host.  ``host``: a numpy uint8 array, a CPU
+    torch uint8 tensor (pinned or not) or bytes; offsets/lengths: host
+    sequences (None = uniform stride/length).  ndev <= 0: the current device;
+    otherwise devices [0, ndev).  Returns (numpy results, seconds)."""
+    import numpy as np
+    if isinstance(host, (bytes, bytearray, memoryview)):
+        host = np.frombuffer(bytes(host), dtype=np.uint8)
+    base = host.data_ptr() if hasattr(host, "data_ptr") else host.ctypes.data
+    offs = None if offsets is None else np.ascontiguousarray(np.asarray(offsets, dtype=np.uint64))
+    lens = None if lengths is None else np.ascontiguousarray(np.asarray(lengths, dtype=np.uint32))
+    if count is None:
+        count = len(offs) if offs is not None else len(lens) if lens is not None else 0
+    out = np.zeros(count, dtype=np.uint64 if kind == ChecksumType.kXXH3 else np.uint32)
+    secs = ctypes.c_double()
+    o32 = out.ctypes.data if kind != ChecksumType.kXXH3 else None
+    o64 = out.ctypes.data if kind == ChecksumType.kXXH3 else None
+    check(lib.mck_host_batch_checksum(int(kind), base, None if offs is None else offs.ctypes.data,
+                                      None if lens is None else lens.ctypes.data, stride, length, count,
+                                      1 if mask else 0, ndev, chunk_bytes, o32, o64, ctypes.byref(secs)),
+          "mck_host_batch_checksum")
+    return out, secs.value
+
+
+__all__ += ["host_batch_checksum"]

@@ -11,6 +11,7 @@
 #include <atomic>
 #include <chrono>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -512,7 +513,7 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, 
 // waves fill the wave slots the CRC workgroup leaves free on every CU.
 // MCK_WAL_PIECES=n (A/B switch, default 8; 1 = one CRC launch then one copy
 // on the caller's stream).
-uint32_t wal_pieces() {
+static uint32_t wal_pieces() {
   static const uint32_t n = [] {
     const char* e = getenv("MCK_WAL_PIECES");
     const int v = e ? atoi(e) : 8;
@@ -521,31 +522,81 @@ uint32_t wal_pieces() {
   return n;
 }
 
-// Side stream and fork/join events, per host thread and device (an event
-// re-recorded by another thread between record and wait would join the
-// wrong work).
+// Side stream and fork/join events of one mck_wal_write_batch call.  Taken
+// from a per-device pool for the duration of the call (so no other thread
+// re-records its events between record and wait) and returned afterwards:
+// the waits already enqueued keep the state of the events at enqueue time,
+// and a later call's work on the side stream queues behind this one's.  The
+// pool holds as many sides as calls ever ran concurrently on the device;
+// mck_wal_side_release() destroys them.
 struct WalSide {
   hipStream_t st = nullptr;
   hipEvent_t ev[17] = {};
 };
+struct WalSidePool {
+  std::mutex mu;
+  std::vector<WalSide*> free_list;
+  std::vector<WalSide*> all;
+};
+static WalSidePool g_wal_side[kMaxDev];
 
-int wal_side(int dev, WalSide** out) {
-  thread_local WalSide side[kMaxDev];
-  WalSide& w = side[dev];
-  if (!w.st) {
-    MCK_HIP(hipStreamCreateWithFlags(&w.st, hipStreamNonBlocking));
-    for (hipEvent_t& e : w.ev) MCK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+static void wal_side_destroy(WalSide* w) {
+  if (w->st) (void)hipStreamDestroy(w->st);
+  for (hipEvent_t& e : w->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete w;
+}
+
+static int wal_side_acquire(int dev, WalSide** out) {
+  WalSidePool& P = g_wal_side[dev];
+  {
+    std::lock_guard<std::mutex> lock(P.mu);
+    if (!P.free_list.empty()) {
+      *out = P.free_list.back();
+      P.free_list.pop_back();
+      return MCK_OK;
+    }
   }
-  *out = &w;
+  WalSide* w = new WalSide;
+  hipError_t e = hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking);
+  for (hipEvent_t& ev : w->ev)
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  if (e != hipSuccess) {
+    set_err("WAL writer side stream/events: %s", hipGetErrorString(e));
+    wal_side_destroy(w);
+    return MCK_EHIP;
+  }
+  std::lock_guard<std::mutex> lock(P.mu);
+  P.all.push_back(w);
+  *out = w;
   return MCK_OK;
 }
 
-int launch_wal_copy(const uint8_t* src, const WalFrag* f, uint32_t n, uint32_t log_number, const uint32_t* crcs,
+static void wal_side_return(int dev, WalSide* w) {
+  WalSidePool& P = g_wal_side[dev];
+  std::lock_guard<std::mutex> lock(P.mu);
+  P.free_list.push_back(w);
+}
+
+static int launch_wal_copy(const uint8_t* src, const WalFrag* f, uint32_t n, uint32_t log_number, const uint32_t* crcs,
                     uint8_t* out, int ncu, hipStream_t st) {
   const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (n + 3) / 4);
   hipLaunchKernelGGL(k_wal_copy<false>, dim3(grid), dim3(256), 0, st, src, f, n, log_number, crcs, out);
   MCK_HIP(hipGetLastError());
   return MCK_OK;
+}
+
+// pieces of at least 16 fragments per CU (one CRC grid's worth of spans)
+static uint32_t wal_pieces_for(uint32_t nfrags, int ncu) {
+  uint32_t pieces = wal_pieces();
+  while (pieces > 1 && nfrags / pieces < 16u * (uint32_t)ncu) pieces--;
+  return pieces;
+}
+
+int mck_wal_write_pieces(uint32_t nfrags) {
+  int ncu;
+  if (int rc = current_device(nullptr, &ncu)) return rc;
+  return (int)wal_pieces_for(nfrags, ncu);
 }
 
 int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t nfrags, uint32_t log_number,
@@ -557,6 +608,10 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
     set_err("src / frags / crc_scratch / out is NULL");
     return MCK_EINVAL;
   }
+  if (reinterpret_cast<uintptr_t>(out) & 15u) {
+    set_err("out must be 16-byte aligned");
+    return MCK_EINVAL;
+  }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const WalFrag* f = reinterpret_cast<const WalFrag*>(frags);
   const uint8_t* s8 = static_cast<const uint8_t*>(src);
@@ -564,30 +619,69 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   const WalTypeCrcs tc = wal_type_crcs(log_number);
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
-  // pieces of at least 16 fragments per CU (one CRC grid's worth of spans)
-  uint32_t pieces = wal_pieces();
-  while (pieces > 1 && nfrags / pieces < 16u * (uint32_t)ncu) pieces--;
+  const uint32_t pieces = wal_pieces_for(nfrags, ncu);
   if (pieces == 1) {
     if (int rc = launch_crc(OpWalFragCrc{s8, f, tc, crc_scratch}, nfrags, st)) return rc;
     return launch_wal_copy(s8, f, nfrags, log_number, crc_scratch, o8, ncu, st);
   }
   WalSide* w;
-  if (int rc = wal_side(dev, &w)) return rc;
-  // the side stream starts after the caller's prior work (inputs ready)
-  MCK_HIP(hipEventRecord(w->ev[16], st));
-  MCK_HIP(hipStreamWaitEvent(w->st, w->ev[16], 0));
-  for (uint32_t k = 0; k < pieces; k++) {
+  if (int rc = wal_side_acquire(dev, &w)) return rc;
+  // fork: the side stream starts after the caller's prior work (inputs ready)
+  int rc = MCK_OK;
+  hipError_t e = hipEventRecord(w->ev[16], st);
+  if (e == hipSuccess) e = hipStreamWaitEvent(w->st, w->ev[16], 0);
+  if (e != hipSuccess) {
+    set_err("WAL writer fork: %s", hipGetErrorString(e));
+    wal_side_return(dev, w);
+    return MCK_EHIP;
+  }
+  for (uint32_t k = 0; k < pieces && !rc; k++) {
     const uint32_t lo = (uint32_t)((uint64_t)nfrags * k / pieces);
     const uint32_t hi = (uint32_t)((uint64_t)nfrags * (k + 1) / pieces);
-    if (int rc = launch_crc(OpWalFragCrc{s8, f + lo, tc, crc_scratch + lo}, hi - lo, st)) return rc;
-    MCK_HIP(hipEventRecord(w->ev[k], st));
-    MCK_HIP(hipStreamWaitEvent(w->st, w->ev[k], 0));
-    if (int rc = launch_wal_copy(s8, f + lo, hi - lo, log_number, crc_scratch + lo, o8, ncu, w->st)) return rc;
+    rc = launch_crc(OpWalFragCrc{s8, f + lo, tc, crc_scratch + lo}, hi - lo, st);
+    if (rc) break;
+    e = hipEventRecord(w->ev[k], st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(w->st, w->ev[k], 0);
+    if (e != hipSuccess) {
+      set_err("WAL writer piece %u: %s", k, hipGetErrorString(e));
+      rc = MCK_EHIP;
+      break;
+    }
+    rc = launch_wal_copy(s8, f + lo, hi - lo, log_number, crc_scratch + lo, o8, ncu, w->st);
   }
-  // join: the caller's stream continues after the last copy
-  MCK_HIP(hipEventRecord(w->ev[16], w->st));
-  MCK_HIP(hipStreamWaitEvent(st, w->ev[16], 0));
-  return MCK_OK;
+  // join, also after a failure partway: the caller's stream continues only
+  // after every copy already queued on the side stream
+  e = hipEventRecord(w->ev[16], w->st);
+  if (e == hipSuccess) e = hipStreamWaitEvent(st, w->ev[16], 0);
+  if (e != hipSuccess) {
+    // the join could not be queued: wait for the side stream here instead
+    (void)hipStreamSynchronize(w->st);
+    if (!rc) {
+      set_err("WAL writer join: %s", hipGetErrorString(e));
+      rc = MCK_EHIP;
+    }
+  }
+  wal_side_return(dev, w);
+  return rc;
+}
+
+void mck_wal_side_release(void) {
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (int d = 0; d < kMaxDev; d++) {
+    WalSidePool& P = g_wal_side[d];
+    std::lock_guard<std::mutex> lock(P.mu);
+    if (P.all.empty()) continue;
+    if (hipSetDevice(d) != hipSuccess) continue;
+    // only sides no call is using; each is idle once its stream drains
+    for (WalSide* w : P.free_list) {
+      (void)hipStreamSynchronize(w->st);
+      P.all.erase(std::find(P.all.begin(), P.all.end(), w));
+      wal_side_destroy(w);
+    }
+    P.free_list.clear();
+  }
+  (void)hipSetDevice(prev);
 }
 
 int mck_wal_gather_batch(const void* wal, const mck_wal_fragment* frags, uint32_t nfrags, void* out,
@@ -596,6 +690,10 @@ int mck_wal_gather_batch(const void* wal, const mck_wal_fragment* frags, uint32_
   if (!nfrags) return MCK_OK;
   if (!wal || !frags || !out) {
     set_err("wal / frags / out is NULL");
+    return MCK_EINVAL;
+  }
+  if (reinterpret_cast<uintptr_t>(out) & 15u) {
+    set_err("out must be 16-byte aligned");
     return MCK_EINVAL;
   }
   int ncu;
@@ -677,60 +775,122 @@ int mck_crc32c_long(const void* data, uint64_t n, uint32_t init_crc, uint32_t* s
 // (pieces hashed in parallel + device combine) instead of one span.
 constexpr size_t kShimLongBytes = 1u << 20;
 
-static uint32_t scalar_u32(int kind, uint32_t init, const void* data, size_t n, int type, int has_last,
-                           char last) {
+// kind 0: Extend(init, data); kind 1: ComputeBuiltinChecksum[WithLastByte].
+static int scalar_u32(int kind, uint32_t init, const void* data, size_t n, int type, int has_last, char last,
+                      uint32_t* res) {
   t_err[0] = 0;
+  if (!res) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  *res = 0;
   if (!data && n) {
     set_err("data is NULL");
-    return 0;
+    return MCK_EINVAL;
   }
   uint8_t* d_data;
   void* d_out;
+  int rc;
   if (kind == 0 && n > kShimLongBytes) {
     uint32_t* d_scratch;
-    if (stage_in(data, n, &d_data, &d_out, 4 * mck_crc32c_long_scratch_words(n), &d_scratch)) return 0;
-    uint32_t v = 0;
-    if (mck_crc32c_long(d_data, n, init, d_scratch, static_cast<uint32_t*>(d_out), nullptr) == 0 &&
-        hipMemcpy(&v, d_out, 4, hipMemcpyDeviceToHost) != hipSuccess)
-      set_err("hipMemcpy failed");
-    return v;
+    if ((rc = stage_in(data, n, &d_data, &d_out, 4 * mck_crc32c_long_scratch_words(n), &d_scratch))) return rc;
+    if ((rc = mck_crc32c_long(d_data, n, init, d_scratch, static_cast<uint32_t*>(d_out), nullptr))) return rc;
+    MCK_HIP(hipMemcpy(res, d_out, 4, hipMemcpyDeviceToHost));
+    return MCK_OK;
   }
   if (n > 0xFFFFFFFFull) {
     set_err("span too long for the scalar shim");
-    return 0;
+    return MCK_EINVAL;
   }
-  if (stage_in(data, n, &d_data, &d_out)) return 0;
+  if ((rc = stage_in(data, n, &d_data, &d_out))) return rc;
   uint8_t* d_last = static_cast<uint8_t*>(d_out) + 32;
-  if (has_last && hipMemcpy(d_last, &last, 1, hipMemcpyHostToDevice) != hipSuccess) {
-    set_err("hipMemcpy failed");
-    return 0;
-  }
+  if (has_last) MCK_HIP(hipMemcpy(d_last, &last, 1, hipMemcpyHostToDevice));
   const mck_spans s{d_data, nullptr, nullptr, 0, (uint32_t)n, 1};
   uint32_t* d_init = static_cast<uint32_t*>(d_out) + 4;
-  int rc;
   if (kind == 0) {
-    if (hipMemcpy(d_init, &init, 4, hipMemcpyHostToDevice) != hipSuccess) {
-      set_err("hipMemcpy failed");
-      return 0;
-    }
+    MCK_HIP(hipMemcpy(d_init, &init, 4, hipMemcpyHostToDevice));
     rc = mck_crc32c_batch(&s, d_init, 0, static_cast<uint32_t*>(d_out), nullptr);
   } else {
     rc = mck_builtin_checksum_batch(type, &s, has_last ? d_last : nullptr, static_cast<uint32_t*>(d_out), nullptr);
   }
-  uint32_t v = 0;
-  if (rc == 0 && hipMemcpy(&v, d_out, 4, hipMemcpyDeviceToHost) != hipSuccess) set_err("hipMemcpy failed");
-  return v;
+  if (rc) return rc;
+  MCK_HIP(hipMemcpy(res, d_out, 4, hipMemcpyDeviceToHost));
+  return MCK_OK;
 }
 
-uint32_t mck_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
-  return scalar_u32(0, init_crc, data, n, 0, 0, 0);
+// kind 0: XXH3_64bits; kind 1: NPHash64(seed).
+static int scalar_u64(int kind, const void* data, size_t n, uint64_t seed, uint64_t* res) {
+  t_err[0] = 0;
+  if (!res) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  *res = 0;
+  if (!data && n) {
+    set_err("data is NULL");
+    return MCK_EINVAL;
+  }
+  if (n > 0xFFFFFFFFull) {
+    set_err("span too long for the scalar shim");
+    return MCK_EINVAL;
+  }
+  uint8_t* d_data;
+  void* d_out;
+  int rc;
+  if ((rc = stage_in(data, n, &d_data, &d_out))) return rc;
+  const mck_spans s{d_data, nullptr, nullptr, 0, (uint32_t)n, 1};
+  rc = kind == 0 ? mck_xxh3_64_batch(&s, static_cast<uint64_t*>(d_out), nullptr)
+                 : mck_np_hash64_batch(&s, seed, static_cast<uint64_t*>(d_out), nullptr);
+  if (rc) return rc;
+  MCK_HIP(hipMemcpy(res, d_out, 8, hipMemcpyDeviceToHost));
+  return MCK_OK;
 }
-uint32_t mck_crc32c_value(const void* data, size_t n) { return scalar_u32(0, 0, data, n, 0, 0, 0); }
+
+int mck_crc32c_extend_r(uint32_t init_crc, const void* data, size_t n, uint32_t* out) {
+  return scalar_u32(0, init_crc, data, n, 0, 0, 0, out);
+}
+int mck_crc32c_value_r(const void* data, size_t n, uint32_t* out) { return scalar_u32(0, 0, data, n, 0, 0, 0, out); }
+int mck_builtin_checksum_r(int type, const void* data, size_t n, uint32_t* out) {
+  return scalar_u32(1, 0, data, n, type, 0, 0, out);
+}
+int mck_builtin_checksum_with_last_byte_r(int type, const void* data, size_t n, char last_byte, uint32_t* out) {
+  return scalar_u32(1, 0, data, n, type, 1, last_byte, out);
+}
+int mck_xxh3_64_r(const void* data, size_t n, uint64_t* out) { return scalar_u64(0, data, n, 0, out); }
+int mck_np_hash64_r(const void* data, size_t n, uint64_t seed, uint64_t* out) {
+  return scalar_u64(1, data, n, seed, out);
+}
+
+// The signature-compatible shims: 0 (and mck_last_error()) on any error.
+uint32_t mck_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
+  uint32_t v = 0;
+  (void)mck_crc32c_extend_r(init_crc, data, n, &v);
+  return v;
+}
+uint32_t mck_crc32c_value(const void* data, size_t n) {
+  uint32_t v = 0;
+  (void)mck_crc32c_value_r(data, n, &v);
+  return v;
+}
 uint32_t mck_builtin_checksum(int type, const void* data, size_t n) {
-  return scalar_u32(1, 0, data, n, type, 0, 0);
+  uint32_t v = 0;
+  (void)mck_builtin_checksum_r(type, data, n, &v);
+  return v;
 }
 uint32_t mck_builtin_checksum_with_last_byte(int type, const void* data, size_t n, char last_byte) {
-  return scalar_u32(1, 0, data, n, type, 1, last_byte);
+  uint32_t v = 0;
+  (void)mck_builtin_checksum_with_last_byte_r(type, data, n, last_byte, &v);
+  return v;
+}
+uint64_t mck_xxh3_64(const void* data, size_t n) {
+  uint64_t v = 0;
+  (void)mck_xxh3_64_r(data, n, &v);
+  return v;
+}
+uint64_t mck_np_hash64(const void* data, size_t n, uint64_t seed) {
+  uint64_t v = 0;
+  (void)mck_np_hash64_r(data, n, seed, &v);
+  return v;
 }
 int mck_np_hash64_batch(const mck_spans* spans, uint64_t seed, uint64_t* out, mck_stream_t stream) {
   t_err[0] = 0;
@@ -791,48 +951,6 @@ int mck_kv_protect_verify_batch(int kind, const mck_spans* keys, const mck_spans
   return launch_xph3(op, values->count, kSeedV, reinterpret_cast<hipStream_t>(stream));
 }
 
-uint64_t mck_np_hash64(const void* data, size_t n, uint64_t seed) {
-  t_err[0] = 0;
-  if (!data && n) {
-    set_err("data is NULL");
-    return 0;
-  }
-  if (n > 0xFFFFFFFFull) {
-    set_err("span too long for the scalar shim");
-    return 0;
-  }
-  uint8_t* d_data;
-  void* d_out;
-  if (stage_in(data, n, &d_data, &d_out)) return 0;
-  const mck_spans s{d_data, nullptr, nullptr, 0, (uint32_t)n, 1};
-  uint64_t v = 0;
-  if (mck_np_hash64_batch(&s, seed, static_cast<uint64_t*>(d_out), nullptr) == 0 &&
-      hipMemcpy(&v, d_out, 8, hipMemcpyDeviceToHost) != hipSuccess)
-    set_err("hipMemcpy failed");
-  return v;
-}
-
-uint64_t mck_xxh3_64(const void* data, size_t n) {
-  t_err[0] = 0;
-  if (!data && n) {
-    set_err("data is NULL");
-    return 0;
-  }
-  if (n > 0xFFFFFFFFull) {
-    set_err("span too long for the scalar shim");
-    return 0;
-  }
-  uint8_t* d_data;
-  void* d_out;
-  if (stage_in(data, n, &d_data, &d_out)) return 0;
-  const mck_spans s{d_data, nullptr, nullptr, 0, (uint32_t)n, 1};
-  uint64_t v = 0;
-  if (mck_xxh3_64_batch(&s, static_cast<uint64_t*>(d_out), nullptr) == 0 &&
-      hipMemcpy(&v, d_out, 8, hipMemcpyDeviceToHost) != hipSuccess)
-    set_err("hipMemcpy failed");
-  return v;
-}
-
 // ---- partitioning + host-resident multi-GPU pipeline -----------------------
 int mck_partition_spans(const uint32_t* host_lengths, uint32_t count, uint32_t length, int parts, uint32_t* first) {
   t_err[0] = 0;
@@ -874,62 +992,149 @@ struct HostJob {
   uint32_t len(uint32_t i) const { return lens ? lens[i] : length; }
 };
 
-// One device's share [lo, hi): spans must be sorted by offset.  Chunks of
-// spans are staged through two device buffers on two streams, so the H2D
-// copy of one chunk overlaps the kernel of the other.
-int run_device_share(int dev, const HostJob& J, uint32_t lo, uint32_t hi) {
+// Per-device staging of the host-resident pipeline, allocated on first use
+// and reused by every later call (grown when a call needs more): kHostSlots
+// slots, each a stream + device chunk/descriptor/result buffers + pinned
+// descriptor/result buffers.  One call at a time per device (the mutex);
+// mck_host_pipeline_release() frees it.
+constexpr int kHostSlots = 2;
+struct HostSlot {
+  hipStream_t st = nullptr;
+  uint8_t* d_data = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t* d_len = nullptr;
+  uint64_t* d_res = nullptr;
+  uint64_t* h_off = nullptr;
+  uint32_t* h_len = nullptr;
+  uint64_t* h_res = nullptr;
+  uint32_t first = 0, n = 0;  // spans of the chunk in flight
+};
+struct HostPipe {
+  std::mutex mu;
+  size_t cap = 0;          // chunk bytes per slot
+  uint32_t max_spans = 0;  // descriptor/result entries per slot
+  HostSlot slot[kHostSlots];
+};
+static HostPipe g_host[kMaxDev];
+
+// Free every buffer of a pipeline (caller holds its mutex, device is current).
+static void host_pipe_free(HostPipe& p) {
+  for (HostSlot& s : p.slot) {
+    if (s.st) (void)hipStreamSynchronize(s.st);
+    if (s.st) (void)hipStreamDestroy(s.st);
+    if (s.d_data) (void)hipFree(s.d_data);
+    if (s.d_off) (void)hipFree(s.d_off);
+    if (s.d_len) (void)hipFree(s.d_len);
+    if (s.d_res) (void)hipFree(s.d_res);
+    if (s.h_off) (void)hipHostFree(s.h_off);
+    if (s.h_len) (void)hipHostFree(s.h_len);
+    if (s.h_res) (void)hipHostFree(s.h_res);
+    s = HostSlot{};
+  }
+  p.cap = 0;
+  p.max_spans = 0;
+}
+
+// Make the pipeline hold at least cap chunk bytes and max_spans entries per
+// slot.  On failure everything is freed (no partial state survives).
+static int host_pipe_reserve(HostPipe& p, size_t cap, uint32_t max_spans) {
+  if (p.cap >= cap && p.max_spans >= max_spans && p.slot[0].st) return MCK_OK;
+  cap = std::max(cap, p.cap);
+  max_spans = std::max(max_spans, p.max_spans);
+  host_pipe_free(p);
+  hipError_t e = hipSuccess;
+  const char* what = "";
+  auto ok = [&](hipError_t r, const char* w) {
+    if (r != hipSuccess && e == hipSuccess) {
+      e = r;
+      what = w;
+    }
+    return e == hipSuccess;
+  };
+  for (HostSlot& s : p.slot) {
+    if (!ok(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking), "hipStreamCreate") ||
+        !ok(hipMalloc(&s.d_data, cap + 64), "hipMalloc(chunk)") ||
+        !ok(hipMalloc(&s.d_off, (size_t)max_spans * 8), "hipMalloc(offsets)") ||
+        !ok(hipMalloc(&s.d_len, (size_t)max_spans * 4), "hipMalloc(lengths)") ||
+        !ok(hipMalloc(&s.d_res, (size_t)max_spans * 8), "hipMalloc(results)") ||
+        !ok(hipHostMalloc(&s.h_off, (size_t)max_spans * 8, hipHostMallocDefault), "hipHostMalloc(offsets)") ||
+        !ok(hipHostMalloc(&s.h_len, (size_t)max_spans * 4, hipHostMallocDefault), "hipHostMalloc(lengths)") ||
+        !ok(hipHostMalloc(&s.h_res, (size_t)max_spans * 8, hipHostMallocDefault), "hipHostMalloc(results)"))
+      break;
+  }
+  if (e != hipSuccess) {
+    host_pipe_free(p);
+    set_err("%s failed: %s (chunk %zu B, %u spans per slot)", what, hipGetErrorString(e), cap, max_spans);
+    return e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation ? MCK_ENOMEM : MCK_EHIP;
+  }
+  p.cap = cap;
+  p.max_spans = max_spans;
+  return MCK_OK;
+}
+
+// One device's share [lo, hi) of a host batch (spans sorted by offset):
+// chunks of spans are staged through the slots round-robin, each on its own
+// stream, so the H2D copy of one chunk overlaps the kernel of the previous
+// one; results come back D2H into pinned memory and are copied out when the
+// slot is reused.  Every exit path leaves no copy in flight.
+static int run_device_share(int dev, const HostJob& J, uint32_t lo, uint32_t hi) {
   MCK_HIP(hipSetDevice(dev));
   if (lo >= hi) return MCK_OK;
   int rc = current_device(nullptr, nullptr);
   if (rc) return rc;
-  // longest span bounds the chunk
+  // the longest span bounds the chunk
   size_t cap = J.chunk_bytes;
-  for (uint32_t i = lo; i < hi; i++) cap = std::max<size_t>(cap, J.len(i) + 32);
+  for (uint32_t i = lo; i < hi; i++) cap = std::max<size_t>(cap, (size_t)J.len(i) + 32);
   const uint32_t max_spans = (uint32_t)std::min<uint64_t>(hi - lo, 1u << 20);
-  struct Slot {
-    hipStream_t st = nullptr;
-    uint8_t* d_data = nullptr;
-    uint64_t* d_off = nullptr;
-    uint32_t* d_len = nullptr;
-    void* d_res = nullptr;
-    uint64_t* h_off = nullptr;
-    uint32_t* h_len = nullptr;
-    void* h_res = nullptr;
-    uint32_t first = 0, n = 0;
-  } slot[2];
+  HostPipe& P = g_host[dev];
+  std::lock_guard<std::mutex> lock(P.mu);
+  if ((rc = host_pipe_reserve(P, cap, max_spans))) return rc;
   const size_t res_sz = J.kind == MCK_kXXH3 ? 8 : 4;
-  for (auto& s : slot) {
-    MCK_HIP(hipStreamCreateWithFlags(&s.st, hipStreamNonBlocking));
-    MCK_HIP(hipMalloc(&s.d_data, cap + 64));
-    MCK_HIP(hipMalloc(&s.d_off, (size_t)max_spans * 8));
-    MCK_HIP(hipMalloc(&s.d_len, (size_t)max_spans * 4));
-    MCK_HIP(hipMalloc(&s.d_res, (size_t)max_spans * res_sz));
-    MCK_HIP(hipHostMalloc(&s.h_off, (size_t)max_spans * 8, hipHostMallocDefault));
-    MCK_HIP(hipHostMalloc(&s.h_len, (size_t)max_spans * 4, hipHostMallocDefault));
-    MCK_HIP(hipHostMalloc(&s.h_res, (size_t)max_spans * res_sz, hipHostMallocDefault));
-  }
-  auto drain = [&](Slot& s) -> int {
+  auto drain = [&](HostSlot& s) -> int {
     if (!s.n) return MCK_OK;
-    MCK_HIP(hipStreamSynchronize(s.st));
-    if (J.kind == MCK_kXXH3)
-      memcpy(J.out64 + s.first, s.h_res, (size_t)s.n * 8);
-    else
-      memcpy(J.out32 + s.first, s.h_res, (size_t)s.n * 4);
+    const hipError_t e = hipStreamSynchronize(s.st);
+    const uint32_t first = s.first, n = s.n;
     s.n = 0;
+    if (e != hipSuccess) {
+      set_err("hipStreamSynchronize failed: %s", hipGetErrorString(e));
+      return MCK_EHIP;
+    }
+    if (J.kind == MCK_kXXH3)
+      memcpy(J.out64 + first, s.h_res, (size_t)n * 8);
+    else
+      memcpy(J.out32 + first, s.h_res, (size_t)n * 4);
+    return MCK_OK;
+  };
+  auto quiesce = [&] {  // error exit: wait for every slot, keep the first error
+    for (HostSlot& s : P.slot) {
+      if (s.st) (void)hipStreamSynchronize(s.st);
+      s.n = 0;
+    }
+  };
+  auto issue = [&](HostSlot& s, uint32_t i, uint32_t j, uint64_t start, uint64_t endb) -> int {
+    MCK_HIP(hipMemcpyAsync(s.d_data, J.base + start, endb - start, hipMemcpyHostToDevice, s.st));
+    MCK_HIP(hipMemcpyAsync(s.d_off, s.h_off, (size_t)(j - i) * 8, hipMemcpyHostToDevice, s.st));
+    MCK_HIP(hipMemcpyAsync(s.d_len, s.h_len, (size_t)(j - i) * 4, hipMemcpyHostToDevice, s.st));
+    const mck_spans sp{s.d_data, s.d_off, s.d_len, 0, 0, j - i};
+    const int r = J.kind == MCK_kXXH3
+                      ? mck_xxh3_64_batch(&sp, s.d_res, reinterpret_cast<mck_stream_t>(s.st))
+                      : mck_crc32c_batch(&sp, nullptr, J.flags, reinterpret_cast<uint32_t*>(s.d_res),
+                                         reinterpret_cast<mck_stream_t>(s.st));
+    if (r) return r;
+    MCK_HIP(hipMemcpyAsync(s.h_res, s.d_res, (size_t)(j - i) * res_sz, hipMemcpyDeviceToHost, s.st));
     return MCK_OK;
   };
   uint32_t i = lo;
-  int k = 0;
-  while (i < hi) {
-    Slot& s = slot[k & 1];
-    if ((rc = drain(s))) return rc;
-    // gather spans [i, j) whose covering byte range fits the chunk
+  for (int k = 0; i < hi; k++) {
+    HostSlot& s = P.slot[k % kHostSlots];
+    if ((rc = drain(s))) break;
+    // spans [i, j) whose covering byte range fits the chunk
     const uint64_t start = J.off(i);
     uint32_t j = i;
     uint64_t endb = start;
-    while (j < hi && j - i < max_spans) {
+    while (j < hi && j - i < P.max_spans) {
       const uint64_t e = J.off(j) + J.len(j);
-      if (j > i && e - start > cap) break;
+      if (j > i && std::max(endb, e) - start > P.cap) break;
       endb = std::max(endb, e);
       s.h_off[j - i] = J.off(j) - start;
       s.h_len[j - i] = J.len(j);
@@ -937,31 +1142,18 @@ int run_device_share(int dev, const HostJob& J, uint32_t lo, uint32_t hi) {
     }
     s.first = i;
     s.n = j - i;
-    MCK_HIP(hipMemcpyAsync(s.d_data, J.base + start, endb - start, hipMemcpyHostToDevice, s.st));
-    MCK_HIP(hipMemcpyAsync(s.d_off, s.h_off, (size_t)s.n * 8, hipMemcpyHostToDevice, s.st));
-    MCK_HIP(hipMemcpyAsync(s.d_len, s.h_len, (size_t)s.n * 4, hipMemcpyHostToDevice, s.st));
-    const mck_spans sp{s.d_data, s.d_off, s.d_len, 0, 0, s.n};
-    rc = J.kind == MCK_kXXH3
-             ? mck_xxh3_64_batch(&sp, static_cast<uint64_t*>(s.d_res), reinterpret_cast<mck_stream_t>(s.st))
-             : mck_crc32c_batch(&sp, nullptr, J.flags, static_cast<uint32_t*>(s.d_res),
-                                reinterpret_cast<mck_stream_t>(s.st));
-    if (rc) return rc;
-    MCK_HIP(hipMemcpyAsync(s.h_res, s.d_res, (size_t)s.n * res_sz, hipMemcpyDeviceToHost, s.st));
+    if ((rc = issue(s, i, j, start, endb))) break;
     i = j;
-    k++;
   }
-  for (auto& s : slot)
-    if ((rc = drain(s))) return rc;
-  for (auto& s : slot) {
-    (void)hipStreamDestroy(s.st);
-    (void)hipFree(s.d_data);
-    (void)hipFree(s.d_off);
-    (void)hipFree(s.d_len);
-    (void)hipFree(s.d_res);
-    (void)hipHostFree(s.h_off);
-    (void)hipHostFree(s.h_len);
-    (void)hipHostFree(s.h_res);
+  if (rc) {
+    quiesce();
+    return rc;
   }
+  for (HostSlot& s : P.slot)
+    if ((rc = drain(s))) {
+      quiesce();
+      return rc;
+    }
   return MCK_OK;
 }
 
@@ -994,7 +1186,7 @@ int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* hos
   if (ndev <= 0) {
     devs.push_back(prev);
   } else {
-    for (int d = 0; d < std::min(ndev, have); d++) devs.push_back(d);
+    for (int d = 0; d < std::min(ndev, std::min(have, kMaxDev)); d++) devs.push_back(d);
   }
   ndev = (int)devs.size();
   if (!chunk_bytes) chunk_bytes = 256u << 20;
@@ -1009,21 +1201,39 @@ int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* hos
             flags & MCK_F_MASK, chunk_bytes, out32, out64};
   std::vector<int> rcs(ndev, 0);
   std::vector<std::string> errs(ndev);
-  std::vector<std::thread> th;
-  for (int d = 0; d < ndev; d++)
-    th.emplace_back([&, d] {
-      rcs[d] = run_device_share(devs[d], J, first[d], first[d + 1]);
-      if (rcs[d]) errs[d] = t_err;
-    });
-  for (auto& t : th) t.join();
+  if (ndev == 1) {
+    rcs[0] = run_device_share(devs[0], J, first[0], first[1]);
+    if (rcs[0]) errs[0] = t_err;
+  } else {
+    std::vector<std::thread> th;
+    for (int d = 0; d < ndev; d++)
+      th.emplace_back([&, d] {
+        rcs[d] = run_device_share(devs[d], J, first[d], first[d + 1]);
+        if (rcs[d]) errs[d] = t_err;
+      });
+    for (auto& t : th) t.join();
+  }
   (void)hipSetDevice(prev);
   for (int d = 0; d < ndev; d++)
     if (rcs[d]) {
-      set_err("device %d: %s", d, errs[d].c_str());
+      set_err("device %d: %s", devs[d], errs[d].c_str());
       return rcs[d];
     }
   if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return MCK_OK;
+}
+
+void mck_host_pipeline_release(void) {
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  for (int d = 0; d < kMaxDev; d++) {
+    HostPipe& P = g_host[d];
+    std::lock_guard<std::mutex> lock(P.mu);
+    if (!P.slot[0].st && !P.cap) continue;
+    if (hipSetDevice(d) != hipSuccess) continue;
+    host_pipe_free(P);
+  }
+  (void)hipSetDevice(prev);
 }
 
 }  // extern "C"

@@ -534,11 +534,16 @@ __device__ __forceinline__ void wal_copy_issue(WalCopyPass& p, const WalFrag& f,
 #ifndef MCK_WAL_COPY_NTST
 #define MCK_WAL_COPY_NTST 1
 #endif
-// 16 aligned output bytes, non-temporal (written once, never re-read here):
-// walwrite 875 vs 867 GiB/s, same box, alternating runs (-DMCK_WAL_COPY_NTST=0
-// for plain stores)
+// 16 aligned output bytes.  The writer's log stream is written once and not
+// re-read by the engine, so its stores are non-temporal (walwrite 875 vs 867
+// GiB/s, one alternating pair on one box -- inside the 864-887 spread of the
+// 8-piece config, so "not slower" rather than a measured gain;
+// -DMCK_WAL_COPY_NTST=0 for plain stores).  The GATHER direction keeps
+// plain stores: its reassembled records are read straight back by the
+// record-checksum XXH3 batch.
+template <bool GATHER>
 __device__ __forceinline__ void wal_store16(uint8_t* p, uint4 v) {
-  if (MCK_WAL_COPY_NTST) {
+  if (MCK_WAL_COPY_NTST && !GATHER) {
     span_u32x4 x = {v.x, v.y, v.z, v.w};
     __builtin_nontemporal_store(x, reinterpret_cast<span_u32x4*>(p));
   } else {
@@ -546,9 +551,10 @@ __device__ __forceinline__ void wal_store16(uint8_t* p, uint4 v) {
   }
 }
 
+template <bool GATHER>
 __device__ __forceinline__ void wal_copy_store(const WalCopyPass& p, uint8_t* __restrict__ out) {
   if (p.hv) out[p.ha] = p.hb;
-  if (p.cv) wal_store16(out + p.ca, p.v);
+  if (p.cv) wal_store16<GATHER>(out + p.ca, p.v);
   if (p.tv) out[p.ta] = p.tb;
 }
 
@@ -560,7 +566,7 @@ __device__ __forceinline__ void wal_copy_rest(const WalCopyPass& p, const WalFra
   for (uint64_t a = p.ha + 64; a < p.head_end; a += 64)
     out[a] = GATHER ? src[f.src_off + (a - p.pay)] : wal_out_byte(f, crc, log_number, hs, src, a);
   for (uint64_t c = p.ca + 16ull * 64; c < p.body1; c += 16ull * 64)
-    wal_store16(out + c, wal_chunk_load(src, f.src_off + (c - p.pay)));
+    wal_store16<GATHER>(out + c, wal_chunk_load(src, f.src_off + (c - p.pay)));
 }
 
 // GATHER: the reverse direction for recovery -- copy each fragment's
@@ -585,7 +591,7 @@ __global__ __launch_bounds__(256) void k_wal_copy(const uint8_t* __restrict__ sr
     const uint32_t nx = more ? fn : fi;
     const WalFrag f2 = frags[nx];
     const uint32_t crc2 = GATHER ? 0u : crcs[nx];
-    wal_copy_store(p, out);
+    wal_copy_store<GATHER>(p, out);
     wal_copy_rest<GATHER>(p, f, crc, log_number, src, out);
     if (!more) break;
     fi = fn;

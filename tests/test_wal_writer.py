@@ -3,7 +3,10 @@ exactly as log::Writer::AddRecord does (compared with the test-side Python
 restatement of db/log_writer.cc, tests/formats.py WalWriter), and the device
 writes the same bytes -- legacy and recyclable headers, records spanning
 blocks, empty records, block-trailer padding, an initial block offset."""
+import os
 import random
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -79,6 +82,7 @@ def test_wal_write_batch_pieces_bit_exact(gpu, oracle, recycle):
     import torch
 
     import speedb_amd as S
+    from speedb_amd import _lib
     rng = np.random.default_rng(5)
     lens = rng.integers(0, 700, size=24000)
     lens[rng.integers(0, len(lens), size=40)] = rng.integers(30000, 70000, size=40)  # block-spanning ones
@@ -90,6 +94,10 @@ def test_wal_write_batch_pieces_bit_exact(gpu, oracle, recycle):
     for o, n in zip(offs, lens):
         w.add_record(src[o:o + n])
     dev = torch.frombuffer(bytearray(src + bytes(64)), dtype=torch.uint8).to("cuda")
+    frags, nf, _, _ = S.wal_plan(offs, [int(n) for n in lens], start % 32768, recycle)
+    pieces = _lib.lib.mck_wal_write_pieces(nf)
+    if os.environ.get("MCK_WAL_PIECES") != "1":
+        assert pieces >= 2, (nf, pieces)  # the overlapped multi-piece path really runs
     wr = S.WalBatchWriter(log_number=91, recycle_log_files=recycle, block_offset=start)
     out = wr.AddRecords(dev, offs, [int(n) for n in lens])
     got = out.cpu().numpy().tobytes()  # the caller's stream: joined after the side stream's copies
@@ -98,6 +106,41 @@ def test_wal_write_batch_pieces_bit_exact(gpu, oracle, recycle):
     if got != want:
         i = next(k for k in range(len(got)) if got[k] != want[k])
         raise AssertionError(f"first difference at stream offset {i + start}")
+
+
+@pytest.mark.gpu
+def test_wal_write_batch_single_piece_subprocess(gpu):
+    """The same group commit with MCK_WAL_PIECES=1 (read once per process):
+    the single-launch path, in a child process, stays byte-exact too."""
+    if os.environ.get("MCK_WAL_PIECES") == "1":
+        pytest.skip("already running single-piece")
+    env = dict(os.environ, MCK_WAL_PIECES="1")
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        os.path.join(here, "test_wal_writer.py") + "::test_wal_write_batch_pieces_bit_exact"],
+                       env=env, cwd=os.path.dirname(here), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "2 passed" in r.stdout, r.stdout[-500:]
+
+
+@pytest.mark.gpu
+def test_wal_write_batch_rejects_misaligned_out(gpu):
+    import torch
+
+    import speedb_amd as S
+    from speedb_amd import _lib
+    src = torch.zeros(4096, dtype=torch.uint8, device="cuda")
+    frags, nf, nbytes, _ = S.wal_plan([0], [100])
+    d_frags = torch.frombuffer(bytearray(bytes(frags)), dtype=torch.uint8).to("cuda")
+    crc = torch.zeros(4, dtype=torch.int32, device="cuda")
+    out = torch.zeros(nbytes + 64, dtype=torch.uint8, device="cuda")
+    rc = _lib.lib.mck_wal_write_batch(src.data_ptr(), d_frags.data_ptr(), nf, 0, crc.data_ptr(),
+                                      out.data_ptr() + 1, None)
+    assert rc == -1 and b"16-byte" in _lib.lib.mck_last_error()
+    rc = _lib.lib.mck_wal_gather_batch(src.data_ptr(), d_frags.data_ptr(), nf, out.data_ptr() + 4, None)
+    assert rc == -1
+    assert _lib.lib.mck_wal_write_batch(src.data_ptr(), d_frags.data_ptr(), nf, 0, crc.data_ptr(),
+                                        out.data_ptr(), None) == 0
 
 
 @pytest.mark.parametrize("recycle", [False, True])
