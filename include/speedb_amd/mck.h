@@ -300,6 +300,79 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes,
                          uint32_t log_number, mck_wal_block_result* results,
                          mck_stream_t stream);
 
+/* ---- log::Reader, the whole log (db/log_reader.cc:69-584) ----------------- */
+
+/* WALRecoveryMode (include/rocksdb/options.h) */
+#define MCK_WAL_kTolerateCorruptedTailRecords 0
+#define MCK_WAL_kAbsoluteConsistency 1
+#define MCK_WAL_kPointInTimeRecovery 2
+#define MCK_WAL_kSkipAnyCorruptedRecords 3
+
+/* Reporter::Corruption reasons (the Status::Corruption messages of
+ * db/log_reader.cc; mck_wal_reason_string gives the text) */
+#define MCK_WAL_R_CHECKSUM_MISMATCH 1
+#define MCK_WAL_R_BAD_RECORD_LENGTH 2
+#define MCK_WAL_R_TRUNCATED_HEADER 3
+#define MCK_WAL_R_TRUNCATED_BODY 4
+#define MCK_WAL_R_ERROR_IN_MIDDLE 5
+#define MCK_WAL_R_MISSING_START_1 6
+#define MCK_WAL_R_MISSING_START_2 7
+#define MCK_WAL_R_PARTIAL_WITHOUT_END_1 8
+#define MCK_WAL_R_PARTIAL_WITHOUT_END_2 9
+#define MCK_WAL_R_TRAILING_DATA 10
+#define MCK_WAL_R_TS_INTERSPERSED 11
+#define MCK_WAL_R_TS_DECODE 12
+#define MCK_WAL_R_UNKNOWN_TYPE_BASE 256 /* + the record type */
+
+/* One Reporter::Corruption(bytes, reason) call. */
+typedef struct mck_wal_report {
+  uint64_t offset; /* file offset of the physical record being read      */
+  uint64_t bytes;  /* the dropped bytes the reader reports              */
+  int32_t reason;  /* MCK_WAL_R_*                                        */
+  uint32_t reserved;
+} mck_wal_report;
+
+/* Outputs of mck_wal_read_records.  Every array pointer may be NULL (counts
+ * only); the *_cap fields give the array sizes. */
+typedef struct mck_wal_read_out {
+  mck_wal_fragment* frags;    /* payload fragments of the returned records */
+  uint64_t frag_cap;
+  uint64_t nfrags;
+  uint64_t* rec_offsets;      /* record r = [rec_offsets[r], +rec_lengths[r])
+                                 of the contiguous record buffer           */
+  uint32_t* rec_lengths;
+  uint64_t* rec_file_offsets; /* file offset of the record's first physical
+                                 record (LastRecordOffset)                */
+  uint64_t rec_cap;
+  uint64_t nrecords;
+  uint64_t records_bytes;     /* size of the contiguous record buffer      */
+  mck_wal_report* reports;    /* in order; up to report_cap are stored     */
+  uint64_t report_cap;
+  uint64_t nreports;
+  uint64_t dropped_bytes;     /* sum of the reported bytes                 */
+  uint64_t end_offset;        /* where ReadRecord returned false           */
+} mck_wal_read_out;
+
+/* log::Reader (checksum = true, no WAL compression) reading a whole WAL
+ * image in HOST memory: ReadRecord (db/log_reader.cc:69-321) called until it
+ * returns false, over ReadPhysicalRecord (:450-584) and ReadMore, in the
+ * given WALRecoveryMode.  The record CRCs are NOT computed here: `verified`
+ * is the host copy of mck_wal_verify_batch's per-block results for the same
+ * image (the device's verdict on every physical record); NULL trusts every
+ * CRC.  Returns the logical records (as fragments of one contiguous buffer,
+ * for mck_wal_gather_batch) and every corruption the reader would report,
+ * with the bytes it drops.  A kSetCompressionType record (compressed WAL):
+ * MCK_ENOTSUP.  Results that do not belong to the image: MCK_EINVAL. */
+int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t log_number,
+                         int recovery_mode,
+                         const mck_wal_block_result* verified,
+                         mck_wal_read_out* out);
+
+/* Text of a MCK_WAL_R_* reason ("checksum mismatch", "unknown record type
+ * 101", ...); Status::Corruption(reason).ToString() is "Corruption: " + it. */
+const char* mck_wal_reason_string(int reason);
+
+
 /* ---- long spans / whole files ----------------------- */
 
 /* Piece size of mck_crc32c_long (a multiple of the 4 KiB kernel round). */

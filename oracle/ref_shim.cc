@@ -8,6 +8,8 @@
 // the golden fixtures under tests/golden/, and (c) as bench.py's
 // "reference" cpu_baseline on the GPU box's host cores.
 //
+// ChecksumModifierForContext is called from the reference's own header
+// (table/format.h, inline; its includes compile header-only).
 // The block-checksum dispatch (table/format.cc:578-645) lives in a file that
 // drags in the whole table layer, so it is restated here over the reference's
 // own crc32c:: and XXH* primitives; the WAL record CRC likewise restates
@@ -21,6 +23,7 @@
 #include <vector>
 
 #include "db/kv_checksum.h"
+#include "table/format.h"
 #include "util/crc32c.h"
 #include "util/hash.h"
 #include "util/xxhash.h"
@@ -84,6 +87,11 @@ uint64_t ref_kv_protect(int mode, const void* key, size_t kn, const void* value,
   uint64_t r;
   memcpy(&r, buf, 8);  // EncodeFixed64 is little-endian
   return r;
+}
+
+// table/format.h:119-146, the reference's own inline function.
+uint32_t ref_context_modifier(uint32_t base_context_checksum, uint64_t offset) {
+  return ROCKSDB_NAMESPACE::ChecksumModifierForContext(base_context_checksum, offset);
 }
 
 // table/format.cc:578-602 over the reference primitives.

@@ -105,6 +105,8 @@ SIGNATURES = [
     ("mck_wal_list_records", ctypes.c_int,
      [vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint64, vp, vp, vp, ctypes.c_uint64, vp, vp]),
     ("mck_wal_gather_batch", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp]),
+    ("mck_wal_read_records", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, vp, vp]),
+    ("mck_wal_reason_string", ctypes.c_char_p, [ctypes.c_int]),
     ("mck_blob_list_records", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
     ("mck_blob_record_batch", ctypes.c_int,
      [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, vp, vp, vp]),

@@ -20,7 +20,7 @@ from __future__ import annotations
 import ctypes
 import enum
 from dataclasses import dataclass
-from typing import Optional
+from typing import NamedTuple, Optional
 
 from ._lib import check, lib, mck_spans, mck_wal_block_result
 
@@ -583,31 +583,139 @@ def wal_list_records(wal: bytes, log_number: int = 0):
     return frags, nf.value, offs[:nr.value], lens[:nr.value], nb.value
 
 
-def WalReadRecords(wal: bytes, log_number: int = 0, device=None, stream=None):
-    """Recovery on the device: every logical record of a WAL image
-    reassembled into one device buffer (mck_wal_gather_batch) and its
-    XXH3_64bits record checksum (ReadRecord's record_checksum) in one batch;
-    the physical records' CRCs per 32 KiB block (mck_wal_verify_batch).
-    Returns (records uint8 tensor, offsets, lengths, xxh3 uint64 numpy,
-    per-block verify results)."""
+class WALRecoveryMode(enum.IntEnum):
+    """include/rocksdb/options.h WALRecoveryMode"""
+    kTolerateCorruptedTailRecords = 0
+    kAbsoluteConsistency = 1
+    kPointInTimeRecovery = 2
+    kSkipAnyCorruptedRecords = 3
+
+
+class mck_wal_report(ctypes.Structure):
+    _fields_ = [("offset", ctypes.c_uint64), ("bytes", ctypes.c_uint64), ("reason", ctypes.c_int32),
+                ("reserved", ctypes.c_uint32)]
+
+
+class mck_wal_read_out(ctypes.Structure):
+    _fields_ = [("frags", ctypes.c_void_p), ("frag_cap", ctypes.c_uint64), ("nfrags", ctypes.c_uint64),
+                ("rec_offsets", ctypes.c_void_p), ("rec_lengths", ctypes.c_void_p),
+                ("rec_file_offsets", ctypes.c_void_p), ("rec_cap", ctypes.c_uint64),
+                ("nrecords", ctypes.c_uint64), ("records_bytes", ctypes.c_uint64),
+                ("reports", ctypes.c_void_p), ("report_cap", ctypes.c_uint64), ("nreports", ctypes.c_uint64),
+                ("dropped_bytes", ctypes.c_uint64), ("end_offset", ctypes.c_uint64)]
+
+
+class WalReadPlan(NamedTuple):
+    """What log::Reader returns and reports over a whole log (host side)."""
+    frags: object            # ctypes array of mck_wal_fragment
+    nfrags: int
+    rec_offsets: object      # numpy uint64: record r in the contiguous buffer
+    rec_lengths: object      # numpy uint32
+    rec_file_offsets: object  # numpy uint64: LastRecordOffset of record r
+    records_bytes: int
+    reports: list            # [(file offset, dropped bytes, reason text)]
+    dropped_bytes: int       # ReportCollector::dropped_bytes_
+    message: str             # ReportCollector::message_ ("Corruption: ..." appended)
+    end_offset: int
+
+
+def wal_read_records(wal: bytes, log_number: int = 0,
+                     recovery_mode: int = WALRecoveryMode.kTolerateCorruptedTailRecords,
+                     verified=None) -> WalReadPlan:
+    """log::Reader::ReadRecord until false (db/log_reader.cc:69-584) over a
+    host WAL image; ``verified`` = the per-block results of
+    mck_wal_verify_batch for the same image (numpy int32 [nblocks, 4] or a
+    tensor), None = trust every CRC."""
+    import numpy as np
+    buf = bytes(wal)
+    ver = None
+    if verified is not None:
+        v = verified.cpu().numpy() if hasattr(verified, "cpu") else np.asarray(verified)
+        ver = np.ascontiguousarray(v.astype(np.int32).reshape(-1, 4))
+    o = mck_wal_read_out()
+    vp = ver.ctypes.data if ver is not None else None
+    check(lib.mck_wal_read_records(buf, len(buf), log_number & 0xFFFFFFFF, int(recovery_mode), vp,
+                                   ctypes.addressof(o)), "mck_wal_read_records")
+    frags = (mck_wal_fragment * max(o.nfrags, 1))()
+    offs = np.zeros(max(o.nrecords, 1), dtype=np.uint64)
+    lens = np.zeros(max(o.nrecords, 1), dtype=np.uint32)
+    foffs = np.zeros(max(o.nrecords, 1), dtype=np.uint64)
+    reps = (mck_wal_report * max(o.nreports, 1))()
+    o2 = mck_wal_read_out(ctypes.addressof(frags), o.nfrags, 0, offs.ctypes.data, lens.ctypes.data,
+                          foffs.ctypes.data, o.nrecords, 0, 0, ctypes.addressof(reps), o.nreports)
+    check(lib.mck_wal_read_records(buf, len(buf), log_number & 0xFFFFFFFF, int(recovery_mode), vp,
+                                   ctypes.addressof(o2)), "mck_wal_read_records")
+    reports = [(r.offset, r.bytes, lib.mck_wal_reason_string(r.reason).decode()) for r in reps[:o2.nreports]]
+    return WalReadPlan(frags, o2.nfrags, offs[:o2.nrecords], lens[:o2.nrecords], foffs[:o2.nrecords],
+                       o2.records_bytes, reports, o2.dropped_bytes,
+                       "".join("Corruption: " + r[2] for r in reports), o2.end_offset)
+
+
+class WalRecovery(NamedTuple):
+    records: object          # device uint8 tensor: every record, back to back
+    rec_offsets: object
+    rec_lengths: object
+    rec_file_offsets: object
+    record_checksums: object  # numpy uint64 XXH3_64bits of every record
+    blocks: object           # device per-block verify results (or None)
+    reports: list
+    dropped_bytes: int
+    message: str
+
+    def Records(self):
+        """The records as bytes (what ReadRecord's *record holds, in order)."""
+        host = bytes(self.records.cpu().numpy().tobytes())
+        return [host[int(o):int(o) + int(n)] for o, n in zip(self.rec_offsets, self.rec_lengths)]
+
+
+def WalRecover(wal: bytes, log_number: int = 0,
+               recovery_mode: int = WALRecoveryMode.kTolerateCorruptedTailRecords,
+               device=None, stream=None, checksum: bool = True) -> WalRecovery:
+    """WAL recovery with the checksum work on the device:
+      1. mck_wal_verify_batch -- every physical record's CRC32C, per 32 KiB
+         block (ReadPhysicalRecord's check);
+      2. mck_wal_read_records -- ReadRecord's walk on the host over those
+         verdicts: records, drops and corruption reports of the given
+         WALRecoveryMode;
+      3. mck_wal_gather_batch + mck_xxh3_64_batch -- the records reassembled
+         into one device buffer and their record_checksum (XXH3_64bits)."""
     import numpy as np
     torch = _torch()
     dev = torch.device("cuda") if device is None else device
-    frags, nf, offs, lens, nbytes = wal_list_records(wal, log_number)
-    img = torch.frombuffer(bytearray(bytes(wal) + bytes(64)), dtype=torch.uint8).to(dev)
+    wal = bytes(wal)
+    img = torch.frombuffer(bytearray(wal + bytes(64)), dtype=torch.uint8).to(dev)
+    blocks = wal_verify_batch(img, len(wal), log_number, stream=stream) if (len(wal) and checksum) else None
+    plan = wal_read_records(wal, log_number, recovery_mode, blocks)
+    nbytes, nf = plan.records_bytes, plan.nfrags
     out = torch.zeros(nbytes + 64, dtype=torch.uint8, device=dev)
-    d_frags = torch.frombuffer(bytearray(bytes(frags)[:nf * ctypes.sizeof(mck_wal_fragment)] or b"\0"),
-                               dtype=torch.uint8).to(dev)
-    check(lib.mck_wal_gather_batch(img.data_ptr(), d_frags.data_ptr(), nf, out.data_ptr(), _stream(stream)),
-          "mck_wal_gather_batch")
-    sp = Spans(out, len(offs), offsets=torch.from_numpy(offs.astype(np.int64)).to(dev),
-               lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
-    x3 = xxh3_64_batch(sp, stream=stream).cpu().numpy().view(np.uint64) if len(offs) else np.zeros(0, np.uint64)
-    blocks = wal_verify_batch(img, len(wal), log_number, stream=stream) if len(wal) else None
-    return out[:nbytes], offs, lens, x3, blocks
+    if nf:
+        d_frags = torch.frombuffer(bytearray(bytes(plan.frags)[:nf * ctypes.sizeof(mck_wal_fragment)]),
+                                   dtype=torch.uint8).to(dev)
+        check(lib.mck_wal_gather_batch(img.data_ptr(), d_frags.data_ptr(), nf, out.data_ptr(), _stream(stream)),
+              "mck_wal_gather_batch")
+    offs, lens = plan.rec_offsets, plan.rec_lengths
+    if len(offs):
+        sp = Spans(out, len(offs), offsets=torch.from_numpy(offs.astype(np.int64)).to(dev),
+                   lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
+        x3 = xxh3_64_batch(sp, stream=stream).cpu().numpy().view(np.uint64)
+    else:
+        x3 = np.zeros(0, np.uint64)
+    return WalRecovery(out[:nbytes], offs, lens, plan.rec_file_offsets, x3, blocks, plan.reports,
+                       plan.dropped_bytes, plan.message)
 
 
-__all__ += ["wal_plan", "WalBatchWriter", "mck_wal_fragment", "wal_list_records", "WalReadRecords"]
+def WalReadRecords(wal: bytes, log_number: int = 0, device=None, stream=None):
+    """Recovery on the device (kTolerateCorruptedTailRecords): every logical
+    record reassembled into one device buffer and its XXH3_64bits record
+    checksum; the physical records' CRCs per 32 KiB block.  Returns (records
+    uint8 tensor, offsets, lengths, xxh3 uint64 numpy, per-block verify
+    results).  See WalRecover for the reports and other recovery modes."""
+    r = WalRecover(wal, log_number, device=device, stream=stream)
+    return r.records, r.rec_offsets, r.rec_lengths, r.record_checksums, r.blocks
+
+
+__all__ += ["wal_plan", "WalBatchWriter", "mck_wal_fragment", "wal_list_records", "WalReadRecords",
+            "WALRecoveryMode", "wal_read_records", "WalReadPlan", "WalRecover", "WalRecovery"]
 
 
 # ---------------------------------------------------------------------------

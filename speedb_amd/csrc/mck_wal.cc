@@ -2,8 +2,10 @@
 // fragmentation log::Writer::AddRecord performs (db/log_writer.cc:79-175),
 // on sizes only.  The bytes are written on the device by
 // mck_wal_write_batch (mck_engine.hip).
+#include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <vector>
 
 #include "../../include/speedb_amd/mck.h"
@@ -76,125 +78,334 @@ extern "C" int mck_wal_plan(const uint64_t* src_offsets, const uint32_t* lengths
   return MCK_OK;
 }
 
-// log::Reader::ReadRecord (db/log_reader.cc:69-321) + ReadPhysicalRecord
-// (:450-584) without the CRC check, on a host image.
+// ---------------------------------------------------------------------------
+// log::Reader (db/log_reader.cc) over a host WAL image, checksums supplied by
+// the device: ReadRecord (:69-321) called until it returns false, on top of
+// ReadPhysicalRecord (:450-584) and ReadMore (:400-448).  The reader reads the
+// file in kBlockSize pieces from offset 0, so "the buffer" is the unread rest
+// of the current 32 KiB block; a short last block sets eof_.  Every
+// Reporter::Corruption call is recorded as (offset, bytes, reason).
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr uint32_t kZeroType = 0, kSetCompressionType = 9, kUserDefinedTimestampSizeType = 10,
+                   kRecyclableUserDefinedTimestampSizeType = 11;
+// ReadPhysicalRecord's extra results (db/log_reader.h:136-156)
+constexpr int kEof = 12, kBadRecord = 13, kBadHeader = 14, kOldRecord = 15, kBadRecordLen = 16,
+              kBadRecordChecksum = 17;
+
+struct WalReader {
+  const uint8_t* d;
+  uint64_t nbytes;
+  uint32_t log_number;
+  int mode;
+  const mck_wal_block_result* verified;
+  // buffer_ = [buf_off, buf_off + buf_size) of the file
+  uint64_t buf_off = 0, buf_size = 0, end_of_buffer_offset = 0;
+  bool eof = false, recycled = false, first_record_read = false;
+  int err = MCK_OK;
+  std::vector<mck_wal_report> reports;
+  uint64_t dropped = 0;
+
+  void report(uint64_t off, uint64_t bytes, int reason) {
+    reports.push_back(mck_wal_report{off, bytes, reason, 0});
+    dropped += bytes;
+  }
+  bool strict() const {  // kAbsoluteConsistency / kPointInTimeRecovery
+    return mode == MCK_WAL_kAbsoluteConsistency || mode == MCK_WAL_kPointInTimeRecovery;
+  }
+
+  // :400-448 ReadMore
+  bool read_more(uint64_t* drop_size, int* error) {
+    if (!eof) {
+      const uint64_t n = std::min<uint64_t>(MCK_WAL_kBlockSize, nbytes - end_of_buffer_offset);
+      buf_off = end_of_buffer_offset;
+      buf_size = n;
+      end_of_buffer_offset += n;
+      if (n < MCK_WAL_kBlockSize) eof = true;
+      return true;
+    }
+    if (buf_size) {  // a truncated header at the end of the file
+      *drop_size = buf_size;
+      buf_size = 0;
+      *error = kBadHeader;
+      return false;
+    }
+    *error = kEof;
+    return false;
+  }
+
+  // the device's verdict on the record whose header is at file offset h
+  bool crc_ok(uint64_t h) {
+    if (!verified) return true;
+    const mck_wal_block_result& r = verified[h / MCK_WAL_kBlockSize];
+    const uint32_t o = (uint32_t)(h % MCK_WAL_kBlockSize);
+    if (o < r.stop_offset) return true;
+    if (o == r.stop_offset && r.status == MCK_WAL_BAD_CHECKSUM) return false;
+    err = MCK_EINVAL;  // the results are not this image's
+    return false;
+  }
+
+  // :450-584 ReadPhysicalRecord; *frag = (file offset, length) of the payload
+  int read_physical(uint64_t* frag_off, uint32_t* frag_len, uint64_t* drop_size) {
+    for (;;) {
+      if (buf_size < MCK_WAL_kHeaderSize) {
+        int r = kEof;
+        if (!read_more(drop_size, &r)) return r;
+        continue;
+      }
+      const uint8_t* h = d + buf_off;
+      const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
+      const uint32_t type = h[6];
+      uint32_t hs = MCK_WAL_kHeaderSize;
+      if ((type >= 5 && type <= 8) || type == kRecyclableUserDefinedTimestampSizeType) {
+        if (end_of_buffer_offset - buf_size == 0) recycled = true;
+        hs = MCK_WAL_kRecyclableHeaderSize;
+        if (buf_size < hs) {
+          int r = kEof;
+          if (!read_more(drop_size, &r)) return r;
+          continue;
+        }
+        const uint32_t ln = (uint32_t)h[7] | ((uint32_t)h[8] << 8) | ((uint32_t)h[9] << 16) | ((uint32_t)h[10] << 24);
+        if (ln != log_number) return kOldRecord;
+      }
+      if (hs + (uint64_t)length > buf_size) {
+        *drop_size = buf_size;
+        buf_size = 0;
+        return kBadRecordLen;
+      }
+      if (type == kZeroType && length == 0) {
+        buf_size = 0;
+        return kBadRecord;
+      }
+      if (!crc_ok(buf_off)) {
+        *drop_size = buf_size;
+        buf_size = 0;
+        return kBadRecordChecksum;
+      }
+      *frag_off = buf_off + hs;
+      *frag_len = length;
+      buf_off += hs + length;
+      buf_size -= hs + length;
+      return (int)type;
+    }
+  }
+};
+
+}  // namespace
+
+extern "C" const char* mck_wal_reason_string(int reason) {
+  switch (reason) {
+    case MCK_WAL_R_CHECKSUM_MISMATCH: return "checksum mismatch";
+    case MCK_WAL_R_BAD_RECORD_LENGTH: return "bad record length";
+    case MCK_WAL_R_TRUNCATED_HEADER: return "truncated header";
+    case MCK_WAL_R_TRUNCATED_BODY: return "truncated record body";
+    case MCK_WAL_R_ERROR_IN_MIDDLE: return "error in middle of record";
+    case MCK_WAL_R_MISSING_START_1: return "missing start of fragmented record(1)";
+    case MCK_WAL_R_MISSING_START_2: return "missing start of fragmented record(2)";
+    case MCK_WAL_R_PARTIAL_WITHOUT_END_1: return "partial record without end(1)";
+    case MCK_WAL_R_PARTIAL_WITHOUT_END_2: return "partial record without end(2)";
+    case MCK_WAL_R_TRAILING_DATA: return "error reading trailing data";
+    case MCK_WAL_R_TS_INTERSPERSED: return "user-defined timestamp size record interspersed partial record";
+    case MCK_WAL_R_TS_DECODE: return "could not decode user-defined timestamp size record";
+    default:
+      if (reason >= MCK_WAL_R_UNKNOWN_TYPE_BASE && reason < MCK_WAL_R_UNKNOWN_TYPE_BASE + 256) {
+        static thread_local char buf[40];
+        snprintf(buf, sizeof buf, "unknown record type %u", (unsigned)(reason - MCK_WAL_R_UNKNOWN_TYPE_BASE));
+        return buf;
+      }
+      return "";
+  }
+}
+
+extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t log_number, int recovery_mode,
+                                    const mck_wal_block_result* verified, mck_wal_read_out* out) {
+  mck_internal_set_error("");
+  if ((!wal && nbytes) || !out) {
+    mck_internal_set_error("wal / out is NULL");
+    return MCK_EINVAL;
+  }
+  if (recovery_mode < MCK_WAL_kTolerateCorruptedTailRecords || recovery_mode > MCK_WAL_kSkipAnyCorruptedRecords) {
+    mck_internal_set_error("unknown WALRecoveryMode");
+    return MCK_EINVAL;
+  }
+  WalReader R{static_cast<const uint8_t*>(wal), nbytes, log_number, recovery_mode, verified};
+  std::vector<mck_wal_fragment> fr;
+  std::vector<uint64_t> roff, rfile;
+  std::vector<uint32_t> rlen;
+  uint64_t dst = 0;             // end of the reassembled buffer
+  uint64_t cur_start = 0;       // dst offset of scratch (the record being assembled)
+  uint64_t cur_file = 0;        // file offset of its first physical record
+  size_t cur_first_frag = 0;    // its first fragment in fr
+  bool in_fragmented_record = false;
+  auto scratch_size = [&] { return dst - cur_start; };
+  auto scratch_clear = [&] {  // scratch->clear(): its fragments are dropped
+    fr.resize(cur_first_frag);
+    dst = cur_start;
+  };
+  auto scratch_assign = [&](uint64_t off, uint32_t len, uint8_t type, uint64_t file_off) {
+    scratch_clear();
+    cur_first_frag = fr.size();
+    cur_file = file_off;
+    fr.push_back(mck_wal_fragment{off, dst, len, type, 0, 0});
+    dst += len;
+  };
+  auto scratch_append = [&](uint64_t off, uint32_t len, uint8_t type) {
+    fr.push_back(mck_wal_fragment{off, dst, len, type, 0, 0});
+    dst += len;
+  };
+  auto emit = [&] {  // ReadRecord returns *record = scratch
+    roff.push_back(cur_start);
+    rlen.push_back((uint32_t)(dst - cur_start));
+    rfile.push_back(cur_file);
+    cur_start = dst;
+    cur_first_frag = fr.size();
+    R.first_record_read = true;
+  };
+  // ReadRecord, called until it returns false (the whole log)
+  bool more = true;
+  while (more && R.err == MCK_OK) {
+    in_fragmented_record = false;
+    scratch_clear();
+    for (;;) {
+      const uint64_t phys = R.end_of_buffer_offset - R.buf_size;
+      uint64_t drop_size = 0, foff = 0;
+      uint32_t flen = 0;
+      const int t = R.read_physical(&foff, &flen, &drop_size);
+      if (R.err) break;
+      if (t == 1 || t == 5) {  // kFullType
+        if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_PARTIAL_WITHOUT_END_1);
+        scratch_assign(foff, flen, (uint8_t)t, phys);
+        emit();
+        break;
+      } else if (t == 2 || t == 6) {  // kFirstType
+        if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_PARTIAL_WITHOUT_END_2);
+        scratch_assign(foff, flen, (uint8_t)t, phys);
+        in_fragmented_record = true;
+      } else if (t == 3 || t == 7) {  // kMiddleType
+        if (!in_fragmented_record)
+          R.report(phys, flen, MCK_WAL_R_MISSING_START_1);
+        else
+          scratch_append(foff, flen, (uint8_t)t);
+      } else if (t == 4 || t == 8) {  // kLastType
+        if (!in_fragmented_record) {
+          R.report(phys, flen, MCK_WAL_R_MISSING_START_2);
+        } else {
+          scratch_append(foff, flen, (uint8_t)t);
+          emit();
+          break;
+        }
+      } else if (t == (int)kSetCompressionType) {
+        // WAL compression (wal_compression != kNoCompression): the records
+        // that follow are compressed streams, outside this engine
+        mck_internal_set_error("WAL compression (kSetCompressionType record) is not supported");
+        return MCK_ENOTSUP;
+      } else if (t == (int)kUserDefinedTimestampSizeType || t == (int)kRecyclableUserDefinedTimestampSizeType) {
+        if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_TS_INTERSPERSED);
+        scratch_clear();
+        if (flen % 6) R.report(phys, flen, MCK_WAL_R_TS_DECODE);  // util/udt_util.h:46-64
+      } else if (t == kBadHeader || t == kEof) {
+        if (t == kBadHeader && R.strict()) R.report(phys, drop_size, MCK_WAL_R_TRUNCATED_HEADER);
+        if (in_fragmented_record) {
+          if (R.strict()) R.report(phys, scratch_size(), MCK_WAL_R_TRAILING_DATA);
+          scratch_clear();
+        }
+        more = false;
+        break;
+      } else if (t == kOldRecord && R.mode != MCK_WAL_kSkipAnyCorruptedRecords) {
+        if (in_fragmented_record) {
+          if (R.strict()) R.report(phys, scratch_size(), MCK_WAL_R_TRAILING_DATA);
+          scratch_clear();
+        }
+        more = false;
+        break;
+      } else if (t == kOldRecord || t == kBadRecord) {
+        // kSkipAnyCorruptedRecords: an old record is skipped like a bad one.
+        // (The reference then re-parses the same header forever: its buffer
+        // is not advanced on kOldRecord; the walk ends here instead.)
+        if (in_fragmented_record) {
+          R.report(phys, scratch_size(), MCK_WAL_R_ERROR_IN_MIDDLE);
+          in_fragmented_record = false;
+          scratch_clear();
+        }
+        if (t == kOldRecord) {
+          more = false;
+          break;
+        }
+      } else if (t == kBadRecordLen && R.eof) {
+        if (R.strict()) R.report(phys, drop_size, MCK_WAL_R_TRUNCATED_BODY);
+        more = false;
+        break;
+      } else if (t == kBadRecordLen || t == kBadRecordChecksum) {
+        if (R.recycled && R.mode == MCK_WAL_kTolerateCorruptedTailRecords) {
+          scratch_clear();
+          more = false;
+          break;
+        }
+        R.report(phys, drop_size, t == kBadRecordLen ? MCK_WAL_R_BAD_RECORD_LENGTH : MCK_WAL_R_CHECKSUM_MISMATCH);
+        if (in_fragmented_record) {
+          R.report(phys, scratch_size(), MCK_WAL_R_ERROR_IN_MIDDLE);
+          in_fragmented_record = false;
+          scratch_clear();
+        }
+      } else {  // unknown record type
+        R.report(phys, flen + (in_fragmented_record ? scratch_size() : 0), MCK_WAL_R_UNKNOWN_TYPE_BASE + (t & 255));
+        in_fragmented_record = false;
+        scratch_clear();
+      }
+    }
+  }
+  if (R.err) {
+    mck_internal_set_error("verify results do not match the WAL image (a record the device did not reach)");
+    return R.err;
+  }
+  scratch_clear();
+  out->nfrags = fr.size();
+  out->nrecords = roff.size();
+  out->records_bytes = dst;
+  out->nreports = R.reports.size();
+  out->dropped_bytes = R.dropped;
+  out->end_offset = R.end_of_buffer_offset - R.buf_size;
+  if (out->frags) {
+    if (out->frag_cap < fr.size()) {
+      mck_internal_set_error("frags capacity too small");
+      return MCK_EINVAL;
+    }
+    memcpy(out->frags, fr.data(), fr.size() * sizeof(mck_wal_fragment));
+  }
+  if (out->rec_offsets || out->rec_lengths || out->rec_file_offsets) {
+    if (out->rec_cap < roff.size()) {
+      mck_internal_set_error("records capacity too small");
+      return MCK_EINVAL;
+    }
+    if (out->rec_offsets) memcpy(out->rec_offsets, roff.data(), roff.size() * 8);
+    if (out->rec_lengths) memcpy(out->rec_lengths, rlen.data(), rlen.size() * 4);
+    if (out->rec_file_offsets) memcpy(out->rec_file_offsets, rfile.data(), rfile.size() * 8);
+  }
+  if (out->reports) {
+    const size_t n = std::min<size_t>(out->report_cap, R.reports.size());
+    memcpy(out->reports, R.reports.data(), n * sizeof(mck_wal_report));
+  }
+  return MCK_OK;
+}
+
+// The reassembly plan alone: mck_wal_read_records without CRCs, in the
+// default kTolerateCorruptedTailRecords mode.
 extern "C" int mck_wal_list_records(const void* wal, uint64_t nbytes, uint32_t log_number, mck_wal_fragment* frags,
                                     uint64_t frag_cap, uint64_t* nfrags, uint64_t* rec_offsets,
                                     uint32_t* rec_lengths, uint64_t rec_cap, uint64_t* nrecords,
                                     uint64_t* records_bytes) {
-  mck_internal_set_error("");
-  if (!wal && nbytes) {
-    mck_internal_set_error("wal is NULL");
-    return MCK_EINVAL;
-  }
-  const uint8_t* d = static_cast<const uint8_t*>(wal);
-  const uint64_t kBlock = MCK_WAL_kBlockSize;
-  std::vector<mck_wal_fragment> fr;
-  std::vector<uint64_t> roff;
-  std::vector<uint32_t> rlen;
-  uint64_t dst = 0;           // end of the reassembled buffer
-  uint64_t cur_start = 0;     // dst offset of the record being assembled
-  size_t cur_first_frag = 0;  // its first fragment in fr
-  bool in_frag = false;
-  auto drop_partial = [&] {
-    if (in_frag) {
-      fr.resize(cur_first_frag);
-      dst = cur_start;
-      in_frag = false;
-    }
-  };
-  auto add_frag = [&](uint64_t src, uint32_t len, uint8_t type) {
-    fr.push_back(mck_wal_fragment{src, dst, len, type, 0, 0});
-    dst += len;
-  };
-  auto emit = [&] {
-    roff.push_back(cur_start);
-    rlen.push_back((uint32_t)(dst - cur_start));
-    in_frag = false;
-  };
-  uint64_t pos = 0;
-  while (pos < nbytes) {
-    const uint64_t block_end = (pos / kBlock + 1) * kBlock;
-    const uint64_t avail = (block_end < nbytes ? block_end : nbytes) - pos;  // buffer_.size()
-    if (avail < MCK_WAL_kHeaderSize) {  // block trailer, or a truncated header at EOF
-      if (block_end >= nbytes) break;
-      pos = block_end;
-      continue;
-    }
-    const uint8_t* h = d + pos;
-    const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
-    const uint8_t type = h[6];
-    uint32_t hs = MCK_WAL_kHeaderSize;
-    if ((type >= 5 && type <= 8) || type == 11) {
-      hs = MCK_WAL_kRecyclableHeaderSize;
-      if (avail < hs) break;  // truncated header at EOF
-      const uint32_t ln = (uint32_t)h[7] | ((uint32_t)h[8] << 8) | ((uint32_t)h[9] << 16) | ((uint32_t)h[10] << 24);
-      if (ln != log_number) break;  // kOldRecord: end of this log's records
-    }
-    if (hs + (uint64_t)length > avail) {  // kBadRecordLen: drop the rest of the block
-      if (block_end >= nbytes) break;     // at EOF: truncated record body
-      drop_partial();
-      pos = block_end;
-      continue;
-    }
-    if (type == 0 && length == 0) {  // kZeroType padding: the buffer is cleared
-      if (block_end >= nbytes) break;
-      pos = block_end;
-      continue;
-    }
-    const uint64_t payload = pos + hs;
-    switch (type) {
-      case 1:
-      case 5:  // kFullType
-        drop_partial();
-        cur_start = dst;
-        cur_first_frag = fr.size();
-        add_frag(payload, length, type);
-        emit();
-        break;
-      case 2:
-      case 6:  // kFirstType
-        drop_partial();
-        cur_start = dst;
-        cur_first_frag = fr.size();
-        add_frag(payload, length, type);
-        in_frag = true;
-        break;
-      case 3:
-      case 7:  // kMiddleType
-        if (in_frag) add_frag(payload, length, type);
-        break;
-      case 4:
-      case 8:  // kLastType
-        if (in_frag) {
-          add_frag(payload, length, type);
-          emit();
-        }
-        break;
-      default:  // kSetCompressionType / timestamp-size records / unknown
-        drop_partial();
-        break;
-    }
-    pos = payload + length;
-  }
-  drop_partial();  // EOF inside a fragmented record: ignored
-  if (nfrags) *nfrags = fr.size();
-  if (nrecords) *nrecords = roff.size();
-  if (records_bytes) *records_bytes = dst;
-  if (frags) {
-    if (frag_cap < fr.size()) {
-      mck_internal_set_error("frags capacity too small");
-      return MCK_EINVAL;
-    }
-    memcpy(frags, fr.data(), fr.size() * sizeof(mck_wal_fragment));
-  }
-  if (rec_offsets || rec_lengths) {
-    if (rec_cap < roff.size()) {
-      mck_internal_set_error("records capacity too small");
-      return MCK_EINVAL;
-    }
-    if (rec_offsets) memcpy(rec_offsets, roff.data(), roff.size() * 8);
-    if (rec_lengths) memcpy(rec_lengths, rlen.data(), rlen.size() * 4);
-  }
+  mck_wal_read_out o;
+  memset(&o, 0, sizeof o);
+  o.frags = frags;
+  o.frag_cap = frag_cap;
+  o.rec_offsets = rec_offsets;
+  o.rec_lengths = rec_lengths;
+  o.rec_cap = rec_cap;
+  const int rc = mck_wal_read_records(wal, nbytes, log_number, MCK_WAL_kTolerateCorruptedTailRecords, nullptr, &o);
+  if (rc) return rc;
+  if (nfrags) *nfrags = o.nfrags;
+  if (nrecords) *nrecords = o.nrecords;
+  if (records_bytes) *records_bytes = o.records_bytes;
   return MCK_OK;
 }

@@ -45,12 +45,12 @@ def _bind(lib, prefix):
             "crc32c_zshift": (c.c_uint32, [c.c_uint32, c.c_uint64]),
             "builtin_checksum_with_last_byte": (c.c_uint32, [c.c_int, c.c_char_p, c.c_size_t,
                                                              c.c_uint8]),
-            "context_modifier": (c.c_uint32, [c.c_uint32, c.c_uint64]),
             "file_checksum_crc32c": (None, [c.c_char_p, c.c_size_t, c.c_char_p]),
             "verify_block": (c.c_int, [c.c_int, c.c_char_p, c.c_size_t, c.c_uint32, c.c_uint64,
                                        ctypes.POINTER(c.c_uint32), ctypes.POINTER(c.c_uint32)]),
         })
     sig.update({
+        "context_modifier": (c.c_uint32, [c.c_uint32, c.c_uint64]),
         "hash64": (c.c_uint64, [c.c_char_p, c.c_size_t, c.c_uint64]),
         "kv_protect": (c.c_uint64, [c.c_int, c.c_char_p, c.c_size_t, c.c_char_p, c.c_size_t,
                                     c.c_uint8, c.c_uint64]),

@@ -9,7 +9,8 @@ the reference's outputs.
 
   blob.bin       128 KiB of splitmix64 bytes (seed 0x5eedb10c), see blob_bytes()
   vectors.json   per-case reference outputs over slices of blob.bin, plus the
-                 block-trailer / WAL-record / context-modifier cases
+                 block-trailer / WAL-record cases and ChecksumModifierForContext
+                 cases from the reference's own inline table/format.h
   kat.json       known-answer values quoted from the reference's own tests
                  (util/crc32c_test.cc, table/table_test.cc)
 
@@ -57,6 +58,7 @@ def load_ref():
         "ref_builtin_checksum": (ctypes.c_uint32, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]),
         "ref_wal_record_crc": (ctypes.c_uint32, [ctypes.c_uint8, ctypes.c_char_p, ctypes.c_size_t,
                                                  ctypes.c_int, ctypes.c_uint32]),
+        "ref_context_modifier": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_uint64]),
         "ref_hash64": (ctypes.c_uint64, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_uint64]),
         "ref_kv_protect": (ctypes.c_uint64, [ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
                                              ctypes.c_size_t, ctypes.c_uint8, ctypes.c_uint64]),
@@ -65,11 +67,6 @@ def load_ref():
         f = getattr(r, k)
         f.restype, f.argtypes = res, args
     return r
-
-
-def context_modifier(base, offset):  # table/format.h:119-146
-    m = base ^ (((offset & 0xFFFFFFFF) + (offset >> 32)) & 0xFFFFFFFF)
-    return m if base else 0
 
 
 def main():
@@ -108,7 +105,14 @@ def main():
     for _ in range(32):
         base = rng.choice([0, rng.getrandbits(32)])
         off = rng.getrandbits(rng.choice([12, 32, 40, 64]))
-        ctx.append({"base": base, "offset": off, "out": context_modifier(base, off)})
+        ctx.append({"base": base, "offset": off, "out": ref.ref_context_modifier(base, off)})
+    # edge offsets (carry out of the low word, 4 GiB multiples, all-ones)
+    # from their own generator so the draws of the other fixtures stay put
+    rng3 = random.Random(20261017)
+    for off in ([0, 1, 0xFFFFFFFF, 1 << 32, (1 << 32) + 1, 0xFFFFFFFFFFFFFFFF, 0x8000000080000000,
+                 0xFFFFFFFF00000001] + [rng3.getrandbits(64) for _ in range(24)]):
+        for base in (0, 1, 0xFFFFFFFF, rng3.getrandbits(32)):
+            ctx.append({"base": base, "offset": off, "out": ref.ref_context_modifier(base, off)})
     wal = []
     for _ in range(40):
         t = rng.choice([1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11])

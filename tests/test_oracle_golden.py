@@ -167,6 +167,11 @@ def test_oracle_vs_live_reference(oracle, ref):
             assert oracle.Builtin(t, d) == ref.ref_builtin_checksum(t, d, n)
         seed = rnd.choice([0, rnd.getrandbits(64)])
         assert oracle.Hash64(d, seed) == ref.ref_hash64(d, n, seed)
+    # table/format.h ChecksumModifierForContext, called from the reference header
+    for _ in range(20000):
+        base = rnd.choice([0, 1, rnd.getrandbits(32)])
+        off = rnd.getrandbits(rnd.choice([8, 32, 33, 64]))
+        assert oracle.ContextModifier(base, off) == ref.ref_context_modifier(base, off)
 
 
 def test_wal_writer_layout(oracle):
