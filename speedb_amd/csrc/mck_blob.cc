@@ -85,7 +85,7 @@ extern "C" int mck_blob_list_records(const void* file, uint64_t size, mck_blob_f
   *nrecords = out.size();
   if (records) {
     if (cap < out.size()) return fail(MCK_EINVAL, "records capacity too small");
-    memcpy(records, out.data(), out.size() * sizeof(mck_blob_record));
+    if (!out.empty()) memcpy(records, out.data(), out.size() * sizeof(mck_blob_record));
   }
   return MCK_OK;
 }

@@ -377,7 +377,7 @@ int mck_sst_list_blocks(const void* file, uint64_t file_size, mck_sst_footer* fo
   if (blocks) {
     if (cap < out.size()) return fail(MCK_EINVAL, "blocks capacity %llu < %llu", (unsigned long long)cap,
                                       (unsigned long long)out.size());
-    memcpy(blocks, out.data(), out.size() * sizeof(mck_sst_block));
+    if (!out.empty()) memcpy(blocks, out.data(), out.size() * sizeof(mck_sst_block));
   }
   return MCK_OK;
 }

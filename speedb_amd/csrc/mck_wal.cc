@@ -371,20 +371,22 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
       mck_internal_set_error("frags capacity too small");
       return MCK_EINVAL;
     }
-    memcpy(out->frags, fr.data(), fr.size() * sizeof(mck_wal_fragment));
+    if (!fr.empty()) memcpy(out->frags, fr.data(), fr.size() * sizeof(mck_wal_fragment));
   }
   if (out->rec_offsets || out->rec_lengths || out->rec_file_offsets) {
     if (out->rec_cap < roff.size()) {
       mck_internal_set_error("records capacity too small");
       return MCK_EINVAL;
     }
-    if (out->rec_offsets) memcpy(out->rec_offsets, roff.data(), roff.size() * 8);
-    if (out->rec_lengths) memcpy(out->rec_lengths, rlen.data(), rlen.size() * 4);
-    if (out->rec_file_offsets) memcpy(out->rec_file_offsets, rfile.data(), rfile.size() * 8);
+    if (!roff.empty()) {
+      if (out->rec_offsets) memcpy(out->rec_offsets, roff.data(), roff.size() * 8);
+      if (out->rec_lengths) memcpy(out->rec_lengths, rlen.data(), rlen.size() * 4);
+      if (out->rec_file_offsets) memcpy(out->rec_file_offsets, rfile.data(), rfile.size() * 8);
+    }
   }
   if (out->reports) {
     const size_t n = std::min<size_t>(out->report_cap, R.reports.size());
-    memcpy(out->reports, R.reports.data(), n * sizeof(mck_wal_report));
+    if (n) memcpy(out->reports, R.reports.data(), n * sizeof(mck_wal_report));
   }
   return MCK_OK;
 }
