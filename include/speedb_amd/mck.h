@@ -587,6 +587,36 @@ int mck_host_batch_checksum(int kind, const void* host_base,
 /* Free the host pipeline's cached staging on every device. */
 void mck_host_pipeline_release(void);
 
+/* ========================================================================= */
+/* 4. Statistics                                                            */
+/* ========================================================================= */
+
+/* Engine counters since load (or the last reset), process-wide:
+ *   block_checksum_compute_count  BLOCK_CHECKSUM_COMPUTE_COUNT
+ *                                 (include/rocksdb/statistics.h:451): blocks
+ *                                 submitted to mck_sst_verify_batch (one per
+ *                                 VerifyBlockChecksum)
+ *   block_checksum_mismatch_count BLOCK_CHECKSUM_MISMATCH_COUNT (:455):
+ *                                 blocks those verifies flagged, counted on
+ *                                 each device (completed work only: sync the
+ *                                 streams first)
+ *   batches / spans               batched device calls and their spans
+ *   bytes_known                   span bytes of the batches whose lengths the
+ *                                 host knows (uniform batches, host batches);
+ *                                 ragged device batches keep their lengths on
+ *                                 the device and are not included */
+typedef struct mck_statistics {
+  uint64_t block_checksum_compute_count;
+  uint64_t block_checksum_mismatch_count;
+  uint64_t batches;
+  uint64_t spans;
+  uint64_t bytes_known;
+} mck_statistics;
+
+/* Fill *out (reads each initialised device's counters: synchronous);
+ * reset != 0 zeroes the counters after reading them. */
+int mck_statistics_get(mck_statistics* out, int reset);
+
 #ifdef __cplusplus
 }
 #endif

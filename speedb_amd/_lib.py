@@ -117,6 +117,7 @@ SIGNATURES = [
       ctypes.c_uint32, ctypes.c_int, ctypes.c_size_t, vp, vp,
       ctypes.POINTER(ctypes.c_double)]),
     ("mck_host_pipeline_release", None, []),
+    ("mck_statistics_get", ctypes.c_int, [vp, ctypes.c_int]),
 ]
 
 for _name, _res, _args in SIGNATURES:

@@ -752,3 +752,28 @@ def host_batch_checksum(kind: int, host, offsets=None, lengths=None, stride: int
 
 
 __all__ += ["host_batch_checksum"]
+
+
+# ---------------------------------------------------------------------------
+# statistics (include/rocksdb/statistics.h tickers of this path)
+# ---------------------------------------------------------------------------
+
+class mck_statistics(ctypes.Structure):
+    _fields_ = [("block_checksum_compute_count", ctypes.c_uint64),
+                ("block_checksum_mismatch_count", ctypes.c_uint64), ("batches", ctypes.c_uint64),
+                ("spans", ctypes.c_uint64), ("bytes_known", ctypes.c_uint64)]
+
+
+def statistics(reset: bool = False) -> dict:
+    """The engine's counters: BLOCK_CHECKSUM_COMPUTE_COUNT /
+    BLOCK_CHECKSUM_MISMATCH_COUNT (statistics.h:451,455; the mismatches are
+    counted on the device -- synchronise first), batches, spans and the
+    bytes of batches with host-known lengths.  reset=True zeroes them."""
+    s = mck_statistics()
+    check(lib.mck_statistics_get(ctypes.addressof(s), 1 if reset else 0), "mck_statistics_get")
+    return {"BLOCK_CHECKSUM_COMPUTE_COUNT": s.block_checksum_compute_count,
+            "BLOCK_CHECKSUM_MISMATCH_COUNT": s.block_checksum_mismatch_count,
+            "batches": s.batches, "spans": s.spans, "bytes_known": s.bytes_known}
+
+
+__all__ += ["statistics"]

@@ -49,6 +49,7 @@ struct DevCtx {
   std::once_flag once;
   int status = MCK_ENODEV;
   int ncu = 0;
+  uint32_t* d_stats = nullptr;  // device counters: [0] block checksum mismatches
 };
 DevCtx g_dev[kMaxDev];
 
@@ -95,6 +96,7 @@ int current_device(int* dev_out, int* ncu_out) {
     }
     d.ncu = prop.multiProcessorCount;
     if (hipMemcpyToSymbol(HIP_SYMBOL(g_crc_tables), &host_tables(), sizeof(CrcTables)) != hipSuccess ||
+        hipMalloc(&d.d_stats, 64) != hipSuccess || hipMemset(d.d_stats, 0, 64) != hipSuccess ||
         hipDeviceSynchronize() != hipSuccess) {
       d.status = MCK_EHIP;
       return;
@@ -109,6 +111,32 @@ int current_device(int* dev_out, int* ncu_out) {
   if (ncu_out) *ncu_out = d.ncu;
   return MCK_OK;
 }
+
+// Engine statistics (mck_statistics_get): host-side counters of the batched
+// calls; the mismatch ticker is counted on each device (DevCtx::d_stats).
+struct HostStats {
+  std::atomic<uint64_t> compute{0}, batches{0}, spans{0}, bytes{0};
+};
+HostStats g_stats;
+
+// engine-internal batched calls (host pipeline chunks, long-span pieces,
+// scalar shims) are not counted again
+thread_local int t_nostat = 0;
+struct NoStat {
+  NoStat() { t_nostat++; }
+  ~NoStat() { t_nostat--; }
+};
+
+void stat_batch(uint64_t spans, uint64_t known_bytes) {
+  if (t_nostat) return;
+  g_stats.batches.fetch_add(1, std::memory_order_relaxed);
+  g_stats.spans.fetch_add(spans, std::memory_order_relaxed);
+  if (known_bytes) g_stats.bytes.fetch_add(known_bytes, std::memory_order_relaxed);
+}
+// bytes of a batch when the host knows them (uniform lengths)
+uint64_t known_bytes(const mck_spans* s) { return s->lengths ? 0 : (uint64_t)s->length * s->count; }
+
+uint32_t* dev_stats(int dev) { return g_dev[dev].d_stats; }
 
 int check_spans(const mck_spans* s) {
   if (!s) {
@@ -381,6 +409,7 @@ int mck_crc32c_batch(const mck_spans* spans, const uint32_t* init_crcs, uint32_t
                      mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(spans)) return rc;
+  stat_batch(spans->count, known_bytes(spans));
   if (spans->count && !out) {
     set_err("out is NULL");
     return MCK_EINVAL;
@@ -394,6 +423,7 @@ int mck_crc32c_batch(const mck_spans* spans, const uint32_t* init_crcs, uint32_t
 int mck_xxh3_64_batch(const mck_spans* spans, uint64_t* out, mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(spans)) return rc;
+  stat_batch(spans->count, known_bytes(spans));
   if (spans->count && !out) {
     set_err("out is NULL");
     return MCK_EINVAL;
@@ -405,6 +435,7 @@ int mck_xxh3_64_batch(const mck_spans* spans, uint64_t* out, mck_stream_t stream
 int mck_xxh32_batch(const mck_spans* spans, uint32_t seed, uint32_t* out, mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(spans)) return rc;
+  stat_batch(spans->count, known_bytes(spans));
   if (spans->count && !out) {
     set_err("out is NULL");
     return MCK_EINVAL;
@@ -416,6 +447,7 @@ int mck_xxh32_batch(const mck_spans* spans, uint32_t seed, uint32_t* out, mck_st
 int mck_xxh64_batch(const mck_spans* spans, uint64_t seed, uint64_t* out, mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(spans)) return rc;
+  stat_batch(spans->count, known_bytes(spans));
   if (spans->count && !out) {
     set_err("out is NULL");
     return MCK_EINVAL;
@@ -428,6 +460,7 @@ int mck_builtin_checksum_batch(int type, const mck_spans* spans, const uint8_t* 
                                mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(spans)) return rc;
+  stat_batch(spans->count, known_bytes(spans));
   if (spans->count && !out) {
     set_err("out is NULL");
     return MCK_EINVAL;
@@ -441,6 +474,7 @@ int mck_sst_trailer_batch(int type, const mck_spans* payloads, const uint8_t* co
                           mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(payloads)) return rc;
+  stat_batch(payloads->count, known_bytes(payloads));
   if (payloads->count && (!out || !comp_types)) {
     set_err("out / comp_types is NULL");
     return MCK_EINVAL;
@@ -454,12 +488,21 @@ int mck_sst_verify_batch(int type, const mck_spans* payloads, const uint64_t* fi
                          uint32_t* mismatch_count, mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(payloads)) return rc;
+  stat_batch(payloads->count, known_bytes(payloads));
   if (payloads->count && !mismatch) {
     set_err("mismatch is NULL");
     return MCK_EINVAL;
   }
   BlockArgs a{to_src(payloads), nullptr, file_offsets, base_context_checksum, computed, mismatch, stored,
               mismatch_count};
+  // BLOCK_CHECKSUM_COMPUTE_COUNT (include/rocksdb/statistics.h:451): one
+  // per VerifyBlockChecksum; mismatches are counted on the device
+  g_stats.compute.fetch_add(payloads->count, std::memory_order_relaxed);
+  int dev = 0;
+  if (payloads->count && hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < kMaxDev) {
+    if (int rc = current_device(nullptr, nullptr)) return rc;
+    a.stats_mismatch = dev_stats(dev);
+  }
   return launch_block<kModeVerify>(type, a, payloads->count, reinterpret_cast<hipStream_t>(stream));
 }
 
@@ -467,6 +510,7 @@ int mck_wal_record_crc_batch(const mck_spans* payloads, const uint8_t* types, ui
                              mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(payloads)) return rc;
+  stat_batch(payloads->count, known_bytes(payloads));
   if (payloads->count && (!out || !types)) {
     set_err("out / types is NULL");
     return MCK_EINVAL;
@@ -744,6 +788,8 @@ int mck_crc32c_long(const void* data, uint64_t n, uint32_t init_crc, uint32_t* s
   }
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
+  stat_batch(1, n);
+  NoStat nostat;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   // seed: ~zshift(~init, n); n == 0 leaves init_crc (Extend(c, "") = c)
   MCK_HIP(hipMemsetD32Async(out, (int)~gf_zshift(~init_crc, n), 1, st));
@@ -779,6 +825,7 @@ constexpr size_t kShimLongBytes = 1u << 20;
 static int scalar_u32(int kind, uint32_t init, const void* data, size_t n, int type, int has_last, char last,
                       uint32_t* res) {
   t_err[0] = 0;
+  NoStat nostat;
   if (!res) {
     set_err("out is NULL");
     return MCK_EINVAL;
@@ -821,6 +868,7 @@ static int scalar_u32(int kind, uint32_t init, const void* data, size_t n, int t
 // kind 0: XXH3_64bits; kind 1: NPHash64(seed).
 static int scalar_u64(int kind, const void* data, size_t n, uint64_t seed, uint64_t* res) {
   t_err[0] = 0;
+  NoStat nostat;
   if (!res) {
     set_err("out is NULL");
     return MCK_EINVAL;
@@ -895,6 +943,7 @@ uint64_t mck_np_hash64(const void* data, size_t n, uint64_t seed) {
 int mck_np_hash64_batch(const mck_spans* spans, uint64_t seed, uint64_t* out, mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(spans)) return rc;
+  stat_batch(spans->count, known_bytes(spans));
   if (spans->count && !out) {
     set_err("out is NULL");
     return MCK_EINVAL;
@@ -1078,6 +1127,7 @@ static int host_pipe_reserve(HostPipe& p, size_t cap, uint32_t max_spans) {
 // one; results come back D2H into pinned memory and are copied out when the
 // slot is reused.  Every exit path leaves no copy in flight.
 static int run_device_share(int dev, const HostJob& J, uint32_t lo, uint32_t hi) {
+  NoStat nostat;
   MCK_HIP(hipSetDevice(dev));
   if (lo >= hi) return MCK_OK;
   int rc = current_device(nullptr, nullptr);
@@ -1219,8 +1269,41 @@ int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* hos
       set_err("device %d: %s", devs[d], errs[d].c_str());
       return rcs[d];
     }
+  uint64_t bytes = 0;
+  for (uint32_t i = 0; i < count; i++) bytes += host_lengths ? host_lengths[i] : length;
+  stat_batch(count, bytes);
   if (seconds) *seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   return MCK_OK;
+}
+
+int mck_statistics_get(mck_statistics* out, int reset) {
+  t_err[0] = 0;
+  if (!out) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  memset(out, 0, sizeof *out);
+  const auto take = [&](std::atomic<uint64_t>& c) { return reset ? c.exchange(0) : c.load(); };
+  out->block_checksum_compute_count = take(g_stats.compute);
+  out->batches = take(g_stats.batches);
+  out->spans = take(g_stats.spans);
+  out->bytes_known = take(g_stats.bytes);
+  int prev = 0;
+  (void)hipGetDevice(&prev);
+  int rc = MCK_OK;
+  for (int d = 0; d < kMaxDev; d++) {
+    if (!g_dev[d].d_stats) continue;
+    uint32_t c[1] = {0};
+    if (hipSetDevice(d) != hipSuccess || hipMemcpy(c, g_dev[d].d_stats, 4, hipMemcpyDeviceToHost) != hipSuccess ||
+        (reset && hipMemset(g_dev[d].d_stats, 0, 4) != hipSuccess)) {
+      set_err("reading the device counters of device %d failed", d);
+      rc = MCK_EHIP;
+      continue;
+    }
+    out->block_checksum_mismatch_count += c[0];
+  }
+  (void)hipSetDevice(prev);
+  return rc;
 }
 
 void mck_host_pipeline_release(void) {

@@ -53,6 +53,7 @@ struct BlockArgs {
   uint8_t* mismatch;       // verify
   uint32_t* stored;        // verify (opt)
   uint32_t* mismatch_count;  // verify (opt)
+  uint32_t* stats_mismatch = nullptr;  // verify: the engine's per-device BLOCK_CHECKSUM_MISMATCH_COUNT
 };
 
 // Epilogue inputs of a block op, loaded by the driver together with the
@@ -103,6 +104,7 @@ __device__ __forceinline__ void block_epilogue(const BlockArgs& a, uint32_t i, u
     if (a.out) a.out[i] = v;
     if (a.stored) a.stored[i] = stored;
     if (bad && a.mismatch_count) atomicAdd(a.mismatch_count, 1u);
+    if (bad && a.stats_mismatch) atomicAdd(a.stats_mismatch, 1u);
   }
 }
 // Same, with the inputs loaded here (drivers without epilogue prefetch).

@@ -126,3 +126,11 @@ def test_python_mirror_exports():
     assert [int(t) for t in S.ChecksumType] == [0, 1, 2, 3, 4]
     assert S.crc32c.kMaskDelta == 0xA282EAD8
     assert S.crc32c.Unmask(S.crc32c.Mask(0x12345678)) == 0x12345678
+
+
+def test_statistics_without_device():
+    import speedb_amd as S
+    st = S.statistics(reset=True)
+    assert set(st) == {"BLOCK_CHECKSUM_COMPUTE_COUNT", "BLOCK_CHECKSUM_MISMATCH_COUNT", "batches", "spans",
+                       "bytes_known"}
+    assert all(v >= 0 for v in st.values())

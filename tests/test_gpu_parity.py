@@ -212,13 +212,21 @@ def test_sst_trailer_and_verify(gpu, oracle, ctype, base_ctx):
     for i in bad:
         pos = offs[i] + rnd.randrange(0, lens[i] + 5)
         cor[pos] ^= 1 << rnd.randrange(8)
-    dev2 = torch.frombuffer(bytes(cor) + bytes(64), dtype=torch.uint8).to("cuda")
+    dev2 = torch.frombuffer(bytearray(bytes(cor) + bytes(64)), dtype=torch.uint8).to("cuda")
     sp2 = spans(torch, S, dev2, offs, lens)
+    torch.cuda.synchronize()
+    S.statistics(reset=True)
     mm, comp, stored, cnt = S.sst_verify_batch(ctype, sp2, file_offsets=foff,
                                                base_context_checksum=base_ctx)
     flagged = [i for i, v in enumerate(mm.cpu().tolist()) if v]
     assert flagged == bad
     assert int(cnt.item()) == len(bad)
+    # statistics.h:451,455 tickers of that one verify batch
+    torch.cuda.synchronize()
+    stats = S.statistics()
+    assert stats["BLOCK_CHECKSUM_COMPUTE_COUNT"] == len(sizes)
+    assert stats["BLOCK_CHECKSUM_MISMATCH_COUNT"] == len(bad)
+    assert stats["batches"] == 1 and stats["spans"] == len(sizes)
     st = u32(stored)
     for i in bad:
         o, n = offs[i], lens[i]
