@@ -34,6 +34,10 @@ Default workload (the headline, BASELINE.json configs[1]): CRC32C over
                        header + blob CRC of every record (mck_blob_record_batch)
   kv       (row a12)   per-KV protection of memtable inserts, README shape
                        (16 B key, 1000 B value): ProtectKVO(...).ProtectS(seq)
+  shim     (8b)        latency of one synchronous scalar shim call
+                       (mck_crc32c_value_r: H2D + launch + D2H) at 64 B,
+                       4 KiB, 32 KiB, 1 MiB vs the reference's crc32c::Value
+                       on one host thread
 
 One step = one pass of the workload's kernel(s) over the rank's whole batch.
 With N > 1 (torchrun, one process per GPU) every rank checksums its own
@@ -80,7 +84,7 @@ def parse():
     # 0.77 -> 0.90 -> 0.76 ms per launch at 1M x 4 KiB): run the workload
     # untimed for this long before the warmup steps, whatever W is
     p.add_argument("--settle-ms", type=float, default=250.0)
-    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file", "walwrite", "blob"], default="crc32c")
+    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file", "walwrite", "blob", "shim"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
     p.add_argument("--sst-bytes", type=int, default=1 << 30, help="per SST image (sst); 2 images")
@@ -506,8 +510,53 @@ def make_workload(args, dev, rank, world):
     return w
 
 
+def shim_latency(args):
+    """Per-call latency of the synchronous scalar shim vs the CPU reference
+    (INTEGRATION.md keeps crc32c::Extend on the CPU below the crossover)."""
+    import numpy as np
+    import torch
+
+    from speedb_amd import _lib
+    torch.cuda.set_device(0)
+    L = _lib.lib
+    ref = None
+    p = os.path.join(REPO, "oracle", "_ref", "libspdb_ref.so")
+    if os.path.exists(p):
+        ref = ctypes.CDLL(p)
+        ref.ref_crc32c_value.restype = ctypes.c_uint32
+        ref.ref_crc32c_value.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    rows = []
+    out = ctypes.c_uint32()
+    for n in (64, 4096, 32768, 1 << 20, 16 << 20):
+        buf = np.random.default_rng(n).integers(0, 256, size=n, dtype=np.uint8)
+        ptr = buf.ctypes.data
+        for _ in range(20):
+            _lib.check(L.mck_crc32c_value_r(ptr, n, ctypes.byref(out)), "mck_crc32c_value_r")
+        reps = max(20, min(2000, int(2e8 // max(n, 1))))
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            L.mck_crc32c_value_r(ptr, n, ctypes.byref(out))
+        gpu_us = (time.perf_counter() - t0) / reps * 1e6
+        row = {"bytes": n, "shim_us": round(gpu_us, 2)}
+        if ref is not None:
+            assert ref.ref_crc32c_value(ptr, n) == out.value
+            r2 = max(reps, 200)
+            t0 = time.perf_counter()
+            for _ in range(r2):
+                ref.ref_crc32c_value(ptr, n)
+            cpu_us = (time.perf_counter() - t0) / r2 * 1e6
+            row["cpu_reference_us"] = round(cpu_us, 3)
+        rows.append(row)
+    print(json.dumps({"metric": "scalar shim latency (mck_crc32c_value_r, pageable host buffer, sync)",
+                      "unit": "us per call", "rows": rows,
+                      "note": "cpu_reference_us = crc32c::Value from oracle/_ref on one host thread, "
+                              "including the ctypes call overhead (~0.3 us)"}))
+
+
 def main():
     args = parse()
+    if args.workload == "shim":
+        return shim_latency(args)
     import torch
     import torch.distributed as dist
 
