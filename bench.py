@@ -34,6 +34,12 @@ Default workload (the headline, BASELINE.json configs[1]): CRC32C over
                        header + blob CRC of every record (mck_blob_record_batch)
   kv       (row a12)   per-KV protection of memtable inserts, README shape
                        (16 B key, 1000 B value): ProtectKVO(...).ProtectS(seq)
+  walrec   (row a10)   EmitPhysicalRecord's CRC of every WAL record of a 1 GiB
+                       group of records of 100-1100 B (README 1 KB values,
+                       db/log_writer.cc:263-311), back to back at any byte
+                       offset: mck_wal_record_crc_batch
+  ragged   (8a a1)     crc32c_batch over ragged spans of --span-min..--span-max
+                       bytes (explicit offsets/lengths), 1 GiB per GPU
   shim     (8b)        latency of one synchronous scalar shim call
                        (mck_crc32c_value_r: H2D + launch + D2H) at 64 B,
                        4 KiB, 32 KiB, 1 MiB vs the reference's crc32c::Value
@@ -84,7 +90,8 @@ def parse():
     # 0.77 -> 0.90 -> 0.76 ms per launch at 1M x 4 KiB): run the workload
     # untimed for this long before the warmup steps, whatever W is
     p.add_argument("--settle-ms", type=float, default=250.0)
-    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file", "walwrite", "blob", "shim"], default="crc32c")
+    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file", "walwrite", "blob", "shim",
+                            "walrec", "ragged"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
     p.add_argument("--sst-bytes", type=int, default=1 << 30, help="per SST image (sst); 2 images")
@@ -96,6 +103,9 @@ def parse():
     p.add_argument("--wal-records", type=int, default=2 << 20, help="logical records per GPU (walwrite)")
     p.add_argument("--blob-records", type=int, default=1 << 20, help="blob records per GPU (blob)")
     p.add_argument("--kvs", type=int, default=1 << 22, help="KVs per GPU (kv)")
+    p.add_argument("--span-min", type=int, default=100, help="smallest span (walrec, ragged)")
+    p.add_argument("--span-max", type=int, default=1100, help="largest span (walrec, ragged)")
+    p.add_argument("--span-bytes", type=int, default=1 << 30, help="span bytes per GPU (walrec, ragged)")
     p.add_argument("--host-blocks", type=int, default=2_500_000,
                    help="pinned 4300-B blocks per GPU (host; configs[4]'s 8-GPU share)")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -355,6 +365,53 @@ def make_workload(args, dev, rank, world):
                 acc = S.crc32c.Crc32cCombine(acc, v, ln)
                 left -= ln
             return acc == int(out.cpu().numpy().view(np.uint32)[0])
+        w.check = check
+    elif args.workload in ("walrec", "ragged"):
+        rng = np.random.default_rng(800 + rank)
+        n_est = int(args.span_bytes // ((args.span_min + args.span_max) / 2))
+        lens = rng.integers(args.span_min, args.span_max + 1, size=n_est).astype(np.int64)
+        gaps = rng.integers(0, 8, size=n_est) if args.workload == "walrec" else np.zeros(n_est, np.int64)
+        # walrec: a WAL payload follows its 7-byte header (+ trailer gaps):
+        # records at any byte offset; ragged: spans back to back
+        step = lens + (7 + gaps if args.workload == "walrec" else 0)
+        offs = np.zeros(n_est, dtype=np.int64)
+        offs[1:] = np.cumsum(step)[:-1]
+        count = n_est
+        data = W.rand_bytes(int(offs[-1] + lens[-1]) + 64, dev, 801 + rank)
+        sp = S.Spans(data, count, offsets=torch.from_numpy(offs).to(dev),
+                     lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
+        out = torch.empty(count, dtype=torch.int32, device=dev)
+        if args.workload == "walrec":
+            types = torch.from_numpy(rng.choice([1, 2, 3, 4], size=count).astype(np.uint8)).to(dev)
+            w.step = lambda: S.wal_record_crc_batch(sp, types, 7, out=out, stream=stream)
+            w.kernel = "mck::k_crc_rows<mck::OpCrcWal>"
+            w.desc = (f"WAL record CRCs (EmitPhysicalRecord, db/log_writer.cc:263-311): {count} records of "
+                      f"{args.span_min}-{args.span_max} B per GPU at any byte offset, mck_wal_record_crc_batch")
+        else:
+            w.step = lambda: S.crc32c_batch(sp, out=out, stream=stream)
+            w.kernel = ("mck::k_crc_rows<mck::OpCrcValue>" if os.environ.get("MCK_CRC_ROWS") == "1"
+                        else "mck::k_crc<mck::OpCrcValue, true>")
+            w.desc = (f"crc32c_batch over {count} ragged spans of {args.span_min}-{args.span_max} B per GPU "
+                      "(explicit offsets/lengths)")
+        w.span_bytes = int(lens.sum())
+        # span bytes + 8 B offset + 4 B length + 4 B out (+1 B type)
+        w.alg_bytes = int(lens.sum()) + count * (16 + (1 if args.workload == "walrec" else 0))
+        w.cfg = {"spans_per_gpu": count, "span_min": args.span_min, "span_max": args.span_max}
+
+        def check():
+            idx = np.random.default_rng(rank).choice(count, size=256, replace=False)
+            hd = data.cpu().numpy()
+            res = out.cpu().numpy().view(np.uint32)
+            tys = types.cpu().numpy() if args.workload == "walrec" else None
+            ok = True
+            for k in idx:
+                b = hd[offs[k]:offs[k] + lens[k]].tobytes()
+                if args.workload == "walrec":
+                    want = S.crc32c.Mask(S.crc32c.Extend(S.crc32c.Value(bytes([int(tys[k])])), b))
+                else:
+                    want = S.crc32c.Value(b)
+                ok &= int(res[k]) == want
+            return ok
         w.check = check
     elif args.workload == "walwrite":
         rng = np.random.default_rng(600 + rank)

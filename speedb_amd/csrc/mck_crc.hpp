@@ -672,7 +672,7 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
     const typename Op::Pre pnxt = op.pre(more ? ni : i, lsp.ptr, lsp.end - lsp.ptr);
     if (T && !(sp.mini && r == sp.rounds - 1)) row_transpose(cur);  // wave-uniform
     s = crc_round(s, cur, sp, r, L);
-    if (r == 0) op.finish(i, crc_finish(s, sp, L), pcur);
+    if (r == 0) op.finish(i, crc_finish(s, sp, L), pcur, (threadIdx.x & 63) == 0);
     if (!more) break;
     i = ni;
     r = nr;
@@ -689,7 +689,9 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
 //   const uint8_t* Op::base(), uint64_t Op::off(i), uint64_t Op::len(i),
 //   uint32_t Op::init_crc(i)                    (per lane, i < count)
 //   Op::Pre Op::pre(i, ptr, len)   epilogue inputs, loaded with the chunks
-//   void Op::finish(i, crc, pre)   (all lanes call it; lane 0 writes)
+//   void Op::finish(i, crc, pre, writer)  (all lanes call it; the lanes
+//                                  with writer set store: lane 0 of the wave
+//                                  here, lane 0 of each row in the row driver)
 // T: row-transposed loads (crc_load_chunk<true>, row_transpose).
 template <class Op, bool T = false>
 __device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, uint8_t* lds,
@@ -787,12 +789,199 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
     if (TLAYOUT && kCrcRowT) row_transpose(cur);
     if (TLAYOUT && !kCrcRowT) quad_transpose(cur, plane & 3);
     s = crc_round(s, cur, sp, r, L);
-    if (r == 0) op.finish(i, crc_finish(s, sp, L));
+    if (r == 0) op.finish(i, crc_finish(s, sp, L), typename Op::Pre{}, (threadIdx.x & 63) == 0);
     if (!more) break;
     i = ni;
     r = nr;
     sp = nsp;
     cur = nxt;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Row driver: one 16-lane ROW per span, four spans per wave.
+//
+// The wave driver above reduces every span across the whole wave (lane-final
+// shift, wave XOR, epilogue): for spans of a few hundred bytes that per-span
+// chain, not bandwidth, sets the rate (a flat ~2.2 G spans/s per GPU,
+// DESIGN.md §10).  Here each row of 16 lanes owns a span and walks it in
+// 1 KiB rounds anchored at the span's 16-byte-aligned end (lane c of the row
+// owns the 64-byte chunk at round_base + 64 c, the same 4-byte table step as
+// the wave driver), so four spans are reduced side by side by one
+// instruction stream: the lane-final shift zshift(s, 64 (15 - c)) is the
+// wave table's lane 48 + c, the row XOR is a 4-step DPP butterfly, and the
+// head/tail/init handling of crc_round runs per row (vector values instead
+// of wave-uniform ones).  Rows take spans statically (row g: g, g + R,
+// g + 2R, ... over the R rows of the grid), the descriptor of a row's next
+// span is loaded one span ahead, and every load is issued unconditionally
+// (exec-masked loads would force vmcnt(0) waits, see crc_load_chunk).
+// LDS: the wave driver's image plus the 960-byte row gap map at kLdsRowGap.
+constexpr uint32_t kLdsRowGap = kLdsLowEnd;  // 512 B, below the step tables
+static_assert(kLdsRowGap + 512 <= kLdsStep, "row gap map must fit below the step tables");
+static_assert(offsetof(CrcTables, gap_row) - offsetof(CrcTables, unshift) == kMaxUnshift * 512, "layout");
+
+__device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
+
+__device__ __forceinline__ void crc_fill_rows(uint8_t* lds, const CrcTables* __restrict__ g) {
+  CrcFill f;
+  crc_fill_load<true>(f, g);
+  const int t = threadIdx.x;
+  const uint4* rg = reinterpret_cast<const uint4*>(&g->gap_row[0][0]);
+  const uint4 x = rg[t < 32 ? t : 0];
+  crc_fill_store<true>(f, lds);
+  if (t < 32) reinterpret_cast<uint4*>(lds + kLdsRowGap)[t] = x;
+}
+
+struct RowSpan {
+  uint64_t ptr;    // first byte
+  uint64_t a0;     // ptr rounded down to 16
+  uint64_t a1;     // end rounded up to 16
+  uint32_t n;      // bytes
+  int32_t rounds;  // 1 KiB row rounds covering [ptr, a1)
+  int32_t owner;   // row lane whose first-round chunk holds ptr (16: none)
+  uint32_t hb;     // ptr - owner's chunk start (< 64)
+  uint32_t kt;     // a1 - end (< 16)
+  uint32_t inj;    // ~init un-shifted by hb bytes
+  uint32_t init;
+};
+
+__device__ __forceinline__ RowSpan row_span(uint64_t ptr, uint32_t n, uint32_t init) {
+  RowSpan s;
+  s.ptr = ptr;
+  s.n = n;
+  s.a0 = ptr & ~15ull;
+  s.a1 = (ptr + n + 15) & ~15ull;
+  s.kt = (uint32_t)(s.a1 - (ptr + n));
+  s.init = init;
+  const uint32_t cover = (uint32_t)(s.a1 - ptr);
+  s.rounds = n == 0 ? 1 : (int32_t)((cover + kRowRoundBytes - 1) / kRowRoundBytes);
+  const uint32_t lead = (uint32_t)kRowRoundBytes * (uint32_t)s.rounds - cover;
+  s.owner = n == 0 ? 16 : (int32_t)(lead >> 6);
+  s.hb = lead & 63u;
+  s.inj = crc_unshift(s.hb, ~init);  // unshift by 0 is the identity
+  return s;
+}
+
+__device__ __forceinline__ RowSpan row_span_sel(bool a, const RowSpan& x, const RowSpan& y) {
+  RowSpan s;
+  s.ptr = a ? x.ptr : y.ptr;
+  s.a0 = a ? x.a0 : y.a0;
+  s.a1 = a ? x.a1 : y.a1;
+  s.n = a ? x.n : y.n;
+  s.rounds = a ? x.rounds : y.rounds;
+  s.owner = a ? x.owner : y.owner;
+  s.hb = a ? x.hb : y.hb;
+  s.kt = a ? x.kt : y.kt;
+  s.inj = a ? x.inj : y.inj;
+  s.init = a ? x.init : y.init;
+  return s;
+}
+
+// Row round r of a span: lane c's 64-byte chunk; in the first round pieces
+// below a0 read a0 (discarded).
+__device__ __forceinline__ Chunk row_load_chunk(const RowSpan& sp, int r, uint32_t c) {
+  const uint64_t b = sp.a1 - (uint64_t)kRowRoundBytes * (uint32_t)(r + 1) + 64ull * c;
+  const bool first = r == sp.rounds - 1;
+  Chunk ch;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    uint64_t a = b + 16ull * j;
+    a = (first && a < sp.a0) ? sp.a0 : a;
+    ch.v[j] = span_load16<false>(a);
+  }
+  return ch;
+}
+
+__device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpan& sp, int r, uint32_t c,
+                                              const CrcLane& L) {
+  const bool first = r == sp.rounds - 1;
+  const bool own = (int32_t)c == sp.owner;
+  if (wave_any(first && own && sp.hb != 0)) crc_zero_head(ch, (first && own) ? sp.hb : 0u);
+  if (wave_any(r == 0 && sp.kt != 0)) crc_keep_head_bytes(ch.v[3], (r == 0 && c == 15) ? 16u - sp.kt : 16u);
+  uint32_t gap = 0;
+  if (wave_any(!first)) gap = crc_nibmap(kLdsRowGap, s);
+  uint32_t x = first ? (own ? sp.inj : 0u) : gap;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&ch.v[0]);
+  x ^= w[0];
+#pragma unroll
+  for (int k = 0; k < 16; k++) x = crc_step4x(x, L, k < 15 ? w[k + 1] : 0u);
+  return (first && (int32_t)c < sp.owner) ? 0u : x;
+}
+
+// XOR over the 16 lanes of each row, in every lane of the row.
+__device__ __forceinline__ uint32_t row_xor32(uint32_t v) {
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  return v;
+}
+
+// The span's CRC (Extend semantics) in every lane of its row; Lf = the lane
+// constants with lane4 = (48 + c) * 4 (shift by 64 (15 - c)).
+__device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, const CrcLane& Lf) {
+  uint32_t p = row_xor32(crc_lane_final(s, Lf));
+  if (wave_any(sp.kt != 0)) p = crc_unshift(sp.kt, p);
+  return sp.n == 0 ? sp.init : ~p;
+}
+
+template <class Op>
+__device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t count, uint8_t* lds,
+                                                const CrcTables* __restrict__ g) {
+  crc_fill_rows(lds, g);
+  __syncthreads();
+  const CrcLane L = crc_lane();
+  CrcLane Lf = L;
+  const uint32_t c = threadIdx.x & 15;
+  Lf.lane4 = (48u + c) << 2;
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t nrows = gridDim.x * wpb * 4;
+  const uint32_t row = (blockIdx.x * wpb + (threadIdx.x >> 6)) * 4 + ((threadIdx.x >> 4) & 3);
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  bool live = row < count;
+  uint32_t i = live ? row : 0;
+  RowSpan sp = row_span(base + op.off(i), (uint32_t)op.len(i), op.init_crc(i));
+  int r = sp.rounds - 1;
+  Chunk cur = row_load_chunk(sp, r, c);
+  typename Op::Pre pcur = op.pre(i, sp.ptr, sp.n);
+  // the row's next span, one span ahead
+  uint32_t ni = row + nrows;
+  uint32_t nic = ni < count ? ni : i;
+  uint64_t noff = op.off(nic);
+  uint32_t nlen = (uint32_t)op.len(nic);
+  uint32_t ninit = op.init_crc(nic);
+  uint32_t s = 0;
+  for (;;) {
+    const bool last = r == 0;  // this round ends the row's span
+    const bool go = live && (!last || ni < count);
+    RowSpan nsp = sp;
+    if (last) nsp = row_span(base + noff, nlen, ninit);
+    const RowSpan lsp = row_span_sel(go && last, nsp, sp);
+    const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
+    const uint32_t li = go && last ? nic : i;
+    // unconditional: the next unit's chunk and epilogue inputs, and the
+    // descriptor of the span after it (the same one again while unused)
+    const Chunk nxt = row_load_chunk(lsp, lr, c);
+    const typename Op::Pre pnxt = op.pre(li, lsp.ptr, lsp.n);
+    const uint32_t nni = go && last ? ni + nrows : ni;
+    const uint32_t nnic = nni < count ? nni : li;
+    const uint64_t noff2 = op.off(nnic);
+    const uint32_t nlen2 = (uint32_t)op.len(nnic);
+    const uint32_t ninit2 = op.init_crc(nnic);
+    s = row_round(s, cur, sp, r, c, L);
+    if (wave_any(live && last)) op.finish(i, row_finish(s, sp, Lf), pcur, live && last && c == 0);
+    if (!wave_any(go)) break;
+    live = go;
+    i = li;
+    ni = nni;
+    nic = nnic;
+    sp = lsp;
+    r = lr;
+    cur = nxt;
+    pcur = pnxt;
+    noff = noff2;
+    nlen = nlen2;
+    ninit = ninit2;
   }
 }
 

@@ -180,13 +180,49 @@ struct CrcRowT<OpWalFragCrc> {
   static constexpr bool value = false;
 };
 
+// Ragged-batch driver per op: the row driver (one 16-lane row per span,
+// crc_rows_driver) where the spans are WAL-sized, the wave driver otherwise.
+// MCK_CRC_ROWS=0|1 forces one for every ragged batch (A/B measurements).
+template <class Op>
+struct CrcRowsDefault {
+  static constexpr bool value = false;
+};
+template <>
+struct CrcRowsDefault<OpWalFragCrc> {
+  static constexpr bool value = true;
+};
+template <>
+struct CrcRowsDefault<OpCrcWal> {
+  static constexpr bool value = true;
+};
+int crc_rows_force() {
+  static const int v = [] {
+    const char* e = getenv("MCK_CRC_ROWS");
+    return !e ? -1 : atoi(e) ? 1 : 0;
+  }();
+  return v;
+}
+
 // ---- launchers -------------------------------------------------------------
+template <class Op>
+int launch_crc_rows(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
+  int rc = ensure_lds(k_crc_rows<Op>, dev);
+  if (rc) return rc;
+  // persistent: one 16-wave workgroup (64 rows) per CU
+  const uint32_t grid = std::min<uint32_t>(ncu, (count + 63) / 64);
+  hipLaunchKernelGGL((k_crc_rows<Op>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, count);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
 template <class Op>
 int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
   if (!count) return MCK_OK;
   int dev, ncu;
   int rc = current_device(&dev, &ncu);
   if (rc) return rc;
+  const int force = crc_rows_force();
+  if (force == 1 || (force < 0 && CrcRowsDefault<Op>::value)) return launch_crc_rows(op, count, st, dev, ncu);
   // persistent: one 16-wave workgroup per CU (160 KiB of LDS each), with
   // row-transposed loads (CrcRowT)
   constexpr bool T = CrcRowT<Op>::value;

@@ -132,8 +132,8 @@ struct OpCrcValue {
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return init ? init[i] : 0u; }
   __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
-  __device__ void finish(uint32_t i, uint32_t crc, const Pre& = Pre{}) const {
-    if ((threadIdx.x & 63) == 0) out[i] = (flags & 1u) ? crc_mask(crc) : crc;
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre&, bool writer) const {
+    if (writer) out[i] = (flags & 1u) ? crc_mask(crc) : crc;
   }
 };
 
@@ -152,8 +152,8 @@ struct OpCrcWal {
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return tc.v[types[i] & 15]; }
   __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
-  __device__ void finish(uint32_t i, uint32_t crc, const Pre& = Pre{}) const {
-    if ((threadIdx.x & 63) == 0) out[i] = crc_mask(crc);
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre&, bool writer) const {
+    if (writer) out[i] = crc_mask(crc);
   }
 };
 
@@ -172,9 +172,9 @@ struct OpCrcBlock {
     return block_pre<MODE>(a, i, ptr + len - (MODE == kModeVerify ? 1 : 0),
                            ptr - reinterpret_cast<uint64_t>(a.s.base), MODE == kModeVerify);
   }
-  __device__ void finish(uint32_t i, uint32_t crc, const Pre& e) const {
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre& e, bool writer) const {
     if (MODE == kModeTrailer || (MODE == kModeBuiltin && a.last)) crc = crc_extend_byte(crc, (uint8_t)e.last);
-    if ((threadIdx.x & 63) == 0) block_epilogue<MODE>(a, i, crc_mask(crc), e);
+    if (writer) block_epilogue<MODE>(a, i, crc_mask(crc), e);
   }
 };
 
@@ -182,6 +182,13 @@ template <class Op, bool T = false>
 __global__ __launch_bounds__(1024) void k_crc(Op op, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   crc_spans_driver<Op, T>(op, count, lds, &g_crc_tables);
+}
+
+// one 16-lane row per span (crc_rows_driver): small and mid-size spans
+template <class Op>
+__global__ __launch_bounds__(1024) void k_crc_rows(Op op, uint32_t count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  crc_rows_driver<Op>(op, count, lds, &g_crc_tables);
 }
 
 // uniform batches (see CrcUniform)
@@ -447,8 +454,8 @@ struct OpWalFragCrc {
   __device__ uint64_t len(uint32_t i) const { return frags[i].length; }
   __device__ uint32_t init_crc(uint32_t i) const { return tc.v[frags[i].type & 15]; }
   __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
-  __device__ void finish(uint32_t i, uint32_t crc, const Pre& = Pre{}) const {
-    if ((threadIdx.x & 63) == 0) out[i] = crc_mask(crc);
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre&, bool writer) const {
+    if (writer) out[i] = crc_mask(crc);
   }
 };
 
@@ -691,10 +698,10 @@ struct OpBlobRecord {
     // (record headers sit at any byte offset: vload16_any, never s_load)
     return Pre{vload16_any(ptr - 32), vload16_any(ptr - 16)};
   }
-  __device__ void finish(uint32_t i, uint32_t crc, const Pre& e) const {
+  __device__ void finish(uint32_t i, uint32_t crc, const Pre& e, bool writer) const {
     const uint32_t hcrc = crc_mask(blob_header_crc(e));
     const uint32_t bcrc = crc_mask(crc);
-    if ((threadIdx.x & 63) != 0) return;
+    if (!writer) return;
     if (WRITE) {  // BlobLogRecord::EncodeHeaderTo: the two CRC fields, LE
       uint8_t* h = const_cast<uint8_t*>(file) + rec_off[i] + 24;
 #pragma unroll

@@ -19,6 +19,10 @@ constexpr int kChunkBytes = 64;
 constexpr int kRoundBytes = 64 * kChunkBytes;                   // 4096
 constexpr int kGapBytes = kRoundBytes - kChunkBytes;            // 4032
 constexpr int kMaxUnshift = 64;                                 // k in [0,64)
+// Row driver (mck_crc.hpp crc_rows_driver): a 16-lane row covers one 1 KiB
+// round of a span.
+constexpr int kRowRoundBytes = 16 * kChunkBytes;                // 1024
+constexpr int kRowGapBytes = kRowRoundBytes - kChunkBytes;      // 960
 
 struct CrcTables {
   uint32_t step[4][256];          // zshift(v << 8t, 4): the 4-byte step
@@ -28,6 +32,7 @@ struct CrcTables {
   uint32_t half[8][16];           // zshift(v << 4n, 32): joins a lane's chains
   uint32_t quarter[8][16];        // zshift(v << 4n, 16)
   uint32_t unshift[kMaxUnshift][8][16];  // zshift^-1(v << 4n, k)
+  uint32_t gap_row[8][16];        // zshift(v << 4n, kRowGapBytes): row driver
 };
 
 // ---- host-side GF(2) helpers (also used by the host shims) ----------------
@@ -74,6 +79,9 @@ inline void build_crc_tables(CrcTables* t) {
       t->half[n][v] = gf_mul((uint32_t)v << (4 * n), k32);
       t->quarter[n][v] = gf_mul((uint32_t)v << (4 * n), k16);
     }
+  const uint32_t kr = gf_xpow8n(kRowGapBytes);
+  for (int n = 0; n < 8; n++)
+    for (int v = 0; v < 16; v++) t->gap_row[n][v] = gf_mul((uint32_t)v << (4 * n), kr);
   for (int k = 0; k < kMaxUnshift; k++)
     for (int n = 0; n < 8; n++)
       for (int v = 0; v < 16; v++) {

@@ -1,0 +1,77 @@
+"""The CRC row driver (one 16-lane row per span, four spans per wave;
+mck_crc.hpp crc_rows_driver) against the oracle: it is the default for WAL
+records and WAL-writer fragments, and MCK_CRC_ROWS=1 routes every ragged
+CRC batch through it -- the generic-op parity tests are re-run that way in a
+child process (the switch is read once per process)."""
+import os
+import random
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from formats import splitmix_bytes
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _batch(torch, seed, lens, gap=64):
+    rnd = random.Random(seed)
+    offs, pos = [], 0
+    for n in lens:
+        pos += rnd.randrange(0, gap)
+        offs.append(pos)
+        pos += n
+    host = splitmix_bytes(seed, pos + 64)
+    dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda")
+    return host, dev, offs
+
+
+def test_wal_record_crc_small_ragged_many(gpu, oracle):
+    """100K WAL records of 0..1100 B at every alignment: far more spans than
+    rows (each row walks ~6 spans), records crossing 1 KiB rounds."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(17)
+    lens = [rnd.randrange(0, 1101) for _ in range(100_000)]
+    lens[:40] = list(range(0, 40))
+    host, dev, offs = _batch(torch, 17, lens)
+    types = [rnd.choice([1, 2, 3, 4, 5, 6, 7, 8]) for _ in lens]
+    sp = S.Spans(dev, len(lens), offsets=torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                 lengths=torch.tensor(lens, dtype=torch.int32, device="cuda"))
+    got = S.wal_record_crc_batch(sp, torch.tensor(types, dtype=torch.uint8, device="cuda"), 0xC0FFEE)
+    got = got.cpu().numpy().view(np.uint32)
+    for k in range(len(lens)):
+        o, n, t = offs[k], lens[k], types[k]
+        assert int(got[k]) == oracle.WalRecordCrc(t, host[o:o + n], t >= 5, 0xC0FFEE), (k, n, t)
+
+
+def test_generic_ops_through_rows_subprocess(gpu):
+    """CRC value/extend/mask, SST trailer + verify (context checksums,
+    corruption), blob records and WAL paths with MCK_CRC_ROWS=1."""
+    env = dict(os.environ, MCK_CRC_ROWS="1")
+    tests = [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
+        "test_crc32c_batch_ragged", "test_crc32c_known_answers_on_device", "test_scalar_shims",
+        "test_checksum_schemas_on_device", "test_builtin_checksum_batch", "test_sst_trailer_and_verify",
+        "test_wal_record_crc_batch", "test_wal_verify_batch", "test_empty_and_zero_inputs",
+        "test_large_ragged_batches_static_and_dynamic_feeds", "test_crc32c_long_vs_oracle",
+        "test_sst_verify_large_static_feed")]
+    tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_sst_file.py")]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider"] + tests,
+                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout
+
+
+def test_wave_driver_for_wal_subprocess(gpu):
+    """And the other way round: MCK_CRC_ROWS=0 keeps WAL records and the WAL
+    writer on the wave driver (both stay covered)."""
+    env = dict(os.environ, MCK_CRC_ROWS="0")
+    tests = [os.path.join(HERE, "test_wal_writer.py"),
+             os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
+                        "-k", "not subprocess"] + tests,
+                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
