@@ -6,7 +6,7 @@ set -o pipefail
 OUT=gpurun_out/${1:-r2rows}
 mkdir -p $OUT
 B="timeout -k 10 120 python bench.py"
-timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 || { tail -30 $OUT/pytest.log; exit 1; }
 tail -2 $OUT/pytest.log
 for w in "walrec" "ragged --span-min 512 --span-max 512" "ragged --span-min 100 --span-max 1100" "ragged --span-min 4096 --span-max 4096" "walwrite" "sst"; do
   tag=$(echo $w | tr ' ' '_' | tr -d '-')

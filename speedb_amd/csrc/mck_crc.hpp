@@ -811,13 +811,25 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
 // instruction stream: the lane-final shift zshift(s, 64 (15 - c)) is the
 // wave table's lane 48 + c, the row XOR is a 4-step DPP butterfly, and the
 // head/tail/init handling of crc_round runs per row (vector values instead
-// of wave-uniform ones).  Rows take spans statically (row g: g, g + R,
-// g + 2R, ... over the R rows of the grid), the descriptor of a row's next
-// span is loaded one span ahead, and every load is issued unconditionally
-// (exec-masked loads would force vmcnt(0) waits, see crc_load_chunk).
-// LDS: the wave driver's image plus the 960-byte row gap map at kLdsRowGap.
+// of wave-uniform ones).  Rows take spans from an LDS ticket of their
+// workgroup's share -- see row_desc_stage for the LDS-staged descriptor feed --
+// and every data load is issued unconditionally (exec-masked loads would
+// force vmcnt(0) waits, see crc_load_chunk).
+// LDS: the wave driver's image plus the 960-byte row gap map, the init
+// tables and the descriptor cache, all below the step tables.
 constexpr uint32_t kLdsRowGap = kLdsLowEnd;  // 512 B, below the step tables
-static_assert(kLdsRowGap + 512 <= kLdsStep, "row gap map must fit below the step tables");
+// How the row driver gets a span's CRC init (Extend's init_crc):
+//   kInitZero  -- always 0 (Value): ~init is injected from a 64-entry LDS
+//                 table of unshift(~0, hb) instead of an 8-lookup map;
+//   kInitTyped -- init = type_crc[key & 15] (WAL records: key = the record
+//                 type byte), from a [16][64] LDS table built at kernel start;
+//   kInitArray -- arbitrary per-span init (key = the init itself).
+// init_key(i) is the only load; the table lookup happens when the span is
+// set up, one iteration later, so no load depends on another in flight.
+enum RowInit : int { kInitZero = 0, kInitTyped = 1, kInitArray = 2 };
+constexpr uint32_t kLdsRowInj = kLdsRowGap + 512;     // [16][64] u32: unshift(~init_t, k)
+constexpr uint32_t kLdsRowInit = kLdsRowInj + 4096;   // [16] u32: init_t
+static_assert(kLdsRowInit + 64 <= kLdsStep, "row tables must fit below the step tables");
 static_assert(offsetof(CrcTables, gap_row) - offsetof(CrcTables, unshift) == kMaxUnshift * 512, "layout");
 
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
@@ -845,20 +857,37 @@ struct RowSpan {
   uint32_t init;
 };
 
-__device__ __forceinline__ RowSpan row_span(uint64_t ptr, uint32_t n, uint32_t init) {
+// Per-workgroup init tables (after the LDS fill): inj[t][k] =
+// unshift(~init_t, k) and init_t, with init_t = the op's typed init for
+// kInitTyped ops and 0 otherwise (row t = 0 then serves kInitZero).
+template <class Op>
+__device__ __forceinline__ void row_init_tables(const Op& op) {
+  const uint32_t t = threadIdx.x;  // kCrcBlock = 1024 = 16 x 64 entries
+  const uint32_t init = Op::kTypedInit ? op.typed_init(t >> 6) : 0u;
+  *lds_p32(kLdsRowInj + 4 * t) = crc_unshift(t & 63, ~init);
+  if ((t & 63) == 0) *lds_p32(kLdsRowInit + 4 * (t >> 6)) = init;
+}
+
+__device__ __forceinline__ RowSpan row_span(uint64_t ptr, uint32_t n, uint32_t key, int kind) {
   RowSpan s;
   s.ptr = ptr;
   s.n = n;
   s.a0 = ptr & ~15ull;
   s.a1 = (ptr + n + 15) & ~15ull;
   s.kt = (uint32_t)(s.a1 - (ptr + n));
-  s.init = init;
   const uint32_t cover = (uint32_t)(s.a1 - ptr);
   s.rounds = n == 0 ? 1 : (int32_t)((cover + kRowRoundBytes - 1) / kRowRoundBytes);
   const uint32_t lead = (uint32_t)kRowRoundBytes * (uint32_t)s.rounds - cover;
   s.owner = n == 0 ? 16 : (int32_t)(lead >> 6);
   s.hb = lead & 63u;
-  s.inj = crc_unshift(s.hb, ~init);  // unshift by 0 is the identity
+  if (kind == kInitArray) {  // wave-uniform
+    s.init = key;
+    s.inj = crc_unshift(s.hb, ~key);  // unshift by 0 is the identity
+  } else {
+    const uint32_t t = kind == kInitTyped ? (key & 15u) : 0u;
+    s.inj = *lds_p32(kLdsRowInj + 4 * (t * 64 + s.hb));
+    s.init = *lds_p32(kLdsRowInit + 4 * t);
+  }
   return s;
 }
 
@@ -925,63 +954,108 @@ __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, co
   return sp.n == 0 ? sp.init : ~p;
 }
 
+// Descriptor feed of the row driver: workgroup b owns spans first + b + G t
+// (t < its share, interleaved as in FeedLds), staged in LDS once as 16-byte
+// records {off, len, key}; a row takes the next one with an LDS ticket when
+// its span ends, one span ahead, so the chunk loads of a new span never wait
+// for a descriptor load (every load in the loop is a data load).  The host
+// splits batches whose share exceeds kRowDescCache into several launches.
+constexpr uint32_t kRowDescCache = 1536;
+constexpr uint32_t kLdsRowDesc = kLdsRowInit + 64;                   // 16 B x 1536
+constexpr uint32_t kLdsRowTicket = kLdsRowDesc + 16 * kRowDescCache;  // u32
+static_assert(kLdsRowTicket + 4 <= kLdsStep, "row descriptor cache must fit below the step tables");
+
 template <class Op>
-__device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t count, uint8_t* lds,
+__device__ __forceinline__ void row_desc_stage(const Op& op, uint32_t first, uint32_t count) {
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t n = (count - b + G - 1) / G;
+  for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+    const uint32_t i = first + b + G * t;
+    const uint64_t off = op.off(i);
+    const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)op.len(i), op.init_key(i)};
+    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsRowDesc + 16 * t)) = d;
+  }
+  if (threadIdx.x == 0) *lds_p32(kLdsRowTicket) = 0;
+}
+
+// Next ticket for every row that asks (take, row-uniform): lane 0 of the row
+// takes it, the row reads it.
+__device__ __forceinline__ uint32_t row_ticket(bool take) {
+  uint32_t t = 0;
+  if ((threadIdx.x & 15) == 0 && take)
+    t = __hip_atomic_fetch_add(lds_p32(kLdsRowTicket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x & 0x30u) << 2), (int)t);
+}
+
+// Descriptor of ticket t; t >= share (no span left) reads slot 0, a valid
+// span of the share (slots past the share hold no descriptor).
+__device__ __forceinline__ uint4 row_desc(uint32_t t, uint32_t share) {
+  const span_u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const span_u32x4*>(
+      static_cast<size_t>(kLdsRowDesc + 16 * (t < share ? t : 0)));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+template <class Op>
+__device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                 const CrcTables* __restrict__ g) {
   crc_fill_rows(lds, g);
+  row_desc_stage(op, first, count);
   __syncthreads();
+  row_init_tables(op);
+  __syncthreads();
+  const int kind = op.init_kind();
   const CrcLane L = crc_lane();
   CrcLane Lf = L;
   const uint32_t c = threadIdx.x & 15;
   Lf.lane4 = (48u + c) << 2;
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint32_t nrows = gridDim.x * wpb * 4;
-  const uint32_t row = (blockIdx.x * wpb + (threadIdx.x >> 6)) * 4 + ((threadIdx.x >> 4) & 3);
+  const uint32_t G = gridDim.x;
+  const uint32_t share = (count - blockIdx.x + G - 1) / G;  // this workgroup's spans
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  bool live = row < count;
-  uint32_t i = live ? row : 0;
-  RowSpan sp = row_span(base + op.off(i), (uint32_t)op.len(i), op.init_crc(i));
+  // the row's current span (ticket t) and the next one (ticket nt, prefetched)
+  uint32_t t = row_ticket(true);
+  bool live = t < share;
+  uint4 d = row_desc(t, share);
+  uint32_t i = first + blockIdx.x + G * (live ? t : 0);
+  RowSpan sp = row_span(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kind);
   int r = sp.rounds - 1;
   Chunk cur = row_load_chunk(sp, r, c);
   typename Op::Pre pcur = op.pre(i, sp.ptr, sp.n);
-  // the row's next span, one span ahead
-  uint32_t ni = row + nrows;
-  uint32_t nic = ni < count ? ni : i;
-  uint64_t noff = op.off(nic);
-  uint32_t nlen = (uint32_t)op.len(nic);
-  uint32_t ninit = op.init_crc(nic);
+  uint32_t nt = row_ticket(true);
+  uint4 nd = row_desc(nt, share);
   uint32_t s = 0;
   for (;;) {
     const bool last = r == 0;  // this round ends the row's span
-    const bool go = live && (!last || ni < count);
+    const bool go = live && (!last || nt < share);
     RowSpan nsp = sp;
-    if (last) nsp = row_span(base + noff, nlen, ninit);
-    const RowSpan lsp = row_span_sel(go && last, nsp, sp);
+    if (last) nsp = row_span(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kind);
+    const bool sw = go && last;  // the row moves to its next span
+    const RowSpan lsp = row_span_sel(sw, nsp, sp);
     const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
-    const uint32_t li = go && last ? nic : i;
-    // unconditional: the next unit's chunk and epilogue inputs, and the
-    // descriptor of the span after it (the same one again while unused)
+    const uint32_t li = sw ? first + blockIdx.x + G * nt : i;
+    // unconditional: the next unit's chunk and epilogue inputs
     const Chunk nxt = row_load_chunk(lsp, lr, c);
     const typename Op::Pre pnxt = op.pre(li, lsp.ptr, lsp.n);
-    const uint32_t nni = go && last ? ni + nrows : ni;
-    const uint32_t nnic = nni < count ? nni : li;
-    const uint64_t noff2 = op.off(nnic);
-    const uint32_t nlen2 = (uint32_t)op.len(nnic);
-    const uint32_t ninit2 = op.init_crc(nnic);
+    // rows that moved on take the ticket after (LDS only)
+    uint32_t nnt = nt;
+    uint4 nnd = nd;
+    if (wave_any(sw)) {
+      const uint32_t tk = row_ticket(sw);
+      if (sw) {
+        nnt = tk;
+        nnd = row_desc(tk, share);
+      }
+    }
     s = row_round(s, cur, sp, r, c, L);
     if (wave_any(live && last)) op.finish(i, row_finish(s, sp, Lf), pcur, live && last && c == 0);
     if (!wave_any(go)) break;
     live = go;
     i = li;
-    ni = nni;
-    nic = nnic;
+    nt = nnt;
+    nd = nnd;
     sp = lsp;
     r = lr;
     cur = nxt;
     pcur = pnxt;
-    noff = noff2;
-    nlen = nlen2;
-    ninit = ninit2;
   }
 }
 

@@ -208,10 +208,16 @@ template <class Op>
 int launch_crc_rows(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
   int rc = ensure_lds(k_crc_rows<Op>, dev);
   if (rc) return rc;
-  // persistent: one 16-wave workgroup (64 rows) per CU
-  const uint32_t grid = std::min<uint32_t>(ncu, (count + 63) / 64);
-  hipLaunchKernelGGL((k_crc_rows<Op>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, count);
-  MCK_HIP(hipGetLastError());
+  // persistent: one 16-wave workgroup (64 rows) per CU; each workgroup
+  // stages its share's descriptors in LDS, so a batch runs in launches of
+  // at most ncu * kRowDescCache spans
+  const uint32_t per = (uint32_t)ncu * kRowDescCache;
+  for (uint32_t first = 0; first < count; first += per) {
+    const uint32_t n = std::min(per, count - first);
+    const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
+    hipLaunchKernelGGL((k_crc_rows<Op>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+    MCK_HIP(hipGetLastError());
+  }
   return MCK_OK;
 }
 

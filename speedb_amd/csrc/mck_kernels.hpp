@@ -16,16 +16,38 @@ extern __device__ CrcTables g_crc_tables;
 constexpr uint32_t kRandomPrime = 0x6b9083d9u;  // table/format.cc:573
 
 // ---- span source: the mck_spans descriptor --------------------------------
+// Descriptor loads go through global (address_space(1)) pointers: written
+// as `lengths ? lengths[i] : length` the compiler may select between the
+// array and the kernel argument's own address and issue a FLAT load, which
+// also counts in lgkmcnt -- every LDS wait of the table steps then waits for
+// that memory load too.
+typedef __attribute__((address_space(1))) const uint32_t gdesc_u32_t;
+typedef __attribute__((address_space(1))) const uint64_t gdesc_u64_t;
+typedef __attribute__((address_space(1))) const uint8_t gdesc_u8_t;
+__device__ __forceinline__ uint32_t ldg_u32(const uint32_t* p, uint32_t i) {
+  return *reinterpret_cast<gdesc_u32_t*>(reinterpret_cast<uint64_t>(p + i));
+}
+__device__ __forceinline__ uint64_t ldg_u64(const uint64_t* p, uint32_t i) {
+  return *reinterpret_cast<gdesc_u64_t*>(reinterpret_cast<uint64_t>(p + i));
+}
+__device__ __forceinline__ uint8_t ldg_u8(const uint8_t* p, uint32_t i) {
+  return *reinterpret_cast<gdesc_u8_t*>(reinterpret_cast<uint64_t>(p + i));
+}
+
 struct SpanSrc {
   const uint8_t* base;
   const uint64_t* offsets;
   const uint32_t* lengths;
   uint64_t stride;
   uint32_t length;
-  __device__ __forceinline__ uint64_t off(uint32_t i) const { return offsets ? offsets[i] : (uint64_t)i * stride; }
-  __device__ __forceinline__ uint64_t len(uint32_t i) const { return lengths ? lengths[i] : length; }
+  __device__ __forceinline__ uint64_t off(uint32_t i) const {
+    return offsets ? ldg_u64(offsets, i) : (uint64_t)i * stride;
+  }
+  __device__ __forceinline__ uint64_t len(uint32_t i) const { return lengths ? ldg_u32(lengths, i) : length; }
   __device__ __forceinline__ const uint8_t* ptr(uint32_t i) const { return base + off(i); }
 };
+
+
 
 // table/format.h:119-146 ChecksumModifierForContext
 __device__ __forceinline__ uint32_t context_modifier(uint32_t base, uint64_t offset) {
@@ -131,6 +153,10 @@ struct OpCrcValue {
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return init ? init[i] : 0u; }
+  static constexpr bool kTypedInit = false;
+  __device__ int init_kind() const { return init ? kInitArray : kInitZero; }
+  __device__ uint32_t init_key(uint32_t i) const { return init ? ldg_u32(init, i) : 0u; }
+  __device__ uint32_t typed_init(uint32_t) const { return 0u; }
   __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
   __device__ void finish(uint32_t i, uint32_t crc, const Pre&, bool writer) const {
     if (writer) out[i] = (flags & 1u) ? crc_mask(crc) : crc;
@@ -151,6 +177,10 @@ struct OpCrcWal {
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return tc.v[types[i] & 15]; }
+  static constexpr bool kTypedInit = true;
+  __device__ int init_kind() const { return kInitTyped; }
+  __device__ uint32_t init_key(uint32_t i) const { return ldg_u8(types, i); }
+  __device__ uint32_t typed_init(uint32_t t) const { return tc.v[t & 15]; }
   __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
   __device__ void finish(uint32_t i, uint32_t crc, const Pre&, bool writer) const {
     if (writer) out[i] = crc_mask(crc);
@@ -167,6 +197,10 @@ struct OpCrcBlock {
   __device__ uint64_t off(uint32_t i) const { return a.s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return a.s.len(i) + (MODE == kModeVerify ? 1 : 0); }
   __device__ uint32_t init_crc(uint32_t) const { return 0u; }
+  static constexpr bool kTypedInit = false;
+  __device__ int init_kind() const { return kInitZero; }
+  __device__ uint32_t init_key(uint32_t) const { return 0u; }
+  __device__ uint32_t typed_init(uint32_t) const { return 0u; }
   __device__ Pre pre(uint32_t i, uint64_t ptr, uint64_t len) const {
     // verify: bytes from the type byte (ptr + len - 1) on
     return block_pre<MODE>(a, i, ptr + len - (MODE == kModeVerify ? 1 : 0),
@@ -186,9 +220,9 @@ __global__ __launch_bounds__(1024) void k_crc(Op op, uint32_t count) {
 
 // one 16-lane row per span (crc_rows_driver): small and mid-size spans
 template <class Op>
-__global__ __launch_bounds__(1024) void k_crc_rows(Op op, uint32_t count) {
+__global__ __launch_bounds__(1024) void k_crc_rows(Op op, uint32_t first, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_rows_driver<Op>(op, count, lds, &g_crc_tables);
+  crc_rows_driver<Op>(op, first, count, lds, &g_crc_tables);
 }
 
 // uniform batches (see CrcUniform)
@@ -453,6 +487,10 @@ struct OpWalFragCrc {
   __device__ uint64_t off(uint32_t i) const { return frags[i].src_off; }
   __device__ uint64_t len(uint32_t i) const { return frags[i].length; }
   __device__ uint32_t init_crc(uint32_t i) const { return tc.v[frags[i].type & 15]; }
+  static constexpr bool kTypedInit = true;
+  __device__ int init_kind() const { return kInitTyped; }
+  __device__ uint32_t init_key(uint32_t i) const { return ldg_u8(&frags[i].type, 0); }
+  __device__ uint32_t typed_init(uint32_t t) const { return tc.v[t & 15]; }
   __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
   __device__ void finish(uint32_t i, uint32_t crc, const Pre&, bool writer) const {
     if (writer) out[i] = crc_mask(crc);
@@ -694,6 +732,10 @@ struct OpBlobRecord {
   __device__ uint64_t off(uint32_t i) const { return rec_off[i] + 32; }
   __device__ uint64_t len(uint32_t i) const { return blob_len[i]; }
   __device__ uint32_t init_crc(uint32_t) const { return 0u; }
+  static constexpr bool kTypedInit = false;
+  __device__ int init_kind() const { return kInitZero; }
+  __device__ uint32_t init_key(uint32_t) const { return 0u; }
+  __device__ uint32_t typed_init(uint32_t) const { return 0u; }
   __device__ Pre pre(uint32_t, uint64_t ptr, uint64_t) const {
     // (record headers sit at any byte offset: vload16_any, never s_load)
     return Pre{vload16_any(ptr - 32), vload16_any(ptr - 16)};
