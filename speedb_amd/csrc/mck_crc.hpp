@@ -830,6 +830,15 @@ enum RowInit : int { kInitZero = 0, kInitTyped = 1, kInitArray = 2 };
 constexpr uint32_t kLdsRowInj = kLdsRowGap + 512;     // [16][64] u32: unshift(~init_t, k)
 constexpr uint32_t kLdsRowInit = kLdsRowInj + 4096;   // [16] u32: init_t
 static_assert(kLdsRowInit + 64 <= kLdsStep, "row tables must fit below the step tables");
+// descriptor cache of the row feed (row_desc_stage) and its ticket
+constexpr uint32_t kRowDescCache = 1536;
+constexpr uint32_t kLdsRowDesc = kLdsRowInit + 64;                   // 16 B x 1536
+constexpr uint32_t kLdsRowTicket = kLdsRowDesc + 16 * kRowDescCache;  // u32
+// byte masks of one 16-byte piece: head[h] keeps bytes >= h, tail[k] keeps
+// the first 16 - k bytes (h, k < 16), as 4 words
+constexpr uint32_t kLdsRowMaskHead = kLdsRowTicket + 64;
+constexpr uint32_t kLdsRowMaskTail = kLdsRowMaskHead + 256;
+static_assert(kLdsRowMaskTail + 256 <= kLdsStep, "row tables must fit below the step tables");
 static_assert(offsetof(CrcTables, gap_row) - offsetof(CrcTables, unshift) == kMaxUnshift * 512, "layout");
 
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
@@ -866,6 +875,19 @@ __device__ __forceinline__ void row_init_tables(const Op& op) {
   const uint32_t init = Op::kTypedInit ? op.typed_init(t >> 6) : 0u;
   *lds_p32(kLdsRowInj + 4 * t) = crc_unshift(t & 63, ~init);
   if ((t & 63) == 0) *lds_p32(kLdsRowInit + 4 * (t >> 6)) = init;
+  if (t < 128) {
+    const int h = (int)(t >> 2) & 15, k = (int)(t & 3);
+    uint32_t m;
+    if (t < 64) {  // keep bytes >= h of the piece
+      const int d = h - 4 * k;
+      m = d <= 0 ? 0xFFFFFFFFu : d >= 4 ? 0u : 0xFFFFFFFFu << (8 * d);
+      *lds_p32(kLdsRowMaskHead + 4 * (t & 63)) = m;
+    } else {  // keep the first 16 - h bytes
+      const int keep = 16 - h - 4 * k;
+      m = keep >= 4 ? 0xFFFFFFFFu : keep <= 0 ? 0u : 0xFFFFFFFFu >> (8 * (4 - keep));
+      *lds_p32(kLdsRowMaskTail + 4 * (t & 63)) = m;
+    }
+  }
 }
 
 __device__ __forceinline__ RowSpan row_span(uint64_t ptr, uint32_t n, uint32_t key, int kind) {
@@ -906,27 +928,59 @@ __device__ __forceinline__ RowSpan row_span_sel(bool a, const RowSpan& x, const 
   return s;
 }
 
-// Row round r of a span: lane c's 64-byte chunk; in the first round pieces
-// below a0 read a0 (discarded).
-__device__ __forceinline__ Chunk row_load_chunk(const RowSpan& sp, int r, uint32_t c) {
+// Row round r of a span: lane c's 64-byte chunk.  In the first round the
+// pieces wholly before a0 read the zero piece `zp` instead, so they need no
+// masking (and lanes before the owner hash zeros); only the piece at a0
+// keeps ptr - a0 < 16 bytes of another span to mask (row_round).
+__device__ __forceinline__ Chunk row_load_chunk(const RowSpan& sp, int r, uint32_t c, uint64_t zp) {
   const uint64_t b = sp.a1 - (uint64_t)kRowRoundBytes * (uint32_t)(r + 1) + 64ull * c;
   const bool first = r == sp.rounds - 1;
+  // first round: b >= a0 - 1024, so the low words give the exact offset
+  const int32_t rel = first ? (int32_t)((uint32_t)b - (uint32_t)sp.a0) : 0;
   Chunk ch;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
-    uint64_t a = b + 16ull * j;
-    a = (first && a < sp.a0) ? sp.a0 : a;
+    const uint64_t a = rel < -16 * j ? zp : b + 16ull * j;
     ch.v[j] = span_load16<false>(a);
   }
   return ch;
+}
+
+__device__ __forceinline__ uint4 lds_u32x4(uint32_t off) {
+  const span_u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const span_u32x4*>(static_cast<size_t>(off));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void and4(uint4& v, const uint4& m) {
+  v.x &= m.x;
+  v.y &= m.y;
+  v.z &= m.z;
+  v.w &= m.w;
 }
 
 __device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpan& sp, int r, uint32_t c,
                                               const CrcLane& L) {
   const bool first = r == sp.rounds - 1;
   const bool own = (int32_t)c == sp.owner;
-  if (wave_any(first && own && sp.hb != 0)) crc_zero_head(ch, (first && own) ? sp.hb : 0u);
-  if (wave_any(r == 0 && sp.kt != 0)) crc_keep_head_bytes(ch.v[3], (r == 0 && c == 15) ? 16u - sp.kt : 16u);
+  const uint32_t h0 = (uint32_t)sp.ptr & 15u;  // bytes of the a0 piece before ptr
+  if (wave_any(first && own && h0 != 0)) {
+    // the owner's a0 piece is its piece hb >> 4 (the ones before it are
+    // zero): w & (m | ~sel) with sel = all-ones on that piece, one bitop3
+    // per word
+    const uint4 m = lds_u32x4(kLdsRowMaskHead + 16 * h0);
+    const uint32_t pa = (first && own) ? sp.hb >> 4 : 4u;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint32_t sel = (uint32_t)j == pa ? ~0u : 0u;
+      ch.v[j].x = __builtin_amdgcn_bitop3_b32(ch.v[j].x, m.x, sel, 0xD0);
+      ch.v[j].y = __builtin_amdgcn_bitop3_b32(ch.v[j].y, m.y, sel, 0xD0);
+      ch.v[j].z = __builtin_amdgcn_bitop3_b32(ch.v[j].z, m.z, sel, 0xD0);
+      ch.v[j].w = __builtin_amdgcn_bitop3_b32(ch.v[j].w, m.w, sel, 0xD0);
+    }
+  }
+  if (wave_any(r == 0 && sp.kt != 0)) {
+    const uint4 m = lds_u32x4(kLdsRowMaskTail + 16 * ((r == 0 && c == 15) ? sp.kt : 0u));
+    and4(ch.v[3], m);
+  }
   uint32_t gap = 0;
   if (wave_any(!first)) gap = crc_nibmap(kLdsRowGap, s);
   uint32_t x = first ? (own ? sp.inj : 0u) : gap;
@@ -934,7 +988,7 @@ __device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpa
   x ^= w[0];
 #pragma unroll
   for (int k = 0; k < 16; k++) x = crc_step4x(x, L, k < 15 ? w[k + 1] : 0u);
-  return (first && (int32_t)c < sp.owner) ? 0u : x;
+  return x;
 }
 
 // XOR over the 16 lanes of each row, in every lane of the row.
@@ -960,10 +1014,7 @@ __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, co
 // its span ends, one span ahead, so the chunk loads of a new span never wait
 // for a descriptor load (every load in the loop is a data load).  The host
 // splits batches whose share exceeds kRowDescCache into several launches.
-constexpr uint32_t kRowDescCache = 1536;
-constexpr uint32_t kLdsRowDesc = kLdsRowInit + 64;                   // 16 B x 1536
-constexpr uint32_t kLdsRowTicket = kLdsRowDesc + 16 * kRowDescCache;  // u32
-static_assert(kLdsRowTicket + 4 <= kLdsStep, "row descriptor cache must fit below the step tables");
+
 
 template <class Op>
 __device__ __forceinline__ void row_desc_stage(const Op& op, uint32_t first, uint32_t count) {
@@ -1018,7 +1069,8 @@ __device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, ui
   uint32_t i = first + blockIdx.x + G * (live ? t : 0);
   RowSpan sp = row_span(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kind);
   int r = sp.rounds - 1;
-  Chunk cur = row_load_chunk(sp, r, c);
+  const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
+  Chunk cur = row_load_chunk(sp, r, c, zp);
   typename Op::Pre pcur = op.pre(i, sp.ptr, sp.n);
   uint32_t nt = row_ticket(true);
   uint4 nd = row_desc(nt, share);
@@ -1033,7 +1085,7 @@ __device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, ui
     const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
     const uint32_t li = sw ? first + blockIdx.x + G * nt : i;
     // unconditional: the next unit's chunk and epilogue inputs
-    const Chunk nxt = row_load_chunk(lsp, lr, c);
+    const Chunk nxt = row_load_chunk(lsp, lr, c, zp);
     const typename Op::Pre pnxt = op.pre(li, lsp.ptr, lsp.n);
     // rows that moved on take the ticket after (LDS only)
     uint32_t nnt = nt;

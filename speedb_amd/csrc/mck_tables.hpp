@@ -33,6 +33,7 @@ struct CrcTables {
   uint32_t quarter[8][16];        // zshift(v << 4n, 16)
   uint32_t unshift[kMaxUnshift][8][16];  // zshift^-1(v << 4n, k)
   uint32_t gap_row[8][16];        // zshift(v << 4n, kRowGapBytes): row driver
+  uint32_t zero16[4];             // a zero piece: the row driver's loads before a span
 };
 
 // ---- host-side GF(2) helpers (also used by the host shims) ----------------
@@ -79,6 +80,7 @@ inline void build_crc_tables(CrcTables* t) {
       t->half[n][v] = gf_mul((uint32_t)v << (4 * n), k32);
       t->quarter[n][v] = gf_mul((uint32_t)v << (4 * n), k16);
     }
+  for (int k = 0; k < 4; k++) t->zero16[k] = 0;
   const uint32_t kr = gf_xpow8n(kRowGapBytes);
   for (int n = 0; n < 8; n++)
     for (int v = 0; v < 16; v++) t->gap_row[n][v] = gf_mul((uint32_t)v << (4 * n), kr);
