@@ -961,26 +961,23 @@ __device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpa
                                               const CrcLane& L) {
   const bool first = r == sp.rounds - 1;
   const bool own = (int32_t)c == sp.owner;
+  // Unconditional (no branch, so no phi copies of the chunk): the owner's
+  // a0 piece -- its piece hb >> 4, the ones before it are zero -- keeps the
+  // bytes from ptr on, w & (m | ~sel) with sel = all-ones on that piece (one
+  // bitop3 per word); lane 15's last piece keeps the bytes before the end.
   const uint32_t h0 = (uint32_t)sp.ptr & 15u;  // bytes of the a0 piece before ptr
-  if (wave_any(first && own && h0 != 0)) {
-    // the owner's a0 piece is its piece hb >> 4 (the ones before it are
-    // zero): w & (m | ~sel) with sel = all-ones on that piece, one bitop3
-    // per word
-    const uint4 m = lds_u32x4(kLdsRowMaskHead + 16 * h0);
-    const uint32_t pa = (first && own) ? sp.hb >> 4 : 4u;
+  const uint4 mh = lds_u32x4(kLdsRowMaskHead + 16 * h0);
+  const uint4 mt = lds_u32x4(kLdsRowMaskTail + 16 * ((r == 0 && c == 15) ? sp.kt : 0u));
+  const uint32_t pa = (first && own) ? sp.hb >> 4 : 4u;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
-      const uint32_t sel = (uint32_t)j == pa ? ~0u : 0u;
-      ch.v[j].x = __builtin_amdgcn_bitop3_b32(ch.v[j].x, m.x, sel, 0xD0);
-      ch.v[j].y = __builtin_amdgcn_bitop3_b32(ch.v[j].y, m.y, sel, 0xD0);
-      ch.v[j].z = __builtin_amdgcn_bitop3_b32(ch.v[j].z, m.z, sel, 0xD0);
-      ch.v[j].w = __builtin_amdgcn_bitop3_b32(ch.v[j].w, m.w, sel, 0xD0);
-    }
+  for (int j = 0; j < 4; j++) {
+    const uint32_t sel = (uint32_t)j == pa ? ~0u : 0u;
+    ch.v[j].x = __builtin_amdgcn_bitop3_b32(ch.v[j].x, mh.x, sel, 0xD0);
+    ch.v[j].y = __builtin_amdgcn_bitop3_b32(ch.v[j].y, mh.y, sel, 0xD0);
+    ch.v[j].z = __builtin_amdgcn_bitop3_b32(ch.v[j].z, mh.z, sel, 0xD0);
+    ch.v[j].w = __builtin_amdgcn_bitop3_b32(ch.v[j].w, mh.w, sel, 0xD0);
   }
-  if (wave_any(r == 0 && sp.kt != 0)) {
-    const uint4 m = lds_u32x4(kLdsRowMaskTail + 16 * ((r == 0 && c == 15) ? sp.kt : 0u));
-    and4(ch.v[3], m);
-  }
+  and4(ch.v[3], mt);
   uint32_t gap = 0;
   if (wave_any(!first)) gap = crc_nibmap(kLdsRowGap, s);
   uint32_t x = first ? (own ? sp.inj : 0u) : gap;
@@ -1078,8 +1075,9 @@ __device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, ui
   for (;;) {
     const bool last = r == 0;  // this round ends the row's span
     const bool go = live && (!last || nt < share);
-    RowSpan nsp = sp;
-    if (last) nsp = row_span(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kind);
+    // set up unconditionally (rows that are not switching discard it): a
+    // branch would merge the span's registers through copies every round
+    const RowSpan nsp = row_span(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kind);
     const bool sw = go && last;  // the row moves to its next span
     const RowSpan lsp = row_span_sel(sw, nsp, sp);
     const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
