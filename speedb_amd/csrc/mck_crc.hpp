@@ -840,14 +840,18 @@ constexpr uint32_t kLdsRowMaskHead = kLdsRowTicket + 64;
 constexpr uint32_t kLdsRowMaskTail = kLdsRowMaskHead + 256;
 static_assert(kLdsRowMaskTail + 256 <= kLdsStep, "row tables must fit below the step tables");
 static_assert(offsetof(CrcTables, gap_row) - offsetof(CrcTables, unshift) == kMaxUnshift * 512, "layout");
+static_assert(sizeof(((CrcTables*)nullptr)->gap_row[0]) == 512, "one row gap map = 32 slots");
 
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
 
+// W: lanes per row (4, 8, 16); the gap map of that width goes to kLdsRowGap
+template <int W>
 __device__ __forceinline__ void crc_fill_rows(uint8_t* lds, const CrcTables* __restrict__ g) {
+  constexpr int wk = W == 4 ? 0 : W == 8 ? 1 : 2;
   CrcFill f;
   crc_fill_load<true>(f, g);
   const int t = threadIdx.x;
-  const uint4* rg = reinterpret_cast<const uint4*>(&g->gap_row[0][0]);
+  const uint4* rg = reinterpret_cast<const uint4*>(&g->gap_row[wk][0][0]);
   const uint4 x = rg[t < 32 ? t : 0];
   crc_fill_store<true>(f, lds);
   if (t < 32) reinterpret_cast<uint4*>(lds + kLdsRowGap)[t] = x;
@@ -858,8 +862,8 @@ struct RowSpan {
   uint64_t a0;     // ptr rounded down to 16
   uint64_t a1;     // end rounded up to 16
   uint32_t n;      // bytes
-  int32_t rounds;  // 1 KiB row rounds covering [ptr, a1)
-  int32_t owner;   // row lane whose first-round chunk holds ptr (16: none)
+  int32_t rounds;  // 64 W-byte row rounds covering [ptr, a1)
+  int32_t owner;   // row lane whose first-round chunk holds ptr (W: none)
   uint32_t hb;     // ptr - owner's chunk start (< 64)
   uint32_t kt;     // a1 - end (< 16)
   uint32_t inj;    // ~init un-shifted by hb bytes
@@ -890,7 +894,9 @@ __device__ __forceinline__ void row_init_tables(const Op& op) {
   }
 }
 
+template <int W>
 __device__ __forceinline__ RowSpan row_span(uint64_t ptr, uint32_t n, uint32_t key, int kind) {
+  constexpr uint32_t R = 64u * W;
   RowSpan s;
   s.ptr = ptr;
   s.n = n;
@@ -898,9 +904,9 @@ __device__ __forceinline__ RowSpan row_span(uint64_t ptr, uint32_t n, uint32_t k
   s.a1 = (ptr + n + 15) & ~15ull;
   s.kt = (uint32_t)(s.a1 - (ptr + n));
   const uint32_t cover = (uint32_t)(s.a1 - ptr);
-  s.rounds = n == 0 ? 1 : (int32_t)((cover + kRowRoundBytes - 1) / kRowRoundBytes);
-  const uint32_t lead = (uint32_t)kRowRoundBytes * (uint32_t)s.rounds - cover;
-  s.owner = n == 0 ? 16 : (int32_t)(lead >> 6);
+  s.rounds = n == 0 ? 1 : (int32_t)((cover + R - 1) / R);
+  const uint32_t lead = R * (uint32_t)s.rounds - cover;
+  s.owner = n == 0 ? W : (int32_t)(lead >> 6);
   s.hb = lead & 63u;
   if (kind == kInitArray) {  // wave-uniform
     s.init = key;
@@ -932,10 +938,11 @@ __device__ __forceinline__ RowSpan row_span_sel(bool a, const RowSpan& x, const 
 // pieces wholly before a0 read the zero piece `zp` instead, so they need no
 // masking (and lanes before the owner hash zeros); only the piece at a0
 // keeps ptr - a0 < 16 bytes of another span to mask (row_round).
+template <int W>
 __device__ __forceinline__ Chunk row_load_chunk(const RowSpan& sp, int r, uint32_t c, uint64_t zp) {
-  const uint64_t b = sp.a1 - (uint64_t)kRowRoundBytes * (uint32_t)(r + 1) + 64ull * c;
+  const uint64_t b = sp.a1 - 64ull * W * (uint32_t)(r + 1) + 64ull * c;
   const bool first = r == sp.rounds - 1;
-  // first round: b >= a0 - 1024, so the low words give the exact offset
+  // first round: b >= a0 - 64 W, so the low words give the exact offset
   const int32_t rel = first ? (int32_t)((uint32_t)b - (uint32_t)sp.a0) : 0;
   Chunk ch;
 #pragma unroll
@@ -957,6 +964,7 @@ __device__ __forceinline__ void and4(uint4& v, const uint4& m) {
   v.w &= m.w;
 }
 
+template <int W>
 __device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpan& sp, int r, uint32_t c,
                                               const CrcLane& L) {
   const bool first = r == sp.rounds - 1;
@@ -967,7 +975,7 @@ __device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpa
   // bitop3 per word); lane 15's last piece keeps the bytes before the end.
   const uint32_t h0 = (uint32_t)sp.ptr & 15u;  // bytes of the a0 piece before ptr
   const uint4 mh = lds_u32x4(kLdsRowMaskHead + 16 * h0);
-  const uint4 mt = lds_u32x4(kLdsRowMaskTail + 16 * ((r == 0 && c == 15) ? sp.kt : 0u));
+  const uint4 mt = lds_u32x4(kLdsRowMaskTail + 16 * ((r == 0 && c == W - 1) ? sp.kt : 0u));
   const uint32_t pa = (first && own) ? sp.hb >> 4 : 4u;
 #pragma unroll
   for (int j = 0; j < 4; j++) {
@@ -988,19 +996,21 @@ __device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpa
   return x;
 }
 
-// XOR over the 16 lanes of each row, in every lane of the row.
+// XOR over the W lanes of each row, in every lane of the row (DPP).
+template <int W>
 __device__ __forceinline__ uint32_t row_xor32(uint32_t v) {
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
+  if (W >= 8) v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if (W >= 16) v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
   return v;
 }
 
 // The span's CRC (Extend semantics) in every lane of its row; Lf = the lane
-// constants with lane4 = (48 + c) * 4 (shift by 64 (15 - c)).
+// constants with lane4 = (64 - W + c) * 4 (shift by 64 (W - 1 - c)).
+template <int W>
 __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, const CrcLane& Lf) {
-  uint32_t p = row_xor32(crc_lane_final(s, Lf));
+  uint32_t p = row_xor32<W>(crc_lane_final(s, Lf));
   if (wave_any(sp.kt != 0)) p = crc_unshift(sp.kt, p);
   return sp.n == 0 ? sp.init : ~p;
 }
@@ -1028,11 +1038,12 @@ __device__ __forceinline__ void row_desc_stage(const Op& op, uint32_t first, uin
 
 // Next ticket for every row that asks (take, row-uniform): lane 0 of the row
 // takes it, the row reads it.
+template <int W>
 __device__ __forceinline__ uint32_t row_ticket(bool take) {
   uint32_t t = 0;
-  if ((threadIdx.x & 15) == 0 && take)
+  if ((threadIdx.x & (W - 1)) == 0 && take)
     t = __hip_atomic_fetch_add(lds_p32(kLdsRowTicket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x & 0x30u) << 2), (int)t);
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x & (63u & ~(uint32_t)(W - 1))) << 2), (int)t);
 }
 
 // Descriptor of ticket t; t >= share (no span left) reads slot 0, a valid
@@ -1043,10 +1054,11 @@ __device__ __forceinline__ uint4 row_desc(uint32_t t, uint32_t share) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <class Op>
+template <class Op, int W>
 __device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                 const CrcTables* __restrict__ g) {
-  crc_fill_rows(lds, g);
+  static_assert(W == 4 || W == 8 || W == 16, "row width");
+  crc_fill_rows<W>(lds, g);
   row_desc_stage(op, first, count);
   __syncthreads();
   row_init_tables(op);
@@ -1054,22 +1066,22 @@ __device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, ui
   const int kind = op.init_kind();
   const CrcLane L = crc_lane();
   CrcLane Lf = L;
-  const uint32_t c = threadIdx.x & 15;
-  Lf.lane4 = (48u + c) << 2;
+  const uint32_t c = threadIdx.x & (W - 1);
+  Lf.lane4 = (64u - W + c) << 2;
   const uint32_t G = gridDim.x;
   const uint32_t share = (count - blockIdx.x + G - 1) / G;  // this workgroup's spans
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   // the row's current span (ticket t) and the next one (ticket nt, prefetched)
-  uint32_t t = row_ticket(true);
+  uint32_t t = row_ticket<W>(true);
   bool live = t < share;
   uint4 d = row_desc(t, share);
   uint32_t i = first + blockIdx.x + G * (live ? t : 0);
-  RowSpan sp = row_span(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kind);
+  RowSpan sp = row_span<W>(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kind);
   int r = sp.rounds - 1;
   const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
-  Chunk cur = row_load_chunk(sp, r, c, zp);
+  Chunk cur = row_load_chunk<W>(sp, r, c, zp);
   typename Op::Pre pcur = op.pre(i, sp.ptr, sp.n);
-  uint32_t nt = row_ticket(true);
+  uint32_t nt = row_ticket<W>(true);
   uint4 nd = row_desc(nt, share);
   uint32_t s = 0;
   for (;;) {
@@ -1077,26 +1089,26 @@ __device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, ui
     const bool go = live && (!last || nt < share);
     // set up unconditionally (rows that are not switching discard it): a
     // branch would merge the span's registers through copies every round
-    const RowSpan nsp = row_span(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kind);
+    const RowSpan nsp = row_span<W>(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kind);
     const bool sw = go && last;  // the row moves to its next span
     const RowSpan lsp = row_span_sel(sw, nsp, sp);
     const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
     const uint32_t li = sw ? first + blockIdx.x + G * nt : i;
     // unconditional: the next unit's chunk and epilogue inputs
-    const Chunk nxt = row_load_chunk(lsp, lr, c, zp);
+    const Chunk nxt = row_load_chunk<W>(lsp, lr, c, zp);
     const typename Op::Pre pnxt = op.pre(li, lsp.ptr, lsp.n);
     // rows that moved on take the ticket after (LDS only)
     uint32_t nnt = nt;
     uint4 nnd = nd;
     if (wave_any(sw)) {
-      const uint32_t tk = row_ticket(sw);
+      const uint32_t tk = row_ticket<W>(sw);
       if (sw) {
         nnt = tk;
         nnd = row_desc(tk, share);
       }
     }
-    s = row_round(s, cur, sp, r, c, L);
-    if (wave_any(live && last)) op.finish(i, row_finish(s, sp, Lf), pcur, live && last && c == 0);
+    s = row_round<W>(s, cur, sp, r, c, L);
+    if (wave_any(live && last)) op.finish(i, row_finish<W>(s, sp, Lf), pcur, live && last && c == 0);
     if (!wave_any(go)) break;
     live = go;
     i = li;

@@ -204,21 +204,45 @@ int crc_rows_force() {
 }
 
 // ---- launchers -------------------------------------------------------------
-template <class Op>
-int launch_crc_rows(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
-  int rc = ensure_lds(k_crc_rows<Op>, dev);
+// Row width (lanes per span) of the row driver; MCK_CRC_ROW_LANES=4|8|16
+// (A/B), default 16.
+int crc_row_lanes() {
+  static const int v = [] {
+    const char* e = getenv("MCK_CRC_ROW_LANES");
+    const int x = e ? atoi(e) : 16;
+    return x == 4 || x == 8 ? x : 16;
+  }();
+  return v;
+}
+
+template <class Op, int W>
+int launch_crc_rows_w(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
+  int rc = ensure_lds(k_crc_rows<Op, W>, dev);
   if (rc) return rc;
-  // persistent: one 16-wave workgroup (64 rows) per CU; each workgroup
-  // stages its share's descriptors in LDS, so a batch runs in launches of
-  // at most ncu * kRowDescCache spans
+  // persistent: one 16-wave workgroup (1024 / W rows) per CU; each
+  // workgroup stages its share's descriptors in LDS, so a batch runs in
+  // launches of at most ncu * kRowDescCache spans
   const uint32_t per = (uint32_t)ncu * kRowDescCache;
+  constexpr uint32_t rows = 1024 / W;
   for (uint32_t first = 0; first < count; first += per) {
     const uint32_t n = std::min(per, count - first);
-    const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
-    hipLaunchKernelGGL((k_crc_rows<Op>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+    const uint32_t grid = std::min<uint32_t>(ncu, (n + rows - 1) / rows);
+    hipLaunchKernelGGL((k_crc_rows<Op, W>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
     MCK_HIP(hipGetLastError());
   }
   return MCK_OK;
+}
+
+template <class Op>
+int launch_crc_rows(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
+  switch (crc_row_lanes()) {
+    case 4:
+      return launch_crc_rows_w<Op, 4>(op, count, st, dev, ncu);
+    case 8:
+      return launch_crc_rows_w<Op, 8>(op, count, st, dev, ncu);
+    default:
+      return launch_crc_rows_w<Op, 16>(op, count, st, dev, ncu);
+  }
 }
 
 template <class Op>

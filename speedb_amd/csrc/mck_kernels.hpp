@@ -219,10 +219,10 @@ __global__ __launch_bounds__(1024) void k_crc(Op op, uint32_t count) {
 }
 
 // one 16-lane row per span (crc_rows_driver): small and mid-size spans
-template <class Op>
+template <class Op, int W>
 __global__ __launch_bounds__(1024) void k_crc_rows(Op op, uint32_t first, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_rows_driver<Op>(op, first, count, lds, &g_crc_tables);
+  crc_rows_driver<Op, W>(op, first, count, lds, &g_crc_tables);
 }
 
 // uniform batches (see CrcUniform)

@@ -19,10 +19,11 @@ constexpr int kChunkBytes = 64;
 constexpr int kRoundBytes = 64 * kChunkBytes;                   // 4096
 constexpr int kGapBytes = kRoundBytes - kChunkBytes;            // 4032
 constexpr int kMaxUnshift = 64;                                 // k in [0,64)
-// Row driver (mck_crc.hpp crc_rows_driver): a 16-lane row covers one 1 KiB
-// round of a span.
-constexpr int kRowRoundBytes = 16 * kChunkBytes;                // 1024
-constexpr int kRowGapBytes = kRowRoundBytes - kChunkBytes;      // 960
+// Row driver (mck_crc.hpp crc_rows_driver): a row of W = 4, 8 or 16 lanes
+// covers one 64 W-byte round of a span; its lanes' chunks are 64 (W - 1)
+// bytes apart between rounds.
+constexpr int kRowWidths = 3;  // W = 4 << k
+constexpr int row_gap_bytes(int k) { return (4 << k) * kChunkBytes - kChunkBytes; }
 
 struct CrcTables {
   uint32_t step[4][256];          // zshift(v << 8t, 4): the 4-byte step
@@ -32,7 +33,7 @@ struct CrcTables {
   uint32_t half[8][16];           // zshift(v << 4n, 32): joins a lane's chains
   uint32_t quarter[8][16];        // zshift(v << 4n, 16)
   uint32_t unshift[kMaxUnshift][8][16];  // zshift^-1(v << 4n, k)
-  uint32_t gap_row[8][16];        // zshift(v << 4n, kRowGapBytes): row driver
+  uint32_t gap_row[kRowWidths][8][16];  // zshift(v << 4n, 64 (W - 1)): row driver
   uint32_t zero16[4];             // a zero piece: the row driver's loads before a span
 };
 
@@ -81,9 +82,11 @@ inline void build_crc_tables(CrcTables* t) {
       t->quarter[n][v] = gf_mul((uint32_t)v << (4 * n), k16);
     }
   for (int k = 0; k < 4; k++) t->zero16[k] = 0;
-  const uint32_t kr = gf_xpow8n(kRowGapBytes);
-  for (int n = 0; n < 8; n++)
-    for (int v = 0; v < 16; v++) t->gap_row[n][v] = gf_mul((uint32_t)v << (4 * n), kr);
+  for (int k = 0; k < kRowWidths; k++) {
+    const uint32_t kr = gf_xpow8n(row_gap_bytes(k));
+    for (int n = 0; n < 8; n++)
+      for (int v = 0; v < 16; v++) t->gap_row[k][n][v] = gf_mul((uint32_t)v << (4 * n), kr);
+  }
   for (int k = 0; k < kMaxUnshift; k++)
     for (int n = 0; n < 8; n++)
       for (int v = 0; v < 16; v++) {

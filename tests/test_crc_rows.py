@@ -75,3 +75,21 @@ def test_wave_driver_for_wal_subprocess(gpu):
                         "-k", "not subprocess"] + tests,
                        env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("lanes", ["4", "8"])
+def test_row_widths_subprocess(gpu, lanes):
+    """The 4- and 8-lane row variants (MCK_CRC_ROW_LANES) on the small-span
+    test and the generic ops (the default width is 16)."""
+    if os.environ.get("MCK_CRC_ROW_LANES"):
+        pytest.skip("already running a forced width")
+    env = dict(os.environ, MCK_CRC_ROWS="1", MCK_CRC_ROW_LANES=lanes)
+    tests = [os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
+    tests += [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
+        "test_crc32c_batch_ragged", "test_sst_trailer_and_verify", "test_empty_and_zero_inputs",
+        "test_large_ragged_batches_static_and_dynamic_feeds", "test_wal_record_crc_batch")]
+    tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_wal_writer.py")]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
+                        "-k", "not subprocess"] + tests,
+                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
