@@ -817,7 +817,11 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
 // force vmcnt(0) waits, see crc_load_chunk).
 // LDS: the wave driver's image plus the 960-byte row gap map, the init
 // tables and the descriptor cache, all below the step tables.
-constexpr uint32_t kLdsRowGap = kLdsLowEnd;  // 512 B, below the step tables
+constexpr uint32_t kLdsRowGap = kLdsLowEnd;  // 3 x 512 B (W = 4, 8, 16), below the step tables
+template <int W>
+constexpr uint32_t row_gap_off() {
+  return kLdsRowGap + 512u * (W == 4 ? 0 : W == 8 ? 1 : 2);
+}
 // How the row driver gets a span's CRC init (Extend's init_crc):
 //   kInitZero  -- always 0 (Value): ~init is injected from a 64-entry LDS
 //                 table of unshift(~0, hb) instead of an 8-lookup map;
@@ -827,11 +831,11 @@ constexpr uint32_t kLdsRowGap = kLdsLowEnd;  // 512 B, below the step tables
 // init_key(i) is the only load; the table lookup happens when the span is
 // set up, one iteration later, so no load depends on another in flight.
 enum RowInit : int { kInitZero = 0, kInitTyped = 1, kInitArray = 2 };
-constexpr uint32_t kLdsRowInj = kLdsRowGap + 512;     // [16][64] u32: unshift(~init_t, k)
+constexpr uint32_t kLdsRowInj = kLdsRowGap + 1536;    // [16][64] u32: unshift(~init_t, k)
 constexpr uint32_t kLdsRowInit = kLdsRowInj + 4096;   // [16] u32: init_t
 static_assert(kLdsRowInit + 64 <= kLdsStep, "row tables must fit below the step tables");
 // descriptor cache of the row feed (row_desc_stage) and its ticket
-constexpr uint32_t kRowDescCache = 1536;
+constexpr uint32_t kRowDescCache = 1528;
 constexpr uint32_t kLdsRowDesc = kLdsRowInit + 64;                   // 16 B x 1536
 constexpr uint32_t kLdsRowTicket = kLdsRowDesc + 16 * kRowDescCache;  // u32
 // byte masks of one 16-byte piece: head[h] keeps bytes >= h, tail[k] keeps
@@ -839,22 +843,21 @@ constexpr uint32_t kLdsRowTicket = kLdsRowDesc + 16 * kRowDescCache;  // u32
 constexpr uint32_t kLdsRowMaskHead = kLdsRowTicket + 64;
 constexpr uint32_t kLdsRowMaskTail = kLdsRowMaskHead + 256;
 static_assert(kLdsRowMaskTail + 256 <= kLdsStep, "row tables must fit below the step tables");
+static_assert(kLdsRowTicket + 16 <= kLdsRowMaskHead, "ticket + total");
 static_assert(offsetof(CrcTables, gap_row) - offsetof(CrcTables, unshift) == kMaxUnshift * 512, "layout");
 static_assert(sizeof(((CrcTables*)nullptr)->gap_row[0]) == 512, "one row gap map = 32 slots");
 
 __device__ __forceinline__ bool wave_any(bool p) { return __ballot(p) != 0ull; }
 
-// W: lanes per row (4, 8, 16); the gap map of that width goes to kLdsRowGap
-template <int W>
+// The wave driver's image plus the row gap maps of every width.
 __device__ __forceinline__ void crc_fill_rows(uint8_t* lds, const CrcTables* __restrict__ g) {
-  constexpr int wk = W == 4 ? 0 : W == 8 ? 1 : 2;
   CrcFill f;
   crc_fill_load<true>(f, g);
   const int t = threadIdx.x;
-  const uint4* rg = reinterpret_cast<const uint4*>(&g->gap_row[wk][0][0]);
-  const uint4 x = rg[t < 32 ? t : 0];
+  const uint4* rg = reinterpret_cast<const uint4*>(&g->gap_row[0][0][0]);
+  const uint4 x = rg[t < 96 ? t : 0];
   crc_fill_store<true>(f, lds);
-  if (t < 32) reinterpret_cast<uint4*>(lds + kLdsRowGap)[t] = x;
+  if (t < 96) reinterpret_cast<uint4*>(lds + kLdsRowGap)[t] = x;
 }
 
 struct RowSpan {
@@ -987,7 +990,7 @@ __device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpa
   }
   and4(ch.v[3], mt);
   uint32_t gap = 0;
-  if (wave_any(!first)) gap = crc_nibmap(kLdsRowGap, s);
+  if (wave_any(!first)) gap = crc_nibmap(row_gap_off<W>(), s);
   uint32_t x = first ? (own ? sp.inj : 0u) : gap;
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&ch.v[0]);
   x ^= w[0];
@@ -1023,17 +1026,31 @@ __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, co
 // splits batches whose share exceeds kRowDescCache into several launches.
 
 
+// Also sums the share's span bytes into the u64 at kLdsRowTotal (zeroed
+// here; valid after the next __syncthreads + the atomics).
+constexpr uint32_t kLdsRowTotal = kLdsRowTicket + 8;  // u64
 template <class Op>
-__device__ __forceinline__ void row_desc_stage(const Op& op, uint32_t first, uint32_t count) {
+__device__ __forceinline__ void row_desc_stage(const Op& op, uint32_t first, uint32_t count, bool total) {
   const uint32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t n = (count - b + G - 1) / G;
+  uint64_t sum = 0;
   for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
     const uint32_t i = first + b + G * t;
     const uint64_t off = op.off(i);
-    const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)op.len(i), op.init_key(i)};
+    const uint32_t len = (uint32_t)op.len(i);
+    sum += len;
+    const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, op.init_key(i)};
     *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsRowDesc + 16 * t)) = d;
   }
   if (threadIdx.x == 0) *lds_p32(kLdsRowTicket) = 0;
+  if (total) {
+    // wave sum, then one LDS atomic per wave (after a barrier zeroes it)
+    for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 64);
+    if (threadIdx.x == 0) *lds_p64(kLdsRowTotal) = 0;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0)
+      __hip_atomic_fetch_add(lds_p64(kLdsRowTotal), sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
 }
 
 // Next ticket for every row that asks (take, row-uniform): lane 0 of the row
@@ -1054,15 +1071,22 @@ __device__ __forceinline__ uint4 row_desc(uint32_t t, uint32_t share) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-template <class Op, int W>
-__device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
-                                                const CrcTables* __restrict__ g) {
-  static_assert(W == 4 || W == 8 || W == 16, "row width");
-  crc_fill_rows<W>(lds, g);
-  row_desc_stage(op, first, count);
+// LDS prologue of the row (and auto) kernels: tables, descriptors, init
+// tables; ends with a barrier.
+template <class Op>
+__device__ __forceinline__ void crc_rows_prologue(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
+                                                  const CrcTables* __restrict__ g, bool total) {
+  crc_fill_rows(lds, g);
+  row_desc_stage(op, first, count, total);
   __syncthreads();
   row_init_tables(op);
   __syncthreads();
+}
+
+template <class Op, int W>
+__device__ __forceinline__ void crc_rows_loop(const Op& op, uint32_t first, uint32_t count,
+                                              const CrcTables* __restrict__ g) {
+  static_assert(W == 4 || W == 8 || W == 16, "row width");
   const int kind = op.init_kind();
   const CrcLane L = crc_lane();
   CrcLane Lf = L;
@@ -1118,6 +1142,57 @@ __device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, ui
     r = lr;
     cur = nxt;
     pcur = pnxt;
+  }
+}
+
+template <class Op, int W>
+__device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
+                                                const CrcTables* __restrict__ g) {
+  crc_rows_prologue(op, first, count, lds, g, false);
+  crc_rows_loop<Op, W>(op, first, count, g);
+}
+
+// The wave driver (crc_drive) fed from the row descriptor cache: one
+// ticket per wave.
+template <class Op>
+struct FeedRowCache {
+  uint32_t first_span, share;
+  int kind;
+  __device__ bool take(uint32_t* span, SpanDesc* d) {
+    const uint32_t t = __builtin_amdgcn_readfirstlane(lds_ticket(lds_p32(kLdsRowTicket)));
+    if (t >= share) return false;
+    *span = first_span + blockIdx.x + gridDim.x * t;
+    const uint4 v = row_desc(t, share);
+    d->off = ((uint64_t)v.y << 32) | v.x;
+    d->len = v.z;
+    d->init = kind == kInitArray ? v.w : *lds_p32(kLdsRowInit + 4 * (kind == kInitTyped ? (v.w & 15u) : 0u));
+    return true;
+  }
+  __device__ bool first(const Op&, const CrcLane&, uint32_t* span, SpanDesc* d) { return take(span, d); }
+  __device__ bool next(const Op&, const CrcLane&, uint32_t* span, SpanDesc* d) { return take(span, d); }
+};
+
+// Ragged batches, driver chosen per workgroup from its share's mean span
+// length (the host cannot see device-resident lengths): 8-lane rows for
+// short spans, 16-lane rows for spans up to a few KiB, the wave driver
+// above that.  force: 0 = by length, 1 = wave, 2 = rows16, 3 = rows8.
+constexpr uint32_t kAutoRows8Max = 640;    // mean span bytes
+constexpr uint32_t kAutoRows16Max = 2560;
+template <class Op, bool T>
+__device__ __forceinline__ void crc_auto_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
+                                                const CrcTables* __restrict__ g, int force) {
+  crc_rows_prologue(op, first, count, lds, g, true);
+  const uint32_t G = gridDim.x;
+  const uint32_t share = (count - blockIdx.x + G - 1) / G;
+  const uint64_t mean = *lds_p64(kLdsRowTotal) / (share ? share : 1);
+  const int mode = force ? force : mean <= kAutoRows8Max ? 3 : mean <= kAutoRows16Max ? 2 : 1;
+  if (mode == 3) {
+    crc_rows_loop<Op, 8>(op, first, count, g);
+  } else if (mode == 2) {
+    crc_rows_loop<Op, 16>(op, first, count, g);
+  } else {
+    FeedRowCache<Op> f{first, share, op.init_kind()};
+    crc_drive<Op, FeedRowCache<Op>, T>(op, f, crc_lane());
   }
 }
 

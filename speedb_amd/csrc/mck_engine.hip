@@ -180,25 +180,24 @@ struct CrcRowT<OpWalFragCrc> {
   static constexpr bool value = false;
 };
 
-// Ragged-batch driver per op: the row driver (one 16-lane row per span,
-// crc_rows_driver) where the spans are WAL-sized, the wave driver otherwise.
-// MCK_CRC_ROWS=0|1 forces one for every ragged batch (A/B measurements).
-template <class Op>
-struct CrcRowsDefault {
-  static constexpr bool value = false;
-};
-template <>
-struct CrcRowsDefault<OpWalFragCrc> {
-  static constexpr bool value = true;
-};
-template <>
-struct CrcRowsDefault<OpCrcWal> {
-  static constexpr bool value = true;
-};
+// Ragged batches run on k_crc_auto, which picks the driver per workgroup
+// from the mean length of its share (crc_auto_driver).  A/B switches, read
+// once per process: MCK_CRC_AUTO=wave|rows16|rows8 forces one driver inside
+// it; MCK_CRC_ROWS=0 restores the standalone wave-driver kernel (k_crc,
+// static feed for big batches), MCK_CRC_ROWS=1 the standalone row kernel
+// (width MCK_CRC_ROW_LANES).
 int crc_rows_force() {
   static const int v = [] {
     const char* e = getenv("MCK_CRC_ROWS");
     return !e ? -1 : atoi(e) ? 1 : 0;
+  }();
+  return v;
+}
+int crc_auto_force() {
+  static const int v = [] {
+    const char* e = getenv("MCK_CRC_AUTO");
+    if (!e) return 0;
+    return !strcmp(e, "wave") ? 1 : !strcmp(e, "rows16") ? 2 : !strcmp(e, "rows8") ? 3 : 0;
   }();
   return v;
 }
@@ -246,13 +245,30 @@ int launch_crc_rows(const Op& op, uint32_t count, hipStream_t st, int dev, int n
 }
 
 template <class Op>
+int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
+  constexpr bool T = CrcRowT<Op>::value;
+  int rc = ensure_lds(k_crc_auto<Op, T>, dev);
+  if (rc) return rc;
+  // one 16-wave workgroup per CU; each stages its share's descriptors in LDS
+  const uint32_t per = (uint32_t)ncu * kRowDescCache;
+  for (uint32_t first = 0; first < count; first += per) {
+    const uint32_t n = std::min(per, count - first);
+    const uint32_t grid = std::min<uint32_t>(ncu, (n + 15) / 16);
+    hipLaunchKernelGGL((k_crc_auto<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n, crc_auto_force());
+    MCK_HIP(hipGetLastError());
+  }
+  return MCK_OK;
+}
+
+template <class Op>
 int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
   if (!count) return MCK_OK;
   int dev, ncu;
   int rc = current_device(&dev, &ncu);
   if (rc) return rc;
   const int force = crc_rows_force();
-  if (force == 1 || (force < 0 && CrcRowsDefault<Op>::value)) return launch_crc_rows(op, count, st, dev, ncu);
+  if (force == 1) return launch_crc_rows(op, count, st, dev, ncu);
+  if (force < 0) return launch_crc_auto(op, count, st, dev, ncu);
   // persistent: one 16-wave workgroup per CU (160 KiB of LDS each), with
   // row-transposed loads (CrcRowT)
   constexpr bool T = CrcRowT<Op>::value;

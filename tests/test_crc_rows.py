@@ -1,8 +1,11 @@
-"""The CRC row driver (one 16-lane row per span, four spans per wave;
-mck_crc.hpp crc_rows_driver) against the oracle: it is the default for WAL
-records and WAL-writer fragments, and MCK_CRC_ROWS=1 routes every ragged
-CRC batch through it -- the generic-op parity tests are re-run that way in a
-child process (the switch is read once per process)."""
+"""The ragged-batch CRC drivers against the oracle.  By default a ragged
+batch runs on k_crc_auto, which picks per workgroup (from its share's mean
+span length) the row driver with 8- or 16-lane rows (one row per span,
+mck_crc.hpp crc_rows_loop) or the wave driver (crc_drive).  Every driver is
+also forced in a child process over the generic-op parity tests (the A/B
+switches are read once per process): MCK_CRC_AUTO=wave|rows16|rows8 inside
+the auto kernel, MCK_CRC_ROWS=1 (+ MCK_CRC_ROW_LANES) for the standalone row
+kernel, MCK_CRC_ROWS=0 for the standalone wave kernel with its static feed."""
 import os
 import random
 import subprocess
@@ -51,6 +54,8 @@ def test_wal_record_crc_small_ragged_many(gpu, oracle):
 def test_generic_ops_through_rows_subprocess(gpu):
     """CRC value/extend/mask, SST trailer + verify (context checksums,
     corruption), blob records and WAL paths with MCK_CRC_ROWS=1."""
+    if os.environ.get("MCK_CRC_ROWS") or os.environ.get("MCK_CRC_AUTO"):
+        pytest.skip("already running a forced driver")
     env = dict(os.environ, MCK_CRC_ROWS="1")
     tests = [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
         "test_crc32c_batch_ragged", "test_crc32c_known_answers_on_device", "test_scalar_shims",
@@ -66,8 +71,10 @@ def test_generic_ops_through_rows_subprocess(gpu):
 
 
 def test_wave_driver_for_wal_subprocess(gpu):
-    """And the other way round: MCK_CRC_ROWS=0 keeps WAL records and the WAL
-    writer on the wave driver (both stay covered)."""
+    """And the standalone wave kernel (MCK_CRC_ROWS=0) on the WAL records and
+    the WAL writer."""
+    if os.environ.get("MCK_CRC_ROWS") or os.environ.get("MCK_CRC_AUTO"):
+        pytest.skip("already running a forced driver")
     env = dict(os.environ, MCK_CRC_ROWS="0")
     tests = [os.path.join(HERE, "test_wal_writer.py"),
              os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
@@ -79,9 +86,9 @@ def test_wave_driver_for_wal_subprocess(gpu):
 
 @pytest.mark.parametrize("lanes", ["4", "8"])
 def test_row_widths_subprocess(gpu, lanes):
-    """The 4- and 8-lane row variants (MCK_CRC_ROW_LANES) on the small-span
-    test and the generic ops (the default width is 16)."""
-    if os.environ.get("MCK_CRC_ROW_LANES"):
+    """The standalone row kernel's 4- and 8-lane variants (MCK_CRC_ROW_LANES)
+    on the small-span test and the generic ops."""
+    if os.environ.get("MCK_CRC_ROW_LANES") or os.environ.get("MCK_CRC_AUTO"):
         pytest.skip("already running a forced width")
     env = dict(os.environ, MCK_CRC_ROWS="1", MCK_CRC_ROW_LANES=lanes)
     tests = [os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
@@ -89,6 +96,26 @@ def test_row_widths_subprocess(gpu, lanes):
         "test_crc32c_batch_ragged", "test_sst_trailer_and_verify", "test_empty_and_zero_inputs",
         "test_large_ragged_batches_static_and_dynamic_feeds", "test_wal_record_crc_batch")]
     tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_wal_writer.py")]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
+                        "-k", "not subprocess"] + tests,
+                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("mode", ["wave", "rows16", "rows8"])
+def test_auto_kernel_forced_drivers_subprocess(gpu, mode):
+    """k_crc_auto with each driver forced (its per-workgroup choice is by
+    mean length, so a parity test of mixed lengths may exercise only one)."""
+    if os.environ.get("MCK_CRC_AUTO") or os.environ.get("MCK_CRC_ROWS"):
+        pytest.skip("already running a forced driver")
+    env = dict(os.environ, MCK_CRC_AUTO=mode)
+    tests = [os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
+    tests += [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
+        "test_crc32c_batch_ragged", "test_sst_trailer_and_verify", "test_empty_and_zero_inputs",
+        "test_large_ragged_batches_static_and_dynamic_feeds", "test_wal_record_crc_batch",
+        "test_crc32c_known_answers_on_device", "test_builtin_checksum_batch", "test_sst_verify_large_static_feed")]
+    tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_wal_writer.py"),
+              os.path.join(HERE, "test_sst_file.py")]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
                         "-k", "not subprocess"] + tests,
                        env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
