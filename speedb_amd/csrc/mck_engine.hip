@@ -249,8 +249,12 @@ int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int n
   constexpr bool T = CrcRowT<Op>::value;
   int rc = ensure_lds(k_crc_auto<Op, T>, dev);
   if (rc) return rc;
-  // one 16-wave workgroup per CU; each stages its share's descriptors in LDS
-  const uint32_t per = (uint32_t)ncu * kRowDescCache;
+  // one 16-wave workgroup per CU; each stages its share's descriptors in
+  // LDS, so a batch runs in launches of at most ncu * kRowDescCache spans,
+  // split evenly (no short last launch)
+  const uint32_t cap = (uint32_t)ncu * kRowDescCache;
+  const uint32_t nl = (count + cap - 1) / cap;
+  const uint32_t per = (uint32_t)(((uint64_t)count + nl - 1) / nl);
   for (uint32_t first = 0; first < count; first += per) {
     const uint32_t n = std::min(per, count - first);
     const uint32_t grid = std::min<uint32_t>(ncu, (n + 15) / 16);
