@@ -95,6 +95,8 @@ def parse():
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
     p.add_argument("--sst-bytes", type=int, default=1 << 30, help="per SST image (sst); 2 images")
+    p.add_argument("--sst-types", choices=["both", "crc32c", "xxh3"], default="both",
+                   help="sst: verify both images (configs[2]) or one (per-kernel measurement)")
     p.add_argument("--wal-blocks", type=int, default=10_000_000,
                    help="32 KiB blocks of the WHOLE job, partitioned over the ranks (wal, configs[3])")
     p.add_argument("--hbm-budget-gib", type=float, default=64.0,
@@ -260,26 +262,30 @@ def make_workload(args, dev, rank, world):
             return None
         w.check = check
     elif args.workload == "sst":
-        imgs = [W.SstImage(args.sst_bytes, t, dev, seed=100 + 2 * rank + k)
-                for k, t in enumerate((S.ChecksumType.kCRC32c, S.ChecksumType.kXXH3))]
+        types = {"both": (S.ChecksumType.kCRC32c, S.ChecksumType.kXXH3), "crc32c": (S.ChecksumType.kCRC32c,),
+                 "xxh3": (S.ChecksumType.kXXH3,)}[args.sst_types]
+        imgs = [W.SstImage(args.sst_bytes, t, dev, seed=100 + 2 * rank + (0 if t == S.ChecksumType.kCRC32c else 1))
+                for t in types]
         res = {}
 
         def step():
             for im in imgs:
                 res[im.checksum_type] = im.verify(stream=stream)
         w.step = step
-        w.launches = 2
-        w.kernel = "mck::k_crc<mck::OpCrcBlock<2>, true> + mck::k_xxh3_wave<mck::OpX3Block<2> >"
+        w.launches = len(imgs)
+        w.kernel = " + ".join({int(S.ChecksumType.kCRC32c): "mck::k_crc_auto<mck::OpCrcBlock<2>, true>",
+                               int(S.ChecksumType.kXXH3): "mck::k_xxh3_wave<mck::OpX3Block<2> >"}[int(t)]
+                              for t in types)
         w.span_bytes = sum(im.payload_bytes + im.count for im in imgs)  # payload + type byte
         # per launch: span bytes + 4 B stored + 8 B offset + 4 B length + 8 B
         # file offset in, 1 B flag + 4 + 4 B out
         w.alg_bytes = sum(im.payload_bytes + im.count * (1 + 4 + 8 + 4 + 8 + 1 + 4 + 4)
-                          for im in imgs) / 2
+                          for im in imgs) / len(imgs)
         w.desc = ("VerifyBlockChecksum over a compaction-shaped run of 4/16/64 KiB (+0..255 B) SST "
                   f"blocks, {args.sst_bytes >> 20} MiB per image, format_version 6 context "
                   "checksums; one kCRC32c + one kXXH3 image per step (BASELINE.json configs[2])")
         w.cfg = {"blocks_per_gpu": sum(im.count for im in imgs), "image_bytes": args.sst_bytes,
-                 "checksum_types": ["kCRC32c", "kXXH3"]}
+                 "checksum_types": [S.ChecksumType(int(t)).name for t in types]}
 
         def check():
             # every block the write-side kernel sealed verifies, and injected
@@ -384,13 +390,13 @@ def make_workload(args, dev, rank, world):
         if args.workload == "walrec":
             types = torch.from_numpy(rng.choice([1, 2, 3, 4], size=count).astype(np.uint8)).to(dev)
             w.step = lambda: S.wal_record_crc_batch(sp, types, 7, out=out, stream=stream)
-            w.kernel = "mck::k_crc_rows<mck::OpCrcWal>"
+            w.kernel = "mck::k_crc_auto<mck::OpCrcWal, true>"
             w.desc = (f"WAL record CRCs (EmitPhysicalRecord, db/log_writer.cc:263-311): {count} records of "
                       f"{args.span_min}-{args.span_max} B per GPU at any byte offset, mck_wal_record_crc_batch")
         else:
             w.step = lambda: S.crc32c_batch(sp, out=out, stream=stream)
-            w.kernel = ("mck::k_crc_rows<mck::OpCrcValue>" if os.environ.get("MCK_CRC_ROWS") == "1"
-                        else "mck::k_crc<mck::OpCrcValue, true>")
+            w.kernel = {"1": "mck::k_crc_rows<mck::OpCrcValue>", "0": "mck::k_crc<mck::OpCrcValue, true>"}.get(
+                os.environ.get("MCK_CRC_ROWS", ""), "mck::k_crc_auto<mck::OpCrcValue, true>")
             w.desc = (f"crc32c_batch over {count} ragged spans of {args.span_min}-{args.span_max} B per GPU "
                       "(explicit offsets/lengths)")
         w.span_bytes = int(lens.sum())
@@ -432,7 +438,7 @@ def make_workload(args, dev, rank, world):
         # the CRC and copy kernels overlap (piecewise, two streams: the
         # engine's mck_wal_write_batch), so the unit timed is the whole step
         w.launches = 1
-        w.kernel = "mck::k_crc<mck::OpWalFragCrc, false> + mck::k_wal_copy<false> (overlapped step)"
+        w.kernel = "mck::k_crc_auto<mck::OpWalFragCrc, false> + mck::k_wal_copy<false> (overlapped step)"
         w.span_bytes = int(lens.sum())
         # per step: CRC reads the payload + 24 B descriptor + 4 B out per
         # fragment; the writer reads the payload + descriptor + crc and
@@ -466,7 +472,7 @@ def make_workload(args, dev, rank, world):
         def step():
             S.blob.record_batch(False, img, offs, lens, status=status, stream=stream)
         w.step = step
-        w.kernel = "mck::k_crc<mck::OpBlobRecord<false>, true>"
+        w.kernel = "mck::k_crc_auto<mck::OpBlobRecord<false>, true>"
         w.span_bytes = n * rec
         w.alg_bytes = n * (rec + 8 + 4 + 1)
         w.desc = (f"blob file verify: {n} records per GPU ({kb} B key, {vb} B value), header CRC + blob CRC "
