@@ -1009,6 +1009,20 @@ __device__ __forceinline__ uint32_t row_xor32(uint32_t v) {
   return v;
 }
 
+// zshift(s, 64*(63-lane)) with the per-lane tables, column lane4 = lane * 4.
+__device__ __forceinline__ uint32_t crc_lane_final4(uint32_t s, uint32_t lane4) {
+  uint32_t x[8];
+#pragma unroll
+  for (int n = 0; n < 8; n++) x[n] = lds_u32(kLdsFinal + n * 4096 + ((((s >> (4 * n)) & 15u) << 8) | lane4));
+  return xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], x[5]), x[6] ^ x[7]);
+}
+template <int W>
+__device__ __forceinline__ uint32_t row_finish4(uint32_t s, const RowSpan& sp, uint32_t lf4) {
+  uint32_t p = row_xor32<W>(crc_lane_final4(s, lf4));
+  if (wave_any(sp.kt != 0)) p = crc_unshift(sp.kt, p);
+  return sp.n == 0 ? sp.init : ~p;
+}
+
 // The span's CRC (Extend semantics) in every lane of its row; Lf = the lane
 // constants with lane4 = (64 - W + c) * 4 (shift by 64 (W - 1 - c)).
 template <int W>

@@ -22,6 +22,7 @@
 namespace mck {
 
 __device__ CrcTables g_crc_tables;
+__device__ uint8_t g_wal_sink[kWalSinkBytes];
 
 namespace {
 
@@ -716,6 +717,16 @@ static int launch_wal_copy(const uint8_t* src, const WalFrag* f, uint32_t n, uin
   return MCK_OK;
 }
 
+// One-pass writer (k_wal_write_rows) unless MCK_WAL_FUSED=0 (A/B: the CRC
+// kernel + k_wal_copy in overlapped pieces).
+static bool wal_fused() {
+  static const bool v = [] {
+    const char* e = getenv("MCK_WAL_FUSED");
+    return !e || strcmp(e, "0") != 0;
+  }();
+  return v;
+}
+
 // pieces of at least 16 fragments per CU (one CRC grid's worth of spans)
 static uint32_t wal_pieces_for(uint32_t nfrags, int ncu) {
   uint32_t pieces = wal_pieces();
@@ -726,7 +737,7 @@ static uint32_t wal_pieces_for(uint32_t nfrags, int ncu) {
 int mck_wal_write_pieces(uint32_t nfrags) {
   int ncu;
   if (int rc = current_device(nullptr, &ncu)) return rc;
-  return (int)wal_pieces_for(nfrags, ncu);
+  return wal_fused() ? 0 : (int)wal_pieces_for(nfrags, ncu);
 }
 
 int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t nfrags, uint32_t log_number,
@@ -749,6 +760,22 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   const WalTypeCrcs tc = wal_type_crcs(log_number);
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
+  if (wal_fused()) {
+    // one pass: CRC + log stream in k_wal_write_rows, in launches of at most
+    // ncu * kRowDescCache fragments (its LDS descriptor / dst_off tables)
+    if (int rc = ensure_lds(k_wal_write_rows<16>, dev)) return rc;
+    const uint32_t cap = (uint32_t)ncu * kRowDescCache;
+    const uint32_t nl = (nfrags + cap - 1) / cap;
+    const uint32_t per = (uint32_t)(((uint64_t)nfrags + nl - 1) / nl);
+    const OpWalWrite op{s8, f, tc, log_number, crc_scratch, o8};
+    for (uint32_t first = 0; first < nfrags; first += per) {
+      const uint32_t n = std::min(per, nfrags - first);
+      const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
+      hipLaunchKernelGGL(k_wal_write_rows<16>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+      MCK_HIP(hipGetLastError());
+    }
+    return MCK_OK;
+  }
   const uint32_t pieces = wal_pieces_for(nfrags, ncu);
   if (pieces == 1) {
     if (int rc = launch_crc(OpWalFragCrc{s8, f, tc, crc_scratch}, nfrags, st)) return rc;

@@ -12,6 +12,9 @@
 namespace mck {
 
 extern __device__ CrcTables g_crc_tables;
+// scratch that the one-pass WAL writer's idle lanes store to (never read)
+constexpr uint32_t kWalSinkBytes = 64 * 16 + 64;
+extern __device__ uint8_t g_wal_sink[kWalSinkBytes];
 
 constexpr uint32_t kRandomPrime = 0x6b9083d9u;  // table/format.cc:573
 
@@ -503,6 +506,206 @@ struct OpWalFragCrc {
     if (writer) out[i] = crc_mask(crc);
   }
 };
+
+// ===================== one-pass WAL writer ==================================
+// mck_wal_write_batch in ONE kernel: the row driver (crc_rows_loop's
+// structure, 16-lane rows) CRCs each fragment and, in the same iteration,
+// writes what log::Writer appends for it (db/log_writer.cc:263-311):
+//   * the payload's 16-byte-aligned OUTPUT pieces of the round: lane c takes
+//     the four pieces whose source starts x = S + e + 16 j lie in its source
+//     chunk [S, S + 64) (e = -delta mod 16, delta = output - source), loads
+//     them dword-aligned (16 B + the next dword, re-read from L1/L2: the CRC
+//     loads of the same bytes were just issued), realigns with v_alignbyte
+//     and stores them non-temporal;
+//   * at the span's last round: the < 16 payload bytes before the first and
+//     after the last full output piece, byte by byte, and the trailer padding
+//     + header ([masked CRC][len][type][log number]) -- the CRC is known then.
+// Stores with nothing to write go to a per-device sink, so every VMEM
+// instruction issues in every iteration (static vmcnt accounting, as for the
+// loads).  The payload is read from HBM once.
+// LDS: the row image; fragments' dst_off at kLdsWalAux, over the un-shift
+// tables k >= 16, which this kernel never reads (typed init: no per-span
+// un-shift; the tail un-shift is < 16).
+constexpr uint32_t kLdsWalAux = kLdsUnshift + 16 * 512;
+static_assert(kLdsWalAux + 8 * kRowDescCache <= kCrcLdsBytes, "WAL aux table must fit");
+
+struct OpWalWrite {
+  const uint8_t* src;
+  const WalFrag* frags;
+  WalTypeCrcs tc;
+  uint32_t log_number;
+  uint32_t* crcs;  // masked fragment CRCs (the API's crc_scratch)
+  uint8_t* out;
+  __device__ const uint8_t* base() const { return src; }
+  __device__ uint64_t off(uint32_t i) const { return frags[i].src_off; }
+  __device__ uint64_t len(uint32_t i) const { return frags[i].length; }
+  static constexpr bool kTypedInit = true;
+  __device__ int init_kind() const { return kInitTyped; }
+  // key = type | pad << 8 (init_kind kInitTyped uses key & 15)
+  __device__ uint32_t init_key(uint32_t i) const {
+    return (uint32_t)ldg_u8(&frags[i].type, 0) | ((uint32_t)ldg_u8(&frags[i].pad, 0) << 8);
+  }
+  __device__ uint32_t typed_init(uint32_t t) const { return tc.v[t & 15]; }
+};
+
+__device__ __forceinline__ uint32_t wal_hdr_byte(uint32_t h, uint32_t crc, uint32_t len, uint32_t type,
+                                                 uint32_t log_number) {
+  // h < header size: [crc LE32][len LE16][type][log number LE32]
+  return h < 4 ? (crc >> (8 * h)) & 0xFF : h < 6 ? (len >> (8 * (h - 4))) & 0xFF : h == 6 ? type
+                                                                                    : (log_number >> (8 * (h - 7))) & 0xFF;
+}
+
+typedef __attribute__((address_space(1))) uint8_t gbl_st_u8_t;
+typedef __attribute__((address_space(1))) uint32_t gbl_st_u32_t;
+typedef __attribute__((address_space(1))) span_u32x4 gbl_st_u32x4_t;
+__device__ __forceinline__ void st_u8(uint64_t a, uint32_t v) { *reinterpret_cast<gbl_st_u8_t*>(a) = (uint8_t)v; }
+__device__ __forceinline__ void st_u32(uint64_t a, uint32_t v) { *reinterpret_cast<gbl_st_u32_t*>(a) = v; }
+__device__ __forceinline__ void st_nt16(uint64_t a, uint4 o) {
+  span_u32x4 q = {o.x, o.y, o.z, o.w};
+  __builtin_nontemporal_store(q, reinterpret_cast<gbl_st_u32x4_t*>(a));
+}
+
+// W = 16: a row's 16 lanes also cover the <= 15 head / tail payload bytes.
+template <int W>
+__device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
+                                               const CrcTables* __restrict__ g) {
+  static_assert(W == 16, "the head/tail byte copies assume 16-lane rows");
+  crc_rows_prologue(op, first, count, lds, g, false);
+  {  // fragments' dst_off, staged like the descriptors (row_desc_stage order)
+    const uint32_t G = gridDim.x, b = blockIdx.x;
+    const uint32_t n = (count - b + G - 1) / G;
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
+      *lds_p64(kLdsWalAux + 8 * t) = op.frags[first + b + G * t].dst_off;
+  }
+  __syncthreads();
+  const CrcLane L = crc_lane();
+  const uint32_t c = threadIdx.x & (W - 1);
+  const uint32_t lf4 = (64u - W + c) << 2;  // lane-final table column
+  const uint32_t G = gridDim.x;
+  const uint32_t share = (count - blockIdx.x + G - 1) / G;
+  const uint64_t base = reinterpret_cast<uint64_t>(op.src);
+  const uint64_t obase = reinterpret_cast<uint64_t>(op.out);
+  // per-lane sink slots (16 B each), never read
+  const uint64_t sink = reinterpret_cast<uint64_t>(&g_wal_sink[0]) + 16ull * (threadIdx.x & 63);
+  const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
+  uint32_t t = row_ticket<W>(true);
+  bool live = t < share;
+  uint4 d = row_desc(t, share);
+  uint64_t dst = *lds_p64(kLdsWalAux + 8 * (t < share ? t : 0));
+  uint32_t i = first + blockIdx.x + G * (live ? t : 0);
+  RowSpan sp = row_span<W>(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kInitTyped);
+  uint32_t key = d.w;
+  int r = sp.rounds - 1;
+  Chunk cur = row_load_chunk<W>(sp, r, c, zp);
+  uint32_t nt = row_ticket<W>(true);
+  uint4 nd = row_desc(nt, share);
+  uint64_t ndst = *lds_p64(kLdsWalAux + 8 * (nt < share ? nt : 0));
+  uint32_t s = 0;
+  for (;;) {
+    const bool last = r == 0;
+    const bool fin = live && last;
+
+    // ---- the output of this (span, round), before the next round's
+    // prefetch is issued: waiting for these loads (L1/L2 hits: the CRC loads
+    // of the same bytes came in one iteration ago) then waits for them alone,
+    // and their registers are dead before the prefetch and the CRC round ----
+    const uint32_t type = key & 0xFF, pad = (key >> 8) & 0xFF;
+    const uint32_t hs = ((type >= 5 && type <= 8) || type == 11) ? 11u : 7u;
+    const uint64_t P = obase + dst + hs;             // payload in the output
+    const uint64_t ps = sp.ptr, pe = sp.ptr + sp.n;  // payload in the source
+    const uint64_t delta = P - ps;                   // (mod 2^64)
+    const uint32_t e = (uint32_t)(0ull - delta) & 15u;
+    const uint32_t be = e & 3u;
+    const uint64_t S = sp.a1 - 64ull * W * (uint32_t)(r + 1) + 64ull * c;
+    uint4 v[4];
+    uint32_t w5[4];
+    bool ok[4];
+    const uint64_t x0 = S + e;  // source start of the lane's first output-aligned piece
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      const uint64_t x = x0 + 16ull * j;
+      ok[j] = live && x >= ps && x + 16 <= pe;
+      const uint64_t f = ok[j] ? (x & ~3ull) : zp;
+      v[j] = span_load16<false>(f);
+      // the fifth dword, unless the piece is dword-aligned (then it could
+      // lie past the payload's last dword: re-read the fourth)
+      w5[j] = *reinterpret_cast<gbl_u32_t*>(ok[j] && be ? f + 16 : f + 12);
+    }
+    const uint64_t h16 = (P + 15) & ~15ull;                   // first full output piece
+    const uint64_t t16 = (P + sp.n) & ~15ull;                 // end of the last full piece
+    const uint64_t hb_end = h16 < P + sp.n ? h16 : P + sp.n;  // head bytes [P, hb_end)
+    const uint64_t tb_beg = t16 > hb_end ? t16 : hb_end;      // tail bytes [tb_beg, P + n)
+    const uint64_t oh = P + c, ot = tb_beg + c;
+    const bool okh = fin && oh < hb_end, okt = fin && ot < P + sp.n;
+    const uint32_t bh = *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : zp);
+    const uint32_t bt = *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : zp);
+
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+      uint4 o;
+      o.x = __builtin_amdgcn_alignbyte(v[j].y, v[j].x, be);
+      o.y = __builtin_amdgcn_alignbyte(v[j].z, v[j].y, be);
+      o.z = __builtin_amdgcn_alignbyte(v[j].w, v[j].z, be);
+      o.w = __builtin_amdgcn_alignbyte(w5[j], v[j].w, be);
+      st_nt16(ok[j] ? x0 + 16ull * j + delta : sink, o);
+    }
+    st_u8(okh ? oh : sink, bh);
+    st_u8(okt ? ot : sink + 1, bt);
+
+    // ---- next unit (as crc_rows_loop) ----
+    const bool go = live && (!last || nt < share);
+    const RowSpan nsp = row_span<W>(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kInitTyped);
+    const bool sw = go && last;
+    const RowSpan lsp = row_span_sel(sw, nsp, sp);
+    const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
+    const uint32_t li = sw ? first + blockIdx.x + G * nt : i;
+    const Chunk nxt = row_load_chunk<W>(lsp, lr, c, zp);
+
+    s = row_round<W>(s, cur, sp, r, c, L);
+    uint32_t crc = 0;
+    if (wave_any(fin)) crc = crc_mask(row_finish4<W>(s, sp, lf4));
+    st_u32(fin && c == 0 ? reinterpret_cast<uint64_t>(op.crcs + i) : sink + 4, crc);
+    // trailer padding + header: bytes c and c + 16 of [dst - pad, dst + hs)
+    const uint64_t hstart = obase + dst - pad;
+#pragma unroll
+    for (int m = 0; m < 2; m++) {
+      const uint32_t b = c + 16u * m;
+      const bool okb = fin && b < pad + hs;
+      const uint32_t val = b < pad ? 0u : wal_hdr_byte(b - pad, crc, sp.n, type, op.log_number);
+      st_u8(okb ? hstart + b : sink + 2 + m, val);
+    }
+
+    // ---- advance ----
+    uint32_t nnt = nt;
+    uint4 nnd = nd;
+    uint64_t nndst = ndst;
+    if (wave_any(sw)) {
+      const uint32_t tk = row_ticket<W>(sw);
+      if (sw) {
+        nnt = tk;
+        nnd = row_desc(tk, share);
+        nndst = *lds_p64(kLdsWalAux + 8 * (tk < share ? tk : 0));
+      }
+    }
+    if (!wave_any(go)) break;
+    key = sw ? nd.w : key;
+    dst = sw ? ndst : dst;
+    live = go;
+    i = li;
+    nt = nnt;
+    nd = nnd;
+    ndst = nndst;
+    sp = lsp;
+    r = lr;
+    cur = nxt;
+  }
+}
+
+template <int W>
+__global__ __launch_bounds__(1024) void k_wal_write_rows(OpWalWrite op, uint32_t first, uint32_t count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  wal_write_rows<W>(op, first, count, lds, &g_crc_tables);
+}
 
 // The physical record image: [pad zeros][crc LE32][len LE16][type]
 // [log number LE32 if recyclable][payload].  One wave per fragment; the

@@ -96,7 +96,9 @@ def test_wal_write_batch_pieces_bit_exact(gpu, oracle, recycle):
     dev = torch.frombuffer(bytearray(src + bytes(64)), dtype=torch.uint8).to("cuda")
     frags, nf, _, _ = S.wal_plan(offs, [int(n) for n in lens], start % 32768, recycle)
     pieces = _lib.lib.mck_wal_write_pieces(nf)
-    if os.environ.get("MCK_WAL_PIECES") != "1":
+    if os.environ.get("MCK_WAL_FUSED", "1") != "0":
+        assert pieces == 0  # the one-pass writer (k_wal_write_rows)
+    elif os.environ.get("MCK_WAL_PIECES") != "1":
         assert pieces >= 2, (nf, pieces)  # the overlapped multi-piece path really runs
     wr = S.WalBatchWriter(log_number=91, recycle_log_files=recycle, block_offset=start)
     out = wr.AddRecords(dev, offs, [int(n) for n in lens])
@@ -109,18 +111,50 @@ def test_wal_write_batch_pieces_bit_exact(gpu, oracle, recycle):
 
 
 @pytest.mark.gpu
-def test_wal_write_batch_single_piece_subprocess(gpu):
-    """The same group commit with MCK_WAL_PIECES=1 (read once per process):
-    the single-launch path, in a child process, stays byte-exact too."""
-    if os.environ.get("MCK_WAL_PIECES") == "1":
-        pytest.skip("already running single-piece")
-    env = dict(os.environ, MCK_WAL_PIECES="1")
+@pytest.mark.parametrize("pieces", ["1", "8"])
+def test_wal_write_batch_two_kernel_paths_subprocess(gpu, pieces):
+    """The two-kernel writer (MCK_WAL_FUSED=0: fragment CRCs, then k_wal_copy
+    in overlapped pieces -- or one launch each with MCK_WAL_PIECES=1), in a
+    child process (the switches are read once per process): byte-exact too."""
+    if os.environ.get("MCK_WAL_FUSED") == "0":
+        pytest.skip("already running the two-kernel path")
+    env = dict(os.environ, MCK_WAL_FUSED="0", MCK_WAL_PIECES=pieces)
     here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
-                        os.path.join(here, "test_wal_writer.py") + "::test_wal_write_batch_pieces_bit_exact"],
-                       env=env, cwd=os.path.dirname(here), capture_output=True, text=True, timeout=240)
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        "-k", "not subprocess", os.path.join(here, "test_wal_writer.py")],
+                       env=env, cwd=os.path.dirname(here), capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
-    assert "2 passed" in r.stdout, r.stdout[-500:]
+    assert " passed" in r.stdout, r.stdout[-500:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_write_batch_small_records_every_alignment(gpu, oracle, recycle):
+    """Records of 0..80 bytes (a payload inside one output piece, head and
+    tail bytes without a full piece, every output and source alignment) and
+    a block-straddling tail: the one-pass writer's byte paths."""
+    import torch
+
+    import speedb_amd as S
+    rng = np.random.default_rng(11)
+    lens = np.concatenate([np.arange(0, 81), rng.integers(0, 300, size=3000), [32761, 5, 40000, 0, 17]])
+    src = rng.integers(0, 256, size=int(lens.sum()) + 5, dtype=np.uint8).tobytes()
+    offs = np.concatenate([[0], np.cumsum(lens[:-1])]) + 5  # source not 16-aligned either
+    for start_pad in (0, 3, 11):
+        w = WalWriter(oracle, log_number=0xABCD, recycle=recycle)
+        if start_pad:
+            w.add_record(b"z" * start_pad)
+        start = len(w.buf)
+        for o, n in zip(offs, lens):
+            w.add_record(src[o:o + n])
+        dev = torch.frombuffer(bytearray(src + bytes(64)), dtype=torch.uint8).to("cuda")
+        wr = S.WalBatchWriter(log_number=0xABCD, recycle_log_files=recycle, block_offset=start)
+        got = wr.AddRecords(dev, offs, [int(n) for n in lens]).cpu().numpy().tobytes()
+        want = bytes(w.buf[start:])
+        assert len(got) == len(want)
+        if got != want:
+            i = next(k for k in range(len(got)) if got[k] != want[k])
+            raise AssertionError(f"start_pad {start_pad}: first difference at stream offset {i + start}")
 
 
 @pytest.mark.gpu
