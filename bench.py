@@ -435,15 +435,23 @@ def make_workload(args, dev, rank, world):
             _lib.check(_lib.lib.mck_wal_write_batch(src.data_ptr(), d_frags.data_ptr(), nf, 7, crc.data_ptr(),
                                                     out.data_ptr(), stream.cuda_stream), "mck_wal_write_batch")
         w.step = step
-        # the CRC and copy kernels overlap (piecewise, two streams: the
-        # engine's mck_wal_write_batch), so the unit timed is the whole step
         w.launches = 1
-        w.kernel = "mck::k_crc_auto<mck::OpWalFragCrc, false> + mck::k_wal_copy<false> (overlapped step)"
         w.span_bytes = int(lens.sum())
-        # per step: CRC reads the payload + 24 B descriptor + 4 B out per
-        # fragment; the writer reads the payload + descriptor + crc and
-        # writes the stream
-        w.alg_bytes = 2 * int(lens.sum()) + nbytes + nf * (24 + 4 + 24 + 4)
+        if _lib.lib.mck_wal_write_pieces(nf) == 0:
+            # one-pass writer: k_wal_write_rows in launches of <= ncu * 1528
+            # fragments, timed together as the step; it reads the payload and
+            # the 24 B descriptor once, writes the stream and the 4 B CRC
+            cap = torch.cuda.get_device_properties(dev).multi_processor_count * 1528
+            nl = -(-nf // cap)
+            w.kernel = f"mck::k_wal_write_rows<16> ({nl} launch(es) per step, timed as the step)"
+            w.alg_bytes = int(lens.sum()) + nbytes + nf * (24 + 4)
+        else:
+            # MCK_WAL_FUSED=0: the CRC and copy kernels overlap (piecewise,
+            # two streams), so the unit timed is the whole step; CRC reads the
+            # payload + 24 B descriptor + 4 B out per fragment, the copy reads
+            # the payload + descriptor + crc and writes the stream
+            w.kernel = "mck::k_crc_auto<mck::OpWalFragCrc, false> + mck::k_wal_copy<false> (overlapped step)"
+            w.alg_bytes = 2 * int(lens.sum()) + nbytes + nf * (24 + 4 + 24 + 4)
         w.desc = (f"device WAL writer: group commit of {len(lens)} records of 1000-1100 B per GPU "
                   f"(README 1 KB values) -> {nf} physical records, {nbytes} B of log stream "
                   "(log::Writer::AddRecord + EmitPhysicalRecord, SURVEY.md 8f row 3)")

@@ -10,7 +10,9 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspeedb_amd.so")
+# SPEEDB_AMD_LIB: an alternative build of the same engine (A/B experiments
+# under microbench/); the default is the in-tree library.
+LIB_PATH = os.environ.get("SPEEDB_AMD_LIB") or os.path.join(_HERE, "libspeedb_amd.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(

@@ -727,6 +727,15 @@ static bool wal_fused() {
   return v;
 }
 
+// Row width of the one-pass writer: MCK_WAL_ROW_LANES=8 or 16 (default).
+static int wal_row_lanes() {
+  static const int v = [] {
+    const char* e = getenv("MCK_WAL_ROW_LANES");
+    return e && atoi(e) == 8 ? 8 : 16;
+  }();
+  return v;
+}
+
 // pieces of at least 16 fragments per CU (one CRC grid's worth of spans)
 static uint32_t wal_pieces_for(uint32_t nfrags, int ncu) {
   uint32_t pieces = wal_pieces();
@@ -763,7 +772,8 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   if (wal_fused()) {
     // one pass: CRC + log stream in k_wal_write_rows, in launches of at most
     // ncu * kRowDescCache fragments (its LDS descriptor / dst_off tables)
-    if (int rc = ensure_lds(k_wal_write_rows<16>, dev)) return rc;
+    const bool w8 = wal_row_lanes() == 8;
+    if (int rc = w8 ? ensure_lds(k_wal_write_rows<8>, dev) : ensure_lds(k_wal_write_rows<16>, dev)) return rc;
     const uint32_t cap = (uint32_t)ncu * kRowDescCache;
     const uint32_t nl = (nfrags + cap - 1) / cap;
     const uint32_t per = (uint32_t)(((uint64_t)nfrags + nl - 1) / nl);
@@ -771,7 +781,10 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
     for (uint32_t first = 0; first < nfrags; first += per) {
       const uint32_t n = std::min(per, nfrags - first);
       const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
-      hipLaunchKernelGGL(k_wal_write_rows<16>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+      if (w8)
+        hipLaunchKernelGGL(k_wal_write_rows<8>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+      else
+        hipLaunchKernelGGL(k_wal_write_rows<16>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
       MCK_HIP(hipGetLastError());
     }
     return MCK_OK;

@@ -13,7 +13,14 @@ namespace mck {
 
 extern __device__ CrcTables g_crc_tables;
 // scratch that the one-pass WAL writer's idle lanes store to (never read)
-constexpr uint32_t kWalSinkBytes = 64 * 16 + 64;
+// MCK_WAL_SINK: how the one-pass writer's stores with nothing to write are
+// handled -- 0: exec-masked (not issued for those lanes), 1: redirected to a
+// per-lane slot shared by every wave, 2: redirected to per-wave slots.
+#ifndef MCK_WAL_SINK
+#define MCK_WAL_SINK 0
+#endif
+constexpr uint32_t kWalSinkWaves = MCK_WAL_SINK == 2 ? 4096 : 1;
+constexpr uint32_t kWalSinkBytes = kWalSinkWaves * 64 * 16 + 64;
 extern __device__ uint8_t g_wal_sink[kWalSinkBytes];
 
 constexpr uint32_t kRandomPrime = 0x6b9083d9u;  // table/format.cc:573
@@ -511,18 +518,20 @@ struct OpWalFragCrc {
 // mck_wal_write_batch in ONE kernel: the row driver (crc_rows_loop's
 // structure, 16-lane rows) CRCs each fragment and, in the same iteration,
 // writes what log::Writer appends for it (db/log_writer.cc:263-311):
-//   * the payload's 16-byte-aligned OUTPUT pieces of the round: lane c takes
-//     the four pieces whose source starts x = S + e + 16 j lie in its source
-//     chunk [S, S + 64) (e = -delta mod 16, delta = output - source), loads
-//     them dword-aligned (16 B + the next dword, re-read from L1/L2: the CRC
-//     loads of the same bytes were just issued), realigns with v_alignbyte
-//     and stores them non-temporal;
+//   * the payload's 16-byte-aligned OUTPUT pieces of the round's source
+//     window [S, S + 64 W): piece q starts at source x = S + e + 16 q
+//     (e = -delta mod 16, delta = output - source); lane c takes q = c + W j,
+//     so every load / store instruction covers 16 W contiguous bytes (with
+//     q = 4 c + j, 64-byte strided 16-byte stores, walwrite took 3.75 ms
+//     instead of 0.92 without the pieces); it loads them dword-aligned (16 B +
+//     the next dword, re-read from L1/L2: the CRC loads of the same bytes
+//     came in one iteration earlier), realigns with v_alignbyte and stores
+//     them;
 //   * at the span's last round: the < 16 payload bytes before the first and
 //     after the last full output piece, byte by byte, and the trailer padding
 //     + header ([masked CRC][len][type][log number]) -- the CRC is known then.
-// Stores with nothing to write go to a per-device sink, so every VMEM
-// instruction issues in every iteration (static vmcnt accounting, as for the
-// loads).  The payload is read from HBM once.
+// Stores with nothing to write are exec-masked (MCK_WAL_SINK above).  The
+// payload is read from HBM once.
 // LDS: the row image; fragments' dst_off at kLdsWalAux, over the un-shift
 // tables k >= 16, which this kernel never reads (typed init: no per-span
 // un-shift; the tail un-shift is < 16).
@@ -560,16 +569,41 @@ typedef __attribute__((address_space(1))) uint32_t gbl_st_u32_t;
 typedef __attribute__((address_space(1))) span_u32x4 gbl_st_u32x4_t;
 __device__ __forceinline__ void st_u8(uint64_t a, uint32_t v) { *reinterpret_cast<gbl_st_u8_t*>(a) = (uint8_t)v; }
 __device__ __forceinline__ void st_u32(uint64_t a, uint32_t v) { *reinterpret_cast<gbl_st_u32_t*>(a) = v; }
+// MCK_WAL_NT=1: non-temporal piece stores (walwrite 1.527 ms vs 1.480 with
+// plain stores, which stay the default).
+#ifndef MCK_WAL_NT
+#define MCK_WAL_NT 0
+#endif
 __device__ __forceinline__ void st_nt16(uint64_t a, uint4 o) {
   span_u32x4 q = {o.x, o.y, o.z, o.w};
-  __builtin_nontemporal_store(q, reinterpret_cast<gbl_st_u32x4_t*>(a));
+  if (MCK_WAL_NT)
+    __builtin_nontemporal_store(q, reinterpret_cast<gbl_st_u32x4_t*>(a));
+  else
+    *reinterpret_cast<gbl_st_u32x4_t*>(a) = q;
 }
 
-// W = 16: a row's 16 lanes also cover the <= 15 head / tail payload bytes.
+// MCK_WAL_EXP (timing experiments only, wrong output): 1 drops the piece
+// copies, 2 the head/tail bytes, 4 the header bytes, 8 the piece stores
+// (loads kept), 16 the piece loads (stores of zeros kept).
+#ifndef MCK_WAL_EXP
+#define MCK_WAL_EXP 0
+#endif
+#if MCK_WAL_SINK
+#define WAL_ST(ok, fn, a, snk, v) fn((ok) ? (a) : (snk), v)
+#else
+#define WAL_ST(ok, fn, a, snk, v) \
+  do {                            \
+    if (ok) fn(a, v);             \
+  } while (0)
+#endif
+
+// W = 8 or 16 lanes per row.
 template <int W>
 __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                const CrcTables* __restrict__ g) {
-  static_assert(W == 16, "the head/tail byte copies assume 16-lane rows");
+  static_assert(W == 8 || W == 16, "row width");
+  constexpr int kHT = 16 / W;  // head / tail payload bytes per lane (< 16 each)
+  constexpr int kHdr = 32 / W;  // padding + header bytes per lane (pad + hs <= 21)
   crc_rows_prologue(op, first, count, lds, g, false);
   {  // fragments' dst_off, staged like the descriptors (row_desc_stage order)
     const uint32_t G = gridDim.x, b = blockIdx.x;
@@ -586,7 +620,9 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
   const uint64_t base = reinterpret_cast<uint64_t>(op.src);
   const uint64_t obase = reinterpret_cast<uint64_t>(op.out);
   // per-lane sink slots (16 B each), never read
-  const uint64_t sink = reinterpret_cast<uint64_t>(&g_wal_sink[0]) + 16ull * (threadIdx.x & 63);
+  const uint32_t wslot = MCK_WAL_SINK == 2 ? (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kWalSinkWaves : 0;
+  const uint64_t sink = reinterpret_cast<uint64_t>(&g_wal_sink[0]) + 1024ull * wslot + 16ull * (threadIdx.x & 63);
+  (void)sink;
   const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
   uint32_t t = row_ticket<W>(true);
   bool live = t < share;
@@ -616,16 +652,18 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
     const uint64_t delta = P - ps;                   // (mod 2^64)
     const uint32_t e = (uint32_t)(0ull - delta) & 15u;
     const uint32_t be = e & 3u;
-    const uint64_t S = sp.a1 - 64ull * W * (uint32_t)(r + 1) + 64ull * c;
+    const uint64_t S = sp.a1 - 64ull * W * (uint32_t)(r + 1);  // the row's source window
     uint4 v[4];
     uint32_t w5[4];
     bool ok[4];
-    const uint64_t x0 = S + e;  // source start of the lane's first output-aligned piece
+    // lane c's pieces: the window's output-aligned pieces c, c + W, c + 2W,
+    // c + 3W -- each load and store instruction covers 16 W contiguous bytes
+    const uint64_t x0 = S + e + 16ull * c;
 #pragma unroll
     for (int j = 0; j < 4; j++) {
-      const uint64_t x = x0 + 16ull * j;
-      ok[j] = live && x >= ps && x + 16 <= pe;
-      const uint64_t f = ok[j] ? (x & ~3ull) : zp;
+      const uint64_t x = x0 + 16ull * W * j;
+      ok[j] = live && x >= ps && x + 16 <= pe && !(MCK_WAL_EXP & 1);
+      const uint64_t f = ok[j] && !(MCK_WAL_EXP & 16) ? (x & ~3ull) : zp;
       v[j] = span_load16<false>(f);
       // the fifth dword, unless the piece is dword-aligned (then it could
       // lie past the payload's last dword: re-read the fourth)
@@ -635,10 +673,18 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
     const uint64_t t16 = (P + sp.n) & ~15ull;                 // end of the last full piece
     const uint64_t hb_end = h16 < P + sp.n ? h16 : P + sp.n;  // head bytes [P, hb_end)
     const uint64_t tb_beg = t16 > hb_end ? t16 : hb_end;      // tail bytes [tb_beg, P + n)
-    const uint64_t oh = P + c, ot = tb_beg + c;
-    const bool okh = fin && oh < hb_end, okt = fin && ot < P + sp.n;
-    const uint32_t bh = *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : zp);
-    const uint32_t bt = *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : zp);
+    uint64_t oh[kHT], ot[kHT];
+    bool okh[kHT], okt[kHT];
+    uint32_t bh[kHT], bt[kHT];
+#pragma unroll
+    for (int m = 0; m < kHT; m++) {
+      oh[m] = P + c + W * m;
+      ot[m] = tb_beg + c + W * m;
+      okh[m] = fin && oh[m] < hb_end && !(MCK_WAL_EXP & 2);
+      okt[m] = fin && ot[m] < P + sp.n && !(MCK_WAL_EXP & 2);
+      bh[m] = *reinterpret_cast<gbl_u8_t*>(okh[m] ? ps + c + W * m : zp);
+      bt[m] = *reinterpret_cast<gbl_u8_t*>(okt[m] ? ps + (ot[m] - P) : zp);
+    }
 
 #pragma unroll
     for (int j = 0; j < 4; j++) {
@@ -647,10 +693,13 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
       o.y = __builtin_amdgcn_alignbyte(v[j].z, v[j].y, be);
       o.z = __builtin_amdgcn_alignbyte(v[j].w, v[j].z, be);
       o.w = __builtin_amdgcn_alignbyte(w5[j], v[j].w, be);
-      st_nt16(ok[j] ? x0 + 16ull * j + delta : sink, o);
+      WAL_ST(ok[j] && !(MCK_WAL_EXP & 8), st_nt16, x0 + 16ull * W * j + delta, sink, o);
     }
-    st_u8(okh ? oh : sink, bh);
-    st_u8(okt ? ot : sink + 1, bt);
+#pragma unroll
+    for (int m = 0; m < kHT; m++) {
+      WAL_ST(okh[m], st_u8, oh[m], sink, bh[m]);
+      WAL_ST(okt[m], st_u8, ot[m], sink + 1, bt[m]);
+    }
 
     // ---- next unit (as crc_rows_loop) ----
     const bool go = live && (!last || nt < share);
@@ -664,15 +713,15 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
     s = row_round<W>(s, cur, sp, r, c, L);
     uint32_t crc = 0;
     if (wave_any(fin)) crc = crc_mask(row_finish4<W>(s, sp, lf4));
-    st_u32(fin && c == 0 ? reinterpret_cast<uint64_t>(op.crcs + i) : sink + 4, crc);
-    // trailer padding + header: bytes c and c + 16 of [dst - pad, dst + hs)
+    WAL_ST(fin && c == 0, st_u32, reinterpret_cast<uint64_t>(op.crcs + i), sink + 4, crc);
+    // trailer padding + header: bytes c + W m of [dst - pad, dst + hs)
     const uint64_t hstart = obase + dst - pad;
 #pragma unroll
-    for (int m = 0; m < 2; m++) {
-      const uint32_t b = c + 16u * m;
-      const bool okb = fin && b < pad + hs;
+    for (int m = 0; m < kHdr; m++) {
+      const uint32_t b = c + (uint32_t)W * m;
+      const bool okb = fin && b < pad + hs && !(MCK_WAL_EXP & 4);
       const uint32_t val = b < pad ? 0u : wal_hdr_byte(b - pad, crc, sp.n, type, op.log_number);
-      st_u8(okb ? hstart + b : sink + 2 + m, val);
+      WAL_ST(okb, st_u8, hstart + b, sink + 2 + m, val);
     }
 
     // ---- advance ----
