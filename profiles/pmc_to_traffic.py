@@ -14,6 +14,7 @@ Writes profiles/traffic_<workload>.json and prints a summary.
 import csv
 import json
 import os
+import re
 import sys
 
 
@@ -41,8 +42,10 @@ def main():
     # "(overlapped step)": the bench times a whole step whose kernels run
     # concurrently in pieces (the device WAL writer); traffic is then per
     # step = per-launch average x launches per step
-    overlapped = kernel.endswith("(overlapped step)")
-    names = [k.strip() for k in kernel.replace("(overlapped step)", "").split(" + ")]
+    # "(N launch(es) per step, timed as the step)": one kernel launched N
+    # times per step (the one-pass WAL writer), likewise per step
+    overlapped = kernel.endswith("(overlapped step)") or kernel.endswith("timed as the step)")
+    names = [k.strip() for k in re.sub(r" \([^()]*(\([^()]*\)[^()]*)*\)$", "", kernel).split(" + ")]
     cfg = {k: v for k, v in line["config"].items() if k not in ("workload", "parallelism")}
     stats = {}
     with open(os.path.join(d, "trace", "trace_kernel_stats.csv")) as f:
@@ -71,7 +74,10 @@ def main():
     rd = 2 * 1024 * sum(fetch) / len(fetch)
     wr = 1024 * sum(write) / len(write)
     if overlapped:
-        per_step = calls / (line["warmup"] + line["steps"])
+        m = re.search(r"\((\d+) launch\(es\) per step", kernel)
+        # launches per step: stated in the label, else the dispatch count over
+        # the warmup + timed steps (an overlapped run without a settle phase)
+        per_step = int(m.group(1)) if m else calls / (line["warmup"] + line["steps"])
         rd, wr = rd * per_step, wr * per_step
         timed_ns = None
     alg = line["roofline"]["alg_bytes_per_launch"]
