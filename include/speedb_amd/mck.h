@@ -431,6 +431,78 @@ int mck_kv_protect_verify_batch(int kind, const mck_spans* keys,
                                 uint32_t* mismatch_count, uint64_t* computed,
                                 mck_stream_t stream);
 
+/* ---- per-KV protection of block entries ------------ */
+
+/* table/block_based/block.cc:1091 Block::InitializeDataBlockProtectionInfo,
+ * :1134 InitializeIndexBlockProtectionInfo, :1183
+ * InitializeMetaIndexBlockProtectionInfo for a batch of uncompressed block
+ * contents (the span of each block = its BlockContents, without the 5-byte
+ * trailer).  For every entry k of block i, in iteration order:
+ *   out[(key_base[i] + k) * prot_bytes ...] =
+ *       ProtectionInfo64().ProtectKV(key, value).Encode(prot_bytes)
+ * (block.h:271-274 GenerateKVChecksum) -- the block's kv_checksum_ array.
+ * The key is the full reassembled key (iter->key()); the value is
+ * iter->value() (data, metaindex) or iter->raw_value() (index: the encoded
+ * IndexValue bytes).  `kind` names the iterator that parses the entries: */
+#define MCK_BLOCK_DATA 0                  /* DataBlockIter (DecodeEntry)      */
+#define MCK_BLOCK_INDEX 1                 /* IndexBlockIter, value_is_full    */
+#define MCK_BLOCK_INDEX_DELTA 2           /* IndexBlockIter, delta-encoded
+                                             values (format_version >= 4)     */
+#define MCK_BLOCK_INDEX_DELTA_FIRST_KEY 3 /* ... + first key in the value
+                                             (kBinarySearchWithFirstKey)      */
+#define MCK_BLOCK_META 4                  /* MetaBlockIter (metaindex)        */
+
+/* Per-block status.  A block that is not OK gets no keys -- the reference
+ * sets its error marker (size_ = 0) and builds no protection. */
+#define MCK_BLOCK_OK 0
+#define MCK_BLOCK_BAD_CONTENTS 1 /* Block ctor error marker / NewDataIterator
+                                    "bad block contents"                       */
+#define MCK_BLOCK_BAD_ENTRY 2    /* "bad entry in block" (BlockIter::
+                                    CorruptionError, block.h:559)             */
+#define MCK_BLOCK_BAD_RESTARTS 3 /* restart array / intervals not as
+                                    BlockBuilder writes them (restart[0] != 0,
+                                    not increasing, shared != 0 at a restart,
+                                    an interval other than the last holding
+                                    fewer or more than block_restart_interval
+                                    entries): the reference only asserts these
+                                    and its output is undefined there          */
+
+/* Scratch for mck_block_kv_layout_batch (device bytes). */
+uint64_t mck_block_kv_scratch_bytes(uint32_t count);
+
+/* Pass 1 (device): every block's entry count and reassembled key bytes,
+ * as exclusive scans: key_base[count + 1] (key_base[count] = total keys),
+ * arena_base[count + 1] (total key bytes at [count]); status[count];
+ * restart_interval[count] (optional: GetRestartInterval, block.h:484).
+ * The caller reads key_base[count] and arena_base[count] back to size the
+ * work area and the output. */
+int mck_block_kv_layout_batch(int kind, const mck_spans* blocks,
+                              uint64_t* key_base, uint64_t* arena_base,
+                              uint32_t* restart_interval, int32_t* status,
+                              void* scratch, mck_stream_t stream);
+
+/* Device bytes of the work area of pass 2 (per-entry spans + key arena). */
+uint64_t mck_block_kv_work_bytes(uint64_t total_keys, uint64_t total_key_bytes);
+
+/* Pass 2: out = total_keys * prot_bytes bytes (device).  prot_bytes 1/2/4/8
+ * (block_protection_bytes_per_key). */
+int mck_block_kv_protect_batch(int kind, const mck_spans* blocks,
+                               uint32_t prot_bytes, const uint64_t* key_base,
+                               const uint64_t* arena_base, uint64_t total_keys,
+                               void* work, uint8_t* out, mck_stream_t stream);
+
+/* Read side: the per-entry check DataBlockIter / IndexBlockIter /
+ * MetaBlockIter run on every key they parse (block.h:567-574
+ * PerKVChecksumCorruptionError) for all entries at once:
+ * mismatch[key] = 0/1 against stored (the kv_checksum_ arrays, laid out as
+ * `out` above); mismatch_count (optional, caller-zeroed) counts them. */
+int mck_block_kv_verify_batch(int kind, const mck_spans* blocks,
+                              uint32_t prot_bytes, const uint64_t* key_base,
+                              const uint64_t* arena_base, uint64_t total_keys,
+                              void* work, const uint8_t* stored,
+                              uint8_t* mismatch, uint32_t* mismatch_count,
+                              mck_stream_t stream);
+
 /* ---- SST files: whole-file verification ------------- */
 
 /* Footer of a block-based table (table/format.h Footer). */

@@ -644,3 +644,170 @@ void orc_file_checksum_crc32c(const void* data, size_t n, uint8_t out[4]) {
   out[2] = (uint8_t)(c >> 8);
   out[3] = (uint8_t)c;
 }
+
+/* ------------------------------------------------------------------ */
+/* Per-KV protection of an uncompressed block's entries                */
+/* ------------------------------------------------------------------ */
+
+/* util/coding.h GetVarint32Ptr / GetVarint64Ptr: NULL when the varint runs
+ * past limit or past 5 / 10 bytes. */
+static const uint8_t* orc_varint(const uint8_t* p, const uint8_t* limit, int max_shift, uint64_t* v) {
+  uint64_t r = 0;
+  for (int shift = 0; shift <= max_shift && p < limit; shift += 7) {
+    uint64_t b = *p++;
+    if (b & 128) {
+      r |= (b & 127) << shift;
+    } else {
+      *v = r | (b << shift);
+      return p;
+    }
+  }
+  return 0;
+}
+
+/* table/block_based/block.cc:994-1027 NumRestarts / IndexType and the Block
+ * constructor (:1036-1083): the restart array offset, or -1 for the
+ * constructor's error marker (size_ = 0).  Hash-index footers (bit 31) only
+ * for blocks <= kMaxBlockSizeSupportedByHashIndex (64 KiB). */
+static int64_t orc_block_restarts(const uint8_t* d, uint32_t size, uint32_t* num_restarts) {
+  *num_restarts = 0;
+  if (size < 4) return -1;
+  uint32_t footer = rd32(d + size - 4);
+  int hash = 0;
+  uint32_t n = footer;
+  if (size <= (1u << 16)) {
+    hash = (footer >> 31) & 1;
+    n = footer & 0x7FFFFFFFu;
+  }
+  *num_restarts = n;
+  if (!hash) {
+    uint32_t ro = size - (1 + n) * 4u;
+    if (ro > size - 4u) return -1;
+    return ro;
+  }
+  if (size < 6) return -1;
+  /* data_block_hash_index.cc:76-84 Initialize (NUM_BUCK u16 before the footer) */
+  uint16_t sz16 = (uint16_t)(size - 4);
+  uint16_t nb = (uint16_t)(d[sz16 - 2] | (d[sz16 - 1] << 8));
+  uint16_t map_offset = (uint16_t)(sz16 - 2 - nb);
+  uint32_t ro = (uint32_t)map_offset - n * 4u;
+  if (ro > map_offset) return -1;
+  return ro;
+}
+
+/* One entry at p (table/block_based/block.cc:37-64 DecodeEntry, :68-97
+ * CheckAndDecodeEntry, :110-139 DecodeEntryV4 + :719-727 DecodeCurrentValue /
+ * table/format.cc:137-162 IndexValue::DecodeFrom for delta-encoded index
+ * values).  Returns the key delta's start, or NULL ("bad entry in block"). */
+static const uint8_t* orc_block_entry(int kind, const uint8_t* p, const uint8_t* limit, uint32_t* shared,
+                                      uint32_t* non_shared, const uint8_t** val, uint32_t* vlen) {
+  uint64_t s, ns, vl = 0;
+  if (limit - p < 3) return 0;
+  if (kind == ORC_BLOCK_INDEX_DELTA || kind == ORC_BLOCK_INDEX_DELTA_FIRST_KEY) {
+    if ((p = orc_varint(p, limit, 28, &s)) == 0) return 0;
+    if ((p = orc_varint(p, limit, 28, &ns)) == 0) return 0;
+    if ((uint64_t)(limit - p) < ns) return 0;
+    const uint8_t* v = p + ns;
+    const uint8_t* q = v;
+    uint64_t x;
+    if (s != 0) { /* delta-encoded size (GetVarsignedint64) */
+      if ((q = orc_varint(q, limit, 63, &x)) == 0) return 0;
+    } else { /* BlockHandle::DecodeFrom: offset, size */
+      if ((q = orc_varint(q, limit, 63, &x)) == 0) return 0;
+      if ((q = orc_varint(q, limit, 63, &x)) == 0) return 0;
+    }
+    if (kind == ORC_BLOCK_INDEX_DELTA_FIRST_KEY) { /* GetLengthPrefixedSlice */
+      if ((q = orc_varint(q, limit, 28, &x)) == 0) return 0;
+      if ((uint64_t)(limit - q) < x) return 0;
+      q += x;
+    }
+    *shared = (uint32_t)s;
+    *non_shared = (uint32_t)ns;
+    *val = v;
+    *vlen = (uint32_t)(q - v);
+    return p;
+  }
+  if ((p = orc_varint(p, limit, 28, &s)) == 0) return 0;
+  if ((p = orc_varint(p, limit, 28, &ns)) == 0) return 0;
+  if ((p = orc_varint(p, limit, 28, &vl)) == 0) return 0;
+  if ((uint64_t)(limit - p) < ns + vl) return 0;
+  *shared = (uint32_t)s;
+  *non_shared = (uint32_t)ns;
+  *val = p + ns;
+  *vlen = (uint32_t)vl;
+  return p;
+}
+
+/* table/block_based/block.cc:1091-1132 Block::InitializeDataBlockProtectionInfo
+ * (:1134-1181 Index, :1183-1222 MetaIndex): walk the entries in order,
+ * reassembling every key from the previous one (ParseNextKey :617-665), and
+ * write ProtectionInfo64().ProtectKV(key, value).Encode(prot_bytes)
+ * (block.h:271-274) per entry.  GetRestartInterval (block.h:484-497) and
+ * NumberOfKeys (:500-512) size the output.  The reference only asserts what
+ * BlockBuilder guarantees (block_builder.cc:188-252: restart array sorted and
+ * on entry starts, shared == 0 at every restart point, every interval but the
+ * last holding exactly block_restart_interval entries); this restatement, like
+ * the engine, reports a block breaking it as ORC_BLOCK_BAD_RESTARTS. */
+int orc_block_kv_protect(int kind, const void* block, size_t n, uint32_t prot_bytes, uint8_t* out,
+                         size_t out_cap, uint32_t* nkeys_out, uint32_t* interval_out) {
+  const uint8_t* d = (const uint8_t*)block;
+  *nkeys_out = 0;
+  if (interval_out) *interval_out = 0;
+  if (n > 0xFFFFFFFFu) return ORC_BLOCK_BAD_CONTENTS;
+  uint32_t nr;
+  int64_t ro = orc_block_restarts(d, (uint32_t)n, &nr);
+  if (ro < 0) return ORC_BLOCK_BAD_CONTENTS;
+  if (nr == 0) return ORC_BLOCK_OK; /* protection_bytes_per_key_ stays 0 */
+  if (n < 8) return ORC_BLOCK_BAD_CONTENTS; /* NewDataIterator: "bad block contents" */
+  const uint8_t* limit = d + ro;
+  const uint8_t* ra = d + ro;
+  /* restart array as BlockBuilder writes it */
+  if (ro != 0 && rd32(ra) != 0) return ORC_BLOCK_BAD_RESTARTS;
+  for (uint32_t r = 1; r < nr; r++)
+    if (rd32(ra + 4 * r) <= rd32(ra + 4 * (r - 1)) || rd32(ra + 4 * r) >= ro) return ORC_BLOCK_BAD_RESTARTS;
+  if (ro == 0) return nr == 1 ? ORC_BLOCK_OK : ORC_BLOCK_BAD_RESTARTS; /* no entries */
+  uint8_t* key = 0;
+  size_t kcap = 0, klen = 0;
+  uint32_t idx = 0, interval = 0, in_cur = 0, r = 0;
+  const uint8_t* p = d;
+  int st = ORC_BLOCK_OK;
+  while (p < limit) {
+    const uint32_t off = (uint32_t)(p - d);
+    const int at_restart = r < nr && off == rd32(ra + 4 * r);
+    if (r < nr && off > rd32(ra + 4 * r)) { st = ORC_BLOCK_BAD_RESTARTS; break; } /* restart inside an entry */
+    if (at_restart) {
+      if (r == 1) interval = in_cur;
+      else if (r > 1 && in_cur != interval) { st = ORC_BLOCK_BAD_RESTARTS; break; }
+      in_cur = 0;
+      r++;
+    }
+    uint32_t sh, ns, vl;
+    const uint8_t* v;
+    const uint8_t* q = orc_block_entry(kind, p, limit, &sh, &ns, &v, &vl);
+    if (!q) { st = ORC_BLOCK_BAD_ENTRY; break; }
+    /* shared != 0 at a restart point: the first entry of the block has no key
+     * to share with (ParseNextKey's raw_key_.Size() < shared); later ones
+     * would reuse the previous interval's key (not a BlockBuilder layout) */
+    if (at_restart && sh != 0) { st = r == 1 ? ORC_BLOCK_BAD_ENTRY : ORC_BLOCK_BAD_RESTARTS; break; }
+    if (klen < sh) { st = ORC_BLOCK_BAD_ENTRY; break; }
+    if (sh + (size_t)ns > kcap) {
+      kcap = 2 * (sh + (size_t)ns) + 64;
+      key = (uint8_t*)realloc(key, kcap);
+    }
+    memcpy(key + sh, q, ns); /* TrimAppend(shared, p, non_shared) */
+    klen = sh + (size_t)ns;
+    const uint64_t h = orc_kv_protect(0, key, klen, v, vl, 0, 0);
+    if ((size_t)(idx + 1) * prot_bytes <= out_cap)
+      for (uint32_t b = 0; b < prot_bytes; b++) out[(size_t)idx * prot_bytes + b] = (uint8_t)(h >> (8 * b));
+    idx++;
+    in_cur++;
+    p = v + vl;
+  }
+  free(key);
+  if (st == ORC_BLOCK_OK && r != nr) st = ORC_BLOCK_BAD_RESTARTS; /* restarts past the last entry */
+  if (st != ORC_BLOCK_OK) return st;
+  if (nr == 1) interval = 0; /* GetRestartInterval: 0 for a single restart */
+  *nkeys_out = idx;
+  if (interval_out) *interval_out = interval;
+  return ORC_BLOCK_OK;
+}

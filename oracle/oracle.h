@@ -77,6 +77,18 @@ uint64_t orc_hash64(const void* data, size_t n, uint64_t seed);
 uint64_t orc_kv_protect(int mode, const void* key, size_t kn, const void* value,
                         size_t vn, uint8_t op, uint64_t extra);
 
+/* Per-KV protection of one uncompressed block's entries
+ * (table/block_based/block.cc:1091 InitializeDataBlockProtectionInfo, :1134
+ * Index, :1183 MetaIndex).  kind: which iterator parses the entries. */
+enum { ORC_BLOCK_DATA = 0, ORC_BLOCK_INDEX = 1, ORC_BLOCK_INDEX_DELTA = 2,
+       ORC_BLOCK_INDEX_DELTA_FIRST_KEY = 3, ORC_BLOCK_META = 4 };
+enum { ORC_BLOCK_OK = 0, ORC_BLOCK_BAD_CONTENTS = 1, ORC_BLOCK_BAD_ENTRY = 2,
+       ORC_BLOCK_BAD_RESTARTS = 3 };
+/* Writes nkeys * prot_bytes checksum bytes (as far as out_cap allows),
+ * *nkeys_out and the restart interval; returns an ORC_BLOCK_* status. */
+int orc_block_kv_protect(int kind, const void* block, size_t n, uint32_t prot_bytes, uint8_t* out,
+                         size_t out_cap, uint32_t* nkeys_out, uint32_t* interval_out);
+
 #ifdef __cplusplus
 }
 #endif

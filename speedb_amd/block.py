@@ -1,0 +1,169 @@
+"""Per-KV protection of block entries over the engine's
+C ABI: table/block_based/block.cc:1091-1222
+Block::Initialize{Data,Index,MetaIndex}BlockProtectionInfo for a whole batch
+of uncompressed blocks at once, and the per-entry check the block iterators
+run while reading (block.h:567-574 PerKVChecksumCorruptionError).
+
+The device walks every block's restart intervals in parallel, reassembles the
+prefix-compressed keys into a key arena and hashes every (key, value) pair
+with ProtectionInfo64().ProtectKV(key, value).Encode(protection_bytes_per_key)
+(block.h:271-274).  Blocks are device-resident torch byte tensors described by
+``checksum.Spans`` (one span = one block's contents, no trailer).
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from dataclasses import dataclass
+from typing import Optional
+
+from ._lib import check, lib
+from .checksum import Spans, Status, _stream, _torch
+
+
+class BlockKind(enum.IntEnum):
+    """Which iterator parses the entries (include/speedb_amd/mck.h)."""
+    kData = 0                 # DataBlockIter
+    kIndex = 1                # IndexBlockIter, value_is_full
+    kIndexDelta = 2           # IndexBlockIter, delta-encoded values
+    kIndexDeltaFirstKey = 3   # ... with the first key in each value
+    kMetaIndex = 4            # MetaBlockIter
+
+
+class BlockStatus(enum.IntEnum):
+    kOk = 0
+    kBadContents = 1
+    kBadEntry = 2
+    kBadRestarts = 3
+
+
+_MESSAGES = {
+    BlockStatus.kBadContents: "bad block contents",
+    BlockStatus.kBadEntry: "bad entry in block",
+    BlockStatus.kBadRestarts: "block restart array or intervals not as BlockBuilder writes them",
+}
+
+
+@dataclass
+class BlockProtection:
+    """The kv_checksum_ arrays of a batch: block i's entries are keys
+    key_base[i] .. key_base[i+1]-1, each ``protection_bytes_per_key`` bytes
+    of ``kv_checksum``."""
+    kind: BlockKind
+    protection_bytes_per_key: int
+    key_base: object          # int64 [count + 1] (device)
+    arena_base: object        # int64 [count + 1] (device)
+    status: object            # int32 [count] (device)
+    restart_interval: object  # int32 [count] (device)
+    total_keys: int
+    total_key_bytes: int
+    work: object              # uint8 work area (device), reused by verify
+    kv_checksum: object       # uint8 [total_keys * protection_bytes_per_key] (device)
+
+    def block_status(self, i: int) -> Status:
+        st = BlockStatus(int(self.status[i]))
+        return Status.OK() if st == BlockStatus.kOk else Status.Corruption(_MESSAGES[st])
+
+    def block_checksums(self, i: int) -> bytes:
+        a, b = int(self.key_base[i]), int(self.key_base[i + 1])
+        p = self.protection_bytes_per_key
+        return bytes(self.kv_checksum[a * p:b * p].cpu().numpy().tobytes())
+
+
+def _layout(kind: int, blocks: Spans, stream):
+    torch = _torch()
+    dev = blocks.base.device
+    n = blocks.count
+    key_base = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    arena_base = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    interval = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    scratch = torch.empty(int(lib.mck_block_kv_scratch_bytes(n)), dtype=torch.uint8, device=dev)
+    s = blocks.c()
+    check(lib.mck_block_kv_layout_batch(int(kind), ctypes.byref(s), key_base.data_ptr(), arena_base.data_ptr(),
+                                        interval.data_ptr(), status.data_ptr(), scratch.data_ptr(),
+                                        _stream(stream)), "mck_block_kv_layout_batch")
+    totals = torch.stack([key_base[n], arena_base[n]]).cpu()
+    return key_base, arena_base, status[:n], interval[:n], int(totals[0]), int(totals[1])
+
+
+def _work(total_keys: int, total_key_bytes: int, device):
+    torch = _torch()
+    nbytes = int(lib.mck_block_kv_work_bytes(total_keys, total_key_bytes))
+    return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+
+
+def InitializeBlockProtectionInfo(kind: int, blocks: Spans, protection_bytes_per_key: int,
+                                  stream=None) -> BlockProtection:
+    """Per-KV checksums of every entry of every block in ``blocks``."""
+    torch = _torch()
+    key_base, arena_base, status, interval, nk, nkb = _layout(kind, blocks, stream)
+    work = _work(nk, nkb, blocks.base.device)
+    out = torch.empty(max(nk * protection_bytes_per_key, 1), dtype=torch.uint8, device=blocks.base.device)
+    s = blocks.c()
+    check(lib.mck_block_kv_protect_batch(int(kind), ctypes.byref(s), protection_bytes_per_key,
+                                         key_base.data_ptr(), arena_base.data_ptr(), nk, work.data_ptr(),
+                                         out.data_ptr(), _stream(stream)), "mck_block_kv_protect_batch")
+    return BlockProtection(BlockKind(kind), protection_bytes_per_key, key_base, arena_base, status, interval,
+                           nk, nkb, work, out[:nk * protection_bytes_per_key])
+
+
+def InitializeDataBlockProtectionInfo(blocks: Spans, protection_bytes_per_key: int,
+                                      stream=None) -> BlockProtection:
+    """block.cc:1091 Block::InitializeDataBlockProtectionInfo."""
+    return InitializeBlockProtectionInfo(BlockKind.kData, blocks, protection_bytes_per_key, stream)
+
+
+def InitializeIndexBlockProtectionInfo(blocks: Spans, protection_bytes_per_key: int, value_is_full: bool,
+                                       index_has_first_key: bool, stream=None) -> BlockProtection:
+    """block.cc:1134 Block::InitializeIndexBlockProtectionInfo."""
+    kind = (BlockKind.kIndex if value_is_full else
+            BlockKind.kIndexDeltaFirstKey if index_has_first_key else BlockKind.kIndexDelta)
+    return InitializeBlockProtectionInfo(kind, blocks, protection_bytes_per_key, stream)
+
+
+def InitializeMetaIndexBlockProtectionInfo(blocks: Spans, protection_bytes_per_key: int,
+                                           stream=None) -> BlockProtection:
+    """block.cc:1183 Block::InitializeMetaIndexBlockProtectionInfo."""
+    return InitializeBlockProtectionInfo(BlockKind.kMetaIndex, blocks, protection_bytes_per_key, stream)
+
+
+def VerifyBlockProtectionInfo(blocks: Spans, prot: BlockProtection, stored=None, stream=None):
+    """Check every entry against ``stored`` (default: prot.kv_checksum, as
+    read back from the block cache).  Returns (mismatch uint8 [total_keys],
+    mismatch_count int32[1])."""
+    torch = _torch()
+    dev = blocks.base.device
+    stored = prot.kv_checksum if stored is None else stored
+    mismatch = torch.empty(max(prot.total_keys, 1), dtype=torch.uint8, device=dev)
+    count = torch.zeros(1, dtype=torch.int32, device=dev)
+    s = blocks.c()
+    check(lib.mck_block_kv_verify_batch(int(prot.kind), ctypes.byref(s), prot.protection_bytes_per_key,
+                                        prot.key_base.data_ptr(), prot.arena_base.data_ptr(), prot.total_keys,
+                                        prot.work.data_ptr(), stored.data_ptr(), mismatch.data_ptr(),
+                                        count.data_ptr(), _stream(stream)), "mck_block_kv_verify_batch")
+    return mismatch[:prot.total_keys], count
+
+
+def PerKVChecksumStatus(prot: BlockProtection, mismatch, entry_offsets: Optional[list] = None) -> list:
+    """(block, Status) for every block holding a mismatching entry, with the
+    reference's message (block.h:567-574): the first bad entry's index and,
+    when ``entry_offsets`` (per block, the entries' byte offsets) is given,
+    its offset."""
+    torch = _torch()
+    bad = torch.nonzero(mismatch).flatten().cpu().tolist()
+    if not bad:
+        return []
+    kb = prot.key_base.cpu().tolist()
+    out, seen = [], set()
+    import bisect
+    for k in bad:
+        i = bisect.bisect_right(kb, k) - 1
+        if i in seen:
+            continue
+        seen.add(i)
+        e = k - kb[i]
+        off = entry_offsets[i][e] if entry_offsets is not None else "?"
+        out.append((i, Status.Corruption("Corrupted block entry: per key-value checksum verification failed."
+                                         f" Offset: {off}. Entry index: {e}.")))
+    return out

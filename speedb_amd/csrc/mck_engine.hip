@@ -18,6 +18,7 @@
 #include "../../include/speedb_amd/mck.h"
 #include "mck_internal.h"
 #include "mck_kernels.hpp"
+#include "mck_block.hpp"
 
 namespace mck {
 
@@ -453,6 +454,87 @@ int stage_in(const void* data, size_t n, uint8_t** d_data, void** d_out, size_t 
   return MCK_OK;
 }
 
+// ---- per-KV protection of block entries: launch helpers ------------------
+template <template <int> class K, class... A>
+int launch_blk(int kind, uint32_t count, hipStream_t st, A... args);
+
+template <int KIND>
+struct BlkLayout {
+  static void go(dim3 g, hipStream_t st, SpanSrc s, uint32_t n, uint64_t* a, uint64_t* b, uint32_t* ri, int32_t* stt) {
+    hipLaunchKernelGGL(k_block_layout<KIND>, g, dim3(256), 0, st, s, n, a, b, ri, stt);
+  }
+};
+template <int KIND>
+struct BlkMat {
+  static void go(dim3 g, hipStream_t st, SpanSrc s, uint32_t n, const uint64_t* kb, const uint64_t* ab, uint8_t* arena,
+                 uint64_t* koff, uint32_t* klen, uint64_t* voff, uint32_t* vlen) {
+    hipLaunchKernelGGL(k_block_materialize<KIND>, g, dim3(256), 0, st, s, n, kb, ab, arena, koff, klen, voff, vlen);
+  }
+};
+
+template <template <int> class K, class... A>
+int launch_blk(int kind, uint32_t count, hipStream_t st, A... args) {
+  int ncu;
+  if (int rc = current_device(nullptr, &ncu)) return rc;
+  const dim3 g(std::min<uint32_t>((uint32_t)ncu * 16, (count + 3) / 4));
+  switch (kind) {
+    case MCK_BLOCK_DATA: K<kBlkData>::go(g, st, args...); break;
+    case MCK_BLOCK_INDEX: K<kBlkIndex>::go(g, st, args...); break;
+    case MCK_BLOCK_INDEX_DELTA: K<kBlkIndexDelta>::go(g, st, args...); break;
+    case MCK_BLOCK_INDEX_DELTA_FIRST_KEY: K<kBlkIndexDeltaFk>::go(g, st, args...); break;
+    case MCK_BLOCK_META: K<kBlkMeta>::go(g, st, args...); break;
+    default:
+      set_err("unknown block kind %d", kind);
+      return MCK_EINVAL;
+  }
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+uint64_t blk_tiles(uint32_t count) { return ((uint64_t)count + kBlkScanTile - 1) / kBlkScanTile; }
+
+// work area: [koff u64 K][voff u64 K][klen u32 K][vlen u32 K] [key arena]
+struct BlkWork {
+  uint64_t *koff, *voff;
+  uint32_t *klen, *vlen;
+  uint8_t* arena;
+};
+uint64_t blk_work_head(uint64_t keys) { return (keys * 24 + 255) & ~255ull; }
+BlkWork blk_work(void* work, uint64_t keys) {
+  uint8_t* w = static_cast<uint8_t*>(work);
+  return BlkWork{reinterpret_cast<uint64_t*>(w), reinterpret_cast<uint64_t*>(w + 8 * keys),
+                 reinterpret_cast<uint32_t*>(w + 16 * keys), reinterpret_cast<uint32_t*>(w + 20 * keys),
+                 w + blk_work_head(keys)};
+}
+
+int blk_entries(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_t* key_base,
+                const uint64_t* arena_base, uint64_t total_keys, void* work, hipStream_t st, BlkWork* w) {
+  if (int rc = check_spans(blocks)) return rc;
+  if (kind < MCK_BLOCK_DATA || kind > MCK_BLOCK_META) {
+    set_err("unknown block kind %d", kind);
+    return MCK_EINVAL;
+  }
+  if (prot_bytes != 1 && prot_bytes != 2 && prot_bytes != 4 && prot_bytes != 8) {
+    set_err("protection_bytes_per_key must be 1, 2, 4 or 8 (got %u)", prot_bytes);
+    return MCK_EINVAL;
+  }
+  if (total_keys > 0xFFFFFFFFull) {
+    set_err("%llu keys in one batch (max 2^32 - 1)", (unsigned long long)total_keys);
+    return MCK_EINVAL;
+  }
+  if (blocks->count && (!key_base || !arena_base)) {
+    set_err("key_base/arena_base is NULL");
+    return MCK_EINVAL;
+  }
+  if (total_keys && !work) {
+    set_err("work is NULL");
+    return MCK_EINVAL;
+  }
+  if (!total_keys || !blocks->count) return MCK_OK;
+  *w = blk_work(work, total_keys);
+  return launch_blk<BlkMat>(kind, blocks->count, st, to_src(blocks), blocks->count, key_base, arena_base, w->arena,
+                            w->koff, w->klen, w->voff, w->vlen);
+}
 }  // namespace
 }  // namespace mck
 
@@ -1124,6 +1206,80 @@ int mck_kv_protect_verify_batch(int kind, const mck_spans* keys, const mck_spans
   const OpKvProtect<true> op{to_src(keys), to_src(values), op_types, extras, kind, computed, stored, prot_bytes,
                              mismatch, mismatch_count};
   return launch_xph3(op, values->count, kSeedV, reinterpret_cast<hipStream_t>(stream));
+}
+
+// ---- per-KV protection of block entries (block.cc:1091-1222) ---------------
+
+uint64_t mck_block_kv_scratch_bytes(uint32_t count) { return 16 * blk_tiles(count) + 64; }
+
+uint64_t mck_block_kv_work_bytes(uint64_t total_keys, uint64_t total_key_bytes) {
+  return blk_work_head(total_keys) + total_key_bytes + 16;
+}
+
+int mck_block_kv_layout_batch(int kind, const mck_spans* blocks, uint64_t* key_base, uint64_t* arena_base,
+                              uint32_t* restart_interval, int32_t* status, void* scratch, mck_stream_t stream) {
+  t_err[0] = 0;
+  if (int rc = check_spans(blocks)) return rc;
+  if (!key_base || !arena_base || (blocks->count && (!status || !scratch))) {
+    set_err("key_base/arena_base/status/scratch is NULL");
+    return MCK_EINVAL;
+  }
+  stat_batch(blocks->count, known_bytes(blocks));
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const uint32_t n = blocks->count;
+  if (!n) {
+    MCK_HIP(hipMemsetAsync(key_base, 0, 8, st));
+    MCK_HIP(hipMemsetAsync(arena_base, 0, 8, st));
+    return MCK_OK;
+  }
+  if (int rc = launch_blk<BlkLayout>(kind, n, st, to_src(blocks), n, key_base, arena_base, restart_interval, status))
+    return rc;
+  const uint32_t tiles = (uint32_t)blk_tiles(n);
+  uint64_t* tsum = static_cast<uint64_t*>(scratch);
+  hipLaunchKernelGGL(k_blk_scan_tiles, dim3(tiles), dim3(kBlkScanThreads), 0, st, key_base, arena_base, n, tsum);
+  hipLaunchKernelGGL(k_blk_scan_top, dim3(1), dim3(kBlkScanThreads), 0, st, tsum, tiles, key_base, arena_base, n);
+  hipLaunchKernelGGL(k_blk_scan_apply, dim3(tiles), dim3(kBlkScanThreads), 0, st, key_base, arena_base, n, tsum);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+int mck_block_kv_protect_batch(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_t* key_base,
+                               const uint64_t* arena_base, uint64_t total_keys, void* work, uint8_t* out,
+                               mck_stream_t stream) {
+  t_err[0] = 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (total_keys && !out) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  BlkWork w{};
+  if (int rc = blk_entries(kind, blocks, prot_bytes, key_base, arena_base, total_keys, work, st, &w)) return rc;
+  if (!total_keys || !blocks->count) return MCK_OK;
+  const uint32_t k = (uint32_t)total_keys;
+  OpKvProtect<false> op{SpanSrc{w.arena, w.koff, w.klen, 0, 0},
+                        SpanSrc{static_cast<const uint8_t*>(blocks->base), w.voff, w.vlen, 0, 0},
+                        nullptr, nullptr, MCK_KV_PROTECT_KV, nullptr, nullptr, prot_bytes, nullptr, nullptr};
+  op.enc = out;
+  return launch_xph3(op, k, kSeedV, st);
+}
+
+int mck_block_kv_verify_batch(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_t* key_base,
+                              const uint64_t* arena_base, uint64_t total_keys, void* work, const uint8_t* stored,
+                              uint8_t* mismatch, uint32_t* mismatch_count, mck_stream_t stream) {
+  t_err[0] = 0;
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (total_keys && (!stored || !mismatch)) {
+    set_err("stored/mismatch is NULL");
+    return MCK_EINVAL;
+  }
+  BlkWork w{};
+  if (int rc = blk_entries(kind, blocks, prot_bytes, key_base, arena_base, total_keys, work, st, &w)) return rc;
+  if (!total_keys || !blocks->count) return MCK_OK;
+  const OpKvProtect<true> op{SpanSrc{w.arena, w.koff, w.klen, 0, 0},
+                             SpanSrc{static_cast<const uint8_t*>(blocks->base), w.voff, w.vlen, 0, 0},
+                             nullptr, nullptr, MCK_KV_PROTECT_KV, nullptr, stored, prot_bytes, mismatch,
+                             mismatch_count};
+  return launch_xph3(op, (uint32_t)total_keys, kSeedV, st);
 }
 
 // ---- partitioning + host-resident multi-GPU pipeline -----------------------

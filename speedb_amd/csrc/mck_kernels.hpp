@@ -394,6 +394,9 @@ struct OpKvProtect {
   uint32_t prot_bytes;
   uint8_t* mismatch;
   uint32_t* mismatch_count;
+  // compute mode: also (or instead of out) the Encode(prot_bytes) form,
+  // prot_bytes little-endian bytes per KV (db/kv_checksum.h:97-121)
+  uint8_t* enc = nullptr;
   typedef KvPre Pre;
   __device__ const uint8_t* base() const { return values.base; }
   __device__ uint64_t off(uint32_t i) const { return values.off(i); }
@@ -427,7 +430,9 @@ struct OpKvProtect {
     if (kind == 2) v ^= xxph3_u64(e.extra, kSeedS);
     if (kind == 3) v ^= xxph3_u32((uint32_t)e.extra, kSeedC);
     if (!VERIFY) {
-      out[i] = v;
+      if (out) out[i] = v;
+      if (enc)
+        for (uint32_t b = 0; b < prot_bytes; b++) enc[(uint64_t)i * prot_bytes + b] = (uint8_t)(v >> (8 * b));
       return;
     }
     const uint64_t sv = e.stored;

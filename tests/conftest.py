@@ -48,6 +48,9 @@ def _bind(lib, prefix):
             "file_checksum_crc32c": (None, [c.c_char_p, c.c_size_t, c.c_char_p]),
             "verify_block": (c.c_int, [c.c_int, c.c_char_p, c.c_size_t, c.c_uint32, c.c_uint64,
                                        ctypes.POINTER(c.c_uint32), ctypes.POINTER(c.c_uint32)]),
+            "block_kv_protect": (c.c_int, [c.c_int, c.c_char_p, c.c_size_t, c.c_uint32, c.c_char_p,
+                                           c.c_size_t, ctypes.POINTER(c.c_uint32),
+                                           ctypes.POINTER(c.c_uint32)]),
         })
     sig.update({
         "context_modifier": (c.c_uint32, [c.c_uint32, c.c_uint64]),
@@ -110,6 +113,17 @@ class _Oracle:
 
     def KvProtect(self, mode, key, value, op=0, extra=0):
         return self.lib.orc_kv_protect(mode, key, len(key), value, len(value), op, extra)
+
+    def BlockKvProtect(self, kind, block, prot_bytes):
+        """(status, kv_checksum bytes, restart interval) of one block
+        (block.cc:1091-1222 Initialize*BlockProtectionInfo)."""
+        nk, ri = ctypes.c_uint32(), ctypes.c_uint32()
+        cap = len(block) * 8 + 64
+        out = ctypes.create_string_buffer(cap)
+        st = self.lib.orc_block_kv_protect(int(kind), block, len(block), prot_bytes, out, cap,
+                                           ctypes.byref(nk), ctypes.byref(ri))
+        assert nk.value * prot_bytes <= cap
+        return st, out.raw[:nk.value * prot_bytes], ri.value
 
     def WalRecordCrc(self, t, payload, recyclable, log_number):
         return self.lib.orc_wal_record_crc(t, payload, len(payload), 1 if recyclable else 0,

@@ -58,10 +58,15 @@ def common_prefix(a: bytes, b: bytes) -> int:
 
 
 def build_block(entries: List[Tuple[bytes, bytes]], restart_interval: int = 16,
-                delta_values: Optional[List[Optional[bytes]]] = None) -> bytes:
+                delta_values: Optional[List[Optional[bytes]]] = None, hash_buckets: int = 0,
+                bucket_fill: int = 0xFF) -> bytes:
     """BlockBuilder: entries (key, value).  With delta_values (index value
     delta encoding, format_version >= 4) there is no value_length field and
-    an entry with shared != 0 stores delta_values[i] instead of its value."""
+    an entry with shared != 0 stores delta_values[i] instead of its value.
+    hash_buckets > 0 appends a data-block hash index of that many buckets
+    (data_block_hash_index.cc DataBlockHashIndexBuilder::Finish: bucket
+    bytes + NUM_BUCK u16) and sets the footer's index-type bit
+    (data_block_footer.cc:24-39)."""
     buf = bytearray()
     restarts = []
     last = b""
@@ -82,7 +87,11 @@ def build_block(entries: List[Tuple[bytes, bytes]], restart_interval: int = 16,
         restarts = [0]
     for r in restarts:
         buf += struct.pack("<I", r)
-    buf += struct.pack("<I", len(restarts))
+    footer = len(restarts)
+    if hash_buckets:
+        buf += bytes([bucket_fill]) * hash_buckets + struct.pack("<H", hash_buckets)
+        footer |= 1 << 31
+    buf += struct.pack("<I", footer)
     return bytes(buf)
 
 

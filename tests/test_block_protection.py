@@ -1,0 +1,305 @@
+"""Per-KV protection of block entries:
+table/block_based/block.cc:1091-1222 Block::Initialize{Data,Index,MetaIndex}
+BlockProtectionInfo, block.h:271-274 GenerateKVChecksum, block.h:567-574
+PerKVChecksumCorruptionError.
+
+Blocks come from the BlockBuilder restatement in tests/sst_format.py (the
+reference's block.cc cannot be built here: it needs util/comparator.cc and
+db/dbformat.cc, which pull in the options/Customizable framework and the
+arena -- so the entry layout is "parity unpinned", as for the SST files).
+Each block's expected kv_checksum array is computed two ways: entry by entry
+from the writer's (key, value) list with ProtectKV (oracle, pinned to the
+reference's db/kv_checksum.h through oracle/_ref), and by the oracle's walk
+of the encoded block; the GPU must match both byte for byte.
+"""
+import random
+import struct
+
+import pytest
+
+from sst_format import build_block, common_prefix, handle, varint, varsigned
+
+DATA, INDEX, INDEX_DELTA, INDEX_DELTA_FK, META = 0, 1, 2, 3, 4
+OK, BAD_CONTENTS, BAD_ENTRY, BAD_RESTARTS = 0, 1, 2, 3
+
+
+def sorted_keys(rnd, n, klo=8, khi=40, prefix=b"", internal=True):
+    """n distinct sorted keys sharing prefixes (user key [+ 8-byte seq/type
+    footer, as internal keys in data blocks])."""
+    ks = set()
+    while len(ks) < n:
+        k = prefix + b"k%06d" % rnd.randrange(10 * n + 10)
+        k += bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(max(0, klo - len(k)), max(1, khi - len(k)))))
+        ks.add(k)
+    out = sorted(ks)
+    if internal:
+        out = [k + struct.pack("<Q", (rnd.getrandbits(56) << 8) | rnd.randrange(2)) for k in out]
+    return out
+
+
+def data_block(rnd, n, ri, vlo=0, vhi=300, **kw):
+    keys = sorted_keys(rnd, n, **kw)
+    entries = [(k, bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(vlo, vhi + 1)))) for k in keys]
+    return entries
+
+
+def raw_kvs(entries, ri, deltas=None):
+    """(key, raw value) per entry as the iterator sees them (block_builder.cc
+    :188-252: delta value only when shared != 0)."""
+    out, last = [], b""
+    for i, (k, v) in enumerate(entries):
+        shared = 0 if i % ri == 0 else common_prefix(last, k)
+        raw = v if deltas is None or shared == 0 else deltas[i]
+        out.append((k, raw))
+        last = k
+    return out
+
+
+def index_entries(rnd, n, first_key):
+    keys = sorted_keys(rnd, n, 6, 30, internal=False)
+    handles, off = [], rnd.randrange(1 << 20)
+    for _ in range(n):
+        sz = rnd.randrange(100, 70000)
+        handles.append((off, sz))
+        off += sz + 5
+    entries, deltas, prev = [], [], None
+    for i, (k, h) in enumerate(zip(keys, handles)):
+        v = handle(*h)
+        dv = varsigned(h[1] - prev[1]) if prev is not None else b""
+        if first_key:
+            fk = varint(len(k) + 3) + k + b"fk!"
+            v += fk
+            dv += fk
+        entries.append((k, v))
+        deltas.append(dv)
+        prev = h
+    return entries, deltas
+
+
+def expected(oracle, kvs, p):
+    out = bytearray()
+    for k, v in kvs:
+        out += struct.pack("<Q", oracle.KvProtect(0, k, v))[:p]
+    return bytes(out)
+
+
+def corpus(rnd):
+    """(kind, block bytes, expected kv_checksum or None, expected status)."""
+    cases = []
+    for ri in (1, 2, 3, 16, 64):
+        for n in (1, 5, 16, 17, 100):
+            e = data_block(rnd, n, ri)
+            cases.append((DATA, build_block(e, ri), raw_kvs(e, ri), OK))
+    # > 64 restart intervals (lane chunk loop), long keys / values (XXPH3 long path)
+    e = data_block(rnd, 300, 2, 0, 40)
+    cases.append((DATA, build_block(e, 2), raw_kvs(e, 2), OK))
+    e = data_block(rnd, 20, 4, 200, 3000, klo=100, khi=400)
+    cases.append((DATA, build_block(e, 4), raw_kvs(e, 4), OK))
+    # hash-index footers (kDataBlockBinaryAndHash)
+    for nb in (1, 7, 200):
+        e = data_block(rnd, 40, 8)
+        cases.append((DATA, build_block(e, 8, hash_buckets=nb), raw_kvs(e, 8), OK))
+    # meta index / properties (MetaBlockIter: restart interval 1, no sharing)
+    e = sorted((b"rocksdb.%s" % bytes(rnd.choice(b"abcdefgh") for _ in range(rnd.randrange(3, 30))),
+                bytes(rnd.getrandbits(8) for _ in range(rnd.randrange(0, 20)))) for _ in range(12))
+    e = list(dict(e).items())
+    cases.append((META, build_block(e, 1), raw_kvs(e, 1), OK))
+    # index blocks: value_is_full, delta-encoded, delta + first key
+    for ri in (1, 4, 16):
+        e, d = index_entries(rnd, 50, False)
+        cases.append((INDEX, build_block(e, ri), raw_kvs(e, ri), OK))
+        cases.append((INDEX_DELTA, build_block(e, ri, d), raw_kvs(e, ri, d), OK))
+        e, d = index_entries(rnd, 50, True)
+        cases.append((INDEX_DELTA_FK, build_block(e, ri, d), raw_kvs(e, ri, d), OK))
+    # empty blocks: BlockBuilder's (one restart at 0), and num_restarts == 0
+    cases.append((DATA, build_block([], 16), [], OK))
+    cases.append((DATA, struct.pack("<I", 0), [], OK))
+    # constructor error markers
+    cases.append((DATA, b"\x01\x00", None, BAD_CONTENTS))                      # < 4 bytes
+    cases.append((DATA, struct.pack("<I", 5), None, BAD_CONTENTS))           # restarts wrap
+    good = build_block(data_block(rnd, 30, 4), 4)
+    cases.append((DATA, good[:-4] + struct.pack("<I", 10 ** 6), None, BAD_CONTENTS))
+    # bad entries: truncated varint, value running into the restart array
+    e = data_block(rnd, 10, 4)
+    b = bytearray(build_block(e, 4))
+    b[2] = 0xFF  # value length of entry 0 now points past the entry area
+    cases.append((DATA, bytes(b), None, BAD_ENTRY))
+    b = bytearray(build_block(e, 4))
+    b[0] = 0x80  # shared varint continues: decodes garbage
+    cases.append((DATA, bytes(b), None, None))
+    b = bytearray(build_block(e, 4))
+    b[0] = 3  # shared != 0 on the block's first entry
+    cases.append((DATA, bytes(b), None, BAD_ENTRY))
+    # restart layouts BlockBuilder never writes
+    e = data_block(rnd, 12, 4)
+    blk = build_block(e, 4)
+    nr = struct.unpack_from("<I", blk, len(blk) - 4)[0]
+    ro = len(blk) - 4 - 4 * nr
+    r = list(struct.unpack_from("<%dI" % nr, blk, ro))
+    r2 = [r[0], r[2], r[1]]
+    cases.append((DATA, blk[:ro] + struct.pack("<3I", *r2) + blk[-4:], None, BAD_RESTARTS))
+    r2 = [r[0], r[1] + 1, r[2]]  # restart inside an entry
+    cases.append((DATA, blk[:ro] + struct.pack("<3I", *r2) + blk[-4:], None, BAD_RESTARTS))
+    e2 = data_block(rnd, 7, 3)
+    # hand-made block: restarts at entries 0, 2, 5 of a 7-entry run (2, 3, 2)
+    body, restarts, last = bytearray(), [], b""
+    for i, (k, v) in enumerate(e2):
+        if i in (0, 2, 5):
+            restarts.append(len(body))
+            sh = 0
+        else:
+            sh = common_prefix(last, k)
+        body += varint(sh) + varint(len(k) - sh) + varint(len(v)) + k[sh:] + v
+        last = k
+    blk = bytes(body) + struct.pack("<%dI" % len(restarts), *restarts) + struct.pack("<I", len(restarts))
+    cases.append((DATA, blk, None, BAD_RESTARTS))
+    return cases
+
+
+def test_oracle_block_protection(oracle):
+    """The oracle's block walk equals ProtectKV over the writer's entries."""
+    rnd = random.Random(7)
+    for kind, blk, kvs, st in corpus(rnd):
+        for p in (1, 8):
+            got_st, got, _ = oracle.BlockKvProtect(kind, blk, p)
+            if st is not None:
+                assert got_st == st, (kind, len(blk), st, got_st)
+            if kvs is not None:
+                assert got == expected(oracle, kvs, p)
+
+
+def test_oracle_restart_interval(oracle):
+    rnd = random.Random(3)
+    for ri, n in ((16, 40), (1, 5), (7, 7), (5, 3)):
+        e = data_block(rnd, n, ri)
+        st, _, got = oracle.BlockKvProtect(DATA, build_block(e, ri), 4)
+        assert st == OK
+        # GetRestartInterval (block.h:484-497): 0 with a single restart
+        assert got == (0 if (n + ri - 1) // ri <= 1 else ri)
+
+
+def test_ref_pins_protect_kv(oracle, ref):
+    """The per-entry function is the reference's own ProtectKV (_ref build of
+    db/kv_checksum.h)."""
+    if ref is None:
+        pytest.skip("oracle/_ref not built")
+    rnd = random.Random(11)
+    for kind, blk, kvs, st in corpus(rnd)[:40]:
+        for k, v in (kvs or []):
+            assert oracle.KvProtect(0, k, v) == ref.ref_kv_protect(0, k, len(k), v, len(v), 0, 0)
+
+
+# ---------------------------------------------------------------------------
+# GPU parity
+# ---------------------------------------------------------------------------
+
+
+def _pack(torch, blocks, rnd, align_any=True):
+    """Blocks at byte offsets in one device buffer (odd offsets: blocks sit
+    after 5-byte trailers in an SST)."""
+    offs, buf = [], bytearray()
+    for b in blocks:
+        buf += bytes(rnd.randrange(0, 7) if align_any else 0)
+        offs.append(len(buf))
+        buf += b
+    buf += bytes(64)
+    dev = torch.frombuffer(bytearray(buf), dtype=torch.uint8).to("cuda")
+    return dev, torch.tensor(offs, dtype=torch.int64, device="cuda"), \
+        torch.tensor([len(b) for b in blocks], dtype=torch.int32, device="cuda")
+
+
+@pytest.mark.gpu
+def test_block_protection_gpu_vs_oracle(gpu, oracle):
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    rnd = random.Random(21)
+    cases = corpus(rnd)
+    for kind in (DATA, INDEX, INDEX_DELTA, INDEX_DELTA_FK, META):
+        sel = [c for c in cases if c[0] == kind or (kind == DATA and c[0] not in (INDEX, INDEX_DELTA,
+                                                                                   INDEX_DELTA_FK, META))]
+        blocks = [c[1] for c in sel]
+        base, offs, lens = _pack(torch, blocks, rnd)
+        spans = speedb_amd.Spans(base, len(blocks), offs, lens)
+        for p in (1, 2, 4, 8):
+            prot = B.InitializeBlockProtectionInfo(kind, spans, p)
+            torch.cuda.synchronize()
+            kb = prot.key_base.cpu().tolist()
+            sts = prot.status.cpu().tolist()
+            ris = prot.restart_interval.cpu().tolist()
+            allck = prot.kv_checksum.cpu().numpy().tobytes()
+            for i, blk in enumerate(blocks):
+                ost, ock, ori = oracle.BlockKvProtect(kind, blk, p)
+                assert sts[i] == ost, (kind, i, sts[i], ost)
+                assert allck[kb[i] * p:kb[i + 1] * p] == ock, (kind, i)
+                assert ris[i] == ori, (kind, i)
+
+
+@pytest.mark.gpu
+def test_block_protection_verify_flags_exact_entries(gpu, oracle):
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    rnd = random.Random(5)
+    blocks = [build_block(data_block(rnd, rnd.randrange(1, 60), rnd.choice((1, 4, 16))), 16) for _ in range(300)]
+    base, offs, lens = _pack(torch, blocks, rnd)
+    spans = speedb_amd.Spans(base, len(blocks), offs, lens)
+    prot = B.InitializeDataBlockProtectionInfo(spans, 2)
+    mism, cnt = B.VerifyBlockProtectionInfo(spans, prot)
+    assert int(cnt.item()) == 0 and int(mism.sum().item()) == 0
+    stored = prot.kv_checksum.clone()
+    bad = sorted(rnd.sample(range(prot.total_keys), 25))
+    for k in bad:
+        stored[2 * k + rnd.randrange(2)] ^= 1 << rnd.randrange(8)
+    mism, cnt = B.VerifyBlockProtectionInfo(spans, prot, stored)
+    assert int(cnt.item()) == len(bad)
+    assert torch.nonzero(mism).flatten().cpu().tolist() == bad
+    st = B.PerKVChecksumStatus(prot, mism)
+    assert st and st[0][1].IsCorruption() and "per key-value checksum verification failed" in st[0][1].message
+
+
+@pytest.mark.gpu
+def test_block_protection_many_blocks_property(gpu, oracle):
+    """> 2048 blocks (multi-tile scans): 64 distinct blocks tiled 80 times --
+    every copy's checksums equal its original's (the oracle's)."""
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    rnd = random.Random(9)
+    uniq = [build_block(data_block(rnd, rnd.randrange(20, 45), 8, 50, 120), 16) for _ in range(64)]
+    want = [oracle.BlockKvProtect(DATA, b, 4)[1] for b in uniq]
+    blocks = uniq * 80
+    base, offs, lens = _pack(torch, blocks, rnd)
+    spans = speedb_amd.Spans(base, len(blocks), offs, lens)
+    prot = B.InitializeDataBlockProtectionInfo(spans, 4)
+    kb = prot.key_base.cpu().tolist()
+    ck = prot.kv_checksum.cpu().numpy().tobytes()
+    assert prot.total_keys == sum(len(w) // 4 for w in want) * 80
+    for i in range(len(blocks)):
+        assert ck[kb[i] * 4:kb[i + 1] * 4] == want[i % 64]
+
+
+@pytest.mark.gpu
+def test_block_protection_empty_and_all_bad(gpu):
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    base = torch.zeros(64, dtype=torch.uint8, device="cuda")
+    prot = B.InitializeDataBlockProtectionInfo(speedb_amd.Spans(base, 0), 8)
+    assert prot.total_keys == 0
+    offs = torch.tensor([0, 8], dtype=torch.int64, device="cuda")
+    lens = torch.tensor([2, 3], dtype=torch.int32, device="cuda")
+    prot = B.InitializeDataBlockProtectionInfo(speedb_amd.Spans(base, 2, offs, lens), 8)
+    assert prot.total_keys == 0 and prot.status.cpu().tolist() == [BAD_CONTENTS, BAD_CONTENTS]
+    assert not prot.block_status(0).ok() and prot.block_status(0).message == "bad block contents"
+
+
+def test_block_protection_abi_errors():
+    """Argument checks need no GPU."""
+    from speedb_amd._lib import lib, mck_spans
+    import ctypes
+    s = mck_spans(None, None, None, 0, 0, 0)
+    assert lib.mck_block_kv_protect_batch(0, ctypes.byref(s), 3, None, None, 0, None, None, None) == -1
+    assert lib.mck_block_kv_protect_batch(9, ctypes.byref(s), 4, None, None, 0, None, None, None) == -1
+    assert lib.mck_block_kv_scratch_bytes(5000) >= 16 * 3
+    assert lib.mck_block_kv_work_bytes(10, 100) >= 10 * 24 + 100
