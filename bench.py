@@ -40,6 +40,11 @@ Default workload (the headline, BASELINE.json configs[1]): CRC32C over
                        offset: mck_wal_record_crc_batch
   ragged   (8a a1)     crc32c_batch over ragged spans of --span-min..--span-max
                        bytes (explicit offsets/lengths), 1 GiB per GPU
+  blockkv  (8f row 4)  Block::InitializeDataBlockProtectionInfo of 1M
+                       uncompressed ~4 KiB data blocks (README 16 B user keys
+                       as internal keys, 1000 B values; --kv-value-bytes),
+                       protection_bytes_per_key 8: layout + key reassembly
+                       + ProtectKV of every entry, one batch per step
   shim     (8b)        latency of one synchronous scalar shim call
                        (mck_crc32c_value_r: H2D + launch + D2H) at 64 B,
                        4 KiB, 32 KiB, 1 MiB vs the reference's crc32c::Value
@@ -90,7 +95,7 @@ def parse():
     # 0.77 -> 0.90 -> 0.76 ms per launch at 1M x 4 KiB): run the workload
     # untimed for this long before the warmup steps, whatever W is
     p.add_argument("--settle-ms", type=float, default=250.0)
-    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file", "walwrite", "blob", "shim",
+    p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file", "walwrite", "blob", "shim", "blockkv",
                             "walrec", "ragged"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
@@ -105,6 +110,8 @@ def parse():
     p.add_argument("--wal-records", type=int, default=2 << 20, help="logical records per GPU (walwrite)")
     p.add_argument("--blob-records", type=int, default=1 << 20, help="blob records per GPU (blob)")
     p.add_argument("--kvs", type=int, default=1 << 22, help="KVs per GPU (kv)")
+    p.add_argument("--kv-value-bytes", type=int, default=1000, help="value bytes (blockkv)")
+    p.add_argument("--kv-prot-bytes", type=int, default=8, help="protection_bytes_per_key (blockkv)")
     p.add_argument("--span-min", type=int, default=100, help="smallest span (walrec, ragged)")
     p.add_argument("--span-max", type=int, default=1100, help="largest span (walrec, ragged)")
     p.add_argument("--span-bytes", type=int, default=1 << 30, help="span bytes per GPU (walrec, ragged)")
@@ -525,6 +532,67 @@ def make_workload(args, dev, rank, world):
                 ok &= int(res[i]) == want
             return ok
         w.check = check
+    elif args.workload == "blockkv":
+        from speedb_amd import _lib
+        L = _lib.lib
+        db = W.DataBlocks(args.blocks, dev, value_bytes=args.kv_value_bytes, seed=30 + rank)
+        n, pb = db.count, args.kv_prot_bytes
+        kbase = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        abase = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        status = torch.empty(n, dtype=torch.int32, device=dev)
+        rint = torch.empty(n, dtype=torch.int32, device=dev)
+        scratch = torch.empty(int(L.mck_block_kv_scratch_bytes(n)), dtype=torch.uint8, device=dev)
+        nkeys = int(db.keys_per_block.sum())
+        kbytes = sum(len(k) for e in db.entries for k, _ in e) * (n // db.distinct) + sum(
+            len(k) for e in db.entries[:n % db.distinct] for k, _ in e)
+        work = torch.empty(int(L.mck_block_kv_work_bytes(nkeys, kbytes)), dtype=torch.uint8, device=dev)
+        out = torch.empty(nkeys * pb, dtype=torch.uint8, device=dev)
+        tot = torch.empty(2, dtype=torch.int64, pin_memory=True)
+        sp = db.spans.c()
+
+        def step():
+            _lib.check(L.mck_block_kv_layout_batch(0, ctypes.byref(sp), kbase.data_ptr(), abase.data_ptr(),
+                                                   rint.data_ptr(),
+                                                   status.data_ptr(), scratch.data_ptr(), stream.cuda_stream),
+                       "mck_block_kv_layout_batch")
+            # the totals size the work area: one 16-byte readback per batch
+            tot[0].copy_(kbase[n], non_blocking=True)
+            tot[1].copy_(abase[n], non_blocking=True)
+            stream.synchronize()
+            assert int(tot[0]) == nkeys and int(tot[1]) == kbytes
+            _lib.check(L.mck_block_kv_protect_batch(0, ctypes.byref(sp), pb, kbase.data_ptr(), abase.data_ptr(),
+                                                    rint.data_ptr(), nkeys, work.data_ptr(), out.data_ptr(), stream.cuda_stream),
+                       "mck_block_kv_protect_batch")
+        w.step = step
+        w.kernel = "k_block_layout + scans + k_block_kv (whole step, incl. the totals readback)"
+        w.span_bytes = db.block_bytes
+        # what the step must move: every block read once, the kv_checksum
+        # array written (+ 8 B offset, 4 B length per block in, 8 B key base
+        # + 4 B status out)
+        w.alg_bytes = db.block_bytes + nkeys * pb + n * (8 + 4 + 8 + 4)
+        w.kern_from_wall = True
+        w.desc = (f"per-KV protection of {n} uncompressed data blocks per GPU (~4 KiB, BlockBuilder layout, "
+                  f"restart interval 16, {len(db.entries[0][0][0])} B internal keys, {args.kv_value_bytes} B "
+                  f"values, {nkeys} entries), protection_bytes_per_key {pb}: "
+                  "Block::InitializeDataBlockProtectionInfo (SURVEY.md 8f row 4)")
+        w.cfg = {"blocks_per_gpu": n, "entries": nkeys, "value_bytes": args.kv_value_bytes, "prot_bytes": pb}
+
+        def check():
+            # sampled entries == ProtectKV composed from scalar NPHash64 calls
+            # (the engine's scalar path, a different kernel)
+            import random
+            kb = kbase.cpu().numpy()
+            ck = out.cpu().numpy()
+            ok = bool((status == 0).all().item())
+            for i in random.Random(rank).sample(range(n), 8):
+                ents = db.entries[i % db.distinct]
+                for e in sorted({0, 1, 2, len(ents) - 2, len(ents) - 1} & set(range(len(ents)))):
+                    k, v = ents[e]
+                    want = S.NPHash64(k, 0) ^ S.NPHash64(v, 0xD28AAD72F49BD50B)
+                    got = ck[(kb[i] + e) * pb:(kb[i] + e + 1) * pb].tobytes()
+                    ok &= got == (want & (2 ** (8 * pb) - 1)).to_bytes(pb, "little")
+            return ok
+        w.check = check
     else:  # host
         from speedb_amd import _lib
         # configs[4]: the 80M-key / 1 KB-value compaction stream cut into
@@ -665,6 +733,8 @@ def main():
     torch.cuda.synchronize(dev)
     wall = shard.reduce_max(time.perf_counter() - t0, dev)
     kern_ms = ev0.elapsed_time(ev1) / (args.steps * w.launches) / getattr(w, "kern_scale", 1.0)
+    if getattr(w, "kern_from_wall", False):  # a step with a host sync inside: the step is the unit
+        kern_ms = wall / args.steps * 1e3
 
     verified = None if args.no_verify else w.check()
     if verified is False:

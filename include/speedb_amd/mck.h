@@ -473,7 +473,7 @@ uint64_t mck_block_kv_scratch_bytes(uint32_t count);
 /* Pass 1 (device): every block's entry count and reassembled key bytes,
  * as exclusive scans: key_base[count + 1] (key_base[count] = total keys),
  * arena_base[count + 1] (total key bytes at [count]); status[count];
- * restart_interval[count] (optional: GetRestartInterval, block.h:484).
+ * restart_interval[count] (GetRestartInterval, block.h:484; pass 2 reads it).
  * The caller reads key_base[count] and arena_base[count] back to size the
  * work area and the output. */
 int mck_block_kv_layout_batch(int kind, const mck_spans* blocks,
@@ -488,8 +488,10 @@ uint64_t mck_block_kv_work_bytes(uint64_t total_keys, uint64_t total_key_bytes);
  * (block_protection_bytes_per_key). */
 int mck_block_kv_protect_batch(int kind, const mck_spans* blocks,
                                uint32_t prot_bytes, const uint64_t* key_base,
-                               const uint64_t* arena_base, uint64_t total_keys,
-                               void* work, uint8_t* out, mck_stream_t stream);
+                               const uint64_t* arena_base,
+                               const uint32_t* restart_interval,
+                               uint64_t total_keys, void* work, uint8_t* out,
+                               mck_stream_t stream);
 
 /* Read side: the per-entry check DataBlockIter / IndexBlockIter /
  * MetaBlockIter run on every key they parse (block.h:567-574
@@ -498,8 +500,10 @@ int mck_block_kv_protect_batch(int kind, const mck_spans* blocks,
  * `out` above); mismatch_count (optional, caller-zeroed) counts them. */
 int mck_block_kv_verify_batch(int kind, const mck_spans* blocks,
                               uint32_t prot_bytes, const uint64_t* key_base,
-                              const uint64_t* arena_base, uint64_t total_keys,
-                              void* work, const uint8_t* stored,
+                              const uint64_t* arena_base,
+                              const uint32_t* restart_interval,
+                              uint64_t total_keys, void* work,
+                              const uint8_t* stored,
                               uint8_t* mismatch, uint32_t* mismatch_count,
                               mck_stream_t stream);
 

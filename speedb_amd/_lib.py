@@ -100,9 +100,9 @@ SIGNATURES = [
      [ctypes.c_int, ctypes.POINTER(mck_spans), vp, vp, vp, vp, vp, vp]),
     ("mck_block_kv_work_bytes", ctypes.c_uint64, [ctypes.c_uint64, ctypes.c_uint64]),
     ("mck_block_kv_protect_batch", ctypes.c_int,
-     [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, vp, vp, ctypes.c_uint64, vp, vp, vp]),
+     [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, vp, vp, vp, ctypes.c_uint64, vp, vp, vp]),
     ("mck_block_kv_verify_batch", ctypes.c_int,
-     [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, vp, vp, ctypes.c_uint64, vp, vp, vp,
+     [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, vp, vp, vp, ctypes.c_uint64, vp, vp, vp,
       vp, vp]),
     ("mck_sst_decode_footer", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
     ("mck_sst_list_blocks", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),

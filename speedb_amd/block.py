@@ -102,7 +102,8 @@ def InitializeBlockProtectionInfo(kind: int, blocks: Spans, protection_bytes_per
     out = torch.empty(max(nk * protection_bytes_per_key, 1), dtype=torch.uint8, device=blocks.base.device)
     s = blocks.c()
     check(lib.mck_block_kv_protect_batch(int(kind), ctypes.byref(s), protection_bytes_per_key,
-                                         key_base.data_ptr(), arena_base.data_ptr(), nk, work.data_ptr(),
+                                         key_base.data_ptr(), arena_base.data_ptr(), interval.data_ptr(), nk,
+                                         work.data_ptr(),
                                          out.data_ptr(), _stream(stream)), "mck_block_kv_protect_batch")
     return BlockProtection(BlockKind(kind), protection_bytes_per_key, key_base, arena_base, status, interval,
                            nk, nkb, work, out[:nk * protection_bytes_per_key])
@@ -139,7 +140,8 @@ def VerifyBlockProtectionInfo(blocks: Spans, prot: BlockProtection, stored=None,
     count = torch.zeros(1, dtype=torch.int32, device=dev)
     s = blocks.c()
     check(lib.mck_block_kv_verify_batch(int(prot.kind), ctypes.byref(s), prot.protection_bytes_per_key,
-                                        prot.key_base.data_ptr(), prot.arena_base.data_ptr(), prot.total_keys,
+                                        prot.key_base.data_ptr(), prot.arena_base.data_ptr(),
+                                        prot.restart_interval.data_ptr(), prot.total_keys,
                                         prot.work.data_ptr(), stored.data_ptr(), mismatch.data_ptr(),
                                         count.data_ptr(), _stream(stream)), "mck_block_kv_verify_batch")
     return mismatch[:prot.total_keys], count

@@ -5,23 +5,29 @@
 // A block is prefix-compressed: an entry's key is the previous key's first
 // `shared` bytes plus its own `non_shared` bytes, and only restart points
 // (every block_restart_interval-th entry, shared == 0) start from nothing.
-// The restart array therefore cuts a block into independent intervals, and
-// the device walks them in parallel: one wave per block, lane r per restart
-// interval r (r += 64 for blocks with more intervals).  Three passes:
+// The restart array therefore cuts a block into independent intervals.
+// One wave per block, the block staged in LDS (blocks up to kBlkSlot bytes;
+// larger ones are read in place), two passes:
 //
-//   k_block_layout       walk every interval: entry count, reassembled key
-//                        bytes, first error; per block the key count and
-//                        key bytes (-> exclusive scans, k_blk_scan_*)
-//   k_block_materialize  walk again, reassembling each key into a key arena
-//                        and writing per-entry key/value spans
-//   k_xph3<OpKvProtect>  ProtectKV(key, value).Encode(prot_bytes) per entry
-//                        on the XXPH3 row driver (the batched KV kernel)
+//   k_block_layout  lane r walks restart interval r (r += 64): entry count,
+//                   reassembled key bytes, first error; per block the key
+//                   count, key bytes, restart interval and status; the
+//                   exclusive scans (k_blk_scan_*) give each block its key
+//                   index base and key-arena base
+//   k_block_kv      lane r walks interval r again, reassembling every key
+//                   into the wave's LDS key area and writing an entry
+//                   descriptor; then lane e hashes entry e:
+//                   ProtectKV(key, value).Encode(prot_bytes), values over
+//                   240 B by the whole wave (XXPH3 long loop, 8 accumulators
+//                   x 8 stripe groups)
 //
 // Entry k of a block lands at key index key_base[block] + k, in the order the
 // reference's SeekToFirst/Next loop generates them (:1116-1123).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 namespace mck {
 
@@ -38,95 +44,120 @@ __device__ __forceinline__ uint32_t blk_u32(const uint8_t* p) {
   return *reinterpret_cast<gbl_u32u_t*>(reinterpret_cast<uint64_t>(p));
 }
 
-// util/coding.h GetVarint32Ptr (max_shift 28) / GetVarint64Ptr (63): nullptr
-// when the varint runs past lim or past its length.
-__device__ __forceinline__ const uint8_t* blk_varint(const uint8_t* p, const uint8_t* lim, int max_shift,
-                                                     uint64_t* v) {
-  uint64_t r = 0;
-  for (int shift = 0; shift <= max_shift && p < lim; shift += 7) {
-    const uint64_t b = blk_u8(p++);
-    r |= (b & 127) << shift;
-    if (!(b & 128)) {
-      *v = r;
-      return p;
-    }
-  }
-  return nullptr;
-}
-
 // block.cc:994-1083 NumRestarts / IndexType / Block::Block: restart array
 // offset `ro` and restart count `nr`; ok = false is the constructor's error
-// marker (size_ = 0) or NewDataIterator's "bad block contents".
+// marker (size_ = 0) or NewDataIterator's "bad block contents" (rd_header).
 struct BlkHdr {
   uint32_t ro, nr;
   bool ok;
 };
-__device__ __forceinline__ BlkHdr blk_header(const uint8_t* d, uint64_t n64) {
-  BlkHdr h{0, 0, false};
-  if (n64 < 4 || n64 > 0xFFFFFFFFull) return h;
-  const uint32_t size = (uint32_t)n64;
-  const uint32_t footer = blk_u32(d + size - 4);
-  bool hash = false;
-  uint32_t nr = footer;
-  if (size <= (1u << 16)) {  // kMaxBlockSizeSupportedByHashIndex
-    hash = footer >> 31;
-    nr = footer & 0x7FFFFFFFu;
+// ---- byte readers: a block (or key area) staged in LDS, or in global memory
+// Offsets are relative to the block's first byte.  The LDS slot holds the
+// 16-byte-aligned global chunks covering the block; `head` = the block's
+// offset in its first chunk.  Unaligned dword/qword reads are assembled from
+// aligned LDS dwords with v_alignbyte (the slot is padded past its end).
+struct LdsRd {
+  const uint32_t* w;
+  uint32_t head;
+  __device__ __forceinline__ uint32_t u8(uint32_t o) const {
+    const uint32_t i = head + o;
+    return (w[i >> 2] >> (8 * (i & 3))) & 255u;
   }
-  h.nr = nr;
-  if (!hash) {
-    const uint32_t ro = size - (1 + nr) * 4u;
-    if (ro > size - 4u) return h;
-    h.ro = ro;
-  } else {
-    if (size < 6) return h;
-    // data_block_hash_index.cc:76-84: NUM_BUCK (u16) before the footer
-    const uint16_t sz16 = (uint16_t)(size - 4);
-    const uint16_t nb = (uint16_t)(blk_u8(d + sz16 - 2) | (blk_u8(d + sz16 - 1) << 8));
-    const uint16_t map_offset = (uint16_t)(sz16 - 2 - nb);
-    const uint32_t ro = (uint32_t)map_offset - nr * 4u;
-    if (ro > map_offset) return h;
-    h.ro = ro;
+  __device__ __forceinline__ uint32_t u32(uint32_t o) const {
+    const uint32_t i = head + o, s = 8 * (i & 3), k = i >> 2;
+    return (uint32_t)((((uint64_t)w[k + 1] << 32) | w[k]) >> s);
   }
-  // NewDataIterator (:1244): a block shorter than 8 bytes with restarts
-  h.ok = nr == 0 || size >= 8;
-  return h;
+  __device__ __forceinline__ uint64_t u64(uint32_t o) const {
+    const uint32_t i = head + o, s = 8 * (i & 3), k = i >> 2;
+    const uint32_t w0 = w[k], w1 = w[k + 1], w2 = w[k + 2];
+    const uint32_t lo = (uint32_t)((((uint64_t)w1 << 32) | w0) >> s);
+    const uint32_t hi = (uint32_t)((((uint64_t)w2 << 32) | w1) >> s);
+    return ((uint64_t)hi << 32) | lo;
+  }
+};
+struct GblRd {
+  const uint8_t* p;
+  __device__ __forceinline__ uint32_t u8(uint32_t o) const { return blk_u8(p + o); }
+  __device__ __forceinline__ uint32_t u32(uint32_t o) const { return blk_u32(p + o); }
+  __device__ __forceinline__ uint64_t u64(uint32_t o) const {
+    return *reinterpret_cast<gbl_u64u_t*>(reinterpret_cast<uint64_t>(p + o));
+  }
+};
+
+template <class R>
+__device__ __forceinline__ uint64_t rd_varint(const R& r, uint32_t& p, uint32_t lim, int max_shift, bool& ok) {
+  uint64_t x = 0;
+  for (int shift = 0; shift <= max_shift; shift += 7) {
+    if (p >= lim) break;
+    const uint64_t b = r.u8(p++);
+    x |= (b & 127) << shift;
+    if (!(b & 128)) return x;
+  }
+  ok = false;
+  return 0;
 }
 
-// One entry at p: DecodeEntry (:37-64) / CheckAndDecodeEntry (:68-97) with
-// the bounds CheckAndDecodeEntry checks; index blocks with delta-encoded
-// values: DecodeEntryV4 (:110-139) and the value's encoded length from
-// IndexValue::DecodeFrom (table/format.cc:137-162: delta size when shared != 0,
-// else a BlockHandle; then the length-prefixed first key).  Returns the key
-// delta's start or nullptr ("bad entry in block").
-template <int KIND>
-__device__ __forceinline__ const uint8_t* blk_entry(const uint8_t* p, const uint8_t* lim, uint32_t* sh,
-                                                    uint32_t* ns, const uint8_t** val, uint32_t* vl) {
-  if (lim - p < 3) return nullptr;
-  uint64_t s, k, x;
-  if ((p = blk_varint(p, lim, 28, &s)) == nullptr) return nullptr;
-  if ((p = blk_varint(p, lim, 28, &k)) == nullptr) return nullptr;
+// One entry at offset p (offsets relative to the block): DecodeEntry
+// (:37-64) / CheckAndDecodeEntry (:68-97) with the bounds CheckAndDecodeEntry
+// checks; index blocks with delta-encoded values: DecodeEntryV4 (:110-139) and
+// the value's encoded length from IndexValue::DecodeFrom (table/format.cc
+// :137-162: delta size when shared != 0, else a BlockHandle; then the
+// length-prefixed first key).  Returns false for "bad entry in block";
+// q = key delta, v = value.
+template <int KIND, class R>
+__device__ __forceinline__ bool rd_entry(const R& r, uint32_t p, uint32_t lim, uint32_t* sh, uint32_t* ns,
+                                         uint32_t* q, uint32_t* v, uint32_t* vl) {
+  if (p > lim || lim - p < 3) return false;
+  bool ok = true;
+  const uint64_t s = rd_varint(r, p, lim, 28, ok);
+  const uint64_t k = ok ? rd_varint(r, p, lim, 28, ok) : 0;
+  if (!ok) return false;
   if (KIND == kBlkIndexDelta || KIND == kBlkIndexDeltaFk) {
-    if ((uint64_t)(lim - p) < k) return nullptr;
-    const uint8_t* v = p + k;
-    const uint8_t* q = blk_varint(v, lim, 63, &x);
-    if (q && s == 0) q = blk_varint(q, lim, 63, &x);
-    if (KIND == kBlkIndexDeltaFk && q) {
-      q = blk_varint(q, lim, 28, &x);
-      if (q && (uint64_t)(lim - q) < x) q = nullptr;
-      if (q) q += x;
+    if ((uint64_t)(lim - p) < k) return false;
+    const uint32_t v0 = p + (uint32_t)k;
+    uint32_t c = v0;
+    (void)rd_varint(r, c, lim, 63, ok);             // delta size, or the handle's offset
+    if (ok && s == 0) (void)rd_varint(r, c, lim, 63, ok);  // the handle's size
+    if (KIND == kBlkIndexDeltaFk && ok) {
+      const uint64_t fk = rd_varint(r, c, lim, 28, ok);
+      ok = ok && (uint64_t)(lim - c) >= fk;
+      c += ok ? (uint32_t)fk : 0u;
     }
-    if (!q) return nullptr;
-    *val = v;
-    *vl = (uint32_t)(q - v);
+    if (!ok) return false;
+    *v = v0;
+    *vl = c - v0;
   } else {
-    if ((p = blk_varint(p, lim, 28, &x)) == nullptr) return nullptr;
-    if ((uint64_t)(lim - p) < k + x) return nullptr;
-    *val = p + k;
+    const uint64_t x = rd_varint(r, p, lim, 28, ok);
+    if (!ok || (uint64_t)(lim - p) < k + x) return false;
+    *v = p + (uint32_t)k;
     *vl = (uint32_t)x;
   }
   *sh = (uint32_t)s;
   *ns = (uint32_t)k;
-  return p;
+  *q = p;
+  return true;
+}
+
+// DecodeEntry's fast path (block.cc:45-50): shared, non_shared and
+// value_length each one byte (< 128) -- one dword read instead of three
+// varint walks; anything else goes through rd_entry.  The dword may reach
+// one byte past the entry area: the restart array follows it.
+template <int KIND, class R>
+__device__ __forceinline__ bool rd_entry_fast(const R& r, uint32_t p, uint32_t lim, uint32_t* sh, uint32_t* ns,
+                                              uint32_t* q, uint32_t* v, uint32_t* vl) {
+  if (p > lim || lim - p < 3) return false;
+  const uint32_t u = r.u32(p);
+  if (KIND != kBlkIndexDelta && KIND != kBlkIndexDeltaFk && (u & 0x808080u) == 0) {
+    const uint32_t k = (u >> 8) & 255u, x = (u >> 16) & 255u;
+    if (lim - (p + 3) < k + x) return false;
+    *sh = u & 255u;
+    *ns = k;
+    *q = p + 3;
+    *v = p + 3 + k;
+    *vl = x;
+    return true;
+  }
+  return rd_entry<KIND>(r, p, lim, sh, ns, q, v, vl);
 }
 
 // Walk of one restart interval [start, end): entry count, reassembled key
@@ -139,19 +170,13 @@ struct BlkWalk {
   uint64_t kbytes;
   uint64_t err;
 };
-template <int KIND>
-__device__ __forceinline__ BlkWalk blk_walk(const uint8_t* d, uint32_t ro, uint32_t r, uint32_t start,
-                                            uint32_t end) {
+template <int KIND, class R>
+__device__ __forceinline__ BlkWalk blk_walk(const R& rd, uint32_t ro, uint32_t r, uint32_t start, uint32_t end) {
   BlkWalk w{0, 0, ~0ull};
-  const uint8_t* lim = d + ro;
-  const uint8_t* p = d + start;
-  const uint8_t* e = d + end;
-  uint32_t kl = 0;
-  while (p < e) {
-    uint32_t sh, ns, vl;
-    const uint8_t* v;
-    const uint8_t* q = blk_entry<KIND>(p, lim, &sh, &ns, &v, &vl);
-    if (!q) {
+  uint32_t p = start, kl = 0;
+  while (p < end) {
+    uint32_t sh, ns, q, v, vl;
+    if (!rd_entry_fast<KIND>(rd, p, ro, &sh, &ns, &q, &v, &vl)) {
       w.err = (uint64_t)r << 2;
       return w;
     }
@@ -168,7 +193,7 @@ __device__ __forceinline__ BlkWalk blk_walk(const uint8_t* d, uint32_t ro, uint3
     w.cnt++;
     p = v + vl;
   }
-  if (p != e) w.err = ((uint64_t)r << 2) | 2u;
+  if (p != end) w.err = ((uint64_t)r << 2) | 2u;
   return w;
 }
 
@@ -192,130 +217,488 @@ __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v, uint32_t lane
   return v;
 }
 
-// Restart array as BlockBuilder writes it: restart[0] == 0 (when there are
-// entries), strictly increasing, inside the entry area.  Wave-uniform result.
-__device__ __forceinline__ bool blk_restarts_ok(const uint8_t* d, const BlkHdr& h, uint32_t lane) {
+// the wave's LDS writes visible to its other lanes
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LDS per wave: the staged block, and (k_block_kv) the reassembled keys and
+// the entry descriptors.  Blocks larger than the slot, or with more entries /
+// key bytes than the areas hold, take the same code over global memory
+// (the block in place, keys in the caller's arena, descriptors in the work
+// arrays).
+constexpr uint32_t kBlkSlot = 6144;                           // block bytes staged
+constexpr uint32_t kBlkSlotWords = (kBlkSlot + 16 + 16 + 16) / 4;  // + head, tail chunk, pad
+constexpr uint32_t kBlkKeyArea = 2048, kBlkKeyWords = (kBlkKeyArea + 16) / 4;
+constexpr uint32_t kBlkMaxDesc = 256;
+
+// Copy the block into the wave's slot; returns the LdsRd over it.
+__device__ __forceinline__ LdsRd blk_stage(const uint8_t* g, uint32_t n, uint32_t* slot, uint32_t lane) {
+  const uint64_t a = reinterpret_cast<uint64_t>(g);
+  const uint32_t head = (uint32_t)(a & 15), nch = (head + n + 15) >> 4;
+  const uint64_t g0 = a - head;
+  for (uint32_t i = lane; i < nch; i += 64) {
+    const uint4 v = span_load16<false>(g0 + 16ull * i);
+    slot[4 * i] = v.x;
+    slot[4 * i + 1] = v.y;
+    slot[4 * i + 2] = v.z;
+    slot[4 * i + 3] = v.w;
+  }
+  wave_lds_sync();
+  return LdsRd{slot, head};
+}
+
+// block.cc:994-1083 NumRestarts / IndexType / the Block constructor;
+// data_block_hash_index.cc:76-84 (NUM_BUCK u16 before the footer)
+template <class R>
+__device__ __forceinline__ BlkHdr rd_header(const R& r, uint64_t n64) {
+  BlkHdr h{0, 0, false};
+  if (n64 < 4 || n64 > 0xFFFFFFFFull) return h;
+  const uint32_t size = (uint32_t)n64;
+  const uint32_t footer = r.u32(size - 4);
+  bool hash = false;
+  uint32_t nr = footer;
+  if (size <= (1u << 16)) {
+    hash = footer >> 31;
+    nr = footer & 0x7FFFFFFFu;
+  }
+  h.nr = nr;
+  if (!hash) {
+    const uint32_t ro = size - (1 + nr) * 4u;
+    if (ro > size - 4u) return h;
+    h.ro = ro;
+  } else {
+    if (size < 6) return h;
+    const uint16_t sz16 = (uint16_t)(size - 4);
+    const uint16_t nb = (uint16_t)(r.u8(sz16 - 2) | (r.u8(sz16 - 1) << 8));
+    const uint16_t map_offset = (uint16_t)(sz16 - 2 - nb);
+    const uint32_t ro = (uint32_t)map_offset - nr * 4u;
+    if (ro > map_offset) return h;
+    h.ro = ro;
+  }
+  h.ok = nr == 0 || size >= 8;
+  return h;
+}
+
+template <class R>
+__device__ __forceinline__ bool rd_restarts_ok(const R& rd, const BlkHdr& h, uint32_t lane) {
   bool bad = false;
-  const uint8_t* ra = d + h.ro;
   for (uint32_t r = lane; r < h.nr; r += 64) {
-    const uint32_t x = blk_u32(ra + 4 * r);
+    const uint32_t x = rd.u32(h.ro + 4 * r);
     if (r == 0)
       bad |= h.ro != 0 && x != 0;
     else
-      bad |= x <= blk_u32(ra + 4 * (r - 1)) || x >= h.ro;
+      bad |= x <= rd.u32(h.ro + 4 * (r - 1)) || x >= h.ro;
   }
   return !__any(bad);
 }
 
-// Pass 1: per block key count / key bytes / status (+ restart interval).
+// Pass 1 body for one block
+template <int KIND, class R>
+__device__ __forceinline__ void blk_layout_one(const R& rd, uint64_t n, uint32_t lane, int* st_out, uint64_t* keys_out,
+                                               uint64_t* kb_out, uint32_t* ri_out) {
+  const BlkHdr h = rd_header(rd, n);
+  int st = kBlkOk;
+  uint64_t keys = 0, kb = 0;
+  uint32_t ri = 0;
+  if (!h.ok) {
+    st = kBlkBadContents;
+  } else if (h.nr == 0) {
+    // empty block: protection stays off, no keys
+  } else if (!rd_restarts_ok(rd, h, lane)) {
+    st = kBlkBadRestarts;
+  } else if (h.ro == 0) {
+    st = h.nr == 1 ? kBlkOk : kBlkBadRestarts;
+  } else {
+    uint64_t err = ~0ull;
+    uint32_t first_cnt = 0;
+    for (uint32_t r0 = 0; r0 < h.nr; r0 += 64) {
+      const uint32_t r = r0 + lane;
+      BlkWalk w{0, 0, ~0ull};
+      if (r < h.nr)
+        w = blk_walk<KIND>(rd, h.ro, r, rd.u32(h.ro + 4 * r), r + 1 < h.nr ? rd.u32(h.ro + 4 * (r + 1)) : h.ro);
+      if (r0 == 0) first_cnt = readlane_u32(w.cnt, 0);
+      // every interval but the last holds interval-0's count (GetRestartInterval)
+      if (r < h.nr && w.err == ~0ull && r + 1 < h.nr && w.cnt != first_cnt) w.err = ((uint64_t)r << 2) | 2u;
+      err = err < w.err ? err : w.err;
+      keys += w.cnt;
+      kb += w.kbytes;
+    }
+    err = wave_min_u64(err);
+    keys = wave_sum_u64(keys);
+    kb = wave_sum_u64(kb);
+    if (err != ~0ull)
+      st = (err & 3) == 0 ? kBlkBadEntry : kBlkBadRestarts;
+    else
+      ri = h.nr > 1 ? first_cnt : 0;
+  }
+  if (st != kBlkOk) keys = kb = ri = 0;
+  *st_out = st;
+  *keys_out = keys;
+  *kb_out = kb;
+  *ri_out = ri;
+}
+
+// Pass 1: per block key count / key bytes / status / restart interval.
 // key_cnt and key_bytes receive the per-block values in place; the scan
 // kernels turn them into exclusive offsets.
 template <int KIND>
 __global__ __launch_bounds__(256) void k_block_layout(SpanSrc blocks, uint32_t count, uint64_t* key_cnt,
                                                       uint64_t* key_bytes, uint32_t* interval_out,
                                                       int32_t* status) {
-  const uint32_t lane = threadIdx.x & 63;
+  __shared__ uint32_t s_slot[4][kBlkSlotWords];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < count; b += nw) {
+  for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + wv; b < count; b += nw) {
     const uint8_t* d = blocks.ptr(b);
-    const BlkHdr h = blk_header(d, blocks.len(b));
-    int st = kBlkOk;
-    uint64_t keys = 0, kb = 0;
-    uint32_t ri = 0;
-    if (!h.ok) {
-      st = kBlkBadContents;
-    } else if (h.nr == 0) {
-      // empty block: protection stays off, no keys
-    } else if (!blk_restarts_ok(d, h, lane)) {
-      st = kBlkBadRestarts;
-    } else if (h.ro == 0) {
-      st = h.nr == 1 ? kBlkOk : kBlkBadRestarts;
+    const uint64_t n = blocks.len(b);
+    int st;
+    uint64_t keys, kb;
+    uint32_t ri;
+    if (n <= kBlkSlot) {
+      const LdsRd rd = blk_stage(d, (uint32_t)n, s_slot[wv], lane);
+      blk_layout_one<KIND>(rd, n, lane, &st, &keys, &kb, &ri);
     } else {
-      const uint8_t* ra = d + h.ro;
-      uint64_t err = ~0ull;
-      uint32_t first_cnt = 0;
-      for (uint32_t r0 = 0; r0 < h.nr; r0 += 64) {
-        const uint32_t r = r0 + lane;
-        BlkWalk w{0, 0, ~0ull};
-        if (r < h.nr) w = blk_walk<KIND>(d, h.ro, r, blk_u32(ra + 4 * r), r + 1 < h.nr ? blk_u32(ra + 4 * (r + 1)) : h.ro);
-        if (r0 == 0) first_cnt = readlane_u32(w.cnt, 0);
-        // every interval but the last holds interval-0's count (GetRestartInterval)
-        if (r < h.nr && w.err == ~0ull && r + 1 < h.nr && w.cnt != first_cnt) w.err = ((uint64_t)r << 2) | 2u;
-        err = err < w.err ? err : w.err;
-        keys += w.cnt;
-        kb += w.kbytes;
-      }
-      err = wave_min_u64(err);
-      keys = wave_sum_u64(keys);
-      kb = wave_sum_u64(kb);
-      if (err != ~0ull) {
-        st = (err & 3) == 0 ? kBlkBadEntry : kBlkBadRestarts;
-      } else {
-        ri = h.nr > 1 ? first_cnt : 0;
-      }
+      blk_layout_one<KIND>(GblRd{d}, n, lane, &st, &keys, &kb, &ri);
     }
-    if (st != kBlkOk) keys = kb = ri = 0;
     if (lane == 0) {
       key_cnt[b] = keys;
       key_bytes[b] = kb;
-      if (interval_out) interval_out[b] = ri;
+      interval_out[b] = ri;
       status[b] = st;
     }
+    wave_lds_sync();  // the slot is rewritten for the next block
   }
 }
 
-// Pass 2: reassemble keys into the arena, write per-entry spans.
-// key_base/arena_base: exclusive scans [count + 1].
-template <int KIND>
-__global__ __launch_bounds__(256) void k_block_materialize(SpanSrc blocks, uint32_t count,
-                                                           const uint64_t* key_base, const uint64_t* arena_base,
-                                                           uint8_t* arena, uint64_t* koff, uint32_t* klen,
-                                                           uint64_t* voff, uint32_t* vlen) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < count; b += nw) {
-    const uint64_t k0 = ldg_u64(key_base, b);
-    if (ldg_u64(key_base, b + 1) == k0) continue;  // no keys (or a bad block)
-    const uint8_t* d = blocks.ptr(b);
-    const uint64_t boff = blocks.off(b);
-    const BlkHdr h = blk_header(d, blocks.len(b));
-    const uint8_t* ra = d + h.ro;
-    const uint8_t* lim = d + h.ro;
-    uint64_t acarry = ldg_u64(arena_base, b);
-    uint32_t ri = 0;
-    for (uint32_t r0 = 0; r0 < h.nr; r0 += 64) {
-      const uint32_t r = r0 + lane;
-      const bool own = r < h.nr;
-      const uint32_t start = own ? blk_u32(ra + 4 * r) : 0;
-      const uint32_t end = own ? (r + 1 < h.nr ? blk_u32(ra + 4 * (r + 1)) : h.ro) : 0;
-      BlkWalk w{0, 0, ~0ull};
-      if (own) w = blk_walk<KIND>(d, h.ro, r, start, end);
-      if (r0 == 0) ri = readlane_u32(w.cnt, 0);
-      const uint64_t incl = wave_incl_scan_u64(w.kbytes, lane);
-      uint64_t a = acarry + incl - w.kbytes;
-      acarry += readlane_u64(incl, 63);
-      if (!own) continue;
-      uint64_t idx = k0 + (uint64_t)r * ri;
-      const uint8_t* p = d + start;
-      const uint8_t* e = d + end;
-      uint64_t prev = a;
-      while (p < e) {
-        uint32_t sh, ns, vl;
-        const uint8_t* v;
-        const uint8_t* q = blk_entry<KIND>(p, lim, &sh, &ns, &v, &vl);
-        // shared prefix from the previous key (this lane wrote it), then the delta
-        for (uint32_t i = 0; i < sh; i++) arena[a + i] = arena[prev + i];
-        for (uint32_t i = 0; i < ns; i++) arena[a + sh + i] = (uint8_t)blk_u8(q + i);
-        koff[idx] = a;
-        klen[idx] = sh + ns;
-        voff[idx] = boff + (uint64_t)(v - d);
-        vlen[idx] = vl;
-        idx++;
-        prev = a;
-        a += sh + ns;
-        p = v + vl;
+// ---- XXPH3 over a reader (util/xxph3.h; see xxph3_short / xxph3_long_lane) --
+template <class R>
+__device__ __forceinline__ uint64_t xp_mix16(const R& r, uint32_t o, int s, uint64_t seed) {
+  return mul128_fold64(r.u64(o) ^ (sec64(s) + seed), r.u64(o + 8) ^ (sec64(s + 8) - seed));
+}
+template <class R>
+__device__ __forceinline__ uint64_t xp_short(const R& r, uint32_t o, uint32_t len, uint64_t seed) {
+  if (len <= 16) {
+    if (len > 8) {
+      const uint64_t lo = r.u64(o) ^ (sec64(0) + seed), hi = r.u64(o + len - 8) ^ (sec64(8) - seed);
+      return xxph3_avalanche(len + (lo + hi) + mul128_fold64(lo, hi));
+    }
+    if (len >= 4) return xxph3_4to8(r.u32(o), r.u32(o + len - 4), len, seed);
+    if (len) return xxph3_1to3(r.u8(o), r.u8(o + (len >> 1)), r.u8(o + len - 1), len, seed);
+    return mul128_fold64(seed + sec64(0), P64_2);
+  }
+  uint64_t acc = (uint64_t)len * P64_1;
+  if (len <= 128) {
+    if (len > 32) {
+      if (len > 64) {
+        if (len > 96) {
+          acc += xp_mix16(r, o + 48, 96, seed);
+          acc += xp_mix16(r, o + len - 64, 112, seed);
+        }
+        acc += xp_mix16(r, o + 32, 64, seed);
+        acc += xp_mix16(r, o + len - 48, 80, seed);
+      }
+      acc += xp_mix16(r, o + 16, 32, seed);
+      acc += xp_mix16(r, o + len - 32, 48, seed);
+    }
+    acc += xp_mix16(r, o, 0, seed);
+    acc += xp_mix16(r, o + len - 16, 16, seed);
+    return xxph3_avalanche(acc);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; i++) acc += xp_mix16(r, o + 16 * i, 16 * i, seed);
+  acc = xxph3_avalanche(acc);
+  const int rounds = (int)len / 16;
+#pragma unroll
+  for (int i = 8; i < 15; i++)
+    if (i < rounds) acc += xp_mix16(r, o + 16 * i, 16 * (i - 8) + 3, seed);
+  acc += xp_mix16(r, o + len - 16, 136 - 17, seed);
+  return xxph3_avalanche(acc);
+}
+// one lane, any length (keys)
+template <class R>
+__device__ __noinline__ uint64_t xp_lane(const R& r, uint32_t o, uint32_t len, uint64_t seed) {
+  if (len <= 240) return xp_short(r, o, len, seed);
+  uint64_t acc[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+  const uint32_t nb = len / 1024;
+  auto stripe = [&](uint32_t p, int soff) {
+    for (int l = 0; l < 8; l++) {
+      const uint64_t d = r.u64(p + 8 * l), k = d ^ csec64(soff + 8 * l, seed);
+      acc[l] += d + mul32to64(k);
+    }
+  };
+  for (uint32_t b = 0; b < nb; b++) {
+    for (int s2 = 0; s2 < 16; s2++) stripe(o + 1024 * b + 64 * s2, 8 * s2);
+    for (int l = 0; l < 8; l++) {
+      uint64_t a = acc[l];
+      a ^= a >> 47;
+      a ^= csec64(128 + 8 * l, seed);
+      acc[l] = a * P32_1;
+    }
+  }
+  const int nst = (int)((len - 1024 * nb) / 64);
+  for (int s2 = 0; s2 < nst; s2++) stripe(o + 1024 * nb + 64 * s2, 8 * s2);
+  if (len & 63) stripe(o + len - 64, 121);
+  uint64_t res = (uint64_t)len * P64_1;
+  for (int l = 0; l < 4; l++)
+    res += mul128_fold64(acc[2 * l] ^ csec64(11 + 16 * l, seed), acc[2 * l + 1] ^ csec64(19 + 16 * l, seed));
+  return xxph3_avalanche(res);
+}
+
+// Per-lane secret words of the wave-cooperative long loop (seed fixed):
+// lane = 8 g + l (accumulator l, stripe group g = stripes g and g + 8).
+struct XpWaveSec {
+  uint64_t s0, s1, scr, last, m;
+};
+__device__ __forceinline__ XpWaveSec xp_wave_sec(uint32_t lane, uint64_t seed) {
+  const int l = lane & 7, g = lane >> 3;
+  XpWaveSec k;
+  k.s0 = csec64(8 * g + 8 * l, seed);
+  k.s1 = csec64(8 * (g + 8) + 8 * l, seed);
+  k.scr = csec64(128 + 8 * l, seed);
+  k.last = csec64(121 + 8 * l, seed);
+  k.m = csec64((l & 1) ? 19 + 16 * (l >> 1) : 11 + 16 * (l >> 1), seed);
+  return k;
+}
+// sum over the 8 lanes with the same (lane & 7)
+__device__ __forceinline__ uint64_t xp_sum_groups(uint64_t v) {
+  v += __shfl_xor(v, 8, 64);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+// XXPH3 long loop (len > 240) of ONE span by the whole wave: within a 1 KiB
+// segment the 128 (stripe, accumulator) terms are independent sums, so lane
+// (g, l) folds stripes g and g + 8 for accumulator l and the 8 groups are
+// summed before the (sequential) scramble.  Result valid on every lane.
+template <class R>
+__device__ __forceinline__ uint64_t xp_wave_long(const R& r, uint32_t o, uint32_t len, const XpWaveSec& k,
+                                                 uint32_t lane) {
+  const uint32_t l = lane & 7, g = lane >> 3;
+  uint64_t acc = l < 4 ? (l < 2 ? (l ? P64_1 : (uint64_t)P32_3) : (l == 2 ? P64_2 : P64_3))
+                      : (l < 6 ? (l == 4 ? P64_4 : (uint64_t)P32_2) : (l == 6 ? P64_5 : (uint64_t)P32_1));
+  const uint32_t nb = len / 1024;
+  for (uint32_t b = 0; b < nb; b++) {
+    const uint32_t p = o + 1024 * b + 64 * g + 8 * l;
+    const uint64_t d0 = r.u64(p), d1 = r.u64(p + 512);
+    acc += xp_sum_groups(d0 + mul32to64(d0 ^ k.s0) + d1 + mul32to64(d1 ^ k.s1));
+    acc ^= acc >> 47;
+    acc ^= k.scr;
+    acc *= P32_1;
+  }
+  const uint32_t nst = (len - 1024 * nb) / 64;
+  uint64_t part = 0;
+  const uint32_t p = o + 1024 * nb + 64 * g + 8 * l;
+  if (g < nst) {
+    const uint64_t d = r.u64(p);
+    part += d + mul32to64(d ^ k.s0);
+  }
+  if (g + 8 < nst) {
+    const uint64_t d = r.u64(p + 512);
+    part += d + mul32to64(d ^ k.s1);
+  }
+  acc += xp_sum_groups(part);
+  if (len & 63) {
+    const uint64_t d = r.u64(o + len - 64 + 8 * l);
+    acc += d + mul32to64(d ^ k.last);
+  }
+  // merge: lanes l = 2j, 2j + 1 pair up
+  // (shuffles outside the ?: -- clang lowers a ?: with call operands to a
+  // branch, and a shuffle there reads masked lanes: found by the
+  // mck_internal_xp_wave test)
+  const uint64_t other = __shfl_xor(acc, 1, 64), mo = __shfl_xor(k.m, 1, 64);
+  const uint64_t f = mul128_fold64(acc ^ k.m, other ^ mo);
+  uint64_t t = (l & 1) ? 0 : f;
+  t += __shfl_xor(t, 2, 64);
+  t += __shfl_xor(t, 4, 64);
+  return xxph3_avalanche((uint64_t)len * P64_1 + readlane_u64(t, 0));
+}
+
+// Pass 2 for one block.  Lane r walks restart interval r, writing one
+// descriptor per entry {shared, non_shared, key delta offset, value length}
+// at its entry index (r * restart_interval + k).  Then lane e takes entry e:
+// its key is reassembled into the key area -- the delta, then the shared
+// prefix from the preceding entries' deltas (walking back while shared
+// shrinks: byte i of key e is byte i - shared_j of the last delta j <= e with
+// shared_j <= i), so keys are built in parallel, not in walk order -- and
+// ProtectKV(key, value) is hashed (values over 240 B by the whole wave).
+// FAST: block, descriptors and keys in LDS.  Otherwise global memory: the
+// block in place, descriptors in the work arrays at k0 (koff = delta offset,
+// klen = shared, voff = non_shared, vlen = value length), keys in the block's
+// arena share.
+template <int KIND, bool VERIFY, bool FAST>
+__device__ __forceinline__ void blk_kv_one(const uint8_t* d, uint64_t n, uint32_t ri, uint64_t k0, uint64_t nk,
+                                           uint32_t* slot, uint8_t* lkeys, uint16_t* ldesc, uint8_t* gkeys,
+                                           uint64_t* gko, uint32_t* gkl, uint64_t* gvo, uint32_t* gvl,
+                                           uint32_t prot_bytes, uint8_t* enc, const uint8_t* stored,
+                                           uint8_t* mismatch, uint32_t* mismatch_count, const XpWaveSec& ws,
+                                           uint32_t lane) {
+  typedef typename std::conditional<FAST, LdsRd, GblRd>::type Rd;
+  Rd rd;
+  if constexpr (FAST)
+    rd = blk_stage(d, (uint32_t)n, slot, lane);
+  else
+    rd = GblRd{d};
+  uint8_t* keys = FAST ? lkeys : gkeys;
+  auto put = [&](uint64_t e, uint32_t sh, uint32_t ns, uint32_t q, uint32_t vl) {
+    if constexpr (FAST) {
+      ldesc[4 * e] = (uint16_t)sh;
+      ldesc[4 * e + 1] = (uint16_t)ns;
+      ldesc[4 * e + 2] = (uint16_t)q;
+      ldesc[4 * e + 3] = (uint16_t)vl;
+    } else {
+      gko[k0 + e] = q;
+      gkl[k0 + e] = sh;
+      gvo[k0 + e] = ns;
+      gvl[k0 + e] = vl;
+    }
+  };
+  auto get_sh = [&](uint64_t e) -> uint32_t {
+    if constexpr (FAST)
+      return ldesc[4 * e];
+    else
+      return gkl[k0 + e];
+  };
+  auto get_q = [&](uint64_t e) -> uint32_t {
+    if constexpr (FAST)
+      return ldesc[4 * e + 2];
+    else
+      return (uint32_t)gko[k0 + e];
+  };
+  const BlkHdr h = rd_header(rd, n);
+  for (uint32_t r = lane; r < h.nr; r += 64) {
+    uint32_t p = rd.u32(h.ro + 4 * r);
+    const uint32_t end = r + 1 < h.nr ? rd.u32(h.ro + 4 * (r + 1)) : h.ro;
+    uint64_t e = (uint64_t)r * ri;
+    while (p < end) {
+      uint32_t sh, ns, q, v, vl;
+      rd_entry_fast<KIND>(rd, p, h.ro, &sh, &ns, &q, &v, &vl);
+      put(e++, sh, ns, q, vl);
+      p = v + vl;
+    }
+  }
+  if constexpr (!FAST) __threadfence_block();
+  wave_lds_sync();
+  typedef typename std::conditional<FAST, LdsRd, GblRd>::type Kr;
+  Kr kr;
+  if constexpr (FAST)
+    kr = LdsRd{reinterpret_cast<const uint32_t*>(lkeys), 0};
+  else
+    kr = GblRd{gkeys};
+  uint32_t carry = 0;
+  for (uint64_t e0 = 0; e0 < nk; e0 += 64) {
+    const uint64_t e = e0 + lane;
+    const bool own = e < nk;
+    uint32_t sh = 0, ns = 0, q = 0, vl = 0;
+    if (own) {
+      if constexpr (FAST) {
+        sh = ldesc[4 * e];
+        ns = ldesc[4 * e + 1];
+        q = ldesc[4 * e + 2];
+        vl = ldesc[4 * e + 3];
+      } else {
+        q = (uint32_t)gko[k0 + e];
+        sh = gkl[k0 + e];
+        ns = (uint32_t)gvo[k0 + e];
+        vl = gvl[k0 + e];
       }
     }
+    const uint32_t kl = sh + ns;
+    const uint32_t incl = (uint32_t)wave_incl_scan_u64(kl, lane);
+    const uint32_t ko = carry + incl - kl;
+    carry += readlane_u32(incl, 63);
+    uint64_t hv = 0;
+    if (own) {
+      for (uint32_t i = 0; i < ns; i++) keys[ko + sh + i] = (uint8_t)rd.u8(q + i);
+      uint32_t lo = sh;
+      for (uint64_t j = e; lo > 0;) {
+        j--;
+        const uint32_t sj = get_sh(j);
+        if (sj < lo) {
+          const uint32_t qj = get_q(j);
+          for (uint32_t i = sj; i < lo; i++) keys[ko + i] = (uint8_t)rd.u8(qj + i - sj);
+          lo = sj;
+        }
+      }
+      if constexpr (!FAST) __threadfence_block();
+      hv = kl <= 240 ? xp_short(kr, ko, kl, kSeedK) : xp_lane(kr, ko, kl, kSeedK);
+      if (vl <= 240) hv ^= xp_short(rd, q + ns, vl, kSeedV);
+    }
+    uint64_t longs = __ballot(own && vl > 240);
+    while (longs) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(longs);
+      longs &= longs - 1;
+      const uint64_t h2 = xp_wave_long(rd, readlane_u32(q + ns, j), readlane_u32(vl, j), ws, lane);
+      if (lane == j) hv ^= h2;
+    }
+    if (own) {
+      const uint64_t k = k0 + e;
+      if constexpr (!VERIFY) {
+        if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0))
+          reinterpret_cast<uint64_t*>(enc)[k] = hv;
+        else
+          for (uint32_t b = 0; b < prot_bytes; b++) enc[k * prot_bytes + b] = (uint8_t)(hv >> (8 * b));
+      } else {
+        uint64_t sv = 0;
+        for (uint32_t b = 0; b < prot_bytes; b++) sv |= (uint64_t)blk_u8(stored + k * prot_bytes + b) << (8 * b);
+        const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
+        const bool bad = sv != (hv & keep);
+        mismatch[k] = bad;
+        if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
+      }
+    }
+  }
+  wave_lds_sync();  // LDS areas are rewritten for the next block
+}
+
+// Pass 2 kernel: one wave per block.  key_base / arena_base: exclusive scans
+// from pass 1; restart_interval from pass 1.
+template <int KIND, bool VERIFY>
+__global__ __launch_bounds__(256) void k_block_kv(SpanSrc blocks, uint32_t count, const uint64_t* key_base,
+                                                  const uint64_t* arena_base, const uint32_t* restart_interval,
+                                                  uint8_t* arena, uint64_t* gko, uint32_t* gkl, uint64_t* gvo,
+                                                  uint32_t* gvl, uint32_t prot_bytes, uint8_t* enc,
+                                                  const uint8_t* stored, uint8_t* mismatch,
+                                                  uint32_t* mismatch_count) {
+  __shared__ uint32_t s_slot[4][kBlkSlotWords];
+  __shared__ uint32_t s_keys[4][kBlkKeyWords];
+  __shared__ uint16_t s_desc[4][4 * kBlkMaxDesc];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
+  const XpWaveSec ws = xp_wave_sec(lane, kSeedV);
+  for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + wv; b < count; b += nw) {
+    const uint64_t k0 = ldg_u64(key_base, b);
+    const uint64_t nk = ldg_u64(key_base, b + 1) - k0;
+    if (!nk) continue;  // no keys (or a bad block)
+    const uint64_t a0 = ldg_u64(arena_base, b);
+    const uint64_t kb = ldg_u64(arena_base, b + 1) - a0;
+    const uint8_t* d = blocks.ptr(b);
+    const uint64_t n = blocks.len(b);
+    const uint32_t ri = ldg_u32(restart_interval, b);
+    uint8_t* lk = reinterpret_cast<uint8_t*>(s_keys[wv]);
+    if (n <= kBlkSlot && nk <= kBlkMaxDesc && kb <= kBlkKeyArea)
+      blk_kv_one<KIND, VERIFY, true>(d, n, ri, k0, nk, s_slot[wv], lk, s_desc[wv], nullptr, nullptr, nullptr,
+                                     nullptr, nullptr, prot_bytes, enc, stored, mismatch, mismatch_count, ws, lane);
+    else
+      blk_kv_one<KIND, VERIFY, false>(d, n, ri, k0, nk, nullptr, nullptr, nullptr, arena + a0, gko, gkl, gvo, gvl,
+                                      prot_bytes, enc, stored, mismatch, mismatch_count, ws, lane);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_dbg_xp(const uint8_t* d, uint32_t len, uint64_t seed, uint64_t* out) {
+  __shared__ uint32_t slot[kBlkSlotWords];
+  const uint32_t lane = threadIdx.x & 63;
+  const XpWaveSec ws = xp_wave_sec(lane, seed);
+  const uint64_t a = xp_wave_long(GblRd{d}, 0, len, ws, lane);
+  const uint64_t b = xp_lane(GblRd{d}, 0, len, seed);
+  uint64_t c = 0;
+  if (len <= kBlkSlot) c = xp_wave_long(blk_stage(d, len, slot, lane), 0, len, ws, lane);
+  if (lane == 0) {
+    out[0] = a;
+    out[1] = b;
+    out[2] = c;
   }
 }
 

@@ -465,10 +465,13 @@ struct BlkLayout {
   }
 };
 template <int KIND>
-struct BlkMat {
-  static void go(dim3 g, hipStream_t st, SpanSrc s, uint32_t n, const uint64_t* kb, const uint64_t* ab, uint8_t* arena,
-                 uint64_t* koff, uint32_t* klen, uint64_t* voff, uint32_t* vlen) {
-    hipLaunchKernelGGL(k_block_materialize<KIND>, g, dim3(256), 0, st, s, n, kb, ab, arena, koff, klen, voff, vlen);
+struct BlkKv {
+  template <class... A>
+  static void go(dim3 g, hipStream_t st, bool verify, A... args) {
+    if (verify)
+      hipLaunchKernelGGL((k_block_kv<KIND, true>), g, dim3(256), 0, st, args...);
+    else
+      hipLaunchKernelGGL((k_block_kv<KIND, false>), g, dim3(256), 0, st, args...);
   }
 };
 
@@ -507,8 +510,9 @@ BlkWork blk_work(void* work, uint64_t keys) {
                  w + blk_work_head(keys)};
 }
 
-int blk_entries(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_t* key_base,
-                const uint64_t* arena_base, uint64_t total_keys, void* work, hipStream_t st, BlkWork* w) {
+int blk_kv(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_t* key_base,
+           const uint64_t* arena_base, const uint32_t* restart_interval, uint64_t total_keys, void* work,
+           uint8_t* enc, const uint8_t* stored, uint8_t* mismatch, uint32_t* mismatch_count, hipStream_t st) {
   if (int rc = check_spans(blocks)) return rc;
   if (kind < MCK_BLOCK_DATA || kind > MCK_BLOCK_META) {
     set_err("unknown block kind %d", kind);
@@ -518,12 +522,8 @@ int blk_entries(int kind, const mck_spans* blocks, uint32_t prot_bytes, const ui
     set_err("protection_bytes_per_key must be 1, 2, 4 or 8 (got %u)", prot_bytes);
     return MCK_EINVAL;
   }
-  if (total_keys > 0xFFFFFFFFull) {
-    set_err("%llu keys in one batch (max 2^32 - 1)", (unsigned long long)total_keys);
-    return MCK_EINVAL;
-  }
-  if (blocks->count && (!key_base || !arena_base)) {
-    set_err("key_base/arena_base is NULL");
+  if (blocks->count && (!key_base || !arena_base || !restart_interval)) {
+    set_err("key_base/arena_base/restart_interval is NULL");
     return MCK_EINVAL;
   }
   if (total_keys && !work) {
@@ -531,9 +531,11 @@ int blk_entries(int kind, const mck_spans* blocks, uint32_t prot_bytes, const ui
     return MCK_EINVAL;
   }
   if (!total_keys || !blocks->count) return MCK_OK;
-  *w = blk_work(work, total_keys);
-  return launch_blk<BlkMat>(kind, blocks->count, st, to_src(blocks), blocks->count, key_base, arena_base, w->arena,
-                            w->koff, w->klen, w->voff, w->vlen);
+  const BlkWork w = blk_work(work, total_keys);
+  const bool verify = stored != nullptr;
+  return launch_blk<BlkKv>(kind, blocks->count, st, verify, to_src(blocks), blocks->count, key_base, arena_base,
+                           restart_interval, w.arena, w.koff, w.klen, w.voff, w.vlen, prot_bytes, enc, stored,
+                           mismatch, mismatch_count);
 }
 }  // namespace
 }  // namespace mck
@@ -1220,8 +1222,8 @@ int mck_block_kv_layout_batch(int kind, const mck_spans* blocks, uint64_t* key_b
                               uint32_t* restart_interval, int32_t* status, void* scratch, mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(blocks)) return rc;
-  if (!key_base || !arena_base || (blocks->count && (!status || !scratch))) {
-    set_err("key_base/arena_base/status/scratch is NULL");
+  if (!key_base || !arena_base || (blocks->count && (!status || !scratch || !restart_interval))) {
+    set_err("key_base/arena_base/status/restart_interval/scratch is NULL");
     return MCK_EINVAL;
   }
   stat_batch(blocks->count, known_bytes(blocks));
@@ -1244,42 +1246,39 @@ int mck_block_kv_layout_batch(int kind, const mck_spans* blocks, uint64_t* key_b
 }
 
 int mck_block_kv_protect_batch(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_t* key_base,
-                               const uint64_t* arena_base, uint64_t total_keys, void* work, uint8_t* out,
-                               mck_stream_t stream) {
+                               const uint64_t* arena_base, const uint32_t* restart_interval, uint64_t total_keys,
+                               void* work, uint8_t* out, mck_stream_t stream) {
   t_err[0] = 0;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (total_keys && !out) {
     set_err("out is NULL");
     return MCK_EINVAL;
   }
-  BlkWork w{};
-  if (int rc = blk_entries(kind, blocks, prot_bytes, key_base, arena_base, total_keys, work, st, &w)) return rc;
-  if (!total_keys || !blocks->count) return MCK_OK;
-  const uint32_t k = (uint32_t)total_keys;
-  OpKvProtect<false> op{SpanSrc{w.arena, w.koff, w.klen, 0, 0},
-                        SpanSrc{static_cast<const uint8_t*>(blocks->base), w.voff, w.vlen, 0, 0},
-                        nullptr, nullptr, MCK_KV_PROTECT_KV, nullptr, nullptr, prot_bytes, nullptr, nullptr};
-  op.enc = out;
-  return launch_xph3(op, k, kSeedV, st);
+  return blk_kv(kind, blocks, prot_bytes, key_base, arena_base, restart_interval, total_keys, work, out, nullptr,
+                nullptr, nullptr, reinterpret_cast<hipStream_t>(stream));
 }
 
 int mck_block_kv_verify_batch(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_t* key_base,
-                              const uint64_t* arena_base, uint64_t total_keys, void* work, const uint8_t* stored,
-                              uint8_t* mismatch, uint32_t* mismatch_count, mck_stream_t stream) {
+                              const uint64_t* arena_base, const uint32_t* restart_interval, uint64_t total_keys,
+                              void* work, const uint8_t* stored, uint8_t* mismatch, uint32_t* mismatch_count,
+                              mck_stream_t stream) {
   t_err[0] = 0;
-  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (total_keys && (!stored || !mismatch)) {
     set_err("stored/mismatch is NULL");
     return MCK_EINVAL;
   }
-  BlkWork w{};
-  if (int rc = blk_entries(kind, blocks, prot_bytes, key_base, arena_base, total_keys, work, st, &w)) return rc;
-  if (!total_keys || !blocks->count) return MCK_OK;
-  const OpKvProtect<true> op{SpanSrc{w.arena, w.koff, w.klen, 0, 0},
-                             SpanSrc{static_cast<const uint8_t*>(blocks->base), w.voff, w.vlen, 0, 0},
-                             nullptr, nullptr, MCK_KV_PROTECT_KV, nullptr, stored, prot_bytes, mismatch,
-                             mismatch_count};
-  return launch_xph3(op, (uint32_t)total_keys, kSeedV, st);
+  return blk_kv(kind, blocks, prot_bytes, key_base, arena_base, restart_interval, total_keys, work, nullptr, stored,
+                mismatch, mismatch_count, reinterpret_cast<hipStream_t>(stream));
+}
+
+// Internal test hook (not part of mck.h): XXPH3 of one device span by the
+// block kernels' wave-cooperative long loop, the per-lane loop, and the wave
+// loop over an LDS-staged copy: out[0..2].
+int mck_internal_xp_wave(const void* data, uint32_t len, uint64_t seed, uint64_t* out, mck_stream_t stream) {
+  if (int rc = current_device(nullptr, nullptr)) return rc;
+  hipLaunchKernelGGL(k_dbg_xp, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(data), len, seed, out);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
 }
 
 // ---- partitioning + host-resident multi-GPU pipeline -----------------------

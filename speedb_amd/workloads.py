@@ -110,3 +110,77 @@ class WalImage:
     def verify(self, stream=None):
         return C.wal_verify_batch(self.data, self.nbytes, self.log_number, stream=stream,
                                   out=self.results)
+
+
+def _varint(v: int) -> bytes:
+    out = bytearray()
+    while v >= 128:
+        out.append((v & 127) | 128)
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+class DataBlocks:
+    """Row 8f-4: uncompressed data blocks as BlockBuilder lays them out
+    (table/block_based/block_builder.cc:188-252: prefix-compressed internal
+    keys, restart every ``restart_interval`` entries, restart array + footer),
+    cut at ``block_bytes`` like FlushBlockBySizePolicy, back to back with a
+    5-byte trailer gap between blocks as in an SST.  ``distinct`` different
+    blocks are built on the host and tiled to ``count`` blocks on the device
+    (throughput does not depend on the bytes repeating: 4 GiB >> L2/MALL).
+    ``entries[j]`` keeps block j's (internal key, value) list for checks."""
+
+    def __init__(self, count: int, device, key_bytes: int = 16, value_bytes: int = 1000,
+                 block_bytes: int = 4096, restart_interval: int = 16, distinct: int = 256, seed: int = 3):
+        rng = np.random.default_rng(seed)
+        self.entries, blobs = [], []
+        uk = 0
+        for _ in range(distinct):
+            ents, size = [], 0
+            while size < block_bytes:
+                user = b"%0*d" % (key_bytes, uk)
+                uk += int(rng.integers(1, 50))
+                ikey = user + int((int(rng.integers(1, 1 << 56)) << 8) | 1).to_bytes(8, "little")
+                val = rng.integers(0, 256, size=value_bytes, dtype=np.uint8).tobytes()
+                ents.append((ikey, val))
+                size += len(ikey) + len(val) + 3
+            self.entries.append(ents)
+            buf, restarts, last = bytearray(), [], b""
+            for i, (k, v) in enumerate(ents):
+                if i % restart_interval == 0:
+                    restarts.append(len(buf))
+                    sh = 0
+                else:
+                    sh = 0
+                    while sh < min(len(k), len(last)) and k[sh] == last[sh]:
+                        sh += 1
+                buf += _varint(sh) + _varint(len(k) - sh) + _varint(len(v)) + k[sh:] + v
+                last = k
+            for r in restarts:
+                buf += int(r).to_bytes(4, "little")
+            buf += len(restarts).to_bytes(4, "little")
+            blobs.append(bytes(buf))
+        lens = np.array([len(b) for b in blobs], dtype=np.int64)
+        tile_offs = np.zeros(distinct, dtype=np.int64)
+        tile_offs[1:] = np.cumsum(lens + 5)[:-1]
+        tile_bytes = int(tile_offs[-1] + lens[-1] + 5)
+        tile = np.zeros(tile_bytes, dtype=np.uint8)
+        for o, b in zip(tile_offs, blobs):
+            tile[o:o + len(b)] = np.frombuffer(b, dtype=np.uint8)
+        reps = (count + distinct - 1) // distinct
+        self.count = count
+        self.distinct = distinct
+        self.nbytes = reps * tile_bytes
+        self.data = torch.empty(self.nbytes + 64, dtype=torch.uint8, device=device)
+        self.data[:self.nbytes].view(reps, tile_bytes).copy_(
+            torch.from_numpy(tile).to(device).unsqueeze(0).expand(reps, tile_bytes))
+        j = np.arange(count) % distinct
+        offs = (np.arange(count) // distinct) * tile_bytes + tile_offs[j]
+        self.block_lengths = lens[j]
+        self.offsets = torch.from_numpy(offs).to(device)
+        self.lengths = torch.from_numpy(self.block_lengths.astype(np.int32)).to(device)
+        self.block_bytes = int(self.block_lengths.sum())
+        self.keys_per_block = np.array([len(e) for e in self.entries])[j]
+        self.spans = C.Spans(self.data, count, offsets=self.offsets, lengths=self.lengths)
+        torch.cuda.synchronize(device)

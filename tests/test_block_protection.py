@@ -299,7 +299,31 @@ def test_block_protection_abi_errors():
     from speedb_amd._lib import lib, mck_spans
     import ctypes
     s = mck_spans(None, None, None, 0, 0, 0)
-    assert lib.mck_block_kv_protect_batch(0, ctypes.byref(s), 3, None, None, 0, None, None, None) == -1
-    assert lib.mck_block_kv_protect_batch(9, ctypes.byref(s), 4, None, None, 0, None, None, None) == -1
+    assert lib.mck_block_kv_protect_batch(0, ctypes.byref(s), 3, None, None, None, 0, None, None, None) == -1
+    assert lib.mck_block_kv_protect_batch(9, ctypes.byref(s), 4, None, None, None, 0, None, None, None) == -1
     assert lib.mck_block_kv_scratch_bytes(5000) >= 16 * 3
     assert lib.mck_block_kv_work_bytes(10, 100) >= 10 * 24 + 100
+
+
+@pytest.mark.gpu
+def test_wave_xxph3_long_loop(gpu, oracle):
+    """The block kernel's wave-cooperative XXPH3 long loop (8 accumulators x
+    8 stripe groups), its per-lane loop and the LDS-staged wave loop against
+    Hash64 (mck_internal_xp_wave, an internal test hook)."""
+    import ctypes
+    from speedb_amd._lib import lib
+    torch = gpu
+    f = lib.mck_internal_xp_wave
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    rnd = random.Random(1)
+    out = torch.zeros(3, dtype=torch.int64, device="cuda")
+    for n in (241, 255, 256, 300, 1000, 1023, 1024, 1025, 2100, 5000, 6144):
+        b = bytes(rnd.getrandbits(8) for _ in range(n))
+        d = torch.frombuffer(bytearray(bytes(rnd.randrange(16)) + b + bytes(64)), dtype=torch.uint8).cuda()
+        off = d.numel() - 64 - n
+        for seed in (0, 0xD28AAD72F49BD50B):
+            assert f(d.data_ptr() + off, n, seed, out.data_ptr(), None) == 0
+            r = [x & (2 ** 64 - 1) for x in out.cpu().tolist()]
+            want = oracle.Hash64(b, seed)
+            assert r == [want, want, want], (n, seed)
