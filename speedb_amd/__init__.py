@@ -12,6 +12,7 @@ from .checksum import __all__ as _checksum_all
 from . import sst  # noqa: F401  (whole-SST-file verification)
 from . import blob  # noqa: F401  (blob file records)
 from . import block  # noqa: F401  (per-KV protection of block entries)
+from . import handoff  # noqa: F401  (WritableFileWriter checksum handoff)
 
 __all__ = list(_checksum_all)
 __version__ = "0.1.0"

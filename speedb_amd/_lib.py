@@ -95,6 +95,7 @@ SIGNATURES = [
     ("mck_kv_protect_verify_batch", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.POINTER(mck_spans), vp, vp, vp,
       ctypes.c_uint32, vp, vp, vp, vp]),
+    ("mck_handoff_checksum_batch", ctypes.c_int, [ctypes.POINTER(mck_spans), vp, vp]),
     ("mck_block_kv_scratch_bytes", ctypes.c_uint64, [ctypes.c_uint32]),
     ("mck_block_kv_layout_batch", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(mck_spans), vp, vp, vp, vp, vp, vp]),

@@ -591,6 +591,12 @@ int mck_crc32c_batch(const mck_spans* spans, const uint32_t* init_crcs, uint32_t
   return launch_crc(op, spans->count, reinterpret_cast<hipStream_t>(stream));
 }
 
+// file/writable_file_writer.cc:743-747: EncodeFixed32(Extend(0, piece)) --
+// the batched CRC with init 0, unmasked (the LE32 bytes are the u32 itself).
+int mck_handoff_checksum_batch(const mck_spans* pieces, uint32_t* out, mck_stream_t stream) {
+  return mck_crc32c_batch(pieces, nullptr, 0u, out, stream);
+}
+
 int mck_xxh3_64_batch(const mck_spans* spans, uint64_t* out, mck_stream_t stream) {
   t_err[0] = 0;
   if (int rc = check_spans(spans)) return rc;
