@@ -10,7 +10,7 @@ Default workload (the headline, BASELINE.json configs[1]): CRC32C over
   sst      configs[2]  compaction-shaped 4/16/64 KiB (+0..255 B) SST blocks
                        with 5-byte trailers, format_version 6 context
                        checksums; VerifyBlockChecksum of every block, one
-                       kCRC32c image and one kXXH3 image per step
+                       kCRC32c image and one kXXH3 image (4 GiB each) per step
   wal      configs[3]  WAL replay: a fixed global batch of 10M x 32 KiB blocks
                        (one kFullType record each) partitioned over the ranks
                        (strong scaling), ReadPhysicalRecord CRC verify of
@@ -99,7 +99,10 @@ def parse():
                             "walrec", "ragged"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
-    p.add_argument("--sst-bytes", type=int, default=1 << 30, help="per SST image (sst); 2 images")
+    p.add_argument("--sst-bytes", type=int, default=4 << 30,
+                   help="per SST image (sst); 2 images.  Each launch pays ~25 us of fixed cost (mostly "
+                        "the last 64 KiB spans' 16 sequential rounds, DESIGN.md 5): 1 GiB images read 0.66 "
+                        "of peak, 4 GiB 0.73")
     p.add_argument("--sst-types", choices=["both", "crc32c", "xxh3"], default="both",
                    help="sst: verify both images (configs[2]) or one (per-kernel measurement)")
     p.add_argument("--wal-blocks", type=int, default=10_000_000,

@@ -485,6 +485,10 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
 }
 
 // ---- XXH3 / XXPH3, one WAVE per span ---------------------------------------
+// MCK_X3_FULL_ROUNDS=0 (A/B): interior units take the general unit path too.
+#ifndef MCK_X3_FULL_ROUNDS
+#define MCK_X3_FULL_ROUNDS 1
+#endif
 // For batches of KiB-sized blocks (SST): spans are dealt to waves like the
 // CRC engine, so a long span is not serialised on one 16-lane row and a
 // ragged batch balances over 4x fewer, 4x faster workers.
@@ -728,12 +732,55 @@ struct X3FeedStatic {
 // hidden by the other waves (16 per CU); prefetching the next unit in
 // registers as well needs ~150 VGPRs, and at 3 waves per SIMD measured
 // slower (4.07 vs 4.91 TB/s on the SST-shaped mix).
+// An interior unit (k + 1 < units) is always a full round -- segments 4k ..
+// 4k + 3 all full (k < rounds - 1 <= nb / 4 - 1) -- so it needs no clamped
+// addresses, no per-stripe masks, no lone-segment / last-stripe / epilogue
+// loads: four 16-byte loads at one base + 256 B immediates (+ the dword
+// before the row's segment when the span is byte-misaligned) and the fold.
+template <bool PREVIEW>
+__device__ __forceinline__ void x3w_full_round(const X3WSpan& sp, uint32_t k, const X3Row& X, uint64_t& a0,
+                                               uint64_t& a1) {
+  const uint32_t sh = rd_shift(sp.ptr);
+  const uint64_t seg = sp.ptr + 1024ull * (4 * k + X.row);
+  const uint64_t a = seg + 64 * X.st4 + 16 * X.q - sh + 4;
+  uint4 d[4];
+#pragma unroll
+  for (int m = 0; m < 4; m++) d[m] = gload16u(a + 256 * m);
+  if (sp.ptr & 3) {  // wave-uniform
+    const uint32_t e0 = gload4(seg - sh);
+    rd_fix_row(d, e0, X.j, rd_sel(sh));
+  }
+  uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+    const uint64_t d0 = ((uint64_t)d[m].y << 32) | d[m].x, d1 = ((uint64_t)d[m].w << 32) | d[m].z;
+    c0 += (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.k0[m]);
+    c1 += (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.k1[m]);
+  }
+  c0 = row_sum_st4(c0);
+  c1 = row_sum_st4(c1);
+  const uint64_t e0 = xl16_64(c0), e1 = xl16_64(c1);
+  const uint64_t C0[4] = {c0, e0, xl32_64(c0), xl32_64(e0)};
+  const uint64_t C1[4] = {c1, e1, xl32_64(c1), xl32_64(e1)};
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    a0 = xxh3_scramble(a0 + C0[r], X.ks0);
+    a1 = xxh3_scramble(a1 + C1[r], X.ks1);
+  }
+}
+
 template <class Op, bool PREVIEW, class Feed>
 __device__ __forceinline__ void xxh3_wave_loop(const Op& op, Feed& f, const X3Row& X) {
   X3WSpan cur;
   while (f.template next<Op, PREVIEW>(op, cur)) {
     uint64_t a0 = X.i0, a1 = X.i1;
+#if MCK_X3_FULL_ROUNDS
+    for (uint32_t k = 0; k + 1 < cur.units; k++) x3w_full_round<PREVIEW>(cur, k, X, a0, a1);
+    {
+      const uint32_t k = cur.units - 1;
+#else
     for (uint32_t k = 0; k < cur.units; k++) {
+#endif
       const X3WLoads L = x3w_load(cur, k, X);
       const typename Op::Pre e = op.pre(cur.i, cur.ptr, cur.len);
       x3w_fold<Op, PREVIEW>(op, cur, k, L, X, a0, a1, e);
