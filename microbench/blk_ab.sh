@@ -1,0 +1,13 @@
+#!/bin/bash
+# Block KV protection: tests, then thread-per-block (default) vs wave kernels.
+out=gpurun_out/$1
+mkdir -p $out
+timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_block_protection.py > $out/t.log 2>&1 || { tail -30 $out/t.log; exit 1; }
+tail -2 $out/t.log
+for vb in 100 1000; do
+  for w in 0 1; do
+    MCK_BLK_WAVE=$w timeout -k 10 300 python bench.py --workload blockkv --kv-value-bytes $vb --steps 20 --warmup 10 > $out/b${vb}_w$w.json 2> $out/b${vb}_w$w.err || exit 1
+  done
+done
+for f in $out/*.json; do python3 -c "
+import json; d=json.load(open('$f')); print('$f', d['value'], d['ms_per_step'], d['roofline']['frac'], d['verified'])"; done

@@ -687,6 +687,140 @@ __global__ __launch_bounds__(256) void k_block_kv(SpanSrc blocks, uint32_t count
   }
 }
 
+// ---- one THREAD per block (default) ------------------------------------------
+// The wave-per-block kernels above keep one lane per restart interval busy --
+// 3 of 64 lanes for a 4 KiB block of 100-byte values -- so their cost is
+// ~1000 (layout) / ~3500 (kv) VALU instructions per block issued for a few
+// lanes (SQ counters, profiles/r2b/blockkv).  Here each lane owns a whole
+// block and walks it in order, exactly as the reference's SeekToFirst/Next
+// loop (and the oracle) does; 64 blocks per wave keep every lane busy and the
+// dependent header reads of thousands of blocks in flight hide the memory
+// latency.  MCK_BLK_WAVE=1 selects the wave kernels (A/B).
+
+// Sequential walk of one block (block.cc:1091-1132 with the restart checks
+// of the layout pass); on_entry(idx, key_len, shared, delta_off, value_off,
+// value_len) per entry.  Returns the status; *nk, *kb, *ri.
+template <int KIND, class R, class F>
+__device__ __forceinline__ int blk_seq_walk(const R& rd, uint64_t n, uint32_t* nk, uint64_t* kb, uint32_t* ri_out,
+                                            F&& on_entry) {
+  *nk = 0;
+  *kb = 0;
+  *ri_out = 0;
+  const BlkHdr h = rd_header(rd, n);
+  if (!h.ok) return kBlkBadContents;
+  if (h.nr == 0) return kBlkOk;
+  for (uint32_t r = 0; r < h.nr; r++) {
+    const uint32_t x = rd.u32(h.ro + 4 * r);
+    if (r == 0 ? (h.ro != 0 && x != 0) : (x <= rd.u32(h.ro + 4 * (r - 1)) || x >= h.ro)) return kBlkBadRestarts;
+  }
+  if (h.ro == 0) return h.nr == 1 ? kBlkOk : kBlkBadRestarts;
+  uint32_t idx = 0, interval = 0, in_cur = 0, r = 0, kl = 0;
+  uint32_t next = rd.u32(h.ro);  // restart point r
+  uint64_t kbytes = 0;
+  uint32_t p = 0;
+  while (p < h.ro) {
+    if (r < h.nr && p > next) return kBlkBadRestarts;  // a restart point inside an entry
+    const bool at_restart = r < h.nr && p == next;
+    if (at_restart) {
+      if (r == 1)
+        interval = in_cur;
+      else if (r > 1 && in_cur != interval)
+        return kBlkBadRestarts;
+      in_cur = 0;
+      r++;
+      next = r < h.nr ? rd.u32(h.ro + 4 * r) : 0xFFFFFFFFu;
+    }
+    uint32_t sh, ns, q, v, vl;
+    if (!rd_entry_fast<KIND>(rd, p, h.ro, &sh, &ns, &q, &v, &vl)) return kBlkBadEntry;
+    if (at_restart && sh != 0) return r == 1 ? kBlkBadEntry : kBlkBadRestarts;
+    if (kl < sh) return kBlkBadEntry;
+    on_entry(idx, sh + ns, sh, q, v, vl);
+    kl = sh + ns;
+    kbytes += kl;
+    idx++;
+    in_cur++;
+    p = v + vl;
+  }
+  if (r != h.nr) return kBlkBadRestarts;
+  *nk = idx;
+  *kb = kbytes;
+  *ri_out = h.nr > 1 ? interval : 0;
+  return kBlkOk;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_block_layout_t(SpanSrc blocks, uint32_t count, uint64_t* key_cnt,
+                                                        uint64_t* key_bytes, uint32_t* interval_out,
+                                                        int32_t* status) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= count) return;
+  uint32_t nk, ri;
+  uint64_t kb;
+  const int st = blk_seq_walk<KIND>(GblRd{blocks.ptr(b)}, blocks.len(b), &nk, &kb, &ri,
+                                    [](uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t) {});
+  key_cnt[b] = st == kBlkOk ? nk : 0;
+  key_bytes[b] = st == kBlkOk ? kb : 0;
+  interval_out[b] = st == kBlkOk ? ri : 0;
+  status[b] = st;
+}
+
+// Pass 2, one thread per block.  The current key lives in a per-thread LDS
+// buffer and is updated in place as IterKey::TrimAppend does
+// (block.cc:641-651): entry e only writes its non_shared bytes at [shared,
+// shared + non_shared) -- the prefix is already there -- and is hashed from
+// the buffer; the value is hashed in place.  A key longer than the buffer
+// moves the thread to its block's arena share (global, same in-place rule).
+constexpr uint32_t kBlkKeyBuf = 128;  // bytes of LDS key buffer per thread
+template <int KIND, bool VERIFY>
+__global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t count, const uint64_t* key_base,
+                                                    const uint64_t* arena_base, uint8_t* arena, uint32_t prot_bytes,
+                                                    uint8_t* enc, const uint8_t* stored, uint8_t* mismatch,
+                                                    uint32_t* mismatch_count) {
+  __shared__ uint32_t s_key[256][kBlkKeyBuf / 4 + 4];  // + 16 B: dword reads past the key end
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= count) return;
+  const uint64_t k0 = ldg_u64(key_base, b);
+  if (ldg_u64(key_base, b + 1) == k0) return;  // no keys (or a bad block)
+  uint8_t* const lkey = reinterpret_cast<uint8_t*>(s_key[threadIdx.x]);
+  uint8_t* const gkey = arena + ldg_u64(arena_base, b);
+  bool global_key = false;
+  const GblRd rd{blocks.ptr(b)};
+  uint32_t nk, ri;
+  uint64_t kb;
+  blk_seq_walk<KIND>(rd, blocks.len(b), &nk, &kb, &ri,
+                     [&](uint32_t idx, uint32_t kl, uint32_t sh, uint32_t q, uint32_t v, uint32_t vl) {
+    if (!global_key && kl > kBlkKeyBuf) {  // rare: move the prefix to the arena
+      for (uint32_t i = 0; i < sh; i++) gkey[i] = lkey[i];
+      global_key = true;
+    }
+    uint64_t hv;
+    if (!global_key) {
+      for (uint32_t i = sh; i < kl; i++) lkey[i] = (uint8_t)rd.u8(q + i - sh);
+      const LdsRd kr{s_key[threadIdx.x], 0};
+      hv = xp_short(kr, 0, kl, kSeedK);
+    } else {
+      for (uint32_t i = sh; i < kl; i++) gkey[i] = (uint8_t)rd.u8(q + i - sh);
+      __threadfence_block();
+      hv = xp_lane(GblRd{gkey}, 0, kl, kSeedK);
+    }
+    hv ^= vl <= 240 ? xp_short(rd, v, vl, kSeedV) : xp_lane(rd, v, vl, kSeedV);
+    const uint64_t k = k0 + idx;
+    if constexpr (!VERIFY) {
+      if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0))
+        reinterpret_cast<uint64_t*>(enc)[k] = hv;
+      else
+        for (uint32_t c = 0; c < prot_bytes; c++) enc[k * prot_bytes + c] = (uint8_t)(hv >> (8 * c));
+    } else {
+      uint64_t sv = 0;
+      for (uint32_t c = 0; c < prot_bytes; c++) sv |= (uint64_t)blk_u8(stored + k * prot_bytes + c) << (8 * c);
+      const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
+      const bool bad = sv != (hv & keep);
+      mismatch[k] = bad;
+      if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
+    }
+  });
+}
+
 __global__ __launch_bounds__(64) void k_dbg_xp(const uint8_t* d, uint32_t len, uint64_t seed, uint64_t* out) {
   __shared__ uint32_t slot[kBlkSlotWords];
   const uint32_t lane = threadIdx.x & 63;

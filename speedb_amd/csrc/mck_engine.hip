@@ -464,6 +464,34 @@ struct BlkLayout {
     hipLaunchKernelGGL(k_block_layout<KIND>, g, dim3(256), 0, st, s, n, a, b, ri, stt);
   }
 };
+// thread-per-block kernels (default) or the wave-per-block LDS kernels
+// (MCK_BLK_WAVE=1, A/B)
+bool blk_wave() {
+  static const bool w = [] {
+    const char* e = getenv("MCK_BLK_WAVE");
+    return e && atoi(e) != 0;
+  }();
+  return w;
+}
+template <int KIND>
+struct BlkLayoutT {
+  static void go(dim3, hipStream_t st, SpanSrc s, uint32_t n, uint64_t* a, uint64_t* b, uint32_t* ri, int32_t* stt) {
+    hipLaunchKernelGGL(k_block_layout_t<KIND>, dim3((n + 255) / 256), dim3(256), 0, st, s, n, a, b, ri, stt);
+  }
+};
+template <int KIND>
+struct BlkKvT {
+  template <class... A>
+  static void go(dim3, hipStream_t st, bool verify, SpanSrc s, uint32_t n, const uint64_t* kb, const uint64_t* ab,
+                 const uint32_t*, uint8_t* arena, uint64_t*, uint32_t*, uint64_t*, uint32_t*, A... rest) {
+    if (verify)
+      hipLaunchKernelGGL((k_block_kv_t<KIND, true>), dim3((n + 255) / 256), dim3(256), 0, st, s, n, kb, ab, arena,
+                         rest...);
+    else
+      hipLaunchKernelGGL((k_block_kv_t<KIND, false>), dim3((n + 255) / 256), dim3(256), 0, st, s, n, kb, ab, arena,
+                         rest...);
+  }
+};
 template <int KIND>
 struct BlkKv {
   template <class... A>
@@ -533,6 +561,10 @@ int blk_kv(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_
   if (!total_keys || !blocks->count) return MCK_OK;
   const BlkWork w = blk_work(work, total_keys);
   const bool verify = stored != nullptr;
+  if (!blk_wave())
+    return launch_blk<BlkKvT>(kind, blocks->count, st, verify, to_src(blocks), blocks->count, key_base, arena_base,
+                              restart_interval, w.arena, w.koff, w.klen, w.voff, w.vlen, prot_bytes, enc, stored,
+                              mismatch, mismatch_count);
   return launch_blk<BlkKv>(kind, blocks->count, st, verify, to_src(blocks), blocks->count, key_base, arena_base,
                            restart_interval, w.arena, w.koff, w.klen, w.voff, w.vlen, prot_bytes, enc, stored,
                            mismatch, mismatch_count);
@@ -1240,7 +1272,10 @@ int mck_block_kv_layout_batch(int kind, const mck_spans* blocks, uint64_t* key_b
     MCK_HIP(hipMemsetAsync(arena_base, 0, 8, st));
     return MCK_OK;
   }
-  if (int rc = launch_blk<BlkLayout>(kind, n, st, to_src(blocks), n, key_base, arena_base, restart_interval, status))
+  if (int rc = blk_wave() ? launch_blk<BlkLayout>(kind, n, st, to_src(blocks), n, key_base, arena_base,
+                                                  restart_interval, status)
+                          : launch_blk<BlkLayoutT>(kind, n, st, to_src(blocks), n, key_base, arena_base,
+                                                   restart_interval, status))
     return rc;
   const uint32_t tiles = (uint32_t)blk_tiles(n);
   uint64_t* tsum = static_cast<uint64_t*>(scratch);

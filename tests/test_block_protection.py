@@ -327,3 +327,20 @@ def test_wave_xxph3_long_loop(gpu, oracle):
             r = [x & (2 ** 64 - 1) for x in out.cpu().tolist()]
             want = oracle.Hash64(b, seed)
             assert r == [want, want, want], (n, seed)
+
+
+@pytest.mark.gpu
+def test_block_protection_wave_kernels_subprocess(gpu):
+    """The wave-per-block LDS kernels (MCK_BLK_WAVE=1, read once per
+    process) in a child process: the same GPU parity tests."""
+    import os
+    import subprocess
+    import sys
+    if os.environ.get("MCK_BLK_WAVE") == "1":
+        pytest.skip("already running the wave kernels")
+    env = dict(os.environ, MCK_BLK_WAVE="1")
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        "-k", "not subprocess", os.path.join(here, "test_block_protection.py")],
+                       env=env, cwd=os.path.dirname(here), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
