@@ -693,7 +693,7 @@ __global__ __launch_bounds__(256) void k_block_kv(SpanSrc blocks, uint32_t count
 // ~1000 (layout) / ~3500 (kv) VALU instructions per block issued for a few
 // lanes (SQ counters, profiles/r2b/blockkv).  Here each lane owns a whole
 // block and walks it in order, exactly as the reference's SeekToFirst/Next
-// loop (and the oracle) does; 64 blocks per wave keep every lane busy and the
+// loop does; 64 blocks per wave keep every lane busy and the
 // dependent header reads of thousands of blocks in flight hide the memory
 // latency.  MCK_BLK_WAVE=1 selects the wave kernels (A/B).
 
