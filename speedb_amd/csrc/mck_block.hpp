@@ -771,54 +771,98 @@ __global__ __launch_bounds__(256) void k_block_layout_t(SpanSrc blocks, uint32_t
 // the buffer; the value is hashed in place.  A key longer than the buffer
 // moves the thread to its block's arena share (global, same in-place rule).
 constexpr uint32_t kBlkKeyBuf = 128;  // bytes of LDS key buffer per thread
+// The lanes step through their blocks' entries together (one entry per lane
+// per iteration); values of kBlkWaveLong bytes or more are not hashed per lane -- 8-byte loads
+// from 64 different blocks per instruction, far from coalesced -- but by the
+// whole wave, one at a time (xp_wave_long: every load instruction reads 512
+// contiguous bytes of the value).  -DMCK_BLK_LANE_LONG=1: per lane (A/B).
+// Measured (1M blocks): 1000-B values 2.41 vs 2.70 ms per step (wave vs
+// lane), 300-B values 5.69 vs 4.37 ms -- so the wave takes values of
+// kBlkWaveLong bytes and more.
+#ifndef MCK_BLK_LANE_LONG
+#define MCK_BLK_LANE_LONG 0
+#endif
+constexpr uint32_t kBlkWaveLong = 512;
 template <int KIND, bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t count, const uint64_t* key_base,
                                                     const uint64_t* arena_base, uint8_t* arena, uint32_t prot_bytes,
                                                     uint8_t* enc, const uint8_t* stored, uint8_t* mismatch,
                                                     uint32_t* mismatch_count) {
   __shared__ uint32_t s_key[256][kBlkKeyBuf / 4 + 4];  // + 16 B: dword reads past the key end
+  [[maybe_unused]] const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= count) return;
-  const uint64_t k0 = ldg_u64(key_base, b);
-  if (ldg_u64(key_base, b + 1) == k0) return;  // no keys (or a bad block)
+  uint64_t k0 = 0;
+  bool active = false;
+  if (b < count) {
+    k0 = ldg_u64(key_base, b);
+    active = ldg_u64(key_base, b + 1) != k0;  // no keys (or a bad block): idle
+  }
   uint8_t* const lkey = reinterpret_cast<uint8_t*>(s_key[threadIdx.x]);
-  uint8_t* const gkey = arena + ldg_u64(arena_base, b);
+  uint8_t* const gkey = active ? arena + ldg_u64(arena_base, b) : arena;
   bool global_key = false;
-  const GblRd rd{blocks.ptr(b)};
-  uint32_t nk, ri;
-  uint64_t kb;
-  blk_seq_walk<KIND>(rd, blocks.len(b), &nk, &kb, &ri,
-                     [&](uint32_t idx, uint32_t kl, uint32_t sh, uint32_t q, uint32_t v, uint32_t vl) {
-    if (!global_key && kl > kBlkKeyBuf) {  // rare: move the prefix to the arena
-      for (uint32_t i = 0; i < sh; i++) gkey[i] = lkey[i];
-      global_key = true;
+  const GblRd rd{active ? blocks.ptr(b) : nullptr};
+  const uint32_t ro = active ? rd_header(rd, blocks.len(b)).ro : 0;  // the layout pass validated the block
+#if !MCK_BLK_LANE_LONG
+  const XpWaveSec ws = xp_wave_sec(lane, kSeedV);
+#endif
+  uint32_t p = 0, idx = 0;
+  while (__any(active)) {
+    uint32_t sh = 0, ns = 0, q = 0, v = 0, vl = 0;
+    uint64_t hv = 0;
+    if (active) {
+      rd_entry_fast<KIND>(rd, p, ro, &sh, &ns, &q, &v, &vl);
+      const uint32_t kl = sh + ns;
+      if (!global_key && kl > kBlkKeyBuf) {  // rare: move the prefix to the arena
+        for (uint32_t i = 0; i < sh; i++) gkey[i] = lkey[i];
+        global_key = true;
+      }
+      // IterKey::TrimAppend: only the non-shared bytes change
+      if (!global_key) {
+        for (uint32_t i = sh; i < kl; i++) lkey[i] = (uint8_t)rd.u8(q + i - sh);
+        const LdsRd kr{s_key[threadIdx.x], 0};
+        hv = xp_short(kr, 0, kl, kSeedK);
+      } else {
+        for (uint32_t i = sh; i < kl; i++) gkey[i] = (uint8_t)rd.u8(q + i - sh);
+        __threadfence_block();
+        hv = xp_lane(GblRd{gkey}, 0, kl, kSeedK);
+      }
+#if MCK_BLK_LANE_LONG
+      hv ^= vl <= 240 ? xp_short(rd, v, vl, kSeedV) : xp_lane(rd, v, vl, kSeedV);
+#else
+      if (vl < kBlkWaveLong) hv ^= vl <= 240 ? xp_short(rd, v, vl, kSeedV) : xp_lane(rd, v, vl, kSeedV);
+#endif
     }
-    uint64_t hv;
-    if (!global_key) {
-      for (uint32_t i = sh; i < kl; i++) lkey[i] = (uint8_t)rd.u8(q + i - sh);
-      const LdsRd kr{s_key[threadIdx.x], 0};
-      hv = xp_short(kr, 0, kl, kSeedK);
-    } else {
-      for (uint32_t i = sh; i < kl; i++) gkey[i] = (uint8_t)rd.u8(q + i - sh);
-      __threadfence_block();
-      hv = xp_lane(GblRd{gkey}, 0, kl, kSeedK);
+#if !MCK_BLK_LANE_LONG
+    uint64_t longs = __ballot(active && vl >= kBlkWaveLong);
+    const uint64_t va = reinterpret_cast<uint64_t>(rd.p) + v;
+    while (longs) {
+      const uint32_t j = (uint32_t)__builtin_ctzll(longs);
+      longs &= longs - 1;
+      const uint64_t h2 = xp_wave_long(GblRd{reinterpret_cast<const uint8_t*>(readlane_u64(va, j))}, 0,
+                                       readlane_u32(vl, j), ws, lane);
+      if (lane == j) hv ^= h2;
     }
-    hv ^= vl <= 240 ? xp_short(rd, v, vl, kSeedV) : xp_lane(rd, v, vl, kSeedV);
-    const uint64_t k = k0 + idx;
-    if constexpr (!VERIFY) {
-      if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0))
-        reinterpret_cast<uint64_t*>(enc)[k] = hv;
-      else
-        for (uint32_t c = 0; c < prot_bytes; c++) enc[k * prot_bytes + c] = (uint8_t)(hv >> (8 * c));
-    } else {
-      uint64_t sv = 0;
-      for (uint32_t c = 0; c < prot_bytes; c++) sv |= (uint64_t)blk_u8(stored + k * prot_bytes + c) << (8 * c);
-      const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
-      const bool bad = sv != (hv & keep);
-      mismatch[k] = bad;
-      if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
+#endif
+    if (active) {
+      const uint64_t k = k0 + idx;
+      if constexpr (!VERIFY) {
+        if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0))
+          reinterpret_cast<uint64_t*>(enc)[k] = hv;
+        else
+          for (uint32_t c = 0; c < prot_bytes; c++) enc[k * prot_bytes + c] = (uint8_t)(hv >> (8 * c));
+      } else {
+        uint64_t sv = 0;
+        for (uint32_t c = 0; c < prot_bytes; c++) sv |= (uint64_t)blk_u8(stored + k * prot_bytes + c) << (8 * c);
+        const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
+        const bool bad = sv != (hv & keep);
+        mismatch[k] = bad;
+        if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
+      }
+      idx++;
+      p = v + vl;
+      active = p < ro;
     }
-  });
+  }
 }
 
 __global__ __launch_bounds__(64) void k_dbg_xp(const uint8_t* d, uint32_t len, uint64_t seed, uint64_t* out) {
