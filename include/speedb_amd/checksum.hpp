@@ -320,6 +320,24 @@ class FileChecksumGenCrc32cFactory {
 };
 
 // ---------------------------------------------------------------------------
+// Per-KV protection of block entries: table/block_based/block.cc:1091-1222
+// Block::Initialize{Data,Index,MetaIndex}BlockProtectionInfo for a batch of
+// uncompressed block contents (host bytes; staged to the device here).
+// kind: MCK_BLOCK_DATA / _INDEX / _INDEX_DELTA / _INDEX_DELTA_FIRST_KEY /
+// _META.  Per block: kv_checksum_ (num_keys * protection_bytes_per_key bytes,
+// ProtectionInfo64().ProtectKV(key, value).Encode(n) per entry, block.h
+// :271-274), the block's status ("bad block contents", "bad entry in block")
+// and GetRestartInterval.
+struct BlockKvChecksums {
+  std::vector<std::string> kv_checksum;
+  std::vector<Status> status;
+  std::vector<uint32_t> restart_interval;
+};
+inline Status InitializeBlockProtectionInfo(int kind, const std::vector<std::string>& blocks,
+                                            uint8_t protection_bytes_per_key, BlockKvChecksums* out,
+                                            mck_stream_t stream = nullptr);
+
+// ---------------------------------------------------------------------------
 // inline definitions of the batched helpers (need HIP for device buffers)
 // ---------------------------------------------------------------------------
 }  // namespace speedb_amd
@@ -413,6 +431,93 @@ inline bool FileChecksumGenCrc32c::UpdateDevice(const void* dev_data, uint64_t n
     return false;
   checksum_ = v;
   return true;
+}
+
+inline Status InitializeBlockProtectionInfo(int kind, const std::vector<std::string>& blocks,
+                                            uint8_t protection_bytes_per_key, BlockKvChecksums* out,
+                                            mck_stream_t stream) {
+  const uint32_t n = static_cast<uint32_t>(blocks.size());
+  out->kv_checksum.assign(n, std::string());
+  out->status.assign(n, Status::OK());
+  out->restart_interval.assign(n, 0);
+  if (!n) return Status::OK();
+  std::vector<uint64_t> offs(n);
+  std::vector<uint32_t> lens(n);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; i++) {
+    offs[i] = total;
+    lens[i] = static_cast<uint32_t>(blocks[i].size());
+    total += (blocks[i].size() + 15) & ~uint64_t(15);
+  }
+  std::string image(total + 64, '\0');
+  for (uint32_t i = 0; i < n; i++) image.replace(offs[i], blocks[i].size(), blocks[i]);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  std::vector<void*> bufs;
+  auto cleanup = [&] {
+    for (void* b : bufs) (void)hipFree(b);
+  };
+  auto alloc = [&](size_t bytes) -> void* {
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) return nullptr;
+    bufs.push_back(p);
+    return p;
+  };
+  uint8_t* d_img = static_cast<uint8_t*>(alloc(image.size()));
+  uint64_t* d_off = static_cast<uint64_t*>(alloc(n * 8));
+  uint32_t* d_len = static_cast<uint32_t*>(alloc(n * 4));
+  uint64_t* d_kb = static_cast<uint64_t*>(alloc((n + 1) * 8));
+  uint64_t* d_ab = static_cast<uint64_t*>(alloc((n + 1) * 8));
+  uint32_t* d_ri = static_cast<uint32_t*>(alloc(n * 4));
+  int32_t* d_st = static_cast<int32_t*>(alloc(n * 4));
+  void* d_scratch = alloc(mck_block_kv_scratch_bytes(n));
+  if (!d_img || !d_off || !d_len || !d_kb || !d_ab || !d_ri || !d_st || !d_scratch) {
+    cleanup();
+    return Status::IOError("hipMalloc failed");
+  }
+  (void)hipMemcpyAsync(d_img, image.data(), image.size(), hipMemcpyHostToDevice, st);
+  (void)hipMemcpyAsync(d_off, offs.data(), n * 8, hipMemcpyHostToDevice, st);
+  (void)hipMemcpyAsync(d_len, lens.data(), n * 4, hipMemcpyHostToDevice, st);
+  const mck_spans sp{d_img, d_off, d_len, 0, 0, n};
+  int rc = mck_block_kv_layout_batch(kind, &sp, d_kb, d_ab, d_ri, d_st, d_scratch, stream);
+  std::vector<uint64_t> kb(n + 1), ab(n + 1);
+  std::vector<int32_t> sts(n);
+  if (!rc) {
+    (void)hipMemcpyAsync(kb.data(), d_kb, (n + 1) * 8, hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(ab.data(), d_ab, (n + 1) * 8, hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(sts.data(), d_st, n * 4, hipMemcpyDeviceToHost, st);
+    (void)hipMemcpyAsync(out->restart_interval.data(), d_ri, n * 4, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) rc = MCK_EHIP;
+  }
+  if (rc) {
+    cleanup();
+    return FromRc(rc, "mck_block_kv_layout_batch");
+  }
+  const uint64_t keys = kb[n], pb = protection_bytes_per_key;
+  void* d_work = alloc(mck_block_kv_work_bytes(keys, ab[n]));
+  uint8_t* d_out = static_cast<uint8_t*>(alloc(keys * pb));
+  if (!d_work || !d_out) {
+    cleanup();
+    return Status::IOError("hipMalloc failed");
+  }
+  rc = mck_block_kv_protect_batch(kind, &sp, protection_bytes_per_key, d_kb, d_ab, d_ri, keys, d_work, d_out, stream);
+  std::string all(keys * pb, '\0');
+  if (!rc && keys) {
+    (void)hipMemcpyAsync(&all[0], d_out, keys * pb, hipMemcpyDeviceToHost, st);
+    if (hipStreamSynchronize(st) != hipSuccess) rc = MCK_EHIP;
+  }
+  cleanup();
+  if (rc) return FromRc(rc, "mck_block_kv_protect_batch");
+  Status first;
+  for (uint32_t i = 0; i < n; i++) {
+    out->kv_checksum[i] = all.substr(kb[i] * pb, (kb[i + 1] - kb[i]) * pb);
+    if (sts[i] != MCK_BLOCK_OK) {
+      out->status[i] = Status::Corruption(sts[i] == MCK_BLOCK_BAD_CONTENTS ? "bad block contents"
+                                          : sts[i] == MCK_BLOCK_BAD_ENTRY  ? "bad entry in block"
+                                                                           : "block restart layout not as written by BlockBuilder");
+      if (first.ok()) first = out->status[i];
+    }
+  }
+  return first;
 }
 
 inline Status VerifySstFile(const std::string& file_name, const char* image, uint64_t size,

@@ -373,6 +373,72 @@ static int VerifySstFileCase(const char* path, long bad_off) {
   return g_fail ? 1 : 0;
 }
 
+// table/block_based/block_test.cc builds blocks with BlockBuilder and checks
+// the per-KV checksums through the iterators; here: a BlockBuilder-layout
+// data block (prefix-compressed keys, restart interval 4), the batched
+// InitializeBlockProtectionInfo against ProtectionInfo64().ProtectKV per
+// entry, and a damaged block's status.
+static std::string Varint32(uint32_t v) {
+  std::string o;
+  while (v >= 128) {
+    o.push_back(static_cast<char>((v & 127) | 128));
+    v >>= 7;
+  }
+  o.push_back(static_cast<char>(v));
+  return o;
+}
+static std::string BuildBlock(const std::vector<std::pair<std::string, std::string>>& kvs, uint32_t ri) {
+  std::string buf, last;
+  std::vector<uint32_t> restarts;
+  for (size_t i = 0; i < kvs.size(); i++) {
+    const std::string& k = kvs[i].first;
+    size_t shared = 0;
+    if (i % ri == 0) {
+      restarts.push_back(static_cast<uint32_t>(buf.size()));
+    } else {
+      while (shared < k.size() && shared < last.size() && k[shared] == last[shared]) shared++;
+    }
+    buf += Varint32(static_cast<uint32_t>(shared)) + Varint32(static_cast<uint32_t>(k.size() - shared)) +
+           Varint32(static_cast<uint32_t>(kvs[i].second.size())) + k.substr(shared) + kvs[i].second;
+    last = k;
+  }
+  if (restarts.empty()) restarts.push_back(0);
+  auto fixed32 = [&](uint32_t v) {
+    for (int b = 0; b < 4; b++) buf.push_back(static_cast<char>(v >> (8 * b)));
+  };
+  for (uint32_t r : restarts) fixed32(r);
+  fixed32(static_cast<uint32_t>(restarts.size()));
+  return buf;
+}
+
+TEST(BlockProtection, DataBlockMatchesProtectKV) {
+  std::vector<std::pair<std::string, std::string>> kvs;
+  for (int i = 0; i < 37; i++) {
+    char k[32];
+    snprintf(k, sizeof k, "user_key_%06d", i * 7);
+    std::string key(k);
+    key += std::string("\x01\x02\x03\x04\x05\x06\x07\x08", 8);  // seqno/type footer
+    kvs.emplace_back(key, std::string(static_cast<size_t>((i * 53) % 400), static_cast<char>('a' + i % 26)));
+  }
+  std::vector<std::string> blocks{BuildBlock(kvs, 4), BuildBlock(kvs, 1), std::string("\x01\x00", 2)};
+  BlockKvChecksums out;
+  Status s = InitializeBlockProtectionInfo(MCK_BLOCK_DATA, blocks, 8, &out);
+  EXPECT_TRUE(s.IsCorruption());  // the third block
+  EXPECT_TRUE(out.status[0].ok());
+  EXPECT_TRUE(out.status[1].ok());
+  EXPECT_TRUE(out.status[2].IsCorruption());
+  EXPECT_EQ(out.restart_interval[0], 4u);
+  EXPECT_EQ(out.kv_checksum[2].size(), 0u);
+  for (int b = 0; b < 2; b++) {
+    EXPECT_EQ(out.kv_checksum[b].size(), kvs.size() * 8);
+    for (size_t i = 0; i < kvs.size() && out.kv_checksum[b].size() == kvs.size() * 8; i++) {
+      char want[8];
+      ProtectionInfo64().ProtectKV(kvs[i].first, kvs[i].second).Encode(8, want);
+      EXPECT_EQ(out.kv_checksum[b].substr(i * 8, 8), std::string(want, 8));
+    }
+  }
+}
+
 int main(int argc, char** argv) {
   if (mck_device_count() < 1) {
     fprintf(stderr, "no gfx950 device\n");
@@ -392,6 +458,7 @@ int main(int argc, char** argv) {
   RUN(HashTest, Hash64SmallValueSchema);
   RUN(KvChecksum, ScalarChainEqualsBatch);
   RUN(FileChecksum, Crc32cGenerator);
+  RUN(BlockProtection, DataBlockMatchesProtectKV);
   printf("%d checks, %d failures\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }
