@@ -160,6 +160,25 @@ __device__ __forceinline__ bool rd_entry_fast(const R& r, uint32_t p, uint32_t l
   return rd_entry<KIND>(r, p, lim, sh, ns, q, v, vl);
 }
 
+// rd_entry_fast with the entry's first dword already loaded (prefetched by
+// the caller right after the previous entry was decoded).
+template <int KIND, class R>
+__device__ __forceinline__ bool rd_entry_pre(const R& r, uint32_t p, uint32_t lim, uint32_t u, uint32_t* sh,
+                                             uint32_t* ns, uint32_t* q, uint32_t* v, uint32_t* vl) {
+  if (p > lim || lim - p < 3) return false;
+  if (KIND != kBlkIndexDelta && KIND != kBlkIndexDeltaFk && (u & 0x808080u) == 0) {
+    const uint32_t k = (u >> 8) & 255u, x = (u >> 16) & 255u;
+    if (lim - (p + 3) < k + x) return false;
+    *sh = u & 255u;
+    *ns = k;
+    *q = p + 3;
+    *v = p + 3 + k;
+    *vl = x;
+    return true;
+  }
+  return rd_entry<KIND>(r, p, lim, sh, ns, q, v, vl);
+}
+
 // Walk of one restart interval [start, end): entry count, reassembled key
 // bytes and the first error, as code (r << 2 | stage): stage 0 bad entry,
 // 1 shared != 0 at a restart point past the first (the reference would reuse
@@ -806,11 +825,15 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
   const XpWaveSec ws = xp_wave_sec(lane, kSeedV);
 #endif
   uint32_t p = 0, idx = 0;
+  uint32_t u = active ? rd.u32(0) : 0;  // the next entry's first dword, one entry ahead
   while (__any(active)) {
     uint32_t sh = 0, ns = 0, q = 0, v = 0, vl = 0;
     uint64_t hv = 0;
     if (active) {
-      rd_entry_fast<KIND>(rd, p, ro, &sh, &ns, &q, &v, &vl);
+      rd_entry_pre<KIND>(rd, p, ro, u, &sh, &ns, &q, &v, &vl);
+      // prefetch: the following entry's header travels with this entry's
+      // key and value loads (one dependent round trip per entry, not two)
+      if (v + vl < ro) u = rd.u32(v + vl);
       const uint32_t kl = sh + ns;
       if (!global_key && kl > kBlkKeyBuf) {  // rare: move the prefix to the arena
         for (uint32_t i = 0; i < sh; i++) gkey[i] = lkey[i];
@@ -818,7 +841,12 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
       }
       // IterKey::TrimAppend: only the non-shared bytes change
       if (!global_key) {
-        for (uint32_t i = sh; i < kl; i++) lkey[i] = (uint8_t)rd.u8(q + i - sh);
+        // the delta in dword loads (a dword may reach 3 bytes past it: the
+        // value or the restart array follows)
+        for (uint32_t i = sh; i < kl; i += 4) {
+          const uint32_t w = rd.u32(q + i - sh);
+          for (uint32_t c = 0; c < 4 && i + c < kl; c++) lkey[i + c] = (uint8_t)(w >> (8 * c));
+        }
         const LdsRd kr{s_key[threadIdx.x], 0};
         hv = xp_short(kr, 0, kl, kSeedK);
       } else {
