@@ -535,6 +535,53 @@ __device__ __forceinline__ uint64_t xp_wave_long(const R& r, uint32_t o, uint32_
   return xxph3_avalanche((uint64_t)len * P64_1 + readlane_u64(t, 0));
 }
 
+// XXPH3 long loop (len > 240) of FOUR spans at once, one per 16-lane row:
+// lane = 16 row + 8 g + l folds accumulator l over the stripes s = g, g + 2,
+// ..., g + 14 of each 1 KiB segment (8 loads per segment, all issued
+// together), the two stripe groups are summed with one DPP-free shuffle and
+// the scramble / last stripe / merge follow the wave version.  `sec` is the
+// seeded secret in LDS as 24 u64 words (word w = bytes 8w of
+// XXPH3_initCustomSecret); klast / km: this lane's last-stripe and merge
+// secret words.  Result valid on every lane of the row.
+template <class R>
+__device__ __forceinline__ uint64_t xp_row_long(const R& r, uint32_t o, uint32_t len, const uint64_t* sec,
+                                                uint64_t klast, uint64_t km, uint32_t lane) {
+  const uint32_t l = lane & 7, g = (lane >> 3) & 1;
+  uint64_t acc = l < 4 ? (l < 2 ? (l ? P64_1 : (uint64_t)P32_3) : (l == 2 ? P64_2 : P64_3))
+                       : (l < 6 ? (l == 4 ? P64_4 : (uint64_t)P32_2) : (l == 6 ? P64_5 : (uint64_t)P32_1));
+  const uint32_t nb = len / 1024, nst = (len - 1024 * nb) / 64;
+  for (uint32_t b = 0; b <= nb; b++) {
+    const uint32_t base = o + 1024 * b + 64 * g + 8 * l;
+    uint64_t part = 0;
+#pragma unroll
+    for (uint32_t m = 0; m < 8; m++) {
+      const uint32_t st = g + 2 * m;
+      if (b < nb || st < nst) {
+        const uint64_t d = r.u64(base + 128 * m);
+        part += d + mul32to64(d ^ sec[st + l]);
+      }
+    }
+    const uint64_t other = __shfl_xor(part, 8, 64);
+    acc += part + other;
+    if (b < nb) {
+      acc ^= acc >> 47;
+      acc ^= sec[16 + l];
+      acc *= P32_1;
+    }
+  }
+  if (len & 63) {
+    const uint64_t d = r.u64(o + len - 64 + 8 * l);
+    acc += d + mul32to64(d ^ klast);
+  }
+  const uint64_t other = __shfl_xor(acc, 1, 64), mo = __shfl_xor(km, 1, 64);
+  const uint64_t f = mul128_fold64(acc ^ km, other ^ mo);
+  uint64_t t = (l & 1) ? 0 : f;
+  t += __shfl_xor(t, 2, 64);
+  t += __shfl_xor(t, 4, 64);
+  const uint64_t t0 = __shfl(t, (int)(lane & ~15u), 64);
+  return xxph3_avalanche((uint64_t)len * P64_1 + t0);
+}
+
 // Pass 2 for one block.  Lane r walks restart interval r, writing one
 // descriptor per entry {shared, non_shared, key delta offset, value length}
 // at its entry index (r * restart_interval + k).  Then lane e takes entry e:
@@ -792,16 +839,22 @@ __global__ __launch_bounds__(256) void k_block_layout_t(SpanSrc blocks, uint32_t
 constexpr uint32_t kBlkKeyBuf = 128;  // bytes of LDS key buffer per thread
 // The lanes step through their blocks' entries together (one entry per lane
 // per iteration); values of kBlkWaveLong bytes or more are not hashed per lane -- 8-byte loads
-// from 64 different blocks per instruction, far from coalesced -- but by the
-// whole wave, one at a time (xp_wave_long: every load instruction reads 512
-// contiguous bytes of the value).  -DMCK_BLK_LANE_LONG=1: per lane (A/B).
-// Measured (1M blocks): 1000-B values 2.41 vs 2.70 ms per step (wave vs
-// lane), 300-B values 5.69 vs 4.37 ms -- so the wave takes values of
-// kBlkWaveLong bytes and more.
+// from 64 different blocks per instruction, far from coalesced -- but four
+// at a time, one per 16-lane row (xp_row_long: each load instruction reads
+// 128 contiguous bytes of each of four values).  -DMCK_BLK_LANE_LONG=1: per
+// lane; -DMCK_BLK_LONG_MIN=n: the threshold (A/B).
+// Measured (1M blocks, ms per step): whole-wave hashing one value at a time
+// lost to per lane below 512 B (300-B values 5.69 vs 4.37); one value per
+// 16-lane row, four at a time (xp_row_long), wins everywhere: 1000-B values
+// 2.01 (wave 2.41, lane 2.70), 500-B 2.68 (lane 3.36), 300-B 3.41 (lane
+// 4.05) -- so every value over 240 B goes to the rows.
 #ifndef MCK_BLK_LANE_LONG
 #define MCK_BLK_LANE_LONG 0
 #endif
-constexpr uint32_t kBlkWaveLong = 512;
+#ifndef MCK_BLK_LONG_MIN
+#define MCK_BLK_LONG_MIN 241
+#endif
+constexpr uint32_t kBlkWaveLong = MCK_BLK_LONG_MIN;
 template <int KIND, bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t count, const uint64_t* key_base,
                                                     const uint64_t* arena_base, uint8_t* arena, uint32_t prot_bytes,
@@ -822,7 +875,12 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
   const GblRd rd{active ? blocks.ptr(b) : nullptr};
   const uint32_t ro = active ? rd_header(rd, blocks.len(b)).ro : 0;  // the layout pass validated the block
 #if !MCK_BLK_LANE_LONG
-  const XpWaveSec ws = xp_wave_sec(lane, kSeedV);
+  __shared__ uint64_t s_sec[24];  // XXPH3_initCustomSecret(kSeedV) as u64 words
+  if (threadIdx.x < 24) s_sec[threadIdx.x] = csec64(8 * (int)threadIdx.x, kSeedV);
+  __syncthreads();
+  const uint32_t l8 = lane & 7;
+  const uint64_t klast = csec64(121 + 8 * (int)l8, kSeedV);
+  const uint64_t km = csec64((l8 & 1) ? 19 + 16 * (int)(l8 >> 1) : 11 + 16 * (int)(l8 >> 1), kSeedV);
 #endif
   uint32_t p = 0, idx = 0;
   uint32_t u = active ? rd.u32(0) : 0;  // the next entry's first dword, one entry ahead
@@ -861,14 +919,29 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
 #endif
     }
 #if !MCK_BLK_LANE_LONG
+    // long values four at a time, one per 16-lane row (xp_row_long)
     uint64_t longs = __ballot(active && vl >= kBlkWaveLong);
     const uint64_t va = reinterpret_cast<uint64_t>(rd.p) + v;
     while (longs) {
-      const uint32_t j = (uint32_t)__builtin_ctzll(longs);
-      longs &= longs - 1;
-      const uint64_t h2 = xp_wave_long(GblRd{reinterpret_cast<const uint8_t*>(readlane_u64(va, j))}, 0,
-                                       readlane_u32(vl, j), ws, lane);
-      if (lane == j) hv ^= h2;
+      uint32_t js[4] = {64, 64, 64, 64};
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+        if (longs) {
+          js[k] = (uint32_t)__builtin_ctzll(longs);
+          longs &= longs - 1;
+        }
+      const uint32_t row = lane >> 4;
+      const uint32_t src = row == 0 ? js[0] : row == 1 ? js[1] : row == 2 ? js[2] : js[3];
+      const uint32_t srcl = src < 64 ? src : 0u;
+      const uint64_t va_r = __shfl(va, (int)srcl, 64);
+      const uint32_t vl_r = (uint32_t)__shfl((int)vl, (int)srcl, 64);
+      uint64_t h2 = 0;
+      if (src < 64) h2 = xp_row_long(GblRd{reinterpret_cast<const uint8_t*>(va_r)}, 0, vl_r, s_sec, klast, km, lane);
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint64_t hk = __shfl(h2, 16 * k, 64);
+        if (lane == js[k]) hv ^= hk;
+      }
     }
 #endif
     if (active) {
@@ -901,11 +974,20 @@ __global__ __launch_bounds__(64) void k_dbg_xp(const uint8_t* d, uint32_t len, u
   const uint64_t b = xp_lane(GblRd{d}, 0, len, seed);
   uint64_t c = 0;
   if (len <= kBlkSlot) c = xp_wave_long(blk_stage(d, len, slot, lane), 0, len, ws, lane);
+  // row k of the wave hashes the span's first len - 61 k bytes
+  __shared__ uint64_t sec[24];
+  if (lane < 24) sec[lane] = csec64(8 * (int)lane, seed);
+  __syncthreads();
+  const uint32_t l8 = lane & 7;
+  const uint64_t klast = csec64(121 + 8 * (int)l8, seed);
+  const uint64_t km = csec64((l8 & 1) ? 19 + 16 * (int)(l8 >> 1) : 11 + 16 * (int)(l8 >> 1), seed);
+  const uint64_t r = xp_row_long(GblRd{d}, 0, len - 61 * (lane >> 4), sec, klast, km, lane);
   if (lane == 0) {
     out[0] = a;
     out[1] = b;
     out[2] = c;
   }
+  if ((lane & 15) == 0) out[3 + (lane >> 4)] = r;
 }
 
 // ---- exclusive scan of two u64 arrays (key counts, key bytes) --------------

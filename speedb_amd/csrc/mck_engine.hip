@@ -1313,7 +1313,8 @@ int mck_block_kv_verify_batch(int kind, const mck_spans* blocks, uint32_t prot_b
 
 // Internal test hook (not part of mck.h): XXPH3 of one device span by the
 // block kernels' wave-cooperative long loop, the per-lane loop, and the wave
-// loop over an LDS-staged copy: out[0..2].
+// loop over an LDS-staged copy: out[0..2]; out[3 + k] = the row-cooperative
+// loop (xp_row_long) over the first len - 61 k bytes, k = 0..3.
 int mck_internal_xp_wave(const void* data, uint32_t len, uint64_t seed, uint64_t* out, mck_stream_t stream) {
   if (int rc = current_device(nullptr, nullptr)) return rc;
   hipLaunchKernelGGL(k_dbg_xp, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),

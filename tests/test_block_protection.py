@@ -307,9 +307,10 @@ def test_block_protection_abi_errors():
 
 @pytest.mark.gpu
 def test_wave_xxph3_long_loop(gpu, oracle):
-    """The block kernel's wave-cooperative XXPH3 long loop (8 accumulators x
-    8 stripe groups), its per-lane loop and the LDS-staged wave loop against
-    Hash64 (mck_internal_xp_wave, an internal test hook)."""
+    """The block kernels' cooperative XXPH3 long loops -- wave (8
+    accumulators x 8 stripe groups), per lane, LDS-staged wave, and four
+    spans of different lengths on the four 16-lane rows -- against Hash64
+    (mck_internal_xp_wave, an internal test hook)."""
     import ctypes
     from speedb_amd._lib import lib
     torch = gpu
@@ -317,8 +318,8 @@ def test_wave_xxph3_long_loop(gpu, oracle):
     f.restype = ctypes.c_int
     f.argtypes = [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
     rnd = random.Random(1)
-    out = torch.zeros(3, dtype=torch.int64, device="cuda")
-    for n in (241, 255, 256, 300, 1000, 1023, 1024, 1025, 2100, 5000, 6144):
+    out = torch.zeros(7, dtype=torch.int64, device="cuda")
+    for n in (425, 426, 500, 1000, 1023, 1024, 1025, 1087, 1088, 2100, 5000, 6144):
         b = bytes(rnd.getrandbits(8) for _ in range(n))
         d = torch.frombuffer(bytearray(bytes(rnd.randrange(16)) + b + bytes(64)), dtype=torch.uint8).cuda()
         off = d.numel() - 64 - n
@@ -326,7 +327,8 @@ def test_wave_xxph3_long_loop(gpu, oracle):
             assert f(d.data_ptr() + off, n, seed, out.data_ptr(), None) == 0
             r = [x & (2 ** 64 - 1) for x in out.cpu().tolist()]
             want = oracle.Hash64(b, seed)
-            assert r == [want, want, want], (n, seed)
+            assert r[:3] == [want, want, want], (n, seed)
+            assert r[3:] == [oracle.Hash64(b[:n - 61 * k], seed) for k in range(4)], (n, seed)
 
 
 @pytest.mark.gpu
