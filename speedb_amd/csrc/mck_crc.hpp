@@ -71,9 +71,13 @@ constexpr uint32_t kCrcLdsBytes = kLdsUnshift + kMaxUnshift * 512;  // 163840
 static_assert(offsetof(CrcTables, gap) - offsetof(CrcTables, lane_final) == kLdsGap - kLdsFinal, "layout");
 static_assert(offsetof(CrcTables, unshift) - offsetof(CrcTables, lane_final) == kLdsLowEnd - kLdsFinal, "layout");
 
-struct alignas(16) Chunk {
-  uint4 v[4];
+// A lane's chunk of P 16-byte pieces (the wave driver and the row driver
+// use P = 4; the one-pass WAL writer's rows P = 5).
+template <int P = 4>
+struct alignas(16) ChunkN {
+  uint4 v[P];
 };
+using Chunk = ChunkN<4>;
 
 // The kernels declare no static __shared__, so the dynamic LDS image starts
 // at LDS address 0 and table addresses are absolute: reading through an
@@ -818,9 +822,11 @@ __device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUnifor
 // LDS: the wave driver's image plus the 960-byte row gap map, the init
 // tables and the descriptor cache, all below the step tables.
 constexpr uint32_t kLdsRowGap = kLdsLowEnd;  // 3 x 512 B (W = 4, 8, 16), below the step tables
-template <int W>
+template <int W, int P = 4>
 constexpr uint32_t row_gap_off() {
-  return kLdsRowGap + 512u * (W == 4 ? 0 : W == 8 ? 1 : 2);
+  // P = 5 (80-byte chunks, W = 16 only): the kernel overwrites the W = 4 map
+  // with CrcTables::gap80 (wal_write_rows)
+  return P == 5 ? kLdsRowGap : kLdsRowGap + 512u * (W == 4 ? 0 : W == 8 ? 1 : 2);
 }
 // How the row driver gets a span's CRC init (Extend's init_crc):
 //   kInitZero  -- always 0 (Value): ~init is injected from a 64-entry LDS
@@ -897,9 +903,15 @@ __device__ __forceinline__ void row_init_tables(const Op& op) {
   }
 }
 
-template <int W>
+// P pieces per lane chunk: Q = 16 P bytes per lane, rounds of Q W bytes.
+// P = 4: inj = unshift(~init, hb), injected at the chunk's start.  P = 5: hb
+// can reach 79, past the 64-entry init table, so inj = unshift(~init,
+// hb & 15) and row_round injects it at piece hb >> 4 instead (the owner's
+// pieces before it are zero, so the two are the same state).
+template <int W, int P = 4>
 __device__ __forceinline__ RowSpan row_span(uint64_t ptr, uint32_t n, uint32_t key, int kind) {
-  constexpr uint32_t R = 64u * W;
+  static_assert(P == 4 || (P == 5 && W == 16), "chunk pieces");
+  constexpr uint32_t Q = 16u * P, R = Q * W;
   RowSpan s;
   s.ptr = ptr;
   s.n = n;
@@ -909,14 +921,15 @@ __device__ __forceinline__ RowSpan row_span(uint64_t ptr, uint32_t n, uint32_t k
   const uint32_t cover = (uint32_t)(s.a1 - ptr);
   s.rounds = n == 0 ? 1 : (int32_t)((cover + R - 1) / R);
   const uint32_t lead = R * (uint32_t)s.rounds - cover;
-  s.owner = n == 0 ? W : (int32_t)(lead >> 6);
-  s.hb = lead & 63u;
+  s.owner = n == 0 ? W : (int32_t)(lead / Q);
+  s.hb = lead % Q;
+  const uint32_t hk = P == 4 ? s.hb : (s.hb & 15u);
   if (kind == kInitArray) {  // wave-uniform
     s.init = key;
-    s.inj = crc_unshift(s.hb, ~key);  // unshift by 0 is the identity
+    s.inj = crc_unshift(hk, ~key);  // unshift by 0 is the identity
   } else {
     const uint32_t t = kind == kInitTyped ? (key & 15u) : 0u;
-    s.inj = *lds_p32(kLdsRowInj + 4 * (t * 64 + s.hb));
+    s.inj = *lds_p32(kLdsRowInj + 4 * (t * 64 + hk));
     s.init = *lds_p32(kLdsRowInit + 4 * t);
   }
   return s;
@@ -941,15 +954,16 @@ __device__ __forceinline__ RowSpan row_span_sel(bool a, const RowSpan& x, const 
 // pieces wholly before a0 read the zero piece `zp` instead, so they need no
 // masking (and lanes before the owner hash zeros); only the piece at a0
 // keeps ptr - a0 < 16 bytes of another span to mask (row_round).
-template <int W>
-__device__ __forceinline__ Chunk row_load_chunk(const RowSpan& sp, int r, uint32_t c, uint64_t zp) {
-  const uint64_t b = sp.a1 - 64ull * W * (uint32_t)(r + 1) + 64ull * c;
+template <int W, int P = 4>
+__device__ __forceinline__ ChunkN<P> row_load_chunk(const RowSpan& sp, int r, uint32_t c, uint64_t zp) {
+  constexpr uint64_t Q = 16u * P;
+  const uint64_t b = sp.a1 - Q * W * (uint32_t)(r + 1) + Q * c;
   const bool first = r == sp.rounds - 1;
-  // first round: b >= a0 - 64 W, so the low words give the exact offset
+  // first round: b >= a0 - Q W, so the low words give the exact offset
   const int32_t rel = first ? (int32_t)((uint32_t)b - (uint32_t)sp.a0) : 0;
-  Chunk ch;
+  ChunkN<P> ch;
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
+  for (int j = 0; j < P; j++) {
     const uint64_t a = rel < -16 * j ? zp : b + 16ull * j;
     ch.v[j] = span_load16<false>(a);
   }
@@ -967,8 +981,8 @@ __device__ __forceinline__ void and4(uint4& v, const uint4& m) {
   v.w &= m.w;
 }
 
-template <int W>
-__device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpan& sp, int r, uint32_t c,
+template <int W, int P = 4>
+__device__ __forceinline__ uint32_t row_round(uint32_t s, ChunkN<P> ch, const RowSpan& sp, int r, uint32_t c,
                                               const CrcLane& L) {
   const bool first = r == sp.rounds - 1;
   const bool own = (int32_t)c == sp.owner;
@@ -979,24 +993,39 @@ __device__ __forceinline__ uint32_t row_round(uint32_t s, Chunk ch, const RowSpa
   const uint32_t h0 = (uint32_t)sp.ptr & 15u;  // bytes of the a0 piece before ptr
   const uint4 mh = lds_u32x4(kLdsRowMaskHead + 16 * h0);
   const uint4 mt = lds_u32x4(kLdsRowMaskTail + 16 * ((r == 0 && c == W - 1) ? sp.kt : 0u));
-  const uint32_t pa = (first && own) ? sp.hb >> 4 : 4u;
+  const uint32_t pa = (first && own) ? sp.hb >> 4 : (uint32_t)P;
+  uint32_t sels[P];
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
+  for (int j = 0; j < P; j++) {
     const uint32_t sel = (uint32_t)j == pa ? ~0u : 0u;
+    sels[j] = sel;
     ch.v[j].x = __builtin_amdgcn_bitop3_b32(ch.v[j].x, mh.x, sel, 0xD0);
     ch.v[j].y = __builtin_amdgcn_bitop3_b32(ch.v[j].y, mh.y, sel, 0xD0);
     ch.v[j].z = __builtin_amdgcn_bitop3_b32(ch.v[j].z, mh.z, sel, 0xD0);
     ch.v[j].w = __builtin_amdgcn_bitop3_b32(ch.v[j].w, mh.w, sel, 0xD0);
   }
-  and4(ch.v[3], mt);
+  and4(ch.v[P - 1], mt);
   uint32_t gap = 0;
-  if (wave_any(!first)) gap = crc_nibmap(row_gap_off<W>(), s);
-  uint32_t x = first ? (own ? sp.inj : 0u) : gap;
+  if (wave_any(!first)) gap = crc_nibmap(row_gap_off<W, P>(), s);
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&ch.v[0]);
-  x ^= w[0];
+  if constexpr (P == 4) {
+    uint32_t x = first ? (own ? sp.inj : 0u) : gap;
+    x ^= w[0];
 #pragma unroll
-  for (int k = 0; k < 16; k++) x = crc_step4x(x, L, k < 15 ? w[k + 1] : 0u);
-  return x;
+    for (int k = 0; k < 16; k++) x = crc_step4x(x, L, k < 15 ? w[k + 1] : 0u);
+    return x;
+  } else {
+    // P = 5: the init enters at the owner's piece pa (sels[pa] is all-ones)
+    const uint32_t inj = sp.inj;
+    uint32_t x = (first ? 0u : gap) ^ w[0] ^ (sels[0] & inj);
+#pragma unroll
+    for (int k = 0; k < 4 * P; k++) {
+      uint32_t nw = 0u;
+      if (k + 1 < 4 * P) nw = ((k + 1) & 3) ? w[k + 1] : (w[k + 1] ^ (sels[(k + 1) >> 2] & inj));
+      x = crc_step4x(x, L, nw);
+    }
+    return x;
+  }
 }
 
 // XOR over the W lanes of each row, in every lane of the row (DPP).

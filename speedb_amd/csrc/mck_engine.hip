@@ -858,6 +858,16 @@ static int wal_row_lanes() {
   return v;
 }
 
+// Lane chunk of the 16-lane one-pass writer: MCK_WAL_CHUNK=64 or 80 (default:
+// 1280-byte rounds, one per ~1 KB fragment).
+static int wal_chunk() {
+  static const int v = [] {
+    const char* e = getenv("MCK_WAL_CHUNK");
+    return e && atoi(e) == 64 ? 64 : 80;
+  }();
+  return v;
+}
+
 // pieces of at least 16 fragments per CU (one CRC grid's worth of spans)
 static uint32_t wal_pieces_for(uint32_t nfrags, int ncu) {
   uint32_t pieces = wal_pieces();
@@ -894,8 +904,11 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   if (wal_fused()) {
     // one pass: CRC + log stream in k_wal_write_rows, in launches of at most
     // ncu * kRowDescCache fragments (its LDS descriptor / dst_off tables)
-    const bool w8 = wal_row_lanes() == 8;
-    if (int rc = w8 ? ensure_lds(k_wal_write_rows<8>, dev) : ensure_lds(k_wal_write_rows<16>, dev)) return rc;
+    const bool w8 = wal_row_lanes() == 8, q80 = !w8 && wal_chunk() == 80;
+    if (int rc = w8    ? ensure_lds(k_wal_write_rows<8>, dev)
+                 : q80 ? ensure_lds(k_wal_write_rows<16, 5>, dev)
+                       : ensure_lds(k_wal_write_rows<16>, dev))
+      return rc;
     const uint32_t cap = (uint32_t)ncu * kRowDescCache;
     const uint32_t nl = (nfrags + cap - 1) / cap;
     const uint32_t per = (uint32_t)(((uint64_t)nfrags + nl - 1) / nl);
@@ -905,6 +918,8 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
       const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
       if (w8)
         hipLaunchKernelGGL(k_wal_write_rows<8>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+      else if (q80)
+        hipLaunchKernelGGL((k_wal_write_rows<16, 5>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
       else
         hipLaunchKernelGGL(k_wal_write_rows<16>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
       MCK_HIP(hipGetLastError());

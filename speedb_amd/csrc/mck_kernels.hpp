@@ -602,11 +602,18 @@ __device__ __forceinline__ void st_nt16(uint64_t a, uint4 o) {
   } while (0)
 #endif
 
-// W = 8 or 16 lanes per row.
-template <int W>
+// W = 8 or 16 lanes per row; NP = 4 pieces (64-byte lane chunks) or, with
+// W = 16, NP = 5: 80-byte chunks, 1280-byte rounds, so a fragment of up to ~1250
+// bytes (the ~1 KB records of the WAL) takes one round instead of two.  The
+// NP = 5 rows use their own lane-final and gap maps (CrcTables::lane_final80
+// / gap80), loaded over LDS tables these rows never read: lane-final columns
+// 0-15 (16-lane rows read columns 48-63) and the W = 4 gap map.
+template <int W, int NP = 4>
 __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                const CrcTables* __restrict__ g) {
   static_assert(W == 8 || W == 16, "row width");
+  static_assert(NP == 4 || (NP == 5 && W == 16), "chunk pieces");
+  constexpr uint64_t Q = 16u * NP;  // lane chunk bytes
   constexpr int kHT = 16 / W;  // head / tail payload bytes per lane (< 16 each)
   constexpr int kHdr = 32 / W;  // padding + header bytes per lane (pad + hs <= 21)
   crc_rows_prologue(op, first, count, lds, g, false);
@@ -616,10 +623,20 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
     for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
       *lds_p64(kLdsWalAux + 8 * t) = op.frags[first + b + G * t].dst_off;
   }
+  if (NP == 5) {  // 80-byte-chunk maps: [n][v] rows of 16 lane-final columns, then the gap map
+    const uint32_t t = threadIdx.x;
+    if (t < 512) {
+      const uint4 x = reinterpret_cast<const uint4*>(&g->lane_final80[0][0][0])[t];
+      *reinterpret_cast<uint4*>(lds + kLdsFinal + 256 * (t >> 2) + 16 * (t & 3)) = x;
+    } else if (t < 544) {
+      const uint4 x = reinterpret_cast<const uint4*>(&g->gap80[0][0])[t - 512];
+      *reinterpret_cast<uint4*>(lds + row_gap_off<W, NP>() + 16 * (t - 512)) = x;
+    }
+  }
   __syncthreads();
   const CrcLane L = crc_lane();
   const uint32_t c = threadIdx.x & (W - 1);
-  const uint32_t lf4 = (64u - W + c) << 2;  // lane-final table column
+  const uint32_t lf4 = (NP == 5 ? c : 64u - W + c) << 2;  // lane-final table column
   const uint32_t G = gridDim.x;
   const uint32_t share = (count - blockIdx.x + G - 1) / G;
   const uint64_t base = reinterpret_cast<uint64_t>(op.src);
@@ -634,10 +651,10 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
   uint4 d = row_desc(t, share);
   uint64_t dst = *lds_p64(kLdsWalAux + 8 * (t < share ? t : 0));
   uint32_t i = first + blockIdx.x + G * (live ? t : 0);
-  RowSpan sp = row_span<W>(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kInitTyped);
+  RowSpan sp = row_span<W, NP>(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kInitTyped);
   uint32_t key = d.w;
   int r = sp.rounds - 1;
-  Chunk cur = row_load_chunk<W>(sp, r, c, zp);
+  ChunkN<NP> cur = row_load_chunk<W, NP>(sp, r, c, zp);
   uint32_t nt = row_ticket<W>(true);
   uint4 nd = row_desc(nt, share);
   uint64_t ndst = *lds_p64(kLdsWalAux + 8 * (nt < share ? nt : 0));
@@ -657,15 +674,15 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
     const uint64_t delta = P - ps;                   // (mod 2^64)
     const uint32_t e = (uint32_t)(0ull - delta) & 15u;
     const uint32_t be = e & 3u;
-    const uint64_t S = sp.a1 - 64ull * W * (uint32_t)(r + 1);  // the row's source window
-    uint4 v[4];
-    uint32_t w5[4];
-    bool ok[4];
+    const uint64_t S = sp.a1 - Q * W * (uint32_t)(r + 1);  // the row's source window
+    uint4 v[NP];
+    uint32_t w5[NP];
+    bool ok[NP];
     // lane c's pieces: the window's output-aligned pieces c, c + W, c + 2W,
-    // c + 3W -- each load and store instruction covers 16 W contiguous bytes
+    // ... -- each load and store instruction covers 16 W contiguous bytes
     const uint64_t x0 = S + e + 16ull * c;
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < NP; j++) {
       const uint64_t x = x0 + 16ull * W * j;
       ok[j] = live && x >= ps && x + 16 <= pe && !(MCK_WAL_EXP & 1);
       const uint64_t f = ok[j] && !(MCK_WAL_EXP & 16) ? (x & ~3ull) : zp;
@@ -692,7 +709,7 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
     }
 
 #pragma unroll
-    for (int j = 0; j < 4; j++) {
+    for (int j = 0; j < NP; j++) {
       uint4 o;
       o.x = __builtin_amdgcn_alignbyte(v[j].y, v[j].x, be);
       o.y = __builtin_amdgcn_alignbyte(v[j].z, v[j].y, be);
@@ -708,14 +725,14 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
 
     // ---- next unit (as crc_rows_loop) ----
     const bool go = live && (!last || nt < share);
-    const RowSpan nsp = row_span<W>(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kInitTyped);
+    const RowSpan nsp = row_span<W, NP>(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kInitTyped);
     const bool sw = go && last;
     const RowSpan lsp = row_span_sel(sw, nsp, sp);
     const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
     const uint32_t li = sw ? first + blockIdx.x + G * nt : i;
-    const Chunk nxt = row_load_chunk<W>(lsp, lr, c, zp);
+    const ChunkN<NP> nxt = row_load_chunk<W, NP>(lsp, lr, c, zp);
 
-    s = row_round<W>(s, cur, sp, r, c, L);
+    s = row_round<W, NP>(s, cur, sp, r, c, L);
     uint32_t crc = 0;
     if (wave_any(fin)) crc = crc_mask(row_finish4<W>(s, sp, lf4));
     WAL_ST(fin && c == 0, st_u32, reinterpret_cast<uint64_t>(op.crcs + i), sink + 4, crc);
@@ -755,10 +772,10 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
   }
 }
 
-template <int W>
+template <int W, int NP = 4>
 __global__ __launch_bounds__(1024) void k_wal_write_rows(OpWalWrite op, uint32_t first, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  wal_write_rows<W>(op, first, count, lds, &g_crc_tables);
+  wal_write_rows<W, NP>(op, first, count, lds, &g_crc_tables);
 }
 
 // The physical record image: [pad zeros][crc LE32][len LE16][type]

@@ -35,6 +35,10 @@ struct CrcTables {
   uint32_t unshift[kMaxUnshift][8][16];  // zshift^-1(v << 4n, k)
   uint32_t gap_row[kRowWidths][8][16];  // zshift(v << 4n, 64 (W - 1)): row driver
   uint32_t zero16[4];             // a zero piece: the row driver's loads before a span
+  // 80-byte lane chunks in 16-lane rows (the one-pass WAL writer: a 1280-byte
+  // round holds a whole ~1 KB record fragment)
+  uint32_t lane_final80[8][16][16];  // zshift(v << 4n, 80 (15 - c))
+  uint32_t gap80[8][16];             // zshift(v << 4n, 80 * 15)
 };
 
 // ---- host-side GF(2) helpers (also used by the host shims) ----------------
@@ -86,6 +90,16 @@ inline void build_crc_tables(CrcTables* t) {
     const uint32_t kr = gf_xpow8n(row_gap_bytes(k));
     for (int n = 0; n < 8; n++)
       for (int v = 0; v < 16; v++) t->gap_row[k][n][v] = gf_mul((uint32_t)v << (4 * n), kr);
+  }
+  for (int c = 0; c < 16; c++) {
+    const uint32_t k = gf_xpow8n(80u * (15 - c));
+    for (int n = 0; n < 8; n++)
+      for (int v = 0; v < 16; v++) t->lane_final80[n][v][c] = gf_mul((uint32_t)v << (4 * n), k);
+  }
+  {
+    const uint32_t k = gf_xpow8n(80u * 15);
+    for (int n = 0; n < 8; n++)
+      for (int v = 0; v < 16; v++) t->gap80[n][v] = gf_mul((uint32_t)v << (4 * n), k);
   }
   for (int k = 0; k < kMaxUnshift; k++)
     for (int n = 0; n < 8; n++)

@@ -128,6 +128,23 @@ def test_wal_write_batch_two_kernel_paths_subprocess(gpu, pieces):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("env", [{"MCK_WAL_CHUNK": "64"}, {"MCK_WAL_ROW_LANES": "8"}])
+def test_wal_write_batch_row_shapes_subprocess(gpu, env):
+    """The one-pass writer's other row shapes -- 64-byte lane chunks (two
+    1 KiB rounds per ~1 KB fragment) and 8-lane rows -- in a child process:
+    byte-exact too (the default is 16-lane rows of 80-byte chunks)."""
+    if any(os.environ.get(k) for k in ("MCK_WAL_CHUNK", "MCK_WAL_ROW_LANES", "MCK_WAL_FUSED")):
+        pytest.skip("already running a non-default writer")
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
+                        "-k", "not subprocess", os.path.join(here, "test_wal_writer.py")],
+                       env=dict(os.environ, **env), cwd=os.path.dirname(here), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout, r.stdout[-500:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("recycle", [False, True])
 def test_wal_write_batch_small_records_every_alignment(gpu, oracle, recycle):
     """Records of 0..80 bytes (a payload inside one output piece, head and
