@@ -954,6 +954,11 @@ __device__ __forceinline__ RowSpan row_span_sel(bool a, const RowSpan& x, const 
 // pieces wholly before a0 read the zero piece `zp` instead, so they need no
 // masking (and lanes before the owner hash zeros); only the piece at a0
 // keeps ptr - a0 < 16 bytes of another span to mask (row_round).
+// MCK_ROW_LOAD_ZERO=1 (timing experiments only, wrong output): every piece
+// reads the zero piece.
+#ifndef MCK_ROW_LOAD_ZERO
+#define MCK_ROW_LOAD_ZERO 0
+#endif
 template <int W, int P = 4>
 __device__ __forceinline__ ChunkN<P> row_load_chunk(const RowSpan& sp, int r, uint32_t c, uint64_t zp) {
   constexpr uint64_t Q = 16u * P;
@@ -964,7 +969,7 @@ __device__ __forceinline__ ChunkN<P> row_load_chunk(const RowSpan& sp, int r, ui
   ChunkN<P> ch;
 #pragma unroll
   for (int j = 0; j < P; j++) {
-    const uint64_t a = rel < -16 * j ? zp : b + 16ull * j;
+    const uint64_t a = rel < -16 * j || MCK_ROW_LOAD_ZERO ? zp : b + 16ull * j;
     ch.v[j] = span_load16<false>(a);
   }
   return ch;
