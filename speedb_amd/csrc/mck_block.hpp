@@ -474,6 +474,66 @@ __device__ __forceinline__ uint64_t xp_mid_fold(const uint64_t (&d)[16], uint32_
   return xxph3_avalanche(acc);
 }
 
+// 64-bit sum over the 8 lanes of each lane octet (DPP: quad swaps, then the
+// half-row mirror), in every lane of the octet.
+__device__ __forceinline__ uint64_t oct_sum_u64(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#define MCK_OCT_STEP(CTRL)                                                              \
+  {                                                                                     \
+    const uint32_t xl = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, CTRL, 0xF, 0xF, false); \
+    const uint32_t xh = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, CTRL, 0xF, 0xF, false); \
+    const uint64_t s = ((uint64_t)hi << 32 | lo) + ((uint64_t)xh << 32 | xl);              \
+    lo = (uint32_t)s;                                                                   \
+    hi = (uint32_t)(s >> 32);                                                           \
+  }
+  MCK_OCT_STEP(0xB1)   // quad_perm [1,0,3,2]
+  MCK_OCT_STEP(0x4E)   // quad_perm [2,3,0,1]
+  MCK_OCT_STEP(0x141)  // row_half_mirror
+#undef MCK_OCT_STEP
+  return (uint64_t)hi << 32 | lo;
+}
+
+// 17..128-byte values of a wave's lanes hashed by lane octets (all 64 lanes
+// call it; `mine`: this lane has such a value, at global address va).  In
+// step j octet g hashes the value of lane 8 g + j, its lane 8 g + t loading
+// piece t (xp_mid_load's order and clamping): each load instruction reads
+// eight contiguous <= 128-byte windows, where a per-lane hash's reads 64
+// scattered pieces -- the per-lane walk is bound by the texture addresser
+// (TA busy ~95 % of the protect kernel, ~64 lanes' worth of cycles per
+// divergent load).  The octet sums its terms with DPP; lane 8 g + j keeps the
+// hash of its own value.  klo / khi: sec64(16 t) + seed, sec64(16 t + 8) - seed.
+__device__ __forceinline__ uint64_t xp_mid_octets(uint64_t va, uint32_t vl, bool mine, uint64_t klo, uint64_t khi,
+                                                  uint32_t lane) {
+  const uint32_t t = lane & 7, gb = lane & ~7u;
+  const uint64_t zp = reinterpret_cast<uint64_t>(&g_zero16[0]);
+  const uint32_t lm_own = mine ? vl : 0u;
+  span_u32x4 d[8];
+  uint32_t lens[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int src = (int)gb + j;
+    const uint64_t a = __shfl(va, src, 64);
+    const uint32_t lm = (uint32_t)__shfl((int)lm_own, src, 64);  // 0: no value there
+    const int last = (int)lm - 16;
+    int off = (t & 1) ? last - 16 * (int)(t >> 1) : 16 * (int)(t >> 1);
+    off = off < 0 ? 0 : off > last ? last : off;
+    const uint64_t addr = lm ? a + (uint32_t)off : zp;
+    d[j] = *reinterpret_cast<__attribute__((address_space(1))) const span_u32x4*>(addr);
+    lens[j] = lm;
+  }
+  uint64_t res = 0;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint64_t lo = (uint64_t)d[j].y << 32 | d[j].x, hi = (uint64_t)d[j].w << 32 | d[j].z;
+    const uint64_t m = mul128_fold64(lo ^ klo, hi ^ khi);
+    const uint32_t pairs = (lens[j] + 31) / 32;
+    const uint64_t sum = oct_sum_u64((t >> 1) < pairs ? m : 0ull);
+    const uint64_t h = xxph3_avalanche((uint64_t)lens[j] * P64_1 + sum);
+    res = t == (uint32_t)j ? h : res;
+  }
+  return res;
+}
+
 // one lane, any length (keys)
 template <class R>
 __device__ __noinline__ uint64_t xp_lane(const R& r, uint32_t o, uint32_t len, uint64_t seed) {
@@ -893,9 +953,11 @@ constexpr uint32_t kBlkKeyBuf = 128;  // bytes of LDS key buffer per thread
 #define MCK_BLK_LONG_MIN 241
 #endif
 constexpr uint32_t kBlkWaveLong = MCK_BLK_LONG_MIN;
-// MCK_BLK_FLAT_MID=0: 17..128-byte values through xp_short (A/B)
+// 17..128-byte values: MCK_BLK_FLAT_MID=2 (default) by lane octets
+// (xp_mid_octets), 1 per lane with batched loads (xp_mid_load), 0 through
+// xp_short (A/B)
 #ifndef MCK_BLK_FLAT_MID
-#define MCK_BLK_FLAT_MID 1
+#define MCK_BLK_FLAT_MID 2
 #endif
 template <int KIND, bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t count, const uint64_t* key_base,
@@ -926,11 +988,16 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
   const uint64_t klast = csec64(121 + 8 * (int)l8, kSeedV);
   const uint64_t km = csec64((l8 & 1) ? 19 + 16 * (int)(l8 >> 1) : 11 + 16 * (int)(l8 >> 1), kSeedV);
 #endif
+#if MCK_BLK_FLAT_MID == 2
+  const uint64_t oklo = sec64(16 * (int)(lane & 7)) + kSeedV, okhi = sec64(16 * (int)(lane & 7) + 8) - kSeedV;
+#endif
   uint32_t p = 0, idx = 0;
   uint32_t u = active ? rd.u32(0) : 0;  // the next entry's first dword, one entry ahead
   while (__any(active)) {
     uint32_t sh = 0, ns = 0, q = 0, v = 0, vl = 0;
     uint64_t hv = 0;
+    uint32_t kw[4];
+    bool vmid = false;
     if (active) {
       rd_entry_pre<KIND>(rd, p, ro, u, &sh, &ns, &q, &v, &vl);
       // prefetch: the following entry's header travels with this entry's
@@ -940,7 +1007,6 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
       // delta's first 16 bytes and a 17..128-byte value's pieces
       // (8 bytes at q are always inside it: 4-byte restart array + 4-byte
       // footer at least), as two 8-byte loads
-      uint32_t kw[4];
       {
         const uint64_t k01 = rd.u64(q), k23 = rd.u64(ns > 8 ? q + 8 : q);
         kw[0] = (uint32_t)k01;
@@ -948,12 +1014,22 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
         kw[2] = (uint32_t)k23;
         kw[3] = (uint32_t)(k23 >> 32);
       }
-      const bool vmid = vl > 16 && vl <= 128 && MCK_BLK_FLAT_MID;
+      vmid = vl > 16 && vl <= 128 && MCK_BLK_FLAT_MID;
+#if MCK_BLK_FLAT_MID == 1
       if (vmid) {
         uint64_t vd[16];
         xp_mid_load(rd, v, vl, vd);
         hv = xp_mid_fold(vd, vl, kSeedV);  // first: the pieces' registers are free before the key work
       }
+#endif
+    }
+#if MCK_BLK_FLAT_MID == 2
+    {
+      const uint64_t hm = xp_mid_octets(reinterpret_cast<uint64_t>(rd.p) + v, vl, vmid, oklo, okhi, lane);
+      hv = vmid ? hm : 0ull;
+    }
+#endif
+    if (active) {
       const uint32_t kl = sh + ns;
       if (!global_key && kl > kBlkKeyBuf) {  // rare: move the prefix to the arena
         for (uint32_t i = 0; i < sh; i++) gkey[i] = lkey[i];
