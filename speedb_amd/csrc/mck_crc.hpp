@@ -1077,13 +1077,31 @@ __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, co
 // Also sums the share's span bytes into the u64 at kLdsRowTotal (zeroed
 // here; valid after the next __syncthreads + the atomics).
 constexpr uint32_t kLdsRowTotal = kLdsRowTicket + 8;  // u64
-template <class Op>
-__device__ __forceinline__ void row_desc_stage(const Op& op, uint32_t first, uint32_t count, bool total) {
+// A workgroup's share of spans [first, first + count): span first + b + G t
+// (interleaved: the grid sweeps the batch front to back together) or, BLK,
+// the contiguous range [count b / G, count (b + 1) / G) (neighbouring spans
+// on one CU, so the cache lines two spans share stay in one XCD's L2).
+struct RowShare {
+  uint32_t start, stride, n;
+  __device__ uint32_t idx(uint32_t t) const { return start + stride * t; }
+};
+template <bool BLK>
+__device__ __forceinline__ RowShare row_share(uint32_t first, uint32_t count) {
   const uint32_t G = gridDim.x, b = blockIdx.x;
-  const uint32_t n = (count - b + G - 1) / G;
+  if (BLK) {
+    const uint32_t lo = (uint32_t)((uint64_t)count * b / G), hi = (uint32_t)((uint64_t)count * (b + 1) / G);
+    return {first + lo, 1u, hi - lo};
+  }
+  return {first + b, G, (count - b + G - 1) / G};
+}
+
+template <class Op, bool BLK = false>
+__device__ __forceinline__ void row_desc_stage(const Op& op, uint32_t first, uint32_t count, bool total) {
+  const RowShare sh = row_share<BLK>(first, count);
+  const uint32_t n = sh.n;
   uint64_t sum = 0;
   for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
-    const uint32_t i = first + b + G * t;
+    const uint32_t i = sh.idx(t);
     const uint64_t off = op.off(i);
     const uint32_t len = (uint32_t)op.len(i);
     sum += len;
@@ -1121,11 +1139,11 @@ __device__ __forceinline__ uint4 row_desc(uint32_t t, uint32_t share) {
 
 // LDS prologue of the row (and auto) kernels: tables, descriptors, init
 // tables; ends with a barrier.
-template <class Op>
+template <bool BLK = false, class Op>
 __device__ __forceinline__ void crc_rows_prologue(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                   const CrcTables* __restrict__ g, bool total) {
   crc_fill_rows(lds, g);
-  row_desc_stage(op, first, count, total);
+  row_desc_stage<Op, BLK>(op, first, count, total);
   __syncthreads();
   row_init_tables(op);
   __syncthreads();

@@ -868,6 +868,17 @@ static int wal_chunk() {
   return v;
 }
 
+// Fragment order of the one-pass writer: contiguous ranges per workgroup
+// (default) or MCK_WAL_ORDER=interleaved (fragment i on workgroup i mod G;
+// with 80-byte chunks only).
+static bool wal_interleaved() {
+  static const bool v = [] {
+    const char* e = getenv("MCK_WAL_ORDER");
+    return e && strcmp(e, "interleaved") == 0;
+  }();
+  return v;
+}
+
 // pieces of at least 16 fragments per CU (one CRC grid's worth of spans)
 static uint32_t wal_pieces_for(uint32_t nfrags, int ncu) {
   uint32_t pieces = wal_pieces();
@@ -904,8 +915,9 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   if (wal_fused()) {
     // one pass: CRC + log stream in k_wal_write_rows, in launches of at most
     // ncu * kRowDescCache fragments (its LDS descriptor / dst_off tables)
-    const bool w8 = wal_row_lanes() == 8, q80 = !w8 && wal_chunk() == 80;
+    const bool w8 = wal_row_lanes() == 8, q80 = !w8 && wal_chunk() == 80, ilv = wal_interleaved();
     if (int rc = w8    ? ensure_lds(k_wal_write_rows<8>, dev)
+                 : ilv ? ensure_lds(k_wal_write_rows<16, 5, false>, dev)
                  : q80 ? ensure_lds(k_wal_write_rows<16, 5>, dev)
                        : ensure_lds(k_wal_write_rows<16>, dev))
       return rc;
@@ -918,6 +930,8 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
       const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
       if (w8)
         hipLaunchKernelGGL(k_wal_write_rows<8>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+      else if (ilv)
+        hipLaunchKernelGGL((k_wal_write_rows<16, 5, false>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
       else if (q80)
         hipLaunchKernelGGL((k_wal_write_rows<16, 5>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
       else

@@ -608,7 +608,7 @@ __device__ __forceinline__ void st_nt16(uint64_t a, uint4 o) {
 // NP = 5 rows use their own lane-final and gap maps (CrcTables::lane_final80
 // / gap80), loaded over LDS tables these rows never read: lane-final columns
 // 0-15 (16-lane rows read columns 48-63) and the W = 4 gap map.
-template <int W, int NP = 4>
+template <int W, int NP = 4, bool BLK = true>
 __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                const CrcTables* __restrict__ g) {
   static_assert(W == 8 || W == 16, "row width");
@@ -616,13 +616,10 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
   constexpr uint64_t Q = 16u * NP;  // lane chunk bytes
   constexpr int kHT = 16 / W;  // head / tail payload bytes per lane (< 16 each)
   constexpr int kHdr = 32 / W;  // padding + header bytes per lane (pad + hs <= 21)
-  crc_rows_prologue(op, first, count, lds, g, false);
-  {  // fragments' dst_off, staged like the descriptors (row_desc_stage order)
-    const uint32_t G = gridDim.x, b = blockIdx.x;
-    const uint32_t n = (count - b + G - 1) / G;
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
-      *lds_p64(kLdsWalAux + 8 * t) = op.frags[first + b + G * t].dst_off;
-  }
+  crc_rows_prologue<BLK>(op, first, count, lds, g, false);
+  const RowShare sh = row_share<BLK>(first, count);
+  // fragments' dst_off, staged like the descriptors (row_desc_stage order)
+  for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) *lds_p64(kLdsWalAux + 8 * t) = op.frags[sh.idx(t)].dst_off;
   if (NP == 5) {  // 80-byte-chunk maps: [n][v] rows of 16 lane-final columns, then the gap map
     const uint32_t t = threadIdx.x;
     if (t < 512) {
@@ -637,8 +634,7 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
   const CrcLane L = crc_lane();
   const uint32_t c = threadIdx.x & (W - 1);
   const uint32_t lf4 = (NP == 5 ? c : 64u - W + c) << 2;  // lane-final table column
-  const uint32_t G = gridDim.x;
-  const uint32_t share = (count - blockIdx.x + G - 1) / G;
+  const uint32_t share = sh.n;
   const uint64_t base = reinterpret_cast<uint64_t>(op.src);
   const uint64_t obase = reinterpret_cast<uint64_t>(op.out);
   // per-lane sink slots (16 B each), never read
@@ -650,7 +646,7 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
   bool live = t < share;
   uint4 d = row_desc(t, share);
   uint64_t dst = *lds_p64(kLdsWalAux + 8 * (t < share ? t : 0));
-  uint32_t i = first + blockIdx.x + G * (live ? t : 0);
+  uint32_t i = sh.idx(live ? t : 0);
   RowSpan sp = row_span<W, NP>(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kInitTyped);
   uint32_t key = d.w;
   int r = sp.rounds - 1;
@@ -729,7 +725,7 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
     const bool sw = go && last;
     const RowSpan lsp = row_span_sel(sw, nsp, sp);
     const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
-    const uint32_t li = sw ? first + blockIdx.x + G * nt : i;
+    const uint32_t li = sw ? sh.idx(nt) : i;
     const ChunkN<NP> nxt = row_load_chunk<W, NP>(lsp, lr, c, zp);
 
     s = row_round<W, NP>(s, cur, sp, r, c, L);
@@ -772,10 +768,10 @@ __device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t fi
   }
 }
 
-template <int W, int NP = 4>
+template <int W, int NP = 4, bool BLK = true>
 __global__ __launch_bounds__(1024) void k_wal_write_rows(OpWalWrite op, uint32_t first, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  wal_write_rows<W, NP>(op, first, count, lds, &g_crc_tables);
+  wal_write_rows<W, NP, BLK>(op, first, count, lds, &g_crc_tables);
 }
 
 // The physical record image: [pad zeros][crc LE32][len LE16][type]
