@@ -456,7 +456,9 @@ def make_workload(args, dev, rank, world):
             # the row shape the engine picks (mck_engine.hip wal_row_lanes / wal_chunk)
             rw = 8 if os.environ.get("MCK_WAL_ROW_LANES") == "8" else 16
             np_ = 5 if rw == 16 and os.environ.get("MCK_WAL_CHUNK") != "64" else 4
-            w.kernel = f"mck::k_wal_write_rows<{rw}, {np_}> ({nl} launch(es) per step, timed as the step)"
+            blk = "" if rw == 8 or np_ == 4 else (", false" if os.environ.get("MCK_WAL_ORDER") == "interleaved"
+                                                  else ", true")
+            w.kernel = f"mck::k_wal_write_rows<{rw}, {np_}{blk}> ({nl} launch(es) per step, timed as the step)"
             w.alg_bytes = int(lens.sum()) + nbytes + nf * (24 + 4)
         else:
             # MCK_WAL_FUSED=0: the CRC and copy kernels overlap (piecewise,

@@ -1149,7 +1149,7 @@ __device__ __forceinline__ void crc_rows_prologue(const Op& op, uint32_t first, 
   __syncthreads();
 }
 
-template <class Op, int W>
+template <class Op, int W, bool BLK = false>
 __device__ __forceinline__ void crc_rows_loop(const Op& op, uint32_t first, uint32_t count,
                                               const CrcTables* __restrict__ g) {
   static_assert(W == 4 || W == 8 || W == 16, "row width");
@@ -1158,14 +1158,14 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, uint32_t first, uint
   CrcLane Lf = L;
   const uint32_t c = threadIdx.x & (W - 1);
   Lf.lane4 = (64u - W + c) << 2;
-  const uint32_t G = gridDim.x;
-  const uint32_t share = (count - blockIdx.x + G - 1) / G;  // this workgroup's spans
+  const RowShare sh = row_share<BLK>(first, count);
+  const uint32_t share = sh.n;  // this workgroup's spans
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   // the row's current span (ticket t) and the next one (ticket nt, prefetched)
   uint32_t t = row_ticket<W>(true);
   bool live = t < share;
   uint4 d = row_desc(t, share);
-  uint32_t i = first + blockIdx.x + G * (live ? t : 0);
+  uint32_t i = sh.idx(live ? t : 0);
   RowSpan sp = row_span<W>(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kind);
   int r = sp.rounds - 1;
   const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
@@ -1183,7 +1183,7 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, uint32_t first, uint
     const bool sw = go && last;  // the row moves to its next span
     const RowSpan lsp = row_span_sel(sw, nsp, sp);
     const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
-    const uint32_t li = sw ? first + blockIdx.x + G * nt : i;
+    const uint32_t li = sw ? sh.idx(nt) : i;
     // unconditional: the next unit's chunk and epilogue inputs
     const Chunk nxt = row_load_chunk<W>(lsp, lr, c, zp);
     const typename Op::Pre pnxt = op.pre(li, lsp.ptr, lsp.n);
@@ -1222,12 +1222,13 @@ __device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, ui
 // ticket per wave.
 template <class Op>
 struct FeedRowCache {
-  uint32_t first_span, share;
+  RowShare sh;
   int kind;
   __device__ bool take(uint32_t* span, SpanDesc* d) {
     const uint32_t t = __builtin_amdgcn_readfirstlane(lds_ticket(lds_p32(kLdsRowTicket)));
+    const uint32_t share = sh.n;
     if (t >= share) return false;
-    *span = first_span + blockIdx.x + gridDim.x * t;
+    *span = sh.idx(t);
     const uint4 v = row_desc(t, share);
     d->off = ((uint64_t)v.y << 32) | v.x;
     d->len = v.z;
@@ -1244,20 +1245,20 @@ struct FeedRowCache {
 // above that.  force: 0 = by length, 1 = wave, 2 = rows16, 3 = rows8.
 constexpr uint32_t kAutoRows8Max = 640;    // mean span bytes
 constexpr uint32_t kAutoRows16Max = 2560;
-template <class Op, bool T>
+template <class Op, bool T, bool BLK = false>
 __device__ __forceinline__ void crc_auto_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                 const CrcTables* __restrict__ g, int force) {
-  crc_rows_prologue(op, first, count, lds, g, true);
-  const uint32_t G = gridDim.x;
-  const uint32_t share = (count - blockIdx.x + G - 1) / G;
+  crc_rows_prologue<BLK>(op, first, count, lds, g, true);
+  const RowShare sh = row_share<BLK>(first, count);
+  const uint32_t share = sh.n;
   const uint64_t mean = *lds_p64(kLdsRowTotal) / (share ? share : 1);
   const int mode = force ? force : mean <= kAutoRows8Max ? 3 : mean <= kAutoRows16Max ? 2 : 1;
   if (mode == 3) {
-    crc_rows_loop<Op, 8>(op, first, count, g);
+    crc_rows_loop<Op, 8, BLK>(op, first, count, g);
   } else if (mode == 2) {
-    crc_rows_loop<Op, 16>(op, first, count, g);
+    crc_rows_loop<Op, 16, BLK>(op, first, count, g);
   } else {
-    FeedRowCache<Op> f{first, share, op.init_kind()};
+    FeedRowCache<Op> f{sh, op.init_kind()};
     crc_drive<Op, FeedRowCache<Op>, T>(op, f, crc_lane());
   }
 }

@@ -246,10 +246,24 @@ int launch_crc_rows(const Op& op, uint32_t count, hipStream_t st, int dev, int n
   }
 }
 
+// Span order of k_crc_auto: contiguous ranges per workgroup (default: the
+// cache lines two neighbouring spans share are read once, into one XCD's L2;
+// WAL records 100-1100 B 0.378 -> 0.413 of peak, 512-B spans 0.445 -> 0.509,
+// SST mix CRC image 0.730 -> 0.736, ragged 4 KiB 0.748 -> 0.727) or, with
+// MCK_CRC_ORDER=interleaved, span i on workgroup i mod G (A/B).
+static bool crc_auto_blocked() {
+  static const bool v = [] {
+    const char* e = getenv("MCK_CRC_ORDER");
+    return !e || strcmp(e, "interleaved") != 0;
+  }();
+  return v;
+}
+
 template <class Op>
 int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
   constexpr bool T = CrcRowT<Op>::value;
-  int rc = ensure_lds(k_crc_auto<Op, T>, dev);
+  const bool blk = crc_auto_blocked();
+  int rc = blk ? ensure_lds(k_crc_auto<Op, T, true>, dev) : ensure_lds(k_crc_auto<Op, T>, dev);
   if (rc) return rc;
   // one 16-wave workgroup per CU; each stages its share's descriptors in
   // LDS, so a batch runs in launches of at most ncu * kRowDescCache spans,
@@ -260,7 +274,11 @@ int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int n
   for (uint32_t first = 0; first < count; first += per) {
     const uint32_t n = std::min(per, count - first);
     const uint32_t grid = std::min<uint32_t>(ncu, (n + 15) / 16);
-    hipLaunchKernelGGL((k_crc_auto<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n, crc_auto_force());
+    if (blk)
+      hipLaunchKernelGGL((k_crc_auto<Op, T, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n,
+                         crc_auto_force());
+    else
+      hipLaunchKernelGGL((k_crc_auto<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n, crc_auto_force());
     MCK_HIP(hipGetLastError());
   }
   return MCK_OK;

@@ -102,13 +102,14 @@ def test_row_widths_subprocess(gpu, lanes):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
 
 
-@pytest.mark.parametrize("mode", ["wave", "rows16", "rows8"])
+@pytest.mark.parametrize("mode", ["wave", "rows16", "rows8", "interleaved"])
 def test_auto_kernel_forced_drivers_subprocess(gpu, mode):
     """k_crc_auto with each driver forced (its per-workgroup choice is by
-    mean length, so a parity test of mixed lengths may exercise only one)."""
-    if os.environ.get("MCK_CRC_AUTO") or os.environ.get("MCK_CRC_ROWS"):
+    mean length, so a parity test of mixed lengths may exercise only one),
+    and with the interleaved span order instead of contiguous ranges."""
+    if os.environ.get("MCK_CRC_AUTO") or os.environ.get("MCK_CRC_ROWS") or os.environ.get("MCK_CRC_ORDER"):
         pytest.skip("already running a forced driver")
-    env = dict(os.environ, MCK_CRC_AUTO=mode)
+    env = dict(os.environ, MCK_CRC_ORDER="interleaved") if mode == "interleaved" else dict(os.environ, MCK_CRC_AUTO=mode)
     tests = [os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
     tests += [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
         "test_crc32c_batch_ragged", "test_sst_trailer_and_verify", "test_empty_and_zero_inputs",

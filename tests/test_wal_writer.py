@@ -128,12 +128,14 @@ def test_wal_write_batch_two_kernel_paths_subprocess(gpu, pieces):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("env", [{"MCK_WAL_CHUNK": "64"}, {"MCK_WAL_ROW_LANES": "8"}])
+@pytest.mark.parametrize("env", [{"MCK_WAL_CHUNK": "64"}, {"MCK_WAL_ROW_LANES": "8"},
+                                 {"MCK_WAL_ORDER": "interleaved"}])
 def test_wal_write_batch_row_shapes_subprocess(gpu, env):
     """The one-pass writer's other row shapes -- 64-byte lane chunks (two
-    1 KiB rounds per ~1 KB fragment) and 8-lane rows -- in a child process:
-    byte-exact too (the default is 16-lane rows of 80-byte chunks)."""
-    if any(os.environ.get(k) for k in ("MCK_WAL_CHUNK", "MCK_WAL_ROW_LANES", "MCK_WAL_FUSED")):
+    1 KiB rounds per ~1 KB fragment) and 8-lane rows -- and the interleaved
+    fragment order, in a child process: byte-exact too (the default is
+    16-lane rows of 80-byte chunks over contiguous fragment ranges)."""
+    if any(os.environ.get(k) for k in ("MCK_WAL_CHUNK", "MCK_WAL_ROW_LANES", "MCK_WAL_FUSED", "MCK_WAL_ORDER")):
         pytest.skip("already running a non-default writer")
     here = os.path.dirname(os.path.abspath(__file__))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
