@@ -458,7 +458,11 @@ def make_workload(args, dev, rank, world):
             np_ = 5 if rw == 16 and os.environ.get("MCK_WAL_CHUNK") != "64" else 4
             blk = "" if rw == 8 or np_ == 4 else (", false" if os.environ.get("MCK_WAL_ORDER") == "interleaved"
                                                   else ", true")
-            w.kernel = f"mck::k_wal_write_rows<{rw}, {np_}{blk}> ({nl} launch(es) per step, timed as the step)"
+            if rw == 16 and np_ == 5 and os.environ.get("MCK_WAL_LAYOUT") != "chunk":
+                kname = f"mck::k_wal_write_il<{blk[2:]}>"
+            else:
+                kname = f"mck::k_wal_write_rows<{rw}, {np_}{blk}>"
+            w.kernel = f"{kname} ({nl} launch(es) per step, timed as the step)"
             w.alg_bytes = int(lens.sum()) + nbytes + nf * (24 + 4)
         else:
             # MCK_WAL_FUSED=0: the CRC and copy kernels overlap (piecewise,

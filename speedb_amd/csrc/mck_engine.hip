@@ -886,6 +886,18 @@ static int wal_chunk() {
   return v;
 }
 
+// Lane layout of the 80-byte-chunk writer: interleaved pieces (default,
+// k_wal_write_il: the copy reuses the CRC's registers) or, with
+// MCK_WAL_LAYOUT=chunk, lane-owned 80-byte chunks (k_wal_write_rows<16, 5>,
+// which re-reads each round's bytes for the copy).
+static bool wal_piece_layout() {
+  static const bool v = [] {
+    const char* e = getenv("MCK_WAL_LAYOUT");
+    return !e || strcmp(e, "chunk") != 0;
+  }();
+  return v;
+}
+
 // Fragment order of the one-pass writer: contiguous ranges per workgroup
 // (default) or MCK_WAL_ORDER=interleaved (fragment i on workgroup i mod G;
 // with 80-byte chunks only).
@@ -934,7 +946,9 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
     // one pass: CRC + log stream in k_wal_write_rows, in launches of at most
     // ncu * kRowDescCache fragments (its LDS descriptor / dst_off tables)
     const bool w8 = wal_row_lanes() == 8, q80 = !w8 && wal_chunk() == 80, ilv = wal_interleaved();
+    const bool pl = q80 && wal_piece_layout();
     if (int rc = w8    ? ensure_lds(k_wal_write_rows<8>, dev)
+                 : pl  ? (ilv ? ensure_lds(k_wal_write_il<false>, dev) : ensure_lds(k_wal_write_il<true>, dev))
                  : ilv ? ensure_lds(k_wal_write_rows<16, 5, false>, dev)
                  : q80 ? ensure_lds(k_wal_write_rows<16, 5>, dev)
                        : ensure_lds(k_wal_write_rows<16>, dev))
@@ -948,6 +962,10 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
       const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
       if (w8)
         hipLaunchKernelGGL(k_wal_write_rows<8>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+      else if (pl && ilv)
+        hipLaunchKernelGGL(k_wal_write_il<false>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+      else if (pl)
+        hipLaunchKernelGGL(k_wal_write_il<true>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
       else if (ilv)
         hipLaunchKernelGGL((k_wal_write_rows<16, 5, false>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
       else if (q80)

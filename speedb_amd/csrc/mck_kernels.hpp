@@ -774,6 +774,274 @@ __global__ __launch_bounds__(1024) void k_wal_write_rows(OpWalWrite op, uint32_t
   wal_write_rows<W, NP, BLK>(op, first, count, lds, &g_crc_tables);
 }
 
+// ---- one-pass writer, interleaved pieces (the default) ---------------------
+// Lane c of a 16-lane row loads pieces c + 16 j (j = 0..4) of the fragment's
+// 1280-byte round: every load instruction reads 256 contiguous bytes per
+// row, and -- the point -- the row already holds the round in the layout the
+// output wants (store j of lane c is output piece c + 16 j), so the copy
+// needs no second read of the payload: output piece k is bytes e.. of source
+// pieces k and k + 1 (lane c + 1's piece j, via DPP; lane 15 takes lane 0's
+// piece j + 1), realigned by the fragment's (dst - src) mod 16.  The piece
+// straddling two rounds (lane 15, j = 4) is stored by lane 0 in the next
+// round from a one-register carry.  The CRC algebra: a lane's pieces are
+// 240 bytes apart, so its state moves piece to piece by zshift(., 244) (the
+// pending 4-byte step + the gap; a 4 KiB byte table), and the lane-final
+// shift is zshift(., 4 + 16 (15 - c)) (CrcTables::lane_final16).
+constexpr uint32_t kLdsWalGap244 = kLdsWalAux + 8 * kRowDescCache + 64;  // [4][256] u32
+constexpr uint32_t kLdsWalCarry = kLdsWalGap244 + 4096;  // 16 B per row
+static_assert(kLdsWalGap244 % 16 == 0 && kLdsWalCarry + 16 * 64 <= kCrcLdsBytes, "gap table must fit");
+
+__device__ __forceinline__ uint32_t il_gap(uint32_t x, uint32_t w) {
+  uint32_t l[4];
+#pragma unroll
+  for (int b = 0; b < 4; b++) l[b] = lds_u32(kLdsWalGap244 + 1024u * b + (((x >> (8 * b)) & 255u) << 2));
+  return xor3(xor3(l[0], l[1], l[2]), l[3], w);
+}
+
+// Round r of a span: lane c's pieces c + 16 j; pieces before the span read
+// the zero piece (only in its first round).
+__device__ __forceinline__ ChunkN<5> il_load(const RowSpan& sp, int r, uint32_t c, uint64_t zp) {
+  const uint64_t b = sp.a1 - 1280ull * (uint32_t)(r + 1) + 16ull * c;
+  ChunkN<5> ch;
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    const uint64_t a = b + 256ull * j;
+    ch.v[j] = span_load16<false>(a < sp.a0 ? zp : a);
+  }
+  return ch;
+}
+
+// Round r's foreign bytes zeroed in place: the piece holding ptr (piece k0 =
+// (ptr - first round start) / 16 of the first round) keeps the bytes from
+// ptr on, lane 15's last piece in the last round those before the end.  The
+// copy only stores whole payload pieces, so it can share the masked chunk.
+__device__ __forceinline__ uint32_t il_owner_piece(const RowSpan& sp, int r, uint32_t c) {
+  const uint32_t k0 = 5u * (uint32_t)sp.owner + (sp.hb >> 4);
+  const bool own = r == sp.rounds - 1 && sp.owner < 16 && c == (k0 & 15u);
+  return own ? k0 >> 4 : 5u;
+}
+__device__ __forceinline__ void il_mask(ChunkN<5>& ch, const RowSpan& sp, int r, uint32_t c) {
+  const uint32_t pa = il_owner_piece(sp, r, c);
+  const uint4 mh = lds_u32x4(kLdsRowMaskHead + 16 * ((uint32_t)sp.ptr & 15u));
+  const uint4 mt = lds_u32x4(kLdsRowMaskTail + 16 * ((r == 0 && c == 15) ? sp.kt : 0u));
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    const uint32_t sel = (uint32_t)j == pa ? ~0u : 0u;
+    ch.v[j].x = __builtin_amdgcn_bitop3_b32(ch.v[j].x, mh.x, sel, 0xD0);
+    ch.v[j].y = __builtin_amdgcn_bitop3_b32(ch.v[j].y, mh.y, sel, 0xD0);
+    ch.v[j].z = __builtin_amdgcn_bitop3_b32(ch.v[j].z, mh.z, sel, 0xD0);
+    ch.v[j].w = __builtin_amdgcn_bitop3_b32(ch.v[j].w, mh.w, sel, 0xD0);
+  }
+  and4(ch.v[4], mt);
+}
+
+// The lane's state after its five (masked) pieces, the last 4-byte step
+// pending; x = the state at its first piece (0 in a span's first round).
+__device__ __forceinline__ uint32_t il_round(uint32_t x, const ChunkN<5>& ch, const RowSpan& sp, int r, uint32_t c,
+                                             const CrcLane& L) {
+  const uint32_t pa = il_owner_piece(sp, r, c);
+  const uint32_t inj = sp.inj;
+  x ^= ch.v[0].x ^ (pa == 0 ? inj : 0u);
+#pragma unroll
+  for (int j = 0; j < 5; j++) {
+    x = crc_step4x(x, L, ch.v[j].y);
+    x = crc_step4x(x, L, ch.v[j].z);
+    x = crc_step4x(x, L, ch.v[j].w);
+    if (j < 4) x = il_gap(x, ch.v[j + 1].x ^ (pa == (uint32_t)(j + 1) ? inj : 0u));
+  }
+  return x;
+}
+
+// 16 bytes at byte e (q2 = e & 8, q1 = e & 4, be = e & 3) of lo || hi.
+__device__ __forceinline__ uint4 il_align(const uint4& lo, const uint4& hi, uint32_t q2, uint32_t q1, uint32_t be) {
+  const uint32_t X[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+  uint32_t Y[6], Z[5];
+#pragma unroll
+  for (int m = 0; m < 6; m++) Y[m] = q2 ? X[m + 2] : X[m];
+#pragma unroll
+  for (int t = 0; t < 5; t++) Z[t] = q1 ? Y[t + 1] : Y[t];
+  uint4 o;
+  o.x = __builtin_amdgcn_alignbyte(Z[1], Z[0], be);
+  o.y = __builtin_amdgcn_alignbyte(Z[2], Z[1], be);
+  o.z = __builtin_amdgcn_alignbyte(Z[3], Z[2], be);
+  o.w = __builtin_amdgcn_alignbyte(Z[4], Z[3], be);
+  return o;
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint4 dpp_u32x4(const uint4& v) {
+  uint4 r;
+  r.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, CTRL, 0xF, 0xF, false);
+  r.y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.y, CTRL, 0xF, 0xF, false);
+  r.z = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.z, CTRL, 0xF, 0xF, false);
+  r.w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w, CTRL, 0xF, 0xF, false);
+  return r;
+}
+constexpr int kDppRowRor15 = 0x12F;  // lane j of a row <- lane j + 1 (mod 16)
+constexpr int kDppRowRor1x = 0x121;  // lane j of a row <- lane j - 1 (mod 16)
+
+template <bool BLK>
+__device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
+                                             const CrcTables* __restrict__ g) {
+  constexpr int W = 16, NP = 5;
+  constexpr int kHdr = 2;  // padding + header bytes per lane (pad + hs <= 21)
+  crc_rows_prologue<BLK>(op, first, count, lds, g, false);
+  const RowShare sh = row_share<BLK>(first, count);
+  // fragments' dst_off, staged like the descriptors (row_desc_stage order)
+  for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) *lds_p64(kLdsWalAux + 8 * t) = op.frags[sh.idx(t)].dst_off;
+  {  // lane-final map over lane-final columns 0-15, the piece-to-piece byte table
+    const uint32_t t = threadIdx.x;
+    if (t < 512) {
+      const uint4 x = reinterpret_cast<const uint4*>(&g->lane_final16[0][0][0])[t];
+      *reinterpret_cast<uint4*>(lds + kLdsFinal + 256 * (t >> 2) + 16 * (t & 3)) = x;
+    } else if (t < 768) {
+      const uint4 x = reinterpret_cast<const uint4*>(&g->gap244[0][0])[t - 512];
+      *reinterpret_cast<uint4*>(lds + kLdsWalGap244 + 16 * (t - 512)) = x;
+    }
+  }
+  __syncthreads();
+  const CrcLane L = crc_lane();
+  const uint32_t c = threadIdx.x & (W - 1);
+  const uint32_t lf4 = c << 2;
+  const uint32_t share = sh.n;
+  const uint64_t base = reinterpret_cast<uint64_t>(op.src);
+  const uint64_t obase = reinterpret_cast<uint64_t>(op.out);
+  const uint64_t sink = reinterpret_cast<uint64_t>(&g_wal_sink[0]) + 16ull * (threadIdx.x & 63);
+  (void)sink;
+  const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
+  uint32_t t = row_ticket<W>(true);
+  bool live = t < share;
+  uint4 d = row_desc(t, share);
+  uint64_t dst = *lds_p64(kLdsWalAux + 8 * (t < share ? t : 0));
+  uint32_t i = sh.idx(live ? t : 0);
+  RowSpan sp = row_span<W, NP>(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kInitTyped);
+  uint32_t key = d.w;
+  int r = sp.rounds - 1;
+  ChunkN<NP> cur = il_load(sp, r, c, zp);
+  uint32_t nt = row_ticket<W>(true);
+  uint4 nd = row_desc(nt, share);
+  uint64_t ndst = *lds_p64(kLdsWalAux + 8 * (nt < share ? nt : 0));
+  uint32_t x = 0;  // the lane's CRC state at its next piece
+  // the row's LDS slot for the previous round's straddling piece
+  const uint32_t carry_slot = kLdsWalCarry + 16u * (threadIdx.x >> 4);
+  for (;;) {
+    const bool last = r == 0;
+    const bool firstr = r == sp.rounds - 1;
+    const bool fin = live && last;
+
+    // ---- the output of this (span, round), from the round's own registers ----
+    const uint32_t type = key & 0xFF, pad = (key >> 8) & 0xFF;
+    const uint32_t hs = ((type >= 5 && type <= 8) || type == 11) ? 11u : 7u;
+    const uint64_t P = obase + dst + hs;             // payload in the output
+    const uint64_t ps = sp.ptr, pe = sp.ptr + sp.n;  // payload in the source
+    const uint64_t delta = P - ps;                   // (mod 2^64)
+    const uint32_t e = (uint32_t)(0ull - delta) & 15u;
+    const uint32_t q2 = e & 8u, q1 = e & 4u, be = e & 3u;
+    il_mask(cur, sp, r, c);
+    // output piece c + 16 j takes source bytes [x0 + 256 j, + 16), x0 = the
+    // round's window start + e + 16 c; whole pieces of the payload only
+    // (rel = offset in the payload, 32-bit: fragments are < 4 GiB)
+    const uint32_t win = (uint32_t)(sp.a1 - ps) - 1280u * (uint32_t)(r + 1);  // window start - ps
+    const int32_t rel0 = (int32_t)(win + e + 16u * c);
+    const int32_t lim = (int32_t)sp.n - 16;
+    const uint64_t oa0 = P + (uint64_t)(int64_t)rel0;  // output address of piece c
+    uint4 rj = dpp_u32x4<kDppRowRor15>(cur.v[0]);  // lane c + 1's piece j
+#pragma unroll
+    for (int j = 0; j < NP; j++) {
+      const uint4 rn = j + 1 < NP ? dpp_u32x4<kDppRowRor15>(cur.v[j + 1]) : rj;
+      const int32_t rel = rel0 + 256 * j;
+      const bool ok = live && rel >= 0 && rel <= lim && !(j == NP - 1 && c == 15 && e != 0);
+      const uint4 nb = (j < NP - 1 && c == 15) ? rn : rj;
+      const uint4 o = il_align(cur.v[j], nb, q2, q1, be);
+      WAL_ST(ok, st_nt16, oa0 + 256ull * j, sink, o);
+      rj = rn;
+      // one piece at a time (the scheduler would otherwise hoist every
+      // piece's DPP moves and selects and spill)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    {  // the piece that straddles the previous round and this one: lane 15's
+       // piece 4 of that round waits in the row's LDS slot
+      const int32_t relm = (int32_t)(win + e) - 16;
+      const bool okm = live && !firstr && e != 0 && c == 0 && relm >= 0 && relm <= lim;
+      if (wave_any(okm)) {
+        const uint4 cm = lds_u32x4(carry_slot);
+        const uint4 o = il_align(cm, cur.v[0], q2, q1, be);
+        WAL_ST(okm, st_nt16, P + (uint64_t)(int64_t)relm, sink, o);
+      }
+    }
+    if (c == 15) {
+      const span_u32x4 cv = {cur.v[NP - 1].x, cur.v[NP - 1].y, cur.v[NP - 1].z, cur.v[NP - 1].w};
+      *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(carry_slot)) = cv;
+    }
+    {  // the < 16 payload bytes before the first and after the last full output piece
+      const uint64_t h16 = (P + 15) & ~15ull;
+      const uint64_t t16 = (P + sp.n) & ~15ull;
+      const uint64_t hb_end = h16 < P + sp.n ? h16 : P + sp.n;
+      const uint64_t tb_beg = t16 > hb_end ? t16 : hb_end;
+      const uint64_t oh = P + c, ot = tb_beg + c;
+      const bool okh = fin && oh < hb_end, okt = fin && ot < P + sp.n;
+      const uint32_t bh = *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : zp);
+      const uint32_t bt = *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : zp);
+      WAL_ST(okh, st_u8, oh, sink, bh);
+      WAL_ST(okt, st_u8, ot, sink + 1, bt);
+    }
+
+    // ---- next unit (as crc_rows_loop) ----
+    const bool go = live && (!last || nt < share);
+    const RowSpan nsp = row_span<W, NP>(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kInitTyped);
+    const bool sw = go && last;
+    const RowSpan lsp = row_span_sel(sw, nsp, sp);
+    const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
+    const uint32_t li = sw ? sh.idx(nt) : i;
+    const ChunkN<NP> nxt = il_load(lsp, lr, c, zp);
+
+    x = il_round(firstr ? 0u : x, cur, sp, r, c, L);
+    uint32_t crc = 0;
+    if (wave_any(fin)) crc = crc_mask(row_finish4<W>(x, sp, lf4));
+    if (wave_any(live && !last)) x = il_gap(x, 0u);  // to the lane's piece in the next round
+    WAL_ST(fin && c == 0, st_u32, reinterpret_cast<uint64_t>(op.crcs + i), sink + 4, crc);
+    // trailer padding + header: bytes c + 16 m of [dst - pad, dst + hs)
+    const uint64_t hstart = obase + dst - pad;
+#pragma unroll
+    for (int m = 0; m < kHdr; m++) {
+      const uint32_t b = c + (uint32_t)W * m;
+      const bool okb = fin && b < pad + hs;
+      const uint32_t val = b < pad ? 0u : wal_hdr_byte(b - pad, crc, sp.n, type, op.log_number);
+      WAL_ST(okb, st_u8, hstart + b, sink + 2 + m, val);
+    }
+
+    // ---- advance ----
+    uint32_t nnt = nt;
+    uint4 nnd = nd;
+    uint64_t nndst = ndst;
+    if (wave_any(sw)) {
+      const uint32_t tk = row_ticket<W>(sw);
+      if (sw) {
+        nnt = tk;
+        nnd = row_desc(tk, share);
+        nndst = *lds_p64(kLdsWalAux + 8 * (tk < share ? tk : 0));
+      }
+    }
+    if (!wave_any(go)) break;
+    key = sw ? nd.w : key;
+    dst = sw ? ndst : dst;
+    live = go;
+    i = li;
+    nt = nnt;
+    nd = nnd;
+    ndst = nndst;
+    sp = lsp;
+    r = lr;
+    cur = nxt;
+  }
+}
+
+template <bool BLK>
+__global__ __launch_bounds__(1024) void k_wal_write_il(OpWalWrite op, uint32_t first, uint32_t count) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  wal_write_il<BLK>(op, first, count, lds, &g_crc_tables);
+}
+
 // The physical record image: [pad zeros][crc LE32][len LE16][type]
 // [log number LE32 if recyclable][payload].  One wave per fragment; the
 // body is written as aligned 16-byte stores assembled from aligned source

@@ -25,7 +25,7 @@ constexpr int kMaxUnshift = 64;                                 // k in [0,64)
 constexpr int kRowWidths = 3;  // W = 4 << k
 constexpr int row_gap_bytes(int k) { return (4 << k) * kChunkBytes - kChunkBytes; }
 
-struct CrcTables {
+struct alignas(16) CrcTables {
   uint32_t step[4][256];          // zshift(v << 8t, 4): the 4-byte step
   uint32_t lane_final[8][16][64]; // zshift(v << 4n, 64*(63-lane))
   uint32_t gap[8][16];            // zshift(v << 4n, kGapBytes)
@@ -39,6 +39,10 @@ struct CrcTables {
   // round holds a whole ~1 KB record fragment)
   uint32_t lane_final80[8][16][16];  // zshift(v << 4n, 80 (15 - c))
   uint32_t gap80[8][16];             // zshift(v << 4n, 80 * 15)
+  // interleaved pieces in 16-lane rows (the one-pass WAL writer's default:
+  // lane c holds pieces c + 16 j of a 1280-byte round, j = 0..4)
+  uint32_t lane_final16[8][16][16];  // zshift(v << 4n, 4 + 16 (15 - c))
+  uint32_t gap244[4][256];           // zshift(v << 8t, 244): piece to piece
 };
 
 // ---- host-side GF(2) helpers (also used by the host shims) ----------------
@@ -100,6 +104,16 @@ inline void build_crc_tables(CrcTables* t) {
     const uint32_t k = gf_xpow8n(80u * 15);
     for (int n = 0; n < 8; n++)
       for (int v = 0; v < 16; v++) t->gap80[n][v] = gf_mul((uint32_t)v << (4 * n), k);
+  }
+  for (int c = 0; c < 16; c++) {
+    const uint32_t k = gf_xpow8n(4u + 16u * (15 - c));
+    for (int n = 0; n < 8; n++)
+      for (int v = 0; v < 16; v++) t->lane_final16[n][v][c] = gf_mul((uint32_t)v << (4 * n), k);
+  }
+  {
+    const uint32_t k = gf_xpow8n(244);
+    for (int b = 0; b < 4; b++)
+      for (int v = 0; v < 256; v++) t->gap244[b][v] = gf_mul((uint32_t)v << (8 * b), k);
   }
   for (int k = 0; k < kMaxUnshift; k++)
     for (int n = 0; n < 8; n++)

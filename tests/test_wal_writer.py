@@ -129,13 +129,16 @@ def test_wal_write_batch_two_kernel_paths_subprocess(gpu, pieces):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("env", [{"MCK_WAL_CHUNK": "64"}, {"MCK_WAL_ROW_LANES": "8"},
-                                 {"MCK_WAL_ORDER": "interleaved"}])
+                                 {"MCK_WAL_ORDER": "interleaved"}, {"MCK_WAL_LAYOUT": "chunk"}])
 def test_wal_write_batch_row_shapes_subprocess(gpu, env):
     """The one-pass writer's other row shapes -- 64-byte lane chunks (two
-    1 KiB rounds per ~1 KB fragment) and 8-lane rows -- and the interleaved
-    fragment order, in a child process: byte-exact too (the default is
-    16-lane rows of 80-byte chunks over contiguous fragment ranges)."""
-    if any(os.environ.get(k) for k in ("MCK_WAL_CHUNK", "MCK_WAL_ROW_LANES", "MCK_WAL_FUSED", "MCK_WAL_ORDER")):
+    1 KiB rounds per ~1 KB fragment), 8-lane rows, lane-owned 80-byte chunks
+    (k_wal_write_rows<16, 5>, which re-reads for the copy) -- and the
+    interleaved fragment order, in a child process: byte-exact too (the
+    default is k_wal_write_il: 16-lane rows of interleaved pieces over
+    contiguous fragment ranges)."""
+    if any(os.environ.get(k) for k in ("MCK_WAL_CHUNK", "MCK_WAL_ROW_LANES", "MCK_WAL_FUSED", "MCK_WAL_ORDER",
+                                       "MCK_WAL_LAYOUT")):
         pytest.skip("already running a non-default writer")
     here = os.path.dirname(os.path.abspath(__file__))
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
