@@ -589,7 +589,8 @@ __device__ __forceinline__ void st_nt16(uint64_t a, uint4 o) {
 
 // MCK_WAL_EXP (timing experiments only, wrong output): 1 drops the piece
 // copies, 2 the head/tail bytes, 4 the header bytes, 8 the piece stores
-// (loads kept), 16 the piece loads (stores of zeros kept).
+// (loads kept), 16 the piece loads (stores of zeros kept), 32 the head/tail
+// byte loads (k_wal_write_il: stores of zeros kept).
 #ifndef MCK_WAL_EXP
 #define MCK_WAL_EXP 0
 #endif
@@ -953,7 +954,7 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
       const bool ok = live && rel >= 0 && rel <= lim && !(j == NP - 1 && c == 15 && e != 0);
       const uint4 nb = (j < NP - 1 && c == 15) ? rn : rj;
       const uint4 o = il_align(cur.v[j], nb, q2, q1, be);
-      WAL_ST(ok, st_nt16, oa0 + 256ull * j, sink, o);
+      WAL_ST(ok && !(MCK_WAL_EXP & 8), st_nt16, oa0 + 256ull * j, sink, o);
       rj = rn;
       // one piece at a time (the scheduler would otherwise hoist every
       // piece's DPP moves and selects and spill)
@@ -980,10 +981,10 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
       const uint64_t tb_beg = t16 > hb_end ? t16 : hb_end;
       const uint64_t oh = P + c, ot = tb_beg + c;
       const bool okh = fin && oh < hb_end, okt = fin && ot < P + sp.n;
-      const uint32_t bh = *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : zp);
-      const uint32_t bt = *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : zp);
-      WAL_ST(okh, st_u8, oh, sink, bh);
-      WAL_ST(okt, st_u8, ot, sink + 1, bt);
+      const uint32_t bh = (MCK_WAL_EXP & 32) ? 0u : *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : zp);
+      const uint32_t bt = (MCK_WAL_EXP & 32) ? 0u : *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : zp);
+      WAL_ST(okh && !(MCK_WAL_EXP & 2), st_u8, oh, sink, bh);
+      WAL_ST(okt && !(MCK_WAL_EXP & 2), st_u8, ot, sink + 1, bt);
     }
 
     // ---- next unit (as crc_rows_loop) ----
@@ -1005,7 +1006,7 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
 #pragma unroll
     for (int m = 0; m < kHdr; m++) {
       const uint32_t b = c + (uint32_t)W * m;
-      const bool okb = fin && b < pad + hs;
+      const bool okb = fin && b < pad + hs && !(MCK_WAL_EXP & 4);
       const uint32_t val = b < pad ? 0u : wal_hdr_byte(b - pad, crc, sp.n, type, op.log_number);
       WAL_ST(okb, st_u8, hstart + b, sink + 2 + m, val);
     }
