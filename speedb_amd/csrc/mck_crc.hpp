@@ -849,7 +849,7 @@ constexpr uint32_t kLdsRowTicket = kLdsRowDesc + 16 * kRowDescCache;  // u32
 constexpr uint32_t kLdsRowMaskHead = kLdsRowTicket + 64;
 constexpr uint32_t kLdsRowMaskTail = kLdsRowMaskHead + 256;
 static_assert(kLdsRowMaskTail + 256 <= kLdsStep, "row tables must fit below the step tables");
-static_assert(kLdsRowTicket + 16 <= kLdsRowMaskHead, "ticket + total");
+static_assert(kLdsRowTicket + 24 <= kLdsRowMaskHead, "ticket + totals");
 static_assert(offsetof(CrcTables, gap_row) - offsetof(CrcTables, unshift) == kMaxUnshift * 512, "layout");
 static_assert(sizeof(((CrcTables*)nullptr)->gap_row[0]) == 512, "one row gap map = 32 slots");
 
@@ -1077,6 +1077,9 @@ __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, co
 // Also sums the share's span bytes into the u64 at kLdsRowTotal (zeroed
 // here; valid after the next __syncthreads + the atomics).
 constexpr uint32_t kLdsRowTotal = kLdsRowTicket + 8;  // u64
+// ... and the bytes the wave driver's 4 KiB rounds would cover (each span
+// rounded up to 4 KiB: a partial round costs it about as much as a full one)
+constexpr uint32_t kLdsRowWaveTotal = kLdsRowTicket + 16;  // u64
 // A workgroup's share of spans [first, first + count): span first + b + G t
 // (interleaved: the grid sweeps the batch front to back together) or, BLK,
 // the contiguous range [count b / G, count (b + 1) / G) (neighbouring spans
@@ -1099,23 +1102,32 @@ template <class Op, bool BLK = false>
 __device__ __forceinline__ void row_desc_stage(const Op& op, uint32_t first, uint32_t count, bool total) {
   const RowShare sh = row_share<BLK>(first, count);
   const uint32_t n = sh.n;
-  uint64_t sum = 0;
+  uint64_t sum = 0, wsum = 0;
   for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
     const uint32_t i = sh.idx(t);
     const uint64_t off = op.off(i);
     const uint32_t len = (uint32_t)op.len(i);
     sum += len;
+    wsum += ((uint64_t)len + 4095) & ~4095ull;
     const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, op.init_key(i)};
     *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsRowDesc + 16 * t)) = d;
   }
   if (threadIdx.x == 0) *lds_p32(kLdsRowTicket) = 0;
   if (total) {
-    // wave sum, then one LDS atomic per wave (after a barrier zeroes it)
-    for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 64);
-    if (threadIdx.x == 0) *lds_p64(kLdsRowTotal) = 0;
+    // wave sums, then one LDS atomic per wave (after a barrier zeroes them)
+    for (int m = 32; m >= 1; m >>= 1) {
+      sum += __shfl_xor(sum, m, 64);
+      wsum += __shfl_xor(wsum, m, 64);
+    }
+    if (threadIdx.x == 0) {
+      *lds_p64(kLdsRowTotal) = 0;
+      *lds_p64(kLdsRowWaveTotal) = 0;
+    }
     __syncthreads();
-    if ((threadIdx.x & 63) == 0)
+    if ((threadIdx.x & 63) == 0) {
       __hip_atomic_fetch_add(lds_p64(kLdsRowTotal), sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      __hip_atomic_fetch_add(lds_p64(kLdsRowWaveTotal), wsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
   }
 }
 
@@ -1245,14 +1257,24 @@ struct FeedRowCache {
 // above that.  force: 0 = by length, 1 = wave, 2 = rows16, 3 = rows8.
 constexpr uint32_t kAutoRows8Max = 640;    // mean span bytes
 constexpr uint32_t kAutoRows16Max = 2560;
+constexpr uint32_t kAutoRows16WasteMax = 8192;  // mean span bytes, with > 25 % of the wave rounds empty
 template <class Op, bool T, bool BLK = false>
 __device__ __forceinline__ void crc_auto_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                 const CrcTables* __restrict__ g, int force) {
   crc_rows_prologue<BLK>(op, first, count, lds, g, true);
   const RowShare sh = row_share<BLK>(first, count);
   const uint32_t share = sh.n;
-  const uint64_t mean = *lds_p64(kLdsRowTotal) / (share ? share : 1);
-  const int mode = force ? force : mean <= kAutoRows8Max ? 3 : mean <= kAutoRows16Max ? 2 : 1;
+  const uint64_t total = *lds_p64(kLdsRowTotal);
+  const uint64_t mean = total / (share ? share : 1);
+  // spans of a few KiB that leave the wave driver's last 4 KiB round mostly
+  // empty (blob records of 16 + 4096 B: 1 full + 1 nearly empty round) go
+  // to 16-lane rows as well (1 KiB rounds): blob verify 0.460 -> 0.559
+  const bool ragged4k = mean <= kAutoRows16WasteMax && 4 * *lds_p64(kLdsRowWaveTotal) > 5 * total;
+  const int mode = force                    ? force
+                   : mean <= kAutoRows8Max  ? 3
+                   : mean <= kAutoRows16Max ? 2
+                   : ragged4k               ? 2
+                                            : 1;
   if (mode == 3) {
     crc_rows_loop<Op, 8, BLK>(op, first, count, g);
   } else if (mode == 2) {
