@@ -217,6 +217,22 @@ def cpu_baseline(args, kind, block, sample, gpu_results):
     }
 
 
+def _auto(op):
+    """k_crc_auto's instantiation name for op (contiguous span ranges unless
+    MCK_CRC_ORDER=interleaved: the third template argument)."""
+    blk = "" if os.environ.get("MCK_CRC_ORDER") == "interleaved" else ", true"
+    return f"mck::k_crc_auto<{op}, true{blk}>"
+
+
+def _launches(count, dev):
+    """Suffix for a k_crc_auto batch the engine splits into launches of at
+    most ncu * 1528 spans (its LDS descriptor cache): the bench times the
+    whole step, profiles/pmc_to_traffic.py then sums the launches."""
+    import torch
+    nl = -(-count // (torch.cuda.get_device_properties(dev).multi_processor_count * 1528))
+    return f" ({nl} launch(es) per step, timed as the step)" if nl > 1 else ""
+
+
 def C_wal_verify(im, nblocks, stream):
     """mck_wal_verify_batch over the first nblocks blocks of a WalImage."""
     import speedb_amd as S
@@ -283,7 +299,7 @@ def make_workload(args, dev, rank, world):
                 res[im.checksum_type] = im.verify(stream=stream)
         w.step = step
         w.launches = len(imgs)
-        w.kernel = " + ".join({int(S.ChecksumType.kCRC32c): "mck::k_crc_auto<mck::OpCrcBlock<2>, true>",
+        w.kernel = " + ".join({int(S.ChecksumType.kCRC32c): _auto("mck::OpCrcBlock<2>"),
                                int(S.ChecksumType.kXXH3): "mck::k_xxh3_wave<mck::OpX3Block<2> >"}[int(t)]
                               for t in types)
         w.span_bytes = sum(im.payload_bytes + im.count for im in imgs)  # payload + type byte
@@ -400,13 +416,13 @@ def make_workload(args, dev, rank, world):
         if args.workload == "walrec":
             types = torch.from_numpy(rng.choice([1, 2, 3, 4], size=count).astype(np.uint8)).to(dev)
             w.step = lambda: S.wal_record_crc_batch(sp, types, 7, out=out, stream=stream)
-            w.kernel = "mck::k_crc_auto<mck::OpCrcWal, true>"
+            w.kernel = _auto("mck::OpCrcWal") + _launches(count, dev)
             w.desc = (f"WAL record CRCs (EmitPhysicalRecord, db/log_writer.cc:263-311): {count} records of "
                       f"{args.span_min}-{args.span_max} B per GPU at any byte offset, mck_wal_record_crc_batch")
         else:
             w.step = lambda: S.crc32c_batch(sp, out=out, stream=stream)
             w.kernel = {"1": "mck::k_crc_rows<mck::OpCrcValue>", "0": "mck::k_crc<mck::OpCrcValue, true>"}.get(
-                os.environ.get("MCK_CRC_ROWS", ""), "mck::k_crc_auto<mck::OpCrcValue, true>")
+                os.environ.get("MCK_CRC_ROWS", ""), _auto("mck::OpCrcValue") + _launches(count, dev))
             w.desc = (f"crc32c_batch over {count} ragged spans of {args.span_min}-{args.span_max} B per GPU "
                       "(explicit offsets/lengths)")
         w.span_bytes = int(lens.sum())
@@ -499,7 +515,7 @@ def make_workload(args, dev, rank, world):
         def step():
             S.blob.record_batch(False, img, offs, lens, status=status, stream=stream)
         w.step = step
-        w.kernel = "mck::k_crc_auto<mck::OpBlobRecord<false>, true>"
+        w.kernel = _auto("mck::OpBlobRecord<false>") + _launches(n, dev)
         w.span_bytes = n * rec
         w.alg_bytes = n * (rec + 8 + 4 + 1)
         w.desc = (f"blob file verify: {n} records per GPU ({kb} B key, {vb} B value), header CRC + blob CRC "
