@@ -180,6 +180,40 @@ def test_wal_write_batch_small_records_every_alignment(gpu, oracle, recycle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_write_batch_round_boundaries(gpu, oracle, recycle):
+    """Fragments whose cover sits at the one-pass writer's 1280-byte round
+    boundaries (one round / two rounds / three), at every source offset mod
+    16 and several output offsets: the piece that straddles two rounds is
+    stored from the previous round's carried piece (k_wal_write_il), the
+    CRC state crosses rounds through the 244-byte map."""
+    import torch
+
+    import speedb_amd as S
+    rng = np.random.default_rng(23)
+    base = [1200, 1249, 1250, 1264, 1265, 1266, 1279, 1280, 1281, 1296, 2500, 2529, 2545, 2560, 2561, 3830, 3840]
+    lens = np.array([n + d for n in base for d in range(0, 16)] * 2, dtype=np.int64)
+    rng.shuffle(lens)
+    src = rng.integers(0, 256, size=int(lens.sum()) + 16, dtype=np.uint8).tobytes()
+    for src_pad, start_pad in ((0, 0), (7, 5), (13, 9)):
+        offs = np.concatenate([[0], np.cumsum(lens[:-1])]) + src_pad
+        w = WalWriter(oracle, log_number=0x5151, recycle=recycle)
+        if start_pad:
+            w.add_record(b"q" * start_pad)
+        start = len(w.buf)
+        for o, n in zip(offs, lens):
+            w.add_record(src[o:o + n])
+        dev = torch.frombuffer(bytearray(src + bytes(64)), dtype=torch.uint8).to("cuda")
+        wr = S.WalBatchWriter(log_number=0x5151, recycle_log_files=recycle, block_offset=start)
+        got = wr.AddRecords(dev, offs, [int(n) for n in lens]).cpu().numpy().tobytes()
+        want = bytes(w.buf[start:])
+        assert len(got) == len(want)
+        if got != want:
+            i = next(k for k in range(len(got)) if got[k] != want[k])
+            raise AssertionError(f"pads {src_pad}/{start_pad}: first difference at stream offset {i + start}")
+
+
+@pytest.mark.gpu
 def test_wal_write_batch_rejects_misaligned_out(gpu):
     import torch
 
