@@ -268,7 +268,9 @@ def make_workload(args, dev, rank, world):
         out64 = torch.empty(count, dtype=torch.int64, device=dev)
         if args.workload == "crc32c":
             w.step = lambda: S.crc32c_batch(spans, out=out32, stream=stream)
-            w.kernel = CRC_UNIFORM_FULL
+            # 16-byte-multiple blocks: the whole-round uniform kernel; any
+            # other size (a 4300-B SST block): the ragged path's unit stream
+            w.kernel = CRC_UNIFORM_FULL if block % 4096 == 0 else _auto("mck::OpCrcValue") + _launches(count, dev)
             w.alg_bytes = count * (block + 4)
         else:
             w.step = lambda: S.xxh3_64_batch(spans, out=out64, stream=stream)

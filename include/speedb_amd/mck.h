@@ -322,7 +322,12 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes,
 #define MCK_WAL_R_TRAILING_DATA 10
 #define MCK_WAL_R_TS_INTERSPERSED 11
 #define MCK_WAL_R_TS_DECODE 12
-#define MCK_WAL_R_UNKNOWN_TYPE_BASE 256 /* + the record type */
+/* Reader::UpdateRecordedTimestampSize (db/log_reader.cc:594-616) */
+#define MCK_WAL_R_TS_ZERO_SIZE 13
+#define MCK_WAL_R_TS_CF_UPDATE 14
+/* "unknown record type %u" of header[6] read as a (signed) char: types
+ * >= 128 print as 4294967xxx, as in the reference */
+#define MCK_WAL_R_UNKNOWN_TYPE_BASE 256 /* + the record type byte */
 
 /* One Reporter::Corruption(bytes, reason) call. */
 typedef struct mck_wal_report {
@@ -371,6 +376,50 @@ int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t log_number,
 /* Text of a MCK_WAL_R_* reason ("checksum mismatch", "unknown record type
  * 101", ...); Status::Corruption(reason).ToString() is "Corruption: " + it. */
 const char* mck_wal_reason_string(int reason);
+
+/* ---- log::FragmentBufferedReader: tailing a WAL that is being written ----
+ * db/log_reader.cc:618-931 (ReadRecord, TryReadMore, TryReadFragment,
+ * UnmarkEOF), the reader of secondary instances and WAL tailing
+ * (allow_retry_read).  Unlike log::Reader it never treats a short read as
+ * the end of the log: a record whose header or body is not yet written is
+ * kept (its fragments across calls) and ReadRecord returns "no record yet";
+ * the caller lets the file grow and calls again.  The file is a host image
+ * that only grows (bytes already handed out must not change); its CRC
+ * verdicts come from mck_wal_verify_batch over the same image, as for
+ * mck_wal_read_records (a block verified while partially written must be
+ * verified again once it grew).  No WAL compression (kSetCompressionType:
+ * MCK_ENOTSUP), no I/O errors (a memory image cannot fail a read). */
+typedef struct mck_wal_tail mck_wal_tail;
+
+/* A reader of log `log_number` (checksum on).  *out = the reader. */
+int mck_wal_tail_create(uint32_t log_number, mck_wal_tail** out);
+void mck_wal_tail_destroy(mck_wal_tail* r);
+
+/* The file as written so far: [wal, wal + nbytes) and the per-block verdicts
+ * for it (NULL = trust every CRC).  Call before ReadRecord whenever the file
+ * grew; the pointers must stay valid until the next call. */
+int mck_wal_tail_set_image(mck_wal_tail* r, const void* wal, uint64_t nbytes,
+                           const mck_wal_block_result* verified);
+
+/* FragmentBufferedReader::ReadRecord.  Returns 1 with a record (*nfrags
+ * payload fragments, *record_bytes, *last_record_offset = LastRecordOffset;
+ * the fragments via mck_wal_tail_record_fragments), 0 when no complete
+ * record is available yet, a negative MCK_E* code on error. */
+int mck_wal_tail_read_record(mck_wal_tail* r, uint64_t* nfrags, uint64_t* record_bytes,
+                             uint64_t* last_record_offset);
+
+/* The fragments of the record the last successful read returned (src_off in
+ * the file, dst_off within the record); cap >= its nfrags. */
+int mck_wal_tail_record_fragments(const mck_wal_tail* r, mck_wal_fragment* frags, uint64_t cap);
+
+/* Reader::UnmarkEOF / IsEOF. */
+int mck_wal_tail_unmark_eof(mck_wal_tail* r);
+int mck_wal_tail_is_eof(const mck_wal_tail* r);
+
+/* Reporter::Corruption calls so far: *n reports (up to cap stored) and the
+ * total dropped bytes. */
+int mck_wal_tail_reports(const mck_wal_tail* r, mck_wal_report* reports, uint64_t cap,
+                         uint64_t* n, uint64_t* dropped_bytes);
 
 
 /* ---- long spans / whole files ----------------------- */

@@ -119,6 +119,14 @@ SIGNATURES = [
     ("mck_wal_gather_batch", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp]),
     ("mck_wal_read_records", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, vp, vp]),
     ("mck_wal_reason_string", ctypes.c_char_p, [ctypes.c_int]),
+    ("mck_wal_tail_create", ctypes.c_int, [ctypes.c_uint32, vp]),
+    ("mck_wal_tail_destroy", None, [vp]),
+    ("mck_wal_tail_set_image", ctypes.c_int, [vp, vp, ctypes.c_uint64, vp]),
+    ("mck_wal_tail_read_record", ctypes.c_int, [vp, vp, vp, vp]),
+    ("mck_wal_tail_record_fragments", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
+    ("mck_wal_tail_unmark_eof", ctypes.c_int, [vp]),
+    ("mck_wal_tail_is_eof", ctypes.c_int, [vp]),
+    ("mck_wal_tail_reports", ctypes.c_int, [vp, vp, ctypes.c_uint64, vp, vp]),
     ("mck_blob_list_records", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
     ("mck_blob_record_batch", ctypes.c_int,
      [ctypes.c_int, vp, vp, vp, ctypes.c_uint32, vp, vp, vp]),

@@ -682,24 +682,31 @@ def WalRecover(wal: bytes, log_number: int = 0,
     import numpy as np
     torch = _torch()
     dev = torch.device("cuda") if device is None else device
+    st = stream if stream is not None else torch.cuda.current_stream(dev)
     wal = bytes(wal)
-    img = torch.frombuffer(bytearray(wal + bytes(64)), dtype=torch.uint8).to(dev)
-    blocks = wal_verify_batch(img, len(wal), log_number, stream=stream) if (len(wal) and checksum) else None
-    plan = wal_read_records(wal, log_number, recovery_mode, blocks)
-    nbytes, nf = plan.records_bytes, plan.nfrags
-    out = torch.zeros(nbytes + 64, dtype=torch.uint8, device=dev)
-    if nf:
-        d_frags = torch.frombuffer(bytearray(bytes(plan.frags)[:nf * ctypes.sizeof(mck_wal_fragment)]),
-                                   dtype=torch.uint8).to(dev)
-        check(lib.mck_wal_gather_batch(img.data_ptr(), d_frags.data_ptr(), nf, out.data_ptr(), _stream(stream)),
-              "mck_wal_gather_batch")
-    offs, lens = plan.rec_offsets, plan.rec_lengths
-    if len(offs):
-        sp = Spans(out, len(offs), offsets=torch.from_numpy(offs.astype(np.int64)).to(dev),
-                   lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
-        x3 = xxh3_64_batch(sp, stream=stream).cpu().numpy().view(np.uint64)
-    else:
-        x3 = np.zeros(0, np.uint64)
+    # uploads, kernels and readbacks all on `st`: inside the context every
+    # torch op (.to, zeros, .cpu) is queued on it, and .cpu() waits for it --
+    # the host walk never reads verdicts the kernel has not written
+    with torch.cuda.stream(st):
+        img = torch.frombuffer(bytearray(wal + bytes(64)), dtype=torch.uint8).to(dev)
+        blocks = wal_verify_batch(img, len(wal), log_number, stream=st) if (len(wal) and checksum) else None
+        if blocks is not None:
+            st.synchronize()
+        plan = wal_read_records(wal, log_number, recovery_mode, blocks)
+        nbytes, nf = plan.records_bytes, plan.nfrags
+        out = torch.zeros(nbytes + 64, dtype=torch.uint8, device=dev)
+        if nf:
+            d_frags = torch.frombuffer(bytearray(bytes(plan.frags)[:nf * ctypes.sizeof(mck_wal_fragment)]),
+                                       dtype=torch.uint8).to(dev)
+            check(lib.mck_wal_gather_batch(img.data_ptr(), d_frags.data_ptr(), nf, out.data_ptr(), _stream(st)),
+                  "mck_wal_gather_batch")
+        offs, lens = plan.rec_offsets, plan.rec_lengths
+        if len(offs):
+            sp = Spans(out, len(offs), offsets=torch.from_numpy(offs.astype(np.int64)).to(dev),
+                       lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
+            x3 = xxh3_64_batch(sp, stream=st).cpu().numpy().view(np.uint64)
+        else:
+            x3 = np.zeros(0, np.uint64)
     return WalRecovery(out[:nbytes], offs, lens, plan.rec_file_offsets, x3, blocks, plan.reports,
                        plan.dropped_bytes, plan.message)
 
@@ -714,8 +721,132 @@ def WalReadRecords(wal: bytes, log_number: int = 0, device=None, stream=None):
     return r.records, r.rec_offsets, r.rec_lengths, r.record_checksums, r.blocks
 
 
+class FragmentBufferedReader:
+    """log::FragmentBufferedReader (db/log_reader.cc:618-931): reads a WAL
+    that is still being written (secondary instances, WAL tailing;
+    allow_retry_read).  ``SetFile(image)`` gives the file as written so far
+    (it may only grow); ``ReadRecord()`` returns the next record's bytes or
+    None when no complete record is available yet (a partly written record
+    is kept; call again after the file grew).  The physical records' CRCs:
+    ``verify="device"`` runs mck_wal_verify_batch on the blocks that changed
+    since the last call (the verdicts a host walk then consumes),
+    ``verify=callable(image) -> per-block results`` supplies them (a CPU
+    walk in the CPU tests), ``verify=None`` trusts every CRC."""
+
+    def __init__(self, log_number: int = 0, verify="device", device=None, stream=None):
+        import numpy as np
+        self._np = np
+        self.log_number = log_number & 0xFFFFFFFF
+        self.verify = verify
+        self.device = device
+        self.stream = stream
+        h = ctypes.c_void_p()
+        check(lib.mck_wal_tail_create(self.log_number, ctypes.byref(h)), "mck_wal_tail_create")
+        self._h = h
+        self._img = b""
+        self._host = None
+        self._ver = None
+        self._dev = None       # device image (capacity grows by doubling)
+        self._dver = None      # device per-block verdicts
+        self._clean = 0        # blocks [0, _clean) were verified complete
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            lib.mck_wal_tail_destroy(h)
+            self._h = None
+
+    def _device_verdicts(self, img: bytes):
+        torch = _torch()
+        np = self._np
+        dev = torch.device("cuda") if self.device is None else self.device
+        st = self.stream if self.stream is not None else torch.cuda.current_stream(dev)
+        nb = -(-len(img) // 32768)
+        with torch.cuda.stream(st):
+            need = nb * 32768 + 64
+            if self._dev is None or self._dev.numel() < need:
+                cap = max(need, 2 * (self._dev.numel() if self._dev is not None else 0), 1 << 20)
+                old = self._dev
+                self._dev = torch.zeros(cap, dtype=torch.uint8, device=dev)
+                ver = torch.zeros((max(nb, cap // 32768), 4), dtype=torch.int32, device=dev)
+                if old is not None:
+                    self._dev[:old.numel()].copy_(old)
+                    ver[:self._dver.shape[0]].copy_(self._dver)
+                self._dver = ver
+            # upload and re-verify from the first block not yet verified complete
+            lo = self._clean
+            start = lo * 32768
+            if len(img) > start:
+                self._dev[start:len(img)].copy_(torch.frombuffer(bytearray(img[start:]), dtype=torch.uint8))
+                check(lib.mck_wal_verify_batch(self._dev.data_ptr() + start, len(img) - start, self.log_number,
+                                               self._dver[lo:].data_ptr(), _stream(st)), "mck_wal_verify_batch")
+            self._clean = len(img) // 32768
+            return np.ascontiguousarray(self._dver[:nb].cpu().numpy().astype(np.int32))
+
+    def SetFile(self, image) -> None:
+        img = bytes(image)
+        if len(img) < len(self._img) or img[:len(self._img)] != self._img:
+            raise ValueError("a WAL file only grows: the bytes already written must not change")
+        self._img = img
+        np = self._np
+        if self.verify == "device":
+            ver = self._device_verdicts(img) if img else None
+        elif callable(self.verify):
+            ver = np.ascontiguousarray(np.asarray(self.verify(img), dtype=np.int64).astype(np.int32)) if img else None
+        else:
+            ver = None
+        self._host = ctypes.create_string_buffer(img, len(img) + 1)
+        self._ver = ver
+        check(lib.mck_wal_tail_set_image(self._h, self._host, len(img),
+                                         ver.ctypes.data if ver is not None else None), "mck_wal_tail_set_image")
+
+    def ReadRecord(self) -> Optional[bytes]:
+        nf, nb, lro = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        rc = lib.mck_wal_tail_read_record(self._h, ctypes.byref(nf), ctypes.byref(nb), ctypes.byref(lro))
+        if rc < 0:
+            check(rc, "mck_wal_tail_read_record")
+        if rc == 0:
+            return None
+        frags = (mck_wal_fragment * max(nf.value, 1))()
+        check(lib.mck_wal_tail_record_fragments(self._h, ctypes.addressof(frags), nf.value),
+              "mck_wal_tail_record_fragments")
+        self.last_record_offset = lro.value
+        out = bytearray(nb.value)
+        for f in frags[:nf.value]:
+            out[f.dst_off:f.dst_off + f.length] = self._img[f.src_off:f.src_off + f.length]
+        return bytes(out)
+
+    def LastRecordOffset(self) -> int:
+        return getattr(self, "last_record_offset", 0)
+
+    def UnmarkEOF(self) -> None:
+        check(lib.mck_wal_tail_unmark_eof(self._h), "mck_wal_tail_unmark_eof")
+
+    def IsEOF(self) -> bool:
+        return bool(lib.mck_wal_tail_is_eof(self._h))
+
+    def _reports(self):
+        n, dropped = ctypes.c_uint64(), ctypes.c_uint64()
+        check(lib.mck_wal_tail_reports(self._h, None, 0, ctypes.byref(n), ctypes.byref(dropped)), "reports")
+        reps = (mck_wal_report * max(n.value, 1))()
+        check(lib.mck_wal_tail_reports(self._h, ctypes.addressof(reps), n.value, ctypes.byref(n),
+                                       ctypes.byref(dropped)), "reports")
+        return [(r.offset, r.bytes, lib.mck_wal_reason_string(r.reason).decode()) for r in reps[:n.value]], \
+            dropped.value
+
+    @property
+    def dropped_bytes(self) -> int:
+        return self._reports()[1]
+
+    @property
+    def message(self) -> str:
+        """ReportCollector::message_: "Corruption: <reason>" per report."""
+        return "".join("Corruption: " + r[2] for r in self._reports()[0])
+
+
 __all__ += ["wal_plan", "WalBatchWriter", "mck_wal_fragment", "wal_list_records", "WalReadRecords",
-            "WALRecoveryMode", "wal_read_records", "WalReadPlan", "WalRecover", "WalRecovery"]
+            "WALRecoveryMode", "wal_read_records", "WalReadPlan", "WalRecover", "WalRecovery",
+            "FragmentBufferedReader"]
 
 
 # ---------------------------------------------------------------------------

@@ -532,9 +532,14 @@ __device__ __forceinline__ uint32_t crc_finish(uint32_t s, const CrcSpan& sp, co
   return sp.empty ? sp.init_crc : ~p;
 }
 
-// CRC Extend by one byte on a finished CRC value (all lanes identical).
+// CRC Extend by one byte on a finished CRC value (all lanes identical):
+// eight shift-and-reduce steps, no table, so it works under every driver's
+// LDS image (the unit driver's has no ext1 map).
 __device__ __forceinline__ uint32_t crc_extend_byte(uint32_t crc, uint8_t b) {
-  return ~crc_nibmap(kLdsExt1, ~crc ^ (uint32_t)b);
+  uint32_t c = ~crc ^ (uint32_t)b;
+#pragma unroll
+  for (int k = 0; k < 8; k++) c = (c >> 1) ^ (kCrc32cPoly & (0u - (c & 1u)));
+  return ~c;
 }
 
 __device__ __forceinline__ uint32_t crc_mask(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
@@ -1255,6 +1260,7 @@ struct FeedRowCache {
 // length (the host cannot see device-resident lengths): 8-lane rows for
 // short spans, 16-lane rows for spans up to a few KiB, the wave driver
 // above that.  force: 0 = by length, 1 = wave, 2 = rows16, 3 = rows8.
+// (Superseded for long spans by crc_auto_units_driver, mck_crc_units.hpp.)
 constexpr uint32_t kAutoRows8Max = 640;    // mean span bytes
 constexpr uint32_t kAutoRows16Max = 2560;
 constexpr uint32_t kAutoRows16WasteMax = 8192;  // mean span bytes, with > 25 % of the wave rounds empty

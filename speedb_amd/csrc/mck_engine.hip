@@ -199,7 +199,7 @@ int crc_auto_force() {
   static const int v = [] {
     const char* e = getenv("MCK_CRC_AUTO");
     if (!e) return 0;
-    return !strcmp(e, "wave") ? 1 : !strcmp(e, "rows16") ? 2 : !strcmp(e, "rows8") ? 3 : 0;
+    return !strcmp(e, "wave") ? 1 : !strcmp(e, "rows16") ? 2 : !strcmp(e, "rows8") ? 3 : !strcmp(e, "units") ? 4 : 0;
   }();
   return v;
 }

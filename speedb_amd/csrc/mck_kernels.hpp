@@ -7,6 +7,7 @@
 #include <stdint.h>
 
 #include "mck_crc.hpp"
+#include "mck_crc_units.hpp"
 #include "mck_xxh.hpp"
 
 namespace mck {
@@ -235,11 +236,11 @@ __global__ __launch_bounds__(1024) void k_crc_rows(Op op, uint32_t first, uint32
   crc_rows_driver<Op, W>(op, first, count, lds, &g_crc_tables);
 }
 
-// ragged batches: driver chosen per workgroup (crc_auto_driver)
+// ragged batches: driver chosen per workgroup (crc_auto_units_driver)
 template <class Op, bool T, bool BLK = false>
 __global__ __launch_bounds__(1024) void k_crc_auto(Op op, uint32_t first, uint32_t count, int force) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_auto_driver<Op, T, BLK>(op, first, count, lds, &g_crc_tables, force);
+  crc_auto_units_driver<Op, T, BLK>(op, first, count, lds, &g_crc_tables, force);
 }
 
 // uniform batches (see CrcUniform)

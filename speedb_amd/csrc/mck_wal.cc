@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <new>
 #include <vector>
 
 #include "../../include/speedb_amd/mck.h"
@@ -94,6 +95,31 @@ constexpr uint32_t kZeroType = 0, kSetCompressionType = 9, kUserDefinedTimestamp
 constexpr int kEof = 12, kBadRecord = 13, kBadHeader = 14, kOldRecord = 15, kBadRecordLen = 16,
               kBadRecordChecksum = 17;
 
+// header[6] as the reference reads it: `const unsigned int type = header[6]`
+// with a (signed) char header, so bytes >= 128 sign-extend.
+inline uint32_t header_type(const uint8_t* h) { return (uint32_t)(int32_t)(int8_t)h[6]; }
+inline int unknown_type_reason(uint32_t type) { return MCK_WAL_R_UNKNOWN_TYPE_BASE + (int)(type & 255); }
+
+// Reader::UpdateRecordedTimestampSize (db/log_reader.cc:594-616) over a
+// decoded UserDefinedTimestampSizeRecord (util/udt_util.h:46-65: [cf LE32,
+// ts size LE16] pairs): the first entry with a zero size, or for a column
+// family already recorded in this log, is the corruption reported.
+struct TsRecorder {
+  std::vector<uint32_t> cfs;
+  // 0 = OK, else the MCK_WAL_R_* reason
+  int update(const uint8_t* p, uint32_t n) {
+    for (uint32_t o = 0; o + 6 <= n; o += 6) {
+      const uint32_t cf = (uint32_t)p[o] | ((uint32_t)p[o + 1] << 8) | ((uint32_t)p[o + 2] << 16) |
+                          ((uint32_t)p[o + 3] << 24);
+      const uint32_t ts = (uint32_t)p[o + 4] | ((uint32_t)p[o + 5] << 8);
+      if (ts == 0) return MCK_WAL_R_TS_ZERO_SIZE;
+      if (std::find(cfs.begin(), cfs.end(), cf) != cfs.end()) return MCK_WAL_R_TS_CF_UPDATE;
+      cfs.push_back(cf);
+    }
+    return 0;
+  }
+};
+
 struct WalReader {
   const uint8_t* d;
   uint64_t nbytes;
@@ -156,7 +182,7 @@ struct WalReader {
       }
       const uint8_t* h = d + buf_off;
       const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
-      const uint32_t type = h[6];
+      const uint32_t type = header_type(h);
       uint32_t hs = MCK_WAL_kHeaderSize;
       if ((type >= 5 && type <= 8) || type == kRecyclableUserDefinedTimestampSizeType) {
         if (end_of_buffer_offset - buf_size == 0) recycled = true;
@@ -208,10 +234,14 @@ extern "C" const char* mck_wal_reason_string(int reason) {
     case MCK_WAL_R_TRAILING_DATA: return "error reading trailing data";
     case MCK_WAL_R_TS_INTERSPERSED: return "user-defined timestamp size record interspersed partial record";
     case MCK_WAL_R_TS_DECODE: return "could not decode user-defined timestamp size record";
+    case MCK_WAL_R_TS_ZERO_SIZE: return "User-defined timestamp size record contains zero timestamp size.";
+    case MCK_WAL_R_TS_CF_UPDATE:
+      return "User-defined timestamp size record contains update to recorded column family.";
     default:
       if (reason >= MCK_WAL_R_UNKNOWN_TYPE_BASE && reason < MCK_WAL_R_UNKNOWN_TYPE_BASE + 256) {
         static thread_local char buf[40];
-        snprintf(buf, sizeof buf, "unknown record type %u", (unsigned)(reason - MCK_WAL_R_UNKNOWN_TYPE_BASE));
+        const uint8_t b = (uint8_t)(reason - MCK_WAL_R_UNKNOWN_TYPE_BASE);
+        snprintf(buf, sizeof buf, "unknown record type %u", (unsigned)(int)(int8_t)b);
         return buf;
       }
       return "";
@@ -230,6 +260,7 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
     return MCK_EINVAL;
   }
   WalReader R{static_cast<const uint8_t*>(wal), nbytes, log_number, recovery_mode, verified};
+  TsRecorder ts;
   std::vector<mck_wal_fragment> fr;
   std::vector<uint64_t> roff, rfile;
   std::vector<uint32_t> rlen;
@@ -302,8 +333,15 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
         return MCK_ENOTSUP;
       } else if (t == (int)kUserDefinedTimestampSizeType || t == (int)kRecyclableUserDefinedTimestampSizeType) {
         if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_TS_INTERSPERSED);
+        // prospective_record_offset = last_record_offset_ = this record's
+        // offset: a record it interrupted and that then completes reports it
+        cur_file = phys;
         scratch_clear();
-        if (flen % 6) R.report(phys, flen, MCK_WAL_R_TS_DECODE);  // util/udt_util.h:46-64
+        if (flen % 6) {
+          R.report(phys, flen, MCK_WAL_R_TS_DECODE);  // util/udt_util.h:46-64
+        } else if (const int why = ts.update(R.d + foff, flen)) {
+          R.report(phys, flen, why);
+        }
       } else if (t == kBadHeader || t == kEof) {
         if (t == kBadHeader && R.strict()) R.report(phys, drop_size, MCK_WAL_R_TRUNCATED_HEADER);
         if (in_fragmented_record) {
@@ -349,7 +387,7 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
           scratch_clear();
         }
       } else {  // unknown record type
-        R.report(phys, flen + (in_fragmented_record ? scratch_size() : 0), MCK_WAL_R_UNKNOWN_TYPE_BASE + (t & 255));
+        R.report(phys, flen + (in_fragmented_record ? scratch_size() : 0), unknown_type_reason((uint32_t)t));
         in_fragmented_record = false;
         scratch_clear();
       }
@@ -409,5 +447,311 @@ extern "C" int mck_wal_list_records(const void* wal, uint64_t nbytes, uint32_t l
   if (nfrags) *nfrags = o.nfrags;
   if (nrecords) *nrecords = o.nrecords;
   if (records_bytes) *records_bytes = o.records_bytes;
+  return MCK_OK;
+}
+
+// ---------------------------------------------------------------------------
+// log::FragmentBufferedReader (db/log_reader.cc:618-931) over a growing host
+// image: the reader of secondary instances / WAL tailing.  The "file" is
+// [0, avail); a read returns what is written so far.  Restated over file
+// offsets: buffer_ = [buf_off, buf_off + buf_size), fragments_ = the payload
+// fragments of the record being assembled (kept across ReadRecord calls).
+// ---------------------------------------------------------------------------
+struct mck_wal_tail {
+  uint32_t log_number = 0;
+  const uint8_t* d = nullptr;
+  uint64_t avail = 0;
+  const mck_wal_block_result* verified = nullptr;
+  uint64_t buf_off = 0, buf_size = 0, end_of_buffer_offset = 0;
+  uint64_t eof_offset = 0;
+  bool eof = false, recycled = false, first_record_read = false, in_fragmented_record = false;
+  uint64_t last_record_offset = 0;
+  std::vector<mck_wal_fragment> fragments;  // fragments_ (dst_off within the record)
+  uint64_t fragments_size = 0;
+  std::vector<mck_wal_fragment> record;     // the last record returned
+  uint64_t record_bytes = 0;
+  std::vector<mck_wal_report> reports;
+  uint64_t dropped = 0;
+  TsRecorder ts;
+  int err = MCK_OK;
+
+  void report(uint64_t off, uint64_t bytes, int reason) {
+    reports.push_back(mck_wal_report{off, bytes, reason, 0});
+    dropped += bytes;
+  }
+  uint64_t file_read(uint64_t n) {  // SequentialFileReader::Read of n bytes
+    const uint64_t got = std::min<uint64_t>(n, avail > end_of_buffer_offset ? avail - end_of_buffer_offset : 0);
+    end_of_buffer_offset += got;
+    return got;
+  }
+  // Reader::UnmarkEOFInternal (:340-397): read the rest of the block the EOF
+  // was in, behind what is left of the buffer
+  void unmark_eof_internal() {
+    const uint64_t remaining = MCK_WAL_kBlockSize - eof_offset;
+    const uint64_t added = file_read(remaining);
+    buf_size += added;  // buffer_ = [consumed, eof_offset + added) of the block
+    if (added < remaining) {
+      eof = true;
+      eof_offset += added;
+    } else {
+      eof_offset = 0;
+    }
+  }
+  // FragmentBufferedReader::UnmarkEOF (:777-783)
+  void unmark_eof() {
+    eof = false;
+    unmark_eof_internal();
+  }
+  // :785-823 TryReadMore (no read errors on a memory image)
+  bool try_read_more() {
+    if (!eof) {  // the last read was a full block: what is left is a trailer
+      buf_off = end_of_buffer_offset;
+      buf_size = file_read(MCK_WAL_kBlockSize);
+      if (buf_size < MCK_WAL_kBlockSize) {
+        eof = true;
+        eof_offset = buf_size;
+      }
+      return true;
+    }
+    unmark_eof();
+    return true;
+  }
+  bool crc_ok(uint64_t h) {
+    if (!verified) return true;
+    const mck_wal_block_result& r = verified[h / MCK_WAL_kBlockSize];
+    const uint32_t o = (uint32_t)(h % MCK_WAL_kBlockSize);
+    if (o < r.stop_offset) return true;
+    if (o == r.stop_offset && r.status == MCK_WAL_BAD_CHECKSUM) return false;
+    err = MCK_EINVAL;  // stale or foreign verdicts (a block verified before it grew)
+    return false;
+  }
+  // :826-931 TryReadFragment; true = the caller processes *type_or_err
+  bool try_read_fragment(uint64_t* frag_off, uint32_t* frag_len, uint64_t* drop_size, uint32_t* type_or_err) {
+    while (buf_size < MCK_WAL_kHeaderSize) {
+      const uint64_t old = buf_size;
+      try_read_more();
+      if (old == buf_size) return false;
+    }
+    const uint8_t* h = d + buf_off;
+    const uint32_t type = header_type(h);
+    const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
+    uint32_t hs = MCK_WAL_kHeaderSize;
+    if ((type >= 5 && type <= 8) || type == kRecyclableUserDefinedTimestampSizeType) {
+      if (end_of_buffer_offset - buf_size == 0) recycled = true;
+      hs = MCK_WAL_kRecyclableHeaderSize;
+      while (buf_size < MCK_WAL_kRecyclableHeaderSize) {
+        const uint64_t old = buf_size;
+        try_read_more();
+        if (old == buf_size) return false;
+      }
+      const uint8_t* g = d + buf_off;
+      const uint32_t ln = (uint32_t)g[7] | ((uint32_t)g[8] << 8) | ((uint32_t)g[9] << 16) | ((uint32_t)g[10] << 24);
+      if (ln != log_number) {
+        *type_or_err = kOldRecord;
+        return true;
+      }
+    }
+    while ((uint64_t)hs + length > buf_size) {
+      const uint64_t old = buf_size;
+      try_read_more();
+      if (old == buf_size) return false;
+    }
+    if (type == kZeroType && length == 0) {
+      buf_size = 0;
+      *type_or_err = kBadRecord;
+      return true;
+    }
+    if (!crc_ok(buf_off)) {
+      *drop_size = buf_size;
+      buf_size = 0;
+      *type_or_err = kBadRecordChecksum;
+      return true;
+    }
+    *frag_off = buf_off + hs;
+    *frag_len = length;
+    buf_off += hs + length;
+    buf_size -= hs + length;
+    *type_or_err = type;
+    return true;
+  }
+  void fragments_clear() {
+    fragments.clear();
+    fragments_size = 0;
+  }
+  void fragments_append(uint64_t off, uint32_t len, uint32_t type) {
+    fragments.push_back(mck_wal_fragment{off, fragments_size, len, (uint8_t)type, 0, 0});
+    fragments_size += len;
+  }
+  // :618-775 ReadRecord; 1 = a record, 0 = none (yet)
+  int read_record() {
+    uint64_t prospective_record_offset = 0;
+    const uint64_t physical_record_offset = end_of_buffer_offset - buf_size;
+    uint64_t drop_size = 0, foff = 0;
+    uint32_t flen = 0, t = 0;
+    while (try_read_fragment(&foff, &flen, &drop_size, &t)) {
+      if (err) return err;
+      if (t == 1 || t == 5) {  // kFullType
+        if (in_fragmented_record && fragments_size) report(physical_record_offset, fragments_size, MCK_WAL_R_PARTIAL_WITHOUT_END_1);
+        fragments_clear();
+        record.assign(1, mck_wal_fragment{foff, 0, flen, (uint8_t)t, 0, 0});
+        record_bytes = flen;
+        prospective_record_offset = physical_record_offset;
+        last_record_offset = prospective_record_offset;
+        first_record_read = true;
+        in_fragmented_record = false;
+        return 1;
+      } else if (t == 2 || t == 6) {  // kFirstType
+        if (in_fragmented_record || fragments_size) report(physical_record_offset, fragments_size, MCK_WAL_R_PARTIAL_WITHOUT_END_2);
+        prospective_record_offset = physical_record_offset;
+        fragments_clear();
+        fragments_append(foff, flen, t);
+        in_fragmented_record = true;
+      } else if (t == 3 || t == 7) {  // kMiddleType
+        if (!in_fragmented_record)
+          report(physical_record_offset, flen, MCK_WAL_R_MISSING_START_1);
+        else
+          fragments_append(foff, flen, t);
+      } else if (t == 4 || t == 8) {  // kLastType
+        if (!in_fragmented_record) {
+          report(physical_record_offset, flen, MCK_WAL_R_MISSING_START_2);
+        } else {
+          fragments_append(foff, flen, t);
+          record = fragments;
+          record_bytes = fragments_size;
+          fragments_clear();
+          last_record_offset = prospective_record_offset;
+          first_record_read = true;
+          in_fragmented_record = false;
+          return 1;
+        }
+      } else if (t == kSetCompressionType) {
+        mck_internal_set_error("WAL compression (kSetCompressionType record) is not supported");
+        return MCK_ENOTSUP;
+      } else if (t == kUserDefinedTimestampSizeType || t == kRecyclableUserDefinedTimestampSizeType) {
+        // (:712 tests scratch, which ReadRecord cleared: never reported)
+        fragments_clear();
+        prospective_record_offset = physical_record_offset;
+        last_record_offset = prospective_record_offset;
+        in_fragmented_record = false;
+        if (flen % 6) {
+          report(physical_record_offset, flen, MCK_WAL_R_TS_DECODE);
+        } else if (const int why = ts.update(d + foff, flen)) {
+          report(physical_record_offset, flen, why);
+        }
+      } else if (t == (uint32_t)kBadHeader || t == (uint32_t)kBadRecord || t == (uint32_t)kEof ||
+                 t == (uint32_t)kOldRecord) {
+        if (in_fragmented_record) {
+          report(physical_record_offset, fragments_size, MCK_WAL_R_ERROR_IN_MIDDLE);
+          in_fragmented_record = false;
+          fragments_clear();
+        }
+        // kOldRecord does not advance the buffer: the reference's loop would
+        // parse the same header again forever; report "no record" instead
+        if (t == (uint32_t)kOldRecord) return 0;
+      } else if (t == (uint32_t)kBadRecordChecksum) {
+        if (recycled) {
+          fragments_clear();
+          return 0;
+        }
+        report(physical_record_offset, drop_size, MCK_WAL_R_CHECKSUM_MISMATCH);
+        if (in_fragmented_record) {
+          report(physical_record_offset, fragments_size, MCK_WAL_R_ERROR_IN_MIDDLE);
+          in_fragmented_record = false;
+          fragments_clear();
+        }
+      } else {
+        report(physical_record_offset, flen + (in_fragmented_record ? fragments_size : 0), unknown_type_reason(t));
+        in_fragmented_record = false;
+        fragments_clear();
+      }
+    }
+    return err ? err : 0;
+  }
+};
+
+extern "C" int mck_wal_tail_create(uint32_t log_number, mck_wal_tail** out) {
+  mck_internal_set_error("");
+  if (!out) {
+    mck_internal_set_error("out is NULL");
+    return MCK_EINVAL;
+  }
+  *out = new (std::nothrow) mck_wal_tail();
+  if (!*out) {
+    mck_internal_set_error("out of memory");
+    return MCK_ENOMEM;
+  }
+  (*out)->log_number = log_number;
+  return MCK_OK;
+}
+
+extern "C" void mck_wal_tail_destroy(mck_wal_tail* r) { delete r; }
+
+extern "C" int mck_wal_tail_set_image(mck_wal_tail* r, const void* wal, uint64_t nbytes,
+                                      const mck_wal_block_result* verified) {
+  mck_internal_set_error("");
+  if (!r || (!wal && nbytes)) {
+    mck_internal_set_error("reader / wal is NULL");
+    return MCK_EINVAL;
+  }
+  if (nbytes < r->end_of_buffer_offset) {
+    mck_internal_set_error("the WAL image shrank below what the reader has read");
+    return MCK_EINVAL;
+  }
+  r->d = static_cast<const uint8_t*>(wal);
+  r->avail = nbytes;
+  r->verified = verified;
+  return MCK_OK;
+}
+
+extern "C" int mck_wal_tail_read_record(mck_wal_tail* r, uint64_t* nfrags, uint64_t* record_bytes,
+                                        uint64_t* last_record_offset) {
+  mck_internal_set_error("");
+  if (!r) {
+    mck_internal_set_error("reader is NULL");
+    return MCK_EINVAL;
+  }
+  if (r->err) return r->err;
+  const int rc = r->read_record();
+  if (rc < 0) {
+    if (rc == MCK_EINVAL) mck_internal_set_error("verify results do not match the WAL image (stale verdicts?)");
+    return rc;
+  }
+  if (rc == 1) {
+    if (nfrags) *nfrags = r->record.size();
+    if (record_bytes) *record_bytes = r->record_bytes;
+    if (last_record_offset) *last_record_offset = r->last_record_offset;
+  }
+  return rc;
+}
+
+extern "C" int mck_wal_tail_record_fragments(const mck_wal_tail* r, mck_wal_fragment* frags, uint64_t cap) {
+  mck_internal_set_error("");
+  if (!r || (!frags && !r->record.empty())) {
+    mck_internal_set_error("reader / frags is NULL");
+    return MCK_EINVAL;
+  }
+  if (cap < r->record.size()) {
+    mck_internal_set_error("frags capacity too small");
+    return MCK_EINVAL;
+  }
+  if (!r->record.empty()) memcpy(frags, r->record.data(), r->record.size() * sizeof(mck_wal_fragment));
+  return MCK_OK;
+}
+
+extern "C" int mck_wal_tail_unmark_eof(mck_wal_tail* r) {
+  if (!r) return MCK_EINVAL;
+  r->unmark_eof();
+  return MCK_OK;
+}
+
+extern "C" int mck_wal_tail_is_eof(const mck_wal_tail* r) { return r && r->eof ? 1 : 0; }
+
+extern "C" int mck_wal_tail_reports(const mck_wal_tail* r, mck_wal_report* reports, uint64_t cap, uint64_t* n,
+                                    uint64_t* dropped_bytes) {
+  if (!r) return MCK_EINVAL;
+  const uint64_t k = std::min<uint64_t>(cap, r->reports.size());
+  if (reports && k) memcpy(reports, r->reports.data(), k * sizeof(mck_wal_report));
+  if (n) *n = r->reports.size();
+  if (dropped_bytes) *dropped_bytes = r->dropped;
   return MCK_OK;
 }

@@ -42,13 +42,18 @@ def handoff_checksum_batch(pieces: Sequence[Piece], stream=None) -> List[int]:
         by_base.setdefault(id(t), (t, []))[1].append((i, s, n))
     for t, items in by_base.values():
         dev = t.device
-        offs = torch.tensor([s for _, s, _ in items], dtype=torch.int64, device=dev)
-        lens = torch.tensor([n for _, _, n in items], dtype=torch.int32, device=dev)
-        res = torch.empty(len(items), dtype=torch.int32, device=dev)
-        sp = Spans(t, len(items), offs, lens).c()
-        check(lib.mck_handoff_checksum_batch(ctypes.byref(sp), res.data_ptr(), _stream(stream)),
-              "mck_handoff_checksum_batch")
-        for (i, _, _), v in zip(items, res.cpu().tolist()):
+        st = stream if stream is not None else torch.cuda.current_stream(dev)
+        # descriptors, kernel and readback all on `st`: .cpu() inside the
+        # context waits for that stream, not for whatever stream is current
+        with torch.cuda.stream(st):
+            offs = torch.tensor([s for _, s, _ in items], dtype=torch.int64, device=dev)
+            lens = torch.tensor([n for _, _, n in items], dtype=torch.int32, device=dev)
+            res = torch.empty(len(items), dtype=torch.int32, device=dev)
+            sp = Spans(t, len(items), offs, lens).c()
+            check(lib.mck_handoff_checksum_batch(ctypes.byref(sp), res.data_ptr(), _stream(st)),
+                  "mck_handoff_checksum_batch")
+            vals = res.cpu().tolist()
+        for (i, _, _), v in zip(items, vals):
             out[i] = v & 0xFFFFFFFF
     return out  # type: ignore[return-value]
 
@@ -114,8 +119,14 @@ class WritableFileWriter:
 
     # -- reference API --------------------------------------------------------
     def Append(self, data, crc32c_checksum: int = 0, start: int = 0, length: Optional[int] = None):
-        """:44-175.  ``data``: device uint8 tensor (bytes [start, start+length))."""
+        """:44-175.  ``data``: device uint8 tensor (bytes [start, start+length)).
+        The bytes are copied at Append time (the reference copies them into
+        buf_, or writes them out, before Append returns), so the caller may
+        reuse its tensor at once: every deferred checksum is over the bytes
+        as they were appended."""
         n = data.numel() - start if length is None else length
+        if n > 0:
+            data, start = data[start:start + n].clone(), 0  # device-to-device snapshot
         left, src = n, start
         if self.cap - self.size < left:  # :68-82 grow the buffer
             cap = self.cap

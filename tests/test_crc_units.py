@@ -1,0 +1,205 @@
+"""The unit-stream CRC driver (mck_crc_units.hpp) against the oracle.
+
+k_crc_auto sends a workgroup whose share has a mean span above 2.5 KiB to
+the unit stream: 1 KiB units anchored at each span's 16-aligned end, four
+units per wave iteration across span boundaries, spans of more than 24
+units split into 16 KiB pieces joined through an LDS accumulator.  The
+cases below are the shapes that stress it: SST data blocks (4096 + 0..255
+bytes + the type byte, never 16-aligned), uniform non-aligned strides,
+every span length around the unit / piece / split boundaries, long spans
+(many pieces per span, pieces of one span finishing on different waves),
+empty spans inside a long-span batch, non-zero Extend inits, and an
+interleaved + forced-driver run in a child process.  Bit-exact throughout."""
+import os
+import random
+import struct
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from formats import splitmix_bytes, sst_blocks
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _u32(t):
+    return t.cpu().numpy().view(np.uint32).astype(np.uint64).tolist()
+
+
+def _pack(torch, seed, lens, gap=64):
+    rnd = random.Random(seed)
+    offs, pos = [], 0
+    for n in lens:
+        pos += rnd.randrange(0, gap)
+        offs.append(pos)
+        pos += n
+    host = splitmix_bytes(seed, pos + 64)
+    dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda")
+    return host, dev, offs
+
+
+def _spans(torch, S, dev, offs, lens):
+    return S.Spans(dev, len(offs), offsets=torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                   lengths=torch.tensor(lens, dtype=torch.int32, device="cuda"))
+
+
+def test_units_sst_block_shapes(gpu, oracle):
+    """40K spans of 4096 + 0..255 (+1) bytes at every alignment: the 5-unit
+    blocks whose last unit shares a wave iteration with the next block."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(5)
+    lens = [4096 + rnd.randrange(0, 256) + 1 for _ in range(40_000)]
+    host, dev, offs = _pack(torch, 5, lens)
+    sp = _spans(torch, S, dev, offs, lens)
+    got = _u32(S.crc32c_batch(sp))
+    masked = _u32(S.crc32c_batch(sp, mask=True))
+    inits = [rnd.getrandbits(32) for _ in lens]
+    ext = _u32(S.crc32c_batch(sp, init_crcs=torch.tensor(np.array(inits, dtype=np.uint32).view(np.int32),
+                                                          device="cuda")))
+    for i in range(0, len(lens), 7):
+        o, n = offs[i], lens[i]
+        d = host[o:o + n]
+        v = oracle.Value(d)
+        assert got[i] == v, (i, o, n)
+        assert masked[i] == oracle.Mask(v), (i, o, n)
+        assert ext[i] == oracle.Extend(inits[i], d), (i, o, n)
+
+
+@pytest.mark.parametrize("stride", [4300, 4101, 5000, 8193])
+def test_units_uniform_unaligned_stride(gpu, oracle, stride):
+    """Uniform batches whose length is not a 16-byte multiple (implicit
+    offsets i * stride): the unit stream, not the aligned uniform kernel."""
+    import speedb_amd as S
+    torch = gpu
+    count = 30_000
+    host = splitmix_bytes(stride, count * stride + 64)
+    dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda")
+    got = _u32(S.crc32c_batch(S.Spans.uniform(dev, stride, count)))
+    for i in list(range(0, count, 97)) + [count - 1]:
+        assert got[i] == oracle.Value(host[i * stride:(i + 1) * stride]), i
+
+
+def test_units_boundary_lengths(gpu, oracle):
+    """Lengths around the 1 KiB unit, the 4-unit iteration, the 24-unit split
+    threshold and the 16 KiB piece boundaries, at every start alignment,
+    mixed with 3-8 KiB spans so the workgroups choose the unit stream."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(11)
+    special = []
+    for u in (1, 2, 3, 4, 5, 8, 16, 17, 23, 24, 25, 26, 40, 41, 48, 49, 64, 65, 100, 257):
+        for d in (-17, -16, -15, -1, 0, 1, 15, 16, 17):
+            special.append(max(0, 1024 * u + d))
+    lens = special + [rnd.randrange(3000, 8000) for _ in range(3000)]
+    rnd.shuffle(lens)
+    host, dev, offs = _pack(torch, 11, lens)
+    sp = _spans(torch, S, dev, offs, lens)
+    inits = [rnd.getrandbits(32) for _ in lens]
+    got = _u32(S.crc32c_batch(sp))
+    ext = _u32(S.crc32c_batch(sp, init_crcs=torch.tensor(np.array(inits, dtype=np.uint32).view(np.int32),
+                                                          device="cuda")))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        d = host[o:o + n]
+        assert got[i] == oracle.Value(d), (i, o, n)
+        assert ext[i] == oracle.Extend(inits[i], d), (i, o, n)
+
+
+def test_units_long_spans_split(gpu, oracle):
+    """Spans of 25 units to 4 MiB (up to 256 pieces each, pieces of one span
+    on different waves), empty spans and short spans in between."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(23)
+    lens = [25 * 1024 + 3, 65536 + 255, 200_000, 1 << 20, (4 << 20) + 7, 0, 5, 1000, 0]
+    lens += [rnd.randrange(20_000, 300_000) for _ in range(300)]
+    rnd.shuffle(lens)
+    host, dev, offs = _pack(torch, 23, lens)
+    sp = _spans(torch, S, dev, offs, lens)
+    inits = [rnd.getrandbits(32) for _ in lens]
+    got = _u32(S.crc32c_batch(sp))
+    ext = _u32(S.crc32c_batch(sp, init_crcs=torch.tensor(np.array(inits, dtype=np.uint32).view(np.int32),
+                                                          device="cuda")))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        d = host[o:o + n]
+        assert got[i] == oracle.Value(d), (i, o, n)
+        assert ext[i] == oracle.Extend(inits[i], d), (i, o, n)
+
+
+def test_units_many_windows(gpu, oracle):
+    """More spans per workgroup than one LDS descriptor window (960): the
+    share is processed in several windows, and in several launches."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(31)
+    lens = np.array([rnd.randrange(2600, 3400) for _ in range(420_000)], dtype=np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens + 3)[:-1]])
+    total = int(offs[-1] + lens[-1] + 64)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(31)
+    dev = torch.randint(0, 256, (total,), dtype=torch.uint8, device="cuda", generator=g)
+    sp = S.Spans(dev, len(lens), offsets=torch.tensor(offs, dtype=torch.int64, device="cuda"),
+                 lengths=torch.tensor(lens.astype(np.int32), device="cuda"))
+    got = _u32(S.crc32c_batch(sp))
+    for i in list(range(0, len(lens), 1009)) + [len(lens) - 1]:
+        o, n = int(offs[i]), int(lens[i])
+        assert got[i] == oracle.Value(bytes(dev[o:o + n].cpu().numpy())), (i, o, n)
+
+
+@pytest.mark.parametrize("ctype", [1])
+def test_units_sst_verify_mix(gpu, oracle, ctype):
+    """VerifyBlockChecksum over a compaction mix of 4/16/64 KiB blocks with
+    jitter (split 64 KiB blocks: the epilogue runs on whichever wave finishes
+    the last piece), context checksums, then flipped bytes."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(77)
+    sizes = [rnd.choice([4096] * 6 + [16384] * 3 + [65536]) + rnd.randrange(0, 256) for _ in range(2000)]
+    payloads = [splitmix_bytes(5000 + i, n) for i, n in enumerate(sizes)]
+    comps = [rnd.choice([0, 1, 7]) for _ in sizes]
+    base_ctx = 0x5EED1234
+    file_start = 12345
+    img, offs, lens = sst_blocks(oracle, payloads, ctype, comps, base_ctx, file_start)
+    dev = torch.frombuffer(bytearray(img + bytes(64)), dtype=torch.uint8).to("cuda")
+    sp = _spans(torch, S, dev, offs, lens)
+    foff = torch.tensor([file_start + o for o in offs], dtype=torch.int64, device="cuda")
+    ct = torch.tensor(comps, dtype=torch.uint8, device="cuda")
+    tr = _u32(S.sst_trailer_batch(ctype, sp, ct, file_offsets=foff, base_context_checksum=base_ctx))
+    for i, o in enumerate(offs):
+        assert tr[i] == struct.unpack_from("<I", img, o + lens[i] + 1)[0], (i, lens[i])
+    mm, comp, stored, cnt = S.sst_verify_batch(ctype, sp, file_offsets=foff, base_context_checksum=base_ctx)
+    assert int(cnt.item()) == 0 and int(mm.sum().item()) == 0
+    bad = sorted(rnd.sample(range(len(sizes)), 25))
+    cor = bytearray(img)
+    for i in bad:
+        cor[offs[i] + rnd.randrange(0, lens[i] + 5)] ^= 1 << rnd.randrange(8)
+    dev2 = torch.frombuffer(bytearray(bytes(cor) + bytes(64)), dtype=torch.uint8).to("cuda")
+    mm, comp, stored, cnt = S.sst_verify_batch(ctype, _spans(torch, S, dev2, offs, lens), file_offsets=foff,
+                                               base_context_checksum=base_ctx)
+    assert [i for i, v in enumerate(mm.cpu().tolist()) if v] == bad
+    assert int(cnt.item()) == len(bad)
+
+
+@pytest.mark.parametrize("env", [{"MCK_CRC_AUTO": "units"}, {"MCK_CRC_ORDER": "interleaved"}])
+def test_units_forced_and_interleaved_subprocess(gpu, env):
+    """Every generic CRC parity test with the unit stream forced for every
+    workgroup (short spans, 0-byte spans, WAL and blob ops included), and the
+    unit tests above with the interleaved span order."""
+    if any(os.environ.get(k) for k in ("MCK_CRC_AUTO", "MCK_CRC_ROWS", "MCK_CRC_ORDER")):
+        pytest.skip("already running a forced driver")
+    tests = [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
+        "test_crc32c_batch_ragged", "test_sst_trailer_and_verify", "test_empty_and_zero_inputs",
+        "test_large_ragged_batches_static_and_dynamic_feeds", "test_wal_record_crc_batch",
+        "test_crc32c_known_answers_on_device", "test_builtin_checksum_batch", "test_sst_verify_large_static_feed",
+        "test_checksum_schemas_on_device", "test_crc32c_long_vs_oracle")]
+    tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_sst_file.py"),
+              os.path.join(HERE, "test_crc_units.py"),
+              os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
+                        "-k", "not subprocess"] + tests,
+                       env=dict(os.environ, **env), cwd=os.path.dirname(HERE), capture_output=True, text=True,
+                       timeout=900)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]

@@ -153,3 +153,56 @@ def test_handoff_checksum_batch_is_encode_fixed32(gpu, oracle):
     raw = out.cpu().numpy().tobytes()
     for i, (o, n) in enumerate(zip(offs, lens)):
         assert raw[4 * i:4 * i + 4] == oracle.Extend(0, data[o:o + n]).to_bytes(4, "little")
+
+
+def _run_reused_staging(torch, device, oracle, crc_batch, rnd):
+    """Every Append comes from ONE staging tensor that the caller overwrites
+    right after the call (a WAL writer reusing its record buffer): the
+    handoff checksums must cover the bytes as appended, as the reference's
+    copy into buf_ guarantees (writable_file_writer.cc:107-165)."""
+    from speedb_amd.handoff import WritableFileWriter
+    items = _workload(rnd, oracle, n=30)
+    ref = RefWriter(oracle, 1 << 20, True)
+    w = WritableFileWriter(1 << 20, True, True, crc_batch=crc_batch)
+    stage = torch.zeros(max(len(d) for d, _ in items) + 16, dtype=torch.uint8, device=device)
+    for d, c in items:
+        stage[:len(d)].copy_(torch.frombuffer(bytearray(d), dtype=torch.uint8))
+        ref.Append(d, c)
+        w.Append(stage, c, start=0, length=len(d))
+        stage.fill_(0xA5)  # the caller reuses its buffer before the writes are resolved
+    ref.Flush()
+    w.Close()
+    assert w.writes == ref.writes
+
+
+def test_handoff_append_snapshots_bytes_cpu(oracle):
+    torch = pytest.importorskip("torch")
+
+    def crc_batch(pieces):
+        return [oracle.Value(bytes(t[s:s + n].numpy().tobytes())) for t, s, n in pieces]
+    _run_reused_staging(torch, "cpu", oracle, crc_batch, random.Random(41))
+
+
+@pytest.mark.gpu
+def test_handoff_append_snapshots_bytes_gpu(gpu, oracle):
+    _run_reused_staging(gpu, "cuda", oracle, None, random.Random(43))
+
+
+@pytest.mark.gpu
+def test_handoff_checksum_batch_side_stream(gpu, oracle):
+    """The batch issued on a non-default stream: the readback waits for that
+    stream (the kernel is queued behind a long one on it)."""
+    from speedb_amd.handoff import handoff_checksum_batch
+    torch = gpu
+    rnd = random.Random(5)
+    data = bytes(rnd.getrandbits(8) for _ in range(300000))
+    d = torch.frombuffer(bytearray(data + bytes(16)), dtype=torch.uint8).cuda()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())  # d is uploaded
+    big = torch.empty(1 << 28, dtype=torch.uint8, device="cuda")
+    with torch.cuda.stream(side):
+        for _ in range(8):
+            big.fill_(1)  # keeps the side stream busy for a while
+    pieces = [(d, o, 9000) for o in range(0, 290000, 9000)]
+    got = handoff_checksum_batch(pieces, stream=side)
+    assert got == [oracle.Value(data[o:o + 9000]) for _, o, _ in pieces]

@@ -281,3 +281,207 @@ def test_reader_reports_and_modes(oracle):
     bad[1, 2] = 0
     with pytest.raises(Exception):
         S.wal_read_records(img, LOG, kTolerate, bad)
+
+
+@pytest.mark.gpu
+def test_wal_recover_on_side_stream(gpu, oracle):
+    """WalRecover with stream= a busy non-default stream: the upload, the
+    verify kernel, the host walk's readback and the XXH3 batch all order on
+    that stream (the walk never reads verdicts not yet written)."""
+    import speedb_amd as S
+    torch = gpu
+    L = Log(oracle, False)
+    msgs = [big_string(str(i), 9000 + 37 * i) for i in range(40)]
+    for m in msgs:
+        L.write(m)
+    img = bytes(L.w.buf)
+    side = torch.cuda.Stream()
+    big = torch.empty(1 << 28, dtype=torch.uint8, device="cuda")
+    with torch.cuda.stream(side):
+        for _ in range(8):
+            big.fill_(3)  # the side stream is busy when WalRecover queues on it
+    r = S.WalRecover(img, LOG, kTolerate, stream=side)
+    assert r.Records() == msgs and r.dropped_bytes == 0
+    assert [int(x) for x in r.record_checksums] == [oracle.XXH3(m) for m in msgs]
+
+
+# ---------------------------------------------------------------------------
+# FragmentBufferedReader (allow_retry_read = true, db/log_reader.cc:618-931):
+# LogTest's cases that run for the retry reader (the ones log_test.cc skips
+# with `if (allow_retry_read_) return;` are skipped here too), the ClearEof
+# cases (ForceEOF = a shorter visible file, UnmarkEOF after it grew) and
+# RetriableLogTest (:879-988, a record written in two parts).  ClearEofError
+# / ClearEofError2 inject I/O errors into the file layer, which an in-memory
+# image does not have: not restated.
+# ---------------------------------------------------------------------------
+RETRY_SKIPPED = {"TruncatedTrailingRecordIsNotIgnored", "BadLength", "BadLengthAtEndIsIgnored",
+                 "BadLengthAtEndIsNotIgnored", "MissingLastIsNotIgnored", "PartialLastIsNotIgnored"}
+RETRY_PARAMS = [(c, r) for c, r in PARAMS if c[0] not in RETRY_SKIPPED]
+RETRY_IDS = [f"{c[0]}-{'recycle' if r else 'legacy'}" for c, r in RETRY_PARAMS]
+
+
+def _tail_reader(oracle, verify):
+    import speedb_amd as S
+    if verify == "oracle":
+        v = lambda img: wal_expected_blocks(img, LOG, oracle)  # noqa: E731
+    else:
+        v = verify
+    return S.FragmentBufferedReader(LOG, verify=v)
+
+
+def _read_all(r):
+    out = []
+    while True:
+        rec = r.ReadRecord()
+        if rec is None:
+            return out
+        out.append(rec)
+
+
+def _retry_case(oracle, case, recycle, verify):
+    L = Log(oracle, recycle)
+    case[1](L)
+    r = _tail_reader(oracle, verify)
+    r.SetFile(bytes(L.w.buf))
+    recs = _read_all(r)
+    _check(case, L, recs, r.dropped_bytes, r.message)
+
+
+@pytest.mark.parametrize("case,recycle", RETRY_PARAMS, ids=RETRY_IDS)
+def test_fragment_buffered_reader_cases(oracle, case, recycle):
+    _retry_case(oracle, case, recycle, "oracle")
+
+
+def _clear_eof_single(oracle, recycle, verify):  # log_test.cc:649-664
+    L = Log(oracle, recycle)
+    L.write(b"foo")
+    L.write(b"bar")
+    r = _tail_reader(oracle, verify)
+    r.SetFile(bytes(L.w.buf[:3 + L.hs + 2]))  # ForceEOF(3 + header_size + 2)
+    assert r.ReadRecord() == b"foo"
+    r.SetFile(bytes(L.w.buf))
+    r.UnmarkEOF()
+    assert r.ReadRecord() == b"bar"
+    assert r.IsEOF()
+    assert r.ReadRecord() is None
+    L.write(b"xxx")
+    r.SetFile(bytes(L.w.buf))
+    r.UnmarkEOF()
+    assert r.ReadRecord() == b"xxx"
+    assert r.IsEOF()
+
+
+def _clear_eof_multi(oracle, recycle, verify):  # log_test.cc:666-683
+    L = Log(oracle, recycle)
+    blocks = 5
+    n = (K_BLOCK - L.hs) * blocks + 25
+    L.write(big_string("foo", n))
+    L.write(big_string("bar", n))
+    r = _tail_reader(oracle, verify)
+    r.SetFile(bytes(L.w.buf[:n + blocks * L.hs + L.hs + 3]))
+    assert r.ReadRecord() == big_string("foo", n)
+    assert r.IsEOF()
+    r.SetFile(bytes(L.w.buf))
+    r.UnmarkEOF()
+    assert r.ReadRecord() == big_string("bar", n)
+    assert r.IsEOF()
+    L.write(big_string("xxx", n))
+    r.SetFile(bytes(L.w.buf))
+    r.UnmarkEOF()
+    assert r.ReadRecord() == big_string("xxx", n)
+    assert r.IsEOF()
+
+
+def _tail_two_parts(oracle, recycle, verify, delta_of_hs, msg):
+    """RetriableLogTest TailLog_PartialHeader (:879, delta = hs - 1),
+    TailLog_FullHeader (:922, hs + 1), NonBlockingReadFullRecord (:965):
+    the reader polls while the record is written in two parts."""
+    L = Log(oracle, recycle)
+    L.write(msg)
+    img = bytes(L.w.buf)
+    delta = delta_of_hs(L.hs)
+    r = _tail_reader(oracle, verify)
+    r.SetFile(img[:delta])
+    assert r.ReadRecord() is None
+    assert r.IsEOF()  # the FirstEOF sync point was reached
+    r.SetFile(img)
+    assert r.ReadRecord() == msg
+    assert r.dropped_bytes == 0 and r.message == ""
+
+
+def _tail_byte_by_byte(oracle, recycle, verify):
+    """A log written a few bytes at a time, polled after every write: every
+    record comes out once, whole, in order (the secondary-instance loop)."""
+    import random
+    L = Log(oracle, recycle)
+    rnd = random.Random(9)
+    msgs = [big_string(str(i), rnd.choice([0, 1, 5, 100, 3000, 40000])) for i in range(40)]
+    for m in msgs:
+        L.write(m)
+    img = bytes(L.w.buf)
+    r = _tail_reader(oracle, verify)
+    got, pos = [], 0
+    while pos < len(img):
+        pos = min(len(img), pos + rnd.choice([1, 3, 7, 11, 500, 9000, 33000]))
+        r.SetFile(img[:pos])
+        got += _read_all(r)
+    assert got == msgs and r.dropped_bytes == 0
+
+
+TAIL_CASES = {
+    "ClearEofSingleBlock": _clear_eof_single,
+    "ClearEofMultiBlock": _clear_eof_multi,
+    "TailLog_PartialHeader": lambda o, rc, v: _tail_two_parts(o, rc, v, lambda hs: hs - 1, b"foo"),
+    "TailLog_FullHeader": lambda o, rc, v: _tail_two_parts(o, rc, v, lambda hs: hs + 1, b"foo"),
+    "NonBlockingReadFullRecord": lambda o, rc, v: _tail_two_parts(o, rc, v, lambda hs: hs - 1, b"foo-bar"),
+    "ByteByByte": _tail_byte_by_byte,
+}
+
+
+@pytest.mark.parametrize("recycle", [False, True])
+@pytest.mark.parametrize("name", list(TAIL_CASES))
+def test_fragment_buffered_reader_tailing(oracle, name, recycle):
+    TAIL_CASES[name](oracle, recycle, "oracle")
+
+
+def test_timestamp_size_record_offsets(oracle):
+    """A user-defined timestamp size record (type 10) in the middle of a
+    fragmented record: ReadRecord reports it interspersed and the record that
+    then completes has LastRecordOffset = the timestamp record's offset
+    (db/log_reader.cc:189-213); a zero size and a second record for the same
+    column family are reported by UpdateRecordedTimestampSize (:594-616)."""
+    import speedb_amd as S
+    L = Log(oracle, False)
+    L.write(b"head")
+    L.w.emit(kFirstType, b"abc")
+    ts_off = len(L.w.buf)
+    L.w.emit(10, struct.pack("<IH", 1, 8))    # cf 1 -> 8-byte timestamps, inside the record
+    L.w.emit(kLastType, b"def")
+    L.w.emit(10, struct.pack("<IH", 2, 0))    # zero size
+    L.w.emit(10, struct.pack("<IH", 1, 4))    # cf 1 again
+    L.write(b"tail")
+    img = bytes(L.w.buf)
+    ver = np.array(wal_expected_blocks(img, LOG, oracle), dtype=np.int64).astype(np.int32)
+    plan = S.wal_read_records(img, LOG, kTolerate, ver)
+    assert _records(plan, img) == [b"head", b"def", b"tail"]
+    assert int(plan.rec_file_offsets[1]) == ts_off
+    assert [(rep[1], rep[2]) for rep in plan.reports] == [
+        (3, "user-defined timestamp size record interspersed partial record"),
+        (6, "User-defined timestamp size record contains zero timestamp size."),
+        (6, "User-defined timestamp size record contains update to recorded column family.")]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case,recycle", RETRY_PARAMS, ids=RETRY_IDS)
+def test_fragment_buffered_reader_cases_on_device(gpu, oracle, case, recycle):
+    """The same cases with the CRC verdicts from mck_wal_verify_batch."""
+    _retry_case(oracle, case, recycle, "device")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True])
+@pytest.mark.parametrize("name", list(TAIL_CASES))
+def test_fragment_buffered_reader_tailing_on_device(gpu, oracle, name, recycle):
+    """Tailing with the device verdicts: every SetFile re-verifies the
+    blocks that grew (a partly written block verified again)."""
+    TAIL_CASES[name](oracle, recycle, "device")
