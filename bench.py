@@ -49,6 +49,10 @@ Default workload (the headline, BASELINE.json configs[1]): CRC32C over
                        (mck_crc32c_value_r: H2D + launch + D2H) at 64 B,
                        4 KiB, 32 KiB, 1 MiB vs the reference's crc32c::Value
                        on one host thread
+  latency  (8f row 1)  latency of one small VerifyBlockChecksum batch of 1,
+                       8, 32, 256 ~4.2 KiB blocks (RetrieveMultipleBlocks),
+                       device-resident and pinned, vs the reference on one
+                       host thread: the crossover INTEGRATION.md 2.1 cites
 
 One step = one pass of the workload's kernel(s) over the rank's whole batch.
 With N > 1 (torchrun, one process per GPU) every rank checksums its own
@@ -66,7 +70,8 @@ wall time of the K timed steps, in GiB/s; roofline = the dominant kernel's
 algorithmic bytes per launch / its average launch time (HIP events on the
 launch stream) against the 8 TB/s HBM3E peak; cpu_baseline = the reference's
 own crc32c / XXH3 (oracle/_ref, compiled from util/crc32c.cc + util/xxhash.cc)
-on every host CPU (os.cpu_count() threads), rank 0 at N=1 only: the
+on the CPUs this process may use (cgroup quota / affinity; "cores"), rank 0
+at N=1 only: the
 DRAM-resident sample of the GPU's own blocks (value) and db_bench's cache-hot
 ChecksumBenchmark loop (tools/db_bench_tool.cc:4392-4412, one 4 KiB 'x'
 buffer), with the GPU's per-block results cross-checked on a sample.
@@ -96,7 +101,7 @@ def parse():
     # untimed for this long before the warmup steps, whatever W is
     p.add_argument("--settle-ms", type=float, default=250.0)
     p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file", "walwrite", "blob", "shim", "blockkv",
-                            "walrec", "ragged"], default="crc32c")
+                            "walrec", "ragged", "latency"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
     p.add_argument("--sst-bytes", type=int, default=4 << 30,
@@ -122,7 +127,8 @@ def parse():
                    help="pinned 4300-B blocks per GPU (host; configs[4]'s 8-GPU share)")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
                    help="approximate CPU-baseline budget (0 disables)")
-    p.add_argument("--cpu-threads", type=int, default=0, help="0 = os.cpu_count()")
+    p.add_argument("--cpu-threads", type=int, default=0,
+                   help="0 = the CPUs this process may use (cgroup quota / affinity)")
     p.add_argument("--no-verify", action="store_true")
     a = p.parse_args()
     if a.steps is None:
@@ -146,6 +152,20 @@ def _cpu_quota():
         return None if q == "max" else round(int(q) / int(per), 2)
     except (OSError, ValueError):
         return None
+
+
+def usable_cpus():
+    """(CPUs this process may actually use, how that was decided): the
+    cgroup CPU quota (cpu.max) when set, capped by the affinity mask; the
+    hardware thread count (os.cpu_count()) only when neither limits it."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    q = _cpu_quota()
+    if q:
+        return max(1, min(aff, int(q))), f"cgroup CPU quota {q}, affinity {aff} CPUs"
+    return aff, f"affinity {aff} CPUs (no cgroup quota)"
 
 
 def cpu_baseline(args, kind, block, sample, gpu_results):
@@ -180,7 +200,8 @@ def cpu_baseline(args, kind, block, sample, gpu_results):
     idx = np.unique(np.linspace(0, nblocks - 1, num=min(4096, nblocks)).astype(np.int64))
     fn = lib.ref_crc32c_value if kind == "crc32c" else lib.ref_xxh3_64
     agree = all(int(fn(buf.ctypes.data + int(i) * block, block)) == int(gpu_results[i]) for i in idx)
-    threads = args.cpu_threads or os.cpu_count() or 1
+    usable, how = usable_cpus()
+    threads = args.cpu_threads or usable
     k = 0 if kind == "crc32c" else 1
     secs, sink = ctypes.c_double(), ctypes.c_uint32()
     lib.ref_bench(k, 1, threads, block, 0, buf.ctypes.data, nblocks, 1, ctypes.byref(secs),
@@ -202,11 +223,12 @@ def cpu_baseline(args, kind, block, sample, gpu_results):
                   if ln.startswith("model name")), "")
     return {
         "value": round(dram, 2), "unit": "GiB/s", "cores": threads, "kind": "reference",
+        "hw_threads": os.cpu_count(), "cores_basis": how,
         "sample": (f"{kind} via oracle/_ref/{name} (reference util/crc32c.cc + util/xxhash.cc), "
                    f"{passes} pass(es) over the GPU workload's first {nblocks} {block}-B blocks "
                    f"({nblocks * block >> 20} MiB host copy, DRAM-resident), one block per call, "
-                   f"blocks strided over {threads} threads (os.cpu_count()), {dram_secs:.1f} s; "
-                   f"host {model}, cgroup CPU quota {_cpu_quota()}"),
+                   f"blocks strided over {threads} threads = the CPUs this process may use ({how}; "
+                   f"the host has {os.cpu_count()} hardware threads), {dram_secs:.1f} s; host {model}"),
         "db_bench_cache_hot": {
             "value": round(hot, 2), "unit": "GiB/s", "threads": threads,
             "sample": (f"tools/db_bench_tool.cc:4392-4412 ChecksumBenchmark loop: one "
@@ -465,30 +487,13 @@ def make_workload(args, dev, rank, world):
         w.step = step
         w.launches = 1
         w.span_bytes = int(lens.sum())
-        if _lib.lib.mck_wal_write_pieces(nf) == 0:
-            # one-pass writer: k_wal_write_rows in launches of <= ncu * 1528
-            # fragments, timed together as the step; it reads the payload and
-            # the 24 B descriptor once, writes the stream and the 4 B CRC
-            cap = torch.cuda.get_device_properties(dev).multi_processor_count * 1528
-            nl = -(-nf // cap)
-            # the row shape the engine picks (mck_engine.hip wal_row_lanes / wal_chunk)
-            rw = 8 if os.environ.get("MCK_WAL_ROW_LANES") == "8" else 16
-            np_ = 5 if rw == 16 and os.environ.get("MCK_WAL_CHUNK") != "64" else 4
-            blk = "" if rw == 8 or np_ == 4 else (", false" if os.environ.get("MCK_WAL_ORDER") == "interleaved"
-                                                  else ", true")
-            if rw == 16 and np_ == 5 and os.environ.get("MCK_WAL_LAYOUT") != "chunk":
-                kname = f"mck::k_wal_write_il<{blk[2:]}>"
-            else:
-                kname = f"mck::k_wal_write_rows<{rw}, {np_}{blk}>"
-            w.kernel = f"{kname} ({nl} launch(es) per step, timed as the step)"
-            w.alg_bytes = int(lens.sum()) + nbytes + nf * (24 + 4)
-        else:
-            # MCK_WAL_FUSED=0: the CRC and copy kernels overlap (piecewise,
-            # two streams), so the unit timed is the whole step; CRC reads the
-            # payload + 24 B descriptor + 4 B out per fragment, the copy reads
-            # the payload + descriptor + crc and writes the stream
-            w.kernel = "mck::k_crc_auto<mck::OpWalFragCrc, false> + mck::k_wal_copy<false> (overlapped step)"
-            w.alg_bytes = 2 * int(lens.sum()) + nbytes + nf * (24 + 4 + 24 + 4)
+        # the one-pass writer k_wal_write_il in launches of <= ncu * 1528
+        # fragments, timed together as the step; it reads the payload and the
+        # 24 B descriptor once, writes the stream and the 4 B CRC
+        cap = torch.cuda.get_device_properties(dev).multi_processor_count * 1528
+        nl = -(-nf // cap)
+        w.kernel = f"mck::k_wal_write_il ({nl} launch(es) per step, timed as the step)"
+        w.alg_bytes = int(lens.sum()) + nbytes + nf * (24 + 4)
         w.desc = (f"device WAL writer: group commit of {len(lens)} records of 1000-1100 B per GPU "
                   f"(README 1 KB values) -> {nf} physical records, {nbytes} B of log stream "
                   "(log::Writer::AddRecord + EmitPhysicalRecord, SURVEY.md 8f row 3)")
@@ -722,10 +727,122 @@ def shim_latency(args):
                               "including the ctypes call overhead (~0.3 us)"}))
 
 
+def batch_latency(args):
+    """Latency of ONE small VerifyBlockChecksum batch -- the RetrieveMultipleBlocks
+    shape (table/block_based/block_based_table_reader_sync_and_async.h
+    :217-228: at most 32 blocks of a MultiGet, read together and verified one
+    by one) -- against the reference verifying the same blocks on the calling
+    thread.  Blocks: 4096 + 0..255 B payload + 5-byte trailer (kCRC32c,
+    FlushBlockBySizePolicy sizes).  Per batch of n blocks:
+      device_us -- blocks already in HBM: mck_sst_verify_batch + stream sync;
+      pinned_us -- blocks in pinned host memory: H2D of the blocks and their
+                   descriptors, the verify, D2H of the n mismatch flags, sync;
+      cpu_us    -- the reference's crc32c::Value over the n blocks on one
+                   host thread (oracle/_ref, cache-hot: the blocks were just
+                   read), what VerifyBlockChecksum costs per block."""
+    import random
+
+    import numpy as np
+    import torch
+
+    import speedb_amd as S
+    from speedb_amd import _lib
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    st = torch.cuda.current_stream(dev)
+    L = _lib.lib
+    ref = None
+    p = os.path.join(REPO, "oracle", "_ref", "libspdb_ref.so")
+    if os.path.exists(p):
+        ref = ctypes.CDLL(p)
+        ref.ref_bench.restype = ctypes.c_uint64
+        ref.ref_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_uint64,
+                                  ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                  ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_uint32)]
+    rows = []
+    rnd = random.Random(1)
+    for n in (1, 8, 32, 256):
+        lens = [4096 + rnd.randrange(0, 256) for _ in range(n)]
+        offs, pos = [], 0
+        for ln in lens:
+            offs.append(pos)
+            pos += ln + 5
+        img = bytearray(np.random.default_rng(n).integers(0, 256, size=pos + 64, dtype=np.uint8).tobytes())
+        for o, ln in zip(offs, lens):  # seal every block (type 0, kCRC32c, no context)
+            img[o + ln] = 0
+            struct_v = S.crc32c.Mask(S.crc32c.Value(bytes(img[o:o + ln + 1])))
+            img[o + ln + 1:o + ln + 5] = struct_v.to_bytes(4, "little")
+        nb = len(img)
+        desc = np.zeros(n * 3, dtype=np.uint32)  # [offsets as 2 x u32][lengths]
+        desc[:2 * n] = np.array(offs, dtype=np.uint64).view(np.uint32)
+        desc[2 * n:] = lens
+        h_img = torch.frombuffer(img, dtype=torch.uint8).pin_memory()
+        h_desc = torch.from_numpy(desc.view(np.uint8)).pin_memory()
+        d_img = torch.empty(nb, dtype=torch.uint8, device=dev)
+        d_desc = torch.empty(h_desc.numel(), dtype=torch.uint8, device=dev)
+        d_mm = torch.empty(n, dtype=torch.uint8, device=dev)
+        h_mm = torch.empty(n, dtype=torch.uint8).pin_memory()
+        d_img.copy_(h_img)
+        d_desc.copy_(h_desc)
+        torch.cuda.synchronize()
+        sp = _lib.mck_spans(d_img.data_ptr(), d_desc.data_ptr(), d_desc.data_ptr() + 8 * n, 0, 0, n)
+        sst = st.cuda_stream
+
+        def verify():
+            _lib.check(L.mck_sst_verify_batch(1, ctypes.byref(sp), None, 0, d_mm.data_ptr(), None, None, None, sst),
+                       "mck_sst_verify_batch")
+
+        def timed(fn, reps):
+            for _ in range(50):
+                fn()
+            st.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            return (time.perf_counter() - t0) / reps * 1e6
+
+        def dev_call():
+            verify()
+            st.synchronize()
+
+        def pinned_call():
+            d_img.copy_(h_img, non_blocking=True)
+            d_desc.copy_(h_desc, non_blocking=True)
+            verify()
+            h_mm.copy_(d_mm, non_blocking=True)
+            st.synchronize()
+
+        dev_us = timed(dev_call, 2000)
+        pin_us = timed(pinned_call, 2000)
+        assert int(h_mm.sum()) == 0
+        row = {"blocks": n, "bytes": sum(lens), "device_us": round(dev_us, 2), "pinned_us": round(pin_us, 2)}
+        if ref is not None:
+            # the reference on one thread over the same n blocks (uniform
+            # 4224-B blocks: the mean of these sizes), cache-hot
+            blk = 4224
+            buf = np.frombuffer(bytes(img[:max(nb, n * blk)]) + bytes(max(0, n * blk - nb)), dtype=np.uint8)
+            secs, sink = ctypes.c_double(), ctypes.c_uint32()
+            passes = max(1, 200000 // n)
+            tot = ref.ref_bench(0, 1, 1, blk, 0, buf.ctypes.data, n, passes, ctypes.byref(secs), ctypes.byref(sink))
+            row["cpu_us"] = round(secs.value / passes * 1e6, 3)
+            row["cpu_GiBps"] = round(tot / secs.value / 2**30, 2)
+        rows.append(row)
+    cross_dev = next((r["blocks"] for r in rows if "cpu_us" in r and r["device_us"] < r["cpu_us"]), None)
+    cross_pin = next((r["blocks"] for r in rows if "cpu_us" in r and r["pinned_us"] < r["cpu_us"]), None)
+    print(json.dumps({"metric": "latency of one small VerifyBlockChecksum batch (RetrieveMultipleBlocks shape)",
+                      "unit": "us per batch", "rows": rows,
+                      "crossover_blocks_device_resident": cross_dev, "crossover_blocks_pinned": cross_pin,
+                      "note": "device_us/pinned_us include the launch and a stream synchronize; cpu_us = "
+                              "crc32c::Value of oracle/_ref over the same number of ~4.2 KiB blocks on one "
+                              "host thread"}))
+
+
 def main():
     args = parse()
     if args.workload == "shim":
         return shim_latency(args)
+    if args.workload == "latency":
+        return batch_latency(args)
     import torch
     import torch.distributed as dist
 

@@ -230,22 +230,11 @@ int mck_wal_plan(const uint64_t* host_src_offsets, const uint32_t* host_lengths,
  * [masked CRC LE32][length LE16][type][log number LE32 if recyclable],
  * payload.  frags: device array [nfrags]; crc_scratch: device u32 [nfrags]
  * (the masked fragment CRCs); out must be 16-byte aligned (any hipMalloc
- * allocation is).  Large batches run in pieces whose copies overlap the next
- * piece's CRCs on an engine-owned side stream (per host thread and device),
- * joined back into `stream` before the call returns: work queued on
- * `stream` afterwards sees the whole log stream written. */
+ * allocation is).  One kernel computes every fragment's CRC and writes the
+ * stream from the same registers (the payload is read once). */
 int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags,
                         uint32_t nfrags, uint32_t log_number,
                         uint32_t* crc_scratch, void* out, mck_stream_t stream);
-/* The number of overlapped pieces mck_wal_write_batch uses for `nfrags`
- * fragments on the current device (1 = one CRC launch then one copy on the
- * caller's stream), or a negative MCK_E* code.  Pieces hold >= 16 fragments
- * per CU; at most MCK_WAL_PIECES (env, default 8). */
-int mck_wal_write_pieces(uint32_t nfrags);
-/* The side streams come from a per-device pool (one side per concurrently
- * running call, created on first need: a stream + 17 events); this destroys
- * the idle ones. */
-void mck_wal_side_release(void);
 
 /* ---- WAL recovery: logical records ----------------- */
 

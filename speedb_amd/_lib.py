@@ -112,8 +112,6 @@ SIGNATURES = [
      [vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp, ctypes.c_uint64, vp, vp, vp]),
     ("mck_wal_write_batch", ctypes.c_int,
      [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]),
-    ("mck_wal_write_pieces", ctypes.c_int, [ctypes.c_uint32]),
-    ("mck_wal_side_release", None, []),
     ("mck_wal_list_records", ctypes.c_int,
      [vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint64, vp, vp, vp, ctypes.c_uint64, vp, vp]),
     ("mck_wal_gather_batch", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp]),

@@ -23,7 +23,6 @@
 namespace mck {
 
 __device__ CrcTables g_crc_tables;
-__device__ uint8_t g_wal_sink[kWalSinkBytes];
 
 namespace {
 
@@ -51,7 +50,7 @@ struct DevCtx {
   std::once_flag once;
   int status = MCK_ENODEV;
   int ncu = 0;
-  uint32_t* d_stats = nullptr;  // device counters: [0] block checksum mismatches
+  unsigned long long* d_stats = nullptr;  // device counters: [0] block checksum mismatches, [1] read-out slot
 };
 DevCtx g_dev[kMaxDev];
 
@@ -138,7 +137,7 @@ void stat_batch(uint64_t spans, uint64_t known_bytes) {
 // bytes of a batch when the host knows them (uniform lengths)
 uint64_t known_bytes(const mck_spans* s) { return s->lengths ? 0 : (uint64_t)s->length * s->count; }
 
-uint32_t* dev_stats(int dev) { return g_dev[dev].d_stats; }
+unsigned long long* dev_stats(int dev) { return g_dev[dev].d_stats; }
 
 int check_spans(const mck_spans* s) {
   if (!s) {
@@ -176,10 +175,6 @@ bool crc_tlayout() {
 template <class Op>
 struct CrcRowT {
   static constexpr bool value = MCK_CRC_GENERIC_T;
-};
-template <>
-struct CrcRowT<OpWalFragCrc> {
-  static constexpr bool value = false;
 };
 
 // Ragged batches run on k_crc_auto, which picks the driver per workgroup
@@ -776,152 +771,15 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, 
 }
 
 // ---- device WAL writer -------------------------------------------------------
-// The writer is two dependent kernels: the fragment CRCs (k_crc, one
-// 16-wave workgroup per CU holding the 160 KiB LDS tables, latency-bound on
-// ~1 KiB spans) and the header + payload copy (k_wal_copy, no LDS).  The
-// fragment list is cut into pieces; the copy of piece k runs on a side
-// stream while the CRC of piece k+1 runs on the caller's stream, so the copy
-// waves fill the wave slots the CRC workgroup leaves free on every CU.
-// MCK_WAL_PIECES=n (A/B switch, default 8; 1 = one CRC launch then one copy
-// on the caller's stream).
-static uint32_t wal_pieces() {
-  static const uint32_t n = [] {
-    const char* e = getenv("MCK_WAL_PIECES");
-    const int v = e ? atoi(e) : 8;
-    return (uint32_t)(v < 1 ? 1 : v > 16 ? 16 : v);
-  }();
-  return n;
-}
-
-// Side stream and fork/join events of one mck_wal_write_batch call.  Taken
-// from a per-device pool for the duration of the call (so no other thread
-// re-records its events between record and wait) and returned afterwards:
-// the waits already enqueued keep the state of the events at enqueue time,
-// and a later call's work on the side stream queues behind this one's.  The
-// pool holds as many sides as calls ever ran concurrently on the device;
-// mck_wal_side_release() destroys them.
-struct WalSide {
-  hipStream_t st = nullptr;
-  hipEvent_t ev[17] = {};
-};
-struct WalSidePool {
-  std::mutex mu;
-  std::vector<WalSide*> free_list;
-  std::vector<WalSide*> all;
-};
-static WalSidePool g_wal_side[kMaxDev];
-
-static void wal_side_destroy(WalSide* w) {
-  if (w->st) (void)hipStreamDestroy(w->st);
-  for (hipEvent_t& e : w->ev)
-    if (e) (void)hipEventDestroy(e);
-  delete w;
-}
-
-static int wal_side_acquire(int dev, WalSide** out) {
-  WalSidePool& P = g_wal_side[dev];
-  {
-    std::lock_guard<std::mutex> lock(P.mu);
-    if (!P.free_list.empty()) {
-      *out = P.free_list.back();
-      P.free_list.pop_back();
-      return MCK_OK;
-    }
-  }
-  WalSide* w = new WalSide;
-  hipError_t e = hipStreamCreateWithFlags(&w->st, hipStreamNonBlocking);
-  for (hipEvent_t& ev : w->ev)
-    if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-  if (e != hipSuccess) {
-    set_err("WAL writer side stream/events: %s", hipGetErrorString(e));
-    wal_side_destroy(w);
-    return MCK_EHIP;
-  }
-  std::lock_guard<std::mutex> lock(P.mu);
-  P.all.push_back(w);
-  *out = w;
-  return MCK_OK;
-}
-
-static void wal_side_return(int dev, WalSide* w) {
-  WalSidePool& P = g_wal_side[dev];
-  std::lock_guard<std::mutex> lock(P.mu);
-  P.free_list.push_back(w);
-}
-
-static int launch_wal_copy(const uint8_t* src, const WalFrag* f, uint32_t n, uint32_t log_number, const uint32_t* crcs,
-                    uint8_t* out, int ncu, hipStream_t st) {
-  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (n + 3) / 4);
-  hipLaunchKernelGGL(k_wal_copy<false>, dim3(grid), dim3(256), 0, st, src, f, n, log_number, crcs, out);
-  MCK_HIP(hipGetLastError());
-  return MCK_OK;
-}
-
-// One-pass writer (k_wal_write_rows) unless MCK_WAL_FUSED=0 (A/B: the CRC
-// kernel + k_wal_copy in overlapped pieces).
-static bool wal_fused() {
-  static const bool v = [] {
-    const char* e = getenv("MCK_WAL_FUSED");
-    return !e || strcmp(e, "0") != 0;
-  }();
-  return v;
-}
-
-// Row width of the one-pass writer: MCK_WAL_ROW_LANES=8 or 16 (default).
-static int wal_row_lanes() {
-  static const int v = [] {
-    const char* e = getenv("MCK_WAL_ROW_LANES");
-    return e && atoi(e) == 8 ? 8 : 16;
-  }();
-  return v;
-}
-
-// Lane chunk of the 16-lane one-pass writer: MCK_WAL_CHUNK=64 or 80 (default:
-// 1280-byte rounds, one per ~1 KB fragment).
-static int wal_chunk() {
-  static const int v = [] {
-    const char* e = getenv("MCK_WAL_CHUNK");
-    return e && atoi(e) == 64 ? 64 : 80;
-  }();
-  return v;
-}
-
-// Lane layout of the 80-byte-chunk writer: interleaved pieces (default,
-// k_wal_write_il: the copy reuses the CRC's registers) or, with
-// MCK_WAL_LAYOUT=chunk, lane-owned 80-byte chunks (k_wal_write_rows<16, 5>,
-// which re-reads each round's bytes for the copy).
-static bool wal_piece_layout() {
-  static const bool v = [] {
-    const char* e = getenv("MCK_WAL_LAYOUT");
-    return !e || strcmp(e, "chunk") != 0;
-  }();
-  return v;
-}
-
-// Fragment order of the one-pass writer: contiguous ranges per workgroup
-// (default) or MCK_WAL_ORDER=interleaved (fragment i on workgroup i mod G;
-// with 80-byte chunks only).
-static bool wal_interleaved() {
-  static const bool v = [] {
-    const char* e = getenv("MCK_WAL_ORDER");
-    return e && strcmp(e, "interleaved") == 0;
-  }();
-  return v;
-}
-
-// pieces of at least 16 fragments per CU (one CRC grid's worth of spans)
-static uint32_t wal_pieces_for(uint32_t nfrags, int ncu) {
-  uint32_t pieces = wal_pieces();
-  while (pieces > 1 && nfrags / pieces < 16u * (uint32_t)ncu) pieces--;
-  return pieces;
-}
-
-int mck_wal_write_pieces(uint32_t nfrags) {
-  int ncu;
-  if (int rc = current_device(nullptr, &ncu)) return rc;
-  return wal_fused() ? 0 : (int)wal_pieces_for(nfrags, ncu);
-}
-
+// ONE kernel, k_wal_write_il (mck_kernels.hpp): the row
+// driver's loop (16-lane rows, 80-byte lane chunks of interleaved 16-byte
+// pieces, one ~1 KB fragment per 1280-byte round) CRCs every fragment and,
+// from the same registers, writes the log stream; contiguous fragment ranges
+// per workgroup.  Launches hold at most ncu * kRowDescCache fragments (its
+// LDS descriptor / dst_off tables).  (Round 2 measured the alternatives --
+// two kernels overlapped in pieces on a side stream, 8-lane rows, 64-byte
+// chunks, re-reading copies, interleaved order -- and kept this one; they
+// were removed from the library in round 3.)
 int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t nfrags, uint32_t log_number,
                         uint32_t* crc_scratch, void* out, mck_stream_t stream) {
   t_err[0] = 0;
@@ -937,108 +795,21 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   }
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const WalFrag* f = reinterpret_cast<const WalFrag*>(frags);
-  const uint8_t* s8 = static_cast<const uint8_t*>(src);
-  uint8_t* o8 = static_cast<uint8_t*>(out);
-  const WalTypeCrcs tc = wal_type_crcs(log_number);
+  const OpWalWrite op{static_cast<const uint8_t*>(src), f, wal_type_crcs(log_number), log_number, crc_scratch,
+                      static_cast<uint8_t*>(out)};
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
-  if (wal_fused()) {
-    // one pass: CRC + log stream in k_wal_write_rows, in launches of at most
-    // ncu * kRowDescCache fragments (its LDS descriptor / dst_off tables)
-    const bool w8 = wal_row_lanes() == 8, q80 = !w8 && wal_chunk() == 80, ilv = wal_interleaved();
-    const bool pl = q80 && wal_piece_layout();
-    if (int rc = w8    ? ensure_lds(k_wal_write_rows<8>, dev)
-                 : pl  ? (ilv ? ensure_lds(k_wal_write_il<false>, dev) : ensure_lds(k_wal_write_il<true>, dev))
-                 : ilv ? ensure_lds(k_wal_write_rows<16, 5, false>, dev)
-                 : q80 ? ensure_lds(k_wal_write_rows<16, 5>, dev)
-                       : ensure_lds(k_wal_write_rows<16>, dev))
-      return rc;
-    const uint32_t cap = (uint32_t)ncu * kRowDescCache;
-    const uint32_t nl = (nfrags + cap - 1) / cap;
-    const uint32_t per = (uint32_t)(((uint64_t)nfrags + nl - 1) / nl);
-    const OpWalWrite op{s8, f, tc, log_number, crc_scratch, o8};
-    for (uint32_t first = 0; first < nfrags; first += per) {
-      const uint32_t n = std::min(per, nfrags - first);
-      const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
-      if (w8)
-        hipLaunchKernelGGL(k_wal_write_rows<8>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
-      else if (pl && ilv)
-        hipLaunchKernelGGL(k_wal_write_il<false>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
-      else if (pl)
-        hipLaunchKernelGGL(k_wal_write_il<true>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
-      else if (ilv)
-        hipLaunchKernelGGL((k_wal_write_rows<16, 5, false>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
-      else if (q80)
-        hipLaunchKernelGGL((k_wal_write_rows<16, 5>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
-      else
-        hipLaunchKernelGGL(k_wal_write_rows<16>, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
-      MCK_HIP(hipGetLastError());
-    }
-    return MCK_OK;
+  if (int rc = ensure_lds(k_wal_write_il, dev)) return rc;
+  const uint32_t cap = (uint32_t)ncu * kRowDescCache;
+  const uint32_t nl = (nfrags + cap - 1) / cap;
+  const uint32_t per = (uint32_t)(((uint64_t)nfrags + nl - 1) / nl);
+  for (uint32_t first = 0; first < nfrags; first += per) {
+    const uint32_t n = std::min(per, nfrags - first);
+    const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
+    hipLaunchKernelGGL(k_wal_write_il, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
+    MCK_HIP(hipGetLastError());
   }
-  const uint32_t pieces = wal_pieces_for(nfrags, ncu);
-  if (pieces == 1) {
-    if (int rc = launch_crc(OpWalFragCrc{s8, f, tc, crc_scratch}, nfrags, st)) return rc;
-    return launch_wal_copy(s8, f, nfrags, log_number, crc_scratch, o8, ncu, st);
-  }
-  WalSide* w;
-  if (int rc = wal_side_acquire(dev, &w)) return rc;
-  // fork: the side stream starts after the caller's prior work (inputs ready)
-  int rc = MCK_OK;
-  hipError_t e = hipEventRecord(w->ev[16], st);
-  if (e == hipSuccess) e = hipStreamWaitEvent(w->st, w->ev[16], 0);
-  if (e != hipSuccess) {
-    set_err("WAL writer fork: %s", hipGetErrorString(e));
-    wal_side_return(dev, w);
-    return MCK_EHIP;
-  }
-  for (uint32_t k = 0; k < pieces && !rc; k++) {
-    const uint32_t lo = (uint32_t)((uint64_t)nfrags * k / pieces);
-    const uint32_t hi = (uint32_t)((uint64_t)nfrags * (k + 1) / pieces);
-    rc = launch_crc(OpWalFragCrc{s8, f + lo, tc, crc_scratch + lo}, hi - lo, st);
-    if (rc) break;
-    e = hipEventRecord(w->ev[k], st);
-    if (e == hipSuccess) e = hipStreamWaitEvent(w->st, w->ev[k], 0);
-    if (e != hipSuccess) {
-      set_err("WAL writer piece %u: %s", k, hipGetErrorString(e));
-      rc = MCK_EHIP;
-      break;
-    }
-    rc = launch_wal_copy(s8, f + lo, hi - lo, log_number, crc_scratch + lo, o8, ncu, w->st);
-  }
-  // join, also after a failure partway: the caller's stream continues only
-  // after every copy already queued on the side stream
-  e = hipEventRecord(w->ev[16], w->st);
-  if (e == hipSuccess) e = hipStreamWaitEvent(st, w->ev[16], 0);
-  if (e != hipSuccess) {
-    // the join could not be queued: wait for the side stream here instead
-    (void)hipStreamSynchronize(w->st);
-    if (!rc) {
-      set_err("WAL writer join: %s", hipGetErrorString(e));
-      rc = MCK_EHIP;
-    }
-  }
-  wal_side_return(dev, w);
-  return rc;
-}
-
-void mck_wal_side_release(void) {
-  int prev = 0;
-  (void)hipGetDevice(&prev);
-  for (int d = 0; d < kMaxDev; d++) {
-    WalSidePool& P = g_wal_side[d];
-    std::lock_guard<std::mutex> lock(P.mu);
-    if (P.all.empty()) continue;
-    if (hipSetDevice(d) != hipSuccess) continue;
-    // only sides no call is using; each is idle once its stream drains
-    for (WalSide* w : P.free_list) {
-      (void)hipStreamSynchronize(w->st);
-      P.all.erase(std::find(P.all.begin(), P.all.end(), w));
-      wal_side_destroy(w);
-    }
-    P.free_list.clear();
-  }
-  (void)hipSetDevice(prev);
+  return MCK_OK;
 }
 
 int mck_wal_gather_batch(const void* wal, const mck_wal_fragment* frags, uint32_t nfrags, void* out,
@@ -1056,9 +827,9 @@ int mck_wal_gather_batch(const void* wal, const mck_wal_fragment* frags, uint32_
   int ncu;
   if (int rc = current_device(nullptr, &ncu)) return rc;
   const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (nfrags + 3) / 4);
-  hipLaunchKernelGGL(k_wal_copy<true>, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                     static_cast<const uint8_t*>(wal), reinterpret_cast<const WalFrag*>(frags), nfrags, 0u,
-                     static_cast<const uint32_t*>(nullptr), static_cast<uint8_t*>(out));
+  hipLaunchKernelGGL(k_wal_gather, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                     static_cast<const uint8_t*>(wal), reinterpret_cast<const WalFrag*>(frags), nfrags,
+                     static_cast<uint8_t*>(out));
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }
@@ -1681,14 +1452,19 @@ int mck_statistics_get(mck_statistics* out, int reset) {
   int rc = MCK_OK;
   for (int d = 0; d < kMaxDev; d++) {
     if (!g_dev[d].d_stats) continue;
-    uint32_t c[1] = {0};
-    if (hipSetDevice(d) != hipSuccess || hipMemcpy(c, g_dev[d].d_stats, 4, hipMemcpyDeviceToHost) != hipSuccess ||
-        (reset && hipMemset(g_dev[d].d_stats, 0, 4) != hipSuccess)) {
+    unsigned long long c = 0;
+    bool ok = hipSetDevice(d) == hipSuccess;
+    if (ok) {
+      hipLaunchKernelGGL(k_stats_take, dim3(1), dim3(64), 0, 0, g_dev[d].d_stats, g_dev[d].d_stats + 1, reset);
+      ok = hipGetLastError() == hipSuccess &&
+           hipMemcpy(&c, g_dev[d].d_stats + 1, sizeof c, hipMemcpyDeviceToHost) == hipSuccess;
+    }
+    if (!ok) {
       set_err("reading the device counters of device %d failed", d);
       rc = MCK_EHIP;
       continue;
     }
-    out->block_checksum_mismatch_count += c[0];
+    out->block_checksum_mismatch_count += c;
   }
   (void)hipSetDevice(prev);
   return rc;

@@ -13,17 +13,6 @@
 namespace mck {
 
 extern __device__ CrcTables g_crc_tables;
-// scratch that the one-pass WAL writer's idle lanes store to (never read)
-// MCK_WAL_SINK: how the one-pass writer's stores with nothing to write are
-// handled -- 0: exec-masked (not issued for those lanes), 1: redirected to a
-// per-lane slot shared by every wave, 2: redirected to per-wave slots.
-#ifndef MCK_WAL_SINK
-#define MCK_WAL_SINK 0
-#endif
-constexpr uint32_t kWalSinkWaves = MCK_WAL_SINK == 2 ? 4096 : 1;
-constexpr uint32_t kWalSinkBytes = kWalSinkWaves * 64 * 16 + 64;
-extern __device__ uint8_t g_wal_sink[kWalSinkBytes];
-
 constexpr uint32_t kRandomPrime = 0x6b9083d9u;  // table/format.cc:573
 
 // ---- span source: the mck_spans descriptor --------------------------------
@@ -86,7 +75,7 @@ struct BlockArgs {
   uint8_t* mismatch;       // verify
   uint32_t* stored;        // verify (opt)
   uint32_t* mismatch_count;  // verify (opt)
-  uint32_t* stats_mismatch = nullptr;  // verify: the engine's per-device BLOCK_CHECKSUM_MISMATCH_COUNT
+  unsigned long long* stats_mismatch = nullptr;  // verify: the engine's per-device BLOCK_CHECKSUM_MISMATCH_COUNT (64-bit)
 };
 
 // Epilogue inputs of a block op, loaded by the driver together with the
@@ -137,7 +126,7 @@ __device__ __forceinline__ void block_epilogue(const BlockArgs& a, uint32_t i, u
     if (a.out) a.out[i] = v;
     if (a.stored) a.stored[i] = stored;
     if (bad && a.mismatch_count) atomicAdd(a.mismatch_count, 1u);
-    if (bad && a.stats_mismatch) atomicAdd(a.stats_mismatch, 1u);
+    if (bad && a.stats_mismatch) atomicAdd(a.stats_mismatch, 1ull);
   }
 }
 // Same, with the inputs loaded here (drivers without epilogue prefetch).
@@ -492,32 +481,13 @@ struct OpNoneBlock {
 };
 
 // ===================== device WAL writer ==================================
-// Fragment CRCs: span = the fragment's payload in the source, init =
-// Value(type [+ LE32 log number]) (db/log_writer.cc:48-51, 281-298).
+// A planned physical record (mck_wal_plan): the fragment's payload in the
+// source, its header's offset in the output, the trailer padding before it.
 struct WalFrag {  // = mck_wal_fragment
   uint64_t src_off, dst_off;
   uint32_t length;
   uint8_t type, pad;
   uint16_t reserved;
-};
-struct OpWalFragCrc {
-  const uint8_t* src;
-  const WalFrag* frags;
-  WalTypeCrcs tc;
-  uint32_t* out;
-  typedef NoPre Pre;
-  __device__ const uint8_t* base() const { return src; }
-  __device__ uint64_t off(uint32_t i) const { return frags[i].src_off; }
-  __device__ uint64_t len(uint32_t i) const { return frags[i].length; }
-  __device__ uint32_t init_crc(uint32_t i) const { return tc.v[frags[i].type & 15]; }
-  static constexpr bool kTypedInit = true;
-  __device__ int init_kind() const { return kInitTyped; }
-  __device__ uint32_t init_key(uint32_t i) const { return ldg_u8(&frags[i].type, 0); }
-  __device__ uint32_t typed_init(uint32_t t) const { return tc.v[t & 15]; }
-  __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
-  __device__ void finish(uint32_t i, uint32_t crc, const Pre&, bool writer) const {
-    if (writer) out[i] = crc_mask(crc);
-  }
 };
 
 // ===================== one-pass WAL writer ==================================
@@ -575,208 +545,13 @@ typedef __attribute__((address_space(1))) uint32_t gbl_st_u32_t;
 typedef __attribute__((address_space(1))) span_u32x4 gbl_st_u32x4_t;
 __device__ __forceinline__ void st_u8(uint64_t a, uint32_t v) { *reinterpret_cast<gbl_st_u8_t*>(a) = (uint8_t)v; }
 __device__ __forceinline__ void st_u32(uint64_t a, uint32_t v) { *reinterpret_cast<gbl_st_u32_t*>(a) = v; }
-// MCK_WAL_NT=1: non-temporal piece stores (walwrite 1.527 ms vs 1.480 with
-// plain stores, which stay the default).
-#ifndef MCK_WAL_NT
-#define MCK_WAL_NT 0
-#endif
-__device__ __forceinline__ void st_nt16(uint64_t a, uint4 o) {
-  span_u32x4 q = {o.x, o.y, o.z, o.w};
-  if (MCK_WAL_NT)
-    __builtin_nontemporal_store(q, reinterpret_cast<gbl_st_u32x4_t*>(a));
-  else
-    *reinterpret_cast<gbl_st_u32x4_t*>(a) = q;
+// 16 bytes at an aligned output address (plain stores: non-temporal ones
+// measured slower for the WAL writer, 1.527 vs 1.480 ms per step)
+__device__ __forceinline__ void st16(uint64_t a, uint4 o) {
+  *reinterpret_cast<gbl_st_u32x4_t*>(a) = span_u32x4{o.x, o.y, o.z, o.w};
 }
 
-// MCK_WAL_EXP (timing experiments only, wrong output): 1 drops the piece
-// copies, 2 the head/tail bytes, 4 the header bytes, 8 the piece stores
-// (loads kept), 16 the piece loads (stores of zeros kept), 32 the head/tail
-// byte loads (k_wal_write_il: stores of zeros kept).
-#ifndef MCK_WAL_EXP
-#define MCK_WAL_EXP 0
-#endif
-#if MCK_WAL_SINK
-#define WAL_ST(ok, fn, a, snk, v) fn((ok) ? (a) : (snk), v)
-#else
-#define WAL_ST(ok, fn, a, snk, v) \
-  do {                            \
-    if (ok) fn(a, v);             \
-  } while (0)
-#endif
-
-// W = 8 or 16 lanes per row; NP = 4 pieces (64-byte lane chunks) or, with
-// W = 16, NP = 5: 80-byte chunks, 1280-byte rounds, so a fragment of up to ~1250
-// bytes (the ~1 KB records of the WAL) takes one round instead of two.  The
-// NP = 5 rows use their own lane-final and gap maps (CrcTables::lane_final80
-// / gap80), loaded over LDS tables these rows never read: lane-final columns
-// 0-15 (16-lane rows read columns 48-63) and the W = 4 gap map.
-template <int W, int NP = 4, bool BLK = true>
-__device__ __forceinline__ void wal_write_rows(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
-                                               const CrcTables* __restrict__ g) {
-  static_assert(W == 8 || W == 16, "row width");
-  static_assert(NP == 4 || (NP == 5 && W == 16), "chunk pieces");
-  constexpr uint64_t Q = 16u * NP;  // lane chunk bytes
-  constexpr int kHT = 16 / W;  // head / tail payload bytes per lane (< 16 each)
-  constexpr int kHdr = 32 / W;  // padding + header bytes per lane (pad + hs <= 21)
-  crc_rows_prologue<BLK>(op, first, count, lds, g, false);
-  const RowShare sh = row_share<BLK>(first, count);
-  // fragments' dst_off, staged like the descriptors (row_desc_stage order)
-  for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) *lds_p64(kLdsWalAux + 8 * t) = op.frags[sh.idx(t)].dst_off;
-  if (NP == 5) {  // 80-byte-chunk maps: [n][v] rows of 16 lane-final columns, then the gap map
-    const uint32_t t = threadIdx.x;
-    if (t < 512) {
-      const uint4 x = reinterpret_cast<const uint4*>(&g->lane_final80[0][0][0])[t];
-      *reinterpret_cast<uint4*>(lds + kLdsFinal + 256 * (t >> 2) + 16 * (t & 3)) = x;
-    } else if (t < 544) {
-      const uint4 x = reinterpret_cast<const uint4*>(&g->gap80[0][0])[t - 512];
-      *reinterpret_cast<uint4*>(lds + row_gap_off<W, NP>() + 16 * (t - 512)) = x;
-    }
-  }
-  __syncthreads();
-  const CrcLane L = crc_lane();
-  const uint32_t c = threadIdx.x & (W - 1);
-  const uint32_t lf4 = (NP == 5 ? c : 64u - W + c) << 2;  // lane-final table column
-  const uint32_t share = sh.n;
-  const uint64_t base = reinterpret_cast<uint64_t>(op.src);
-  const uint64_t obase = reinterpret_cast<uint64_t>(op.out);
-  // per-lane sink slots (16 B each), never read
-  const uint32_t wslot = MCK_WAL_SINK == 2 ? (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) % kWalSinkWaves : 0;
-  const uint64_t sink = reinterpret_cast<uint64_t>(&g_wal_sink[0]) + 1024ull * wslot + 16ull * (threadIdx.x & 63);
-  (void)sink;
-  const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
-  uint32_t t = row_ticket<W>(true);
-  bool live = t < share;
-  uint4 d = row_desc(t, share);
-  uint64_t dst = *lds_p64(kLdsWalAux + 8 * (t < share ? t : 0));
-  uint32_t i = sh.idx(live ? t : 0);
-  RowSpan sp = row_span<W, NP>(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kInitTyped);
-  uint32_t key = d.w;
-  int r = sp.rounds - 1;
-  ChunkN<NP> cur = row_load_chunk<W, NP>(sp, r, c, zp);
-  uint32_t nt = row_ticket<W>(true);
-  uint4 nd = row_desc(nt, share);
-  uint64_t ndst = *lds_p64(kLdsWalAux + 8 * (nt < share ? nt : 0));
-  uint32_t s = 0;
-  for (;;) {
-    const bool last = r == 0;
-    const bool fin = live && last;
-
-    // ---- the output of this (span, round), before the next round's
-    // prefetch is issued: waiting for these loads (L1/L2 hits: the CRC loads
-    // of the same bytes came in one iteration ago) then waits for them alone,
-    // and their registers are dead before the prefetch and the CRC round ----
-    const uint32_t type = key & 0xFF, pad = (key >> 8) & 0xFF;
-    const uint32_t hs = ((type >= 5 && type <= 8) || type == 11) ? 11u : 7u;
-    const uint64_t P = obase + dst + hs;             // payload in the output
-    const uint64_t ps = sp.ptr, pe = sp.ptr + sp.n;  // payload in the source
-    const uint64_t delta = P - ps;                   // (mod 2^64)
-    const uint32_t e = (uint32_t)(0ull - delta) & 15u;
-    const uint32_t be = e & 3u;
-    const uint64_t S = sp.a1 - Q * W * (uint32_t)(r + 1);  // the row's source window
-    uint4 v[NP];
-    uint32_t w5[NP];
-    bool ok[NP];
-    // lane c's pieces: the window's output-aligned pieces c, c + W, c + 2W,
-    // ... -- each load and store instruction covers 16 W contiguous bytes
-    const uint64_t x0 = S + e + 16ull * c;
-#pragma unroll
-    for (int j = 0; j < NP; j++) {
-      const uint64_t x = x0 + 16ull * W * j;
-      ok[j] = live && x >= ps && x + 16 <= pe && !(MCK_WAL_EXP & 1);
-      const uint64_t f = ok[j] && !(MCK_WAL_EXP & 16) ? (x & ~3ull) : zp;
-      v[j] = span_load16<false>(f);
-      // the fifth dword, unless the piece is dword-aligned (then it could
-      // lie past the payload's last dword: re-read the fourth)
-      w5[j] = *reinterpret_cast<gbl_u32_t*>(ok[j] && be ? f + 16 : f + 12);
-    }
-    const uint64_t h16 = (P + 15) & ~15ull;                   // first full output piece
-    const uint64_t t16 = (P + sp.n) & ~15ull;                 // end of the last full piece
-    const uint64_t hb_end = h16 < P + sp.n ? h16 : P + sp.n;  // head bytes [P, hb_end)
-    const uint64_t tb_beg = t16 > hb_end ? t16 : hb_end;      // tail bytes [tb_beg, P + n)
-    uint64_t oh[kHT], ot[kHT];
-    bool okh[kHT], okt[kHT];
-    uint32_t bh[kHT], bt[kHT];
-#pragma unroll
-    for (int m = 0; m < kHT; m++) {
-      oh[m] = P + c + W * m;
-      ot[m] = tb_beg + c + W * m;
-      okh[m] = fin && oh[m] < hb_end && !(MCK_WAL_EXP & 2);
-      okt[m] = fin && ot[m] < P + sp.n && !(MCK_WAL_EXP & 2);
-      bh[m] = *reinterpret_cast<gbl_u8_t*>(okh[m] ? ps + c + W * m : zp);
-      bt[m] = *reinterpret_cast<gbl_u8_t*>(okt[m] ? ps + (ot[m] - P) : zp);
-    }
-
-#pragma unroll
-    for (int j = 0; j < NP; j++) {
-      uint4 o;
-      o.x = __builtin_amdgcn_alignbyte(v[j].y, v[j].x, be);
-      o.y = __builtin_amdgcn_alignbyte(v[j].z, v[j].y, be);
-      o.z = __builtin_amdgcn_alignbyte(v[j].w, v[j].z, be);
-      o.w = __builtin_amdgcn_alignbyte(w5[j], v[j].w, be);
-      WAL_ST(ok[j] && !(MCK_WAL_EXP & 8), st_nt16, x0 + 16ull * W * j + delta, sink, o);
-    }
-#pragma unroll
-    for (int m = 0; m < kHT; m++) {
-      WAL_ST(okh[m], st_u8, oh[m], sink, bh[m]);
-      WAL_ST(okt[m], st_u8, ot[m], sink + 1, bt[m]);
-    }
-
-    // ---- next unit (as crc_rows_loop) ----
-    const bool go = live && (!last || nt < share);
-    const RowSpan nsp = row_span<W, NP>(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kInitTyped);
-    const bool sw = go && last;
-    const RowSpan lsp = row_span_sel(sw, nsp, sp);
-    const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
-    const uint32_t li = sw ? sh.idx(nt) : i;
-    const ChunkN<NP> nxt = row_load_chunk<W, NP>(lsp, lr, c, zp);
-
-    s = row_round<W, NP>(s, cur, sp, r, c, L);
-    uint32_t crc = 0;
-    if (wave_any(fin)) crc = crc_mask(row_finish4<W>(s, sp, lf4));
-    WAL_ST(fin && c == 0, st_u32, reinterpret_cast<uint64_t>(op.crcs + i), sink + 4, crc);
-    // trailer padding + header: bytes c + W m of [dst - pad, dst + hs)
-    const uint64_t hstart = obase + dst - pad;
-#pragma unroll
-    for (int m = 0; m < kHdr; m++) {
-      const uint32_t b = c + (uint32_t)W * m;
-      const bool okb = fin && b < pad + hs && !(MCK_WAL_EXP & 4);
-      const uint32_t val = b < pad ? 0u : wal_hdr_byte(b - pad, crc, sp.n, type, op.log_number);
-      WAL_ST(okb, st_u8, hstart + b, sink + 2 + m, val);
-    }
-
-    // ---- advance ----
-    uint32_t nnt = nt;
-    uint4 nnd = nd;
-    uint64_t nndst = ndst;
-    if (wave_any(sw)) {
-      const uint32_t tk = row_ticket<W>(sw);
-      if (sw) {
-        nnt = tk;
-        nnd = row_desc(tk, share);
-        nndst = *lds_p64(kLdsWalAux + 8 * (tk < share ? tk : 0));
-      }
-    }
-    if (!wave_any(go)) break;
-    key = sw ? nd.w : key;
-    dst = sw ? ndst : dst;
-    live = go;
-    i = li;
-    nt = nnt;
-    nd = nnd;
-    ndst = nndst;
-    sp = lsp;
-    r = lr;
-    cur = nxt;
-  }
-}
-
-template <int W, int NP = 4, bool BLK = true>
-__global__ __launch_bounds__(1024) void k_wal_write_rows(OpWalWrite op, uint32_t first, uint32_t count) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  wal_write_rows<W, NP, BLK>(op, first, count, lds, &g_crc_tables);
-}
-
-// ---- one-pass writer, interleaved pieces (the default) ---------------------
+// ---- one-pass WAL writer: interleaved pieces -------------------------------
 // Lane c of a 16-lane row loads pieces c + 16 j (j = 0..4) of the fragment's
 // 1280-byte round: every load instruction reads 256 contiguous bytes per
 // row, and -- the point -- the row already holds the round in the layout the
@@ -882,9 +657,9 @@ __device__ __forceinline__ uint4 dpp_u32x4(const uint4& v) {
 constexpr int kDppRowRor15 = 0x12F;  // lane j of a row <- lane j + 1 (mod 16)
 constexpr int kDppRowRor1x = 0x121;  // lane j of a row <- lane j - 1 (mod 16)
 
-template <bool BLK>
 __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
                                              const CrcTables* __restrict__ g) {
+  constexpr bool BLK = true;  // contiguous fragment ranges per workgroup
   constexpr int W = 16, NP = 5;
   constexpr int kHdr = 2;  // padding + header bytes per lane (pad + hs <= 21)
   crc_rows_prologue<BLK>(op, first, count, lds, g, false);
@@ -908,8 +683,6 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
   const uint32_t share = sh.n;
   const uint64_t base = reinterpret_cast<uint64_t>(op.src);
   const uint64_t obase = reinterpret_cast<uint64_t>(op.out);
-  const uint64_t sink = reinterpret_cast<uint64_t>(&g_wal_sink[0]) + 16ull * (threadIdx.x & 63);
-  (void)sink;
   const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
   uint32_t t = row_ticket<W>(true);
   bool live = t < share;
@@ -935,7 +708,7 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
     const uint32_t type = key & 0xFF, pad = (key >> 8) & 0xFF;
     const uint32_t hs = ((type >= 5 && type <= 8) || type == 11) ? 11u : 7u;
     const uint64_t P = obase + dst + hs;             // payload in the output
-    const uint64_t ps = sp.ptr, pe = sp.ptr + sp.n;  // payload in the source
+    const uint64_t ps = sp.ptr;  // payload in the source
     const uint64_t delta = P - ps;                   // (mod 2^64)
     const uint32_t e = (uint32_t)(0ull - delta) & 15u;
     const uint32_t q2 = e & 8u, q1 = e & 4u, be = e & 3u;
@@ -955,7 +728,7 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
       const bool ok = live && rel >= 0 && rel <= lim && !(j == NP - 1 && c == 15 && e != 0);
       const uint4 nb = (j < NP - 1 && c == 15) ? rn : rj;
       const uint4 o = il_align(cur.v[j], nb, q2, q1, be);
-      WAL_ST(ok && !(MCK_WAL_EXP & 8), st_nt16, oa0 + 256ull * j, sink, o);
+      if (ok) st16(oa0 + 256ull * j, o);
       rj = rn;
       // one piece at a time (the scheduler would otherwise hoist every
       // piece's DPP moves and selects and spill)
@@ -968,7 +741,7 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
       if (wave_any(okm)) {
         const uint4 cm = lds_u32x4(carry_slot);
         const uint4 o = il_align(cm, cur.v[0], q2, q1, be);
-        WAL_ST(okm, st_nt16, P + (uint64_t)(int64_t)relm, sink, o);
+        if (okm) st16(P + (uint64_t)(int64_t)relm, o);
       }
     }
     if (c == 15) {
@@ -982,10 +755,10 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
       const uint64_t tb_beg = t16 > hb_end ? t16 : hb_end;
       const uint64_t oh = P + c, ot = tb_beg + c;
       const bool okh = fin && oh < hb_end, okt = fin && ot < P + sp.n;
-      const uint32_t bh = (MCK_WAL_EXP & 32) ? 0u : *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : zp);
-      const uint32_t bt = (MCK_WAL_EXP & 32) ? 0u : *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : zp);
-      WAL_ST(okh && !(MCK_WAL_EXP & 2), st_u8, oh, sink, bh);
-      WAL_ST(okt && !(MCK_WAL_EXP & 2), st_u8, ot, sink + 1, bt);
+      const uint32_t bh = *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : zp);
+      const uint32_t bt = *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : zp);
+      if (okh) st_u8(oh, bh);
+      if (okt) st_u8(ot, bt);
     }
 
     // ---- next unit (as crc_rows_loop) ----
@@ -1001,15 +774,15 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
     uint32_t crc = 0;
     if (wave_any(fin)) crc = crc_mask(row_finish4<W>(x, sp, lf4));
     if (wave_any(live && !last)) x = il_gap(x, 0u);  // to the lane's piece in the next round
-    WAL_ST(fin && c == 0, st_u32, reinterpret_cast<uint64_t>(op.crcs + i), sink + 4, crc);
+    if (fin && c == 0) st_u32(reinterpret_cast<uint64_t>(op.crcs + i), crc);
     // trailer padding + header: bytes c + 16 m of [dst - pad, dst + hs)
     const uint64_t hstart = obase + dst - pad;
 #pragma unroll
     for (int m = 0; m < kHdr; m++) {
       const uint32_t b = c + (uint32_t)W * m;
-      const bool okb = fin && b < pad + hs && !(MCK_WAL_EXP & 4);
+      const bool okb = fin && b < pad + hs;
       const uint32_t val = b < pad ? 0u : wal_hdr_byte(b - pad, crc, sp.n, type, op.log_number);
-      WAL_ST(okb, st_u8, hstart + b, sink + 2 + m, val);
+      if (okb) st_u8(hstart + b, val);
     }
 
     // ---- advance ----
@@ -1038,42 +811,18 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
   }
 }
 
-template <bool BLK>
 __global__ __launch_bounds__(1024) void k_wal_write_il(OpWalWrite op, uint32_t first, uint32_t count) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  wal_write_il<BLK>(op, first, count, lds, &g_crc_tables);
+  wal_write_il(op, first, count, lds, &g_crc_tables);
 }
 
-// The physical record image: [pad zeros][crc LE32][len LE16][type]
-// [log number LE32 if recyclable][payload].  One wave per fragment; the
-// body is written as aligned 16-byte stores assembled from aligned source
-// dwords (v_alignbyte), the head (padding + header + the first payload
-// bytes up to a 16-byte boundary) and the tail byte-wise.
-__device__ __forceinline__ uint8_t wal_out_byte(const WalFrag& f, uint32_t crc, uint32_t log_number, uint32_t hs,
-                                                const uint8_t* src, uint64_t a) {
-  // a: output offset within [dst_off - pad, dst_off + hs + length)
-  if (a < f.dst_off) return 0;  // block trailer padding
-  const uint64_t h = a - f.dst_off;
-  if (h < 4) return (uint8_t)(crc >> (8 * h));
-  if (h < 6) return (uint8_t)(f.length >> (8 * (h - 4)));
-  if (h == 6) return f.type;
-  if (h < hs) return (uint8_t)(log_number >> (8 * (h - 7)));
-  return src[f.src_off + (h - hs)];
-}
-
-#ifndef MCK_WAL_COPY_PIPE
-#define MCK_WAL_COPY_PIPE 1
-#endif
-#if MCK_WAL_COPY_PIPE
-// One fragment's pass in k_wal_copy: every load of the fragment's first
-// 1 KiB (head bytes, first 16-byte body chunk of each lane, tail bytes) is
-// issued before any of its stores, and the next fragment's descriptor is
-// loaded before them -- a wave waits one memory round trip per typical
-// (1 KB) fragment instead of one per head / body / tail loop.  Bytes beyond
-// the first pass (long fragments, a head > 64 bytes from an odd pad) run in
-// wal_copy_rest.  Measured (walwrite bench, 2.16M fragments): 1.038 vs
-// 1.143 ms; with non-temporal body loads 1.100; with two fragments' loads
-// issued before either's stores 1.354 (1.388 with nt loads).
+// ---- WAL recovery: reassemble logical records (mck_wal_gather_batch) -----
+// Copy each fragment's payload to out + dst_off: one wave per fragment, the
+// body as aligned 16-byte stores assembled from dword-aligned source loads
+// (v_alignbyte), the < 16-byte head and tail byte-wise.  Every load of a
+// fragment's first KiB is issued before any of its stores and the next
+// fragment's descriptor before them -- one memory round trip per typical
+// (1 KB) fragment (1.038 vs 1.143 ms per 2.16M fragments, round 1).
 struct WalCopyPass {
   uint64_t pay, body0, body1, end, head_end;
   uint64_t ha, ca, ta;  // this lane's head byte, body chunk, tail byte (output offsets)
@@ -1100,154 +849,53 @@ __device__ __forceinline__ uint4 wal_chunk_load(const uint8_t* src, uint64_t s) 
   return v;
 }
 
-template <bool GATHER>
-__device__ __forceinline__ void wal_copy_issue(WalCopyPass& p, const WalFrag& f, uint32_t crc, uint32_t log_number,
-                                               const uint8_t* __restrict__ src, uint32_t lane) {
-  const uint32_t hs = GATHER ? 0u : (f.type >= 5 && f.type <= 8) || f.type == 11 ? 11u : 7u;
-  const uint64_t start = f.dst_off - (GATHER ? 0u : f.pad);
-  p.end = f.dst_off + hs + f.length;
-  p.pay = f.dst_off + hs;                // output offset of payload byte 0
+__device__ __forceinline__ void wal_gather_issue(WalCopyPass& p, const WalFrag& f, const uint8_t* __restrict__ src,
+                                                 uint32_t lane) {
+  p.end = f.dst_off + f.length;
+  p.pay = f.dst_off;                     // output offset of payload byte 0
   p.body0 = (p.pay + 15) & ~15ull;       // first 16-aligned chunk of payload
   p.body1 = p.end & ~15ull;              // end of the last full chunk
   const bool body = p.body0 < p.body1;
-  // head: [start, body0) byte-wise -- or the whole record when it has no
-  // full 16-byte payload chunk; tail: [body1, end) byte-wise (< 16 bytes)
+  // head: [pay, body0) byte-wise -- or the whole fragment when it has no
+  // full 16-byte chunk; tail: [body1, end) byte-wise (< 16 bytes)
   p.head_end = body ? p.body0 : p.end;
-  p.ha = start + lane;
+  p.ha = p.pay + lane;
   p.hv = p.ha < p.head_end;
   p.ca = p.body0 + 16ull * lane;
   p.cv = body && p.ca < p.body1;
   p.ta = p.body1 + lane;
   p.tv = body && p.ta < p.end;
   p.hb = p.tb = 0;
-  if (p.hv) p.hb = GATHER ? src[f.src_off + (p.ha - p.pay)] : wal_out_byte(f, crc, log_number, hs, src, p.ha);
-  if (p.tv) p.tb = GATHER ? src[f.src_off + (p.ta - p.pay)] : wal_out_byte(f, crc, log_number, hs, src, p.ta);
+  if (p.hv) p.hb = src[f.src_off + (p.ha - p.pay)];
+  if (p.tv) p.tb = src[f.src_off + (p.ta - p.pay)];
   if (p.cv) p.v = wal_chunk_load(src, f.src_off + (p.ca - p.pay));
 }
 
-#ifndef MCK_WAL_COPY_NTST
-#define MCK_WAL_COPY_NTST 1
-#endif
-// 16 aligned output bytes.  The writer's log stream is written once and not
-// re-read by the engine, so its stores are non-temporal (walwrite 875 vs 867
-// GiB/s, one alternating pair on one box -- inside the 864-887 spread of the
-// 8-piece config, so "not slower" rather than a measured gain;
-// -DMCK_WAL_COPY_NTST=0 for plain stores).  The GATHER direction keeps
-// plain stores: its reassembled records are read straight back by the
-// record-checksum XXH3 batch.
-template <bool GATHER>
-__device__ __forceinline__ void wal_store16(uint8_t* p, uint4 v) {
-  if (MCK_WAL_COPY_NTST && !GATHER) {
-    span_u32x4 x = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(x, reinterpret_cast<span_u32x4*>(p));
-  } else {
-    *reinterpret_cast<uint4*>(p) = v;
-  }
-}
-
-template <bool GATHER>
-__device__ __forceinline__ void wal_copy_store(const WalCopyPass& p, uint8_t* __restrict__ out) {
-  if (p.hv) out[p.ha] = p.hb;
-  if (p.cv) wal_store16<GATHER>(out + p.ca, p.v);
-  if (p.tv) out[p.ta] = p.tb;
-}
-
-template <bool GATHER>
-__device__ __forceinline__ void wal_copy_rest(const WalCopyPass& p, const WalFrag& f, uint32_t crc,
-                                              uint32_t log_number, const uint8_t* __restrict__ src,
-                                              uint8_t* __restrict__ out) {
-  const uint32_t hs = GATHER ? 0u : (f.type >= 5 && f.type <= 8) || f.type == 11 ? 11u : 7u;
-  for (uint64_t a = p.ha + 64; a < p.head_end; a += 64)
-    out[a] = GATHER ? src[f.src_off + (a - p.pay)] : wal_out_byte(f, crc, log_number, hs, src, a);
-  for (uint64_t c = p.ca + 16ull * 64; c < p.body1; c += 16ull * 64)
-    wal_store16<GATHER>(out + c, wal_chunk_load(src, f.src_off + (c - p.pay)));
-}
-
-// GATHER: the reverse direction for recovery -- copy each fragment's
-// payload (no header, no padding) to out + dst_off, reassembling logical
-// records (mck_wal_gather_batch).
-template <bool GATHER>
-__global__ __launch_bounds__(256) void k_wal_copy(const uint8_t* __restrict__ src, const WalFrag* __restrict__ frags,
-                                                  uint32_t nfrags, uint32_t log_number,
-                                                  const uint32_t* __restrict__ crcs, uint8_t* __restrict__ out) {
+__global__ __launch_bounds__(256) void k_wal_gather(const uint8_t* __restrict__ src, const WalFrag* __restrict__ frags,
+                                                    uint32_t nfrags, uint8_t* __restrict__ out) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t nw = gridDim.x * wpb;
   uint32_t fi = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
   if (fi >= nfrags) return;
   WalFrag f = frags[fi];
-  uint32_t crc = GATHER ? 0u : crcs[fi];
   for (;;) {
     WalCopyPass p;
-    wal_copy_issue<GATHER>(p, f, crc, log_number, src, lane);
+    wal_gather_issue(p, f, src, lane);
     const uint32_t fn = fi + nw;
     const bool more = fn < nfrags;
-    const uint32_t nx = more ? fn : fi;
-    const WalFrag f2 = frags[nx];
-    const uint32_t crc2 = GATHER ? 0u : crcs[nx];
-    wal_copy_store<GATHER>(p, out);
-    wal_copy_rest<GATHER>(p, f, crc, log_number, src, out);
+    const WalFrag f2 = frags[more ? fn : fi];
+    if (p.hv) out[p.ha] = p.hb;
+    if (p.cv) *reinterpret_cast<uint4*>(out + p.ca) = p.v;
+    if (p.tv) out[p.ta] = p.tb;
+    // the rest of a long fragment (beyond the first 64 x 16 bytes)
+    for (uint64_t c = p.ca + 16ull * 64; c < p.body1; c += 16ull * 64)
+      *reinterpret_cast<uint4*>(out + c) = wal_chunk_load(src, f.src_off + (c - p.pay));
     if (!more) break;
     fi = fn;
     f = f2;
-    crc = crc2;
   }
 }
-
-#else
-// GATHER: the reverse direction for recovery -- copy each fragment's
-// payload (no header, no padding) to out + dst_off, reassembling logical
-// records (mck_wal_gather_batch).
-template <bool GATHER>
-__global__ __launch_bounds__(256) void k_wal_copy(const uint8_t* __restrict__ src, const WalFrag* __restrict__ frags,
-                                                  uint32_t nfrags, uint32_t log_number,
-                                                  const uint32_t* __restrict__ crcs, uint8_t* __restrict__ out) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint32_t nw = gridDim.x * wpb;
-  for (uint32_t fi = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)); fi < nfrags; fi += nw) {
-    const WalFrag f = frags[fi];
-    const uint32_t crc = GATHER ? 0u : crcs[fi];
-    const uint32_t hs = GATHER ? 0u : (f.type >= 5 && f.type <= 8) || f.type == 11 ? 11u : 7u;
-    const uint64_t start = f.dst_off - (GATHER ? 0u : f.pad);
-    const uint64_t end = f.dst_off + hs + f.length;
-    const uint64_t pay = f.dst_off + hs;              // output offset of payload byte 0
-    const uint64_t body0 = (pay + 15) & ~15ull;       // first 16-aligned chunk of payload
-    const uint64_t body1 = end & ~15ull;              // end of the last full chunk
-    // head: [start, body0) byte-wise -- or the whole record when it has no
-    // full 16-byte payload chunk
-    const uint64_t head_end = body0 < body1 ? body0 : end;
-    for (uint64_t a = start + lane; a < head_end; a += 64)
-      out[a] = GATHER ? src[f.src_off + (a - pay)] : wal_out_byte(f, crc, log_number, hs, src, a);
-    if (body0 < body1) {
-      // body: 16-byte chunks; chunk c covers payload bytes [c - pay, +16) of
-      // the fragment = source bytes s = f.src_off + (c - pay) ...
-      for (uint64_t c = body0 + 16ull * lane; c < body1; c += 16ull * 64) {
-        const uint64_t s = f.src_off + (c - pay);
-        const uint64_t s4 = s & ~3ull;
-        const uint32_t sh = (uint32_t)(s & 3);
-        const uint32_t* w = reinterpret_cast<const uint32_t*>(src + s4);
-        // aligned source dwords; with sh == 0 the fifth is not needed (and
-        // could lie past the payload's last dword): re-read the fourth
-        uint32_t x[5];
-#pragma unroll
-        for (int k = 0; k < 4; k++) x[k] = w[k];
-        x[4] = w[sh ? 4 : 3];
-        uint4 v;
-        v.x = __builtin_amdgcn_alignbyte(x[1], x[0], sh);
-        v.y = __builtin_amdgcn_alignbyte(x[2], x[1], sh);
-        v.z = __builtin_amdgcn_alignbyte(x[3], x[2], sh);
-        v.w = __builtin_amdgcn_alignbyte(x[4], x[3], sh);
-        *reinterpret_cast<uint4*>(out + c) = v;
-      }
-      // tail: [body1, end) byte-wise
-      for (uint64_t a = body1 + lane; a < end; a += 64)
-        out[a] = GATHER ? src[f.src_off + (a - pay)] : wal_out_byte(f, crc, log_number, hs, src, a);
-    }
-  }
-}
-
-#endif
 
 // ===================== blob log records ===================================
 // db/blob/blob_log_format.cc:97-135 BlobLogRecord: a 32-byte header
@@ -1348,6 +996,13 @@ __global__ __launch_bounds__(256) void k_crc_combine(const uint32_t* __restrict_
   }
   term = wave_xor32(term);
   if ((threadIdx.x & 63) == 0 && term) atomicXor(out, term);
+}
+
+// Read (and with reset, clear) the per-device mismatch ticker in ONE atomic
+// step: a verify kernel running concurrently loses no count between the read
+// and the clear (mck_statistics_get).
+__global__ void k_stats_take(unsigned long long* ctr, unsigned long long* out, int reset) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) *out = reset ? atomicExch(ctr, 0ull) : atomicAdd(ctr, 0ull);
 }
 
 // ============================ WAL verify ==================================

@@ -96,9 +96,8 @@ def test_data_shims_fail_cleanly_without_gpu():
     # argument errors come before any device work
     assert _lib.lib.mck_crc32c_value_r(None, 3, ctypes.byref(out32)) == -1
     assert _lib.lib.mck_crc32c_value_r(b"abc", 3, None) == -1
-    # host pipeline / side-stream pools: releasing with nothing cached is a no-op
+    # the host pipeline's staging: releasing with nothing cached is a no-op
     _lib.lib.mck_host_pipeline_release()
-    _lib.lib.mck_wal_side_release()
 
 
 def test_product_does_not_use_oracle():
