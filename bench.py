@@ -130,6 +130,11 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="0 = the CPUs this process may use (cgroup quota / affinity)")
     p.add_argument("--no-verify", action="store_true")
+    p.add_argument("--crc-driver", choices=["auto", "wave", "rows16", "rows8", "units"], default="auto",
+                   help="force the ragged CRC driver for every workgroup (A/B measurements; the engine's "
+                        "test hook mck_test_set_crc_driver)")
+    p.add_argument("--crc-order", choices=["blocked", "interleaved"], default="blocked",
+                   help="ragged CRC span order per workgroup (A/B measurements)")
     a = p.parse_args()
     if a.steps is None:
         a.steps = 3 if a.workload == "host" else 50
@@ -140,9 +145,8 @@ def parse():
     return a
 
 
-# whole-round uniform CRC kernel: transposed loads unless MCK_CRC_LAYOUT=0
-CRC_UNIFORM_FULL = ("mck::k_crc_uniform<mck::OpCrcValue, true, false>" if os.environ.get("MCK_CRC_LAYOUT") == "0"
-                    else "mck::k_crc_uniform<mck::OpCrcValue, true, true>")
+# whole-round uniform CRC kernel (row-transposed, non-temporal loads)
+CRC_UNIFORM_FULL = "mck::k_crc_uniform<mck::OpCrcValue, true, true>"
 
 
 def _cpu_quota():
@@ -240,10 +244,8 @@ def cpu_baseline(args, kind, block, sample, gpu_results):
 
 
 def _auto(op):
-    """k_crc_auto's instantiation name for op (contiguous span ranges unless
-    MCK_CRC_ORDER=interleaved: the third template argument)."""
-    blk = "" if os.environ.get("MCK_CRC_ORDER") == "interleaved" else ", true"
-    return f"mck::k_crc_auto<{op}, true{blk}>"
+    """k_crc_auto's instantiation name for op (contiguous span ranges)."""
+    return f"mck::k_crc_auto<{op}, true, true>"
 
 
 def _launches(count, dev):
@@ -445,8 +447,7 @@ def make_workload(args, dev, rank, world):
                       f"{args.span_min}-{args.span_max} B per GPU at any byte offset, mck_wal_record_crc_batch")
         else:
             w.step = lambda: S.crc32c_batch(sp, out=out, stream=stream)
-            w.kernel = {"1": "mck::k_crc_rows<mck::OpCrcValue>", "0": "mck::k_crc<mck::OpCrcValue, true>"}.get(
-                os.environ.get("MCK_CRC_ROWS", ""), _auto("mck::OpCrcValue") + _launches(count, dev))
+            w.kernel = _auto("mck::OpCrcValue") + _launches(count, dev)
             w.desc = (f"crc32c_batch over {count} ragged spans of {args.span_min}-{args.span_max} B per GPU "
                       "(explicit offsets/lengths)")
         w.span_bytes = int(lens.sum())
@@ -648,7 +649,7 @@ def make_workload(args, dev, rank, world):
                 1, hbuf.data_ptr(), None, None, block, block, count, 0, 0, 256 << 20,
                 out.ctypes.data, None, ctypes.byref(secs)), "mck_host_batch_checksum")
         w.step = step
-        w.kernel = "mck::k_crc<mck::OpCrcValue, true> (H2D/D2H overlapped)"
+        w.kernel = _auto("mck::OpCrcValue") + " (H2D/D2H overlapped)"
         w.span_bytes = count * block
         w.alg_bytes = count * (block + 4 + 8 + 4)
         w.desc = (f"host-resident pinned {count} x {block} B blocks per GPU (the 8-GPU share of the "
@@ -854,7 +855,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from speedb_amd import shard
+    from speedb_amd import _lib, shard
+    if args.crc_driver != "auto" or args.crc_order != "blocked":
+        drv = {"auto": 0, "wave": 1, "rows16": 2, "rows8": 3, "units": 4}[args.crc_driver]
+        _lib.check(_lib.lib.mck_test_set_crc_driver(drv, 1 if args.crc_order == "interleaved" else 0),
+                   "mck_test_set_crc_driver")
     w = make_workload(args, dev, rank, world)
     stream = torch.cuda.current_stream(dev)
     # clock settle: untimed work for --settle-ms, then the W warmup steps

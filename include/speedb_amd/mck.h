@@ -741,8 +741,18 @@ typedef struct mck_statistics {
 } mck_statistics;
 
 /* Fill *out (reads each initialised device's counters: synchronous);
- * reset != 0 zeroes the counters after reading them. */
+ * reset != 0 zeroes them: each device's mismatch ticker (64-bit) is read and
+ * cleared in one atomic exchange, so no count of a verify kernel running
+ * concurrently is lost. */
 int mck_statistics_get(mck_statistics* out, int reset);
+
+/* TEST HOOK (parity tests only; never needed in production): ragged CRC
+ * batches choose their driver per workgroup from the share's mean span
+ * length, so a mixed parity batch may exercise only one driver.  driver:
+ * 0 = by length (the default), 1 = 4 KiB-round wave driver, 2 = 16-lane
+ * rows, 3 = 8-lane rows, 4 = unit stream; interleaved != 0 deals spans to
+ * workgroups round-robin instead of in contiguous ranges.  Process-wide. */
+int mck_test_set_crc_driver(int driver, int interleaved);
 
 #ifdef __cplusplus
 }

@@ -136,6 +136,7 @@ SIGNATURES = [
       ctypes.POINTER(ctypes.c_double)]),
     ("mck_host_pipeline_release", None, []),
     ("mck_statistics_get", ctypes.c_int, [vp, ctypes.c_int]),
+    ("mck_test_set_crc_driver", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
 ]
 
 for _name, _res, _args in SIGNATURES:

@@ -551,103 +551,10 @@ struct SpanDesc {
   uint32_t init;
 };
 
-template <class Op>
-__device__ __forceinline__ SpanDesc crc_desc_fetch(const Op& op, uint32_t first, uint32_t stride, uint32_t end,
-                                                   const CrcLane& L) {
-  SpanDesc d{0, 0, 0};
-  const uint64_t i = (uint64_t)first + (uint64_t)L.plane * stride;
-  if (i < end) {
-    d.off = op.off((uint32_t)i);
-    d.len = op.len((uint32_t)i);
-    d.init = op.init_crc((uint32_t)i);
-  }
-  return d;
-}
-__device__ __forceinline__ SpanDesc crc_desc_pick(const SpanDesc& d, uint32_t k) {
-  SpanDesc r;
-  r.off = readlane_u64(d.off, k);
-  r.len = readlane_u64(d.len, k);
-  r.init = readlane_u32(d.init, k);
-  return r;
-}
-
-// ---- span feeds: which span a wave hashes next ----------------------------
-// Static: spans wave_id, wave_id + nwaves, ... over the whole grid; span
-// descriptors are fetched 64 at a time (lane l loads the wave's l-th next
-// descriptor) and read back with v_readlane.
-template <class Op>
-struct FeedStatic {
-  uint32_t i, k, nwaves, count;
-  SpanDesc db;
-  __device__ bool first(const Op& op, const CrcLane& L, uint32_t* span, SpanDesc* d) {
-    const uint32_t wpb = blockDim.x >> 6;
-    i = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-    nwaves = gridDim.x * wpb;
-    if (i >= count) return false;
-    k = 0;
-    db = crc_desc_fetch(op, i, nwaves, count, L);
-    *d = crc_desc_pick(db, 0);
-    *span = i;
-    return true;
-  }
-  __device__ bool next(const Op& op, const CrcLane& L, uint32_t* span, SpanDesc* d) {
-    const uint32_t ni = i + nwaves;
-    if (ni >= count) return false;
-    if (++k == 64) {
-      db = crc_desc_fetch(op, ni, nwaves, count, L);
-      k = 0;
-    }
-    *d = crc_desc_pick(db, k);
-    *span = i = ni;
-    return true;
-  }
-};
-
-// Dynamic: workgroup b owns spans b, b + G, b + 2G, ... (interleaved, so
-// runs of similar spans spread over all CUs); their descriptors are staged
-// in LDS once, and each wave takes the next one with an LDS ticket when it
-// frees up -- ragged batches stay balanced inside the CU.  Used when a
-// workgroup's share fits the LDS descriptor cache.
-constexpr uint32_t kDescCache = 1536;
-constexpr uint32_t kLdsDescOff = kLdsLowEnd;                     // u64 [1536]
-constexpr uint32_t kLdsDescLen = kLdsDescOff + 8 * kDescCache;   // u32 [1536]
-constexpr uint32_t kLdsDescInit = kLdsDescLen + 4 * kDescCache;  // u32 [1536]
-constexpr uint32_t kLdsTicket = kLdsDescInit + 4 * kDescCache;   // u32
-static_assert(kLdsTicket + 4 <= kLdsStep, "descriptor cache must fit below the step tables");
-
 typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
 typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
 __device__ __forceinline__ lds_u32_t* lds_p32(uint32_t off) { return reinterpret_cast<lds_u32_t*>(static_cast<size_t>(off)); }
 __device__ __forceinline__ lds_u64_t* lds_p64(uint32_t off) { return reinterpret_cast<lds_u64_t*>(static_cast<size_t>(off)); }
-
-template <class Op>
-__device__ __forceinline__ void feed_lds_stage(const Op& op, uint32_t count) {
-  const uint32_t G = gridDim.x, b = blockIdx.x;
-  const uint32_t n = (count - b + G - 1) / G;
-  for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
-    const uint32_t i = b + G * t;
-    *lds_p64(kLdsDescOff + 8 * t) = op.off(i);
-    *lds_p32(kLdsDescLen + 4 * t) = (uint32_t)op.len(i);
-    *lds_p32(kLdsDescInit + 4 * t) = op.init_crc(i);
-  }
-  if (threadIdx.x == 0) *lds_p32(kLdsTicket) = 0;
-}
-
-template <class Op>
-struct FeedLds {
-  uint32_t n;
-  __device__ bool take(uint32_t* span, SpanDesc* d) {
-    const uint32_t t = __builtin_amdgcn_readfirstlane(lds_ticket(lds_p32(kLdsTicket)));
-    if (t >= n) return false;
-    *span = blockIdx.x + gridDim.x * t;
-    d->off = *lds_p64(kLdsDescOff + 8 * t);
-    d->len = *lds_p32(kLdsDescLen + 4 * t);
-    d->init = *lds_p32(kLdsDescInit + 4 * t);
-    return true;
-  }
-  __device__ bool first(const Op&, const CrcLane&, uint32_t* span, SpanDesc* d) { return take(span, d); }
-  __device__ bool next(const Op&, const CrcLane&, uint32_t* span, SpanDesc* d) { return take(span, d); }
-};
 
 template <class Op, class Feed, bool T = false>
 __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& L) {
@@ -691,9 +598,9 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
   }
 }
 
-// Persistent, software-pipelined driver: each wave walks (span, round) pairs
-// of the spans its feed hands it; the next pair's chunk is loaded before the
-// current one is hashed.
+// crc_drive: the persistent, software-pipelined wave driver -- each wave
+// walks (span, round) pairs of the spans its feed hands it (FeedRowCache,
+// below); the next pair's chunk is loaded before the current one is hashed.
 // Op supplies the spans and consumes the results:
 //   const uint8_t* Op::base(), uint64_t Op::off(i), uint64_t Op::len(i),
 //   uint32_t Op::init_crc(i)                    (per lane, i < count)
@@ -702,24 +609,6 @@ __device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& 
 //                                  with writer set store: lane 0 of the wave
 //                                  here, lane 0 of each row in the row driver)
 // T: row-transposed loads (crc_load_chunk<true>, row_transpose).
-template <class Op, bool T = false>
-__device__ __forceinline__ void crc_spans_driver(const Op& op, uint32_t count, uint8_t* lds,
-                                                 const CrcTables* __restrict__ g) {
-  crc_fill_lds(lds, g);
-  const uint32_t share = (count + gridDim.x - 1) / gridDim.x;  // largest workgroup share
-  const bool dyn = share <= kDescCache;                       // grid-uniform
-  if (dyn) feed_lds_stage(op, count);
-  __syncthreads();
-  const CrcLane L = crc_lane();
-  if (dyn) {
-    FeedLds<Op> f{(count - blockIdx.x + gridDim.x - 1) / gridDim.x};
-    crc_drive<Op, FeedLds<Op>, T>(op, f, L);
-  } else {
-    FeedStatic<Op> f;
-    f.count = count;
-    crc_drive<Op, FeedStatic<Op>, T>(op, f, L);
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Uniform batches: every span has the same 16-byte-multiple length and a
@@ -1226,13 +1115,6 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, uint32_t first, uint
     cur = nxt;
     pcur = pnxt;
   }
-}
-
-template <class Op, int W>
-__device__ __forceinline__ void crc_rows_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
-                                                const CrcTables* __restrict__ g) {
-  crc_rows_prologue(op, first, count, lds, g, false);
-  crc_rows_loop<Op, W>(op, first, count, g);
 }
 
 // The wave driver (crc_drive) fed from the row descriptor cache: one

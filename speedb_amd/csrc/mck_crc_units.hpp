@@ -186,7 +186,7 @@ struct UItem {
   uint32_t U;     // units of the span
   uint32_t M, m;  // pieces of the span, this piece (0 = last)
   uint32_t kt;    // a1 - end
-  uint32_t inj;   // unshift(~init, ptr & 15)
+  uint32_t inj;   // unshift(~init, ptr & 15): Extend's init state at the piece holding ptr
   __device__ uint32_t klo() const { return kPieceUnits * m; }
   __device__ uint32_t khi() const { return m == M - 1 ? U - 1 : kPieceUnits * m + kPieceUnits - 1; }
   // head unit: lanes below own load zeros, lane own holds ptr
@@ -195,14 +195,16 @@ struct UItem {
   __device__ uint64_t n() const { return a1 - kt - ptr; }
 };
 
-__device__ __forceinline__ uint32_t unit_pieces(uint32_t U) {
-  return U <= kSplitUnits ? 1u : (U - 9u) / kPieceUnits + 1u;
-}
 __device__ __forceinline__ uint32_t unit_count(uint64_t ptr, uint32_t n) {
   const uint64_t a0 = ptr & ~15ull, a1 = (ptr + n + 15) & ~15ull;
-  return (uint32_t)(((a1 - a0) >> 4) + 63) >> 6;
+  return n ? (uint32_t)(((a1 - a0) >> 4) + 63) >> 6 : 0u;
+}
+// items of a span: 0 for an empty span (finished when the window is staged)
+__device__ __forceinline__ uint32_t unit_pieces(uint32_t U) {
+  return U == 0 ? 0u : U <= kSplitUnits ? 1u : (U - 9u) / kPieceUnits + 1u;
 }
 
+// staged descriptor: {off lo, off hi, len, inj}
 __device__ __forceinline__ uint4 unit_desc(uint32_t t) {
   const span_u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const span_u32x4*>(
       static_cast<size_t>(kULdsDesc + 16 * t));
@@ -229,130 +231,77 @@ struct UShare {
   __device__ uint32_t idx(uint32_t t) const { return start + stride * t; }
 };
 
-// Take the next item of the window (lane 0 runs the CAS on the {slot,
-// piece} ticket, the result is wave-uniform).  Empty spans finish here.
-// Returns false when the window is exhausted.
-template <class Op>
-__device__ __forceinline__ bool unit_take(const Op& op, const UShare& sh, uint32_t wn, uint64_t base, int kind,
-                                          UItem* it) {
-  for (;;) {
-    uint32_t t = 0xFFFFFFFFu, q = 0;
-    if ((threadIdx.x & 63) == 0) {
-      uint64_t old = __hip_atomic_load(lds_p64(kULdsTicket), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      for (;;) {
-        const uint32_t ot = (uint32_t)old, oq = (uint32_t)(old >> 32);
-        if (ot >= wn) break;
-        const uint4 d = unit_desc(ot);
-        const uint64_t p = base + (((uint64_t)d.y << 32) | d.x);
-        const uint32_t M = d.z ? unit_pieces(unit_count(p, d.z)) : 1u;
-        const uint64_t nw = oq + 1 < M ? old + (1ull << 32) : (uint64_t)(ot + 1);
-        if (__hip_atomic_compare_exchange_strong(lds_p64(kULdsTicket), &old, nw, __ATOMIC_RELAXED,
-                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-          t = ot;
-          q = oq;
-          break;
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// Take the next item of the window: lane 0 advances the {slot, piece}
+// ticket with a CAS (empty spans, finished at staging, are skipped); the
+// item is wave-uniform.  Only LDS traffic (no memory op: the caller's
+// in-flight loads are not waited for).  False when the window is exhausted.
+__device__ __forceinline__ bool unit_take(uint32_t wn, uint64_t base, UItem* it) {
+  uint32_t t = 0xFFFFFFFFu, q = 0;
+  uint4 d = make_uint4(0, 0, 0, 0);
+  if ((threadIdx.x & 63) == 0) {
+    uint64_t old = __hip_atomic_load(lds_p64(kULdsTicket), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (;;) {
+      const uint32_t ot = (uint32_t)old, oq = (uint32_t)(old >> 32);
+      if (ot >= wn) break;
+      const uint4 x = unit_desc(ot);
+      const uint32_t M = unit_pieces(unit_count(base + (((uint64_t)x.y << 32) | x.x), x.z));
+      const uint64_t nw = oq + 1 < M ? old + (1ull << 32) : (uint64_t)(ot + 1);
+      if (__hip_atomic_compare_exchange_strong(lds_p64(kULdsTicket), &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        if (M == 0) {  // an empty span: nothing to hash
+          old = nw;
+          continue;
         }
+        t = ot;
+        q = oq;
+        d = x;
+        break;
       }
     }
-    t = (uint32_t)__builtin_amdgcn_readfirstlane((int)t);
-    q = (uint32_t)__builtin_amdgcn_readfirstlane((int)q);
-    if (t >= wn) return false;
-    const uint4 d = unit_desc(t);
-    const uint64_t ptr = base + (((uint64_t)d.y << 32) | d.x);
-    const uint32_t n = d.z;
-    if (n == 0) {  // Extend(init, "") = init
-      const uint32_t i = sh.idx(t);
-      op.finish(i, unit_init(op, kind, d.w), unit_pre(op, i, ptr, 0), (threadIdx.x & 63) == 0);
-      continue;
-    }
-    it->ptr = ptr;
-    it->t = t;
-    it->a1 = (ptr + n + 15) & ~15ull;
-    it->U = unit_count(ptr, n);
-    it->M = unit_pieces(it->U);
-    it->m = it->M - 1 - q;
-    it->kt = (uint32_t)(it->a1 - (ptr + n));
-    const uint32_t ninit = ~unit_init(op, kind, d.w);
-    const uint32_t hb = it->hb();
-    it->inj = hb ? unit_unshift(hb, ninit) : ninit;
-    return true;
   }
+  t = rfl(t);
+  if (t >= wn) return false;
+  q = rfl(q);
+  const uint64_t ptr = base + (((uint64_t)rfl(d.y) << 32) | rfl(d.x));
+  const uint32_t n = rfl(d.z);
+  it->ptr = ptr;
+  it->t = t;
+  it->a1 = (ptr + n + 15) & ~15ull;
+  it->U = unit_count(ptr, n);
+  it->M = unit_pieces(it->U);
+  it->m = it->M - 1 - q;
+  it->kt = (uint32_t)(it->a1 - (ptr + n));
+  it->inj = rfl(d.w);
+  return true;
 }
 
-// One iteration's four unit slots: slots [0, na) are units ka, ka - 1, ...
-// of item A, slots [na, na + nb) units B.khi(), ... of item B.  A plan ends
-// at most one item (A): B is taken only if it continues past the plan, so
-// one set of epilogue inputs per iteration suffices.
+// One iteration's four unit slots, precomputed when the iteration is planned
+// (wave-uniform, SGPRs): slots [0, na) are units of item A (the cursor's
+// item), slots [na, na + nb) the first units of item B (the prefetched
+// next item); the rest are empty.  A plan ends at most one item (A): B is
+// taken only if it continues past the plan, so one set of epilogue inputs
+// per iteration suffices.
+constexpr uint32_t kUFirst = 1u, kUHead = 16u, kUTail = 256u, kUAEnd = 4096u;  // << slot
 struct UPlan {
-  UItem A, B;
-  uint32_t ka, na, nb;
-  bool a_first, a_end;
+  uint64_t base[4];   // slot j's unit: [base, base + 1 KiB)
+  uint32_t below[4];  // lanes below this load the zero piece (64: empty slot)
+  uint32_t flags;     // kUFirst << j: an item starts at slot j; kUHead << j: ... at its span's
+                      // head unit; kUTail << j: slot j is its span's last unit; kUAEnd: A ends
+  uint32_t na;
+  uint32_t hA, hB;    // own | hb << 8 | kt << 16 of A's and B's spans
+  uint32_t injA, injB;
+  uint32_t At, Am;    // A's window slot and piece (the flush re-reads the rest)
 };
-
-// Fold one unit into a lane's state (see the header comment).
-__device__ __forceinline__ uint32_t unit_fold(uint32_t s, uint4 v, uint32_t k, const UItem& I, bool first,
-                                              const UnitLane& UL) {
-  const bool head = k == I.U - 1;  // wave-uniform (implies first)
-  const uint32_t own = I.own();
-  if (head) {
-    const uint4 mh = lds_u32x4(kULdsMaskHead + 16 * (UL.lane == own ? I.hb() : 0u));
-    and4(v, mh);
-  }
-  if (k == 0 && I.kt) {
-    const uint4 mt = lds_u32x4(kULdsMaskTail + 16 * (UL.lane == 63 ? I.kt : 0u));
-    and4(v, mt);
-  }
-  uint32_t x;
-  if (first)
-    x = ((head && UL.lane == own) ? I.inj : 0u) ^ v.x;
-  else
-    x = crc_gap4x(s, UL, v.x);
-  x = crc_step4x(x, UL.S, v.y);
-  x = crc_step4x(x, UL.S, v.z);
-  return crc_step4x(x, UL.S, v.w);
-}
-
-// Item I's last unit is folded: reduce, and either run the epilogue or
-// (piece of a split span) add the partial to the span's accumulator.
-template <class Op>
-__device__ __forceinline__ void unit_flush(const Op& op, const UShare& sh, const UItem& I, uint32_t s,
-                                           const typename Op::Pre& pre, const UnitLane& UL,
-                                           const CrcTables* __restrict__ g) {
-  uint32_t p = wave_xor32(unit_lane_final(s, UL.fl));  // pure state at a1 - 1024 klo
-  const uint32_t i = sh.idx(I.t);
-  if (I.M > 1) {
-    for (uint32_t m = I.m, b = 0; m; m >>= 1, b++)
-      if (m & 1) p = gmem_nibmap(g->pow16k[b], p);
-    uint32_t c = 0;
-    if (UL.lane == 0) {
-      __hip_atomic_fetch_xor(lds_p32(kULdsAcc + 8 * I.t), p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      c = __hip_atomic_fetch_add(lds_p32(kULdsAcc + 8 * I.t + 4), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (c == I.M - 1)
-        p = __hip_atomic_load(lds_p32(kULdsAcc + 8 * I.t), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    c = (uint32_t)__builtin_amdgcn_readfirstlane((int)c);
-    if (c != I.M - 1) return;
-    p = (uint32_t)__builtin_amdgcn_readfirstlane((int)p);
-    if (I.kt) p = unit_unshift(I.kt, p);
-    op.finish(i, ~p, unit_pre(op, i, I.ptr, I.n()), UL.lane == 0);
-    return;
-  }
-  if (I.kt) p = unit_unshift(I.kt, p);
-  op.finish(i, ~p, pre, UL.lane == 0);
-}
-
-// Lane address of unit k's piece (zero piece for lanes before the span).
-__device__ __forceinline__ uint64_t unit_addr(const UItem& I, uint32_t k, uint32_t lane, uint64_t zp) {
-  const uint32_t below = k == I.U - 1 ? I.own() : 0u;
-  const uint64_t a = I.a1 - (uint64_t)kUnitBytes * (k + 1) + 16ull * lane;
-  return lane < below ? zp : a;
-}
 
 struct UnitCursor {
   UItem C, N;  // current item (units kc, kc - 1, ... not yet loaded), prefetched next item
   uint32_t kc;
   bool cv, nv;  // valid
 };
+
+__device__ __forceinline__ uint32_t unit_hpack(const UItem& I) { return I.own() | (I.hb() << 8) | (I.kt << 16); }
 
 // Plan the next iteration from the cursor; sets *consumed when N was used
 // (the caller takes a new N after issuing the loads).
@@ -366,49 +315,128 @@ __device__ __forceinline__ UPlan unit_plan(UnitCursor& q, bool* consumed) {
     q.nv = false;
     *consumed = true;
   }
-  P.A = q.C;
-  P.B = q.N;
-  P.ka = q.kc;
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    P.base[j] = 0;
+    P.below[j] = 64;
+  }
+  P.flags = 0;
   P.na = 0;
-  P.nb = 0;
-  P.a_first = false;
-  P.a_end = false;
+  P.hA = P.hB = P.injA = P.injB = 0;
+  P.At = q.C.t;
+  P.Am = q.C.m;
   if (!q.cv) return P;
-  const uint32_t avail = q.kc - q.C.klo() + 1;
-  P.na = avail < 4 ? avail : 4;
-  P.a_first = q.kc == q.C.khi();
-  P.a_end = avail <= 4;
-  if (!P.a_end) {
+  const UItem& C = q.C;
+  const uint32_t avail = q.kc - C.klo() + 1;
+  const uint32_t na = avail < 4 ? avail : 4;
+  P.na = na;
+  P.hA = unit_hpack(C);
+  P.injA = C.inj;
+  const uint32_t ownA = C.own();
+#pragma unroll
+  for (uint32_t j = 0; j < 4; j++) {
+    if (j < na) {
+      const uint32_t k = q.kc - j;
+      P.base[j] = C.a1 - (uint64_t)kUnitBytes * (k + 1);
+      P.below[j] = k == C.U - 1 ? ownA : 0u;
+      P.flags |= (k == C.U - 1 ? kUHead << j : 0u) | (k == 0 && C.kt ? kUTail << j : 0u);
+    }
+  }
+  if (q.kc == C.khi()) P.flags |= kUFirst;
+  if (avail > 4) {
     q.kc -= 4;
     return P;
   }
+  P.flags |= kUAEnd;
   q.cv = false;
-  if (P.na < 4 && q.nv) {
-    const uint32_t bu = q.N.khi() - q.N.klo() + 1;
-    if (bu > 4 - P.na) {  // B continues past this plan
-      P.nb = 4 - P.na;
+  if (na < 4 && q.nv) {
+    const UItem& N = q.N;
+    const uint32_t bu = N.khi() - N.klo() + 1;
+    if (bu > 4 - na) {  // B continues past this plan (so none of its slots is its last unit)
+      const uint32_t kh = N.khi(), ownB = N.own();
+#pragma unroll
+      for (uint32_t j = 1; j < 4; j++) {
+        if (j >= na) {
+          const uint32_t k = kh - (j - na);
+          P.base[j] = N.a1 - (uint64_t)kUnitBytes * (k + 1);
+          P.below[j] = k == N.U - 1 ? ownB : 0u;
+          P.flags |= (k == N.U - 1 ? kUHead << j : 0u) | (j == na ? kUFirst << j : 0u);
+        }
+      }
+      P.hB = unit_hpack(N);
+      P.injB = N.inj;
       q.nv = false;
       *consumed = true;
-      q.C = q.N;
-      q.kc = q.N.khi() - P.nb;
+      q.C = N;
+      q.kc = kh - (4 - na);
       q.cv = true;
     }
   }
   return P;
 }
 
-__device__ __forceinline__ Chunk unit_load(const UPlan& P, uint32_t lane, uint64_t zp) {
+// The four loads of plan P: lane l's piece of every slot's unit (the zero
+// piece for lanes before a span's head and for empty slots).  Straight-line,
+// so every load is unconditional and the waits exact.
+__device__ __forceinline__ Chunk unit_load(const UPlan& P, uint32_t lane16, uint32_t lane, uint64_t zp) {
   Chunk c;
 #pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    uint64_t a = zp;
-    if (j < P.na)
-      a = unit_addr(P.A, P.ka - j, lane, zp);
-    else if (j < P.na + P.nb)
-      a = unit_addr(P.B, P.B.khi() - (j - P.na), lane, zp);
-    c.v[j] = span_load16<true>(a);
-  }
+  for (int j = 0; j < 4; j++) c.v[j] = span_load16<true>(lane < P.below[j] ? zp : P.base[j] + lane16);
   return c;
+}
+
+// keep bytes >= h of a 16-byte piece (h < 16)
+__device__ __forceinline__ void unit_mask_head(uint4& v, uint32_t h) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int z = (int)h - 4 * q;
+    w[q] &= z <= 0 ? 0xFFFFFFFFu : z >= 4 ? 0u : 0xFFFFFFFFu << (8 * z);
+  }
+}
+// keep the first 16 - k bytes (k < 16)
+__device__ __forceinline__ void unit_mask_tail(uint4& v, uint32_t k) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(&v);
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int keep = 16 - (int)k - 4 * q;
+    w[q] &= keep >= 4 ? 0xFFFFFFFFu : keep <= 0 ? 0u : 0xFFFFFFFFu >> (8 * (4 - keep));
+  }
+}
+
+// Item (window slot t, piece m) has its last unit folded (lane state s):
+// reduce, and either run the epilogue or (piece of a split span) add the
+// partial to the span's accumulator; the wave completing the span's last
+// piece runs the epilogue.
+template <class Op>
+__device__ __forceinline__ void unit_flush(const Op& op, const UShare& sh, uint64_t base, uint32_t t, uint32_t m,
+                                           uint32_t s, const typename Op::Pre& pre, const UnitLane& UL,
+                                           const CrcTables* __restrict__ g) {
+  uint32_t p = wave_xor32(unit_lane_final(s, UL.fl));  // pure state at a1 - 1024 klo
+  const uint4 d = unit_desc(t);
+  const uint64_t ptr = base + (((uint64_t)d.y << 32) | d.x);
+  const uint32_t n = d.z;
+  const uint32_t kt = (uint32_t)(((ptr + n + 15) & ~15ull) - (ptr + n));
+  const uint32_t M = unit_pieces(unit_count(ptr, n));
+  const uint32_t i = sh.idx(t);
+  if (M > 1) {
+    for (uint32_t mm = m, b = 0; mm; mm >>= 1, b++)
+      if (mm & 1) p = gmem_nibmap(g->pow16k[b], p);
+    uint32_t c = 0;
+    if (UL.lane == 0) {
+      __hip_atomic_fetch_xor(lds_p32(kULdsAcc + 8 * t), p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      c = __hip_atomic_fetch_add(lds_p32(kULdsAcc + 8 * t + 4), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (c == M - 1) p = __hip_atomic_load(lds_p32(kULdsAcc + 8 * t), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    c = rfl(c);
+    if (c != M - 1) return;
+    p = rfl(p);
+    if (kt) p = unit_unshift(kt, p);
+    op.finish(i, ~p, unit_pre(op, i, ptr, n), UL.lane == 0);
+    return;
+  }
+  if (kt) p = unit_unshift(kt, p);
+  op.finish(i, ~p, pre, UL.lane == 0);
 }
 
 // The wave loop over one share window.
@@ -416,40 +444,57 @@ template <class Op>
 __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh, uint32_t wn,
                                                  const CrcTables* __restrict__ g) {
   const UnitLane UL = unit_lane();
+  const uint32_t lane16 = 16u * UL.lane;
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
-  const int kind = op.init_kind();
   typedef typename Op::Pre Pre;
   UnitCursor q;
   q.cv = false;
   q.kc = 0;
-  q.nv = unit_take(op, sh, wn, base, kind, &q.N);
+  q.nv = unit_take(wn, base, &q.N);
   if (!q.nv) return;
   q.C = q.N;
   bool consumed;
   UPlan P = unit_plan(q, &consumed);
-  // epilogue inputs of the plan's ending item, issued before its chunks
-  // (so the wait for the chunks covers them; the load count per iteration
-  // differs, the order keeps vmcnt exact)
-  Pre pre{};
-  if (P.a_end && P.A.M == 1) pre = unit_pre(op, sh.idx(P.A.t), P.A.ptr, P.A.n());
-  Chunk cur = unit_load(P, UL.lane, zp);
-  if (consumed) q.nv = unit_take(op, sh, wn, base, kind, &q.N);
+  Chunk cur = unit_load(P, lane16, UL.lane, zp);
+  // epilogue inputs of the item the plan ends, issued after its chunks in
+  // every iteration (a fixed number of loads per iteration keeps vmcnt exact)
+  const auto pre_of = [&](const UPlan& X) {
+    const uint4 d = unit_desc(X.At);
+    return unit_pre(op, sh.idx(X.At), base + (((uint64_t)d.y << 32) | d.x), d.z);
+  };
+  Pre pre = pre_of(P);
+  if (consumed) q.nv = unit_take(wn, base, &q.N);
   uint32_t s = 0;
   while (P.na) {
     bool cn;
     const UPlan Q = unit_plan(q, &cn);
-    Pre pn{};
-    if (Q.a_end && Q.A.M == 1) pn = unit_pre(op, sh.idx(Q.A.t), Q.A.ptr, Q.A.n());
-    const Chunk nxt = unit_load(Q, UL.lane, zp);
-    if (cn) q.nv = unit_take(op, sh, wn, base, kind, &q.N);
+    const Chunk nxt = unit_load(Q, lane16, UL.lane, zp);
+    const Pre pn = pre_of(Q);
+    if (cn) q.nv = unit_take(wn, base, &q.N);
+    uint32_t sA = s;
+    const uint32_t f = P.flags;
 #pragma unroll
-    for (uint32_t j = 0; j < 4; j++)
-      if (j < P.na) s = unit_fold(s, cur.v[j], P.ka - j, P.A, P.a_first && j == 0, UL);
-    if (P.a_end) unit_flush(op, sh, P.A, s, pre, UL, g);
-#pragma unroll
-    for (uint32_t j = 1; j < 4; j++)
-      if (j >= P.na && j < P.na + P.nb) s = unit_fold(s, cur.v[j], P.B.khi() - (j - P.na), P.B, j == P.na, UL);
+    for (uint32_t j = 0; j < 4; j++) {
+      uint4 v = cur.v[j];
+      uint32_t extra = 0;
+      if (f & (kUHead << j)) {  // wave-uniform: the head unit of a span
+        const uint32_t h = j < P.na ? P.hA : P.hB;
+        if (UL.lane == (h & 255u)) {
+          unit_mask_head(v, (h >> 8) & 15u);
+          extra = j < P.na ? P.injA : P.injB;
+        }
+      }
+      if ((f & (kUTail << j)) && UL.lane == 63) unit_mask_tail(v, P.hA >> 16);
+      // a unit's first piece: zshift(state, 1012) ^ w0 -- from state 0 (and
+      // the init injected at the head piece) when an item starts here
+      uint32_t x = crc_gap4x((f & (kUFirst << j)) ? 0u : s, UL, v.x ^ extra);
+      x = crc_step4x(x, UL.S, v.y);
+      x = crc_step4x(x, UL.S, v.z);
+      s = crc_step4x(x, UL.S, v.w);
+      if (j + 1 == P.na) sA = s;  // A's last unit in this plan
+    }
+    if (f & kUAEnd) unit_flush(op, sh, base, P.At, P.Am, sA, pre, UL, g);
     P = Q;
     cur = nxt;
     pre = pn;
@@ -475,6 +520,9 @@ __device__ __forceinline__ void crc_units_driver(const Op& op, uint32_t first, u
     stride = G;
     n = count > b ? (count - b + G - 1) / G : 0;
   }
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  const int kind = op.init_kind();
+  __syncthreads();  // the un-shift tables are read by the staging
   for (uint32_t w0 = 0; w0 < n; w0 += kUDescCache) {
     const uint32_t wn = n - w0 < kUDescCache ? n - w0 : kUDescCache;
     const UShare sh{start + stride * w0, stride};
@@ -482,9 +530,15 @@ __device__ __forceinline__ void crc_units_driver(const Op& op, uint32_t first, u
     for (uint32_t t = threadIdx.x; t < wn; t += blockDim.x) {
       const uint32_t i = sh.idx(t);
       const uint64_t off = op.off(i);
-      const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), (uint32_t)op.len(i), op.init_key(i)};
+      const uint32_t len = (uint32_t)op.len(i);
+      const uint32_t init = unit_init(op, kind, op.init_key(i));
+      const uint32_t hb = (uint32_t)(base + off) & 15u;
+      const uint32_t inj = hb ? unit_unshift(hb, ~init) : ~init;
+      const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, inj};
       *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kULdsDesc + 16 * t)) = d;
       *lds_p64(kULdsAcc + 8 * t) = 0;
+      // Extend(init, "") = init: empty spans finish here (the ticket skips them)
+      if (len == 0) op.finish(i, init, op.pre(i, base + off, 0), true);
     }
     if (threadIdx.x == 0) *lds_p64(kULdsTicket) = 0;
     __syncthreads();

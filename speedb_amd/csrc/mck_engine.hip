@@ -155,108 +155,24 @@ SpanSrc to_src(const mck_spans* s) {
   return SpanSrc{static_cast<const uint8_t*>(s->base), s->offsets, s->lengths, s->stride, s->length};
 }
 
-// Uniform whole-round CRC load layout: transposed (contiguous,
-// non-temporal) unless MCK_CRC_LAYOUT=0 selects the chunk layout (A/B).
-bool crc_tlayout() {
-  static const bool t = [] {
-    const char* e = getenv("MCK_CRC_LAYOUT");
-    return !e || strcmp(e, "0") != 0;
-  }();
-  return t;
-}
-
-// Generic CRC driver load layout per op: row-transposed, non-temporal loads
-// (k_crc<Op, true>: SST mix 63.0 -> 66.4 %, ragged 4 KiB 65.0 -> 69.3 %,
-// 64 KiB 74.7 -> 83.4 %) except for the ~1 KiB WAL-writer fragments, where
-// the chunk layout measured 0.285 vs 0.276.  -DMCK_CRC_GENERIC_T=0 turns it off.
-#ifndef MCK_CRC_GENERIC_T
-#define MCK_CRC_GENERIC_T 1
-#endif
-template <class Op>
-struct CrcRowT {
-  static constexpr bool value = MCK_CRC_GENERIC_T;
-};
+// Generic CRC driver load layout: row-transposed, non-temporal loads
+// (crc_drive<Op, true>: SST mix 63.0 -> 66.4 %, ragged 4 KiB 65.0 -> 69.3 %,
+// 64 KiB 74.7 -> 83.4 %).
+constexpr bool kCrcGenericT = true;
 
 // Ragged batches run on k_crc_auto, which picks the driver per workgroup
-// from the mean length of its share (crc_auto_driver).  A/B switches, read
-// once per process: MCK_CRC_AUTO=wave|rows16|rows8 forces one driver inside
-// it; MCK_CRC_ROWS=0 restores the standalone wave-driver kernel (k_crc,
-// static feed for big batches), MCK_CRC_ROWS=1 the standalone row kernel
-// (width MCK_CRC_ROW_LANES).
-int crc_rows_force() {
-  static const int v = [] {
-    const char* e = getenv("MCK_CRC_ROWS");
-    return !e ? -1 : atoi(e) ? 1 : 0;
-  }();
-  return v;
-}
-int crc_auto_force() {
-  static const int v = [] {
-    const char* e = getenv("MCK_CRC_AUTO");
-    if (!e) return 0;
-    return !strcmp(e, "wave") ? 1 : !strcmp(e, "rows16") ? 2 : !strcmp(e, "rows8") ? 3 : !strcmp(e, "units") ? 4 : 0;
-  }();
-  return v;
-}
-
-// ---- launchers -------------------------------------------------------------
-// Row width (lanes per span) of the row driver; MCK_CRC_ROW_LANES=4|8|16
-// (A/B), default 16.
-int crc_row_lanes() {
-  static const int v = [] {
-    const char* e = getenv("MCK_CRC_ROW_LANES");
-    const int x = e ? atoi(e) : 16;
-    return x == 4 || x == 8 ? x : 16;
-  }();
-  return v;
-}
-
-template <class Op, int W>
-int launch_crc_rows_w(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
-  int rc = ensure_lds(k_crc_rows<Op, W>, dev);
-  if (rc) return rc;
-  // persistent: one 16-wave workgroup (1024 / W rows) per CU; each
-  // workgroup stages its share's descriptors in LDS, so a batch runs in
-  // launches of at most ncu * kRowDescCache spans
-  const uint32_t per = (uint32_t)ncu * kRowDescCache;
-  constexpr uint32_t rows = 1024 / W;
-  for (uint32_t first = 0; first < count; first += per) {
-    const uint32_t n = std::min(per, count - first);
-    const uint32_t grid = std::min<uint32_t>(ncu, (n + rows - 1) / rows);
-    hipLaunchKernelGGL((k_crc_rows<Op, W>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
-    MCK_HIP(hipGetLastError());
-  }
-  return MCK_OK;
-}
-
-template <class Op>
-int launch_crc_rows(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
-  switch (crc_row_lanes()) {
-    case 4:
-      return launch_crc_rows_w<Op, 4>(op, count, st, dev, ncu);
-    case 8:
-      return launch_crc_rows_w<Op, 8>(op, count, st, dev, ncu);
-    default:
-      return launch_crc_rows_w<Op, 16>(op, count, st, dev, ncu);
-  }
-}
-
-// Span order of k_crc_auto: contiguous ranges per workgroup (default: the
-// cache lines two neighbouring spans share are read once, into one XCD's L2;
-// WAL records 100-1100 B 0.378 -> 0.413 of peak, 512-B spans 0.445 -> 0.509,
-// SST mix CRC image 0.730 -> 0.736, ragged 4 KiB 0.748 -> 0.727) or, with
-// MCK_CRC_ORDER=interleaved, span i on workgroup i mod G (A/B).
-static bool crc_auto_blocked() {
-  static const bool v = [] {
-    const char* e = getenv("MCK_CRC_ORDER");
-    return !e || strcmp(e, "interleaved") != 0;
-  }();
-  return v;
-}
+// from the mean length of its share (crc_auto_units_driver: 8- or 16-lane
+// rows, the unit stream) over contiguous span ranges per workgroup.  Tests
+// force one driver / the interleaved order through mck_test_set_crc_driver
+// (the per-workgroup choice by length means a mixed parity batch might
+// exercise only one); production code never calls it.
+std::atomic<int> g_crc_force{0}, g_crc_interleaved{0};
+int crc_auto_force() { return g_crc_force.load(std::memory_order_relaxed); }
+bool crc_auto_blocked() { return g_crc_interleaved.load(std::memory_order_relaxed) == 0; }
 
 template <class Op>
 int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
-  constexpr bool T = CrcRowT<Op>::value;
+  constexpr bool T = kCrcGenericT;
   const bool blk = crc_auto_blocked();
   int rc = blk ? ensure_lds(k_crc_auto<Op, T, true>, dev) : ensure_lds(k_crc_auto<Op, T>, dev);
   if (rc) return rc;
@@ -285,18 +201,7 @@ int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
   int dev, ncu;
   int rc = current_device(&dev, &ncu);
   if (rc) return rc;
-  const int force = crc_rows_force();
-  if (force == 1) return launch_crc_rows(op, count, st, dev, ncu);
-  if (force < 0) return launch_crc_auto(op, count, st, dev, ncu);
-  // persistent: one 16-wave workgroup per CU (160 KiB of LDS each), with
-  // row-transposed loads (CrcRowT)
-  constexpr bool T = CrcRowT<Op>::value;
-  rc = ensure_lds(k_crc<Op, T>, dev);
-  if (rc) return rc;
-  const uint32_t grid = std::min<uint32_t>(ncu, (count + 15) / 16);
-  hipLaunchKernelGGL((k_crc<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, count);
-  MCK_HIP(hipGetLastError());
-  return MCK_OK;
+  return launch_crc_auto(op, count, st, dev, ncu);
 }
 
 // Uniform batch fast path: geometry precomputed here (crc_uniform_driver).
@@ -318,14 +223,10 @@ int launch_crc_uniform(const Op& op, const mck_spans* sp, hipStream_t st) {
   for (uint32_t b = 0; b < 8 * U.hb; b++) inj = gf_unmulx(inj);
   U.inj = inj;
   const uint32_t grid = std::min<uint32_t>(ncu, (count + 15) / 16);
-  if (U.owner == 0 && U.hb == 0 && crc_tlayout()) {
+  if (U.owner == 0 && U.hb == 0) {  // whole 4 KiB rounds: row-transposed, non-temporal loads
     rc = ensure_lds(k_crc_uniform<Op, true, true>, dev);
     if (rc) return rc;
     hipLaunchKernelGGL((k_crc_uniform<Op, true, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, U, count);
-  } else if (U.owner == 0 && U.hb == 0) {
-    rc = ensure_lds(k_crc_uniform<Op, true>, dev);
-    if (rc) return rc;
-    hipLaunchKernelGGL((k_crc_uniform<Op, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, U, count);
   } else {
     rc = ensure_lds(k_crc_uniform<Op, false>, dev);
     if (rc) return rc;
@@ -344,19 +245,13 @@ bool is_uniform_aligned(const mck_spans* s) {
 // row gets the same work; measured 5495 vs 4849 GiB/s at 1M x 4 KiB),
 // one wave per span for ragged batches (a long span is not serialised on one
 // row and waves balance better: SST verify mix 3287 vs 2752 GiB/s).
-// MCK_XXH3_DRIVER=rows|wave forces one (A/B measurements).
 template <class Op>
 int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform) {
   if (!count) return MCK_OK;
   int ncu;
   int rc = current_device(nullptr, &ncu);
   if (rc) return rc;
-  static const int force = [] {
-    const char* e = getenv("MCK_XXH3_DRIVER");
-    return !e ? 0 : !strcmp(e, "rows") ? 1 : !strcmp(e, "wave") ? 2 : 0;
-  }();
-  const bool wave = force ? force == 2 : !uniform;
-  if (wave) {
+  if (!uniform) {
     // one workgroup per CU, spans dealt by LDS tickets
     const uint32_t wpb = kX3WaveThreads / 64;
     const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + wpb - 1) / wpb);
@@ -472,21 +367,6 @@ template <template <int> class K, class... A>
 int launch_blk(int kind, uint32_t count, hipStream_t st, A... args);
 
 template <int KIND>
-struct BlkLayout {
-  static void go(dim3 g, hipStream_t st, SpanSrc s, uint32_t n, uint64_t* a, uint64_t* b, uint32_t* ri, int32_t* stt) {
-    hipLaunchKernelGGL(k_block_layout<KIND>, g, dim3(256), 0, st, s, n, a, b, ri, stt);
-  }
-};
-// thread-per-block kernels (default) or the wave-per-block LDS kernels
-// (MCK_BLK_WAVE=1, A/B)
-bool blk_wave() {
-  static const bool w = [] {
-    const char* e = getenv("MCK_BLK_WAVE");
-    return e && atoi(e) != 0;
-  }();
-  return w;
-}
-template <int KIND>
 struct BlkLayoutT {
   static void go(dim3, hipStream_t st, SpanSrc s, uint32_t n, uint64_t* a, uint64_t* b, uint32_t* ri, int32_t* stt) {
     hipLaunchKernelGGL(k_block_layout_t<KIND>, dim3((n + 255) / 256), dim3(256), 0, st, s, n, a, b, ri, stt);
@@ -505,17 +385,6 @@ struct BlkKvT {
                          rest...);
   }
 };
-template <int KIND>
-struct BlkKv {
-  template <class... A>
-  static void go(dim3 g, hipStream_t st, bool verify, A... args) {
-    if (verify)
-      hipLaunchKernelGGL((k_block_kv<KIND, true>), g, dim3(256), 0, st, args...);
-    else
-      hipLaunchKernelGGL((k_block_kv<KIND, false>), g, dim3(256), 0, st, args...);
-  }
-};
-
 template <template <int> class K, class... A>
 int launch_blk(int kind, uint32_t count, hipStream_t st, A... args) {
   int ncu;
@@ -574,13 +443,9 @@ int blk_kv(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_
   if (!total_keys || !blocks->count) return MCK_OK;
   const BlkWork w = blk_work(work, total_keys);
   const bool verify = stored != nullptr;
-  if (!blk_wave())
-    return launch_blk<BlkKvT>(kind, blocks->count, st, verify, to_src(blocks), blocks->count, key_base, arena_base,
-                              restart_interval, w.arena, w.koff, w.klen, w.voff, w.vlen, prot_bytes, enc, stored,
-                              mismatch, mismatch_count);
-  return launch_blk<BlkKv>(kind, blocks->count, st, verify, to_src(blocks), blocks->count, key_base, arena_base,
-                           restart_interval, w.arena, w.koff, w.klen, w.voff, w.vlen, prot_bytes, enc, stored,
-                           mismatch, mismatch_count);
+  return launch_blk<BlkKvT>(kind, blocks->count, st, verify, to_src(blocks), blocks->count, key_base, arena_base,
+                            restart_interval, w.arena, w.koff, w.klen, w.voff, w.vlen, prot_bytes, enc, stored,
+                            mismatch, mismatch_count);
 }
 }  // namespace
 }  // namespace mck
@@ -1108,10 +973,7 @@ int mck_block_kv_layout_batch(int kind, const mck_spans* blocks, uint64_t* key_b
     MCK_HIP(hipMemsetAsync(arena_base, 0, 8, st));
     return MCK_OK;
   }
-  if (int rc = blk_wave() ? launch_blk<BlkLayout>(kind, n, st, to_src(blocks), n, key_base, arena_base,
-                                                  restart_interval, status)
-                          : launch_blk<BlkLayoutT>(kind, n, st, to_src(blocks), n, key_base, arena_base,
-                                                   restart_interval, status))
+  if (int rc = launch_blk<BlkLayoutT>(kind, n, st, to_src(blocks), n, key_base, arena_base, restart_interval, status))
     return rc;
   const uint32_t tiles = (uint32_t)blk_tiles(n);
   uint64_t* tsum = static_cast<uint64_t*>(scratch);
@@ -1468,6 +1330,17 @@ int mck_statistics_get(mck_statistics* out, int reset) {
   }
   (void)hipSetDevice(prev);
   return rc;
+}
+
+int mck_test_set_crc_driver(int driver, int interleaved) {
+  t_err[0] = 0;
+  if (driver < 0 || driver > 4) {
+    set_err("driver must be 0..4");
+    return MCK_EINVAL;
+  }
+  g_crc_force.store(driver, std::memory_order_relaxed);
+  g_crc_interleaved.store(interleaved ? 1 : 0, std::memory_order_relaxed);
+  return MCK_OK;
 }
 
 void mck_host_pipeline_release(void) {

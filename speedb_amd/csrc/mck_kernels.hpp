@@ -212,19 +212,6 @@ struct OpCrcBlock {
   }
 };
 
-template <class Op, bool T = false>
-__global__ __launch_bounds__(1024) void k_crc(Op op, uint32_t count) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_spans_driver<Op, T>(op, count, lds, &g_crc_tables);
-}
-
-// one 16-lane row per span (crc_rows_driver): small and mid-size spans
-template <class Op, int W>
-__global__ __launch_bounds__(1024) void k_crc_rows(Op op, uint32_t first, uint32_t count) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_rows_driver<Op, W>(op, first, count, lds, &g_crc_tables);
-}
-
 // ragged batches: driver chosen per workgroup (crc_auto_units_driver)
 template <class Op, bool T, bool BLK = false>
 __global__ __launch_bounds__(1024) void k_crc_auto(Op op, uint32_t first, uint32_t count, int force) {

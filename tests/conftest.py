@@ -21,9 +21,23 @@ ORACLE_DIR = os.path.join(REPO, "oracle")
 GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
+# Child pytest processes of the forced-driver tests set these; the engine
+# itself reads no environment (mck_test_set_crc_driver is its test hook).
+CRC_DRIVERS = {"wave": 1, "rows16": 2, "rows8": 3, "units": 4}
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: long-running")
+    drv = os.environ.get("SPEEDB_AMD_TEST_CRC_DRIVER")
+    order = os.environ.get("SPEEDB_AMD_TEST_CRC_ORDER")
+    if drv or order:
+        import sys
+        if REPO not in sys.path:
+            sys.path.insert(0, REPO)
+        from speedb_amd import _lib
+        _lib.check(_lib.lib.mck_test_set_crc_driver(CRC_DRIVERS.get(drv, 0), 1 if order == "interleaved" else 0),
+                   "mck_test_set_crc_driver")
 
 
 def _bind(lib, prefix):

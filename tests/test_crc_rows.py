@@ -1,11 +1,11 @@
-"""The ragged-batch CRC drivers against the oracle.  By default a ragged
-batch runs on k_crc_auto, which picks per workgroup (from its share's mean
-span length) the row driver with 8- or 16-lane rows (one row per span,
-mck_crc.hpp crc_rows_loop) or the wave driver (crc_drive).  Every driver is
-also forced in a child process over the generic-op parity tests (the A/B
-switches are read once per process): MCK_CRC_AUTO=wave|rows16|rows8 inside
-the auto kernel, MCK_CRC_ROWS=1 (+ MCK_CRC_ROW_LANES) for the standalone row
-kernel, MCK_CRC_ROWS=0 for the standalone wave kernel with its static feed."""
+"""The ragged-batch CRC drivers against the oracle.  A ragged batch runs on
+k_crc_auto, which picks per workgroup (from its share's mean span length)
+8- or 16-lane rows (one row per span, mck_crc.hpp crc_rows_loop) or the unit
+stream (mck_crc_units.hpp).  Every driver -- and the round-2 wave driver
+still reachable through the test hook -- is also forced for every workgroup
+in a child process over the generic-op parity tests
+(mck_test_set_crc_driver, set by tests/conftest.py from
+SPEEDB_AMD_TEST_CRC_DRIVER / _ORDER)."""
 import os
 import random
 import subprocess
@@ -51,73 +51,32 @@ def test_wal_record_crc_small_ragged_many(gpu, oracle):
         assert int(got[k]) == oracle.WalRecordCrc(t, host[o:o + n], t >= 5, 0xC0FFEE), (k, n, t)
 
 
-def test_generic_ops_through_rows_subprocess(gpu):
-    """CRC value/extend/mask, SST trailer + verify (context checksums,
-    corruption), blob records and WAL paths with MCK_CRC_ROWS=1."""
-    if os.environ.get("MCK_CRC_ROWS") or os.environ.get("MCK_CRC_AUTO"):
-        pytest.skip("already running a forced driver")
-    env = dict(os.environ, MCK_CRC_ROWS="1")
-    tests = [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
-        "test_crc32c_batch_ragged", "test_crc32c_known_answers_on_device", "test_scalar_shims",
-        "test_checksum_schemas_on_device", "test_builtin_checksum_batch", "test_sst_trailer_and_verify",
-        "test_wal_record_crc_batch", "test_wal_verify_batch", "test_empty_and_zero_inputs",
-        "test_large_ragged_batches_static_and_dynamic_feeds", "test_crc32c_long_vs_oracle",
-        "test_sst_verify_large_static_feed")]
-    tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_sst_file.py")]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider"] + tests,
-                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-    assert " passed" in r.stdout
-
-
-def test_wave_driver_for_wal_subprocess(gpu):
-    """And the standalone wave kernel (MCK_CRC_ROWS=0) on the WAL records and
-    the WAL writer."""
-    if os.environ.get("MCK_CRC_ROWS") or os.environ.get("MCK_CRC_AUTO"):
-        pytest.skip("already running a forced driver")
-    env = dict(os.environ, MCK_CRC_ROWS="0")
-    tests = [os.path.join(HERE, "test_wal_writer.py"),
-             os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
-                        "-k", "not subprocess"] + tests,
-                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-
-
-@pytest.mark.parametrize("lanes", ["4", "8"])
-def test_row_widths_subprocess(gpu, lanes):
-    """The standalone row kernel's 4- and 8-lane variants (MCK_CRC_ROW_LANES)
-    on the small-span test and the generic ops."""
-    if os.environ.get("MCK_CRC_ROW_LANES") or os.environ.get("MCK_CRC_AUTO"):
-        pytest.skip("already running a forced width")
-    env = dict(os.environ, MCK_CRC_ROWS="1", MCK_CRC_ROW_LANES=lanes)
-    tests = [os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
-    tests += [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
-        "test_crc32c_batch_ragged", "test_sst_trailer_and_verify", "test_empty_and_zero_inputs",
-        "test_large_ragged_batches_static_and_dynamic_feeds", "test_wal_record_crc_batch")]
-    tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_wal_writer.py")]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
-                        "-k", "not subprocess"] + tests,
-                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
-
-
-@pytest.mark.parametrize("mode", ["wave", "rows16", "rows8", "interleaved"])
-def test_auto_kernel_forced_drivers_subprocess(gpu, mode):
-    """k_crc_auto with each driver forced (its per-workgroup choice is by
-    mean length, so a parity test of mixed lengths may exercise only one),
-    and with the interleaved span order instead of contiguous ranges."""
-    if os.environ.get("MCK_CRC_AUTO") or os.environ.get("MCK_CRC_ROWS") or os.environ.get("MCK_CRC_ORDER"):
-        pytest.skip("already running a forced driver")
-    env = dict(os.environ, MCK_CRC_ORDER="interleaved") if mode == "interleaved" else dict(os.environ, MCK_CRC_AUTO=mode)
+def _forced(env):
+    """Run the generic CRC parity tests in a child pytest whose conftest sets
+    the engine's test hook (mck_test_set_crc_driver) from env."""
     tests = [os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
     tests += [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
         "test_crc32c_batch_ragged", "test_sst_trailer_and_verify", "test_empty_and_zero_inputs",
         "test_large_ragged_batches_static_and_dynamic_feeds", "test_wal_record_crc_batch",
-        "test_crc32c_known_answers_on_device", "test_builtin_checksum_batch", "test_sst_verify_large_static_feed")]
-    tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_wal_writer.py"),
-              os.path.join(HERE, "test_sst_file.py")]
+        "test_crc32c_known_answers_on_device", "test_builtin_checksum_batch", "test_sst_verify_large_static_feed",
+        "test_checksum_schemas_on_device", "test_scalar_shims", "test_crc32c_long_vs_oracle")]
+    tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_sst_file.py"),
+              os.path.join(HERE, "test_crc_units.py")]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
                         "-k", "not subprocess"] + tests,
-                       env=env, cwd=os.path.dirname(HERE), capture_output=True, text=True, timeout=600)
+                       env=dict(os.environ, **env), cwd=os.path.dirname(HERE), capture_output=True, text=True,
+                       timeout=900)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout
+
+
+@pytest.mark.parametrize("mode", ["wave", "rows16", "rows8", "units", "interleaved"])
+def test_auto_kernel_forced_drivers_subprocess(gpu, mode):
+    """k_crc_auto with each driver forced for every workgroup (its choice is
+    by mean length, so a parity test of mixed lengths may exercise only one):
+    short spans, 0-byte spans, WAL / blob / SST ops on every driver; and the
+    interleaved span order instead of contiguous ranges."""
+    if os.environ.get("SPEEDB_AMD_TEST_CRC_DRIVER") or os.environ.get("SPEEDB_AMD_TEST_CRC_ORDER"):
+        pytest.skip("already running a forced driver")
+    _forced({"SPEEDB_AMD_TEST_CRC_ORDER": "interleaved"} if mode == "interleaved"
+            else {"SPEEDB_AMD_TEST_CRC_DRIVER": mode})

@@ -8,13 +8,12 @@ cases below are the shapes that stress it: SST data blocks (4096 + 0..255
 bytes + the type byte, never 16-aligned), uniform non-aligned strides,
 every span length around the unit / piece / split boundaries, long spans
 (many pieces per span, pieces of one span finishing on different waves),
-empty spans inside a long-span batch, non-zero Extend inits, and an
-interleaved + forced-driver run in a child process.  Bit-exact throughout."""
-import os
+empty spans inside a long-span batch, non-zero Extend inits.  The unit
+stream forced on every generic CRC test (short spans, WAL, blob) and these
+tests with the interleaved span order: test_crc_rows.py
+test_auto_kernel_forced_drivers_subprocess.  Bit-exact throughout."""
 import random
 import struct
-import subprocess
-import sys
 
 import numpy as np
 import pytest
@@ -22,7 +21,6 @@ import pytest
 from formats import splitmix_bytes, sst_blocks
 
 pytestmark = pytest.mark.gpu
-HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _u32(t):
@@ -183,23 +181,3 @@ def test_units_sst_verify_mix(gpu, oracle, ctype):
     assert int(cnt.item()) == len(bad)
 
 
-@pytest.mark.parametrize("env", [{"MCK_CRC_AUTO": "units"}, {"MCK_CRC_ORDER": "interleaved"}])
-def test_units_forced_and_interleaved_subprocess(gpu, env):
-    """Every generic CRC parity test with the unit stream forced for every
-    workgroup (short spans, 0-byte spans, WAL and blob ops included), and the
-    unit tests above with the interleaved span order."""
-    if any(os.environ.get(k) for k in ("MCK_CRC_AUTO", "MCK_CRC_ROWS", "MCK_CRC_ORDER")):
-        pytest.skip("already running a forced driver")
-    tests = [os.path.join(HERE, "test_gpu_parity.py") + "::" + t for t in (
-        "test_crc32c_batch_ragged", "test_sst_trailer_and_verify", "test_empty_and_zero_inputs",
-        "test_large_ragged_batches_static_and_dynamic_feeds", "test_wal_record_crc_batch",
-        "test_crc32c_known_answers_on_device", "test_builtin_checksum_batch", "test_sst_verify_large_static_feed",
-        "test_checksum_schemas_on_device", "test_crc32c_long_vs_oracle")]
-    tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_sst_file.py"),
-              os.path.join(HERE, "test_crc_units.py"),
-              os.path.join(HERE, "test_crc_rows.py") + "::test_wal_record_crc_small_ragged_many"]
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
-                        "-k", "not subprocess"] + tests,
-                       env=dict(os.environ, **env), cwd=os.path.dirname(HERE), capture_output=True, text=True,
-                       timeout=900)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
