@@ -104,10 +104,9 @@ def parse():
                             "walrec", "ragged", "latency"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
     p.add_argument("--block-bytes", type=int, default=4096)
-    p.add_argument("--sst-bytes", type=int, default=4 << 30,
-                   help="per SST image (sst); 2 images.  Each launch pays ~25 us of fixed cost (mostly "
-                        "the last 64 KiB spans' 16 sequential rounds, DESIGN.md 5): 1 GiB images read 0.66 "
-                        "of peak, 4 GiB 0.73")
+    p.add_argument("--sst-bytes", type=int, default=1 << 30,
+                   help="per SST image (sst); 2 images, ~2 GiB per step as BASELINE.md states.  One image "
+                        "is one SST file's VerifyChecksumInBlocks batch: 64/256 MiB points in DESIGN.md 5")
     p.add_argument("--sst-types", choices=["both", "crc32c", "xxh3"], default="both",
                    help="sst: verify both images (configs[2]) or one (per-kernel measurement)")
     p.add_argument("--wal-blocks", type=int, default=10_000_000,
