@@ -10,7 +10,8 @@ Default workload (the headline, BASELINE.json configs[1]): CRC32C over
   sst      configs[2]  compaction-shaped 4/16/64 KiB (+0..255 B) SST blocks
                        with 5-byte trailers, format_version 6 context
                        checksums; VerifyBlockChecksum of every block, one
-                       kCRC32c image and one kXXH3 image (4 GiB each) per step
+                       kCRC32c image and one kXXH3 image (1 GiB each: ~2 GiB
+                       per step) per step
   wal      configs[3]  WAL replay: a fixed global batch of 10M x 32 KiB blocks
                        (one kFullType record each) partitioned over the ranks
                        (strong scaling), ReadPhysicalRecord CRC verify of
@@ -129,7 +130,7 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="0 = the CPUs this process may use (cgroup quota / affinity)")
     p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--crc-driver", choices=["auto", "wave", "rows16", "rows8", "units"], default="auto",
+    p.add_argument("--crc-driver", choices=["auto", "wave", "rows16", "rows8", "units", "rows4"], default="auto",
                    help="force the ragged CRC driver for every workgroup (A/B measurements; the engine's "
                         "test hook mck_test_set_crc_driver)")
     p.add_argument("--crc-order", choices=["blocked", "interleaved"], default="blocked",
@@ -599,7 +600,7 @@ def make_workload(args, dev, rank, world):
                                                     rint.data_ptr(), nkeys, work.data_ptr(), out.data_ptr(), stream.cuda_stream),
                        "mck_block_kv_protect_batch")
         w.step = step
-        w.kernel = "k_block_layout + scans + k_block_kv (whole step, incl. the totals readback)"
+        w.kernel = "k_block_layout_t + scans + k_block_kv_t + k_block_long (whole step, incl. the totals readback)"
         w.span_bytes = db.block_bytes
         # what the step must move: every block read once, the kv_checksum
         # array written (+ 8 B offset, 4 B length per block in, 8 B key base
@@ -856,7 +857,7 @@ def main():
 
     from speedb_amd import _lib, shard
     if args.crc_driver != "auto" or args.crc_order != "blocked":
-        drv = {"auto": 0, "wave": 1, "rows16": 2, "rows8": 3, "units": 4}[args.crc_driver]
+        drv = {"auto": 0, "wave": 1, "rows16": 2, "rows8": 3, "units": 4, "rows4": 5}[args.crc_driver]
         _lib.check(_lib.lib.mck_test_set_crc_driver(drv, 1 if args.crc_order == "interleaved" else 0),
                    "mck_test_set_crc_driver")
     w = make_workload(args, dev, rank, world)

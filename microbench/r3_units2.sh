@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-r3u2}
 mkdir -p $O
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_crc_units.py tests/test_gpu_parity.py -k "units or xxh3 or large_ragged or sst" > $O/units_tests.log 2>&1 || { tail -30 $O/units_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_crc_units.py tests/test_block_protection.py tests/test_gpu_parity.py -k "units or xxh3 or large_ragged or sst or block or xxph3" > $O/units_tests.log 2>&1 || { tail -30 $O/units_tests.log; exit 1; }
 tail -2 $O/units_tests.log
 B="timeout -k 10 180 python -u bench.py --steps 20 --warmup 20 --cpu-seconds 0"
 for d in units wave; do
@@ -17,6 +17,8 @@ for d in units wave; do
 done
 $B --workload sst --sst-types xxh3 --sst-bytes $((1<<30)) > $O/sst1g_x3.json || exit 1
 $B --workload sst --sst-bytes $((1<<30)) > $O/sst1g_both.json || exit 1
+$B --workload blockkv --kv-value-bytes 1000 > $O/blk1000.json || exit 1
+$B --workload blockkv --kv-value-bytes 100 > $O/blk100.json || exit 1
 for f in $O/*.json; do echo "$f $(python3 -c "import json,sys; d=json.load(open('$f')); print(d['value'], d['roofline']['frac'], d['roofline']['kernel_avg_ms'], d['verified'])")"; done
 for d in units wave; do
   timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-trace -d $O/pmc_$d -o pmc --output-format csv -- python3 bench.py --crc-driver $d --workload crc32c --block-bytes 4300 --blocks 1000000 --steps 2 --warmup 1 --settle-ms 0 --no-verify --cpu-seconds 0 > $O/pmc_$d.txt 2>&1 || { tail -5 $O/pmc_$d.txt; exit 1; }

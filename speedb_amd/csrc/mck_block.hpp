@@ -5,29 +5,25 @@
 // A block is prefix-compressed: an entry's key is the previous key's first
 // `shared` bytes plus its own `non_shared` bytes, and only restart points
 // (every block_restart_interval-th entry, shared == 0) start from nothing.
-// The restart array therefore cuts a block into independent intervals.
-// One wave per block, the block staged in LDS (blocks up to kBlkSlot bytes;
-// larger ones are read in place), two passes:
+// One THREAD per block walks it in order, as the reference's
+// SeekToFirst/Next loop does (64 blocks per wave keep every lane busy and
+// the dependent header reads of thousands of blocks in flight), in passes:
 //
-//   k_block_layout  lane r walks restart interval r (r += 64): entry count,
-//                   reassembled key bytes, first error; per block the key
-//                   count, key bytes, restart interval and status; the
-//                   exclusive scans (k_blk_scan_*) give each block its key
-//                   index base and key-arena base
-//   k_block_kv      lane r walks interval r again, reassembling every key
-//                   into the wave's LDS key area and writing an entry
-//                   descriptor; then lane e hashes entry e:
-//                   ProtectKV(key, value).Encode(prot_bytes), values over
-//                   240 B by the whole wave (XXPH3 long loop, 8 accumulators
-//                   x 8 stripe groups)
+//   k_block_layout_t  entry count, reassembled key bytes, restart interval
+//                     and status per block; the exclusive scans
+//                     (k_blk_scan_*) give each block its key index base and
+//                     key-arena base
+//   k_block_kv_t      walks again, reassembling every key in a per-thread
+//                     LDS buffer: ProtectKV(key, value).Encode(prot_bytes)
+//                     for every entry, values over 240 B left to
+//   k_block_long      the long-value list in key order, XXPH3 by 16-lane
+//                     rows (mck_kernels.hpp OpBlkLong)
 //
 // Entry k of a block lands at key index key_base[block] + k, in the order the
 // reference's SeekToFirst/Next loop generates them (:1116-1123).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-
-#include <type_traits>
 
 namespace mck {
 
@@ -187,54 +183,6 @@ __device__ __forceinline__ bool rd_entry_pre(const R& r, uint32_t p, uint32_t li
   return rd_entry<KIND>(r, p, lim, sh, ns, q, v, vl);
 }
 
-// Walk of one restart interval [start, end): entry count, reassembled key
-// bytes and the first error, as code (r << 2 | stage): stage 0 bad entry,
-// 1 shared != 0 at a restart point past the first (the reference would reuse
-// the previous interval's key; BlockBuilder never writes it), 2 an entry
-// running over the next restart point.  ~0 = no error.
-struct BlkWalk {
-  uint32_t cnt;
-  uint64_t kbytes;
-  uint64_t err;
-};
-template <int KIND, class R>
-__device__ __forceinline__ BlkWalk blk_walk(const R& rd, uint32_t ro, uint32_t r, uint32_t start, uint32_t end) {
-  BlkWalk w{0, 0, ~0ull};
-  uint32_t p = start, kl = 0;
-  while (p < end) {
-    uint32_t sh, ns, q, v, vl;
-    if (!rd_entry_fast<KIND>(rd, p, ro, &sh, &ns, &q, &v, &vl)) {
-      w.err = (uint64_t)r << 2;
-      return w;
-    }
-    if (w.cnt == 0 && sh != 0) {
-      w.err = ((uint64_t)r << 2) | (r ? 1u : 0u);
-      return w;
-    }
-    if (kl < sh) {
-      w.err = (uint64_t)r << 2;
-      return w;
-    }
-    kl = sh + ns;
-    w.kbytes += kl;
-    w.cnt++;
-    p = v + vl;
-  }
-  if (p != end) w.err = ((uint64_t)r << 2) | 2u;
-  return w;
-}
-
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v) {
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
-  for (int o = 32; o >= 1; o >>= 1) {
-    const uint64_t u = __shfl_xor(v, o, 64);
-    v = u < v ? u : v;
-  }
-  return v;
-}
 // inclusive scan across the wave
 __device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v, uint32_t lane) {
   for (int o = 1; o < 64; o <<= 1) {
@@ -251,15 +199,10 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// LDS per wave: the staged block, and (k_block_kv) the reassembled keys and
-// the entry descriptors.  Blocks larger than the slot, or with more entries /
-// key bytes than the areas hold, take the same code over global memory
-// (the block in place, keys in the caller's arena, descriptors in the work
-// arrays).
-constexpr uint32_t kBlkSlot = 6144;                           // block bytes staged
+// A wave's LDS slot for a staged span (k_dbg_xp: the wave-cooperative long
+// loop over an LDS copy).
+constexpr uint32_t kBlkSlot = 6144;                           // bytes staged
 constexpr uint32_t kBlkSlotWords = (kBlkSlot + 16 + 16 + 16) / 4;  // + head, tail chunk, pad
-constexpr uint32_t kBlkKeyArea = 2048, kBlkKeyWords = (kBlkKeyArea + 16) / 4;
-constexpr uint32_t kBlkMaxDesc = 256;
 
 // Copy the block into the wave's slot; returns the LdsRd over it.
 __device__ __forceinline__ LdsRd blk_stage(const uint8_t* g, uint32_t n, uint32_t* slot, uint32_t lane) {
@@ -307,97 +250,6 @@ __device__ __forceinline__ BlkHdr rd_header(const R& r, uint64_t n64) {
   }
   h.ok = nr == 0 || size >= 8;
   return h;
-}
-
-template <class R>
-__device__ __forceinline__ bool rd_restarts_ok(const R& rd, const BlkHdr& h, uint32_t lane) {
-  bool bad = false;
-  for (uint32_t r = lane; r < h.nr; r += 64) {
-    const uint32_t x = rd.u32(h.ro + 4 * r);
-    if (r == 0)
-      bad |= h.ro != 0 && x != 0;
-    else
-      bad |= x <= rd.u32(h.ro + 4 * (r - 1)) || x >= h.ro;
-  }
-  return !__any(bad);
-}
-
-// Pass 1 body for one block
-template <int KIND, class R>
-__device__ __forceinline__ void blk_layout_one(const R& rd, uint64_t n, uint32_t lane, int* st_out, uint64_t* keys_out,
-                                               uint64_t* kb_out, uint32_t* ri_out) {
-  const BlkHdr h = rd_header(rd, n);
-  int st = kBlkOk;
-  uint64_t keys = 0, kb = 0;
-  uint32_t ri = 0;
-  if (!h.ok) {
-    st = kBlkBadContents;
-  } else if (h.nr == 0) {
-    // empty block: protection stays off, no keys
-  } else if (!rd_restarts_ok(rd, h, lane)) {
-    st = kBlkBadRestarts;
-  } else if (h.ro == 0) {
-    st = h.nr == 1 ? kBlkOk : kBlkBadRestarts;
-  } else {
-    uint64_t err = ~0ull;
-    uint32_t first_cnt = 0;
-    for (uint32_t r0 = 0; r0 < h.nr; r0 += 64) {
-      const uint32_t r = r0 + lane;
-      BlkWalk w{0, 0, ~0ull};
-      if (r < h.nr)
-        w = blk_walk<KIND>(rd, h.ro, r, rd.u32(h.ro + 4 * r), r + 1 < h.nr ? rd.u32(h.ro + 4 * (r + 1)) : h.ro);
-      if (r0 == 0) first_cnt = readlane_u32(w.cnt, 0);
-      // every interval but the last holds interval-0's count (GetRestartInterval)
-      if (r < h.nr && w.err == ~0ull && r + 1 < h.nr && w.cnt != first_cnt) w.err = ((uint64_t)r << 2) | 2u;
-      err = err < w.err ? err : w.err;
-      keys += w.cnt;
-      kb += w.kbytes;
-    }
-    err = wave_min_u64(err);
-    keys = wave_sum_u64(keys);
-    kb = wave_sum_u64(kb);
-    if (err != ~0ull)
-      st = (err & 3) == 0 ? kBlkBadEntry : kBlkBadRestarts;
-    else
-      ri = h.nr > 1 ? first_cnt : 0;
-  }
-  if (st != kBlkOk) keys = kb = ri = 0;
-  *st_out = st;
-  *keys_out = keys;
-  *kb_out = kb;
-  *ri_out = ri;
-}
-
-// Pass 1: per block key count / key bytes / status / restart interval.
-// key_cnt and key_bytes receive the per-block values in place; the scan
-// kernels turn them into exclusive offsets.
-template <int KIND>
-__global__ __launch_bounds__(256) void k_block_layout(SpanSrc blocks, uint32_t count, uint64_t* key_cnt,
-                                                      uint64_t* key_bytes, uint32_t* interval_out,
-                                                      int32_t* status) {
-  __shared__ uint32_t s_slot[4][kBlkSlotWords];
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + wv; b < count; b += nw) {
-    const uint8_t* d = blocks.ptr(b);
-    const uint64_t n = blocks.len(b);
-    int st;
-    uint64_t keys, kb;
-    uint32_t ri;
-    if (n <= kBlkSlot) {
-      const LdsRd rd = blk_stage(d, (uint32_t)n, s_slot[wv], lane);
-      blk_layout_one<KIND>(rd, n, lane, &st, &keys, &kb, &ri);
-    } else {
-      blk_layout_one<KIND>(GblRd{d}, n, lane, &st, &keys, &kb, &ri);
-    }
-    if (lane == 0) {
-      key_cnt[b] = keys;
-      key_bytes[b] = kb;
-      interval_out[b] = ri;
-      status[b] = st;
-    }
-    wave_lds_sync();  // the slot is rewritten for the next block
-  }
 }
 
 // ---- XXPH3 over a reader (util/xxph3.h; see xxph3_short / xxph3_long_lane) --
@@ -680,186 +532,14 @@ __device__ __forceinline__ uint64_t xp_row_long(const R& r, uint32_t o, uint32_t
   return xxph3_avalanche((uint64_t)len * P64_1 + t0);
 }
 
-// Pass 2 for one block.  Lane r walks restart interval r, writing one
-// descriptor per entry {shared, non_shared, key delta offset, value length}
-// at its entry index (r * restart_interval + k).  Then lane e takes entry e:
-// its key is reassembled into the key area -- the delta, then the shared
-// prefix from the preceding entries' deltas (walking back while shared
-// shrinks: byte i of key e is byte i - shared_j of the last delta j <= e with
-// shared_j <= i), so keys are built in parallel, not in walk order -- and
-// ProtectKV(key, value) is hashed (values over 240 B by the whole wave).
-// FAST: block, descriptors and keys in LDS.  Otherwise global memory: the
-// block in place, descriptors in the work arrays at k0 (koff = delta offset,
-// klen = shared, voff = non_shared, vlen = value length), keys in the block's
-// arena share.
-template <int KIND, bool VERIFY, bool FAST>
-__device__ __forceinline__ void blk_kv_one(const uint8_t* d, uint64_t n, uint32_t ri, uint64_t k0, uint64_t nk,
-                                           uint32_t* slot, uint8_t* lkeys, uint16_t* ldesc, uint8_t* gkeys,
-                                           uint64_t* gko, uint32_t* gkl, uint64_t* gvo, uint32_t* gvl,
-                                           uint32_t prot_bytes, uint8_t* enc, const uint8_t* stored,
-                                           uint8_t* mismatch, uint32_t* mismatch_count, const XpWaveSec& ws,
-                                           uint32_t lane) {
-  typedef typename std::conditional<FAST, LdsRd, GblRd>::type Rd;
-  Rd rd;
-  if constexpr (FAST)
-    rd = blk_stage(d, (uint32_t)n, slot, lane);
-  else
-    rd = GblRd{d};
-  uint8_t* keys = FAST ? lkeys : gkeys;
-  auto put = [&](uint64_t e, uint32_t sh, uint32_t ns, uint32_t q, uint32_t vl) {
-    if constexpr (FAST) {
-      ldesc[4 * e] = (uint16_t)sh;
-      ldesc[4 * e + 1] = (uint16_t)ns;
-      ldesc[4 * e + 2] = (uint16_t)q;
-      ldesc[4 * e + 3] = (uint16_t)vl;
-    } else {
-      gko[k0 + e] = q;
-      gkl[k0 + e] = sh;
-      gvo[k0 + e] = ns;
-      gvl[k0 + e] = vl;
-    }
-  };
-  auto get_sh = [&](uint64_t e) -> uint32_t {
-    if constexpr (FAST)
-      return ldesc[4 * e];
-    else
-      return gkl[k0 + e];
-  };
-  auto get_q = [&](uint64_t e) -> uint32_t {
-    if constexpr (FAST)
-      return ldesc[4 * e + 2];
-    else
-      return (uint32_t)gko[k0 + e];
-  };
-  const BlkHdr h = rd_header(rd, n);
-  for (uint32_t r = lane; r < h.nr; r += 64) {
-    uint32_t p = rd.u32(h.ro + 4 * r);
-    const uint32_t end = r + 1 < h.nr ? rd.u32(h.ro + 4 * (r + 1)) : h.ro;
-    uint64_t e = (uint64_t)r * ri;
-    while (p < end) {
-      uint32_t sh, ns, q, v, vl;
-      rd_entry_fast<KIND>(rd, p, h.ro, &sh, &ns, &q, &v, &vl);
-      put(e++, sh, ns, q, vl);
-      p = v + vl;
-    }
-  }
-  if constexpr (!FAST) __threadfence_block();
-  wave_lds_sync();
-  typedef typename std::conditional<FAST, LdsRd, GblRd>::type Kr;
-  Kr kr;
-  if constexpr (FAST)
-    kr = LdsRd{reinterpret_cast<const uint32_t*>(lkeys), 0};
-  else
-    kr = GblRd{gkeys};
-  uint32_t carry = 0;
-  for (uint64_t e0 = 0; e0 < nk; e0 += 64) {
-    const uint64_t e = e0 + lane;
-    const bool own = e < nk;
-    uint32_t sh = 0, ns = 0, q = 0, vl = 0;
-    if (own) {
-      if constexpr (FAST) {
-        sh = ldesc[4 * e];
-        ns = ldesc[4 * e + 1];
-        q = ldesc[4 * e + 2];
-        vl = ldesc[4 * e + 3];
-      } else {
-        q = (uint32_t)gko[k0 + e];
-        sh = gkl[k0 + e];
-        ns = (uint32_t)gvo[k0 + e];
-        vl = gvl[k0 + e];
-      }
-    }
-    const uint32_t kl = sh + ns;
-    const uint32_t incl = (uint32_t)wave_incl_scan_u64(kl, lane);
-    const uint32_t ko = carry + incl - kl;
-    carry += readlane_u32(incl, 63);
-    uint64_t hv = 0;
-    if (own) {
-      for (uint32_t i = 0; i < ns; i++) keys[ko + sh + i] = (uint8_t)rd.u8(q + i);
-      uint32_t lo = sh;
-      for (uint64_t j = e; lo > 0;) {
-        j--;
-        const uint32_t sj = get_sh(j);
-        if (sj < lo) {
-          const uint32_t qj = get_q(j);
-          for (uint32_t i = sj; i < lo; i++) keys[ko + i] = (uint8_t)rd.u8(qj + i - sj);
-          lo = sj;
-        }
-      }
-      if constexpr (!FAST) __threadfence_block();
-      hv = kl <= 240 ? xp_short(kr, ko, kl, kSeedK) : xp_lane(kr, ko, kl, kSeedK);
-      if (vl <= 240) hv ^= xp_short(rd, q + ns, vl, kSeedV);
-    }
-    uint64_t longs = __ballot(own && vl > 240);
-    while (longs) {
-      const uint32_t j = (uint32_t)__builtin_ctzll(longs);
-      longs &= longs - 1;
-      const uint64_t h2 = xp_wave_long(rd, readlane_u32(q + ns, j), readlane_u32(vl, j), ws, lane);
-      if (lane == j) hv ^= h2;
-    }
-    if (own) {
-      const uint64_t k = k0 + e;
-      if constexpr (!VERIFY) {
-        if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0))
-          reinterpret_cast<uint64_t*>(enc)[k] = hv;
-        else
-          for (uint32_t b = 0; b < prot_bytes; b++) enc[k * prot_bytes + b] = (uint8_t)(hv >> (8 * b));
-      } else {
-        uint64_t sv = 0;
-        for (uint32_t b = 0; b < prot_bytes; b++) sv |= (uint64_t)blk_u8(stored + k * prot_bytes + b) << (8 * b);
-        const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
-        const bool bad = sv != (hv & keep);
-        mismatch[k] = bad;
-        if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
-      }
-    }
-  }
-  wave_lds_sync();  // LDS areas are rewritten for the next block
-}
-
-// Pass 2 kernel: one wave per block.  key_base / arena_base: exclusive scans
-// from pass 1; restart_interval from pass 1.
-template <int KIND, bool VERIFY>
-__global__ __launch_bounds__(256) void k_block_kv(SpanSrc blocks, uint32_t count, const uint64_t* key_base,
-                                                  const uint64_t* arena_base, const uint32_t* restart_interval,
-                                                  uint8_t* arena, uint64_t* gko, uint32_t* gkl, uint64_t* gvo,
-                                                  uint32_t* gvl, uint32_t prot_bytes, uint8_t* enc,
-                                                  const uint8_t* stored, uint8_t* mismatch,
-                                                  uint32_t* mismatch_count) {
-  __shared__ uint32_t s_slot[4][kBlkSlotWords];
-  __shared__ uint32_t s_keys[4][kBlkKeyWords];
-  __shared__ uint16_t s_desc[4][4 * kBlkMaxDesc];
-  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const uint32_t nw = gridDim.x * (blockDim.x >> 6);
-  const XpWaveSec ws = xp_wave_sec(lane, kSeedV);
-  for (uint32_t b = blockIdx.x * (blockDim.x >> 6) + wv; b < count; b += nw) {
-    const uint64_t k0 = ldg_u64(key_base, b);
-    const uint64_t nk = ldg_u64(key_base, b + 1) - k0;
-    if (!nk) continue;  // no keys (or a bad block)
-    const uint64_t a0 = ldg_u64(arena_base, b);
-    const uint64_t kb = ldg_u64(arena_base, b + 1) - a0;
-    const uint8_t* d = blocks.ptr(b);
-    const uint64_t n = blocks.len(b);
-    const uint32_t ri = ldg_u32(restart_interval, b);
-    uint8_t* lk = reinterpret_cast<uint8_t*>(s_keys[wv]);
-    if (n <= kBlkSlot && nk <= kBlkMaxDesc && kb <= kBlkKeyArea)
-      blk_kv_one<KIND, VERIFY, true>(d, n, ri, k0, nk, s_slot[wv], lk, s_desc[wv], nullptr, nullptr, nullptr,
-                                     nullptr, nullptr, prot_bytes, enc, stored, mismatch, mismatch_count, ws, lane);
-    else
-      blk_kv_one<KIND, VERIFY, false>(d, n, ri, k0, nk, nullptr, nullptr, nullptr, arena + a0, gko, gkl, gvo, gvl,
-                                      prot_bytes, enc, stored, mismatch, mismatch_count, ws, lane);
-  }
-}
-
-// ---- one THREAD per block (default) ------------------------------------------
-// The wave-per-block kernels above keep one lane per restart interval busy --
-// 3 of 64 lanes for a 4 KiB block of 100-byte values -- so their cost is
-// ~1000 (layout) / ~3500 (kv) VALU instructions per block issued for a few
-// lanes (SQ counters, profiles/r2b/blockkv).  Here each lane owns a whole
+// ---- one THREAD per block ----------------------------------------------------
+// Each lane owns a whole
 // block and walks it in order, exactly as the reference's SeekToFirst/Next
 // loop does; 64 blocks per wave keep every lane busy and the
 // dependent header reads of thousands of blocks in flight hide the memory
-// latency.  MCK_BLK_WAVE=1 selects the wave kernels (A/B).
+// latency.  (Round 2 measured one wave per block, one lane per restart
+// interval: ~1000 (layout) / ~3500 (kv) VALU instructions per block issued
+// for a few lanes -- removed.)
 
 // Sequential walk of one block (block.cc:1091-1132 with the restart checks
 // of the layout pass); on_entry(idx, key_len, shared, delta_off, value_off,
@@ -935,39 +615,32 @@ __global__ __launch_bounds__(256) void k_block_layout_t(SpanSrc blocks, uint32_t
 // the buffer; the value is hashed in place.  A key longer than the buffer
 // moves the thread to its block's arena share (global, same in-place rule).
 constexpr uint32_t kBlkKeyBuf = 128;  // bytes of LDS key buffer per thread
-// The lanes step through their blocks' entries together (one entry per lane
-// per iteration); values of kBlkWaveLong bytes or more are not hashed per lane -- 8-byte loads
-// from 64 different blocks per instruction, far from coalesced -- but four
-// at a time, one per 16-lane row (xp_row_long: each load instruction reads
-// 128 contiguous bytes of each of four values).  -DMCK_BLK_LANE_LONG=1: per
-// lane; -DMCK_BLK_LONG_MIN=n: the threshold (A/B).
-// Measured (1M blocks, ms per step): whole-wave hashing one value at a time
-// lost to per lane below 512 B (300-B values 5.69 vs 4.37); one value per
-// 16-lane row, four at a time (xp_row_long), wins everywhere: 1000-B values
-// 2.01 (wave 2.41, lane 2.70), 500-B 2.68 (lane 3.36), 300-B 3.41 (lane
-// 4.05) -- so every value over 240 B goes to the rows.
-#ifndef MCK_BLK_LANE_LONG
-#define MCK_BLK_LANE_LONG 0
-#endif
-#ifndef MCK_BLK_LONG_MIN
-#define MCK_BLK_LONG_MIN 241
-#endif
-constexpr uint32_t kBlkWaveLong = MCK_BLK_LONG_MIN;
-// 17..128-byte values: MCK_BLK_FLAT_MID=2 (default) by lane octets
-// (xp_mid_octets), 1 per lane with batched loads (xp_mid_load), 0 through
-// xp_short (A/B)
-#ifndef MCK_BLK_FLAT_MID
-#define MCK_BLK_FLAT_MID 2
-#endif
+// Values of more than 240 bytes (XXPH3's long loop) are not hashed by the
+// walk (round 3): a lane's long value would be read with 8-byte loads from
+// 64 different blocks per instruction, or, four at a time by 16-lane rows
+// (round 2), serialise the bandwidth-bound hashing behind the latency-bound
+// walk in one wave.  The walk writes the entry's hash WITHOUT the value's
+// (ProtectKV XORs the per-field hashes, and the Encode truncation commutes
+// with XOR) and records the value in a LONG-VALUE LIST indexed by the key
+// index k -- so the list is in memory order (keys follow blocks, entries
+// follow each other) and needs no scan: long_len[k] = value length (0: no
+// long value; the host zeroes the array), long_off[k] = value address,
+// and, to verify, long_part[k] = the partial hash.  k_block_long then
+// sweeps the key range front to back with the XXPH3 row driver (one value
+// per 16-lane row, 16-byte loads), XORs the value hash into enc[k] (protect)
+// or compares partial ^ value hash with the stored bytes (verify).
+constexpr uint32_t kBlkLong = 241;
+// 17..128-byte values are hashed by lane octets (xp_mid_octets)
 template <int KIND, bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t count, const uint64_t* key_base,
-                                                    const uint64_t* arena_base, uint8_t* arena, uint32_t prot_bytes,
+                                                    const uint64_t* arena_base, uint8_t* arena, uint64_t* long_off,
+                                                    uint32_t* long_len, uint64_t* long_part, uint32_t prot_bytes,
                                                     uint8_t* enc, const uint8_t* stored, uint8_t* mismatch,
                                                     uint32_t* mismatch_count) {
   // + 20 B: dword reads and the 16-byte delta write past the key end; an odd
   // stride in dwords keeps the 64 lanes' buffers on distinct banks
   __shared__ uint32_t s_key[256][kBlkKeyBuf / 4 + 5];
-  [[maybe_unused]] const uint32_t lane = threadIdx.x & 63;
+  const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t k0 = 0;
   bool active = false;
@@ -980,17 +653,7 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
   bool global_key = false;
   const GblRd rd{active ? blocks.ptr(b) : nullptr};
   const uint32_t ro = active ? rd_header(rd, blocks.len(b)).ro : 0;  // the layout pass validated the block
-#if !MCK_BLK_LANE_LONG
-  __shared__ uint64_t s_sec[24];  // XXPH3_initCustomSecret(kSeedV) as u64 words
-  if (threadIdx.x < 24) s_sec[threadIdx.x] = csec64(8 * (int)threadIdx.x, kSeedV);
-  __syncthreads();
-  const uint32_t l8 = lane & 7;
-  const uint64_t klast = csec64(121 + 8 * (int)l8, kSeedV);
-  const uint64_t km = csec64((l8 & 1) ? 19 + 16 * (int)(l8 >> 1) : 11 + 16 * (int)(l8 >> 1), kSeedV);
-#endif
-#if MCK_BLK_FLAT_MID == 2
   const uint64_t oklo = sec64(16 * (int)(lane & 7)) + kSeedV, okhi = sec64(16 * (int)(lane & 7) + 8) - kSeedV;
-#endif
   uint32_t p = 0, idx = 0;
   uint32_t u = active ? rd.u32(0) : 0;  // the next entry's first dword, one entry ahead
   while (__any(active)) {
@@ -1004,31 +667,20 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
       // key and value loads (one dependent round trip per entry, not two)
       if (v + vl < ro) u = rd.u32(v + vl);
       // this entry's loads, all issued before any is waited for: the key
-      // delta's first 16 bytes and a 17..128-byte value's pieces
-      // (8 bytes at q are always inside it: 4-byte restart array + 4-byte
-      // footer at least), as two 8-byte loads
-      {
-        const uint64_t k01 = rd.u64(q), k23 = rd.u64(ns > 8 ? q + 8 : q);
-        kw[0] = (uint32_t)k01;
-        kw[1] = (uint32_t)(k01 >> 32);
-        kw[2] = (uint32_t)k23;
-        kw[3] = (uint32_t)(k23 >> 32);
-      }
-      vmid = vl > 16 && vl <= 128 && MCK_BLK_FLAT_MID;
-#if MCK_BLK_FLAT_MID == 1
-      if (vmid) {
-        uint64_t vd[16];
-        xp_mid_load(rd, v, vl, vd);
-        hv = xp_mid_fold(vd, vl, kSeedV);  // first: the pieces' registers are free before the key work
-      }
-#endif
+      // delta's first 16 bytes (8 bytes at q are always inside the block: the
+      // 4-byte restart array + 4-byte footer at least), as two 8-byte loads
+      const uint64_t k01 = rd.u64(q), k23 = rd.u64(ns > 8 ? q + 8 : q);
+      kw[0] = (uint32_t)k01;
+      kw[1] = (uint32_t)(k01 >> 32);
+      kw[2] = (uint32_t)k23;
+      kw[3] = (uint32_t)(k23 >> 32);
+      vmid = vl > 16 && vl <= 128;
     }
-#if MCK_BLK_FLAT_MID == 2
     {
       const uint64_t hm = xp_mid_octets(reinterpret_cast<uint64_t>(rd.p) + v, vl, vmid, oklo, okhi, lane);
       hv = vmid ? hm : 0ull;
     }
-#endif
+    const bool lng = active && vl >= kBlkLong;
     if (active) {
       const uint32_t kl = sh + ns;
       if (!global_key && kl > kBlkKeyBuf) {  // rare: move the prefix to the arena
@@ -1052,48 +704,21 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
         __threadfence_block();
         hv ^= xp_lane(GblRd{gkey}, 0, kl, kSeedK);
       }
-      if (!vmid) {
-#if MCK_BLK_LANE_LONG
-        hv ^= vl <= 240 ? xp_short(rd, v, vl, kSeedV) : xp_lane(rd, v, vl, kSeedV);
-#else
-        if (vl < kBlkWaveLong) hv ^= vl <= 240 ? xp_short(rd, v, vl, kSeedV) : xp_lane(rd, v, vl, kSeedV);
-#endif
-      }
+      if (!vmid && !lng) hv ^= xp_short(rd, v, vl, kSeedV);  // <= 16 or 129..240 bytes
     }
-#if !MCK_BLK_LANE_LONG
-    // long values four at a time, one per 16-lane row (xp_row_long)
-    uint64_t longs = __ballot(active && vl >= kBlkWaveLong);
-    const uint64_t va = reinterpret_cast<uint64_t>(rd.p) + v;
-    while (longs) {
-      uint32_t js[4] = {64, 64, 64, 64};
-#pragma unroll
-      for (int k = 0; k < 4; k++)
-        if (longs) {
-          js[k] = (uint32_t)__builtin_ctzll(longs);
-          longs &= longs - 1;
-        }
-      const uint32_t row = lane >> 4;
-      const uint32_t src = row == 0 ? js[0] : row == 1 ? js[1] : row == 2 ? js[2] : js[3];
-      const uint32_t srcl = src < 64 ? src : 0u;
-      const uint64_t va_r = __shfl(va, (int)srcl, 64);
-      const uint32_t vl_r = (uint32_t)__shfl((int)vl, (int)srcl, 64);
-      uint64_t h2 = 0;
-      if (src < 64) h2 = xp_row_long(GblRd{reinterpret_cast<const uint8_t*>(va_r)}, 0, vl_r, s_sec, klast, km, lane);
-#pragma unroll
-      for (int k = 0; k < 4; k++) {
-        const uint64_t hk = __shfl(h2, 16 * k, 64);
-        if (lane == js[k]) hv ^= hk;
-      }
-    }
-#endif
     if (active) {
       const uint64_t k = k0 + idx;
+      if (lng) {  // to the long-value list; k_block_long completes the entry
+        long_off[k] = reinterpret_cast<uint64_t>(rd.p) + v;
+        long_len[k] = vl;
+        if constexpr (VERIFY) long_part[k] = hv;
+      }
       if constexpr (!VERIFY) {
         if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0))
           reinterpret_cast<uint64_t*>(enc)[k] = hv;
         else
           for (uint32_t c = 0; c < prot_bytes; c++) enc[k * prot_bytes + c] = (uint8_t)(hv >> (8 * c));
-      } else {
+      } else if (!lng) {
         uint64_t sv = 0;
         for (uint32_t c = 0; c < prot_bytes; c++) sv |= (uint64_t)blk_u8(stored + k * prot_bytes + c) << (8 * c);
         const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
@@ -1104,6 +729,74 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
       idx++;
       p = v + vl;
       active = p < ro;
+    }
+  }
+}
+
+// The long-value list (see k_block_kv_t), swept front to back: wave w takes
+// keys [64 c, 64 c + 64) for c = w, w + W, ... (one coalesced read of 64
+// lengths; a chunk without long values costs nothing more), its long values
+// four at a time, one per 16-lane row (xp_row_long: every load instruction
+// reads 128 contiguous bytes of each of four neighbouring values).
+template <bool VERIFY>
+__global__ __launch_bounds__(256) void k_block_long(const uint64_t* key_base, uint32_t nblocks,
+                                                    const uint64_t* long_off, const uint32_t* long_len,
+                                                    const uint64_t* long_part, uint32_t prot_bytes, uint8_t* enc,
+                                                    const uint8_t* stored, uint8_t* mismatch,
+                                                    uint32_t* mismatch_count) {
+  __shared__ uint64_t s_sec[24];  // XXPH3_initCustomSecret(kSeedV) as u64 words
+  if (threadIdx.x < 24) s_sec[threadIdx.x] = csec64(8 * (int)threadIdx.x, kSeedV);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, l8 = lane & 7;
+  const uint64_t klast = csec64(121 + 8 * (int)l8, kSeedV);
+  const uint64_t km = csec64((l8 & 1) ? 19 + 16 * (int)(l8 >> 1) : 11 + 16 * (int)(l8 >> 1), kSeedV);
+  const uint64_t K = ldg_u64(key_base, nblocks);  // keys of the batch
+  const uint64_t wpb = blockDim.x >> 6;
+  const uint64_t nw = gridDim.x * wpb, w = blockIdx.x * wpb + (threadIdx.x >> 6);
+  const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
+  for (uint64_t c = 64 * w; c < K; c += 64 * nw) {
+    const uint64_t k = c + lane;
+    const uint32_t vl = k < K ? long_len[k] : 0u;
+    uint64_t longs = __ballot(vl != 0);
+    if (!longs) continue;  // wave-uniform
+    const uint64_t va = vl ? long_off[k] : 0;
+    const uint64_t part = VERIFY && vl ? long_part[k] : 0;
+    uint64_t hv = 0;
+    while (longs) {
+      uint32_t js[4] = {64, 64, 64, 64};
+#pragma unroll
+      for (int m = 0; m < 4; m++)
+        if (longs) {
+          js[m] = (uint32_t)__builtin_ctzll(longs);
+          longs &= longs - 1;
+        }
+      const uint32_t row = lane >> 4;
+      const uint32_t src = row == 0 ? js[0] : row == 1 ? js[1] : row == 2 ? js[2] : js[3];
+      const uint32_t srcl = src < 64 ? src : 0u;
+      const uint64_t va_r = __shfl(va, (int)srcl, 64);
+      const uint32_t vl_r = (uint32_t)__shfl((int)vl, (int)srcl, 64);
+      uint64_t h2 = 0;
+      if (src < 64) h2 = xp_row_long(GblRd{reinterpret_cast<const uint8_t*>(va_r)}, 0, vl_r, s_sec, klast, km, lane);
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const uint64_t hm = __shfl(h2, 16 * m, 64);
+        if (lane == js[m]) hv = hm;
+      }
+    }
+    if (vl) {
+      if constexpr (!VERIFY) {  // enc[k] holds Encode(partial): XOR the value's hash in
+        if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0)) {
+          reinterpret_cast<uint64_t*>(enc)[k] ^= hv;
+        } else {
+          for (uint32_t b = 0; b < prot_bytes; b++) enc[k * prot_bytes + b] ^= (uint8_t)(hv >> (8 * b));
+        }
+      } else {
+        uint64_t sv = 0;
+        for (uint32_t b = 0; b < prot_bytes; b++) sv |= (uint64_t)blk_u8(stored + k * prot_bytes + b) << (8 * b);
+        const bool bad = sv != ((part ^ hv) & keep);
+        mismatch[k] = bad;
+        if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
+      }
     }
   }
 }

@@ -1141,7 +1141,7 @@ struct FeedRowCache {
 // Ragged batches, driver chosen per workgroup from its share's mean span
 // length (the host cannot see device-resident lengths): 8-lane rows for
 // short spans, 16-lane rows for spans up to a few KiB, the wave driver
-// above that.  force: 0 = by length, 1 = wave, 2 = rows16, 3 = rows8.
+// above that.  force: 0 = by length, 1 = wave, 2 = rows16, 3 = rows8, 5 = rows4.
 // (Superseded for long spans by crc_auto_units_driver, mck_crc_units.hpp.)
 constexpr uint32_t kAutoRows8Max = 640;    // mean span bytes
 constexpr uint32_t kAutoRows16Max = 2560;
@@ -1163,7 +1163,9 @@ __device__ __forceinline__ void crc_auto_driver(const Op& op, uint32_t first, ui
                    : mean <= kAutoRows16Max ? 2
                    : ragged4k               ? 2
                                             : 1;
-  if (mode == 3) {
+  if (mode == 5) {
+    crc_rows_loop<Op, 4, BLK>(op, first, count, g);
+  } else if (mode == 3) {
     crc_rows_loop<Op, 8, BLK>(op, first, count, g);
   } else if (mode == 2) {
     crc_rows_loop<Op, 16, BLK>(op, first, count, g);

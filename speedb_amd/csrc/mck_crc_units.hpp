@@ -550,7 +550,7 @@ __device__ __forceinline__ void crc_units_driver(const Op& op, uint32_t first, u
 // span length (the host cannot see device-resident lengths): 8-lane rows up
 // to 640 B, 16-lane rows up to 2.5 KiB, the unit stream above.
 // force: 0 = by length, 1 = the 4 KiB-round wave driver, 2 = rows16,
-// 3 = rows8, 4 = unit stream.
+// 3 = rows8, 4 = unit stream, 5 = rows4.
 constexpr uint32_t kAutoUnitsMin = 2560;  // mean span bytes
 template <class Op, bool T, bool BLK>
 __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,

@@ -255,7 +255,10 @@ int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform) {
     // one workgroup per CU, spans dealt by LDS tickets
     const uint32_t wpb = kX3WaveThreads / 64;
     const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + wpb - 1) / wpb);
-    hipLaunchKernelGGL((k_xxh3_wave<Op>), dim3(grid), dim3(kX3WaveThreads), 0, st, op, count);
+    if ((count + grid - 1) / grid <= kX3DescCache)
+      hipLaunchKernelGGL((k_xxh3_wave<Op>), dim3(grid), dim3(kX3WaveThreads), 0, st, op, count);
+    else
+      hipLaunchKernelGGL((k_xxh3_wave_static<Op>), dim3(grid), dim3(kX3WaveThreads), 0, st, op, count);
   } else {
     // 16 rows (spans) per 256-thread workgroup
     const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 15) / 16);
@@ -376,13 +379,13 @@ template <int KIND>
 struct BlkKvT {
   template <class... A>
   static void go(dim3, hipStream_t st, bool verify, SpanSrc s, uint32_t n, const uint64_t* kb, const uint64_t* ab,
-                 const uint32_t*, uint8_t* arena, uint64_t*, uint32_t*, uint64_t*, uint32_t*, A... rest) {
+                 uint8_t* arena, uint64_t* long_off, uint32_t* long_len, uint64_t* long_part, A... rest) {
     if (verify)
       hipLaunchKernelGGL((k_block_kv_t<KIND, true>), dim3((n + 255) / 256), dim3(256), 0, st, s, n, kb, ab, arena,
-                         rest...);
+                         long_off, long_len, long_part, rest...);
     else
       hipLaunchKernelGGL((k_block_kv_t<KIND, false>), dim3((n + 255) / 256), dim3(256), 0, st, s, n, kb, ab, arena,
-                         rest...);
+                         long_off, long_len, long_part, rest...);
   }
 };
 template <template <int> class K, class... A>
@@ -406,18 +409,18 @@ int launch_blk(int kind, uint32_t count, hipStream_t st, A... args) {
 
 uint64_t blk_tiles(uint32_t count) { return ((uint64_t)count + kBlkScanTile - 1) / kBlkScanTile; }
 
-// work area: [koff u64 K][voff u64 K][klen u32 K][vlen u32 K] [key arena]
+// work area: [long_off u64 K][long_part u64 K][long_len u32 K][4 B x K spare] [key arena]
+// (the long-value list of k_block_kv_t / k_block_long, indexed by key)
 struct BlkWork {
-  uint64_t *koff, *voff;
-  uint32_t *klen, *vlen;
+  uint64_t *long_off, *long_part;
+  uint32_t* long_len;
   uint8_t* arena;
 };
 uint64_t blk_work_head(uint64_t keys) { return (keys * 24 + 255) & ~255ull; }
 BlkWork blk_work(void* work, uint64_t keys) {
   uint8_t* w = static_cast<uint8_t*>(work);
   return BlkWork{reinterpret_cast<uint64_t*>(w), reinterpret_cast<uint64_t*>(w + 8 * keys),
-                 reinterpret_cast<uint32_t*>(w + 16 * keys), reinterpret_cast<uint32_t*>(w + 20 * keys),
-                 w + blk_work_head(keys)};
+                 reinterpret_cast<uint32_t*>(w + 16 * keys), w + blk_work_head(keys)};
 }
 
 int blk_kv(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_t* key_base,
@@ -443,9 +446,22 @@ int blk_kv(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_
   if (!total_keys || !blocks->count) return MCK_OK;
   const BlkWork w = blk_work(work, total_keys);
   const bool verify = stored != nullptr;
-  return launch_blk<BlkKvT>(kind, blocks->count, st, verify, to_src(blocks), blocks->count, key_base, arena_base,
-                            restart_interval, w.arena, w.koff, w.klen, w.voff, w.vlen, prot_bytes, enc, stored,
-                            mismatch, mismatch_count);
+  MCK_HIP(hipMemsetAsync(w.long_len, 0, 4 * total_keys, st));  // no long value unless the walk records one
+  if (int rc = launch_blk<BlkKvT>(kind, blocks->count, st, verify, to_src(blocks), blocks->count, key_base,
+                                  arena_base, w.arena, w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored,
+                                  mismatch, mismatch_count))
+    return rc;
+  int ncu;
+  if (int rc = current_device(nullptr, &ncu)) return rc;
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)ncu * 16, (total_keys + 255) / 256);
+  if (verify)
+    hipLaunchKernelGGL(k_block_long<true>, dim3(grid), dim3(256), 0, st, key_base, blocks->count, w.long_off,
+                       w.long_len, w.long_part, prot_bytes, enc, stored, mismatch, mismatch_count);
+  else
+    hipLaunchKernelGGL(k_block_long<false>, dim3(grid), dim3(256), 0, st, key_base, blocks->count, w.long_off,
+                       w.long_len, w.long_part, prot_bytes, enc, stored, mismatch, mismatch_count);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
 }
 }  // namespace
 }  // namespace mck
@@ -1334,8 +1350,8 @@ int mck_statistics_get(mck_statistics* out, int reset) {
 
 int mck_test_set_crc_driver(int driver, int interleaved) {
   t_err[0] = 0;
-  if (driver < 0 || driver > 4) {
-    set_err("driver must be 0..4");
+  if (driver < 0 || driver > 5) {
+    set_err("driver must be 0..5");
     return MCK_EINVAL;
   }
   g_crc_force.store(driver, std::memory_order_relaxed);

@@ -237,9 +237,14 @@ __global__ __launch_bounds__(256) void k_xxh3(Op op, uint32_t count) {
 #define MCK_X3W_THREADS 1024
 #endif
 constexpr int kX3WaveThreads = MCK_X3W_THREADS;
+static_assert(kX3WaveThreads / 64 <= kX3MaxWaves, "X3Lds holds a parked-sum buffer per wave");
 template <class Op>
 __global__ __launch_bounds__(kX3WaveThreads) void k_xxh3_wave(Op op, uint32_t count) {
   xxh3_wave_driver<Op, false>(op, count, 0);
+}
+template <class Op>
+__global__ __launch_bounds__(kX3WaveThreads) void k_xxh3_wave_static(Op op, uint32_t count) {
+  xxh3_wave_static_driver<Op, false>(op, count, 0);
 }
 
 // XXH3 ops.  Both drivers call pre(i, ptr, hlen) with the span's loads (the

@@ -555,7 +555,7 @@ __device__ __forceinline__ uint64_t xl32_64(uint64_t v) {
 // batch).  When its share fits, the descriptors are staged in LDS and each
 // wave takes the next span with an LDS ticket as it frees up (balanced
 // inside the CU); otherwise the waves walk the share round-robin.
-constexpr uint32_t kX3DescCache = 1536;
+constexpr uint32_t kX3DescCache = 1024;
 
 // One span on the wave, cut into "units": unit k < rounds is round k (four
 // segments, one per row); the last unit (k = units - 1) also carries the
@@ -705,31 +705,14 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
 // Span feeds of the wave driver (compile-time variants, so the dynamic feed
 // has no global load that the in-order vmcnt would make wait behind the
 // prefetched unit):
-//   X3FeedLds    -- the workgroup's share is staged in LDS; waves take spans
-//                   with an LDS ticket as they free up (balanced in the CU);
+//   X3FeedPieces (below) -- the workgroup's share is staged in LDS; waves
+//                   take pieces of spans with an LDS ticket as they free up
+//                   (balanced in the CU);
 //   X3FeedStatic -- share too large for LDS: the wave walks positions
 //                   wid, wid + wpb, ... and fetches 64 descriptors at a time
-//                   (lane l: the l-th next), read back with v_readlane.
+//                   (lane l: the l-th next), read back with v_readlane; a
+//                   span is not split.
 // Both skip short spans (done before the loop).
-struct X3FeedLds {
-  const uint64_t* off;  // LDS
-  const uint32_t* len;  // LDS
-  uint32_t* ctr;        // LDS
-  uint32_t n, b, G;
-  uint64_t base;
-  template <class Op, bool PREVIEW>
-  __device__ __forceinline__ bool next(const Op&, X3WSpan& sp) {
-    for (;;) {
-      const uint32_t t = __builtin_amdgcn_readfirstlane(lds_ticket(ctr));
-      if (t >= n) return false;
-      const uint64_t n_t = readfirstlane_u64((uint64_t)len[t]);
-      if (n_t > 240) {
-        sp = x3w_span<PREVIEW>(readfirstlane_u64(base + off[t]), n_t, b + G * t);
-        return true;
-      }
-    }
-  }
-};
 struct X3FeedStatic {
   uint32_t t, k, n, b, G, wpb;
   uint64_t base;
@@ -771,9 +754,12 @@ struct X3FeedStatic {
 // addresses, no per-stripe masks, no lone-segment / last-stripe / epilogue
 // loads: four 16-byte loads at one base + 256 B immediates (+ the dword
 // before the row's segment when the span is byte-misaligned) and the fold.
+// x3w_round_c: the round's four segment sums C_g (row 0's lanes hold segments
+// 4k .. 4k + 3 in order, for their accumulator pair q); x3w_full_round
+// chains them into the accumulators.
 template <bool PREVIEW>
-__device__ __forceinline__ void x3w_full_round(const X3WSpan& sp, uint32_t k, const X3Row& X, uint64_t& a0,
-                                               uint64_t& a1) {
+__device__ __forceinline__ void x3w_round_c(const X3WSpan& sp, uint32_t k, const X3Row& X, uint64_t (&C0)[4],
+                                            uint64_t (&C1)[4]) {
   const uint32_t sh = rd_shift(sp.ptr);
   const uint64_t seg = sp.ptr + 1024ull * (4 * k + X.row);
   const uint64_t a = seg + 64 * X.st4 + 16 * X.q - sh + 4;
@@ -794,12 +780,162 @@ __device__ __forceinline__ void x3w_full_round(const X3WSpan& sp, uint32_t k, co
   c0 = row_sum_st4(c0);
   c1 = row_sum_st4(c1);
   const uint64_t e0 = xl16_64(c0), e1 = xl16_64(c1);
-  const uint64_t C0[4] = {c0, e0, xl32_64(c0), xl32_64(e0)};
-  const uint64_t C1[4] = {c1, e1, xl32_64(c1), xl32_64(e1)};
+  C0[0] = c0;
+  C0[1] = e0;
+  C0[2] = xl32_64(c0);
+  C0[3] = xl32_64(e0);
+  C1[0] = c1;
+  C1[1] = e1;
+  C1[2] = xl32_64(c1);
+  C1[3] = xl32_64(e1);
+}
+template <bool PREVIEW>
+__device__ __forceinline__ void x3w_full_round(const X3WSpan& sp, uint32_t k, const X3Row& X, uint64_t& a0,
+                                               uint64_t& a1) {
+  uint64_t C0[4], C1[4];
+  x3w_round_c<PREVIEW>(sp, k, X, C0, C1);
 #pragma unroll
   for (int r = 0; r < 4; r++) {
     a0 = xxh3_scramble(a0 + C0[r], X.ks0);
     a1 = xxh3_scramble(a1 + C1[r], X.ks1);
+  }
+}
+
+// ---- long spans in pieces (round 3) -----------------------------------------
+// A span of more than kX3PieceRounds rounds (16 KiB) no longer runs on one
+// wave, round after dependent round -- at the end of a launch the last 64 KiB
+// spans' 16 sequential round trips were the whole GPU's tail (~25 us per
+// launch).  Its rounds are dealt out in pieces of
+// kX3PieceRounds, like single spans, to whichever waves of the workgroup
+// free up.  The segment sums C_g do not depend on the accumulators, so every
+// piece computes its C_g in parallel and parks them in its wave's LDS
+// buffer; only the chain acc = scramble(acc + C_g) is sequential (8 x u64,
+// a few VALU per segment).  Piece p waits for piece p - 1's accumulators
+// (LDS, per span), chains its own segments and publishes them; the last
+// piece issues the final unit's loads (partial segment, last stripe,
+// epilogue inputs) before it waits, then folds and finishes the span.
+// Pieces are handed out in order, so the piece a wave waits for is held by
+// a wave that started earlier and never waits on a later one: the oldest
+// unfinished piece always runs, and every wave of the workgroup is resident.
+#ifndef MCK_X3_PIECE_ROUNDS
+#define MCK_X3_PIECE_ROUNDS 4
+#endif
+constexpr uint32_t kX3PieceRounds = MCK_X3_PIECE_ROUNDS;
+constexpr uint32_t kX3MaxWaves = 16;
+
+template <bool PREVIEW>
+__device__ __forceinline__ uint32_t x3w_pieces(uint64_t len) {
+  if (len <= 240) return 0;  // the short classes, done per lane before the loop
+  return (x3w_span<PREVIEW>(0, len, 0).units + kX3PieceRounds - 1) / kX3PieceRounds;
+}
+
+// Workgroup LDS of the piece feed.
+struct X3Lds {
+  uint64_t off[kX3DescCache];
+  uint32_t len[kX3DescCache];
+  uint32_t pre[kX3DescCache + 1];  // exclusive prefix of pieces per span; [n] = total
+  uint32_t done[kX3DescCache];     // pieces of span t chained so far
+  uint32_t wsum[kX3MaxWaves];
+  uint32_t ctr;
+  ulonglong2 acc[kX3DescCache][4];                       // span t's accumulators, pair q
+  ulonglong2 csum[kX3MaxWaves][4 * kX3PieceRounds][4];  // a wave's parked C_g, pair q
+};
+
+struct X3Piece {
+  X3WSpan sp;
+  uint32_t t, p, np;
+};
+// Tickets count pieces; a wave's tickets increase, so it finds its span by
+// a forward search from the last one (one LDS read per lane per 64 spans).
+struct X3FeedPieces {
+  X3Lds* s;
+  uint32_t n, b, G, tc;
+  uint64_t base;
+  template <bool PREVIEW>
+  __device__ __forceinline__ bool next(X3Piece& pc) {
+    const uint32_t item = __builtin_amdgcn_readfirstlane(lds_ticket(&s->ctr));
+    if (item >= s->pre[n]) return false;
+    const uint32_t lane = threadIdx.x & 63;
+    for (;;) {  // first span t >= tc with pre[t + 1] > item (exists: item < pre[n])
+      const uint32_t tt = tc + lane;
+      const uint32_t c = (uint32_t)__popcll(__ballot(tt < n && s->pre[tt + 1] <= item));
+      tc += c;
+      if (c < 64) break;
+    }
+    const uint32_t t = tc;
+    const uint32_t p0 = __builtin_amdgcn_readfirstlane(s->pre[t]);
+    pc.t = t;
+    pc.p = item - p0;
+    pc.np = __builtin_amdgcn_readfirstlane(s->pre[t + 1]) - p0;
+    pc.sp = x3w_span<PREVIEW>(readfirstlane_u64(base + s->off[t]), readfirstlane_u64((uint64_t)s->len[t]),
+                              b + G * t);
+    return true;
+  }
+};
+
+// Park the piece's segment sums (rounds k0 .. ke - 1) in the wave's buffer.
+template <bool PREVIEW>
+__device__ __forceinline__ void x3p_park(const X3WSpan& sp, uint32_t k0, uint32_t ke, const X3Row& X,
+                                         ulonglong2 (*cs)[4]) {
+  for (uint32_t k = k0; k < ke; k++) {
+    uint64_t C0[4], C1[4];
+    x3w_round_c<PREVIEW>(sp, k, X, C0, C1);
+    if (X.lane < 4) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) cs[4 * (k - k0) + r][X.q] = make_ulonglong2(C0[r], C1[r]);
+    }
+  }
+}
+// Wait for piece p - 1 of span t, then chain the parked segments.
+__device__ __forceinline__ void x3p_chain(X3Lds* s, uint32_t t, uint32_t p, uint32_t segs, const X3Row& X,
+                                          ulonglong2 (*cs)[4], uint64_t& a0, uint64_t& a1) {
+  if (p) {
+    while (__builtin_amdgcn_readfirstlane(
+               __hip_atomic_load(&s->done[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != p)
+      __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    const ulonglong2 a = s->acc[t][X.q];
+    a0 = a.x;
+    a1 = a.y;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");  // the parked sums to the other lanes
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+  for (uint32_t g = 0; g < segs; g++) {
+    const ulonglong2 c = cs[g][X.q];
+    a0 = xxh3_scramble(a0 + c.x, X.ks0);
+    a1 = xxh3_scramble(a1 + c.y, X.ks1);
+  }
+}
+__device__ __forceinline__ void x3p_publish(X3Lds* s, uint32_t t, uint32_t p, const X3Row& X, uint64_t a0,
+                                            uint64_t a1) {
+  if (X.lane < 4) s->acc[t][X.q] = make_ulonglong2(a0, a1);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if (X.lane == 0) __hip_atomic_store(&s->done[t], p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <class Op, bool PREVIEW>
+__device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, const X3Row& X) {
+  ulonglong2(*const cs)[4] = f.s->csum[threadIdx.x >> 6];
+  X3Piece pc;
+  while (f.template next<PREVIEW>(pc)) {
+    const X3WSpan& cur = pc.sp;
+    uint64_t a0 = X.i0, a1 = X.i1;
+    // a whole span (np = 1) is its own last piece: the same code
+    const uint32_t kl = cur.units - 1;  // the last unit
+    const uint32_t k0 = pc.p * kX3PieceRounds;
+    const bool last = pc.p + 1 == pc.np;
+    const uint32_t ke = last ? kl : k0 + kX3PieceRounds;
+    x3p_park<PREVIEW>(cur, k0, ke, X, cs);
+    if (!last) {
+      x3p_chain(f.s, pc.t, pc.p, 4 * kX3PieceRounds, X, cs, a0, a1);
+      x3p_publish(f.s, pc.t, pc.p, X, a0, a1);
+      continue;
+    }
+    const X3WLoads L = x3w_load(cur, kl, X);
+    const typename Op::Pre e = op.pre(cur.i, cur.ptr, cur.len);
+    x3p_chain(f.s, pc.t, pc.p, 4 * (kl - k0), X, cs, a0, a1);
+    x3w_fold<Op, PREVIEW>(op, cur, kl, L, X, a0, a1, e);
   }
 }
 
@@ -822,42 +958,79 @@ __device__ __forceinline__ void xxh3_wave_loop(const Op& op, Feed& f, const X3Ro
   }
 }
 
+// Short spans (<= 240 bytes: the three small-input classes) first, one per
+// lane -- outside the pipelined loop.
+template <class Op, bool PREVIEW, class Len, class Off>
+__device__ __forceinline__ void x3w_short_spans(const Op& op, uint32_t n, uint32_t b, uint32_t G, uint64_t seed,
+                                                Len len_of, Off off_of) {
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  for (uint32_t tt = threadIdx.x; tt < n; tt += blockDim.x) {
+    const uint64_t len = len_of(tt);
+    if (len <= 240) {
+      const uint8_t* p = reinterpret_cast<const uint8_t*>(base + off_of(tt));
+      op.finish(b + G * tt, PREVIEW ? xxph3_short(p, len, seed) : xxh3_short(p, len));
+    }
+  }
+}
+
+// The workgroup's share (spans b, b + G, ...) fits the LDS descriptor cache
+// (host: ceil(count / G) <= kX3DescCache): staged, long spans in pieces.
 template <class Op, bool PREVIEW>
 __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, uint64_t seed) {
   const X3Row X = x3_row(seed);
-  __shared__ uint64_t s_off[kX3DescCache];
-  __shared__ uint32_t s_len[kX3DescCache];
-  __shared__ uint32_t s_ctr;
+  __shared__ X3Lds s;
   const uint32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t n = (count - b + G - 1) / G;
-  const bool dyn = (count + G - 1) / G <= kX3DescCache;  // grid-uniform
-  if (dyn) {
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
-      s_off[t] = op.off(b + G * t);
-      s_len[t] = (uint32_t)op.hlen(b + G * t);
-    }
-    if (threadIdx.x == 0) s_ctr = 0;
+  const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
+  for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
+    s.off[t] = op.off(b + G * t);
+    s.len[t] = (uint32_t)op.hlen(b + G * t);
+    s.done[t] = 0;
   }
+  if (threadIdx.x == 0) s.ctr = 0;
+  // pieces per span, exclusive prefix (a chunk of blockDim spans at a time)
+  uint32_t carry = 0;
+  for (uint32_t c0 = 0; c0 < n; c0 += blockDim.x) {
+    const uint32_t t = c0 + threadIdx.x;
+    const uint32_t v = t < n ? x3w_pieces<PREVIEW>(op.hlen(b + G * t)) : 0;
+    uint32_t x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+      x += lane >= (uint32_t)d ? y : 0u;
+    }
+    if (lane == 63) s.wsum[wid] = x;
+    __syncthreads();
+    uint32_t below = 0, tot = 0;
+    for (uint32_t w = 0; w < wpb; w++) {
+      const uint32_t ws = s.wsum[w];
+      below += w < wid ? ws : 0u;
+      tot += ws;
+    }
+    if (t < n) s.pre[t] = carry + below + x - v;
+    carry += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) s.pre[n] = carry;
   __syncthreads();
+  x3w_short_spans<Op, PREVIEW>(
+      op, n, b, G, seed, [&](uint32_t t) { return (uint64_t)s.len[t]; }, [&](uint32_t t) { return s.off[t]; });
+  X3FeedPieces f{&s, n, b, G, 0, reinterpret_cast<uint64_t>(op.base())};
+  xxh3_piece_loop<Op, PREVIEW>(op, f, X);
+}
+
+// A share too large for the cache: the waves walk it round-robin, whole
+// spans (a separate kernel: the two loops in one exceed 128 VGPRs).
+template <class Op, bool PREVIEW>
+__device__ __forceinline__ void xxh3_wave_static_driver(const Op& op, uint32_t count, uint64_t seed) {
+  const X3Row X = x3_row(seed);
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t n = (count - b + G - 1) / G;
   const uint32_t wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
-  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  // short spans (n <= 240: the three small-input classes) first, one per
-  // lane -- outside the pipelined loop
-  for (uint32_t tt = threadIdx.x; tt < n; tt += blockDim.x) {
-    const uint32_t i = b + G * tt;
-    const uint64_t len = dyn ? (uint64_t)s_len[tt] : op.hlen(i);
-    if (len <= 240) {
-      const uint8_t* p = reinterpret_cast<const uint8_t*>(base + (dyn ? s_off[tt] : op.off(i)));
-      op.finish(i, PREVIEW ? xxph3_short(p, len, seed) : xxh3_short(p, len));
-    }
-  }
-  if (dyn) {
-    X3FeedLds f{s_off, s_len, &s_ctr, n, b, G, base};
-    xxh3_wave_loop<Op, PREVIEW>(op, f, X);
-  } else {
-    X3FeedStatic f{wid, 64, n, b, G, wpb, base, 0, 0};
-    xxh3_wave_loop<Op, PREVIEW>(op, f, X);
-  }
+  x3w_short_spans<Op, PREVIEW>(
+      op, n, b, G, seed, [&](uint32_t t) { return op.hlen(b + G * t); }, [&](uint32_t t) { return op.off(b + G * t); });
+  X3FeedStatic f{wid, 64, n, b, G, wpb, reinterpret_cast<uint64_t>(op.base()), 0, 0};
+  xxh3_wave_loop<Op, PREVIEW>(op, f, X);
 }
 
 // ---- legacy XXH32 / XXH64, one lane per span ----------------------------

@@ -259,6 +259,39 @@ def test_block_protection_verify_flags_exact_entries(gpu, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("p", [1, 8])
+def test_block_protection_long_value_list(gpu, oracle, p):
+    """Values over 240 bytes go through the long-value list (k_block_kv_t
+    records them by key index, k_block_long hashes them in key order): blocks
+    of 241..3000-byte values mixed with short ones, protect against the
+    oracle, then verify with corrupted stored bytes on long and short
+    entries alike."""
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    rnd = random.Random(70 + p)
+    blocks = [build_block(data_block(rnd, rnd.randrange(1, 12), rnd.choice((1, 2, 16)),
+                                     rnd.choice((0, 241, 241)), rnd.choice((300, 1100, 3000))), 16)
+              for _ in range(400)]
+    base, offs, lens = _pack(torch, blocks, rnd)
+    spans = speedb_amd.Spans(base, len(blocks), offs, lens)
+    prot = B.InitializeDataBlockProtectionInfo(spans, p)
+    kb = prot.key_base.cpu().tolist()
+    ck = prot.kv_checksum.cpu().numpy().tobytes()
+    for i, blk in enumerate(blocks):
+        assert ck[kb[i] * p:kb[i + 1] * p] == oracle.BlockKvProtect(DATA, blk, p)[1], i
+    mism, cnt = B.VerifyBlockProtectionInfo(spans, prot)
+    assert int(cnt.item()) == 0 and int(mism.sum().item()) == 0
+    stored = prot.kv_checksum.clone()
+    bad = sorted(rnd.sample(range(prot.total_keys), 40))
+    for k in bad:
+        stored[p * k + rnd.randrange(p)] ^= 1 << rnd.randrange(8)
+    mism, cnt = B.VerifyBlockProtectionInfo(spans, prot, stored)
+    assert int(cnt.item()) == len(bad)
+    assert torch.nonzero(mism).flatten().cpu().tolist() == bad
+
+
+@pytest.mark.gpu
 def test_block_protection_many_blocks_property(gpu, oracle):
     """> 2048 blocks (multi-tile scans): 64 distinct blocks tiled 80 times --
     every copy's checksums equal its original's (the oracle's)."""
@@ -329,20 +362,3 @@ def test_wave_xxph3_long_loop(gpu, oracle):
             want = oracle.Hash64(b, seed)
             assert r[:3] == [want, want, want], (n, seed)
             assert r[3:] == [oracle.Hash64(b[:n - 61 * k], seed) for k in range(4)], (n, seed)
-
-
-@pytest.mark.gpu
-def test_block_protection_wave_kernels_subprocess(gpu):
-    """The wave-per-block LDS kernels (MCK_BLK_WAVE=1, read once per
-    process) in a child process: the same GPU parity tests."""
-    import os
-    import subprocess
-    import sys
-    if os.environ.get("MCK_BLK_WAVE") == "1":
-        pytest.skip("already running the wave kernels")
-    env = dict(os.environ, MCK_BLK_WAVE="1")
-    here = os.path.dirname(os.path.abspath(__file__))
-    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "gpu",
-                        "-k", "not subprocess", os.path.join(here, "test_block_protection.py")],
-                       env=env, cwd=os.path.dirname(here), capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]

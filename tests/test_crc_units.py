@@ -147,11 +147,12 @@ def test_units_many_windows(gpu, oracle):
         assert got[i] == oracle.Value(bytes(dev[o:o + n].cpu().numpy())), (i, o, n)
 
 
-@pytest.mark.parametrize("ctype", [1])
+@pytest.mark.parametrize("ctype", [1, 4])
 def test_units_sst_verify_mix(gpu, oracle, ctype):
     """VerifyBlockChecksum over a compaction mix of 4/16/64 KiB blocks with
     jitter (split 64 KiB blocks: the epilogue runs on whichever wave finishes
-    the last piece), context checksums, then flipped bytes."""
+    the last piece -- the CRC unit stream, and for kXXH3 the wave driver's
+    pieces), context checksums, then flipped bytes."""
     import speedb_amd as S
     torch = gpu
     rnd = random.Random(77)

@@ -483,9 +483,10 @@ def test_kv_protect_verify(gpu, oracle, prot_bytes):
 
 
 def test_large_ragged_batches_static_and_dynamic_feeds(gpu, oracle):
-    """Ragged batches above and below the per-workgroup LDS descriptor cache
-    (1536 spans per workgroup share): the static round-robin feed and the
-    LDS-ticket feed must give identical, oracle-exact results."""
+    """Ragged batches above and below the per-workgroup LDS descriptor caches
+    (XXH3: 1024 spans per workgroup share, k_xxh3_wave vs k_xxh3_wave_static):
+    the static round-robin feed and the LDS-ticket feed must give identical,
+    oracle-exact results."""
     import speedb_amd as S
     torch = gpu
     rnd = random.Random(77)
@@ -508,6 +509,28 @@ def test_large_ragged_batches_static_and_dynamic_feeds(gpu, oracle):
             b = host[offs[i]:offs[i] + lens[i]]
             assert crc[i] == oracle.Value(b), (count, i, lens[i])
             assert x3[i] == oracle.XXH3(b), (count, i, lens[i])
+
+
+def test_xxh3_long_spans_in_pieces(gpu, oracle):
+    """k_xxh3_wave splits spans of more than 4 rounds (16 KiB) into pieces
+    dealt to different waves, chained through LDS: lengths at every piece
+    boundary (1 KiB segments, the lone partial segment, the last stripe), at
+    every start alignment, mixed with short and 4 KiB spans, and spans of
+    hundreds of pieces."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(41)
+    lens = []
+    for m in (15, 16, 17, 19, 20, 21, 32, 33, 36, 37, 48, 64, 65, 68, 69, 80, 100, 257):
+        for d in (-64, -1, 0, 1, 2, 63, 64, 65, 1023):
+            lens.append(1024 * m + d)
+    lens += [4 << 20, (4 << 20) + 4097, 0, 3, 240, 241, 5000]
+    lens += [rnd.randrange(241, 70_000) for _ in range(4000)]
+    rnd.shuffle(lens)
+    host, dev, offs, lens = make_batch(torch, 41, lens)
+    got = u64(S.xxh3_64_batch(spans(torch, S, dev, offs, lens)))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert got[i] == oracle.XXH3(host[o:o + n]), (i, o, n)
 
 
 # ---- long spans / whole-file checksum (SURVEY.md 8f row 2) -----------------
