@@ -15,6 +15,10 @@ for d in units wave; do
   $B --crc-driver $d --workload ragged --span-min 4096 --span-max 4096 --span-bytes $((4<<30)) > $O/r4096_$d.json || exit 1
   $B --crc-driver $d --workload sst --sst-types crc32c --sst-bytes $((1<<30)) > $O/sst1g_$d.json || exit 1
 done
+TK="env SPEEDB_AMD_LIB=$PWD/microbench/_variants/units_ticket.so"
+$TK $B --crc-driver units --workload crc32c --block-bytes 4300 --blocks 1000000 > $O/u4300_ticket.json || exit 1
+$TK $B --crc-driver units --workload ragged --span-min 4100 --span-max 4400 --span-bytes $((4<<30)) > $O/r4100_ticket.json || exit 1
+$TK $B --workload sst --sst-bytes $((1<<30)) > $O/sst1g_both_old.json || exit 1
 $B --workload sst --sst-types xxh3 --sst-bytes $((1<<30)) > $O/sst1g_x3.json || exit 1
 $B --workload sst --sst-bytes $((1<<30)) > $O/sst1g_both.json || exit 1
 $B --workload blockkv --kv-value-bytes 1000 > $O/blk1000.json || exit 1

@@ -28,17 +28,21 @@
 // un-shifted by the < 16 bytes appended.  (The algebra of Crc32cCombine,
 // util/crc32c.cc:1221-1266, as in mck_crc.hpp.)
 //
-// Stream.  Each wave consumes UNITS, four per loop iteration (4 KiB in
+// Streams.  A window of the workgroup's spans (up to kUDescCache) is laid
+// out as one sequence of units -- spans in window order, each span's units
+// in address order -- and cut into W equal STREAMS, one per wave: wave w
+// folds units [T w / W, T (w + 1) / W), four per loop iteration (4 KiB in
 // flight, the next iteration's loads issued before the current one is
-// folded), from a queue of ITEMS that crosses span boundaries: a 4300-B
-// block is 5 units, and an iteration holds the last unit of one block and
-// the first three of the next.  Items come from an LDS ticket shared by the
-// workgroup's 16 waves.  Spans of more than 24 units are split into 16 KiB
-// PIECES (items of their own, end-anchored, the head piece 9..24 units):
-// a piece's partial state is moved to the span end by zshift(16384 m)
-// (pow16k), XORed into the span's LDS accumulator, and the wave that
-// completes the span's last piece (an LDS counter) runs the epilogue -- no
-// span keeps one wave busy for more than 24 units.
+// folded), across span boundaries: a 4300-B block is 5 units, and an
+// iteration may hold the last unit of one block and the first three of the
+// next.  The slots of an iteration are worked out lane-parallel from the
+// units' prefix in LDS (unit_slots).  A span cut by a stream boundary (at
+// most W - 1 per window, and every span longer than a stream) is shared:
+// each stream's portion is reduced, moved to the span end by zshift(1024 m)
+// (pow1k, m = units after the portion) and XORed into the span's LDS
+// accumulator, and the stream that completes the last portion (an LDS
+// counter) runs the epilogue.  No tickets, no per-span scheduling: every
+// wave does the same number of units.
 //
 // LDS image (160 KiB, filled once per persistent workgroup):
 //   [0, 64K)    gap1012 byte tables, 8 copies: entry (t, v, c) at
@@ -49,24 +53,24 @@
 //               (n, nib, l) at n << 13 | nib << 9 | (l >> 5) << 8 | 128 |
 //               (l & 31) << 2 (bank = l & 31: conflict-free)
 //   [64K, 128K) the 4-byte step tables (kLdsStep layout, CrcLane)
-//   [128K, ..)  un-shift by k < 16, byte masks, ticket, the share's
-//               descriptors and the split spans' accumulators.
+//   [128K, ..)  un-shift by k < 16, byte masks, the staging scan's wave
+//               sums, the window's descriptors, the shared spans'
+//               accumulators and the units' prefix.
 #pragma once
 #include "mck_crc.hpp"
 
 namespace mck {
 
 constexpr uint32_t kUnitBytes = 1024;
-constexpr uint32_t kPieceUnits = 16;    // units per piece of a split span
-constexpr uint32_t kSplitUnits = 24;    // spans of more units are split
 constexpr uint32_t kULdsUnshift = 131072;                        // [16][8][16]
 constexpr uint32_t kULdsMaskHead = kULdsUnshift + 16 * 512;      // [16] x 16 B: keep bytes >= h
 constexpr uint32_t kULdsMaskTail = kULdsMaskHead + 256;          // [16] x 16 B: keep the first 16 - k
-constexpr uint32_t kULdsTicket = kULdsMaskTail + 256;            // u64 {slot, piece}
-constexpr uint32_t kUDescCache = 960;                            // descriptors per window
-constexpr uint32_t kULdsDesc = kULdsTicket + 64;                 // 16 B {off lo, off hi, len, key}
+constexpr uint32_t kULdsWaveSum = kULdsMaskTail + 256;           // u32 per wave (staging scan)
+constexpr uint32_t kUDescCache = 832;                            // descriptors per window
+constexpr uint32_t kULdsDesc = kULdsWaveSum + 64;                // 16 B {off lo, off hi, len, inj}
 constexpr uint32_t kULdsAcc = kULdsDesc + 16 * kUDescCache;      // {xor, count} per slot
-constexpr uint32_t kULdsEnd = kULdsAcc + 8 * kUDescCache;
+constexpr uint32_t kULdsUpre = kULdsAcc + 8 * kUDescCache;       // u32 per slot + 65 (lookahead pad)
+constexpr uint32_t kULdsEnd = kULdsUpre + 4 * (kUDescCache + 65);
 static_assert(kULdsEnd <= kCrcLdsBytes, "unit driver LDS image must fit");
 
 // ---- LDS fill -----------------------------------------------------------
@@ -175,33 +179,10 @@ __device__ __forceinline__ uint32_t gmem_nibmap(const uint32_t (*tab)[16], uint3
   return r;
 }
 
-// ---- items ----------------------------------------------------------------
-// One item = one span (<= 24 units) or one 16 KiB piece of a longer span.
-// Wave-uniform (SGPRs).  Units are processed from khi down to klo (address
-// order).
-struct UItem {
-  uint64_t ptr;   // span start (device address)
-  uint64_t a1;    // span end rounded up to 16
-  uint32_t t;     // slot in the share window
-  uint32_t U;     // units of the span
-  uint32_t M, m;  // pieces of the span, this piece (0 = last)
-  uint32_t kt;    // a1 - end
-  uint32_t inj;   // unshift(~init, ptr & 15): Extend's init state at the piece holding ptr
-  __device__ uint32_t klo() const { return kPieceUnits * m; }
-  __device__ uint32_t khi() const { return m == M - 1 ? U - 1 : kPieceUnits * m + kPieceUnits - 1; }
-  // head unit: lanes below own load zeros, lane own holds ptr
-  __device__ uint32_t own() const { return 64u * U - (uint32_t)((a1 - (ptr & ~15ull)) >> 4); }
-  __device__ uint32_t hb() const { return (uint32_t)ptr & 15u; }
-  __device__ uint64_t n() const { return a1 - kt - ptr; }
-};
-
+// ---- spans and units ---------------------------------------------------------
 __device__ __forceinline__ uint32_t unit_count(uint64_t ptr, uint32_t n) {
   const uint64_t a0 = ptr & ~15ull, a1 = (ptr + n + 15) & ~15ull;
   return n ? (uint32_t)(((a1 - a0) >> 4) + 63) >> 6 : 0u;
-}
-// items of a span: 0 for an empty span (finished when the window is staged)
-__device__ __forceinline__ uint32_t unit_pieces(uint32_t U) {
-  return U == 0 ? 0u : U <= kSplitUnits ? 1u : (U - 9u) / kPieceUnits + 1u;
 }
 
 // staged descriptor: {off lo, off hi, len, inj}
@@ -210,6 +191,8 @@ __device__ __forceinline__ uint4 unit_desc(uint32_t t) {
       static_cast<size_t>(kULdsDesc + 16 * t));
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// exclusive prefix of the window's units: upre(t) = first unit of span t
+__device__ __forceinline__ uint32_t upre(uint32_t t) { return *lds_p32(kULdsUpre + 4 * t); }
 
 template <class Op>
 __device__ __forceinline__ uint32_t unit_init(const Op& op, int kind, uint32_t key) {
@@ -233,144 +216,72 @@ struct UShare {
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
-// Take the next item of the window: lane 0 advances the {slot, piece}
-// ticket with a CAS (empty spans, finished at staging, are skipped); the
-// item is wave-uniform.  Only LDS traffic (no memory op: the caller's
-// in-flight loads are not waited for).  False when the window is exhausted.
-__device__ __forceinline__ bool unit_take(uint32_t wn, uint64_t base, UItem* it) {
-  uint32_t t = 0xFFFFFFFFu, q = 0;
-  uint4 d = make_uint4(0, 0, 0, 0);
-  if ((threadIdx.x & 63) == 0) {
-    uint64_t old = __hip_atomic_load(lds_p64(kULdsTicket), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    for (;;) {
-      const uint32_t ot = (uint32_t)old, oq = (uint32_t)(old >> 32);
-      if (ot >= wn) break;
-      const uint4 x = unit_desc(ot);
-      const uint32_t M = unit_pieces(unit_count(base + (((uint64_t)x.y << 32) | x.x), x.z));
-      const uint64_t nw = oq + 1 < M ? old + (1ull << 32) : (uint64_t)(ot + 1);
-      if (__hip_atomic_compare_exchange_strong(lds_p64(kULdsTicket), &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP)) {
-        if (M == 0) {  // an empty span: nothing to hash
-          old = nw;
-          continue;
-        }
-        t = ot;
-        q = oq;
-        d = x;
-        break;
-      }
-    }
-  }
-  t = rfl(t);
-  if (t >= wn) return false;
-  q = rfl(q);
-  const uint64_t ptr = base + (((uint64_t)rfl(d.y) << 32) | rfl(d.x));
-  const uint32_t n = rfl(d.z);
-  it->ptr = ptr;
-  it->t = t;
-  it->a1 = (ptr + n + 15) & ~15ull;
-  it->U = unit_count(ptr, n);
-  it->M = unit_pieces(it->U);
-  it->m = it->M - 1 - q;
-  it->kt = (uint32_t)(it->a1 - (ptr + n));
-  it->inj = rfl(d.w);
-  return true;
-}
-
-// One iteration's four unit slots, precomputed when the iteration is planned
-// (wave-uniform, SGPRs): slots [0, na) are units of item A (the cursor's
-// item), slots [na, na + nb) the first units of item B (the prefetched
-// next item); the rest are empty.  A plan ends at most one item (A): B is
-// taken only if it continues past the plan, so one set of epilogue inputs
-// per iteration suffices.
-constexpr uint32_t kUFirst = 1u, kUHead = 16u, kUTail = 256u, kUAEnd = 4096u;  // << slot
-struct UPlan {
+// One iteration's four unit slots (wave-uniform, SGPRs), worked out
+// lane-parallel (lane j mod 4 computes slot j) and read back with
+// v_readlane / ballots: slot j is window unit g0 + j of the wave's stream.
+constexpr uint32_t kUFirst = 1u, kUHead = 16u, kUTail = 256u, kUEnd = 4096u;  // << slot
+struct USlots {
   uint64_t base[4];   // slot j's unit: [base, base + 1 KiB)
-  uint32_t below[4];  // lanes below this load the zero piece (64: empty slot)
-  uint32_t flags;     // kUFirst << j: an item starts at slot j; kUHead << j: ... at its span's
-                      // head unit; kUTail << j: slot j is its span's last unit; kUAEnd: A ends
-  uint32_t na;
-  uint32_t hA, hB;    // own | hb << 8 | kt << 16 of A's and B's spans
-  uint32_t injA, injB;
-  uint32_t At, Am;    // A's window slot and piece (the flush re-reads the rest)
+  uint32_t below[4];  // lanes below this load the zero piece (64: no unit)
+  uint32_t h[4];      // own | hb << 8 | kt << 16 of the slot's span
+  uint32_t inj[4];    // the span's injected init state (head slots)
+  uint32_t t[4];      // the slot's span (window slot)
+  uint32_t flags;     // kUFirst << j: the lane state restarts (span head or stream start);
+                      // kUHead << j: the span's head unit; kUTail << j: its last unit, with
+                      // bytes past the end; kUEnd << j: the stream's portion of the span ends
+  uint32_t g0;
 };
 
-struct UnitCursor {
-  UItem C, N;  // current item (units kc, kc - 1, ... not yet loaded), prefetched next item
-  uint32_t kc;
-  bool cv, nv;  // valid
-};
-
-__device__ __forceinline__ uint32_t unit_hpack(const UItem& I) { return I.own() | (I.hb() << 8) | (I.kt << 16); }
-
-// Plan the next iteration from the cursor; sets *consumed when N was used
-// (the caller takes a new N after issuing the loads).
-__device__ __forceinline__ UPlan unit_plan(UnitCursor& q, bool* consumed) {
-  UPlan P;
-  *consumed = false;
-  if (!q.cv && q.nv) {  // the previous item ended on the iteration boundary
-    q.C = q.N;
-    q.kc = q.C.khi();
-    q.cv = true;
-    q.nv = false;
-    *consumed = true;
+// Plan the slots of units g0 .. g0 + 3 of stream [gs, ge); tc = a span at or
+// before the span of unit g0 (advanced here).
+__device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t ge, uint32_t& tc, uint64_t base,
+                                             uint32_t lane) {
+  USlots P;
+  P.g0 = g0;
+  // spans tc + 1 + lane: the units before g0 + j belong to spans counted by
+  // the ballot (empty spans included, the window's upre padded with ~0)
+  uint32_t v = upre(tc + 1 + lane);
+  uint32_t c3 = (uint32_t)__popcll(__ballot(v <= g0 + 3));
+  while (c3 == 64) {  // more than 63 spans end before g0 + 3 (empty spans): skip ahead
+    tc += 64;
+    v = upre(tc + 1 + lane);
+    c3 = (uint32_t)__popcll(__ballot(v <= g0 + 3));
   }
+  const uint32_t t0 = tc + (uint32_t)__popcll(__ballot(v <= g0));
+  const uint32_t t1 = tc + (uint32_t)__popcll(__ballot(v <= g0 + 1));
+  const uint32_t t2 = tc + (uint32_t)__popcll(__ballot(v <= g0 + 2));
+  const uint32_t t3 = tc + c3;
+  P.t[0] = t0;
+  P.t[1] = t1;
+  P.t[2] = t2;
+  P.t[3] = t3;
+  tc = t3;
+  const uint32_t j = lane & 3u;
+  const uint32_t g = g0 + j;
+  const bool live = g < ge;
+  const uint32_t t = j == 0 ? t0 : j == 1 ? t1 : j == 2 ? t2 : t3;
+  const uint4 d = unit_desc(live ? t : t0);
+  const uint32_t u0 = upre(t), u1 = upre(t + 1);
+  const uint64_t ptr = base + (((uint64_t)d.y << 32) | d.x);
+  const uint64_t a1 = (ptr + d.z + 15) & ~15ull;
+  const uint32_t kt = (uint32_t)(a1 - (ptr + d.z));
+  const uint32_t U = u1 - u0, kk = u1 - 1 - g;  // unit kk from the span's end
+  const bool head = live && kk == U - 1;
+  const uint32_t own = 64u * U - (uint32_t)((a1 - (ptr & ~15ull)) >> 4);
+  const uint64_t ub = a1 - (uint64_t)kUnitBytes * (kk + 1);
+  const uint32_t below = live ? (head ? own : 0u) : 64u;
+  const uint32_t h = own | (((uint32_t)ptr & 15u) << 8) | (kt << 16);
+  const bool tail = live && kk == 0 && kt != 0;
+  const bool first = live && (g == gs || head);
+  const bool end = live && (g + 1 == ge || kk == 0);
+  P.flags = ((uint32_t)__ballot(first) & 15u) * kUFirst | ((uint32_t)__ballot(head) & 15u) * kUHead |
+            ((uint32_t)__ballot(tail) & 15u) * kUTail | ((uint32_t)__ballot(end) & 15u) * kUEnd;
 #pragma unroll
-  for (int j = 0; j < 4; j++) {
-    P.base[j] = 0;
-    P.below[j] = 64;
-  }
-  P.flags = 0;
-  P.na = 0;
-  P.hA = P.hB = P.injA = P.injB = 0;
-  P.At = q.C.t;
-  P.Am = q.C.m;
-  if (!q.cv) return P;
-  const UItem& C = q.C;
-  const uint32_t avail = q.kc - C.klo() + 1;
-  const uint32_t na = avail < 4 ? avail : 4;
-  P.na = na;
-  P.hA = unit_hpack(C);
-  P.injA = C.inj;
-  const uint32_t ownA = C.own();
-#pragma unroll
-  for (uint32_t j = 0; j < 4; j++) {
-    if (j < na) {
-      const uint32_t k = q.kc - j;
-      P.base[j] = C.a1 - (uint64_t)kUnitBytes * (k + 1);
-      P.below[j] = k == C.U - 1 ? ownA : 0u;
-      P.flags |= (k == C.U - 1 ? kUHead << j : 0u) | (k == 0 && C.kt ? kUTail << j : 0u);
-    }
-  }
-  if (q.kc == C.khi()) P.flags |= kUFirst;
-  if (avail > 4) {
-    q.kc -= 4;
-    return P;
-  }
-  P.flags |= kUAEnd;
-  q.cv = false;
-  if (na < 4 && q.nv) {
-    const UItem& N = q.N;
-    const uint32_t bu = N.khi() - N.klo() + 1;
-    if (bu > 4 - na) {  // B continues past this plan (so none of its slots is its last unit)
-      const uint32_t kh = N.khi(), ownB = N.own();
-#pragma unroll
-      for (uint32_t j = 1; j < 4; j++) {
-        if (j >= na) {
-          const uint32_t k = kh - (j - na);
-          P.base[j] = N.a1 - (uint64_t)kUnitBytes * (k + 1);
-          P.below[j] = k == N.U - 1 ? ownB : 0u;
-          P.flags |= (k == N.U - 1 ? kUHead << j : 0u) | (j == na ? kUFirst << j : 0u);
-        }
-      }
-      P.hB = unit_hpack(N);
-      P.injB = N.inj;
-      q.nv = false;
-      *consumed = true;
-      q.C = N;
-      q.kc = kh - (4 - na);
-      q.cv = true;
-    }
+  for (int q = 0; q < 4; q++) {
+    P.base[q] = readlane_u64(ub, (uint32_t)q);
+    P.below[q] = readlane_u32(below, (uint32_t)q);
+    P.h[q] = readlane_u32(h, (uint32_t)q);
+    P.inj[q] = readlane_u32(d.w, (uint32_t)q);
   }
   return P;
 }
@@ -378,7 +289,7 @@ __device__ __forceinline__ UPlan unit_plan(UnitCursor& q, bool* consumed) {
 // The four loads of plan P: lane l's piece of every slot's unit (the zero
 // piece for lanes before a span's head and for empty slots).  Straight-line,
 // so every load is unconditional and the waits exact.
-__device__ __forceinline__ Chunk unit_load(const UPlan& P, uint32_t lane16, uint32_t lane, uint64_t zp) {
+__device__ __forceinline__ Chunk unit_load(const USlots& P, uint32_t lane16, uint32_t lane, uint64_t zp) {
   Chunk c;
 #pragma unroll
   for (int j = 0; j < 4; j++) c.v[j] = span_load16<true>(lane < P.below[j] ? zp : P.base[j] + lane16);
@@ -404,32 +315,36 @@ __device__ __forceinline__ void unit_mask_tail(uint4& v, uint32_t k) {
   }
 }
 
-// Item (window slot t, piece m) has its last unit folded (lane state s):
-// reduce, and either run the epilogue or (piece of a split span) add the
-// partial to the span's accumulator; the wave completing the span's last
-// piece runs the epilogue.
+// The stream's portion of span t ends with unit g (lane state s): reduce it
+// to the state at the unit's end.  A span inside the stream [gs, ge) is
+// finished at once; a span cut by stream boundaries has its portion moved to
+// the span end by zshift(1024 kk) (kk = units after g: pow1k) and XORed into
+// the span's LDS accumulator, whose counter sums the portions' units: the
+// stream whose portion completes the span's U units runs the epilogue.
 template <class Op>
-__device__ __forceinline__ void unit_flush(const Op& op, const UShare& sh, uint64_t base, uint32_t t, uint32_t m,
-                                           uint32_t s, const typename Op::Pre& pre, const UnitLane& UL,
-                                           const CrcTables* __restrict__ g) {
-  uint32_t p = wave_xor32(unit_lane_final(s, UL.fl));  // pure state at a1 - 1024 klo
+__device__ __forceinline__ void unit_flush(const Op& op, const UShare& sh, uint64_t base, uint32_t t, uint32_t g,
+                                           uint32_t s, const typename Op::Pre& pre, uint32_t gs, uint32_t ge,
+                                           const UnitLane& UL, const CrcTables* __restrict__ gt) {
+  uint32_t p = wave_xor32(unit_lane_final(s, UL.fl));  // pure state at the end of unit g
   const uint4 d = unit_desc(t);
   const uint64_t ptr = base + (((uint64_t)d.y << 32) | d.x);
   const uint32_t n = d.z;
   const uint32_t kt = (uint32_t)(((ptr + n + 15) & ~15ull) - (ptr + n));
-  const uint32_t M = unit_pieces(unit_count(ptr, n));
+  const uint32_t u0 = upre(t), u1 = upre(t + 1);
   const uint32_t i = sh.idx(t);
-  if (M > 1) {
-    for (uint32_t mm = m, b = 0; mm; mm >>= 1, b++)
-      if (mm & 1) p = gmem_nibmap(g->pow16k[b], p);
+  if (u0 < gs || u1 > ge) {  // wave-uniform: a shared span
+    const uint32_t pu = g + 1 - (u0 > gs ? u0 : gs);  // this portion's units
+    for (uint32_t kk = u1 - 1 - g, b = 0; kk; kk >>= 1, b++)
+      if (kk & 1) p = gmem_nibmap(gt->pow1k[b], p);
     uint32_t c = 0;
     if (UL.lane == 0) {
       __hip_atomic_fetch_xor(lds_p32(kULdsAcc + 8 * t), p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      c = __hip_atomic_fetch_add(lds_p32(kULdsAcc + 8 * t + 4), 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (c == M - 1) p = __hip_atomic_load(lds_p32(kULdsAcc + 8 * t), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      c = __hip_atomic_fetch_add(lds_p32(kULdsAcc + 8 * t + 4), pu, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (c + pu == u1 - u0)
+        p = __hip_atomic_load(lds_p32(kULdsAcc + 8 * t), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     c = rfl(c);
-    if (c != M - 1) return;
+    if (c + pu != u1 - u0) return;
     p = rfl(p);
     if (kt) p = unit_unshift(kt, p);
     op.finish(i, ~p, unit_pre(op, i, ptr, n), UL.lane == 0);
@@ -439,71 +354,92 @@ __device__ __forceinline__ void unit_flush(const Op& op, const UShare& sh, uint6
   op.finish(i, ~p, pre, UL.lane == 0);
 }
 
-// The wave loop over one share window.
+// The wave's stream over one share window: units [gs, ge) of the window's
+// unit sequence (spans in window order, each span's units in address order),
+// four per iteration, the next iteration's four loads and the epilogue
+// inputs of its first two span ends issued before the current one is folded.
 template <class Op>
 __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh, uint32_t wn,
                                                  const CrcTables* __restrict__ g) {
   const UnitLane UL = unit_lane();
-  const uint32_t lane16 = 16u * UL.lane;
+  const uint32_t lane = UL.lane, lane16 = 16u * lane;
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
   typedef typename Op::Pre Pre;
-  UnitCursor q;
-  q.cv = false;
-  q.kc = 0;
-  q.nv = unit_take(wn, base, &q.N);
-  if (!q.nv) return;
-  q.C = q.N;
-  bool consumed;
-  UPlan P = unit_plan(q, &consumed);
-  Chunk cur = unit_load(P, lane16, UL.lane, zp);
-  // epilogue inputs of the item the plan ends, issued after its chunks in
-  // every iteration (a fixed number of loads per iteration keeps vmcnt exact)
-  const auto pre_of = [&](const UPlan& X) {
-    const uint4 d = unit_desc(X.At);
-    return unit_pre(op, sh.idx(X.At), base + (((uint64_t)d.y << 32) | d.x), d.z);
+  const uint32_t T = rfl(upre(wn));  // the window's units
+  const uint32_t W = blockDim.x >> 6, w = threadIdx.x >> 6;
+  const uint32_t gs = rfl((uint32_t)((uint64_t)T * w / W)), ge = rfl((uint32_t)((uint64_t)T * (w + 1) / W));
+  if (gs >= ge) return;
+  uint32_t tc = 0;
+  // epilogue inputs of the plan's first two span ends (any span when fewer:
+  // a fixed number of loads per iteration keeps vmcnt exact)
+  const auto pre_of = [&](const USlots& X, uint32_t e) {
+    // (a select chain, not X.t[e]: a runtime index would put the plan in scratch)
+    const uint32_t t = e == 0 ? X.t[0] : e == 1 ? X.t[1] : e == 2 ? X.t[2] : X.t[3];
+    const uint4 d = unit_desc(t);
+    return unit_pre(op, sh.idx(t), base + (((uint64_t)d.y << 32) | d.x), d.z);
   };
-  Pre pre = pre_of(P);
-  if (consumed) q.nv = unit_take(wn, base, &q.N);
+  const auto ends = [](const USlots& X, uint32_t* e0, uint32_t* e1) {
+    const uint32_t m = (X.flags / kUEnd) & 15u;
+    *e0 = m ? (uint32_t)__builtin_ctz(m) : 0u;
+    const uint32_t m1 = m & (m - 1);
+    *e1 = m1 ? (uint32_t)__builtin_ctz(m1) : *e0;
+  };
+  USlots P = unit_slots(gs, gs, ge, tc, base, lane);
+  Chunk cur = unit_load(P, lane16, lane, zp);
+  uint32_t e0, e1;
+  ends(P, &e0, &e1);
+  Pre pre0 = pre_of(P, e0), pre1 = pre_of(P, e1);
   uint32_t s = 0;
-  while (P.na) {
-    bool cn;
-    const UPlan Q = unit_plan(q, &cn);
-    const Chunk nxt = unit_load(Q, lane16, UL.lane, zp);
-    const Pre pn = pre_of(Q);
-    if (cn) q.nv = unit_take(wn, base, &q.N);
-    uint32_t sA = s;
+  for (uint32_t g0 = gs; g0 < ge; g0 += 4) {
+    const USlots Q = unit_slots(g0 + 4, gs, ge, tc, base, lane);
+    const Chunk nxt = unit_load(Q, lane16, lane, zp);
+    uint32_t q0, q1;
+    ends(Q, &q0, &q1);
+    const Pre pn0 = pre_of(Q, q0), pn1 = pre_of(Q, q1);
     const uint32_t f = P.flags;
+    uint32_t se[4];  // the lane state after each slot (the span ends' states)
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
       uint4 v = cur.v[j];
       uint32_t extra = 0;
       if (f & (kUHead << j)) {  // wave-uniform: the head unit of a span
-        const uint32_t h = j < P.na ? P.hA : P.hB;
-        if (UL.lane == (h & 255u)) {
-          unit_mask_head(v, (h >> 8) & 15u);
-          extra = j < P.na ? P.injA : P.injB;
+        if (lane == (P.h[j] & 255u)) {
+          unit_mask_head(v, (P.h[j] >> 8) & 15u);
+          extra = P.inj[j];
         }
       }
-      if ((f & (kUTail << j)) && UL.lane == 63) unit_mask_tail(v, P.hA >> 16);
+      if ((f & (kUTail << j)) && lane == 63) unit_mask_tail(v, P.h[j] >> 16);
       // a unit's first piece: zshift(state, 1012) ^ w0 -- from state 0 (and
-      // the init injected at the head piece) when an item starts here
+      // the init injected at the head piece) when a portion starts here
       uint32_t x = crc_gap4x((f & (kUFirst << j)) ? 0u : s, UL, v.x ^ extra);
       x = crc_step4x(x, UL.S, v.y);
       x = crc_step4x(x, UL.S, v.z);
       s = crc_step4x(x, UL.S, v.w);
-      if (j + 1 == P.na) sA = s;  // A's last unit in this plan
+      se[j] = s;
     }
-    if (f & kUAEnd) unit_flush(op, sh, base, P.At, P.Am, sA, pre, UL, g);
+    // the portions that end in this iteration (one code copy for all four)
+    uint32_t nend = 0;
+    for (uint32_t m = (f / kUEnd) & 15u; m; m &= m - 1, nend++) {
+      const uint32_t j = (uint32_t)__builtin_ctz(m);
+      const uint32_t sj = j == 0 ? se[0] : j == 1 ? se[1] : j == 2 ? se[2] : se[3];
+      const uint32_t tj = j == 0 ? P.t[0] : j == 1 ? P.t[1] : j == 2 ? P.t[2] : P.t[3];
+      const Pre pr = nend == 0 ? pre0 : nend == 1 ? pre1 : pre_of(P, j);
+      unit_flush(op, sh, base, tj, P.g0 + j, sj, pr, gs, ge, UL, g);
+    }
     P = Q;
     cur = nxt;
-    pre = pn;
+    pre0 = pn0;
+    pre1 = pn1;
   }
 }
 
 // Ragged batch [first, first + count): workgroup b owns the contiguous
 // range [count b / G, count (b + 1) / G) (BLK) or spans b, b + G, ...;
-// processed in windows of kUDescCache descriptors.
+// processed in windows of kUDescCache descriptors.  A window's units are
+// cut into W equal streams, one per wave: every wave gets the same number of
+// units (no tickets), and a span longer than a stream is simply shared by
+// the neighbouring streams.
 template <class Op, bool BLK>
 __device__ __forceinline__ void crc_units_driver(const Op& op, uint32_t first, uint32_t count,
                                                  const CrcTables* __restrict__ g) {
@@ -522,25 +458,51 @@ __device__ __forceinline__ void crc_units_driver(const Op& op, uint32_t first, u
   }
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   const int kind = op.init_kind();
+  const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wpb = blockDim.x >> 6;
   __syncthreads();  // the un-shift tables are read by the staging
   for (uint32_t w0 = 0; w0 < n; w0 += kUDescCache) {
     const uint32_t wn = n - w0 < kUDescCache ? n - w0 : kUDescCache;
     const UShare sh{start + stride * w0, stride};
     if (w0) __syncthreads();  // the previous window's waves are done with its slots
-    for (uint32_t t = threadIdx.x; t < wn; t += blockDim.x) {
-      const uint32_t i = sh.idx(t);
-      const uint64_t off = op.off(i);
-      const uint32_t len = (uint32_t)op.len(i);
-      const uint32_t init = unit_init(op, kind, op.init_key(i));
-      const uint32_t hb = (uint32_t)(base + off) & 15u;
-      const uint32_t inj = hb ? unit_unshift(hb, ~init) : ~init;
-      const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, inj};
-      *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kULdsDesc + 16 * t)) = d;
-      *lds_p64(kULdsAcc + 8 * t) = 0;
-      // Extend(init, "") = init: empty spans finish here (the ticket skips them)
-      if (len == 0) op.finish(i, init, op.pre(i, base + off, 0), true);
+    // descriptors, accumulators, and the units' exclusive prefix (a chunk of
+    // blockDim spans at a time); padded with ~0 for the streams' lookahead
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < wn; c0 += blockDim.x) {
+      const uint32_t t = c0 + threadIdx.x;
+      uint32_t u = 0;
+      if (t < wn) {
+        const uint32_t i = sh.idx(t);
+        const uint64_t off = op.off(i);
+        const uint32_t len = (uint32_t)op.len(i);
+        const uint32_t init = unit_init(op, kind, op.init_key(i));
+        const uint32_t hb = (uint32_t)(base + off) & 15u;
+        const uint32_t inj = hb ? unit_unshift(hb, ~init) : ~init;
+        const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, inj};
+        *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kULdsDesc + 16 * t)) = d;
+        *lds_p64(kULdsAcc + 8 * t) = 0;
+        u = unit_count(base + off, len);
+        // Extend(init, "") = init: empty spans (no units) finish here
+        if (len == 0) op.finish(i, init, op.pre(i, base + off, 0), true);
+      }
+      uint32_t x = u;
+#pragma unroll
+      for (int dd = 1; dd < 64; dd <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, dd, 64);
+        x += lane >= (uint32_t)dd ? y : 0u;
+      }
+      if (lane == 63) *lds_p32(kULdsWaveSum + 4 * wid) = x;
+      __syncthreads();
+      uint32_t below = 0, tot = 0;
+      for (uint32_t q = 0; q < wpb; q++) {
+        const uint32_t ws = *lds_p32(kULdsWaveSum + 4 * q);
+        below += q < wid ? ws : 0u;
+        tot += ws;
+      }
+      if (t < wn) *lds_p32(kULdsUpre + 4 * t) = carry + below + x - u;
+      carry += tot;
+      __syncthreads();
     }
-    if (threadIdx.x == 0) *lds_p64(kULdsTicket) = 0;
+    if (threadIdx.x <= 64) *lds_p32(kULdsUpre + 4 * (wn + threadIdx.x)) = threadIdx.x ? 0xFFFFFFFFu : carry;
     __syncthreads();
     crc_units_window(op, sh, wn, g);
   }

@@ -1022,6 +1022,17 @@ __device__ __forceinline__ uint32_t crc_span_wave(const uint8_t* p, uint64_t n, 
   return crc_finish(s, sp, L);
 }
 
+// The block's first header comes from a 16-byte vector load issued while
+// the previous block is hashed (one memory round trip per 32 KiB block
+// saved: configs[3] blocks hold one record each, whose ~8 CRC rounds the
+// header read used to precede); later records of a block read theirs on
+// demand.  A 16-byte load at a block start stays in the 16-byte granule
+// holding the block's first byte, so it never leaves the image's pages.
+__device__ __forceinline__ uint4 wal_hdr16(const uint8_t* wal, uint32_t b) {
+  return vload16_any(reinterpret_cast<uint64_t>(wal) + (uint64_t)b * 32768);
+}
+__device__ __forceinline__ uint32_t rfl_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
 template <bool T>
 __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_t nbytes, uint32_t log_number,
                                                      WalResult* res, uint32_t nblocks) {
@@ -1031,7 +1042,12 @@ __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_
   const CrcLane L = crc_lane();
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t nw = gridDim.x * wpb;
-  for (uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6)); b < nblocks; b += nw) {
+  uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+  if (b >= nblocks) return;
+  uint4 nh = wal_hdr16(wal, b);
+  for (; b < nblocks; b += nw) {
+    const uint4 h0 = nh;
+    nh = wal_hdr16(wal, b + nw < nblocks ? b + nw : b);  // the next block's first header
     const uint8_t* blk = wal + (uint64_t)b * 32768;
     const uint64_t rem = nbytes - (uint64_t)b * 32768;
     const uint32_t size = rem < 32768 ? (uint32_t)rem : 32768u;
@@ -1047,8 +1063,19 @@ __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_
         break;
       }
       const uint8_t* h = blk + pos;
-      const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
-      const uint32_t type = h[6];
+      // header words: [0, 4) CRC, [4, 6) length, 6 type, [7, 11) log number
+      uint32_t w0, w1, w2;
+      if (pos == 0) {
+        w0 = rfl_u32(h0.x);
+        w1 = rfl_u32(h0.y);
+        w2 = rfl_u32(h0.z);
+      } else {
+        w0 = rd32_bytes(h);
+        w1 = (uint32_t)h[4] | ((uint32_t)h[5] << 8) | ((uint32_t)h[6] << 16);
+        w2 = 0;
+      }
+      const uint32_t length = w1 & 0xFFFFu;
+      const uint32_t type = (w1 >> 16) & 0xFFu;
       uint32_t hsize = 7;
       if ((type >= 5 && type <= 8) || type == 11) {
         hsize = 11;
@@ -1056,7 +1083,8 @@ __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_
           if (last_block) status = 5;
           break;
         }
-        if (rd32_bytes(h + 7) != log_number) {
+        const uint32_t lognum = pos == 0 ? (w1 >> 24) | (w2 << 8) : rd32_bytes(h + 7);
+        if (lognum != log_number) {
           status = 4;  // kOldRecord
           break;
         }
@@ -1069,7 +1097,7 @@ __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_
         status = 3;  // kZeroType, length 0: buffer cleared
         break;
       }
-      const uint32_t stored = rd32_bytes(h);
+      const uint32_t stored = w0;
       const uint32_t actual = crc_span_wave<T>(h + 6, length + hsize - 6, 0u, L);
       // Unmask(stored) == actual  <=>  stored == Mask(actual)
       if (crc_mask(actual) != stored) {

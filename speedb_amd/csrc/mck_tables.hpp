@@ -24,9 +24,10 @@ constexpr int kMaxUnshift = 64;                                 // k in [0,64)
 // bytes apart between rounds.
 constexpr int kRowWidths = 3;  // W = 4 << k
 constexpr int row_gap_bytes(int k) { return (4 << k) * kChunkBytes - kChunkBytes; }
-// Unit-stream driver: spans are cut into 16 KiB pieces; a piece's partial
-// state is moved to the span end by zshift(16384 m), m < 2^18 (spans < 4 GiB).
-constexpr int kPowBits = 18;
+// Unit-stream driver: a span shared by several waves' streams has each
+// portion's state moved to the span end by zshift(1024 m), m < 2^22 units
+// (spans < 4 GiB).
+constexpr int kPowBits = 22;
 
 struct alignas(16) CrcTables {
   uint32_t step[4][256];          // zshift(v << 8t, 4): the 4-byte step
@@ -51,7 +52,7 @@ struct alignas(16) CrcTables {
   // 16-aligned end
   uint32_t gap1012[4][256];           // zshift(v << 8t, 4 + 1008): piece to the lane's next piece
   uint32_t ulane_final[8][16][64];    // zshift(v << 4n, 4 + 16 (63 - l)): to the unit's end
-  uint32_t pow16k[kPowBits][8][16];   // zshift(v << 4n, 16384 * 2^b): span pieces to the span end
+  uint32_t pow1k[kPowBits][8][16];    // zshift(v << 4n, 1024 * 2^b): stream portions to the span end
 };
 
 // ---- host-side GF(2) helpers (also used by the host shims) ----------------
@@ -135,9 +136,9 @@ inline void build_crc_tables(CrcTables* t) {
       for (int v = 0; v < 16; v++) t->ulane_final[n][v][l] = gf_mul((uint32_t)v << (4 * n), k);
   }
   for (int b = 0; b < kPowBits; b++) {
-    const uint32_t k = gf_xpow8n(16384ull << b);
+    const uint32_t k = gf_xpow8n(1024ull << b);
     for (int n = 0; n < 8; n++)
-      for (int v = 0; v < 16; v++) t->pow16k[b][n][v] = gf_mul((uint32_t)v << (4 * n), k);
+      for (int v = 0; v < 16; v++) t->pow1k[b][n][v] = gf_mul((uint32_t)v << (4 * n), k);
   }
   for (int k = 0; k < kMaxUnshift; k++)
     for (int n = 0; n < 8; n++)

@@ -1,14 +1,15 @@
 """The unit-stream CRC driver (mck_crc_units.hpp) against the oracle.
 
 k_crc_auto sends a workgroup whose share has a mean span above 2.5 KiB to
-the unit stream: 1 KiB units anchored at each span's 16-aligned end, four
-units per wave iteration across span boundaries, spans of more than 24
-units split into 16 KiB pieces joined through an LDS accumulator.  The
-cases below are the shapes that stress it: SST data blocks (4096 + 0..255
-bytes + the type byte, never 16-aligned), uniform non-aligned strides,
-every span length around the unit / piece / split boundaries, long spans
-(many pieces per span, pieces of one span finishing on different waves),
-empty spans inside a long-span batch, non-zero Extend inits.  The unit
+the unit stream: 1 KiB units anchored at each span's 16-aligned end, the
+window's units cut into one equal stream per wave, four units per wave
+iteration across span boundaries; a span cut by stream boundaries is
+joined through an LDS accumulator (portions moved to the span end by
+zshift(1024 m)).  The cases below are the shapes that stress it: SST data
+blocks (4096 + 0..255 bytes + the type byte, never 16-aligned), uniform
+non-aligned strides, every span length around the unit / iteration
+boundaries, long spans (shared by many streams, portions finishing on
+different waves), runs of empty spans, non-zero Extend inits.  The unit
 stream forced on every generic CRC test (short spans, WAL, blob) and these
 tests with the interleaved span order: test_crc_rows.py
 test_auto_kernel_forced_drivers_subprocess.  Bit-exact throughout."""
@@ -82,9 +83,9 @@ def test_units_uniform_unaligned_stride(gpu, oracle, stride):
 
 
 def test_units_boundary_lengths(gpu, oracle):
-    """Lengths around the 1 KiB unit, the 4-unit iteration, the 24-unit split
-    threshold and the 16 KiB piece boundaries, at every start alignment,
-    mixed with 3-8 KiB spans so the workgroups choose the unit stream."""
+    """Lengths around the 1 KiB unit, the 4-unit iteration and multiples of
+    16 units, at every start alignment, mixed with 3-8 KiB spans so the
+    workgroups choose the unit stream."""
     import speedb_amd as S
     torch = gpu
     rnd = random.Random(11)
@@ -107,8 +108,9 @@ def test_units_boundary_lengths(gpu, oracle):
 
 
 def test_units_long_spans_split(gpu, oracle):
-    """Spans of 25 units to 4 MiB (up to 256 pieces each, pieces of one span
-    on different waves), empty spans and short spans in between."""
+    """Spans of 25 units to 4 MiB (a 4 MiB span is longer than a whole
+    window's stream: shared by all 16 waves), empty spans and short spans in
+    between."""
     import speedb_amd as S
     torch = gpu
     rnd = random.Random(23)
@@ -127,8 +129,30 @@ def test_units_long_spans_split(gpu, oracle):
         assert ext[i] == oracle.Extend(inits[i], d), (i, o, n)
 
 
+def test_units_runs_of_empty_spans(gpu, oracle):
+    """Runs of 0..200 empty spans between 3-9 KiB spans: a stream's lookahead
+    over the units' prefix passes more than 63 empty spans at once."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(57)
+    lens = []
+    for _ in range(600):
+        lens += [0] * rnd.choice([0, 0, 1, 5, 63, 64, 65, 130, 200])
+        lens.append(rnd.randrange(3000, 9000))
+    host, dev, offs = _pack(torch, 57, lens, gap=8)
+    sp = _spans(torch, S, dev, offs, lens)
+    inits = [rnd.getrandbits(32) for _ in lens]
+    got = _u32(S.crc32c_batch(sp))
+    ext = _u32(S.crc32c_batch(sp, init_crcs=torch.tensor(np.array(inits, dtype=np.uint32).view(np.int32),
+                                                          device="cuda")))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        d = host[o:o + n]
+        assert got[i] == oracle.Value(d), (i, o, n)
+        assert ext[i] == oracle.Extend(inits[i], d), (i, o, n)
+
+
 def test_units_many_windows(gpu, oracle):
-    """More spans per workgroup than one LDS descriptor window (960): the
+    """More spans per workgroup than one LDS descriptor window (832): the
     share is processed in several windows, and in several launches."""
     import speedb_amd as S
     torch = gpu
@@ -150,9 +174,9 @@ def test_units_many_windows(gpu, oracle):
 @pytest.mark.parametrize("ctype", [1, 4])
 def test_units_sst_verify_mix(gpu, oracle, ctype):
     """VerifyBlockChecksum over a compaction mix of 4/16/64 KiB blocks with
-    jitter (split 64 KiB blocks: the epilogue runs on whichever wave finishes
-    the last piece -- the CRC unit stream, and for kXXH3 the wave driver's
-    pieces), context checksums, then flipped bytes."""
+    jitter (64 KiB blocks cut by stream boundaries: the epilogue runs on
+    whichever wave finishes the last portion -- the CRC unit stream, and for
+    kXXH3 the wave driver's pieces), context checksums, then flipped bytes."""
     import speedb_amd as S
     torch = gpu
     rnd = random.Random(77)
