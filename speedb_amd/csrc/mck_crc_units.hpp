@@ -234,23 +234,39 @@ struct USlots {
 
 // Plan the slots of units g0 .. g0 + 3 of stream [gs, ge); tc = a span at or
 // before the span of unit g0 (advanced here).
-__device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t ge, uint32_t& tc, uint64_t base,
-                                             uint32_t lane) {
+__device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t ge, uint32_t wn, uint32_t& tc,
+                                             uint64_t base, uint32_t lane) {
   USlots P;
   P.g0 = g0;
-  // spans tc + 1 + lane: the units before g0 + j belong to spans counted by
-  // the ballot (empty spans included, the window's upre padded with ~0)
+  // spans tc + 1 + lane: the spans that start at or before unit g are
+  // counted by a ballot over the window's unit prefix (empty spans included,
+  // the prefix padded with ~0); tc stays at or before the span of g0
   uint32_t v = upre(tc + 1 + lane);
-  uint32_t c3 = (uint32_t)__popcll(__ballot(v <= g0 + 3));
-  while (c3 == 64) {  // more than 63 spans end before g0 + 3 (empty spans): skip ahead
+  uint32_t c0 = (uint32_t)__popcll(__ballot(v <= g0));
+  while (c0 == 64) {  // 64 or more spans start in (tc, g0]: skip ahead
     tc += 64;
     v = upre(tc + 1 + lane);
-    c3 = (uint32_t)__popcll(__ballot(v <= g0 + 3));
+    c0 = (uint32_t)__popcll(__ballot(v <= g0));
   }
-  const uint32_t t0 = tc + (uint32_t)__popcll(__ballot(v <= g0));
-  const uint32_t t1 = tc + (uint32_t)__popcll(__ballot(v <= g0 + 1));
-  const uint32_t t2 = tc + (uint32_t)__popcll(__ballot(v <= g0 + 2));
-  const uint32_t t3 = tc + c3;
+  // the later slots from the same lookahead; a full count (64 spans starting
+  // in (tc, g0 + j]: runs of empty spans) walks on from tc + 64
+  const auto span_at = [&](uint32_t gj) {
+    uint32_t c = (uint32_t)__popcll(__ballot(v <= gj));
+    uint32_t tb = tc;
+    while (c == 64) {
+      tb += 64;
+      c = (uint32_t)__popcll(__ballot(upre(tb + 1 + lane) <= gj));
+    }
+    return tb + c;
+  };
+  // slots past the window's last unit (the last stream's final plan) count
+  // upre(wn) = T too: clamp them to the last span, so every descriptor and
+  // epilogue load such a slot issues is a real span's
+  const uint32_t tl = wn - 1;
+  const uint32_t t0 = min(tc + c0, tl);
+  const uint32_t t1 = min(span_at(g0 + 1), tl);
+  const uint32_t t2 = min(span_at(g0 + 2), tl);
+  const uint32_t t3 = min(span_at(g0 + 3), tl);
   P.t[0] = t0;
   P.t[1] = t1;
   P.t[2] = t2;
@@ -260,7 +276,7 @@ __device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t 
   const uint32_t g = g0 + j;
   const bool live = g < ge;
   const uint32_t t = j == 0 ? t0 : j == 1 ? t1 : j == 2 ? t2 : t3;
-  const uint4 d = unit_desc(live ? t : t0);
+  const uint4 d = unit_desc(t);
   const uint32_t u0 = upre(t), u1 = upre(t + 1);
   const uint64_t ptr = base + (((uint64_t)d.y << 32) | d.x);
   const uint64_t a1 = (ptr + d.z + 15) & ~15ull;
@@ -385,14 +401,14 @@ __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh,
     const uint32_t m1 = m & (m - 1);
     *e1 = m1 ? (uint32_t)__builtin_ctz(m1) : *e0;
   };
-  USlots P = unit_slots(gs, gs, ge, tc, base, lane);
+  USlots P = unit_slots(gs, gs, ge, wn, tc, base, lane);
   Chunk cur = unit_load(P, lane16, lane, zp);
   uint32_t e0, e1;
   ends(P, &e0, &e1);
   Pre pre0 = pre_of(P, e0), pre1 = pre_of(P, e1);
   uint32_t s = 0;
   for (uint32_t g0 = gs; g0 < ge; g0 += 4) {
-    const USlots Q = unit_slots(g0 + 4, gs, ge, tc, base, lane);
+    const USlots Q = unit_slots(g0 + 4, gs, ge, wn, tc, base, lane);
     const Chunk nxt = unit_load(Q, lane16, lane, zp);
     uint32_t q0, q1;
     ends(Q, &q0, &q1);
