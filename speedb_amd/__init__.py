@@ -6,6 +6,7 @@ C ABI (include/speedb_amd/mck.h) and built in-tree into
 speedb_amd/libspeedb_amd.so.  Importing this package without that library
 raises ImportError: there is no CPU fallback.
 """
+import torch  # noqa: F401  (torch's HIP runtime is mapped before the engine's dlopen, as the tests do)
 from . import _lib  # noqa: F401  (fails loudly if the engine is not built)
 from .checksum import *  # noqa: F401,F403
 from .checksum import __all__ as _checksum_all

@@ -216,24 +216,33 @@ struct UShare {
 
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
-// One iteration's four unit slots (wave-uniform, SGPRs), worked out
-// lane-parallel (lane j mod 4 computes slot j) and read back with
-// v_readlane / ballots: slot j is window unit g0 + j of the wave's stream.
-constexpr uint32_t kUFirst = 1u, kUHead = 16u, kUTail = 256u, kUEnd = 4096u;  // << slot
+// One iteration's NU unit slots, worked out lane-parallel (lane j mod NU
+// computes slot j): the load addresses come back as scalars (v_readlane),
+// the flags as ballots; the rest stays in the lanes and is read (v_readlane,
+// in wave-uniform branches) only by a head, tail or end slot.  Slot j is
+// window unit g0 + j of the wave's stream.
+#ifndef MCK_UNIT_SLOTS
+#define MCK_UNIT_SLOTS 8
+#endif
+constexpr uint32_t kUSlots = MCK_UNIT_SLOTS;
+static_assert(kUSlots == 4 || kUSlots == 8, "unit slots per iteration");
+// flags: 8 bits each, bit j = slot j
+constexpr uint32_t kUFirst = 1u, kUHead = 1u << 8, kUTail = 1u << 16, kUEnd = 1u << 24;
 struct USlots {
-  uint64_t base[4];   // slot j's unit: [base, base + 1 KiB)
-  uint32_t below[4];  // lanes below this load the zero piece (64: no unit)
-  uint32_t h[4];      // own | hb << 8 | kt << 16 of the slot's span
-  uint32_t inj[4];    // the span's injected init state (head slots)
-  uint32_t t[4];      // the slot's span (window slot)
-  uint32_t flags;     // kUFirst << j: the lane state restarts (span head or stream start);
-                      // kUHead << j: the span's head unit; kUTail << j: its last unit, with
-                      // bytes past the end; kUEnd << j: the stream's portion of the span ends
+  uint64_t base[kUSlots];   // slot j's unit: [base, base + 1 KiB)
+  uint32_t below[kUSlots];  // lanes below this load the zero piece (64: no unit)
+  uint32_t flags;           // kUFirst << j: the lane state restarts (span head or stream
+                            // start); kUHead << j: the span's head unit; kUTail << j: its
+                            // last unit, with bytes past the end; kUEnd << j: the stream's
+                            // portion of the span ends
   uint32_t g0;
+  // per lane (slot lane & (NU - 1)): own | hb << 8 | kt << 16, the injected
+  // init state, the window slot
+  uint32_t h, inj, t;
 };
 
-// Plan the slots of units g0 .. g0 + 3 of stream [gs, ge); tc = a span at or
-// before the span of unit g0 (advanced here).
+// Plan the slots of units g0 .. g0 + NU - 1 of stream [gs, ge); tc = a span
+// at or before the span of unit g0 (advanced here).
 __device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t ge, uint32_t wn, uint32_t& tc,
                                              uint64_t base, uint32_t lane) {
   USlots P;
@@ -249,33 +258,29 @@ __device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t 
     c0 = (uint32_t)__popcll(__ballot(v <= g0));
   }
   // the later slots from the same lookahead; a full count (64 spans starting
-  // in (tc, g0 + j]: runs of empty spans) walks on from tc + 64
-  const auto span_at = [&](uint32_t gj) {
-    uint32_t c = (uint32_t)__popcll(__ballot(v <= gj));
+  // in (tc, g0 + j]: runs of empty spans) walks on from tc + 64.  Slots past
+  // the window's last unit (the last stream's final plans) count upre(wn) =
+  // T too: they are clamped to the last span, so every descriptor and
+  // epilogue load such a slot issues is a real span's.
+  const uint32_t tl = wn - 1;
+  const uint32_t j = lane & (kUSlots - 1);
+  uint32_t t = min(tc + c0, tl), tlast = t;
+#pragma unroll
+  for (uint32_t q = 1; q < kUSlots; q++) {
+    const uint32_t gq = g0 + q;
+    uint32_t c = (uint32_t)__popcll(__ballot(v <= gq));
     uint32_t tb = tc;
     while (c == 64) {
       tb += 64;
-      c = (uint32_t)__popcll(__ballot(upre(tb + 1 + lane) <= gj));
+      c = (uint32_t)__popcll(__ballot(upre(tb + 1 + lane) <= gq));
     }
-    return tb + c;
-  };
-  // slots past the window's last unit (the last stream's final plan) count
-  // upre(wn) = T too: clamp them to the last span, so every descriptor and
-  // epilogue load such a slot issues is a real span's
-  const uint32_t tl = wn - 1;
-  const uint32_t t0 = min(tc + c0, tl);
-  const uint32_t t1 = min(span_at(g0 + 1), tl);
-  const uint32_t t2 = min(span_at(g0 + 2), tl);
-  const uint32_t t3 = min(span_at(g0 + 3), tl);
-  P.t[0] = t0;
-  P.t[1] = t1;
-  P.t[2] = t2;
-  P.t[3] = t3;
-  tc = t3;
-  const uint32_t j = lane & 3u;
+    const uint32_t tq = min(tb + c, tl);
+    t = j == q ? tq : t;
+    tlast = tq;
+  }
+  tc = tlast;
   const uint32_t g = g0 + j;
   const bool live = g < ge;
-  const uint32_t t = j == 0 ? t0 : j == 1 ? t1 : j == 2 ? t2 : t3;
   const uint4 d = unit_desc(t);
   const uint32_t u0 = upre(t), u1 = upre(t + 1);
   const uint64_t ptr = base + (((uint64_t)d.y << 32) | d.x);
@@ -286,29 +291,30 @@ __device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t 
   const uint32_t own = 64u * U - (uint32_t)((a1 - (ptr & ~15ull)) >> 4);
   const uint64_t ub = a1 - (uint64_t)kUnitBytes * (kk + 1);
   const uint32_t below = live ? (head ? own : 0u) : 64u;
-  const uint32_t h = own | (((uint32_t)ptr & 15u) << 8) | (kt << 16);
   const bool tail = live && kk == 0 && kt != 0;
   const bool first = live && (g == gs || head);
   const bool end = live && (g + 1 == ge || kk == 0);
-  P.flags = ((uint32_t)__ballot(first) & 15u) * kUFirst | ((uint32_t)__ballot(head) & 15u) * kUHead |
-            ((uint32_t)__ballot(tail) & 15u) * kUTail | ((uint32_t)__ballot(end) & 15u) * kUEnd;
+  constexpr uint32_t m = (1u << kUSlots) - 1u;
+  P.flags = ((uint32_t)__ballot(first) & m) * kUFirst | ((uint32_t)__ballot(head) & m) * kUHead |
+            ((uint32_t)__ballot(tail) & m) * kUTail | ((uint32_t)__ballot(end) & m) * kUEnd;
 #pragma unroll
-  for (int q = 0; q < 4; q++) {
-    P.base[q] = readlane_u64(ub, (uint32_t)q);
-    P.below[q] = readlane_u32(below, (uint32_t)q);
-    P.h[q] = readlane_u32(h, (uint32_t)q);
-    P.inj[q] = readlane_u32(d.w, (uint32_t)q);
+  for (uint32_t q = 0; q < kUSlots; q++) {
+    P.base[q] = readlane_u64(ub, q);
+    P.below[q] = readlane_u32(below, q);
   }
+  P.h = own | (((uint32_t)ptr & 15u) << 8) | (kt << 16);
+  P.inj = d.w;
+  P.t = t;
   return P;
 }
 
-// The four loads of plan P: lane l's piece of every slot's unit (the zero
-// piece for lanes before a span's head and for empty slots).  Straight-line,
-// so every load is unconditional and the waits exact.
-__device__ __forceinline__ Chunk unit_load(const USlots& P, uint32_t lane16, uint32_t lane, uint64_t zp) {
-  Chunk c;
+// The plan's loads: lane l's piece of every slot's unit (the zero piece for
+// lanes before a span's head and for empty slots).  Straight-line, so every
+// load is unconditional and the waits exact.
+__device__ __forceinline__ ChunkN<kUSlots> unit_load(const USlots& P, uint32_t lane16, uint32_t lane, uint64_t zp) {
+  ChunkN<kUSlots> c;
 #pragma unroll
-  for (int j = 0; j < 4; j++) c.v[j] = span_load16<true>(lane < P.below[j] ? zp : P.base[j] + lane16);
+  for (uint32_t j = 0; j < kUSlots; j++) c.v[j] = span_load16<true>(lane < P.below[j] ? zp : P.base[j] + lane16);
   return c;
 }
 
@@ -372,8 +378,8 @@ __device__ __forceinline__ void unit_flush(const Op& op, const UShare& sh, uint6
 
 // The wave's stream over one share window: units [gs, ge) of the window's
 // unit sequence (spans in window order, each span's units in address order),
-// four per iteration, the next iteration's four loads and the epilogue
-// inputs of its first two span ends issued before the current one is folded.
+// NU per iteration, the next iteration's loads and the epilogue inputs of its
+// first two span ends issued before the current one is folded.
 template <class Op>
 __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh, uint32_t wn,
                                                  const CrcTables* __restrict__ g) {
@@ -387,45 +393,43 @@ __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh,
   const uint32_t gs = rfl((uint32_t)((uint64_t)T * w / W)), ge = rfl((uint32_t)((uint64_t)T * (w + 1) / W));
   if (gs >= ge) return;
   uint32_t tc = 0;
-  // epilogue inputs of the plan's first two span ends (any span when fewer:
-  // a fixed number of loads per iteration keeps vmcnt exact)
-  const auto pre_of = [&](const USlots& X, uint32_t e) {
-    // (a select chain, not X.t[e]: a runtime index would put the plan in scratch)
-    const uint32_t t = e == 0 ? X.t[0] : e == 1 ? X.t[1] : e == 2 ? X.t[2] : X.t[3];
+  // epilogue inputs of span end number e of a plan (its first two: a fixed
+  // number of loads per iteration keeps vmcnt exact; fewer ends repeat one)
+  const auto end_slot = [](const USlots& X, uint32_t e) {
+    uint32_t m = X.flags / kUEnd;
+    if (e) m &= m - 1;
+    return m ? (uint32_t)__builtin_ctz(m) : 0u;
+  };
+  const auto pre_of = [&](const USlots& X, uint32_t j) {
+    const uint32_t t = readlane_u32(X.t, j);
     const uint4 d = unit_desc(t);
     return unit_pre(op, sh.idx(t), base + (((uint64_t)d.y << 32) | d.x), d.z);
   };
-  const auto ends = [](const USlots& X, uint32_t* e0, uint32_t* e1) {
-    const uint32_t m = (X.flags / kUEnd) & 15u;
-    *e0 = m ? (uint32_t)__builtin_ctz(m) : 0u;
-    const uint32_t m1 = m & (m - 1);
-    *e1 = m1 ? (uint32_t)__builtin_ctz(m1) : *e0;
-  };
   USlots P = unit_slots(gs, gs, ge, wn, tc, base, lane);
-  Chunk cur = unit_load(P, lane16, lane, zp);
-  uint32_t e0, e1;
-  ends(P, &e0, &e1);
-  Pre pre0 = pre_of(P, e0), pre1 = pre_of(P, e1);
+  ChunkN<kUSlots> cur = unit_load(P, lane16, lane, zp);
+  Pre pre0 = pre_of(P, end_slot(P, 0)), pre1 = pre_of(P, end_slot(P, 1));
   uint32_t s = 0;
-  for (uint32_t g0 = gs; g0 < ge; g0 += 4) {
-    const USlots Q = unit_slots(g0 + 4, gs, ge, wn, tc, base, lane);
-    const Chunk nxt = unit_load(Q, lane16, lane, zp);
-    uint32_t q0, q1;
-    ends(Q, &q0, &q1);
-    const Pre pn0 = pre_of(Q, q0), pn1 = pre_of(Q, q1);
+  for (uint32_t g0 = gs; g0 < ge; g0 += kUSlots) {
+    const USlots Q = unit_slots(g0 + kUSlots, gs, ge, wn, tc, base, lane);
+    const ChunkN<kUSlots> nxt = unit_load(Q, lane16, lane, zp);
+    const Pre pn0 = pre_of(Q, end_slot(Q, 0)), pn1 = pre_of(Q, end_slot(Q, 1));
     const uint32_t f = P.flags;
-    uint32_t se[4];  // the lane state after each slot (the span ends' states)
+    uint32_t se[kUSlots];  // the lane state after each slot (the span ends' states)
 #pragma unroll
-    for (uint32_t j = 0; j < 4; j++) {
+    for (uint32_t j = 0; j < kUSlots; j++) {
       uint4 v = cur.v[j];
       uint32_t extra = 0;
       if (f & (kUHead << j)) {  // wave-uniform: the head unit of a span
-        if (lane == (P.h[j] & 255u)) {
-          unit_mask_head(v, (P.h[j] >> 8) & 15u);
-          extra = P.inj[j];
+        const uint32_t h = readlane_u32(P.h, j);
+        if (lane == (h & 255u)) {
+          unit_mask_head(v, (h >> 8) & 15u);
+          extra = readlane_u32(P.inj, j);
         }
       }
-      if ((f & (kUTail << j)) && lane == 63) unit_mask_tail(v, P.h[j] >> 16);
+      if (f & (kUTail << j)) {
+        const uint32_t h = readlane_u32(P.h, j);
+        if (lane == 63) unit_mask_tail(v, h >> 16);
+      }
       // a unit's first piece: zshift(state, 1012) ^ w0 -- from state 0 (and
       // the init injected at the head piece) when a portion starts here
       uint32_t x = crc_gap4x((f & (kUFirst << j)) ? 0u : s, UL, v.x ^ extra);
@@ -434,14 +438,15 @@ __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh,
       s = crc_step4x(x, UL.S, v.w);
       se[j] = s;
     }
-    // the portions that end in this iteration (one code copy for all four)
+    // the portions that end in this iteration (one code copy for all)
     uint32_t nend = 0;
-    for (uint32_t m = (f / kUEnd) & 15u; m; m &= m - 1, nend++) {
+    for (uint32_t m = f / kUEnd; m; m &= m - 1, nend++) {
       const uint32_t j = (uint32_t)__builtin_ctz(m);
-      const uint32_t sj = j == 0 ? se[0] : j == 1 ? se[1] : j == 2 ? se[2] : se[3];
-      const uint32_t tj = j == 0 ? P.t[0] : j == 1 ? P.t[1] : j == 2 ? P.t[2] : P.t[3];
+      uint32_t sj = se[0];
+#pragma unroll
+      for (uint32_t q = 1; q < kUSlots; q++) sj = j == q ? se[q] : sj;
       const Pre pr = nend == 0 ? pre0 : nend == 1 ? pre1 : pre_of(P, j);
-      unit_flush(op, sh, base, tj, P.g0 + j, sj, pr, gs, ge, UL, g);
+      unit_flush(op, sh, base, readlane_u32(P.t, j), P.g0 + j, sj, pr, gs, ge, UL, g);
     }
     P = Q;
     cur = nxt;

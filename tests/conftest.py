@@ -35,6 +35,11 @@ def pytest_configure(config):
         import sys
         if REPO not in sys.path:
             sys.path.insert(0, REPO)
+        # torch's HIP runtime first, as in every other process (the gpu
+        # fixture initialises torch before it imports speedb_amd): a child
+        # that loaded the engine first saw mck_device_count() == 0
+        import torch
+        torch.cuda.is_available()
         from speedb_amd import _lib
         _lib.check(_lib.lib.mck_test_set_crc_driver(CRC_DRIVERS.get(drv, 0), 1 if order == "interleaved" else 0),
                    "mck_test_set_crc_driver")
