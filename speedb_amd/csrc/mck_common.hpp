@@ -75,4 +75,64 @@ __device__ __forceinline__ uint32_t lds_ticket(P ctr) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(0, (int)t);
 }
 
+// Byte-balanced contiguous shares of a ragged batch of `count` spans.  A
+// share of spans b, b + G, ... (or of count / G consecutive spans) holds a
+// random number of the big spans: in a compaction-shaped 4/16/64 KiB mix of
+// 1 GiB the fullest of 256 shares carries 1.23x the mean bytes, and the
+// launch lasts as long as its workgroup.  Here every workgroup reads all the
+// lengths (a few hundred KiB at most, L2-resident after the first workgroup
+// of an XCD) and takes [lo, hi): span i belongs to workgroup b when the
+// batch offset of its first byte (the sum of the lengths before it) lies in
+// [total b / G, total (b + 1) / G).  All workgroups compute the same prefix,
+// so the ranges partition [0, count) exactly.  lds: blockDim / 64 u64.
+// Ends with a barrier.
+#ifndef MCK_BALANCE_MAX_SPANS
+#define MCK_BALANCE_MAX_SPANS (1u << 18)
+#endif
+constexpr uint32_t kBalanceMaxSpans = MCK_BALANCE_MAX_SPANS;  // beyond: shares by count (their bytes average out)
+template <class Len>
+__device__ __forceinline__ void balanced_range(Len len, uint32_t count, uint64_t* lds, uint32_t* lo, uint32_t* hi) {
+  const uint32_t nt = blockDim.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
+  const uint32_t per = (count + nt - 1) / nt;
+  const uint32_t c0 = min(tid * per, count), c1 = min(c0 + per, count);
+  uint64_t sum = 0;
+  for (uint32_t i = c0; i < c1; i++) sum += len(i);
+  uint64_t x = sum;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(x, d, 64);
+    x += lane >= (uint32_t)d ? y : 0ull;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  uint64_t below = 0, total = 0;
+  for (uint32_t w = 0; w < nw; w++) {
+    const uint64_t v = lds[w];
+    below += w < wid ? v : 0ull;
+    total += v;
+  }
+  __syncthreads();
+  const uint64_t G = gridDim.x, b = blockIdx.x;
+  const uint64_t tlo = total * b / G, thi = total * (b + 1) / G;
+  // spans whose first byte lies below tlo / thi (the prefix never decreases)
+  uint32_t nlo = 0, nhi = 0;
+  uint64_t p = below + x - sum;
+  if (p < thi) {
+    for (uint32_t i = c0; i < c1; i++) {
+      nlo += p < tlo ? 1u : 0u;
+      nhi += p < thi ? 1u : 0u;
+      p += len(i);
+    }
+  }
+  uint64_t r = ((uint64_t)nhi << 32) | nlo;
+  for (int m = 32; m >= 1; m >>= 1) r += __shfl_xor(r, m, 64);
+  if (lane == 0) lds[wid] = r;
+  __syncthreads();
+  uint64_t tot = 0;
+  for (uint32_t w = 0; w < nw; w++) tot += lds[w];
+  *lo = (uint32_t)tot;
+  *hi = (uint32_t)(tot >> 32);
+  __syncthreads();
+}
+
 }  // namespace mck

@@ -462,13 +462,17 @@ __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh,
 // units (no tickets), and a span longer than a stream is simply shared by
 // the neighbouring streams.
 template <class Op, bool BLK>
-__device__ __forceinline__ void crc_units_driver(const Op& op, uint32_t first, uint32_t count,
+__device__ __forceinline__ void crc_units_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                  const CrcTables* __restrict__ g) {
   crc_units_fill(g);
   const uint32_t G = gridDim.x, b = blockIdx.x;
   uint32_t start, stride, n;
   if (BLK) {
-    const uint32_t lo = (uint32_t)((uint64_t)count * b / G), hi = (uint32_t)((uint64_t)count * (b + 1) / G);
+    uint32_t lo = (uint32_t)((uint64_t)count * b / G), hi = (uint32_t)((uint64_t)count * (b + 1) / G);
+    // equal bytes per workgroup (the descriptor area is free until staging)
+    if (count <= kBalanceMaxSpans)
+      balanced_range([&](uint32_t i) { return op.len(first + i); }, count,
+                     reinterpret_cast<uint64_t*>(lds + kULdsDesc), &lo, &hi);
     start = first + lo;
     stride = 1;
     n = hi - lo;
@@ -553,7 +557,7 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
     mode = mean <= kAutoRows8Max ? 3 : mean <= kAutoUnitsMin ? 2 : 4;
   }
   if (mode == 4)
-    crc_units_driver<Op, BLK>(op, first, count, g);
+    crc_units_driver<Op, BLK>(op, first, count, lds, g);
   else
     crc_auto_driver<Op, T, BLK>(op, first, count, lds, g, mode);
 }

@@ -255,10 +255,7 @@ int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform) {
     // one workgroup per CU, spans dealt by LDS tickets
     const uint32_t wpb = kX3WaveThreads / 64;
     const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + wpb - 1) / wpb);
-    if ((count + grid - 1) / grid <= kX3DescCache)
-      hipLaunchKernelGGL((k_xxh3_wave<Op>), dim3(grid), dim3(kX3WaveThreads), 0, st, op, count);
-    else
-      hipLaunchKernelGGL((k_xxh3_wave_static<Op>), dim3(grid), dim3(kX3WaveThreads), 0, st, op, count);
+    hipLaunchKernelGGL((k_xxh3_wave<Op>), dim3(grid), dim3(kX3WaveThreads), 0, st, op, count);
   } else {
     // 16 rows (spans) per 256-thread workgroup
     const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 15) / 16);

@@ -242,10 +242,6 @@ template <class Op>
 __global__ __launch_bounds__(kX3WaveThreads) void k_xxh3_wave(Op op, uint32_t count) {
   xxh3_wave_driver<Op, false>(op, count, 0);
 }
-template <class Op>
-__global__ __launch_bounds__(kX3WaveThreads) void k_xxh3_wave_static(Op op, uint32_t count) {
-  xxh3_wave_static_driver<Op, false>(op, count, 0);
-}
 
 // XXH3 ops.  Both drivers call pre(i, ptr, hlen) with the span's loads (the
 // wave driver with every unit, the row driver with every segment) and

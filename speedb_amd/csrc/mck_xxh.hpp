@@ -519,10 +519,6 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
 }
 
 // ---- XXH3 / XXPH3, one WAVE per span ---------------------------------------
-// MCK_X3_FULL_ROUNDS=0 (A/B): interior units take the general unit path too.
-#ifndef MCK_X3_FULL_ROUNDS
-#define MCK_X3_FULL_ROUNDS 1
-#endif
 // For batches of KiB-sized blocks (SST): spans are dealt to waves like the
 // CRC engine, so a long span is not serialised on one 16-lane row and a
 // ragged batch balances over 4x fewer, 4x faster workers.
@@ -563,7 +559,7 @@ constexpr uint32_t kX3DescCache = 1024;
 // unit issues the same loads per lane -- six dword-aligned 16-byte loads and
 // three dwords for the realignment (rd_fix), clamped to the span's first
 // dwords where a load has no work -- all before any is used, so a unit costs
-// one HBM round trip (see xxh3_wave_loop; the next unit is not prefetched).
+// one HBM round trip (the next unit is not prefetched).
 struct X3WSpan {
   uint64_t ptr, len;
   uint32_t i;       // span index
@@ -701,45 +697,6 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
   a0 = X.i0;
   a1 = X.i1;
 }
-
-// Span feeds of the wave driver (compile-time variants, so the dynamic feed
-// has no global load that the in-order vmcnt would make wait behind the
-// prefetched unit):
-//   X3FeedPieces (below) -- the workgroup's share is staged in LDS; waves
-//                   take pieces of spans with an LDS ticket as they free up
-//                   (balanced in the CU);
-//   X3FeedStatic -- share too large for LDS: the wave walks positions
-//                   wid, wid + wpb, ... and fetches 64 descriptors at a time
-//                   (lane l: the l-th next), read back with v_readlane; a
-//                   span is not split.
-// Both skip short spans (done before the loop).
-struct X3FeedStatic {
-  uint32_t t, k, n, b, G, wpb;
-  uint64_t base;
-  uint64_t d_off;  // per lane: descriptor of position t + lane * wpb
-  uint32_t d_len;
-  template <class Op, bool PREVIEW>
-  __device__ __forceinline__ bool next(const Op& op, X3WSpan& sp) {
-    for (;;) {
-      if (k == 64) {  // refill: the wave's next 64 positions
-        const uint32_t tl = t + (uint32_t)(threadIdx.x & 63) * wpb;
-        d_off = tl < n ? op.off(b + G * tl) : 0;
-        d_len = tl < n ? (uint32_t)op.hlen(b + G * tl) : 0;
-        k = 0;
-      }
-      if (t >= n) return false;
-      const uint64_t len = readlane_u32(d_len, k);
-      const uint64_t off = readlane_u64(d_off, k);
-      const uint32_t i = b + G * t;
-      t += wpb;
-      k++;
-      if (len > 240) {
-        sp = x3w_span<PREVIEW>(base + off, len, i);
-        return true;
-      }
-    }
-  }
-};
 
 // Every unit issues all its loads -- the four round loads, the lone partial
 // segment, the last stripe and the epilogue inputs -- before any is used, so
@@ -939,98 +896,72 @@ __device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, c
   }
 }
 
-template <class Op, bool PREVIEW, class Feed>
-__device__ __forceinline__ void xxh3_wave_loop(const Op& op, Feed& f, const X3Row& X) {
-  X3WSpan cur;
-  while (f.template next<Op, PREVIEW>(op, cur)) {
-    uint64_t a0 = X.i0, a1 = X.i1;
-#if MCK_X3_FULL_ROUNDS
-    for (uint32_t k = 0; k + 1 < cur.units; k++) x3w_full_round<PREVIEW>(cur, k, X, a0, a1);
-    {
-      const uint32_t k = cur.units - 1;
-#else
-    for (uint32_t k = 0; k < cur.units; k++) {
-#endif
-      const X3WLoads L = x3w_load(cur, k, X);
-      const typename Op::Pre e = op.pre(cur.i, cur.ptr, cur.len);
-      x3w_fold<Op, PREVIEW>(op, cur, k, L, X, a0, a1, e);
-    }
-  }
-}
-
-// Short spans (<= 240 bytes: the three small-input classes) first, one per
-// lane -- outside the pipelined loop.
-template <class Op, bool PREVIEW, class Len, class Off>
-__device__ __forceinline__ void x3w_short_spans(const Op& op, uint32_t n, uint32_t b, uint32_t G, uint64_t seed,
-                                                Len len_of, Off off_of) {
-  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  for (uint32_t tt = threadIdx.x; tt < n; tt += blockDim.x) {
-    const uint64_t len = len_of(tt);
-    if (len <= 240) {
-      const uint8_t* p = reinterpret_cast<const uint8_t*>(base + off_of(tt));
-      op.finish(b + G * tt, PREVIEW ? xxph3_short(p, len, seed) : xxh3_short(p, len));
-    }
-  }
-}
-
-// The workgroup's share (spans b, b + G, ...) fits the LDS descriptor cache
-// (host: ceil(count / G) <= kX3DescCache): staged, long spans in pieces.
+// Workgroup b's share: a contiguous range of the batch with equal bytes per
+// workgroup (balanced_range; beyond kBalanceMaxSpans spans, spans b, b + G,
+// ...), staged in windows of kX3DescCache spans, long spans in pieces.
 template <class Op, bool PREVIEW>
 __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, uint64_t seed) {
   const X3Row X = x3_row(seed);
   __shared__ X3Lds s;
   const uint32_t G = gridDim.x, b = blockIdx.x;
-  const uint32_t n = (count - b + G - 1) / G;
   const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
-  for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
-    s.off[t] = op.off(b + G * t);
-    s.len[t] = (uint32_t)op.hlen(b + G * t);
-    s.done[t] = 0;
+  uint32_t start = b, stride = G, n = count > b ? (count - b + G - 1) / G : 0;
+  if (count <= kBalanceMaxSpans) {
+    uint32_t lo, hi;
+    balanced_range([&](uint32_t i) { return op.hlen(i); }, count, reinterpret_cast<uint64_t*>(&s.acc[0][0]), &lo,
+                   &hi);
+    start = lo;
+    stride = 1;
+    n = hi - lo;
   }
-  if (threadIdx.x == 0) s.ctr = 0;
-  // pieces per span, exclusive prefix (a chunk of blockDim spans at a time)
-  uint32_t carry = 0;
-  for (uint32_t c0 = 0; c0 < n; c0 += blockDim.x) {
-    const uint32_t t = c0 + threadIdx.x;
-    const uint32_t v = t < n ? x3w_pieces<PREVIEW>(op.hlen(b + G * t)) : 0;
-    uint32_t x = v;
+  for (uint32_t w0 = 0; w0 < n; w0 += kX3DescCache) {
+    const uint32_t wn = n - w0 < kX3DescCache ? n - w0 : kX3DescCache;
+    const uint32_t wb = start + stride * w0;  // span of window slot t: wb + stride t
+    if (w0) __syncthreads();  // the previous window's waves are done with its slots
+    for (uint32_t t = threadIdx.x; t < wn; t += blockDim.x) {
+      s.off[t] = op.off(wb + stride * t);
+      s.len[t] = (uint32_t)op.hlen(wb + stride * t);
+      s.done[t] = 0;
+    }
+    if (threadIdx.x == 0) s.ctr = 0;
+    // pieces per span, exclusive prefix (a chunk of blockDim spans at a time)
+    uint32_t carry = 0;
+    for (uint32_t c0 = 0; c0 < wn; c0 += blockDim.x) {
+      const uint32_t t = c0 + threadIdx.x;
+      const uint32_t v = t < wn ? x3w_pieces<PREVIEW>(op.hlen(wb + stride * t)) : 0;
+      uint32_t x = v;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
-      x += lane >= (uint32_t)d ? y : 0u;
+      for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        x += lane >= (uint32_t)d ? y : 0u;
+      }
+      if (lane == 63) s.wsum[wid] = x;
+      __syncthreads();
+      uint32_t below = 0, tot = 0;
+      for (uint32_t w = 0; w < wpb; w++) {
+        const uint32_t ws = s.wsum[w];
+        below += w < wid ? ws : 0u;
+        tot += ws;
+      }
+      if (t < wn) s.pre[t] = carry + below + x - v;
+      carry += tot;
+      __syncthreads();
     }
-    if (lane == 63) s.wsum[wid] = x;
+    if (threadIdx.x == 0) s.pre[wn] = carry;
     __syncthreads();
-    uint32_t below = 0, tot = 0;
-    for (uint32_t w = 0; w < wpb; w++) {
-      const uint32_t ws = s.wsum[w];
-      below += w < wid ? ws : 0u;
-      tot += ws;
+    // short spans (<= 240 bytes: the three small-input classes) first, one
+    // per lane -- outside the pipelined loop
+    const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+    for (uint32_t t = threadIdx.x; t < wn; t += blockDim.x) {
+      const uint64_t len = s.len[t];
+      if (len <= 240) {
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(base + s.off[t]);
+        op.finish(wb + stride * t, PREVIEW ? xxph3_short(p, len, seed) : xxh3_short(p, len));
+      }
     }
-    if (t < n) s.pre[t] = carry + below + x - v;
-    carry += tot;
-    __syncthreads();
+    X3FeedPieces f{&s, wn, wb, stride, 0, base};
+    xxh3_piece_loop<Op, PREVIEW>(op, f, X);
   }
-  if (threadIdx.x == 0) s.pre[n] = carry;
-  __syncthreads();
-  x3w_short_spans<Op, PREVIEW>(
-      op, n, b, G, seed, [&](uint32_t t) { return (uint64_t)s.len[t]; }, [&](uint32_t t) { return s.off[t]; });
-  X3FeedPieces f{&s, n, b, G, 0, reinterpret_cast<uint64_t>(op.base())};
-  xxh3_piece_loop<Op, PREVIEW>(op, f, X);
-}
-
-// A share too large for the cache: the waves walk it round-robin, whole
-// spans (a separate kernel: the two loops in one exceed 128 VGPRs).
-template <class Op, bool PREVIEW>
-__device__ __forceinline__ void xxh3_wave_static_driver(const Op& op, uint32_t count, uint64_t seed) {
-  const X3Row X = x3_row(seed);
-  const uint32_t G = gridDim.x, b = blockIdx.x;
-  const uint32_t n = (count - b + G - 1) / G;
-  const uint32_t wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
-  x3w_short_spans<Op, PREVIEW>(
-      op, n, b, G, seed, [&](uint32_t t) { return op.hlen(b + G * t); }, [&](uint32_t t) { return op.off(b + G * t); });
-  X3FeedStatic f{wid, 64, n, b, G, wpb, reinterpret_cast<uint64_t>(op.base()), 0, 0};
-  xxh3_wave_loop<Op, PREVIEW>(op, f, X);
 }
 
 // ---- legacy XXH32 / XXH64, one lane per span ----------------------------
