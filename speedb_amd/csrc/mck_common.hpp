@@ -83,15 +83,20 @@ __device__ __forceinline__ uint32_t lds_ticket(P ctr) {
 // lengths (a few hundred KiB at most, L2-resident after the first workgroup
 // of an XCD) and takes [lo, hi): span i belongs to workgroup b when the
 // batch offset of its first byte (the sum of the lengths before it) lies in
-// [total b / G, total (b + 1) / G).  All workgroups compute the same prefix,
-// so the ranges partition [0, count) exactly.  lds: blockDim / 64 u64.
-// Ends with a barrier.
+// [total b / G, total (b + 1) / G) (the last workgroup also takes trailing
+// empty spans).  Each boundary is then clamped to within `slack` spans of
+// the boundary by count (count b / G), which bounds a share at count / G +
+// 1 + 2 slack spans for drivers with a fixed descriptor cache.  All
+// workgroups compute the same prefix and the same clamps, so the ranges
+// partition [0, count) exactly.  lds: blockDim / 64 u64.  Ends with a
+// barrier.
 #ifndef MCK_BALANCE_MAX_SPANS
 #define MCK_BALANCE_MAX_SPANS (1u << 18)
 #endif
 constexpr uint32_t kBalanceMaxSpans = MCK_BALANCE_MAX_SPANS;  // beyond: shares by count (their bytes average out)
 template <class Len>
-__device__ __forceinline__ void balanced_range(Len len, uint32_t count, uint64_t* lds, uint32_t* lo, uint32_t* hi) {
+__device__ __forceinline__ void balanced_range(Len len, uint32_t count, uint32_t slack, uint64_t* lds, uint32_t* lo,
+                                               uint32_t* hi) {
   const uint32_t nt = blockDim.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
   const uint32_t per = (count + nt - 1) / nt;
   const uint32_t c0 = min(tid * per, count), c1 = min(c0 + per, count);
@@ -130,8 +135,13 @@ __device__ __forceinline__ void balanced_range(Len len, uint32_t count, uint64_t
   __syncthreads();
   uint64_t tot = 0;
   for (uint32_t w = 0; w < nw; w++) tot += lds[w];
-  *lo = (uint32_t)tot;
-  *hi = (uint32_t)(tot >> 32);
+  const auto clampb = [&](uint32_t x, uint64_t bb) {
+    const uint32_t c = (uint32_t)((uint64_t)count * bb / G);
+    const uint32_t a = c > slack ? c - slack : 0u, z = count - c > slack ? c + slack : count;
+    return x < a ? a : x > z ? z : x;
+  };
+  *lo = clampb((uint32_t)tot, b);
+  *hi = b + 1 == G ? count : clampb((uint32_t)(tot >> 32), b + 1);
   __syncthreads();
 }
 

@@ -992,9 +992,8 @@ __device__ __forceinline__ RowShare row_share(uint32_t first, uint32_t count) {
   return {first + b, G, (count - b + G - 1) / G};
 }
 
-template <class Op, bool BLK = false>
-__device__ __forceinline__ void row_desc_stage(const Op& op, uint32_t first, uint32_t count, bool total) {
-  const RowShare sh = row_share<BLK>(first, count);
+template <class Op>
+__device__ __forceinline__ void row_desc_stage(const Op& op, const RowShare& sh, bool total) {
   const uint32_t n = sh.n;
   uint64_t sum = 0, wsum = 0;
   for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
@@ -1045,26 +1044,24 @@ __device__ __forceinline__ uint4 row_desc(uint32_t t, uint32_t share) {
 
 // LDS prologue of the row (and auto) kernels: tables, descriptors, init
 // tables; ends with a barrier.
-template <bool BLK = false, class Op>
-__device__ __forceinline__ void crc_rows_prologue(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
+template <class Op>
+__device__ __forceinline__ void crc_rows_prologue(const Op& op, const RowShare& sh, uint8_t* lds,
                                                   const CrcTables* __restrict__ g, bool total) {
   crc_fill_rows(lds, g);
-  row_desc_stage<Op, BLK>(op, first, count, total);
+  row_desc_stage<Op>(op, sh, total);
   __syncthreads();
   row_init_tables(op);
   __syncthreads();
 }
 
-template <class Op, int W, bool BLK = false>
-__device__ __forceinline__ void crc_rows_loop(const Op& op, uint32_t first, uint32_t count,
-                                              const CrcTables* __restrict__ g) {
+template <class Op, int W>
+__device__ __forceinline__ void crc_rows_loop(const Op& op, const RowShare& sh, const CrcTables* __restrict__ g) {
   static_assert(W == 4 || W == 8 || W == 16, "row width");
   const int kind = op.init_kind();
   const CrcLane L = crc_lane();
   CrcLane Lf = L;
   const uint32_t c = threadIdx.x & (W - 1);
   Lf.lane4 = (64u - W + c) << 2;
-  const RowShare sh = row_share<BLK>(first, count);
   const uint32_t share = sh.n;  // this workgroup's spans
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   // the row's current span (ticket t) and the next one (ticket nt, prefetched)
@@ -1146,11 +1143,10 @@ struct FeedRowCache {
 constexpr uint32_t kAutoRows8Max = 640;    // mean span bytes
 constexpr uint32_t kAutoRows16Max = 2560;
 constexpr uint32_t kAutoRows16WasteMax = 8192;  // mean span bytes, with > 25 % of the wave rounds empty
-template <class Op, bool T, bool BLK = false>
-__device__ __forceinline__ void crc_auto_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
+template <class Op, bool T>
+__device__ __forceinline__ void crc_auto_driver(const Op& op, const RowShare& sh, uint8_t* lds,
                                                 const CrcTables* __restrict__ g, int force) {
-  crc_rows_prologue<BLK>(op, first, count, lds, g, true);
-  const RowShare sh = row_share<BLK>(first, count);
+  crc_rows_prologue<Op>(op, sh, lds, g, true);
   const uint32_t share = sh.n;
   const uint64_t total = *lds_p64(kLdsRowTotal);
   const uint64_t mean = total / (share ? share : 1);
@@ -1164,11 +1160,11 @@ __device__ __forceinline__ void crc_auto_driver(const Op& op, uint32_t first, ui
                    : ragged4k               ? 2
                                             : 1;
   if (mode == 5) {
-    crc_rows_loop<Op, 4, BLK>(op, first, count, g);
+    crc_rows_loop<Op, 4>(op, sh, g);
   } else if (mode == 3) {
-    crc_rows_loop<Op, 8, BLK>(op, first, count, g);
+    crc_rows_loop<Op, 8>(op, sh, g);
   } else if (mode == 2) {
-    crc_rows_loop<Op, 16, BLK>(op, first, count, g);
+    crc_rows_loop<Op, 16>(op, sh, g);
   } else {
     FeedRowCache<Op> f{sh, op.init_kind()};
     crc_drive<Op, FeedRowCache<Op>, T>(op, f, crc_lane());

@@ -461,26 +461,10 @@ __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh,
 // cut into W equal streams, one per wave: every wave gets the same number of
 // units (no tickets), and a span longer than a stream is simply shared by
 // the neighbouring streams.
-template <class Op, bool BLK>
-__device__ __forceinline__ void crc_units_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
-                                                 const CrcTables* __restrict__ g) {
+template <class Op>
+__device__ __forceinline__ void crc_units_driver(const Op& op, const RowShare& share, const CrcTables* __restrict__ g) {
   crc_units_fill(g);
-  const uint32_t G = gridDim.x, b = blockIdx.x;
-  uint32_t start, stride, n;
-  if (BLK) {
-    uint32_t lo = (uint32_t)((uint64_t)count * b / G), hi = (uint32_t)((uint64_t)count * (b + 1) / G);
-    // equal bytes per workgroup (the descriptor area is free until staging)
-    if (count <= kBalanceMaxSpans)
-      balanced_range([&](uint32_t i) { return op.len(first + i); }, count,
-                     reinterpret_cast<uint64_t*>(lds + kULdsDesc), &lo, &hi);
-    start = first + lo;
-    stride = 1;
-    n = hi - lo;
-  } else {
-    start = first + b;
-    stride = G;
-    n = count > b ? (count - b + G - 1) / G : 0;
-  }
+  const uint32_t start = share.start, stride = share.stride, n = share.n;
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   const int kind = op.init_kind();
   const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, wpb = blockDim.x >> 6;
@@ -542,9 +526,23 @@ constexpr uint32_t kAutoUnitsMin = 2560;  // mean span bytes
 template <class Op, bool T, bool BLK>
 __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                       const CrcTables* __restrict__ g, int force) {
+  // the workgroup's share -- every driver works on it, so whatever each
+  // workgroup chooses, the shares partition the batch: contiguous ranges of
+  // equal bytes (balanced_range) when the batch is ragged and small enough
+  // to scan, else by count
+  RowShare sh = row_share<BLK>(first, count);
+  if (BLK && count <= kBalanceMaxSpans) {
+    // the row drivers stage at most kRowDescCache descriptors: the host keeps
+    // count / G below it, the slack keeps every share within it
+    const uint32_t per = (uint32_t)(((uint64_t)count + gridDim.x - 1) / gridDim.x);
+    const uint32_t slack = per + 1 < kRowDescCache ? (kRowDescCache - per - 1) / 2 : 0u;
+    uint32_t lo, hi;
+    balanced_range([&](uint32_t i) { return op.len(first + i); }, count, slack,
+                   reinterpret_cast<uint64_t*>(lds + kULdsDesc), &lo, &hi);
+    sh = RowShare{first + lo, 1u, hi - lo};
+  }
   int mode = force;
   if (!mode) {
-    const RowShare sh = row_share<BLK>(first, count);
     uint64_t sum = 0;
     for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) sum += op.len(sh.idx(t));
     for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 64);
@@ -557,9 +555,9 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
     mode = mean <= kAutoRows8Max ? 3 : mean <= kAutoUnitsMin ? 2 : 4;
   }
   if (mode == 4)
-    crc_units_driver<Op, BLK>(op, first, count, lds, g);
+    crc_units_driver<Op>(op, sh, g);
   else
-    crc_auto_driver<Op, T, BLK>(op, first, count, lds, g, mode);
+    crc_auto_driver<Op, T>(op, sh, lds, g, mode);
 }
 
 }  // namespace mck

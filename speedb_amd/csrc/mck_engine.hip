@@ -184,7 +184,9 @@ int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int n
   const uint32_t per = (uint32_t)(((uint64_t)count + nl - 1) / nl);
   for (uint32_t first = 0; first < count; first += per) {
     const uint32_t n = std::min(per, count - first);
-    const uint32_t grid = std::min<uint32_t>(ncu, (n + 15) / 16);
+    // (>= 4 spans per workgroup: a batch of a few thousand large spans -- one
+    // 64 MiB SST file -- still fills every CU; shares are byte-balanced)
+    const uint32_t grid = std::min<uint32_t>(ncu, (n + 3) / 4);
     if (blk)
       hipLaunchKernelGGL((k_crc_auto<Op, T, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n,
                          crc_auto_force());
@@ -253,8 +255,7 @@ int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform) {
   if (rc) return rc;
   if (!uniform) {
     // one workgroup per CU, spans dealt by LDS tickets
-    const uint32_t wpb = kX3WaveThreads / 64;
-    const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + wpb - 1) / wpb);
+    const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + 3) / 4);
     hipLaunchKernelGGL((k_xxh3_wave<Op>), dim3(grid), dim3(kX3WaveThreads), 0, st, op, count);
   } else {
     // 16 rows (spans) per 256-thread workgroup

@@ -650,8 +650,8 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
   constexpr bool BLK = true;  // contiguous fragment ranges per workgroup
   constexpr int W = 16, NP = 5;
   constexpr int kHdr = 2;  // padding + header bytes per lane (pad + hs <= 21)
-  crc_rows_prologue<BLK>(op, first, count, lds, g, false);
   const RowShare sh = row_share<BLK>(first, count);
+  crc_rows_prologue<OpWalWrite>(op, sh, lds, g, false);
   // fragments' dst_off, staged like the descriptors (row_desc_stage order)
   for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) *lds_p64(kLdsWalAux + 8 * t) = op.frags[sh.idx(t)].dst_off;
   {  // lane-final map over lane-final columns 0-15, the piece-to-piece byte table

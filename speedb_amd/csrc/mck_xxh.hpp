@@ -908,8 +908,8 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
   uint32_t start = b, stride = G, n = count > b ? (count - b + G - 1) / G : 0;
   if (count <= kBalanceMaxSpans) {
     uint32_t lo, hi;
-    balanced_range([&](uint32_t i) { return op.hlen(i); }, count, reinterpret_cast<uint64_t*>(&s.acc[0][0]), &lo,
-                   &hi);
+    balanced_range([&](uint32_t i) { return op.hlen(i); }, count, count,
+                   reinterpret_cast<uint64_t*>(&s.acc[0][0]), &lo, &hi);  // (windows: no size bound)
     start = lo;
     stride = 1;
     n = hi - lo;
