@@ -1063,6 +1063,7 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, const RowShare& sh, 
   const uint32_t c = threadIdx.x & (W - 1);
   Lf.lane4 = (64u - W + c) << 2;
   const uint32_t share = sh.n;  // this workgroup's spans
+  if (share == 0) return;        // (slot 0 would be read unstaged)
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   // the row's current span (ticket t) and the next one (ticket nt, prefetched)
   uint32_t t = row_ticket<W>(true);

@@ -541,6 +541,9 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
                    reinterpret_cast<uint64_t*>(lds + kULdsDesc), &lo, &hi);
     sh = RowShare{first + lo, 1u, hi - lo};
   }
+  // a byte-balanced share can be empty (its bytes all in a neighbour's big
+  // span): nothing to stage -- the row feed would read an unstaged slot 0
+  if (sh.n == 0) return;  // workgroup-uniform
   int mode = force;
   if (!mode) {
     uint64_t sum = 0;
