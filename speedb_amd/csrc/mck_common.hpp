@@ -94,14 +94,46 @@ __device__ __forceinline__ uint32_t lds_ticket(P ctr) {
 #define MCK_BALANCE_MAX_SPANS (1u << 18)
 #endif
 constexpr uint32_t kBalanceMaxSpans = MCK_BALANCE_MAX_SPANS;  // beyond: shares by count (their bytes average out)
+// (The lengths are read 8 per batch with clamped indices, so every load of
+// a batch is in flight at once: a thread's chunk of ~50 lengths read one by
+// one cost ~80 us per launch of serial L2 round trips.)
+constexpr uint32_t kLenBatch = 8;  // lengths in flight per thread
+template <class Len>
+__device__ __forceinline__ uint64_t chunk_sum(Len len, uint32_t c0, uint32_t c1) {
+  uint64_t sum = 0;
+  for (uint32_t i = c0; i < c1; i += kLenBatch) {
+    uint32_t v[kLenBatch];
+#pragma unroll
+    for (uint32_t k = 0; k < kLenBatch; k++) v[k] = (uint32_t)len(i + k < c1 ? i + k : c0);
+#pragma unroll
+    for (uint32_t k = 0; k < kLenBatch; k++) sum += i + k < c1 ? v[k] : 0u;
+  }
+  return sum;
+}
+// spans of [c0, c1) whose first byte (p0 + the lengths before them) is below t
+template <class Len>
+__device__ __forceinline__ uint32_t chunk_below(Len len, uint32_t c0, uint32_t c1, uint64_t p0, uint64_t t) {
+  uint32_t n = 0;
+  uint64_t p = p0;
+  for (uint32_t i = c0; i < c1; i += kLenBatch) {
+    uint32_t v[kLenBatch];
+#pragma unroll
+    for (uint32_t k = 0; k < kLenBatch; k++) v[k] = (uint32_t)len(i + k < c1 ? i + k : c0);
+#pragma unroll
+    for (uint32_t k = 0; k < kLenBatch; k++) {
+      n += i + k < c1 && p < t ? 1u : 0u;
+      p += i + k < c1 ? v[k] : 0u;
+    }
+  }
+  return n;
+}
 template <class Len>
 __device__ __forceinline__ void balanced_range(Len len, uint32_t count, uint32_t slack, uint64_t* lds, uint32_t* lo,
                                                uint32_t* hi) {
   const uint32_t nt = blockDim.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
   const uint32_t per = (count + nt - 1) / nt;
   const uint32_t c0 = min(tid * per, count), c1 = min(c0 + per, count);
-  uint64_t sum = 0;
-  for (uint32_t i = c0; i < c1; i++) sum += len(i);
+  const uint64_t sum = chunk_sum(len, c0, c1);
   uint64_t x = sum;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -119,26 +151,26 @@ __device__ __forceinline__ void balanced_range(Len len, uint32_t count, uint32_t
   __syncthreads();
   const uint64_t G = gridDim.x, b = blockIdx.x;
   const uint64_t tlo = total * b / G, thi = total * (b + 1) / G;
-  // spans whose first byte lies below tlo / thi (the prefix never decreases)
-  uint32_t nlo = 0, nhi = 0;
-  uint64_t p = below + x - sum;
-  if (p < thi) {
-    for (uint32_t i = c0; i < c1; i++) {
-      nlo += p < tlo ? 1u : 0u;
-      nhi += p < thi ? 1u : 0u;
-      p += len(i);
-    }
-  }
-  uint64_t r = ((uint64_t)nhi << 32) | nlo;
+  // spans whose first byte lies below tlo / thi (the prefix never
+  // decreases): a chunk that ends below the target counts whole, one that
+  // starts at or above it not at all; only the chunk holding the target
+  // walks its lengths
+  const uint64_t e = below + x - sum;  // the chunk's first byte
+  const auto cnt = [&](uint64_t t) -> uint32_t {
+    if (e + sum < t) return c1 - c0;
+    if (e >= t) return 0u;
+    return chunk_below(len, c0, c1, e, t);
+  };
+  uint64_t r = ((uint64_t)cnt(thi) << 32) | cnt(tlo);
   for (int m = 32; m >= 1; m >>= 1) r += __shfl_xor(r, m, 64);
   if (lane == 0) lds[wid] = r;
   __syncthreads();
   uint64_t tot = 0;
   for (uint32_t w = 0; w < nw; w++) tot += lds[w];
-  const auto clampb = [&](uint32_t x, uint64_t bb) {
+  const auto clampb = [&](uint32_t v, uint64_t bb) {
     const uint32_t c = (uint32_t)((uint64_t)count * bb / G);
     const uint32_t a = c > slack ? c - slack : 0u, z = count - c > slack ? c + slack : count;
-    return x < a ? a : x > z ? z : x;
+    return v < a ? a : v > z ? z : v;
   };
   *lo = clampb((uint32_t)tot, b);
   *hi = b + 1 == G ? count : clampb((uint32_t)(tot >> 32), b + 1);

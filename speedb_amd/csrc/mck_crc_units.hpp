@@ -221,16 +221,24 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin
 // the flags as ballots; the rest stays in the lanes and is read (v_readlane,
 // in wave-uniform branches) only by a head, tail or end slot.  Slot j is
 // window unit g0 + j of the wave's stream.
+// NU = 8 for ops without epilogue inputs (OpCrcValue: two iterations' 16
+// pieces and plans fit 128 VGPRs), 4 for the block / WAL / blob ops, whose
+// two prefetched epilogue inputs per plan would spill at 8 (A/B: 4300-B
+// Value blocks 0.599 at 8 vs 0.585 at 4; the SST verify mix spilled 80 B
+// per lane at 8 and lost 20 %).  -DMCK_UNIT_SLOTS=4|8 forces one (A/B).
 #ifndef MCK_UNIT_SLOTS
-#define MCK_UNIT_SLOTS 8
+#define MCK_UNIT_SLOTS 0
 #endif
-constexpr uint32_t kUSlots = MCK_UNIT_SLOTS;
-static_assert(kUSlots == 4 || kUSlots == 8, "unit slots per iteration");
+template <class Op>
+constexpr uint32_t unit_slots_of() {
+  return MCK_UNIT_SLOTS ? MCK_UNIT_SLOTS : sizeof(typename Op::Pre) <= 4 ? 8u : 4u;
+}
 // flags: 8 bits each, bit j = slot j
 constexpr uint32_t kUFirst = 1u, kUHead = 1u << 8, kUTail = 1u << 16, kUEnd = 1u << 24;
+template <uint32_t NU>
 struct USlots {
-  uint64_t base[kUSlots];   // slot j's unit: [base, base + 1 KiB)
-  uint32_t below[kUSlots];  // lanes below this load the zero piece (64: no unit)
+  uint64_t base[NU];   // slot j's unit: [base, base + 1 KiB)
+  uint32_t below[NU];  // lanes below this load the zero piece (64: no unit)
   uint32_t flags;           // kUFirst << j: the lane state restarts (span head or stream
                             // start); kUHead << j: the span's head unit; kUTail << j: its
                             // last unit, with bytes past the end; kUEnd << j: the stream's
@@ -243,9 +251,11 @@ struct USlots {
 
 // Plan the slots of units g0 .. g0 + NU - 1 of stream [gs, ge); tc = a span
 // at or before the span of unit g0 (advanced here).
-__device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t ge, uint32_t wn, uint32_t& tc,
-                                             uint64_t base, uint32_t lane) {
-  USlots P;
+template <uint32_t NU>
+__device__ __forceinline__ USlots<NU> unit_slots(uint32_t g0, uint32_t gs, uint32_t ge, uint32_t wn, uint32_t& tc,
+                                                 uint64_t base, uint32_t lane) {
+  static_assert(NU == 4 || NU == 8, "unit slots per iteration");
+  USlots<NU> P;
   P.g0 = g0;
   // spans tc + 1 + lane: the spans that start at or before unit g are
   // counted by a ballot over the window's unit prefix (empty spans included,
@@ -263,10 +273,10 @@ __device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t 
   // T too: they are clamped to the last span, so every descriptor and
   // epilogue load such a slot issues is a real span's.
   const uint32_t tl = wn - 1;
-  const uint32_t j = lane & (kUSlots - 1);
+  const uint32_t j = lane & (NU - 1);
   uint32_t t = min(tc + c0, tl), tlast = t;
 #pragma unroll
-  for (uint32_t q = 1; q < kUSlots; q++) {
+  for (uint32_t q = 1; q < NU; q++) {
     const uint32_t gq = g0 + q;
     uint32_t c = (uint32_t)__popcll(__ballot(v <= gq));
     uint32_t tb = tc;
@@ -294,11 +304,11 @@ __device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t 
   const bool tail = live && kk == 0 && kt != 0;
   const bool first = live && (g == gs || head);
   const bool end = live && (g + 1 == ge || kk == 0);
-  constexpr uint32_t m = (1u << kUSlots) - 1u;
+  constexpr uint32_t m = (1u << NU) - 1u;
   P.flags = ((uint32_t)__ballot(first) & m) * kUFirst | ((uint32_t)__ballot(head) & m) * kUHead |
             ((uint32_t)__ballot(tail) & m) * kUTail | ((uint32_t)__ballot(end) & m) * kUEnd;
 #pragma unroll
-  for (uint32_t q = 0; q < kUSlots; q++) {
+  for (uint32_t q = 0; q < NU; q++) {
     P.base[q] = readlane_u64(ub, q);
     P.below[q] = readlane_u32(below, q);
   }
@@ -311,10 +321,11 @@ __device__ __forceinline__ USlots unit_slots(uint32_t g0, uint32_t gs, uint32_t 
 // The plan's loads: lane l's piece of every slot's unit (the zero piece for
 // lanes before a span's head and for empty slots).  Straight-line, so every
 // load is unconditional and the waits exact.
-__device__ __forceinline__ ChunkN<kUSlots> unit_load(const USlots& P, uint32_t lane16, uint32_t lane, uint64_t zp) {
-  ChunkN<kUSlots> c;
+template <uint32_t NU>
+__device__ __forceinline__ ChunkN<NU> unit_load(const USlots<NU>& P, uint32_t lane16, uint32_t lane, uint64_t zp) {
+  ChunkN<NU> c;
 #pragma unroll
-  for (uint32_t j = 0; j < kUSlots; j++) c.v[j] = span_load16<true>(lane < P.below[j] ? zp : P.base[j] + lane16);
+  for (uint32_t j = 0; j < NU; j++) c.v[j] = span_load16<true>(lane < P.below[j] ? zp : P.base[j] + lane16);
   return c;
 }
 
@@ -388,6 +399,8 @@ __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh,
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
   typedef typename Op::Pre Pre;
+  constexpr uint32_t NU = unit_slots_of<Op>();
+  typedef USlots<NU> Slots;
   const uint32_t T = rfl(upre(wn));  // the window's units
   const uint32_t W = blockDim.x >> 6, w = threadIdx.x >> 6;
   const uint32_t gs = rfl((uint32_t)((uint64_t)T * w / W)), ge = rfl((uint32_t)((uint64_t)T * (w + 1) / W));
@@ -395,28 +408,28 @@ __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh,
   uint32_t tc = 0;
   // epilogue inputs of span end number e of a plan (its first two: a fixed
   // number of loads per iteration keeps vmcnt exact; fewer ends repeat one)
-  const auto end_slot = [](const USlots& X, uint32_t e) {
+  const auto end_slot = [](const Slots& X, uint32_t e) {
     uint32_t m = X.flags / kUEnd;
     if (e) m &= m - 1;
     return m ? (uint32_t)__builtin_ctz(m) : 0u;
   };
-  const auto pre_of = [&](const USlots& X, uint32_t j) {
+  const auto pre_of = [&](const Slots& X, uint32_t j) {
     const uint32_t t = readlane_u32(X.t, j);
     const uint4 d = unit_desc(t);
     return unit_pre(op, sh.idx(t), base + (((uint64_t)d.y << 32) | d.x), d.z);
   };
-  USlots P = unit_slots(gs, gs, ge, wn, tc, base, lane);
-  ChunkN<kUSlots> cur = unit_load(P, lane16, lane, zp);
+  Slots P = unit_slots<NU>(gs, gs, ge, wn, tc, base, lane);
+  ChunkN<NU> cur = unit_load(P, lane16, lane, zp);
   Pre pre0 = pre_of(P, end_slot(P, 0)), pre1 = pre_of(P, end_slot(P, 1));
   uint32_t s = 0;
-  for (uint32_t g0 = gs; g0 < ge; g0 += kUSlots) {
-    const USlots Q = unit_slots(g0 + kUSlots, gs, ge, wn, tc, base, lane);
-    const ChunkN<kUSlots> nxt = unit_load(Q, lane16, lane, zp);
+  for (uint32_t g0 = gs; g0 < ge; g0 += NU) {
+    const Slots Q = unit_slots<NU>(g0 + NU, gs, ge, wn, tc, base, lane);
+    const ChunkN<NU> nxt = unit_load(Q, lane16, lane, zp);
     const Pre pn0 = pre_of(Q, end_slot(Q, 0)), pn1 = pre_of(Q, end_slot(Q, 1));
     const uint32_t f = P.flags;
-    uint32_t se[kUSlots];  // the lane state after each slot (the span ends' states)
+    uint32_t se[NU];  // the lane state after each slot (the span ends' states)
 #pragma unroll
-    for (uint32_t j = 0; j < kUSlots; j++) {
+    for (uint32_t j = 0; j < NU; j++) {
       uint4 v = cur.v[j];
       uint32_t extra = 0;
       if (f & (kUHead << j)) {  // wave-uniform: the head unit of a span
@@ -444,7 +457,7 @@ __device__ __forceinline__ void crc_units_window(const Op& op, const UShare& sh,
       const uint32_t j = (uint32_t)__builtin_ctz(m);
       uint32_t sj = se[0];
 #pragma unroll
-      for (uint32_t q = 1; q < kUSlots; q++) sj = j == q ? se[q] : sj;
+      for (uint32_t q = 1; q < NU; q++) sj = j == q ? se[q] : sj;
       const Pre pr = nend == 0 ? pre0 : nend == 1 ? pre1 : pre_of(P, j);
       unit_flush(op, sh, base, readlane_u32(P.t, j), P.g0 + j, sj, pr, gs, ge, UL, g);
     }
@@ -519,10 +532,12 @@ __device__ __forceinline__ void crc_units_driver(const Op& op, const RowShare& s
 
 // Ragged batches: the driver is chosen per workgroup from its share's mean
 // span length (the host cannot see device-resident lengths): 8-lane rows up
-// to 640 B, 16-lane rows up to 2.5 KiB, the unit stream above.
+// to 640 B, 16-lane rows up to 2.5 KiB, the unit stream up to 8 KiB when the
+// spans would leave the wave driver's 4 KiB rounds > 20 % empty, else the
+// wave driver.
 // force: 0 = by length, 1 = the 4 KiB-round wave driver, 2 = rows16,
 // 3 = rows8, 4 = unit stream, 5 = rows4.
-constexpr uint32_t kAutoUnitsMin = 2560;  // mean span bytes
+constexpr uint32_t kAutoUnitsMin = 2560, kAutoUnitsMax = 8192;  // mean span bytes
 template <class Op, bool T, bool BLK>
 __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                       const CrcTables* __restrict__ g, int force) {
@@ -546,16 +561,39 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
   if (sh.n == 0) return;  // workgroup-uniform
   int mode = force;
   if (!mode) {
-    uint64_t sum = 0;
-    for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) sum += op.len(sh.idx(t));
-    for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 64);
-    if ((threadIdx.x & 63) == 0) *lds_p64(kULdsDesc + 8 * (threadIdx.x >> 6)) = sum;
+    // the share's bytes, and the bytes the wave driver's 4 KiB rounds would
+    // cover (each span rounded up to 4 KiB)
+    uint64_t sum = 0, wsum = 0;
+    for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) {
+      const uint64_t n = op.len(sh.idx(t));
+      sum += n;
+      wsum += (n + 4095) & ~4095ull;
+    }
+    for (int m = 32; m >= 1; m >>= 1) {
+      sum += __shfl_xor(sum, m, 64);
+      wsum += __shfl_xor(wsum, m, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      *lds_p64(kULdsDesc + 16 * (threadIdx.x >> 6)) = sum;
+      *lds_p64(kULdsDesc + 16 * (threadIdx.x >> 6) + 8) = wsum;
+    }
     __syncthreads();
-    uint64_t total = 0;
-    for (uint32_t w = 0; w < blockDim.x / 64; w++) total += *lds_p64(kULdsDesc + 8 * w);
+    uint64_t total = 0, wtotal = 0;
+    for (uint32_t w = 0; w < blockDim.x / 64; w++) {
+      total += *lds_p64(kULdsDesc + 16 * w);
+      wtotal += *lds_p64(kULdsDesc + 16 * w + 8);
+    }
     __syncthreads();  // the scratch is overwritten by the drivers' fills
     const uint64_t mean = total / (sh.n ? sh.n : 1);
-    mode = mean <= kAutoRows8Max ? 3 : mean <= kAutoUnitsMin ? 2 : 4;
+    // the unit stream for spans of a few KiB that waste the wave driver's
+    // rounds (4100-4400 B: 0.60 vs 0.54 of peak); aligned 4 KiB multiples
+    // and the long spans of the SST mix stay on the wave driver (4096 B: 0.74
+    // vs 0.69; 4/16/64 KiB mix: 0.67 vs 0.57)
+    const bool waste = 4 * wtotal > 5 * total;
+    mode = mean <= kAutoRows8Max        ? 3
+           : mean <= kAutoUnitsMin      ? 2
+           : mean <= kAutoUnitsMax && waste ? 4
+                                        : 1;
   }
   if (mode == 4)
     crc_units_driver<Op>(op, sh, g);
