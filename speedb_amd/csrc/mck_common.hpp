@@ -94,46 +94,71 @@ __device__ __forceinline__ uint32_t lds_ticket(P ctr) {
 #define MCK_BALANCE_MAX_SPANS (1u << 18)
 #endif
 constexpr uint32_t kBalanceMaxSpans = MCK_BALANCE_MAX_SPANS;  // beyond: shares by count (their bytes average out)
-// (The lengths are read 8 per batch with clamped indices, so every load of
-// a batch is in flight at once: a thread's chunk of ~50 lengths read one by
-// one cost ~80 us per launch of serial L2 round trips.)
-constexpr uint32_t kLenBatch = 8;  // lengths in flight per thread
-template <class Len>
-__device__ __forceinline__ uint64_t chunk_sum(Len len, uint32_t c0, uint32_t c1) {
+// (The lengths are read as 16-byte vectors, eight vectors -- 32 lengths --
+// in flight per thread, with clamped addresses so every load of a batch is
+// issued at once; a first version read one length per load and waited for
+// each, ~80 us of serial L2 round trips per launch.)
+constexpr uint32_t kLenVecs = 8;
+// sum of lens[c0, c1) (c0 a multiple of 4, lens 16-byte aligned)
+__device__ __forceinline__ uint64_t lens_sum(const uint32_t* lens, uint32_t c0, uint32_t c1) {
   uint64_t sum = 0;
-  for (uint32_t i = c0; i < c1; i += kLenBatch) {
-    uint32_t v[kLenBatch];
+  for (uint32_t i = c0; i < c1; i += 4 * kLenVecs) {
+    uint4 v[kLenVecs];
 #pragma unroll
-    for (uint32_t k = 0; k < kLenBatch; k++) v[k] = (uint32_t)len(i + k < c1 ? i + k : c0);
+    for (uint32_t k = 0; k < kLenVecs; k++) {
+      const uint32_t j = i + 4 * k < c1 ? i + 4 * k : c0;
+      v[k] = *reinterpret_cast<const uint4*>(lens + j);
+    }
 #pragma unroll
-    for (uint32_t k = 0; k < kLenBatch; k++) sum += i + k < c1 ? v[k] : 0u;
+    for (uint32_t k = 0; k < kLenVecs; k++) {
+      const uint32_t j = i + 4 * k;
+      sum += (j < c1 ? v[k].x : 0u) + (j + 1 < c1 ? v[k].y : 0u);
+      sum += (j + 2 < c1 ? v[k].z : 0u) + (j + 3 < c1 ? v[k].w : 0u);
+    }
   }
   return sum;
 }
-// spans of [c0, c1) whose first byte (p0 + the lengths before them) is below t
-template <class Len>
-__device__ __forceinline__ uint32_t chunk_below(Len len, uint32_t c0, uint32_t c1, uint64_t p0, uint64_t t) {
+// spans of [c0, c1) whose first byte (p0 + the lengths before them) lies
+// below t
+__device__ __forceinline__ uint32_t lens_below(const uint32_t* lens, uint32_t c0, uint32_t c1, uint64_t p0,
+                                               uint64_t t) {
   uint32_t n = 0;
   uint64_t p = p0;
-  for (uint32_t i = c0; i < c1; i += kLenBatch) {
-    uint32_t v[kLenBatch];
+  for (uint32_t i = c0; i < c1; i += 4 * kLenVecs) {
+    uint4 v[kLenVecs];
 #pragma unroll
-    for (uint32_t k = 0; k < kLenBatch; k++) v[k] = (uint32_t)len(i + k < c1 ? i + k : c0);
+    for (uint32_t k = 0; k < kLenVecs; k++) {
+      const uint32_t j = i + 4 * k < c1 ? i + 4 * k : c0;
+      v[k] = *reinterpret_cast<const uint4*>(lens + j);
+    }
 #pragma unroll
-    for (uint32_t k = 0; k < kLenBatch; k++) {
-      n += i + k < c1 && p < t ? 1u : 0u;
-      p += i + k < c1 ? v[k] : 0u;
+    for (uint32_t k = 0; k < kLenVecs; k++) {
+      const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        const bool in = i + 4 * k + q < c1;
+        n += in && p < t ? 1u : 0u;
+        p += in ? w[q] : 0u;
+      }
     }
   }
   return n;
 }
-template <class Len>
-__device__ __forceinline__ void balanced_range(Len len, uint32_t count, uint32_t slack, uint64_t* lds, uint32_t* lo,
-                                               uint32_t* hi) {
+// lens: the batch's length array (nullptr: every span the same length --
+// the shares by count are balanced already)
+__device__ __forceinline__ void balanced_range(const uint32_t* lens, uint32_t count, uint32_t slack, uint64_t* lds,
+                                               uint32_t* lo, uint32_t* hi) {
+  const uint64_t G = gridDim.x, b = blockIdx.x;
+  if (lens == nullptr || (reinterpret_cast<uint64_t>(lens) & 15)) {  // grid-uniform
+    // (an unaligned length array -- a sliced view -- keeps the shares by count)
+    *lo = (uint32_t)((uint64_t)count * b / G);
+    *hi = (uint32_t)((uint64_t)count * (b + 1) / G);
+    return;
+  }
   const uint32_t nt = blockDim.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, nw = nt >> 6;
-  const uint32_t per = (count + nt - 1) / nt;
+  const uint32_t per = ((count + nt - 1) / nt + 3) & ~3u;
   const uint32_t c0 = min(tid * per, count), c1 = min(c0 + per, count);
-  const uint64_t sum = chunk_sum(len, c0, c1);
+  const uint64_t sum = lens_sum(lens, c0, c1);
   uint64_t x = sum;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -149,7 +174,6 @@ __device__ __forceinline__ void balanced_range(Len len, uint32_t count, uint32_t
     total += v;
   }
   __syncthreads();
-  const uint64_t G = gridDim.x, b = blockIdx.x;
   const uint64_t tlo = total * b / G, thi = total * (b + 1) / G;
   // spans whose first byte lies below tlo / thi (the prefix never
   // decreases): a chunk that ends below the target counts whole, one that
@@ -159,7 +183,7 @@ __device__ __forceinline__ void balanced_range(Len len, uint32_t count, uint32_t
   const auto cnt = [&](uint64_t t) -> uint32_t {
     if (e + sum < t) return c1 - c0;
     if (e >= t) return 0u;
-    return chunk_below(len, c0, c1, e, t);
+    return lens_below(lens, c0, c1, e, t);
   };
   uint64_t r = ((uint64_t)cnt(thi) << 32) | cnt(tlo);
   for (int m = 32; m >= 1; m >>= 1) r += __shfl_xor(r, m, 64);

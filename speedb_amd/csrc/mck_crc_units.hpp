@@ -552,7 +552,7 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
     const uint32_t per = (uint32_t)(((uint64_t)count + gridDim.x - 1) / gridDim.x);
     const uint32_t slack = per + 1 < kRowDescCache ? (kRowDescCache - per - 1) / 2 : 0u;
     uint32_t lo, hi;
-    balanced_range([&](uint32_t i) { return op.len(first + i); }, count, slack,
+    balanced_range(op.lens() ? op.lens() + first : nullptr, count, slack,
                    reinterpret_cast<uint64_t*>(lds + kULdsDesc), &lo, &hi);
     sh = RowShare{first + lo, 1u, hi - lo};
   }

@@ -901,19 +901,19 @@ __device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, c
 // ...), staged in windows of kX3DescCache spans, long spans in pieces.
 template <class Op, bool PREVIEW>
 __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, uint64_t seed) {
-  const X3Row X = x3_row(seed);
   __shared__ X3Lds s;
   const uint32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
   uint32_t start = b, stride = G, n = count > b ? (count - b + G - 1) / G : 0;
   if (count <= kBalanceMaxSpans) {
     uint32_t lo, hi;
-    balanced_range([&](uint32_t i) { return op.hlen(i); }, count, count,
-                   reinterpret_cast<uint64_t*>(&s.acc[0][0]), &lo, &hi);  // (windows: no size bound)
+    balanced_range(op.lens(), count, count, reinterpret_cast<uint64_t*>(&s.acc[0][0]), &lo,
+                   &hi);  // (windows: no size bound)
     start = lo;
     stride = 1;
     n = hi - lo;
   }
+  const X3Row X = x3_row(seed);  // (after the length scan: its registers are free again)
   for (uint32_t w0 = 0; w0 < n; w0 += kX3DescCache) {
     const uint32_t wn = n - w0 < kX3DescCache ? n - w0 : kX3DescCache;
     const uint32_t wb = start + stride * w0;  // span of window slot t: wb + stride t
