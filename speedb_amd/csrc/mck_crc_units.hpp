@@ -541,24 +541,10 @@ constexpr uint32_t kAutoUnitsMin = 2560, kAutoUnitsMax = 8192;  // mean span byt
 template <class Op, bool T, bool BLK>
 __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                       const CrcTables* __restrict__ g, int force) {
-  // the workgroup's share -- every driver works on it, so whatever each
-  // workgroup chooses, the shares partition the batch: contiguous ranges of
-  // equal bytes (balanced_range) when the batch is ragged and small enough
-  // to scan, else by count
-  RowShare sh = row_share<BLK>(first, count);
-  if (BLK && count <= kBalanceMaxSpans) {
-    // the row drivers stage at most kRowDescCache descriptors: the host keeps
-    // count / G below it, the slack keeps every share within it
-    const uint32_t per = (uint32_t)(((uint64_t)count + gridDim.x - 1) / gridDim.x);
-    const uint32_t slack = per + 1 < kRowDescCache ? (kRowDescCache - per - 1) / 2 : 0u;
-    uint32_t lo, hi;
-    balanced_range(op.lens() ? op.lens() + first : nullptr, count, slack,
-                   reinterpret_cast<uint64_t*>(lds + kULdsDesc), &lo, &hi);
-    sh = RowShare{first + lo, 1u, hi - lo};
-  }
-  // a byte-balanced share can be empty (its bytes all in a neighbour's big
-  // span): nothing to stage -- the row feed would read an unstaged slot 0
-  if (sh.n == 0) return;  // workgroup-uniform
+  // the workgroup's share (contiguous ranges: neighbouring spans on one CU;
+  // interleaved under the test hook) -- every driver works on the same one
+  const RowShare sh = row_share<BLK>(first, count);
+  if (sh.n == 0) return;  // workgroup-uniform (the row feed would read an unstaged slot 0)
   int mode = force;
   if (!mode) {
     // the share's bytes, and the bytes the wave driver's 4 KiB rounds would

@@ -149,7 +149,6 @@ struct OpCrcValue {
   uint32_t flags;
   uint32_t* out;
   typedef NoPre Pre;
-  __device__ const uint32_t* lens() const { return s.lengths; }  // (nullptr: uniform)
   __device__ const uint8_t* base() const { return s.base; }
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
@@ -176,7 +175,6 @@ struct OpCrcWal {
   typedef NoPre Pre;
   __device__ const uint8_t* base() const { return s.base; }
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
-  __device__ const uint32_t* lens() const { return s.lengths; }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }
   __device__ uint32_t init_crc(uint32_t i) const { return tc.v[types[i] & 15]; }
   static constexpr bool kTypedInit = true;
@@ -197,7 +195,6 @@ struct OpCrcBlock {
   typedef BlockPre Pre;
   __device__ const uint8_t* base() const { return a.s.base; }
   __device__ uint64_t off(uint32_t i) const { return a.s.off(i); }
-  __device__ const uint32_t* lens() const { return a.s.lengths; }
   __device__ uint64_t len(uint32_t i) const { return a.s.len(i) + (MODE == kModeVerify ? 1 : 0); }
   __device__ uint32_t init_crc(uint32_t) const { return 0u; }
   static constexpr bool kTypedInit = false;
@@ -256,7 +253,6 @@ struct OpX3Value {
   typedef NoPre Pre;
   __device__ const uint8_t* base() const { return s.base; }
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
-  __device__ const uint32_t* lens() const { return s.lengths; }
   __device__ uint64_t hlen(uint32_t i) const { return s.len(i); }
   __device__ Pre pre(uint32_t, uint64_t, uint64_t) const { return Pre{}; }
   __device__ void finish(uint32_t i, uint64_t h, const Pre& = Pre{}) const { out[i] = h; }
@@ -270,7 +266,6 @@ struct OpX3Block {
   typedef BlockPre Pre;
   __device__ const uint8_t* base() const { return a.s.base; }
   __device__ uint64_t off(uint32_t i) const { return a.s.off(i); }
-  __device__ const uint32_t* lens() const { return a.s.lengths; }
   __device__ uint64_t hlen(uint32_t i) const {
     const uint64_t n = a.s.len(i);
     // verify: payload || type byte -> hash the payload; trailer / explicit
@@ -918,7 +913,6 @@ struct OpBlobRecord {
   typedef BlobPre Pre;
   __device__ const uint8_t* base() const { return file; }
   __device__ uint64_t off(uint32_t i) const { return rec_off[i] + 32; }
-  __device__ const uint32_t* lens() const { return blob_len; }
   __device__ uint64_t len(uint32_t i) const { return blob_len[i]; }
   __device__ uint32_t init_crc(uint32_t) const { return 0u; }
   static constexpr bool kTypedInit = false;
