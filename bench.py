@@ -110,6 +110,9 @@ def parse():
                         "is one SST file's VerifyChecksumInBlocks batch: 64/256 MiB points in DESIGN.md 5")
     p.add_argument("--sst-types", choices=["both", "crc32c", "xxh3"], default="both",
                    help="sst: verify both images (configs[2]) or one (per-kernel measurement)")
+    p.add_argument("--sst-streams", type=int, choices=[1, 2], default=1,
+                   help="sst: verify the two images one after the other on one stream (1) or "
+                        "concurrently on two, as two input files of a compaction would be (2)")
     p.add_argument("--wal-blocks", type=int, default=10_000_000,
                    help="32 KiB blocks of the WHOLE job, partitioned over the ranks (wal, configs[3])")
     p.add_argument("--hbm-budget-gib", type=float, default=64.0,
@@ -319,10 +322,22 @@ def make_workload(args, dev, rank, world):
         imgs = [W.SstImage(args.sst_bytes, t, dev, seed=100 + 2 * rank + (0 if t == S.ChecksumType.kCRC32c else 1))
                 for t in types]
         res = {}
+        side = torch.cuda.Stream(dev) if args.sst_streams == 2 and len(imgs) == 2 else None
+        fork, join = torch.cuda.Event(), torch.cuda.Event()
 
         def step():
-            for im in imgs:
-                res[im.checksum_type] = im.verify(stream=stream)
+            if side is None:
+                for im in imgs:
+                    res[im.checksum_type] = im.verify(stream=stream)
+                return
+            # two files at once: the second on a side stream (its workgroups
+            # take the CUs the first kernel's tail leaves idle), joined back
+            fork.record(stream)
+            side.wait_event(fork)
+            res[imgs[0].checksum_type] = imgs[0].verify(stream=stream)
+            res[imgs[1].checksum_type] = imgs[1].verify(stream=side)
+            join.record(side)
+            stream.wait_event(join)
         w.step = step
         w.launches = len(imgs)
         w.kernel = " + ".join({int(S.ChecksumType.kCRC32c): _auto("mck::OpCrcBlock<2>"),
@@ -338,6 +353,8 @@ def make_workload(args, dev, rank, world):
                   "checksums; one kCRC32c + one kXXH3 image per step (BASELINE.json configs[2])")
         w.cfg = {"blocks_per_gpu": sum(im.count for im in imgs), "image_bytes": args.sst_bytes,
                  "checksum_types": [S.ChecksumType(int(t)).name for t in types]}
+        if side is not None:
+            w.cfg["streams"] = 2
 
         def check():
             # every block the write-side kernel sealed verifies, and injected
@@ -375,7 +392,7 @@ def make_workload(args, dev, rank, world):
         w.step = step
         w.launches = len(passes)
         w.scaling = "strong"
-        w.kernel = "mck::k_wal_verify<1>"
+        w.kernel = "mck::k_wal_verify<true>"
         w.span_bytes = share * (W.WalImage.PAYLOAD + 1)  # CRC span: type + payload
         # per launch (a full pass): the image + 16 B of result per block
         w.alg_bytes = res * (32768 + 16)
