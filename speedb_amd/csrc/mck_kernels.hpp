@@ -1029,6 +1029,61 @@ __device__ __forceinline__ uint4 wal_hdr16(const uint8_t* wal, uint32_t b) {
 }
 __device__ __forceinline__ uint32_t rfl_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
+// ReadPhysicalRecord's header checks (db/log_reader.cc:450-560) for the
+// record at a block offset with `left` bytes to the block's end: go = 1 when
+// the record is to be hashed, else status says why the block stops there (0:
+// a < 7-byte trailer, skipped).  w0/w1 are the header's first 7 bytes (CRC,
+// length, type); lognum() reads the recyclable header's log number.
+struct WalRec {
+  uint32_t go;
+  int32_t status;
+  uint32_t hsize;
+  uint32_t length;
+};
+template <class LogNum>
+__device__ __forceinline__ WalRec wal_parse(uint32_t left, bool last_block, uint32_t log_number, uint32_t w1,
+                                            LogNum lognum) {
+  WalRec r{0u, 0, 7u, 0u};
+  if (left < 7) {
+    // fewer than kHeaderSize bytes: block trailer (skip), or at EOF a
+    // truncated header (db/log_reader.cc:432-440)
+    if (last_block && left > 0) r.status = 5;  // MCK_WAL_BAD_HEADER
+    return r;
+  }
+  r.length = w1 & 0xFFFFu;
+  const uint32_t type = (w1 >> 16) & 0xFFu;
+  if ((type >= 5 && type <= 8) || type == 11) {
+    r.hsize = 11;
+    if (left < 11) {
+      if (last_block) r.status = 5;
+      return r;
+    }
+    if (lognum() != log_number) {
+      r.status = 4;  // kOldRecord
+      return r;
+    }
+  }
+  if (r.hsize + r.length > left) {
+    r.status = 2;  // kBadRecordLen
+    return r;
+  }
+  if (type == 0 && r.length == 0) {
+    r.status = 3;  // kZeroType, length 0: buffer cleared
+    return r;
+  }
+  r.go = 1;
+  return r;
+}
+
+// One wave per block; a wave's records form one software pipeline: each
+// record is hashed round by round with the next round's chunk in flight,
+// and when a record ends its block (configs[3]: one record per block) its
+// last round already loads the first round of the wave's NEXT block, whose
+// header was read at the record's start, so the wave never waits a memory
+// trip between blocks.  A record followed by another in the same block
+// hands over without that overlap (its header is read on demand, byte by
+// byte, as ReadPhysicalRecord reads the buffer), and so does one whose
+// checksum fails or whose successor header does not parse.
 template <bool T>
 __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_t nbytes, uint32_t log_number,
                                                      WalResult* res, uint32_t nblocks) {
@@ -1038,79 +1093,118 @@ __global__ __launch_bounds__(1024) void k_wal_verify(const uint8_t* wal, uint64_
   const CrcLane L = crc_lane();
   const uint32_t wpb = blockDim.x >> 6;
   const uint32_t nw = gridDim.x * wpb;
-  uint32_t b = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-  if (b >= nblocks) return;
-  uint4 nh = wal_hdr16(wal, b);
-  for (; b < nblocks; b += nw) {
-    const uint4 h0 = nh;
-    nh = wal_hdr16(wal, b + nw < nblocks ? b + nw : b);  // the next block's first header
-    const uint8_t* blk = wal + (uint64_t)b * 32768;
-    const uint64_t rem = nbytes - (uint64_t)b * 32768;
-    const uint32_t size = rem < 32768 ? (uint32_t)rem : 32768u;
-    const bool last_block = rem <= 32768;  // reader reaches EOF inside it
-    uint32_t pos = 0, ok = 0, bytes_ok = 0;
-    int32_t status = 0;
-    for (;;) {
-      const uint32_t left = size - pos;
-      if (left < 7) {
-        // fewer than kHeaderSize bytes: block trailer (skip), or at EOF a
-        // truncated header (db/log_reader.cc:432-440)
-        if (last_block && left > 0) status = 5;  // MCK_WAL_BAD_HEADER
-        break;
-      }
-      const uint8_t* h = blk + pos;
-      // header words: [0, 4) CRC, [4, 6) length, 6 type, [7, 11) log number
-      uint32_t w0, w1, w2;
-      if (pos == 0) {
-        w0 = rfl_u32(h0.x);
-        w1 = rfl_u32(h0.y);
-        w2 = rfl_u32(h0.z);
-      } else {
-        w0 = rd32_bytes(h);
-        w1 = (uint32_t)h[4] | ((uint32_t)h[5] << 8) | ((uint32_t)h[6] << 16);
-        w2 = 0;
-      }
-      const uint32_t length = w1 & 0xFFFFu;
-      const uint32_t type = (w1 >> 16) & 0xFFu;
-      uint32_t hsize = 7;
-      if ((type >= 5 && type <= 8) || type == 11) {
-        hsize = 11;
-        if (left < 11) {
-          if (last_block) status = 5;
-          break;
-        }
-        const uint32_t lognum = pos == 0 ? (w1 >> 24) | (w2 << 8) : rd32_bytes(h + 7);
-        if (lognum != log_number) {
-          status = 4;  // kOldRecord
-          break;
-        }
-      }
-      if (hsize + length > left) {
-        status = 2;  // kBadRecordLen
-        break;
-      }
-      if (type == 0 && length == 0) {
-        status = 3;  // kZeroType, length 0: buffer cleared
-        break;
-      }
-      const uint32_t stored = w0;
-      const uint32_t actual = crc_span_wave<T>(h + 6, length + hsize - 6, 0u, L);
-      // Unmask(stored) == actual  <=>  stored == Mask(actual)
-      if (crc_mask(actual) != stored) {
-        status = 1;  // kBadRecordChecksum
-        break;
-      }
-      ok++;
-      pos += hsize + length;
-      bytes_ok += hsize + length;
-    }
+  uint32_t cb = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
+  if (cb >= nblocks) return;
+  auto block_size = [&](uint32_t k) {
+    const uint64_t rem = nbytes - (uint64_t)k * 32768;
+    return rem < 32768 ? (uint32_t)rem : 32768u;
+  };
+  auto last_block = [&](uint32_t k) { return nbytes - (uint64_t)k * 32768 <= 32768; };  // EOF inside it
+  auto emit = [&](uint32_t k, uint32_t ok, int32_t status, uint32_t pos) {
     if ((threadIdx.x & 63) == 0) {
-      WalResult r;
-      r.records_ok = ok;
-      r.status = status;
-      r.stop_offset = status ? pos : size;
-      r.bytes_ok = bytes_ok;
-      res[b] = r;
+      WalResult o;
+      o.records_ok = ok;
+      o.status = status;
+      o.stop_offset = status ? pos : block_size(k);
+      o.bytes_ok = pos;
+      res[k] = o;
+    }
+  };
+  // a block's first record from the 16-byte vector load h of its start
+  auto parse_first = [&](uint32_t k, const uint4& h) {
+    const uint32_t w1 = rfl_u32(h.y);
+    return wal_parse(block_size(k), last_block(k), log_number, w1,
+                     [&] { return (w1 >> 24) | (rfl_u32(h.z) << 8); });
+  };
+  uint32_t cpos = 0, cok = 0;          // current record: block offset, records verified before it
+  uint4 hb = wal_hdr16(wal, cb);       // the current block's first header (cpos == 0)
+  bool seek = true;                    // the current record still has to be parsed and loaded
+  WalRec rec{};
+  uint32_t stored = 0;
+  CrcSpan sp = crc_span(wal, 0, 0u);
+  Chunk cur{};
+  for (;;) {
+    if (seek) {
+      for (;;) {  // finish blocks until a record to hash
+        const uint32_t left = block_size(cb) - cpos;
+        const uint8_t* h = wal + (uint64_t)cb * 32768 + cpos;
+        if (cpos == 0) {
+          rec = parse_first(cb, hb);
+          stored = rfl_u32(hb.x);
+        } else {
+          uint32_t w1 = 0;
+          if (left >= 7) {  // (rfl: the header words are wave-uniform, so is the control flow)
+            stored = rfl_u32(rd32_bytes(h));
+            w1 = rfl_u32((uint32_t)h[4] | ((uint32_t)h[5] << 8) | ((uint32_t)h[6] << 16));
+          }
+          rec = wal_parse(left, last_block(cb), log_number, w1, [&] { return rfl_u32(rd32_bytes(h + 7)); });
+        }
+        if (rec.go) break;
+        emit(cb, cok, rec.status, cpos);
+        cb += nw;
+        if (cb >= nblocks) return;
+        cpos = 0;
+        cok = 0;
+        hb = wal_hdr16(wal, cb);
+      }
+      sp = crc_span(wal + (uint64_t)cb * 32768 + cpos + 6, rec.length + rec.hsize - 6, 0u);
+      cur = crc_load_chunk<T>(sp, sp.rounds - 1, L);
+    }
+    // does the block end with this record (if it passes)?  Then the next
+    // record is the first of the wave's next block: its header now, its
+    // first round with this record's last.
+    const uint32_t size = block_size(cb);
+    const uint32_t e = cpos + rec.hsize + rec.length;
+    const uint32_t nb = cb + nw;
+    const bool spec = size - e < 7 && nb < nblocks;
+    const uint4 hn = wal_hdr16(wal, spec ? nb : cb);
+    WalRec nrec = rec;
+    auto next_span = [&] {
+      return nrec.go ? crc_span(wal + (uint64_t)nb * 32768 + 6, nrec.length + nrec.hsize - 6, 0u)
+                     : crc_span(wal + (uint64_t)nb * 32768, 0, 0u);
+    };
+    uint32_t s = 0;
+    for (int r = sp.rounds - 1; r >= 0; r--) {
+      Chunk nxt;
+      // unconditional loads (see crc_load_chunk); without a next block,
+      // round 0 of this record is read again and never used.  The next
+      // span's geometry lives only for its load (SGPRs are the limit here)
+      if (r > 0 || !spec) {
+        nxt = crc_load_chunk<T>(sp, r > 0 ? r - 1 : 0, L);
+      } else {
+        nrec = parse_first(nb, hn);
+        const CrcSpan nsp = next_span();
+        nxt = crc_load_chunk<T>(nsp, nsp.rounds - 1, L);
+      }
+      if (T && !(sp.mini && r == sp.rounds - 1)) row_transpose(cur);  // wave-uniform
+      s = crc_round(s, cur, sp, r, L);
+      cur = nxt;
+    }
+    // Unmask(stored) == actual  <=>  stored == Mask(actual).  (Every lane
+    // holds the CRC; rfl tells the compiler, so the record stream's state
+    // stays in SGPRs and its control flow scalar.)
+    const bool pass = crc_mask(rfl_u32(crc_finish(s, sp, L))) == stored;
+    if (!pass) {
+      emit(cb, cok, 1, cpos);  // kBadRecordChecksum
+    } else if (size - e < 7) {
+      // the block's trailer (skipped), or at EOF a truncated header
+      emit(cb, cok + 1, last_block(cb) && size > e ? 5 : 0, e);
+    } else {  // the next record of the same block
+      cok++;
+      cpos = e;
+      seek = true;
+      continue;
+    }
+    if (nb >= nblocks) return;
+    cb = nb;
+    cpos = 0;
+    cok = 0;
+    hb = spec ? hn : wal_hdr16(wal, cb);
+    seek = !(spec && nrec.go);
+    if (!seek) {  // pipelined: the record's first round is in cur
+      rec = nrec;
+      sp = next_span();
+      stored = rfl_u32(hn.x);
     }
   }
 }

@@ -295,6 +295,68 @@ def test_wal_verify_batch(gpu, oracle, recycle):
     assert res3 == wal_expected_blocks(data, 124, oracle)
 
 
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_verify_many_blocks_per_wave(gpu, oracle, recycle):
+    """More blocks than waves (the kernel runs at most 16 x CUs waves), so each
+    wave walks a chain of blocks and its record pipeline hands over from a
+    record that ends a block to the next block's first record, whose header
+    and first round it loaded in advance.  Mixed layouts: full blocks,
+    records spilling over blocks, several records per block, trailers of
+    1..6 bytes; then payload flips (kBadRecordChecksum on the pipelined
+    record and on later records of a block), broken first headers of the
+    next block (bad length, zero type: the pipeline restarts) and a
+    truncated tail."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(7 + recycle)
+    w = WalWriter(oracle, log_number=99, recycle=recycle)
+    pool = splitmix_bytes(1234 + recycle, 1 << 20)
+    waves = 16 * torch.cuda.get_device_properties(0).multi_processor_count
+    nblocks = waves + 700
+    while len(w.buf) < nblocks * 32768:
+        kind = rnd.random()
+        hs = 11 if recycle else 7
+        if kind < 0.45:  # exactly fills the rest of the block
+            n = 32768 - (len(w.buf) % 32768) - hs
+            n = n if n >= 0 else 0
+        elif kind < 0.6:  # leaves a 1..6-byte trailer (skipped)
+            n = max(0, 32768 - (len(w.buf) % 32768) - hs - rnd.randrange(1, 7))
+        elif kind < 0.8:
+            n = rnd.randrange(0, 3000)
+        else:
+            n = rnd.randrange(30000, 120000)
+        off = rnd.randrange(0, len(pool) - 1)
+        payload = (pool[off:] + pool)[:n] if n else b""
+        w.add_record(payload)
+    data = bytes(w.buf)
+    nb = (len(data) + 32767) // 32768
+    assert nb > waves
+    dev = torch.frombuffer(bytearray(data + bytes(64)), dtype=torch.uint8).to("cuda")
+    res = [tuple(r) for r in S.wal_verify_batch(dev, len(data), 99).cpu().tolist()]
+    assert res == wal_expected_blocks(data, 99, oracle)
+    assert all(r[1] == 0 for r in res)
+    cor = bytearray(data)
+    for b in rnd.sample(range(nb - 1), 60):
+        lo = b * 32768
+        what = rnd.randrange(4)
+        if what == 0:  # payload flip somewhere in the block
+            cor[lo + rnd.randrange(16, 32768)] ^= 0x04
+        elif what == 1:  # the first header's length beyond the block
+            cor[lo + 4], cor[lo + 5] = 0xFF, 0xFF
+        elif what == 2:  # zero type, length 0
+            cor[lo + 4:lo + 7] = b"\0\0\0"
+        else:  # the stored CRC
+            cor[lo] ^= 0x80
+    cut = len(cor) - rnd.randrange(1, 32768)
+    cor = bytes(cor[:cut])
+    dev2 = torch.frombuffer(bytearray(cor + bytes(64)), dtype=torch.uint8).to("cuda")
+    res2 = [tuple(r) for r in S.wal_verify_batch(dev2, len(cor), 99).cpu().tolist()]
+    assert res2 == wal_expected_blocks(cor, 99, oracle)
+    assert sum(r[1] != 0 for r in res2) >= 30
+    res3 = [tuple(r) for r in S.wal_verify_batch(dev, len(data), 98).cpu().tolist()]
+    assert res3 == wal_expected_blocks(data, 98, oracle)
+
+
 def test_empty_and_zero_inputs(gpu, oracle):
     import speedb_amd as S
     torch = gpu
