@@ -750,7 +750,8 @@ int mck_statistics_get(mck_statistics* out, int reset);
  * batches choose their driver per workgroup from the share's mean span
  * length, so a mixed parity batch may exercise only one driver.  driver:
  * 0 = by length (the default), 1 = 4 KiB-round wave driver, 2 = 16-lane
- * rows, 3 = 8-lane rows, 4 = unit stream, 5 = 4-lane rows; interleaved != 0 deals spans to
+ * rows, 3 = 8-lane rows, 4 = unit stream, 5 = 4-lane rows, 6 = one lane per
+ * span; interleaved != 0 deals spans to
  * workgroups round-robin instead of in contiguous ranges.  Process-wide. */
 int mck_test_set_crc_driver(int driver, int interleaved);
 

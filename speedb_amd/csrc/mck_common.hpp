@@ -34,6 +34,9 @@ __device__ __forceinline__ uint4 span_load16(uint64_t addr) {
 // scalar loads are dword-granular (they drop the low two address bits) --
 // a misaligned uniform 16-byte load then reads the wrong bytes.  The empty
 // asm makes the address a VGPR value.
+// A value every lane holds, as the scalar the compiler can branch on.
+__device__ __forceinline__ uint32_t rfl_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
 __device__ __forceinline__ uint4 vload16_any(uint64_t addr) {
   asm volatile("" : "+v"(addr));
   return span_load16<false>(addr);

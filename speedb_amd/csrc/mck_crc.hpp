@@ -850,6 +850,9 @@ __device__ __forceinline__ RowSpan row_span_sel(bool a, const RowSpan& x, const 
 // keeps ptr - a0 < 16 bytes of another span to mask (row_round).
 // MCK_ROW_LOAD_ZERO=1 (timing experiments only, wrong output): every piece
 // reads the zero piece.
+#ifndef MCK_PROLOGUE_ONLY
+#define MCK_PROLOGUE_ONLY 0
+#endif
 #ifndef MCK_ROW_LOAD_ZERO
 #define MCK_ROW_LOAD_ZERO 0
 #endif
@@ -904,8 +907,11 @@ __device__ __forceinline__ uint32_t row_round(uint32_t s, ChunkN<P> ch, const Ro
     ch.v[j].w = __builtin_amdgcn_bitop3_b32(ch.v[j].w, mh.w, sel, 0xD0);
   }
   and4(ch.v[P - 1], mt);
-  uint32_t gap = 0;
-  if (wave_any(!first)) gap = crc_nibmap(row_gap_off<W, P>(), s);
+  uint32_t gap = s;  // W = 1: a lane's rounds are adjacent (no gap to shift over)
+  if constexpr (W > 1) {
+    gap = 0;
+    if (wave_any(!first)) gap = crc_nibmap(row_gap_off<W, P>(), s);
+  }
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&ch.v[0]);
   if constexpr (P == 4) {
     uint32_t x = first ? (own ? sp.inj : 0u) : gap;
@@ -955,7 +961,8 @@ __device__ __forceinline__ uint32_t row_finish4(uint32_t s, const RowSpan& sp, u
 // constants with lane4 = (64 - W + c) * 4 (shift by 64 (W - 1 - c)).
 template <int W>
 __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, const CrcLane& Lf) {
-  uint32_t p = row_xor32<W>(crc_lane_final(s, Lf));
+  uint32_t p = s;  // W = 1: the lane's state is the span's (no shift, no row XOR)
+  if constexpr (W > 1) p = row_xor32<W>(crc_lane_final(s, Lf));
   if (wave_any(sp.kt != 0)) p = crc_unshift(sp.kt, p);
   return sp.n == 0 ? sp.init : ~p;
 }
@@ -992,9 +999,33 @@ __device__ __forceinline__ RowShare row_share(uint32_t first, uint32_t count) {
   return {first + b, G, (count - b + G - 1) / G};
 }
 
+// Longest-first order for the wave driver (lpt): a wave hashes its span
+// alone, at about 1/16 of the CU's rate while the others run, so a 64 KiB
+// span taken last keeps the workgroup busy ~30 us after the rest is done
+// (the SST mix's per-launch tail).  Slots are staged by length class, long
+// first; the slot's share position rides in the high bits of the offset word
+// (offsets < 2^53), read back by FeedRowCache.
+constexpr int kLptClasses = 4;
+constexpr uint32_t kLdsLptCount = kLdsRowTicket + 32;   // [4] u32
+constexpr uint32_t kLdsLptCursor = kLdsRowTicket + 48;  // [4] u32
+constexpr uint32_t kLptSlotShift = 21;
+static_assert(kRowDescCache <= (1u << (32 - kLptSlotShift)), "slot bits");
+static_assert(kLdsLptCursor + 16 <= kLdsRowMaskHead, "lpt counters");
+__device__ __forceinline__ uint32_t lpt_class(uint32_t len) {
+  return len >= 49152 ? 0u : len >= 24576 ? 1u : len >= 8192 ? 2u : 3u;
+}
+
 template <class Op>
-__device__ __forceinline__ void row_desc_stage(const Op& op, const RowShare& sh, bool total) {
+__device__ __forceinline__ void row_desc_stage(const Op& op, const RowShare& sh, bool total, bool lpt = false) {
   const uint32_t n = sh.n;
+  if (lpt) {  // workgroup-uniform: count the classes first
+    if (threadIdx.x < 2 * kLptClasses) *lds_p32(kLdsLptCount + 4 * threadIdx.x) = 0;  // counts, cursors
+    __syncthreads();
+    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
+      __hip_atomic_fetch_add(lds_p32(kLdsLptCount + 4 * lpt_class((uint32_t)op.len(sh.idx(t)))), 1u,
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+  }
   uint64_t sum = 0, wsum = 0;
   for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
     const uint32_t i = sh.idx(t);
@@ -1002,8 +1033,18 @@ __device__ __forceinline__ void row_desc_stage(const Op& op, const RowShare& sh,
     const uint32_t len = (uint32_t)op.len(i);
     sum += len;
     wsum += ((uint64_t)len + 4095) & ~4095ull;
-    const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, op.init_key(i)};
-    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsRowDesc + 16 * t)) = d;
+    span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, op.init_key(i)};
+    uint32_t pos = t;
+    if (lpt) {
+      const uint32_t c = lpt_class(len);
+      uint32_t below = 0;
+#pragma unroll
+      for (uint32_t k = 0; k < kLptClasses - 1; k++) below += k < c ? *lds_p32(kLdsLptCount + 4 * k) : 0u;
+      pos = below + __hip_atomic_fetch_add(lds_p32(kLdsLptCursor + 4 * c), 1u, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+      d.y |= t << kLptSlotShift;
+    }
+    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsRowDesc + 16 * pos)) = d;
   }
   if (threadIdx.x == 0) *lds_p32(kLdsRowTicket) = 0;
   if (total) {
@@ -1046,9 +1087,9 @@ __device__ __forceinline__ uint4 row_desc(uint32_t t, uint32_t share) {
 // tables; ends with a barrier.
 template <class Op>
 __device__ __forceinline__ void crc_rows_prologue(const Op& op, const RowShare& sh, uint8_t* lds,
-                                                  const CrcTables* __restrict__ g, bool total) {
+                                                  const CrcTables* __restrict__ g, bool total, bool lpt = false) {
   crc_fill_rows(lds, g);
-  row_desc_stage<Op>(op, sh, total);
+  row_desc_stage<Op>(op, sh, total, lpt);
   __syncthreads();
   row_init_tables(op);
   __syncthreads();
@@ -1056,7 +1097,7 @@ __device__ __forceinline__ void crc_rows_prologue(const Op& op, const RowShare& 
 
 template <class Op, int W>
 __device__ __forceinline__ void crc_rows_loop(const Op& op, const RowShare& sh, const CrcTables* __restrict__ g) {
-  static_assert(W == 4 || W == 8 || W == 16, "row width");
+  static_assert(W == 1 || W == 4 || W == 8 || W == 16, "row width");
   const int kind = op.init_kind();
   const CrcLane L = crc_lane();
   CrcLane Lf = L;
@@ -1116,18 +1157,20 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, const RowShare& sh, 
 }
 
 // The wave driver (crc_drive) fed from the row descriptor cache: one
-// ticket per wave.
+// ticket per wave; lpt: the slots were staged longest first (row_desc_stage).
 template <class Op>
 struct FeedRowCache {
   RowShare sh;
   int kind;
+  bool lpt;
   __device__ bool take(uint32_t* span, SpanDesc* d) {
     const uint32_t t = __builtin_amdgcn_readfirstlane(lds_ticket(lds_p32(kLdsRowTicket)));
     const uint32_t share = sh.n;
     if (t >= share) return false;
-    *span = sh.idx(t);
     const uint4 v = row_desc(t, share);
-    d->off = ((uint64_t)v.y << 32) | v.x;
+    const uint32_t hi = lpt ? v.y & ((1u << kLptSlotShift) - 1) : v.y;
+    *span = sh.idx(lpt ? v.y >> kLptSlotShift : t);
+    d->off = ((uint64_t)hi << 32) | v.x;
     d->len = v.z;
     d->init = kind == kInitArray ? v.w : *lds_p32(kLdsRowInit + 4 * (kind == kInitTyped ? (v.w & 15u) : 0u));
     return true;
@@ -1139,7 +1182,8 @@ struct FeedRowCache {
 // Ragged batches, driver chosen per workgroup from its share's mean span
 // length (the host cannot see device-resident lengths): 8-lane rows for
 // short spans, 16-lane rows for spans up to a few KiB, the wave driver
-// above that.  force: 0 = by length, 1 = wave, 2 = rows16, 3 = rows8, 5 = rows4.
+// above that.  force: 0 = by length, 1 = wave, 2 = rows16, 3 = rows8,
+// 5 = rows4, 6 = one lane per span.
 // (Superseded for long spans by crc_auto_units_driver, mck_crc_units.hpp.)
 constexpr uint32_t kAutoRows8Max = 640;    // mean span bytes
 constexpr uint32_t kAutoRows16Max = 2560;
@@ -1147,7 +1191,11 @@ constexpr uint32_t kAutoRows16WasteMax = 8192;  // mean span bytes, with > 25 % 
 template <class Op, bool T>
 __device__ __forceinline__ void crc_auto_driver(const Op& op, const RowShare& sh, uint8_t* lds,
                                                 const CrcTables* __restrict__ g, int force) {
-  crc_rows_prologue<Op>(op, sh, lds, g, true);
+  const bool lpt = force == 1;  // the wave driver, chosen before staging
+  crc_rows_prologue<Op>(op, sh, lds, g, true, lpt);
+#if MCK_PROLOGUE_ONLY == 1  // timing experiments only (wrong output): the prologue alone
+  return;
+#endif
   const uint32_t share = sh.n;
   const uint64_t total = *lds_p64(kLdsRowTotal);
   const uint64_t mean = total / (share ? share : 1);
@@ -1160,14 +1208,16 @@ __device__ __forceinline__ void crc_auto_driver(const Op& op, const RowShare& sh
                    : mean <= kAutoRows16Max ? 2
                    : ragged4k               ? 2
                                             : 1;
-  if (mode == 5) {
+  if (mode == 6) {
+    crc_rows_loop<Op, 1>(op, sh, g);
+  } else if (mode == 5) {
     crc_rows_loop<Op, 4>(op, sh, g);
   } else if (mode == 3) {
     crc_rows_loop<Op, 8>(op, sh, g);
   } else if (mode == 2) {
     crc_rows_loop<Op, 16>(op, sh, g);
   } else {
-    FeedRowCache<Op> f{sh, op.init_kind()};
+    FeedRowCache<Op> f{sh, op.init_kind(), lpt};
     crc_drive<Op, FeedRowCache<Op>, T>(op, f, crc_lane());
   }
 }

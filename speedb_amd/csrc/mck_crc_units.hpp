@@ -538,6 +538,7 @@ __device__ __forceinline__ void crc_units_driver(const Op& op, const RowShare& s
 // force: 0 = by length, 1 = the 4 KiB-round wave driver, 2 = rows16,
 // 3 = rows8, 4 = unit stream, 5 = rows4.
 constexpr uint32_t kAutoUnitsMin = 2560, kAutoUnitsMax = 8192;  // mean span bytes
+constexpr uint32_t kAutoRows1Max = 80;
 template <class Op, bool T, bool BLK>
 __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t first, uint32_t count, uint8_t* lds,
                                                       const CrcTables* __restrict__ g, int force) {
@@ -545,6 +546,9 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
   // interleaved under the test hook) -- every driver works on the same one
   const RowShare sh = row_share<BLK>(first, count);
   if (sh.n == 0) return;  // workgroup-uniform (the row feed would read an unstaged slot 0)
+#if MCK_PROLOGUE_ONLY == 2  // timing experiments only (wrong output): an empty kernel
+  return;
+#endif
   int mode = force;
   if (!mode) {
     // the share's bytes, and the bytes the wave driver's 4 KiB rounds would
@@ -571,12 +575,17 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
     }
     __syncthreads();  // the scratch is overwritten by the drivers' fills
     const uint64_t mean = total / (sh.n ? sh.n : 1);
+    // one lane per span below ~80 B (20-100 B: 0.16-0.19 vs 0.09 of peak on
+    // 8-lane rows, whose 512-B rounds are mostly padding there; 50-150 B:
+    // 0.14 vs 0.15, 100-300 B: 0.17 vs 0.25 -- a lane's span switch every
+    // few rounds costs the whole wave);
     // the unit stream for spans of a few KiB that waste the wave driver's
     // rounds (4100-4400 B: 0.60 vs 0.54 of peak); aligned 4 KiB multiples
     // and the long spans of the SST mix stay on the wave driver (4096 B: 0.74
     // vs 0.69; 4/16/64 KiB mix: 0.67 vs 0.57)
     const bool waste = 4 * wtotal > 5 * total;
-    mode = mean <= kAutoRows8Max        ? 3
+    mode = mean <= kAutoRows1Max        ? 6
+           : mean <= kAutoRows8Max      ? 3
            : mean <= kAutoUnitsMin      ? 2
            : mean <= kAutoUnitsMax && waste ? 4
                                         : 1;

@@ -1027,7 +1027,6 @@ __device__ __forceinline__ uint32_t crc_span_wave(const uint8_t* p, uint64_t n, 
 __device__ __forceinline__ uint4 wal_hdr16(const uint8_t* wal, uint32_t b) {
   return vload16_any(reinterpret_cast<uint64_t>(wal) + (uint64_t)b * 32768);
 }
-__device__ __forceinline__ uint32_t rfl_u32(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 // ReadPhysicalRecord's header checks (db/log_reader.cc:450-560) for the
 // record at a block offset with `left` bytes to the block's end: go = 1 when
