@@ -552,12 +552,14 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
   int mode = force;
   if (!mode) {
     // the share's bytes, and the bytes the wave driver's 4 KiB rounds would
-    // cover (each span rounded up to 4 KiB)
+    // cover (each span's 16-byte-aligned extent rounded up to 4 KiB: a
+    // 4096-B span off the 16-byte grid takes two rounds)
     uint64_t sum = 0, wsum = 0;
     for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) {
-      const uint64_t n = op.len(sh.idx(t));
+      const uint32_t i = sh.idx(t);
+      const uint64_t n = op.len(i), o = op.off(i) & 15u;
       sum += n;
-      wsum += (n + 4095) & ~4095ull;
+      wsum += (((o + n + 15) & ~15ull) + 4095) & ~4095ull;
     }
     for (int m = 32; m >= 1; m >>= 1) {
       sum += __shfl_xor(sum, m, 64);
@@ -583,11 +585,15 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
     // rounds (4100-4400 B: 0.60 vs 0.54 of peak); aligned 4 KiB multiples
     // and the long spans of the SST mix stay on the wave driver (4096 B: 0.74
     // vs 0.69; 4/16/64 KiB mix: 0.67 vs 0.57)
+    // Ops with epilogue inputs run 4 unit slots (unit_slots_of) and lose
+    // there: blob records of 16 + 4096 B at 16-byte-misaligned offsets read
+    // 0.42 of peak on the unit stream, 0.55 on 16-lane rows.
     const bool waste = 4 * wtotal > 5 * total;
+    const int few = unit_slots_of<Op>() == 8 ? 4 : 2;
     mode = mean <= kAutoRows1Max        ? 6
            : mean <= kAutoRows8Max      ? 3
            : mean <= kAutoUnitsMin      ? 2
-           : mean <= kAutoUnitsMax && waste ? 4
+           : mean <= kAutoUnitsMax && waste ? few
                                         : 1;
   }
   if (mode == 4)
