@@ -78,4 +78,63 @@ __device__ __forceinline__ uint32_t lds_ticket(P ctr) {
   return (uint32_t)__builtin_amdgcn_ds_bpermute(0, (int)t);
 }
 
+// Byte-balanced contiguous shares of a ragged batch [first, first + count)
+// over the grid.  Workgroup b's boundary is the first span whose offset
+// reaches b/G of the batch's offset range, searched over S = min(count, 8192)
+// evenly spaced samples of the offsets (span k * count / S, one load per
+// thread per 1024 samples); "the first sample at or past a target" is
+// monotone in the target for ANY offsets, so the shares always partition the
+// batch, and they are balanced to ~count/S spans when the offsets grow with
+// the bytes (an SST or blob file image).  Each boundary is clamped to within
+// `slack` spans of the count-balanced one (the row drivers' descriptor cache
+// bounds a share's spans).  Count-balanced shares hand the SST verify mix's
+// workgroups up to 1.2x the mean bytes (their end times spread 165-209 us
+// over a 1 GiB image).  scratch: 2 x u32 in LDS.  Workgroup-uniform; has
+// barriers.
+template <class F>
+__device__ __forceinline__ uint32_t k_or_count(uint32_t k, uint32_t S, uint32_t count, const F& idx) {
+  return k >= S ? count : idx(k);
+}
+template <class Op, class P>
+__device__ __forceinline__ void share_by_bytes(const Op& op, uint32_t first, uint32_t count, uint32_t slack,
+                                               P scratch, uint32_t* lo, uint32_t* hi) {
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t clo = (uint32_t)((uint64_t)count * b / G), chi = (uint32_t)((uint64_t)count * (b + 1) / G);
+  constexpr uint32_t kS = 8192;  // 2^13
+  const uint32_t S = count < kS ? count : kS;
+  if (S == 0 || G == 1) {
+    *lo = clo;
+    *hi = chi;
+    return;
+  }
+  if (threadIdx.x < 2) scratch[threadIdx.x] = S;
+  __syncthreads();
+  const uint64_t o0 = op.off(first), oL = op.off(first + count - 1);
+  const uint64_t range = oL > o0 ? oL - o0 : 0;
+  const uint64_t tb = o0 + range * b / G, te = o0 + range * (b + 1) / G;
+  uint32_t kb = S, ke = S;
+  // sample k is span k * count / S: k itself when S = count, else (S = 2^13)
+  // a shift (no 64-bit division per sample)
+  for (uint32_t k = threadIdx.x; k < S; k += blockDim.x) {
+    const uint32_t i = S == count ? k : (uint32_t)(((uint64_t)k * count) >> 13);
+    const uint64_t o = op.off(first + i);
+    kb = (o >= tb && k < kb) ? k : kb;
+    ke = (o >= te && k < ke) ? k : ke;
+  }
+  if (kb < S) __hip_atomic_fetch_min(&scratch[0], kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (ke < S) __hip_atomic_fetch_min(&scratch[1], ke, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __syncthreads();
+  kb = scratch[0];
+  ke = scratch[1];
+  __syncthreads();  // the scratch may be reused
+  const auto clampb = [&](uint32_t x, uint32_t c) {
+    const uint32_t a = c > slack ? c - slack : 0u;
+    const uint64_t z = (uint64_t)c + slack < count ? (uint64_t)c + slack : count;
+    return x < a ? a : x > z ? (uint32_t)z : x;
+  };
+  const auto idx = [&](uint32_t k) { return S == count ? k : (uint32_t)(((uint64_t)k * count) >> 13); };
+  *lo = b == 0 ? 0u : clampb(k_or_count(kb, S, count, idx), clo);
+  *hi = b + 1 == G ? count : clampb(k_or_count(ke, S, count, idx), chi);
+}
+
 }  // namespace mck

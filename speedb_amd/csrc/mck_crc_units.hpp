@@ -536,7 +536,7 @@ __device__ __forceinline__ void crc_units_driver(const Op& op, const RowShare& s
 // spans would leave the wave driver's 4 KiB rounds > 20 % empty, else the
 // wave driver.
 // force: 0 = by length, 1 = the 4 KiB-round wave driver, 2 = rows16,
-// 3 = rows8, 4 = unit stream, 5 = rows4.
+// 3 = rows8, 4 = unit stream, 5 = rows4, 6 = one lane per span.
 constexpr uint32_t kAutoUnitsMin = 2560, kAutoUnitsMax = 8192;  // mean span bytes
 constexpr uint32_t kAutoRows1Max = 80;
 template <class Op, bool T, bool BLK>
@@ -590,11 +590,11 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
     // 0.42 of peak on the unit stream, 0.55 on 16-lane rows.
     const bool waste = 4 * wtotal > 5 * total;
     const int few = unit_slots_of<Op>() == 8 ? 4 : 2;
-    mode = mean <= kAutoRows1Max        ? 6
-           : mean <= kAutoRows8Max      ? 3
-           : mean <= kAutoUnitsMin      ? 2
+    mode = mean <= kAutoRows1Max            ? 6
+           : mean <= kAutoRows8Max          ? 3
+           : mean <= kAutoUnitsMin          ? 2
            : mean <= kAutoUnitsMax && waste ? few
-                                        : 1;
+                                            : 1;
   }
   if (mode == 4)
     crc_units_driver<Op>(op, sh, g);

@@ -902,15 +902,15 @@ __device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, c
   }
 }
 
-// Workgroup b's share: spans b, b + G, ... (interleaved: the grid sweeps the
-// batch front to back together), staged in windows of kX3DescCache spans,
-// long spans in pieces.
+// Workgroup b's share: a byte-balanced contiguous range (share_by_bytes),
+// staged in windows of kX3DescCache spans, long spans in pieces.
 template <class Op, bool PREVIEW>
 __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, uint64_t seed) {
   __shared__ X3Lds s;
-  const uint32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
-  const uint32_t start = b, stride = G, n = count > b ? (count - b + G - 1) / G : 0;
+  uint32_t lo, hi;
+  share_by_bytes(op, 0u, count, 0xFFFFFFFFu, &s.wsum[0], &lo, &hi);
+  const uint32_t start = lo, stride = 1, n = hi - lo;
   const X3Row X = x3_row(seed);
   for (uint32_t w0 = 0; w0 < n; w0 += kX3DescCache) {
     const uint32_t wn = n - w0 < kX3DescCache ? n - w0 : kX3DescCache;
