@@ -442,6 +442,9 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
   uint64_t shv = 0;
   bool sv = false;
 #endif
+  // the raw last dword (d[3].w) of each lane's previous segment: lane 15's is
+  // the dword before the row's next segment (e0 below)
+  uint32_t pw = 0;
   while (__any(act)) {
     // loads first and unconditional (clamped when a stripe is not part of
     // the segment, or the row is idle), so they are counted and in flight
@@ -468,7 +471,23 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
     // at 4 KiB (PMC traffic 1.09x, non-temporal loads do not keep the line)
     const uint64_t lsa = full ? seg + 16 * X.q - sh + 4 : lst + 16 * X.q - shl + 4;
     uint4 dl = gload16u(act ? lsa : idle);
-    const uint32_t e0 = gload4(act && seg - sh >= idle ? seg - sh : idle);
+    // the dword before the segment: loaded only at the span's first segment;
+    // later it is the previous segment's last dword, already in lane 15's
+    // registers -- re-reading it fetched that line again (non-temporal loads
+    // do not keep it): PMC traffic 1.107x at 4 KiB
+    // (XXH3 only: the XXPH3 users -- per-KV protection, ~1 KiB spans of one
+    // segment -- would pay the register for nothing: OpKvProtect<true> went
+    // from 128 to 130 VGPRs, 4 -> 3 waves per SIMD, -6 %)
+    uint32_t e0;
+    if constexpr (!PREVIEW) {
+      const uint32_t e0l = gload4(act && rs.g == 0 && seg - sh >= idle ? seg - sh : act ? seg - sh + 4 : idle);
+      const uint32_t w3 = d[3].w;
+      const uint32_t e0p = dpp32<kDppRowRor1>(pw);  // lane 0 of the row (the one user) <- lane 15
+      e0 = rs.g ? e0p : e0l;
+      pw = w3;
+    } else {
+      e0 = gload4(act && seg - sh >= idle ? seg - sh : idle);
+    }
     const uint32_t el = gload4(act ? (full ? seg - sh + 4 : lst - shl) : idle);
 #if !MCK_X3_STASH
     // the span's epilogue inputs travel with its data (see BlockPre / KvPre)
