@@ -743,7 +743,7 @@ constexpr uint32_t kLdsRowTicket = kLdsRowDesc + 16 * kRowDescCache;  // u32
 constexpr uint32_t kLdsRowMaskHead = kLdsRowTicket + 64;
 constexpr uint32_t kLdsRowMaskTail = kLdsRowMaskHead + 256;
 static_assert(kLdsRowMaskTail + 256 <= kLdsStep, "row tables must fit below the step tables");
-static_assert(kLdsRowTicket + 24 <= kLdsRowMaskHead, "ticket + totals");
+static_assert(kLdsRowTicket + 32 <= kLdsRowMaskHead, "ticket + totals");
 static_assert(offsetof(CrcTables, gap_row) - offsetof(CrcTables, unshift) == kMaxUnshift * 512, "layout");
 static_assert(sizeof(((CrcTables*)nullptr)->gap_row[0]) == 512, "one row gap map = 32 slots");
 
@@ -981,6 +981,7 @@ constexpr uint32_t kLdsRowTotal = kLdsRowTicket + 8;  // u64
 // ... and the bytes the wave driver's 4 KiB rounds would cover (each span
 // rounded up to 4 KiB: a partial round costs it about as much as a full one)
 constexpr uint32_t kLdsRowWaveTotal = kLdsRowTicket + 16;  // u64
+constexpr uint32_t kLdsRowLongs = kLdsRowTicket + 24;      // u32: spans of >= 8 KiB
 // A workgroup's share of spans [first, first + count): span first + b + G t
 // (interleaved: the grid sweeps the batch front to back together) or, BLK,
 // the contiguous range [count b / G, count (b + 1) / G) (neighbouring spans
@@ -1027,12 +1028,17 @@ __device__ __forceinline__ void row_desc_stage(const Op& op, const RowShare& sh,
     __syncthreads();
   }
   uint64_t sum = 0, wsum = 0;
+  uint32_t longs = 0;  // spans of >= 8 KiB (longest-first order matters only with them)
   for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
     const uint32_t i = sh.idx(t);
     const uint64_t off = op.off(i);
     const uint32_t len = (uint32_t)op.len(i);
     sum += len;
-    wsum += ((uint64_t)len + 4095) & ~4095ull;
+    longs += lpt_class(len) < 3 ? 1u : 0u;
+    // the bytes the wave driver's 4 KiB rounds would cover: the span's
+    // 16-byte-aligned extent rounded up to 4 KiB (a 4096-B span off the
+    // 16-byte grid takes two rounds)
+    wsum += ((((off + reinterpret_cast<uint64_t>(op.base())) & 15u) + len + 15 + 4095) & ~4095ull);
     span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, op.init_key(i)};
     uint32_t pos = t;
     if (lpt) {
@@ -1052,15 +1058,18 @@ __device__ __forceinline__ void row_desc_stage(const Op& op, const RowShare& sh,
     for (int m = 32; m >= 1; m >>= 1) {
       sum += __shfl_xor(sum, m, 64);
       wsum += __shfl_xor(wsum, m, 64);
+      longs += (uint32_t)__shfl_xor((int)longs, m, 64);
     }
     if (threadIdx.x == 0) {
       *lds_p64(kLdsRowTotal) = 0;
       *lds_p64(kLdsRowWaveTotal) = 0;
+      *lds_p32(kLdsRowLongs) = 0;
     }
     __syncthreads();
     if ((threadIdx.x & 63) == 0) {
       __hip_atomic_fetch_add(lds_p64(kLdsRowTotal), sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __hip_atomic_fetch_add(lds_p64(kLdsRowWaveTotal), wsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (longs) __hip_atomic_fetch_add(lds_p32(kLdsRowLongs), longs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
 }
@@ -1188,14 +1197,11 @@ struct FeedRowCache {
 constexpr uint32_t kAutoRows8Max = 640;    // mean span bytes
 constexpr uint32_t kAutoRows16Max = 2560;
 constexpr uint32_t kAutoRows16WasteMax = 8192;  // mean span bytes, with > 25 % of the wave rounds empty
+// The drivers over a staged share (crc_rows_prologue done): force = the
+// driver chosen, else by the staging's totals.
 template <class Op, bool T>
-__device__ __forceinline__ void crc_auto_driver(const Op& op, const RowShare& sh, uint8_t* lds,
-                                                const CrcTables* __restrict__ g, int force) {
-  const bool lpt = force == 1;  // the wave driver, chosen before staging
-  crc_rows_prologue<Op>(op, sh, lds, g, true, lpt);
-#if MCK_PROLOGUE_ONLY == 1  // timing experiments only (wrong output): the prologue alone
-  return;
-#endif
+__device__ __forceinline__ void crc_auto_dispatch(const Op& op, const RowShare& sh, const CrcTables* __restrict__ g,
+                                                  int force, bool lpt) {
   const uint32_t share = sh.n;
   const uint64_t total = *lds_p64(kLdsRowTotal);
   const uint64_t mean = total / (share ? share : 1);

@@ -550,32 +550,17 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
   return;
 #endif
   int mode = force;
+  bool lpt = force == 1;
   if (!mode) {
-    // the share's bytes, and the bytes the wave driver's 4 KiB rounds would
-    // cover (each span's 16-byte-aligned extent rounded up to 4 KiB: a
-    // 4096-B span off the 16-byte grid takes two rounds)
-    uint64_t sum = 0, wsum = 0;
-    for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) {
-      const uint32_t i = sh.idx(t);
-      const uint64_t n = op.len(i), o = op.off(i) & 15u;
-      sum += n;
-      wsum += (((o + n + 15) & ~15ull) + 4095) & ~4095ull;
-    }
-    for (int m = 32; m >= 1; m >>= 1) {
-      sum += __shfl_xor(sum, m, 64);
-      wsum += __shfl_xor(wsum, m, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      *lds_p64(kULdsDesc + 16 * (threadIdx.x >> 6)) = sum;
-      *lds_p64(kULdsDesc + 16 * (threadIdx.x >> 6) + 8) = wsum;
-    }
-    __syncthreads();
-    uint64_t total = 0, wtotal = 0;
-    for (uint32_t w = 0; w < blockDim.x / 64; w++) {
-      total += *lds_p64(kULdsDesc + 16 * w);
-      wtotal += *lds_p64(kULdsDesc + 16 * w + 8);
-    }
-    __syncthreads();  // the scratch is overwritten by the drivers' fills
+    // Stage the share for the row drivers first (LDS tables, descriptors,
+    // init tables) and choose from the staging's totals: the share's bytes
+    // and the bytes the wave driver's 4 KiB rounds would cover.  Row-driver
+    // shares (short spans, many launches per batch) then read their lengths
+    // once instead of twice; the wave driver restages longest first and the
+    // unit stream stages its own.
+    crc_rows_prologue<Op>(op, sh, lds, g, true, false);
+    const uint64_t total = *lds_p64(kLdsRowTotal), wtotal = *lds_p64(kLdsRowWaveTotal);
+    const bool longs = *lds_p32(kLdsRowLongs) != 0;
     const uint64_t mean = total / (sh.n ? sh.n : 1);
     // one lane per span below ~80 B (20-100 B: 0.16-0.19 vs 0.09 of peak on
     // 8-lane rows, whose 512-B rounds are mostly padding there; 50-150 B:
@@ -595,11 +580,19 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
            : mean <= kAutoUnitsMin          ? 2
            : mean <= kAutoUnitsMax && waste ? few
                                             : 1;
+    __syncthreads();  // every wave has read the totals (the unit stream refills the LDS)
+    if (mode == 1 && longs) {  // longest first for the wave driver (with spans of >= 8 KiB)
+      row_desc_stage<Op>(op, sh, false, true);
+      __syncthreads();
+    }
+    lpt = mode == 1 && longs;
+  } else if (force != 4) {
+    crc_rows_prologue<Op>(op, sh, lds, g, true, force == 1);
   }
   if (mode == 4)
     crc_units_driver<Op>(op, sh, g);
   else
-    crc_auto_driver<Op, T>(op, sh, lds, g, mode);
+    crc_auto_dispatch<Op, T>(op, sh, g, mode, lpt);
 }
 
 }  // namespace mck
