@@ -47,6 +47,7 @@ typedef struct ihipStream_t* mck_stream_t;
 #define MCK_ENOMEM (-4)   /* staging allocation failed                    */
 #define MCK_ECORRUPT (-5) /* corrupt SST structure (footer, handles ...)  */
 #define MCK_ENOTSUP (-6)  /* valid but unsupported here (e.g. compressed index) */
+#define MCK_EAGAIN (-7)   /* call again after supplying what the call asked for */
 
 /* ---- checksum types: include/rocksdb/table.h:69-75 ChecksumType ---------- */
 #define MCK_kNoChecksum 0
@@ -393,7 +394,9 @@ int mck_wal_tail_set_image(mck_wal_tail* r, const void* wal, uint64_t nbytes,
 /* FragmentBufferedReader::ReadRecord.  Returns 1 with a record (*nfrags
  * payload fragments, *record_bytes, *last_record_offset = LastRecordOffset;
  * the fragments via mck_wal_tail_record_fragments), 0 when no complete
- * record is available yet, a negative MCK_E* code on error. */
+ * record is available yet, MCK_EAGAIN when it needs CRC verdicts no block
+ * result holds (see mck_wal_tail_pending_verify), another negative MCK_E*
+ * code on error. */
 int mck_wal_tail_read_record(mck_wal_tail* r, uint64_t* nfrags, uint64_t* record_bytes,
                              uint64_t* last_record_offset);
 
@@ -404,6 +407,27 @@ int mck_wal_tail_record_fragments(const mck_wal_tail* r, mck_wal_fragment* frags
 /* Reader::UnmarkEOF / IsEOF. */
 int mck_wal_tail_unmark_eof(mck_wal_tail* r);
 int mck_wal_tail_is_eof(const mck_wal_tail* r);
+
+/* After MCK_EAGAIN: the reader passed a checksum failure inside a block that
+ * was partly written when it was verified (the failure dropped a buffer that
+ * ended at the file's end; the block then grew and UnmarkEOF reads on behind
+ * it, db/log_reader.cc:340-397), and a block result stops at its block's
+ * first failure.  Returns 1 with [*file_offset, +*nbytes) = the rest of that
+ * block as written so far: verify it as one block (mck_wal_verify_batch over
+ * wal + *file_offset, *nbytes bytes -> one result), hand the result to
+ * mck_wal_tail_add_verdict and call ReadRecord again (nothing was consumed).
+ * 0 when no verdict is pending. */
+int mck_wal_tail_pending_verify(const mck_wal_tail* r, uint64_t* file_offset, uint64_t* nbytes);
+int mck_wal_tail_add_verdict(mck_wal_tail* r, uint64_t file_offset, const mck_wal_block_result* result);
+
+/* 1 when the last ReadRecord stopped at a recyclable record of an OLDER log
+ * instance (its log number is not this reader's): *header_offset = that
+ * header's file offset.  The reference's FragmentBufferedReader re-parses the
+ * same header forever there (db/log_reader.cc:736-747 + :864-867); this
+ * reader returns "no record" without consuming it, so every later call stops
+ * at the same header whatever is appended -- a caller tells that stall apart
+ * from "waiting for data" here.  0 otherwise. */
+int mck_wal_tail_old_record(const mck_wal_tail* r, uint64_t* header_offset);
 
 /* Reporter::Corruption calls so far: *n reports (up to cap stored) and the
  * total dropped bytes. */

@@ -124,6 +124,9 @@ SIGNATURES = [
     ("mck_wal_tail_record_fragments", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("mck_wal_tail_unmark_eof", ctypes.c_int, [vp]),
     ("mck_wal_tail_is_eof", ctypes.c_int, [vp]),
+    ("mck_wal_tail_old_record", ctypes.c_int, [vp, vp]),
+    ("mck_wal_tail_pending_verify", ctypes.c_int, [vp, vp, vp]),
+    ("mck_wal_tail_add_verdict", ctypes.c_int, [vp, ctypes.c_uint64, vp]),
     ("mck_wal_tail_reports", ctypes.c_int, [vp, vp, ctypes.c_uint64, vp, vp]),
     ("mck_blob_list_records", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
     ("mck_blob_record_batch", ctypes.c_int,

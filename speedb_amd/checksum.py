@@ -24,6 +24,8 @@ from typing import NamedTuple, Optional
 
 from ._lib import check, lib, mck_spans, mck_wal_block_result
 
+MCK_EAGAIN = -7  # mck.h: call again after supplying what the call asked for
+
 # ---------------------------------------------------------------------------
 # enums / status
 # ---------------------------------------------------------------------------
@@ -743,9 +745,10 @@ class FragmentBufferedReader:
         h = ctypes.c_void_p()
         check(lib.mck_wal_tail_create(self.log_number, ctypes.byref(h)), "mck_wal_tail_create")
         self._h = h
-        self._img = b""
-        self._host = None
-        self._ver = None
+        self._buf = ctypes.create_string_buffer(1)  # host image (capacity grows by doubling)
+        self._len = 0
+        self._ver = None       # per-block verdicts of a callable verifier
+        self._hver = None
         self._dev = None       # device image (capacity grows by doubling)
         self._dver = None      # device per-block verdicts
         self._clean = 0        # blocks [0, _clean) were verified complete
@@ -784,25 +787,79 @@ class FragmentBufferedReader:
             return np.ascontiguousarray(self._dver[:nb].cpu().numpy().astype(np.int32))
 
     def SetFile(self, image) -> None:
-        img = bytes(image)
-        if len(img) < len(self._img) or img[:len(self._img)] != self._img:
-            raise ValueError("a WAL file only grows: the bytes already written must not change")
-        self._img = img
+        """The file as written so far.  It only grows: the bytes already
+        handed out must not change (checked over the last block before the
+        old end, not the whole prefix, so a poll costs the appended bytes)."""
         np = self._np
+        img = memoryview(bytes(image) if not isinstance(image, (bytes, bytearray)) else image)
+        old = self._len
+        n = len(img)
+        lo = max(0, old - 32768)
+        if n < old or bytes(img[lo:old]) != bytes(self._buf[lo:old]):
+            raise ValueError("a WAL file only grows: the bytes already written must not change")
+        if n + 1 > len(self._buf):  # the host image: capacity doubles, only the suffix is copied
+            buf = ctypes.create_string_buffer(max(n + 1, 2 * len(self._buf), 1 << 16))
+            ctypes.memmove(buf, self._buf, old)
+            self._buf = buf
+        if n > old:
+            ctypes.memmove(ctypes.addressof(self._buf) + old, bytes(img[old:n]), n - old)
+        self._len = n
+        nb = -(-n // 32768)
         if self.verify == "device":
-            ver = self._device_verdicts(img) if img else None
+            ver = self._device_verdicts(img) if n else None
         elif callable(self.verify):
-            ver = np.ascontiguousarray(np.asarray(self.verify(img), dtype=np.int64).astype(np.int32)) if img else None
+            # re-verify from the first block not verified complete (the blocks
+            # before it cannot change)
+            if self._ver is None or self._ver.shape[0] < nb:
+                v = np.zeros((max(nb, 1), 4), np.int32)
+                if self._ver is not None:
+                    v[:self._ver.shape[0]] = self._ver
+                self._ver = v
+            c = self._clean
+            if n > c * 32768:
+                res = np.asarray(self.verify(bytes(img[c * 32768:n])), dtype=np.int64).astype(np.int32)
+                self._ver[c:c + len(res)] = res.reshape(-1, 4)
+            self._clean = n // 32768
+            ver = self._ver if n else None
         else:
             ver = None
-        self._host = ctypes.create_string_buffer(img, len(img) + 1)
-        self._ver = ver
-        check(lib.mck_wal_tail_set_image(self._h, self._host, len(img),
+        self._hver = ver
+        check(lib.mck_wal_tail_set_image(self._h, self._buf, n,
                                          ver.ctypes.data if ver is not None else None), "mck_wal_tail_set_image")
+
+    @property
+    def _img(self) -> bytes:
+        return self._buf.raw[:self._len]
+
+    def _supply_verdict(self) -> None:
+        """MCK_EAGAIN: verify the rest of a block the reader passed a checksum
+        failure in (mck_wal_tail_pending_verify) as one block."""
+        np = self._np
+        off, n = ctypes.c_uint64(), ctypes.c_uint64()
+        if not lib.mck_wal_tail_pending_verify(self._h, ctypes.byref(off), ctypes.byref(n)):
+            raise RuntimeError("mck_wal_tail_read_record asked for a verdict but none is pending")
+        o, k = off.value, n.value
+        if self.verify == "device":
+            torch = _torch()
+            dev = torch.device("cuda") if self.device is None else self.device
+            st = self.stream if self.stream is not None else torch.cuda.current_stream(dev)
+            with torch.cuda.stream(st):
+                res = torch.zeros((1, 4), dtype=torch.int32, device=dev)
+                check(lib.mck_wal_verify_batch(self._dev.data_ptr() + o, k, self.log_number, res.data_ptr(),
+                                               _stream(st)), "mck_wal_verify_batch")
+                r = np.ascontiguousarray(res.cpu().numpy().astype(np.int32))
+        else:
+            r = np.ascontiguousarray(np.asarray(self.verify(self._buf.raw[o:o + k]), dtype=np.int64)
+                                     .astype(np.int32)[:1])
+        check(lib.mck_wal_tail_add_verdict(self._h, o, r.ctypes.data), "mck_wal_tail_add_verdict")
 
     def ReadRecord(self) -> Optional[bytes]:
         nf, nb, lro = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-        rc = lib.mck_wal_tail_read_record(self._h, ctypes.byref(nf), ctypes.byref(nb), ctypes.byref(lro))
+        while True:
+            rc = lib.mck_wal_tail_read_record(self._h, ctypes.byref(nf), ctypes.byref(nb), ctypes.byref(lro))
+            if rc != MCK_EAGAIN:
+                break
+            self._supply_verdict()
         if rc < 0:
             check(rc, "mck_wal_tail_read_record")
         if rc == 0:
@@ -812,9 +869,18 @@ class FragmentBufferedReader:
               "mck_wal_tail_record_fragments")
         self.last_record_offset = lro.value
         out = bytearray(nb.value)
+        raw = self._buf
         for f in frags[:nf.value]:
-            out[f.dst_off:f.dst_off + f.length] = self._img[f.src_off:f.src_off + f.length]
+            out[f.dst_off:f.dst_off + f.length] = ctypes.string_at(ctypes.addressof(raw) + f.src_off, f.length)
         return bytes(out)
+
+    def OldRecordOffset(self) -> Optional[int]:
+        """The header offset of an older log instance's record the reader is
+        stopped at (it returns "no record" there forever, where the
+        reference's FragmentBufferedReader would re-parse the same header
+        without end), or None."""
+        off = ctypes.c_uint64()
+        return off.value if lib.mck_wal_tail_old_record(self._h, ctypes.byref(off)) else None
 
     def LastRecordOffset(self) -> int:
         return getattr(self, "last_record_offset", 0)

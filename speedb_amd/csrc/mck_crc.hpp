@@ -1038,7 +1038,7 @@ __device__ __forceinline__ void row_desc_stage(const Op& op, const RowShare& sh,
     // the bytes the wave driver's 4 KiB rounds would cover: the span's
     // 16-byte-aligned extent rounded up to 4 KiB (a 4096-B span off the
     // 16-byte grid takes two rounds)
-    wsum += ((((off + reinterpret_cast<uint64_t>(op.base())) & 15u) + len + 15 + 4095) & ~4095ull);
+    wsum += (((((off + reinterpret_cast<uint64_t>(op.base())) & 15u) + len + 15) & ~15ull) + 4095) & ~4095ull;
     span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, op.init_key(i)};
     uint32_t pos = t;
     if (lpt) {

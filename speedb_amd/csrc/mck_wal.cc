@@ -464,6 +464,9 @@ struct mck_wal_tail {
   const mck_wal_block_result* verified = nullptr;
   uint64_t buf_off = 0, buf_size = 0, end_of_buffer_offset = 0;
   uint64_t eof_offset = 0;
+  // the header of a record of an older log instance the reader stopped at
+  // (~0: none); see mck_wal_tail_old_record
+  uint64_t old_record_offset = ~0ull;
   bool eof = false, recycled = false, first_record_read = false, in_fragmented_record = false;
   uint64_t last_record_offset = 0;
   std::vector<mck_wal_fragment> fragments;  // fragments_ (dst_off within the record)
@@ -516,14 +519,40 @@ struct mck_wal_tail {
     unmark_eof();
     return true;
   }
-  bool crc_ok(uint64_t h) {
-    if (!verified) return true;
-    const mck_wal_block_result& r = verified[h / MCK_WAL_kBlockSize];
+  // Verdicts of records after a checksum failure inside a block: only the
+  // tailing reader reaches them (the failure dropped a buffer that ended at
+  // the file's end, the block grew, and UnmarkEOF reads on behind it), and a
+  // block's verdict stops at its first failure.  The caller verifies the
+  // block from the first such record on (mck_wal_tail_pending_verify /
+  // mck_wal_tail_add_verdict); those verdicts are kept here.
+  struct SubVerdict {
+    uint64_t from;  // file offset the verification started at
+    mck_wal_block_result r;
+  };
+  std::vector<SubVerdict> sub;
+  uint64_t need_from = ~0ull;  // a verdict is needed from this offset on
+  // 1 = the CRC holds, 0 = it does not, -1 = no verdict covers h yet
+  int crc_ok(uint64_t h) {
+    if (!verified) return 1;
+    const uint64_t blk = h / MCK_WAL_kBlockSize;
+    for (size_t k = sub.size(); k-- > 0;) {  // the latest verification of h's block from at or before h
+      const SubVerdict& v = sub[k];
+      if (v.from / MCK_WAL_kBlockSize != blk || v.from > h) continue;
+      const uint64_t o = h - v.from;
+      if (o < v.r.stop_offset) return 1;
+      if (o == v.r.stop_offset && v.r.status == MCK_WAL_BAD_CHECKSUM) return 0;
+      break;
+    }
+    const mck_wal_block_result& r = verified[blk];
     const uint32_t o = (uint32_t)(h % MCK_WAL_kBlockSize);
-    if (o < r.stop_offset) return true;
-    if (o == r.stop_offset && r.status == MCK_WAL_BAD_CHECKSUM) return false;
+    if (o < r.stop_offset) return 1;
+    if (o == r.stop_offset && r.status == MCK_WAL_BAD_CHECKSUM) return 0;
+    if (r.status == MCK_WAL_BAD_CHECKSUM) {  // past the block's first failure
+      need_from = h;
+      return -1;
+    }
     err = MCK_EINVAL;  // stale or foreign verdicts (a block verified before it grew)
-    return false;
+    return 0;
   }
   // :826-931 TryReadFragment; true = the caller processes *type_or_err
   bool try_read_fragment(uint64_t* frag_off, uint32_t* frag_len, uint64_t* drop_size, uint32_t* type_or_err) {
@@ -547,6 +576,7 @@ struct mck_wal_tail {
       const uint8_t* g = d + buf_off;
       const uint32_t ln = (uint32_t)g[7] | ((uint32_t)g[8] << 8) | ((uint32_t)g[9] << 16) | ((uint32_t)g[10] << 24);
       if (ln != log_number) {
+        old_record_offset = buf_off;
         *type_or_err = kOldRecord;
         return true;
       }
@@ -556,13 +586,20 @@ struct mck_wal_tail {
       try_read_more();
       if (old == buf_size) return false;
     }
+    // buffer_.clear() (:880, :889-891): the window moves past what it held,
+    // so buf_off + buf_size stays end_of_buffer_offset and a later
+    // UnmarkEOFInternal appends the NEW bytes behind it
     if (type == kZeroType && length == 0) {
+      buf_off += buf_size;
       buf_size = 0;
       *type_or_err = kBadRecord;
       return true;
     }
-    if (!crc_ok(buf_off)) {
+    const int ok = crc_ok(buf_off);
+    if (ok < 0) return false;  // nothing consumed: ReadRecord returns MCK_EAGAIN
+    if (!ok) {
       *drop_size = buf_size;
+      buf_off += buf_size;
       buf_size = 0;
       *type_or_err = kBadRecordChecksum;
       return true;
@@ -588,6 +625,8 @@ struct mck_wal_tail {
     const uint64_t physical_record_offset = end_of_buffer_offset - buf_size;
     uint64_t drop_size = 0, foff = 0;
     uint32_t flen = 0, t = 0;
+    old_record_offset = ~0ull;
+    need_from = ~0ull;
     while (try_read_fragment(&foff, &flen, &drop_size, &t)) {
       if (err) return err;
       if (t == 1 || t == 5) {  // kFullType
@@ -665,7 +704,8 @@ struct mck_wal_tail {
         fragments_clear();
       }
     }
-    return err ? err : 0;
+    if (err) return err;
+    return need_from != ~0ull ? MCK_EAGAIN : 0;
   }
 };
 
@@ -745,6 +785,35 @@ extern "C" int mck_wal_tail_unmark_eof(mck_wal_tail* r) {
 }
 
 extern "C" int mck_wal_tail_is_eof(const mck_wal_tail* r) { return r && r->eof ? 1 : 0; }
+
+extern "C" int mck_wal_tail_pending_verify(const mck_wal_tail* r, uint64_t* file_offset, uint64_t* nbytes) {
+  if (!r || r->need_from == ~0ull) return 0;
+  const uint64_t end = std::min<uint64_t>((r->need_from / MCK_WAL_kBlockSize + 1) * MCK_WAL_kBlockSize, r->avail);
+  if (file_offset) *file_offset = r->need_from;
+  if (nbytes) *nbytes = end - r->need_from;
+  return 1;
+}
+
+extern "C" int mck_wal_tail_add_verdict(mck_wal_tail* r, uint64_t file_offset, const mck_wal_block_result* res) {
+  mck_internal_set_error("");
+  if (!r || !res) {
+    mck_internal_set_error("reader / result is NULL");
+    return MCK_EINVAL;
+  }
+  if (file_offset >= r->avail) {
+    mck_internal_set_error("verdict offset past the image");
+    return MCK_EINVAL;
+  }
+  r->sub.push_back(mck_wal_tail::SubVerdict{file_offset, *res});
+  r->need_from = ~0ull;
+  return MCK_OK;
+}
+
+extern "C" int mck_wal_tail_old_record(const mck_wal_tail* r, uint64_t* header_offset) {
+  if (!r || r->old_record_offset == ~0ull) return 0;
+  if (header_offset) *header_offset = r->old_record_offset;
+  return 1;
+}
 
 extern "C" int mck_wal_tail_reports(const mck_wal_tail* r, mck_wal_report* reports, uint64_t cap, uint64_t* n,
                                     uint64_t* dropped_bytes) {

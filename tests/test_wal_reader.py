@@ -428,7 +428,61 @@ def _tail_byte_by_byte(oracle, recycle, verify):
     assert got == msgs and r.dropped_bytes == 0
 
 
+def _tail_corrupt_then_append(oracle, recycle, verify):
+    """A checksum failure in a partly written block, then more records
+    appended to the same block: the failure drops only the buffer
+    up to the file's end (db/log_reader.cc:889-891 buffer_.clear()), the
+    reader reads on behind it (TryReadMore -> UnmarkEOF, :340-397, :785-823)
+    and returns every appended record; the bad record is reported once
+    (legacy) or ends the read silently (recyclable, :757-760)."""
+    L = Log(oracle, recycle)
+    L.write(b"foo")
+    bar_hdr = L.written()
+    L.write(b"bar")
+    L.increment_byte(bar_hdr + L.hs, 1)  # a payload byte of "bar"
+    r = _tail_reader(oracle, verify)
+    r.SetFile(bytes(L.w.buf))
+    assert r.ReadRecord() == b"foo"
+    assert r.ReadRecord() is None
+    _, first_dropped = r._reports()[1], r.dropped_bytes
+    L.write(b"baz")
+    L.write(big_string("qux", 1000))
+    r.SetFile(bytes(L.w.buf))
+    r.UnmarkEOF()
+    assert _read_all(r) == [b"baz", big_string("qux", 1000)]
+    reps, dropped = r._reports()
+    if recycle:
+        assert reps == [] and dropped == 0
+    else:
+        assert [(x[1], x[2]) for x in reps] == [(L.hs + 3, "checksum mismatch")]
+        assert dropped == first_dropped == L.hs + 3
+    assert r.OldRecordOffset() is None
+
+
+def _tail_old_record(oracle, recycle, verify):
+    """A recycled log whose tail still holds a record of the previous log
+    instance: the reader stops there and says so (OldRecordOffset), however
+    the file grows."""
+    if not recycle:
+        return
+    L = Log(oracle, recycle)
+    L.write(b"foo")
+    stale = WalWriter(oracle, log_number=LOG - 1, recycle=True)
+    stale.add_record(b"old!")
+    at = L.written()
+    L.w.buf += stale.buf
+    r = _tail_reader(oracle, verify)
+    r.SetFile(bytes(L.w.buf))
+    assert r.ReadRecord() == b"foo"
+    assert r.ReadRecord() is None
+    assert r.OldRecordOffset() == at
+    r.SetFile(bytes(L.w.buf) + b"\0" * 100)
+    assert r.ReadRecord() is None and r.OldRecordOffset() == at
+
+
 TAIL_CASES = {
+    "CorruptThenAppend": _tail_corrupt_then_append,
+    "OldRecordStall": _tail_old_record,
     "ClearEofSingleBlock": _clear_eof_single,
     "ClearEofMultiBlock": _clear_eof_multi,
     "TailLog_PartialHeader": lambda o, rc, v: _tail_two_parts(o, rc, v, lambda hs: hs - 1, b"foo"),
