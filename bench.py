@@ -133,7 +133,7 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="0 = the CPUs this process may use (cgroup quota / affinity)")
     p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--crc-driver", choices=["auto", "wave", "rows16", "rows8", "units", "rows4", "rows1"], default="auto",
+    p.add_argument("--crc-driver", choices=["auto", "wave", "rows16", "rows8", "units", "rows4", "rows1", "bh"], default="auto",
                    help="force the ragged CRC driver for every workgroup (A/B measurements; the engine's "
                         "test hook mck_test_set_crc_driver)")
     p.add_argument("--crc-order", choices=["blocked", "interleaved"], default="blocked",
@@ -874,7 +874,7 @@ def main():
 
     from speedb_amd import _lib, shard
     if args.crc_driver != "auto" or args.crc_order != "blocked":
-        drv = {"auto": 0, "wave": 1, "rows16": 2, "rows8": 3, "units": 4, "rows4": 5, "rows1": 6}[args.crc_driver]
+        drv = {"auto": 0, "wave": 1, "rows16": 2, "rows8": 3, "units": 4, "rows4": 5, "rows1": 6, "bh": 7}[args.crc_driver]
         _lib.check(_lib.lib.mck_test_set_crc_driver(drv, 1 if args.crc_order == "interleaved" else 0),
                    "mck_test_set_crc_driver")
     w = make_workload(args, dev, rank, world)

@@ -1,0 +1,573 @@
+// mck_crc_bh.hpp -- the body/head CRC32C driver for ragged batches of spans
+// of a few KiB and more (SST data blocks of 4096 + 0..255 B + the type byte,
+// the 4/16/64 KiB compaction mix, blob records).
+//
+// Why.  The wave driver (mck_crc.hpp crc_drive) walks a span in 4 KiB
+// rounds anchored at its 16-aligned end.  A 4300-B block is one full round
+// plus a head "mini round" of ~200 bytes, and the loop iteration that loads
+// that mini round keeps 1 KiB in flight for the wave instead of 4 KiB: the
+// rate of a wave is set by the bytes it has in flight per memory latency, so
+// a 4 KiB + jitter block costs almost two full rounds (0.54 of the HBM peak
+// against 0.74 for aligned 4 KiB).  A 64 KiB span is 16 dependent rounds on
+// one wave: the last ones of a launch run while the rest of the GPU drains.
+//
+// Decomposition.  Span [ptr, ptr + n), a1 = its end rounded up to 16,
+// cover = a1 - ptr: BODY = the F = cover / 4096 whole 4 KiB rounds ending at
+// a1, HEAD = the h = cover % 4096 bytes before them (the whole span when
+// F = 0).  CRC-32C is linear (util/crc32c.cc:1221-1266, Crc32cCombine): the
+// span's pure state at a1 is
+//     zshift(head state, 4096 F)  ^  XOR_j zshift(piece j state, 16384 j)
+// where the body is cut into PIECES of at most 4 rounds anchored at a1
+// (piece j = rounds 4j .. 4j + 3 counted from the end).  ~init is injected
+// at ptr (in the head; in the body's first round when h = 0) and the < 16
+// bytes past the end are masked and un-shifted at the end, as in crc_drive.
+//   * pieces run on the wave driver's round (row-transposed non-temporal
+//     loads, 4 KiB in flight per wave, the 4032-byte gap map between rounds,
+//     the per-lane final shift and the wave XOR at the piece end);
+//   * heads run EIGHT AT A TIME, one per 8-lane row, on the row driver's
+//     round (512-byte rounds of 64-byte lane chunks anchored at the head's
+//     end, lanes before the head load the zero piece): one iteration per 8
+//     heads of <= 512 bytes instead of one per head;
+//   * each part XORs its state, moved to a1 by zshift(4096 m) (nibble maps
+//     of 4096 * 2^b in LDS, one per set bit of m), into the span's LDS
+//     accumulator and decrements its part counter; the part that brings it
+//     to zero un-shifts the tail and runs the epilogue.  A span of ONE part
+//     (a head-only span; a span whose cover is a multiple of 4 KiB and at
+//     most 16 KiB) finishes at once.
+//
+// Scheduling.  A workgroup walks its share in WINDOWS of kBNC spans staged
+// in LDS (descriptors, accumulators, the exclusive prefix of the pieces, the
+// list of spans with a head).  Its waves take TICKETS from one LDS counter:
+// tickets [0, HB) are head batches (8 consecutive heads of the list), the
+// rest body pieces in address order (a wave finds a piece's span by a ballot
+// over the prefix, searching forward from its previous one).  Heads first:
+// a piece -- the span end above all, which holds the epilogue inputs -- is
+// then normally the last part of its span.  Every wave keeps one unit (a
+// 4 KiB body round or an 8-head round) loaded ahead of the one it folds.
+//
+// LDS image (160 KiB):
+//   [0, 32K)        per-lane final shift (kLdsFinal, as the wave driver)
+//   [32K, +512)     gap map 4032 (kLdsGap)
+//   then            8-lane row gap map (448 B), head / tail byte masks,
+//                   init injection tables, control words, zshift(4096 * 2^b)
+//                   maps, un-shift maps k < 16, the window's head list
+//   [64K, 128K)     the 4-byte step tables (kLdsStep, CrcLane)
+//   [128K, 160K)    the window's descriptors, accumulators, piece prefix
+#pragma once
+#include "mck_crc_units.hpp"
+
+namespace mck {
+
+constexpr uint32_t kBNC = 1024;                          // spans per window (<= kCrcBlock)
+constexpr uint32_t kBLdsRowGap = kLdsGap + 512;          // zshift(., 64 * 7): 8-lane rows
+constexpr uint32_t kBLdsMaskHead = kBLdsRowGap + 512;    // [16] x 16 B: keep bytes >= h
+constexpr uint32_t kBLdsMaskTail = kBLdsMaskHead + 256;  // [16] x 16 B: keep the first 16 - k
+constexpr uint32_t kBLdsInj = kBLdsMaskTail + 256;       // [16 types][16 k]: unshift(~init_t, k)
+constexpr uint32_t kBLdsInit = kBLdsInj + 1024;          // [16] init_t
+constexpr uint32_t kBLdsCtl = kBLdsInit + 64;            // ticket, nheads, npieces; wave sums
+constexpr uint32_t kBLdsWsum = kBLdsCtl + 16;            // u64 x 16 waves
+constexpr uint32_t kBPowBits = 21;                       // 4096 * 2^b, b <= 20 (spans < 4 GiB)
+constexpr uint32_t kBLdsPow = kBLdsCtl + 256;            // [21][8][16]
+constexpr uint32_t kBLdsUnshift = kBLdsPow + kBPowBits * 512;  // [16][8][16]
+constexpr uint32_t kBLdsHlist = kBLdsUnshift + 16 * 512;       // u32 x kBNC
+static_assert(kBLdsHlist + 4 * kBNC <= kLdsStep, "BH low image overlaps the step tables");
+constexpr uint32_t kBLdsDesc = kLdsStep + 65536;               // 16 B x kBNC {off lo, off hi, len, key}
+constexpr uint32_t kBLdsAcc = kBLdsDesc + 16 * kBNC;           // {xor, parts left} x kBNC
+constexpr uint32_t kBLdsBpre = kBLdsAcc + 8 * kBNC;            // u32 x (kBNC + 65)
+static_assert(kBLdsBpre + 4 * (kBNC + 65) <= kCrcLdsBytes, "BH image must fit the LDS");
+static_assert(kPowBits >= (int)kBPowBits + 2, "pow1k holds zshift(4096 * 2^b) as entry b + 2");
+static_assert(kBNC <= (uint32_t)kCrcBlock, "one staging slot per thread");
+
+__device__ __forceinline__ uint32_t bh_init_of(int kind, uint32_t key, uint32_t typed) {
+  return kind == kInitArray ? key : kind == kInitTyped ? typed : 0u;
+}
+
+// ---- LDS fill: tables from the device copy, then the computed ones -------------
+template <class Op>
+__device__ __forceinline__ void crc_bh_fill(const Op& op, const CrcTables* __restrict__ g) {
+  const uint32_t t = threadIdx.x;
+  constexpr int kLow = (int)(kLdsGap + 512) / 16;  // lane_final + gap: 2080 slots
+  uint32_t st[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t i = t + kCrcBlock * k;
+    st[k] = g->step[(i >> 2) & 3][i >> 4];
+  }
+  const uint4* lo = reinterpret_cast<const uint4*>(&g->lane_final[0][0][0]);
+  uint4 l[3];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int i = (int)t + kCrcBlock * k;
+    l[k] = lo[i < kLow ? i : 0];
+  }
+  // row gap (32 slots), pow maps (b + 2 of pow1k: 672 slots), un-shift k < 16 (512)
+  const uint4 rg = reinterpret_cast<const uint4*>(&g->gap_row[1][0][0])[t < 32 ? t : 0];
+  const uint4 pw = reinterpret_cast<const uint4*>(&g->pow1k[2][0][0])[t < kBPowBits * 32 ? t : 0];
+  const uint4 us = reinterpret_cast<const uint4*>(&g->unshift[0][0][0])[t < 512 ? t : 0];
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t x = st[k];
+    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(
+        static_cast<size_t>(kLdsStep + 16 * (t + kCrcBlock * k))) = span_u32x4{x, x, x, x};
+  }
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const int i = (int)t + kCrcBlock * k;
+    if (i < kLow)
+      *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(16 * i)) =
+          span_u32x4{l[k].x, l[k].y, l[k].z, l[k].w};
+  }
+  typedef __attribute__((address_space(3))) span_u32x4 lds_u32x4_t;
+  if (t < 32) *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsRowGap + 16 * t)) = span_u32x4{rg.x, rg.y, rg.z, rg.w};
+  if (t < kBPowBits * 32)
+    *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsPow + 16 * t)) = span_u32x4{pw.x, pw.y, pw.z, pw.w};
+  if (t < 512) *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsUnshift + 16 * t)) = span_u32x4{us.x, us.y, us.z, us.w};
+  if (t < 128) {  // byte masks of a 16-byte piece
+    const int h = (int)(t >> 2) & 15, k = (int)(t & 3);
+    if (t < 64) {  // keep bytes >= h
+      const int d = h - 4 * k;
+      *lds_p32(kBLdsMaskHead + 4 * (t & 63)) = d <= 0 ? 0xFFFFFFFFu : d >= 4 ? 0u : 0xFFFFFFFFu << (8 * d);
+    } else {  // keep the first 16 - h bytes
+      const int keep = 16 - h - 4 * k;
+      *lds_p32(kBLdsMaskTail + 4 * (t & 63)) = keep >= 4 ? 0xFFFFFFFFu : keep <= 0 ? 0u : 0xFFFFFFFFu >> (8 * (4 - keep));
+    }
+  }
+  __syncthreads();
+  // init injection: inj[ty][k] = unshift(~init_ty, k) (ty = 0 serves init 0)
+  if (t < 256) {
+    const uint32_t init = Op::kTypedInit ? op.typed_init(t >> 4) : 0u;
+    *lds_p32(kBLdsInj + 4 * t) = crc_nibmap(kBLdsUnshift + (t & 15) * 512, ~init);
+    if ((t & 15) == 0) *lds_p32(kBLdsInit + 4 * (t >> 4)) = init;
+  }
+}
+
+// ---- window staging -----------------------------------------------------------
+__device__ __forceinline__ uint4 bh_desc(uint32_t t) {
+  const span_u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const span_u32x4*>(
+      static_cast<size_t>(kBLdsDesc + 16 * t));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t bh_bpre(uint32_t t) { return *lds_p32(kBLdsBpre + 4 * t); }
+
+// Geometry of a span from its descriptor.
+struct BhGeo {
+  uint64_t ptr, a1;
+  uint32_t n, F, h, kt;
+};
+__device__ __forceinline__ BhGeo bh_geo(uint64_t base, const uint4& d) {
+  BhGeo x;
+  x.ptr = base + (((uint64_t)d.y << 32) | d.x);
+  x.n = d.z;
+  x.a1 = (x.ptr + x.n + 15) & ~15ull;
+  const uint64_t cover = x.a1 - x.ptr;
+  x.F = (uint32_t)(cover >> 12);
+  x.h = (uint32_t)cover & 4095u;
+  x.kt = (uint32_t)(x.a1 - (x.ptr + x.n));
+  return x;
+}
+
+// Stage window slots [0, wn) = spans sh.idx(t): descriptors, accumulators
+// {0, parts}, the head list and the pieces' exclusive prefix (padded for the
+// ballot search); empty spans finish here (Extend(init, "") = init).  Ends
+// with a barrier; the totals are at kBLdsCtl + 4 / + 8.
+template <class Op>
+__device__ __forceinline__ void crc_bh_stage(const Op& op, const UShare& sh, uint32_t wn, uint64_t base, int kind) {
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
+  uint32_t hh = 0, P = 0;
+  if (t < wn) {
+    const uint32_t i = sh.idx(t);
+    const uint64_t off = op.off(i);
+    const uint32_t len = (uint32_t)op.len(i);
+    const uint32_t key = op.init_key(i);
+    const uint4 d = make_uint4((uint32_t)off, (uint32_t)(off >> 32), len, key);
+    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kBLdsDesc + 16 * t)) =
+        span_u32x4{d.x, d.y, d.z, d.w};
+    const BhGeo x = bh_geo(base, d);
+    if (len == 0) {
+      const uint32_t init = bh_init_of(kind, key, *lds_p32(kBLdsInit + 4 * (key & 15u)));
+      op.finish(i, init, op.pre(i, x.ptr, 0), true);
+    } else {
+      hh = (x.F == 0 || x.h != 0) ? 1u : 0u;
+      P = (x.F + 3) >> 2;
+    }
+    *lds_p64(kBLdsAcc + 8 * t) = (uint64_t)(P + hh) << 32;
+  }
+  // exclusive scans of (heads, pieces), packed: heads < 2^16 per window
+  const uint64_t v = ((uint64_t)P << 16) | hh;
+  uint64_t x = v;
+#pragma unroll
+  for (int dd = 1; dd < 64; dd <<= 1) {
+    const uint64_t y = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(x >> 32), dd, 64) << 32) |
+                       (uint32_t)__shfl_up((int)(uint32_t)x, dd, 64);
+    x += lane >= (uint32_t)dd ? y : 0ull;
+  }
+  if (lane == 63) *lds_p64(kBLdsWsum + 8 * w) = x;
+  __syncthreads();
+  uint64_t below = 0, tot = 0;
+  for (uint32_t q = 0; q < nw; q++) {
+    const uint64_t ws = *lds_p64(kBLdsWsum + 8 * q);
+    below += q < w ? ws : 0ull;
+    tot += ws;
+  }
+  const uint64_t ex = below + x - v;
+  if (t < wn) {
+    *lds_p32(kBLdsBpre + 4 * t) = (uint32_t)(ex >> 16);
+    if (hh) *lds_p32(kBLdsHlist + 4 * (uint32_t)(ex & 0xFFFFu)) = t;
+  }
+  const uint32_t nheads = (uint32_t)(tot & 0xFFFFu), npieces = (uint32_t)(tot >> 16);
+  if (t <= 64) *lds_p32(kBLdsBpre + 4 * (wn + t)) = t ? 0xFFFFFFFFu : npieces;
+  if (t == 0) {
+    *lds_p32(kBLdsCtl) = 0;  // ticket
+    *lds_p32(kBLdsCtl + 4) = nheads;
+    *lds_p32(kBLdsCtl + 8) = npieces;
+  }
+  __syncthreads();
+}
+
+// ---- one unit of work ---------------------------------------------------------
+// kind 2: round r of a body piece (rounds rhi down to rlo, wave-uniform);
+// kind 1: round q of a head batch (row values; R = the batch's rounds);
+// kind 0: nothing left.
+struct BhUnit {
+  int32_t kind;
+  // body piece (wave-uniform)
+  uint32_t bt;          // window slot
+  int32_t r, rlo, rhi;  // current / last / first round of the piece (from the span end)
+  uint64_t ba1;
+  uint32_t bkt;
+  uint32_t binj;        // ~init at lane 0 of round rhi (h = 0, the span's first piece), else 0
+  uint32_t bparts;      // the span's parts (1: finish at once)
+  // head batch (per row; the rest of the head's geometry is derived, bh_hgeo)
+  uint32_t ht;          // window slot
+  bool hlive;
+  uint64_t hptr;        // the span's first byte
+  uint32_t hn;          // the SPAN's bytes
+  int32_t hrounds;      // 512-byte rounds of the head
+  uint32_t hinj;        // ~init, un-shifted by (hptr & 15): injected at the piece holding hptr
+  int32_t q, R;
+};
+
+// 0: no unit
+__device__ __forceinline__ BhUnit bh_none() {
+  BhUnit u;
+  u.kind = 0;
+  u.bt = 0;
+  u.r = u.rlo = u.rhi = 0;
+  u.ba1 = 0;
+  u.bkt = 0;
+  u.binj = 0;
+  u.bparts = 1;
+  u.ht = 0;
+  u.hlive = false;
+  u.hptr = 0;
+  u.hn = 0;
+  u.hrounds = 0;
+  u.hinj = 0;
+  u.q = 0;
+  u.R = 0;
+  return u;
+}
+
+// A head's geometry: [ptr, a1 - kt) with a1 16-aligned -- the whole span
+// (F = 0) or the h bytes before its body -- in 512-byte rounds anchored at
+// a1; `owner` = the row lane whose first-round chunk holds ptr, hb = ptr -
+// that chunk's start.
+struct BhHead {
+  uint64_t a0, a1;
+  uint32_t F, kt, cover;
+  int32_t owner;
+  uint32_t hb;
+};
+__device__ __forceinline__ BhHead bh_hgeo(uint64_t ptr, uint32_t n, int32_t rounds) {
+  BhHead x;
+  x.a0 = ptr & ~15ull;
+  const uint64_t a1 = (ptr + n + 15) & ~15ull;
+  x.F = (uint32_t)((a1 - ptr) >> 12);
+  x.a1 = a1 - ((uint64_t)x.F << 12);
+  x.kt = x.F ? 0u : (uint32_t)(a1 - (ptr + n));
+  x.cover = (uint32_t)(x.a1 - ptr);
+  const uint32_t lead = 512u * (uint32_t)rounds - x.cover;
+  x.owner = (int32_t)(lead >> 6);
+  x.hb = lead & 63u;
+  return x;
+}
+
+template <class Op>
+__device__ __forceinline__ BhUnit bh_take(const Op& op, uint64_t base, int kind, uint32_t nheads, uint32_t npieces,
+                                          uint32_t& tc, uint32_t lane) {
+  BhUnit u = bh_none();
+  const uint32_t k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
+  const uint32_t hb = (nheads + 7) >> 3;
+  if (k < hb) {  // head batch: row `lane / 8` takes head 8 k + row of the list
+    u.kind = 1;
+    const uint32_t e = 8 * k + (lane >> 3);
+    u.hlive = e < nheads;
+    u.ht = *lds_p32(kBLdsHlist + 4 * (u.hlive ? e : 8 * k));
+    const uint4 d = bh_desc(u.ht);
+    const BhGeo x = bh_geo(base, d);
+    u.hptr = x.ptr;
+    u.hn = x.n;
+    // the head: the whole span (F = 0) or the h bytes before the body
+    const uint32_t cover = x.F ? x.h : (uint32_t)(x.a1 - x.ptr);  // > 0
+    u.hrounds = (int32_t)((cover + 511) >> 9);
+    const uint32_t hk = (uint32_t)x.ptr & 15u;  // = the owner's hb % 16 (chunks are 16-aligned)
+    u.hinj = kind == kInitArray ? crc_nibmap(kBLdsUnshift + hk * 512, ~d.w)
+                                : *lds_p32(kBLdsInj + 4 * ((kind == kInitTyped ? (d.w & 15u) * 16 : 0u) + hk));
+    uint32_t m = u.hlive ? (uint32_t)u.hrounds : 0u, R = 0;
+#pragma unroll
+    for (uint32_t rw = 0; rw < 8; rw++) R = max(R, readlane_u32(m, 8 * rw));
+    u.R = (int32_t)R;
+    u.q = 0;
+  } else if (k - hb < npieces) {  // body piece k - hb
+    u.kind = 2;
+    const uint32_t q = k - hb;
+    uint32_t v = bh_bpre(tc + 1 + lane);
+    uint32_t c0 = (uint32_t)__popcll(__ballot(v <= q));
+    while (c0 == 64) {
+      tc += 64;
+      v = bh_bpre(tc + 1 + lane);
+      c0 = (uint32_t)__popcll(__ballot(v <= q));
+    }
+    tc += c0;
+    u.bt = tc;
+    const uint4 d = bh_desc(tc);
+    const uint4 ds = make_uint4(rfl(d.x), rfl(d.y), rfl(d.z), rfl(d.w));
+    const BhGeo x = bh_geo(base, ds);
+    const uint32_t P = (x.F + 3) >> 2;
+    const uint32_t j = P - 1 - (q - rfl(bh_bpre(tc)));  // pieces in address order
+    u.rlo = (int32_t)(4 * j);
+    u.rhi = (int32_t)min(4 * j + 3, x.F - 1);
+    u.r = u.rhi;
+    u.ba1 = x.a1;
+    u.bkt = x.kt;
+    const bool first = j == P - 1 && x.h == 0;  // the span starts at this piece's first round
+    u.binj = first ? ~bh_init_of(kind, ds.w, *lds_p32(kBLdsInit + 4 * (ds.w & 15u))) : 0u;
+    u.bparts = P + (x.h != 0 ? 1u : 0u);
+  }
+  return u;
+}
+
+// The unit's loads (always 4 x 16 B per lane, so the waits stay exact).
+// Body: the row-transposed layout of the round (crc_load_chunk_rt), non-
+// temporal; head: lane c of a row the 64-byte chunk c of its round (the
+// pieces wholly before the head and idle rows read the zero piece).
+__device__ __forceinline__ Chunk bh_load(const BhUnit& u, uint32_t lane, uint64_t zp) {
+  Chunk ch;
+  if (u.kind == 2) {
+    const uint64_t b = u.ba1 - (uint64_t)kRoundBytes * (uint32_t)(u.r + 1) + 64ull * (lane & 15) + 16ull * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < 4; j++) ch.v[j] = span_load16<true>(b + 1024ull * j);
+  } else {
+    const uint32_t c = lane & 7;
+    const BhHead x = bh_hgeo(u.hptr, u.hn, u.hrounds);
+    const int32_t rr = u.hrounds - 1 - u.q;
+    const bool act = u.hlive && rr >= 0;
+    const uint64_t b = x.a1 - 512ull * (uint32_t)(rr + 1) + 64ull * c;
+    const int32_t rel = rr == u.hrounds - 1 ? (int32_t)((uint32_t)b - (uint32_t)x.a0) : 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) ch.v[j] = span_load16<false>((!act || rel < -16 * j) ? zp : b + 16ull * j);
+  }
+  return ch;
+}
+
+// Epilogue inputs of the unit's span(s): every part of a span loads the
+// span's own (Op::pre depends on the span only), so whichever part finishes
+// it has them.  Vector loads: the body's arguments are wave-uniform.
+template <class Op>
+__device__ __forceinline__ typename Op::Pre bh_pre(const Op& op, bool body, uint32_t bt, uint32_t ht, uint64_t hptr,
+                                                   uint32_t hn, const UShare& sh, uint64_t base) {
+  const uint32_t t = body ? bt : ht;
+  const uint4 d = bh_desc(bt);
+  uint64_t ptr = body ? base + (((uint64_t)d.y << 32) | d.x) : hptr;
+  const uint32_t n = body ? d.z : hn;
+  uint32_t i = sh.idx(t);
+  asm volatile("" : "+v"(i), "+v"(ptr));
+  return op.pre(i, ptr, n);
+}
+
+__device__ __forceinline__ uint32_t bh_unshift(uint32_t k, uint32_t s) { return crc_nibmap(kBLdsUnshift + k * 512, s); }
+
+// zshift(p, 4096 m), one nibble map per set bit of m (m wave-uniform).
+__device__ __forceinline__ uint32_t bh_pow_u(uint32_t p, uint32_t m) {
+  for (; m; m &= m - 1) p = crc_nibmap(kBLdsPow + (uint32_t)__builtin_ctz(m) * 512, p);
+  return p;
+}
+// The same with m per lane.
+__device__ __forceinline__ uint32_t bh_pow_v(uint32_t p, uint32_t m) {
+  while (wave_any(m != 0)) {
+    const uint32_t b = (uint32_t)__builtin_ctz(m | 0x80000000u) & 31u;
+    const uint32_t x = crc_nibmap(kBLdsPow + (b < kBPowBits ? b : 0u) * 512, p);
+    p = m ? x : p;
+    m &= m - 1;
+  }
+  return p;
+}
+
+// A body piece ends: p = its pure state at the piece end (wave-uniform).
+template <class Op>
+__device__ __forceinline__ void bh_body_end(const Op& op, const BhUnit& u, uint32_t p, const typename Op::Pre& pre,
+                                            const UShare& sh, uint64_t base, uint32_t lane) {
+  p = bh_pow_u(p, (uint32_t)u.rlo);  // the piece end is 4096 rlo bytes before a1
+  if (u.bparts != 1) {
+    uint32_t left = 0;
+    if (lane == 0) {
+      __hip_atomic_fetch_xor(lds_p32(kBLdsAcc + 8 * u.bt), p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      left = __hip_atomic_fetch_add(lds_p32(kBLdsAcc + 8 * u.bt + 4), 0xFFFFFFFFu, __ATOMIC_ACQ_REL,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (left == 1) p = __hip_atomic_load(lds_p32(kBLdsAcc + 8 * u.bt), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (rfl(left) != 1) return;
+    p = rfl(p);
+  }
+  if (u.bkt) p = bh_unshift(u.bkt, p);
+  op.finish(sh.idx(u.bt), ~p, pre, lane == 0);
+}
+
+// Head rows end (fin: the row's head ends in this round): p = the pure state
+// at the head end, in every lane of the row.
+template <class Op>
+__device__ __forceinline__ void bh_head_end(const Op& op, const BhUnit& u, uint32_t p, bool fin,
+                                            const typename Op::Pre& pre, const UShare& sh, uint32_t lane) {
+  const bool lead = (lane & 7) == 0;
+  const uint32_t F = (uint32_t)((((u.hptr + u.hn + 15) & ~15ull) - u.hptr) >> 12);
+  const bool direct = F == 0;  // the head is the whole span
+  bool done = fin && direct;
+  if (wave_any(fin && !direct)) {
+    const bool part = fin && !direct;
+    const uint32_t q = bh_pow_v(p, part ? F : 0u);  // the head end is 4096 F bytes before a1
+    p = part ? q : p;
+    uint32_t left = 0;
+    if (part && lead) {
+      __hip_atomic_fetch_xor(lds_p32(kBLdsAcc + 8 * u.ht), p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      left = __hip_atomic_fetch_add(lds_p32(kBLdsAcc + 8 * u.ht + 4), 0xFFFFFFFFu, __ATOMIC_ACQ_REL,
+                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (left == 1) p = __hip_atomic_load(lds_p32(kBLdsAcc + 8 * u.ht), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    // the row leader's values to its row
+    const int src = (int)((lane & ~7u) << 2);
+    left = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)left);
+    const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)p);
+    p = part ? pl : p;
+    done = done || (part && left == 1);
+  }
+  if (!wave_any(done)) return;
+  const uint32_t kt = (uint32_t)(0u - (uint32_t)(u.hptr + u.hn)) & 15u;
+  const uint32_t x = bh_unshift(kt, p);
+  p = kt ? x : p;
+  op.finish(sh.idx(u.ht), ~p, pre, done && lead);
+}
+
+// One 512-byte round of the head batch (row values; q wave-uniform).
+__device__ __forceinline__ uint32_t bh_head_round(uint32_t s, Chunk ch, const BhUnit& u, uint32_t c, const CrcLane& L) {
+  const BhHead hg = bh_hgeo(u.hptr, u.hn, u.hrounds);
+  const int32_t rr = u.hrounds - 1 - u.q;
+  const bool first = u.q == 0;  // every live row starts its head in the batch's first round
+  const bool own = (int32_t)c == hg.owner;
+  const uint32_t h0 = (uint32_t)u.hptr & 15u;
+  const uint4 mh = lds_u32x4(kBLdsMaskHead + 16 * h0);
+  const uint4 mt = lds_u32x4(kBLdsMaskTail + 16 * ((rr == 0 && c == 7) ? hg.kt : 0u));
+  const uint32_t pa = (first && own) ? hg.hb >> 4 : 4u;
+  uint32_t sels[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint32_t sel = (uint32_t)j == pa ? ~0u : 0u;
+    sels[j] = sel;
+    ch.v[j].x = __builtin_amdgcn_bitop3_b32(ch.v[j].x, mh.x, sel, 0xD0);
+    ch.v[j].y = __builtin_amdgcn_bitop3_b32(ch.v[j].y, mh.y, sel, 0xD0);
+    ch.v[j].z = __builtin_amdgcn_bitop3_b32(ch.v[j].z, mh.z, sel, 0xD0);
+    ch.v[j].w = __builtin_amdgcn_bitop3_b32(ch.v[j].w, mh.w, sel, 0xD0);
+  }
+  and4(ch.v[3], mt);
+  const uint32_t gap = first ? 0u : crc_nibmap(kBLdsRowGap, s);
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&ch.v[0]);
+  const uint32_t inj = u.hinj;
+  uint32_t x = gap ^ w[0] ^ (sels[0] & inj);
+#pragma unroll
+  for (int k = 0; k < 16; k++) {
+    uint32_t nw = 0u;
+    if (k + 1 < 16) nw = ((k + 1) & 3) ? w[k + 1] : (w[k + 1] ^ (sels[(k + 1) >> 2] & inj));
+    x = crc_step4x(x, L, nw);
+  }
+  return x;
+}
+
+// One 4 KiB round of a body piece (chunk already row-transposed).
+__device__ __forceinline__ uint32_t bh_body_round(uint32_t s, Chunk ch, const BhUnit& u, uint32_t lane,
+                                                  const CrcLane& L) {
+  const bool first = u.r == u.rhi;
+  uint32_t x = first ? (lane == 0 ? u.binj : 0u) : crc_nibmap(kLdsGap, s);
+  if (u.r == 0 && u.bkt && lane == 63) crc_keep_head_bytes(ch.v[3], 16 - u.bkt);  // bytes past the end
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&ch.v[0]);
+  x ^= w[0];
+#pragma unroll
+  for (int k = 0; k < 16; k++) x = crc_step4x(x, L, k < 15 ? w[k + 1] : 0u);
+  return x;
+}
+
+template <class Op, bool T>
+__device__ __forceinline__ void crc_bh_window(const Op& op, const UShare& sh, uint64_t base, const CrcTables* __restrict__ g) {
+  const int kind = op.init_kind();
+  const CrcLane L = crc_lane();
+  const uint32_t lane = threadIdx.x & 63, c = lane & 7;
+  const uint32_t lf4 = (56u + c) << 2;  // 8-lane rows: lane-final column 64 - 8 + c
+  const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
+  const uint32_t nheads = *lds_p32(kBLdsCtl + 4), npieces = *lds_p32(kBLdsCtl + 8);
+  typedef typename Op::Pre Pre;
+  uint32_t tc = 0;
+  BhUnit u = bh_take(op, base, kind, nheads, npieces, tc, lane);
+  if (u.kind == 0) return;
+  Chunk cur = bh_load(u, lane, zp);
+  Pre pcur = bh_pre(op, u.kind == 2, u.bt, u.ht, u.hptr, u.hn, sh, base);
+  uint32_t s = 0;
+  for (;;) {
+    BhUnit nu;
+    if (u.kind == 2 && u.r > u.rlo) {
+      nu = u;
+      nu.r = u.r - 1;
+    } else if (u.kind == 1 && u.q + 1 < u.R) {
+      nu = u;
+      nu.q = u.q + 1;
+    } else {
+      nu = bh_take(op, base, kind, nheads, npieces, tc, lane);
+    }
+    // unconditional: the next unit's loads (the zero piece when none is left)
+    const Chunk nxt = bh_load(nu, lane, zp);
+    const bool nb = nu.kind ? nu.kind == 2 : u.kind == 2;
+    const Pre pnxt = bh_pre(op, nb, nu.kind ? nu.bt : u.bt, nu.kind ? nu.ht : u.ht, nu.kind ? nu.hptr : u.hptr,
+                            nu.kind ? nu.hn : u.hn, sh, base);
+    if (u.kind == 2) {
+      if (T) row_transpose(cur);
+      s = bh_body_round(s, cur, u, lane, L);
+      if (u.r == u.rlo) bh_body_end(op, u, wave_xor32(crc_lane_final(s, L)), pcur, sh, base, lane);
+    } else {
+      s = bh_head_round(s, cur, u, c, L);
+      const bool fin = u.hlive && u.hrounds - 1 - u.q == 0;
+      if (wave_any(fin)) bh_head_end(op, u, row_xor32<8>(crc_lane_final4(s, lf4)), fin, pcur, sh, lane);
+    }
+    if (nu.kind == 0) break;
+    u = nu;
+    cur = nxt;
+    pcur = pnxt;
+  }
+}
+
+// A workgroup's share [start, start + n) (contiguous), in windows of at most
+// kBNC spans, as even as the share allows.
+template <class Op, bool T>
+__device__ __forceinline__ void crc_bh_driver(const Op& op, const RowShare& share, const CrcTables* __restrict__ g) {
+  crc_bh_fill(op, g);
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  const int kind = op.init_kind();
+  const uint32_t n = share.n;
+  const uint32_t nwin = (n + kBNC - 1) / kBNC;
+  __syncthreads();  // the init tables (read by the staging of empty spans)
+  for (uint32_t wi = 0; wi < nwin; wi++) {
+    const uint32_t w0 = (uint32_t)((uint64_t)n * wi / nwin), w1 = (uint32_t)((uint64_t)n * (wi + 1) / nwin);
+    const UShare sh{share.start + share.stride * w0, share.stride};
+    if (wi) __syncthreads();  // the previous window's waves are done with its slots
+    crc_bh_stage(op, sh, w1 - w0, base, kind);
+    crc_bh_window<Op, T>(op, sh, base, g);
+  }
+}
+
+}  // namespace mck

@@ -586,7 +586,7 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
       __syncthreads();
     }
     lpt = mode == 1 && longs;
-  } else if (force != 4) {
+  } else if (force != 4 && force != 7) {
     crc_rows_prologue<Op>(op, sh, lds, g, true, force == 1);
   }
   if (mode == 4)

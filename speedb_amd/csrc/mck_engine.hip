@@ -203,11 +203,22 @@ int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int n
 }
 
 template <class Op>
+int launch_crc_bh(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
+  constexpr bool T = kCrcGenericT;
+  if (int rc = ensure_lds(k_crc_bh<Op, T>, dev)) return rc;
+  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + 3) / 4);
+  hipLaunchKernelGGL((k_crc_bh<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+template <class Op>
 int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
   if (!count) return MCK_OK;
   int dev, ncu;
   int rc = current_device(&dev, &ncu);
   if (rc) return rc;
+  if (crc_auto_force() == 7) return launch_crc_bh(op, count, st, dev, ncu);
   return launch_crc_auto(op, count, st, dev, ncu);
 }
 
@@ -1353,8 +1364,8 @@ int mck_statistics_get(mck_statistics* out, int reset) {
 
 int mck_test_set_crc_driver(int driver, int interleaved) {
   t_err[0] = 0;
-  if (driver < 0 || driver > 6) {
-    set_err("driver must be 0..6");
+  if (driver < 0 || driver > 7) {
+    set_err("driver must be 0..7");
     return MCK_EINVAL;
   }
   g_crc_force.store(driver, std::memory_order_relaxed);

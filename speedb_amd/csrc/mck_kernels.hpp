@@ -8,6 +8,7 @@
 
 #include "mck_crc.hpp"
 #include "mck_crc_units.hpp"
+#include "mck_crc_bh.hpp"
 #include "mck_xxh.hpp"
 
 namespace mck {
@@ -217,6 +218,14 @@ template <class Op, bool T, bool BLK = false>
 __global__ __launch_bounds__(1024) void k_crc_auto(Op op, uint32_t first, uint32_t count, int force) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   crc_auto_units_driver<Op, T, BLK>(op, first, count, lds, &g_crc_tables, force);
+}
+
+// ragged batches on the body/head driver alone (mck_crc_bh.hpp)
+template <class Op, bool T>
+__global__ __launch_bounds__(1024) void k_crc_bh(Op op, uint32_t first, uint32_t count) {
+  const RowShare sh = row_share<true>(first, count);
+  if (sh.n == 0) return;
+  crc_bh_driver<Op, T>(op, sh, &g_crc_tables);
 }
 
 // uniform batches (see CrcUniform)

@@ -27,7 +27,7 @@ constexpr int row_gap_bytes(int k) { return (4 << k) * kChunkBytes - kChunkBytes
 // Unit-stream driver: a span shared by several waves' streams has each
 // portion's state moved to the span end by zshift(1024 m), m < 2^22 units
 // (spans < 4 GiB).
-constexpr int kPowBits = 22;
+constexpr int kPowBits = 23;
 
 struct alignas(16) CrcTables {
   uint32_t step[4][256];          // zshift(v << 8t, 4): the 4-byte step

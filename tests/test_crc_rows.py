@@ -70,7 +70,7 @@ def _forced(env):
     assert " passed" in r.stdout
 
 
-@pytest.mark.parametrize("mode", ["wave", "rows16", "rows8", "rows4", "rows1", "units", "interleaved"])
+@pytest.mark.parametrize("mode", ["wave", "rows16", "rows8", "rows4", "rows1", "units", "bh", "interleaved"])
 def test_auto_kernel_forced_drivers_subprocess(gpu, mode):
     """k_crc_auto with each driver forced for every workgroup (its choice is
     by mean length, so a parity test of mixed lengths may exercise only one):
