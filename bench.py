@@ -93,7 +93,12 @@ HBM_PEAK = 8.0e12  # B/s, MI355X_MICROARCH.md
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one process per GPU).  Without WORLD_SIZE in the environment and N > 1, "
+                        "bench.py starts N fresh ranks itself (torch.distributed.run, a child process); "
+                        "under torchrun it must equal WORLD_SIZE")
+    p.add_argument("--host-ndev", type=int, default=0,
+                   help="host: devices ONE process drives through mck_host_batch_checksum (0 = the rank's own)")
     p.add_argument("--steps", type=int, default=None, help="timed steps (default 50; host 3)")
     p.add_argument("--warmup", type=int, default=None, help="untimed warmup steps (default 100; host 1)")
     # the first ~25 back-to-back launches (~20 ms) of a streaming kernel run
@@ -653,6 +658,11 @@ def make_workload(args, dev, rank, world):
         # FlushBlockBySizePolicy), 8-GPU share per GPU, in pinned host memory
         block = 4300
         count = args.host_blocks
+        ndev = args.host_ndev
+        if ndev > 0 and (world > 1 or ndev > torch.cuda.device_count()):
+            raise SystemExit(f"bench: --host-ndev {ndev} needs one process and {ndev} visible GPU(s) "
+                             f"(world {world}, {torch.cuda.device_count()} visible)")
+        count *= max(1, ndev)  # configs[4]'s per-GPU share for each device
         hbuf = torch.empty(count * block + 64, dtype=torch.uint8, pin_memory=True)
         tile = torch.randint(0, 256, (256 << 20,), dtype=torch.uint8, generator=torch.Generator().manual_seed(5))
         for o in range(0, hbuf.numel(), tile.numel()):  # 256 MiB of random bytes, tiled
@@ -663,16 +673,20 @@ def make_workload(args, dev, rank, world):
 
         def step():
             _lib.check(_lib.lib.mck_host_batch_checksum(
-                1, hbuf.data_ptr(), None, None, block, block, count, 0, 0, 256 << 20,
+                1, hbuf.data_ptr(), None, None, block, block, count, 0, ndev, 256 << 20,
                 out.ctypes.data, None, ctypes.byref(secs)), "mck_host_batch_checksum")
         w.step = step
         w.kernel = _auto("mck::OpCrcValue") + " (H2D/D2H overlapped)"
         w.span_bytes = count * block
         w.alg_bytes = count * (block + 4 + 8 + 4)
-        w.desc = (f"host-resident pinned {count} x {block} B blocks per GPU (the 8-GPU share of the "
+        per = count // max(1, ndev)
+        w.desc = (f"host-resident pinned {per} x {block} B blocks per GPU (the 8-GPU share of the "
                   "80M-key/1KB-value README stream, SST-sized blocks) -> H2D + CRC32C + D2H, 256 MiB "
-                  "double-buffered chunks, copy-inclusive (BASELINE.json configs[4])")
-        w.cfg = {"blocks_per_gpu": count, "block_bytes": block, "pcie_inclusive": True}
+                  "double-buffered chunks, copy-inclusive (BASELINE.json configs[4])"
+                  + (f"; one process driving {ndev} GPUs" if ndev > 0 else ""))
+        w.cfg = {"blocks_per_gpu": per, "block_bytes": block, "pcie_inclusive": True}
+        if ndev > 0:
+            w.cfg["host_ndev"] = ndev
 
         def device_only():
             # the same blocks already in HBM (a 4 GiB slice): kernel-only rate
@@ -855,6 +869,34 @@ def batch_latency(args):
                               "host thread"}))
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(argv, nprocs: int, script: str = None, env=None) -> int:
+    """Start `nprocs` fresh ranks of `script` (default: this file) with
+    torch.distributed.run on this node and return its exit code.  A child
+    process, never an exec: the caller has not touched the GPU (counting
+    devices does not), and on this pool exec'ing a process that has is
+    fatal."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nprocs}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", script or os.path.abspath(__file__)]
+    return subprocess.call(cmd + list(argv), env=env)
+
+
+def check_world(requested, world_env) -> int:
+    """The ranks this process belongs to: WORLD_SIZE when launched by
+    torchrun (which --gpus, if given, must equal), else 1."""
+    world = int(world_env) if world_env else 1
+    if requested is not None and requested != world:
+        raise SystemExit(f"bench: --gpus {requested} but WORLD_SIZE={world}")
+    return world
+
+
 def main():
     args = parse()
     if args.workload == "shim":
@@ -864,13 +906,25 @@ def main():
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and (args.gpus or 1) > 1:
+        # --gpus N from a plain `python bench.py`: N ranks, one per GPU, started
+        # here (device_count does not initialise the GPU on this image)
+        have = torch.cuda.device_count()
+        if args.gpus > have:
+            print(f"bench: --gpus {args.gpus} but only {have} GPU(s) visible", file=sys.stderr)
+            return 2
+        return launch_ranks(sys.argv[1:], args.gpus)
+    world = check_world(args.gpus, os.environ.get("WORLD_SIZE"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if local >= torch.cuda.device_count():
+        print(f"bench: rank {rank} has local rank {local} but {torch.cuda.device_count()} GPU(s)", file=sys.stderr)
+        return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_world_size() == world, (dist.get_world_size(), world)
 
     from speedb_amd import _lib, shard
     if args.crc_driver != "auto" or args.crc_order != "blocked":
@@ -936,7 +990,8 @@ def main():
                 print("bench: GPU checksums disagree with the reference", file=sys.stderr)
     if rank == 0:
         line = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 2), "unit": "GiB/s",
+            "n_gpus": dist.get_world_size() if world > 1 else world * max(1, args.host_ndev),
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(wall / args.steps * 1e3, 4), "higher_is_better": True,
             "scaling": getattr(w, "scaling", "weak"), "vs_baseline": None, "dtype": "u8",
@@ -954,4 +1009,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

@@ -715,7 +715,8 @@ int mck_partition_spans(const uint32_t* host_lengths, uint32_t count,
 /* Host-resident batch: spans live in host memory (pinned or pageable; pinned
  * gives full PCIe rate), sorted by offset.  The batch is partitioned by bytes
  * across devices [0, ndev) -- or, with ndev <= 0, runs on the calling
- * thread's current device only (one process per GPU) -- and streamed
+ * thread's current device only (one process per GPU); ndev above the
+ * devices the process sees is MCK_ENODEV, not a clamp -- and streamed
  * through each device in double-buffered chunks of
  * `chunk_bytes` (H2D copy of chunk k+1 overlaps the kernel on chunk k); the
  * per-span results come back to host memory.

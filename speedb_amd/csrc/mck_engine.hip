@@ -1287,7 +1287,14 @@ int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* hos
   if (ndev <= 0) {
     devs.push_back(prev);
   } else {
-    for (int d = 0; d < std::min(ndev, std::min(have, kMaxDev)); d++) devs.push_back(d);
+    // asking for more devices than the process sees is an error, never a
+    // silent clamp (a caller that believes it spreads over 8 GPUs must not
+    // time 1)
+    if (ndev > have || ndev > kMaxDev) {
+      set_err("ndev = %d devices asked for, %d present", ndev, have);
+      return MCK_ENODEV;
+    }
+    for (int d = 0; d < ndev; d++) devs.push_back(d);
   }
   ndev = (int)devs.size();
   if (!chunk_bytes) chunk_bytes = 256u << 20;
