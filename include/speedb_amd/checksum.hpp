@@ -20,6 +20,7 @@
 #include <stdint.h>
 
 #include <memory>
+#include <stdexcept>
 #include <string>
 #include <vector>
 
@@ -79,10 +80,46 @@ inline Status FromRc(int rc, const char* what) {
   return rc == MCK_EINVAL ? Status::InvalidArgument(m) : Status::IOError(m);
 }
 
+// The reference's checksum functions return a bare value and cannot fail.
+// Here the data-reading ones run on the GPU and CAN (no device, a HIP
+// error): a re-pointed call site must never receive a made-up checksum (a
+// trailer writer would store it, a verifier would compare against it), so
+// the mirror's reference-named functions go through the error-reporting
+// *_r entry points and throw DeviceError on failure -- never the plain
+// mck_* shims, which return 0.  Callers that cannot take an exception use
+// the *_r functions of mck.h directly.
+class DeviceError : public std::runtime_error {
+ public:
+  DeviceError(const char* what, int rc)
+      : std::runtime_error(std::string(what) + " failed (rc=" + std::to_string(rc) + "): " + mck_last_error()),
+        rc_(rc) {}
+  int rc() const { return rc_; }
+
+ private:
+  int rc_;
+};
+
+inline uint32_t CheckedU32(int rc, uint32_t v, const char* what) {
+  if (rc != MCK_OK) throw DeviceError(what, rc);
+  return v;
+}
+inline uint64_t CheckedU64(int rc, uint64_t v, const char* what) {
+  if (rc != MCK_OK) throw DeviceError(what, rc);
+  return v;
+}
+
 namespace crc32c {
 static const uint32_t kMaskDelta = 0xa282ead8ul;
-inline uint32_t Extend(uint32_t init_crc, const char* data, size_t n) { return mck_crc32c_extend(init_crc, data, n); }
-inline uint32_t Value(const char* data, size_t n) { return mck_crc32c_value(data, n); }
+inline uint32_t Extend(uint32_t init_crc, const char* data, size_t n) {
+  uint32_t v = 0;
+  const int rc = mck_crc32c_extend_r(init_crc, data, n, &v);
+  return CheckedU32(rc, v, "crc32c::Extend");
+}
+inline uint32_t Value(const char* data, size_t n) {
+  uint32_t v = 0;
+  const int rc = mck_crc32c_value_r(data, n, &v);
+  return CheckedU32(rc, v, "crc32c::Value");
+}
 inline uint32_t Mask(uint32_t crc) { return mck_crc32c_mask(crc); }
 inline uint32_t Unmask(uint32_t masked_crc) { return mck_crc32c_unmask(masked_crc); }
 inline uint32_t Crc32cCombine(uint32_t crc1, uint32_t crc2, size_t crc2len) {
@@ -90,14 +127,22 @@ inline uint32_t Crc32cCombine(uint32_t crc1, uint32_t crc2, size_t crc2len) {
 }
 }  // namespace crc32c
 
-inline uint64_t XXH3_64bits(const void* data, size_t n) { return mck_xxh3_64(data, n); }
+inline uint64_t XXH3_64bits(const void* data, size_t n) {
+  uint64_t v = 0;
+  const int rc = mck_xxh3_64_r(data, n, &v);
+  return CheckedU64(rc, v, "XXH3_64bits");
+}
 
 inline uint32_t ComputeBuiltinChecksum(ChecksumType type, const char* data, size_t data_size) {
-  return mck_builtin_checksum(type, data, data_size);
+  uint32_t v = 0;
+  const int rc = mck_builtin_checksum_r(type, data, data_size, &v);
+  return CheckedU32(rc, v, "ComputeBuiltinChecksum");
 }
 inline uint32_t ComputeBuiltinChecksumWithLastByte(ChecksumType type, const char* data, size_t data_size,
                                                    char last_byte) {
-  return mck_builtin_checksum_with_last_byte(type, data, data_size, last_byte);
+  uint32_t v = 0;
+  const int rc = mck_builtin_checksum_with_last_byte_r(type, data, data_size, last_byte, &v);
+  return CheckedU32(rc, v, "ComputeBuiltinChecksumWithLastByte");
 }
 inline uint32_t ChecksumModifierForContext(uint32_t base_context_checksum, uint64_t offset) {
   return mck_context_modifier(base_context_checksum, offset);
@@ -204,9 +249,14 @@ inline uint32_t PhysicalRecordCrc(RecordType t, const char* payload, size_t n, u
 }
 }  // namespace log
 
-// util/hash.h:45 NPHash64 / util/hash.cc:81 Hash64 -- XXPH3 on the GPU.
-inline uint64_t NPHash64(const char* data, size_t n, uint64_t seed = 0) { return mck_np_hash64(data, n, seed); }
-inline uint64_t Hash64(const char* data, size_t n, uint64_t seed = 0) { return mck_np_hash64(data, n, seed); }
+// util/hash.h:45 NPHash64 / util/hash.cc:81 Hash64 -- XXPH3 on the GPU
+// (DeviceError on failure, as above).
+inline uint64_t NPHash64(const char* data, size_t n, uint64_t seed = 0) {
+  uint64_t v = 0;
+  const int rc = mck_np_hash64_r(data, n, seed, &v);
+  return CheckedU64(rc, v, "NPHash64");
+}
+inline uint64_t Hash64(const char* data, size_t n, uint64_t seed = 0) { return NPHash64(data, n, seed); }
 
 // db/kv_checksum.h ProtectionInfo64, flattened: one value type whose Protect*
 // / Strip* / Update* steps XOR in the NPHash64 of a field with that field's
@@ -283,25 +333,41 @@ class FileChecksumGenerator {
 // checksum_ = crc32c::Extend over every Update, from 0; Finalize stores it as
 // 4 big-endian bytes.  Update() takes host bytes (inputs over 1 MiB go
 // through the engine's long-span path); UpdateDevice() takes bytes already
-// in device memory (mck_crc32c_long, no host copy).
+// in device memory (mck_crc32c_long, no host copy).  Exceptions never escape
+// (include/rocksdb/file_checksum.h:47-49) and a generator has no error
+// channel: after a device error the generator is failed() and Finalize
+// gives kUnknownFileChecksum (the file's checksum is then unknown, never
+// wrong).
 class FileChecksumGenCrc32c : public FileChecksumGenerator {
  public:
   explicit FileChecksumGenCrc32c(const FileChecksumGenContext& /*context*/) {}
   ~FileChecksumGenCrc32c() override;
-  void Update(const char* data, size_t n) override { checksum_ = crc32c::Extend(checksum_, data, n); }
-  // Returns false (checksum unchanged, mck_last_error() set) on a HIP error;
-  // exceptions never escape (include/rocksdb/file_checksum.h:47-49).
+  void Update(const char* data, size_t n) override {
+    uint32_t v = 0;
+    if (failed_ || mck_crc32c_extend_r(checksum_, data, n, &v) != MCK_OK) {
+      failed_ = true;
+      return;
+    }
+    checksum_ = v;
+  }
+  // Returns false (the generator failed, mck_last_error() set) on a HIP error.
   bool UpdateDevice(const void* dev_data, uint64_t n, mck_stream_t stream = nullptr);
   void Finalize() override {
+    if (failed_) {
+      checksum_str_ = kUnknownFileChecksum;
+      return;
+    }
     char b[4];
     for (int i = 0; i < 4; i++) b[i] = static_cast<char>(checksum_ >> (24 - 8 * i));
     checksum_str_.assign(b, 4);
   }
+  bool failed() const { return failed_; }
   std::string GetChecksum() const override { return checksum_str_; }
   const char* Name() const override { return "FileChecksumCrc32c"; }
 
  private:
   uint32_t checksum_ = 0;
+  bool failed_ = false;
   std::string checksum_str_;
   uint32_t* d_scratch_ = nullptr;  // device: long-span piece CRCs + result
   uint64_t scratch_words_ = 0;
@@ -415,6 +481,8 @@ inline FileChecksumGenCrc32c::~FileChecksumGenCrc32c() {
 }
 
 inline bool FileChecksumGenCrc32c::UpdateDevice(const void* dev_data, uint64_t n, mck_stream_t stream) {
+  if (failed_) return false;
+  failed_ = true;  // until this update has completed
   const uint64_t need = mck_crc32c_long_scratch_words(n) + 1;  // + result word
   if (need > scratch_words_) {
     if (d_scratch_) (void)hipFree(d_scratch_);
@@ -430,6 +498,7 @@ inline bool FileChecksumGenCrc32c::UpdateDevice(const void* dev_data, uint64_t n
       hipStreamSynchronize(st) != hipSuccess)
     return false;
   checksum_ = v;
+  failed_ = false;
   return true;
 }
 

@@ -439,7 +439,50 @@ TEST(BlockProtection, DataBlockMatchesProtectKV) {
   }
 }
 
+// No device: every reference-named function of the mirror that reads data
+// must refuse loudly (DeviceError), never hand back a checksum of 0; the file
+// checksum generator (no exceptions, no error channel) ends unknown.
+static int NoDeviceCases() {
+  const char d[] = "123456789";
+  int thrown = 0, n = 0;
+  auto expect_throw = [&](const char* name, auto fn) {
+    n++;
+    try {
+      (void)fn();
+      fprintf(stderr, "%s returned a value without a device\n", name);
+    } catch (const DeviceError& e) {
+      thrown++;
+      printf("[  OK  ] %s: %s\n", name, e.what());
+    }
+  };
+  expect_throw("crc32c::Value", [&] { return crc32c::Value(d, 9); });
+  expect_throw("crc32c::Extend", [&] { return crc32c::Extend(0, d, 9); });
+  expect_throw("XXH3_64bits", [&] { return XXH3_64bits(d, 9); });
+  expect_throw("ComputeBuiltinChecksum", [&] { return ComputeBuiltinChecksum(kCRC32c, d, 9); });
+  expect_throw("ComputeBuiltinChecksumWithLastByte",
+               [&] { return ComputeBuiltinChecksumWithLastByte(kXXH3, d, 9, 'x'); });
+  expect_throw("NPHash64", [&] { return NPHash64(d, 9, 0); });
+  expect_throw("log::PhysicalRecordCrc", [&] { return log::PhysicalRecordCrc(log::kFullType, d, 9, 7); });
+  expect_throw("VerifyBlockChecksum", [&] {
+    Footer f;
+    f.checksum_type = kCRC32c;
+    char blk[16] = {0};
+    return VerifyBlockChecksum(f, blk, 8, "x.sst", 0).ok();
+  });
+  // host algebra needs no device
+  n++;
+  if (crc32c::Unmask(crc32c::Mask(0xE3069283u)) == 0xE3069283u) thrown++;
+  FileChecksumGenCrc32c gen(FileChecksumGenContext{});
+  gen.Update(d, 9);
+  gen.Finalize();
+  n++;
+  if (gen.failed() && gen.GetChecksum() == kUnknownFileChecksum) thrown++;
+  printf("%d checks, %d failures\n", n, n - thrown);
+  return thrown == n ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
+  if (argc == 2 && !strcmp(argv[1], "--nodevice")) return NoDeviceCases();
   if (mck_device_count() < 1) {
     fprintf(stderr, "no gfx950 device\n");
     return 2;

@@ -28,6 +28,19 @@ def test_cpp_mirror_builds():
     assert os.path.exists(build())
 
 
+def test_cpp_mirror_fails_loudly_without_a_device():
+    """the reference-named functions must not turn a HIP
+    error into a checksum of 0 (a re-pointed trailer writer would store it):
+    with no GPU visible every one throws DeviceError, and the file checksum
+    generator ends kUnknownFileChecksum."""
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="-1", ROCR_VISIBLE_DEVICES="-1", CUDA_VISIBLE_DEVICES="-1")
+    out = subprocess.run([build(), "--nodevice"], capture_output=True, text=True, timeout=120, env=env)
+    print(out.stdout)
+    print(out.stderr)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "0 failures" in out.stdout
+
+
 @pytest.mark.gpu
 def test_cpp_mirror_reference_cases(gpu):
     out = subprocess.run([build()], capture_output=True, text=True, timeout=300)
