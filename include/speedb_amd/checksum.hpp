@@ -185,6 +185,39 @@ inline Status VerifyBlockChecksum(const Footer& footer, const char* data, size_t
   return BlockChecksumMismatch(type, stored, computed, modifier != 0, file_name, offset, block_size);
 }
 
+// PerfLevel / PerfContext::block_checksum_time (include/rocksdb/perf_level.h,
+// include/rocksdb/perf_context.h:97), per thread: at a timing level every
+// verify batch's DEVICE time is accumulated (mck_perf_context_get).
+enum PerfLevel : unsigned char {
+  kUninitialized = 0,
+  kDisable = 1,
+  kEnableCount = 2,
+  kEnableTimeExceptForMutex = 3,
+  kEnableTimeAndCPUTimeExceptForMutex = 4,
+  kEnableTime = 5,
+};
+inline void SetPerfLevel(PerfLevel level) { (void)mck_set_perf_level(level); }
+inline PerfLevel GetPerfLevel() { return static_cast<PerfLevel>(mck_get_perf_level()); }
+struct PerfContext {
+  uint64_t block_checksum_time = 0;   // ns of device time
+  uint64_t block_checksum_count = 0;  // blocks verified
+  void Reset() {
+    mck_perf_context c;
+    (void)mck_perf_context_get(&c, 1);
+    block_checksum_time = block_checksum_count = 0;
+  }
+};
+// This thread's context, brought up to date (waits for its timed batches).
+inline PerfContext* get_perf_context() {
+  static thread_local PerfContext ctx;
+  mck_perf_context c;
+  if (mck_perf_context_get(&c, 0) == MCK_OK) {
+    ctx.block_checksum_time = c.block_checksum_time;
+    ctx.block_checksum_count = c.block_checksum_count;
+  }
+  return &ctx;
+}
+
 // A block handle (table/format.h BlockHandle): payload offset and size.
 struct BlockHandle {
   uint64_t offset;

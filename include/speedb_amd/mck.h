@@ -771,6 +771,32 @@ typedef struct mck_statistics {
  * concurrently is lost. */
 int mck_statistics_get(mck_statistics* out, int reset);
 
+/* PerfContext (include/rocksdb/perf_context.h:97 block_checksum_time; the
+ * reference times every VerifyBlockChecksum with PERF_TIMER_GUARD,
+ * table/block_based/reader_common.cc:29).  Per calling thread, as the
+ * reference's thread-local perf context.  level: the reference's PerfLevel
+ * values (include/rocksdb/perf_level.h: 1 kDisable, 2 kEnableCount -- the
+ * default --, 3..5 also time).  At a timing level every
+ * mck_sst_verify_batch call brackets its kernel(s) with two HIP events on
+ * its stream; block_checksum_time is the DEVICE time of those batches in
+ * nanoseconds, available once they completed: mck_perf_context_get waits
+ * for this thread's outstanding batches.  block_checksum_count = blocks
+ * verified (kEnableCount and up), batches = verify calls. */
+#define MCK_PERF_kDisable 1
+#define MCK_PERF_kEnableCount 2
+#define MCK_PERF_kEnableTimeExceptForMutex 3
+#define MCK_PERF_kEnableTime 5
+typedef struct mck_perf_context {
+  uint64_t block_checksum_time;   /* ns of device time, timed levels only */
+  uint64_t block_checksum_count;  /* blocks verified */
+  uint64_t block_checksum_batches;
+} mck_perf_context;
+int mck_set_perf_level(int level);
+int mck_get_perf_level(void);
+/* Fill *out for the calling thread (synchronous on this thread's timed
+ * batches); reset != 0 zeroes it (PerfContext::Reset). */
+int mck_perf_context_get(mck_perf_context* out, int reset);
+
 /* TEST HOOK (parity tests only; never needed in production): ragged CRC
  * batches choose their driver per workgroup from the share's mean span
  * length, so a mixed parity batch may exercise only one driver.  driver:

@@ -974,3 +974,43 @@ def statistics(reset: bool = False) -> dict:
 
 
 __all__ += ["statistics"]
+
+
+# ---------------------------------------------------------------------------
+# PerfContext: block_checksum_time (include/rocksdb/perf_context.h:97,
+# table/block_based/reader_common.cc:29), per thread
+# ---------------------------------------------------------------------------
+
+class PerfLevel(enum.IntEnum):
+    """include/rocksdb/perf_level.h"""
+    kDisable = 1
+    kEnableCount = 2
+    kEnableTimeExceptForMutex = 3
+    kEnableTimeAndCPUTimeExceptForMutex = 4
+    kEnableTime = 5
+
+
+class mck_perf_context(ctypes.Structure):
+    _fields_ = [("block_checksum_time", ctypes.c_uint64), ("block_checksum_count", ctypes.c_uint64),
+                ("block_checksum_batches", ctypes.c_uint64)]
+
+
+def SetPerfLevel(level: int) -> None:
+    check(lib.mck_set_perf_level(int(level)), "mck_set_perf_level")
+
+
+def GetPerfLevel() -> PerfLevel:
+    return PerfLevel(lib.mck_get_perf_level())
+
+
+def get_perf_context(reset: bool = False) -> dict:
+    """This thread's perf context: block_checksum_time = nanoseconds of DEVICE
+    time of the VerifyBlockChecksum batches it issued at a timing level
+    (waits for them), block_checksum_count = blocks verified, batches."""
+    c = mck_perf_context()
+    check(lib.mck_perf_context_get(ctypes.addressof(c), 1 if reset else 0), "mck_perf_context_get")
+    return {"block_checksum_time": c.block_checksum_time, "block_checksum_count": c.block_checksum_count,
+            "block_checksum_batches": c.block_checksum_batches}
+
+
+__all__ += ["PerfLevel", "SetPerfLevel", "GetPerfLevel", "get_perf_context"]

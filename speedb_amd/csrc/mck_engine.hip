@@ -139,6 +139,63 @@ uint64_t known_bytes(const mck_spans* s) { return s->lengths ? 0 : (uint64_t)s->
 
 unsigned long long* dev_stats(int dev) { return g_dev[dev].d_stats; }
 
+// PerfContext::block_checksum_time (mck_perf_context_get): per thread, the
+// device time of the verify batches this thread issued at a timing level,
+// measured by an event pair on each batch's stream and read when asked for.
+struct PerfPending {
+  hipEvent_t a, b;
+  int dev;
+};
+struct PerfCtx {
+  int level = MCK_PERF_kEnableCount;  // the reference's default PerfLevel
+  uint64_t time_ns = 0, count = 0, batches = 0;
+  std::vector<PerfPending> pending;
+  std::vector<std::pair<int, hipEvent_t>> pool;  // (device, event) for reuse
+  // (events are not destroyed at thread exit: the runtime may be gone)
+};
+thread_local PerfCtx t_perf;
+
+hipEvent_t perf_event(int dev) {
+  for (size_t k = t_perf.pool.size(); k-- > 0;)
+    if (t_perf.pool[k].first == dev) {
+      hipEvent_t e = t_perf.pool[k].second;
+      t_perf.pool.erase(t_perf.pool.begin() + k);
+      return e;
+    }
+  hipEvent_t e = nullptr;
+  return hipEventCreate(&e) == hipSuccess ? e : nullptr;
+}
+
+// Brackets one verify batch: begin() before its launches, end() after.
+struct PerfScope {
+  hipStream_t st;
+  int dev = -1;
+  hipEvent_t a = nullptr;
+  PerfScope(hipStream_t s, uint64_t blocks) : st(s) {
+    if (t_perf.level < MCK_PERF_kEnableCount) return;
+    t_perf.count += blocks;
+    t_perf.batches++;
+    if (t_perf.level < MCK_PERF_kEnableTimeExceptForMutex || !blocks || hipGetDevice(&dev) != hipSuccess) return;
+    a = perf_event(dev);
+    if (a && hipEventRecord(a, st) != hipSuccess) {
+      t_perf.pool.push_back({dev, a});
+      a = nullptr;
+    }
+  }
+  void end(bool ok) {
+    if (!a) return;
+    hipEvent_t b = ok ? perf_event(dev) : nullptr;
+    if (b && hipEventRecord(b, st) == hipSuccess) {
+      t_perf.pending.push_back(PerfPending{a, b, dev});
+    } else {
+      t_perf.pool.push_back({dev, a});
+      if (b) t_perf.pool.push_back({dev, b});
+    }
+    a = nullptr;
+  }
+  ~PerfScope() { end(false); }
+};
+
 int check_spans(const mck_spans* s) {
   if (!s) {
     set_err("spans is NULL");
@@ -620,7 +677,10 @@ int mck_sst_verify_batch(int type, const mck_spans* payloads, const uint64_t* fi
     if (int rc = current_device(nullptr, nullptr)) return rc;
     a.stats_mismatch = dev_stats(dev);
   }
-  return launch_block<kModeVerify>(type, a, payloads->count, reinterpret_cast<hipStream_t>(stream));
+  PerfScope perf(reinterpret_cast<hipStream_t>(stream), payloads->count);
+  const int rc = launch_block<kModeVerify>(type, a, payloads->count, reinterpret_cast<hipStream_t>(stream));
+  perf.end(rc == MCK_OK);
+  return rc;
 }
 
 int mck_wal_record_crc_batch(const mck_spans* payloads, const uint8_t* types, uint32_t log_number, uint32_t* out,
@@ -1366,6 +1426,44 @@ int mck_statistics_get(mck_statistics* out, int reset) {
     out->block_checksum_mismatch_count += c;
   }
   (void)hipSetDevice(prev);
+  return rc;
+}
+
+int mck_set_perf_level(int level) {
+  t_err[0] = 0;
+  if (level < MCK_PERF_kDisable || level > MCK_PERF_kEnableTime) {
+    set_err("perf level must be %d..%d", MCK_PERF_kDisable, MCK_PERF_kEnableTime);
+    return MCK_EINVAL;
+  }
+  t_perf.level = level;
+  return MCK_OK;
+}
+
+int mck_get_perf_level(void) { return t_perf.level; }
+
+int mck_perf_context_get(mck_perf_context* out, int reset) {
+  t_err[0] = 0;
+  if (!out) {
+    set_err("out is NULL");
+    return MCK_EINVAL;
+  }
+  int rc = MCK_OK;
+  for (const PerfPending& p : t_perf.pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+      t_perf.time_ns += (uint64_t)((double)ms * 1e6);
+    } else if (rc == MCK_OK) {
+      set_err("timing a verify batch failed");
+      rc = MCK_EHIP;
+    }
+    t_perf.pool.push_back({p.dev, p.a});
+    t_perf.pool.push_back({p.dev, p.b});
+  }
+  t_perf.pending.clear();
+  out->block_checksum_time = t_perf.time_ns;
+  out->block_checksum_count = t_perf.count;
+  out->block_checksum_batches = t_perf.batches;
+  if (reset) t_perf.time_ns = t_perf.count = t_perf.batches = 0;
   return rc;
 }
 

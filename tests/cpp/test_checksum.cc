@@ -477,8 +477,42 @@ static int NoDeviceCases() {
   gen.Finalize();
   n++;
   if (gen.failed() && gen.GetChecksum() == kUnknownFileChecksum) thrown++;
+  // PerfContext needs no device to be read
+  n++;
+  SetPerfLevel(kEnableTime);
+  get_perf_context()->Reset();
+  if (GetPerfLevel() == kEnableTime && get_perf_context()->block_checksum_time == 0) thrown++;
+  SetPerfLevel(kEnableCount);
   printf("%d checks, %d failures\n", n, n - thrown);
   return thrown == n ? 0 : 1;
+}
+
+// PERF_TIMER_GUARD(block_checksum_time) (reader_common.cc:29): the batched
+// verify's device time lands in this thread's perf context at a timing level.
+TEST(Perf, BlockChecksumTime) {
+  std::vector<uint8_t> img(64 * 4101 + 64, 0);
+  std::vector<BlockHandle> h;
+  for (int i = 0; i < 64; i++) {
+    char* p = reinterpret_cast<char*>(img.data()) + i * 4101;
+    for (int k = 0; k < 4096; k++) p[k] = static_cast<char>(k * 7 + i);
+    p[4096] = 0;
+    const uint32_t c = crc32c::Mask(crc32c::Value(p, 4097));
+    for (int k = 0; k < 4; k++) p[4097 + k] = static_cast<char>(c >> (8 * k));
+    h.push_back(BlockHandle{static_cast<uint64_t>(i) * 4101, 4096});
+  }
+  void* d = nullptr;
+  EXPECT_EQ(hipMalloc(&d, img.size()), hipSuccess);
+  EXPECT_EQ(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice), hipSuccess);
+  Footer f;
+  f.checksum_type = kCRC32c;
+  SetPerfLevel(kEnableTimeExceptForMutex);
+  get_perf_context()->Reset();
+  std::vector<Status> per;
+  EXPECT_TRUE(VerifyBlockChecksums(f, d, 0, h, "perf.sst", &per).ok());
+  EXPECT_EQ(get_perf_context()->block_checksum_count, 64u);
+  EXPECT_TRUE(get_perf_context()->block_checksum_time > 0);
+  SetPerfLevel(kEnableCount);
+  (void)hipFree(d);
 }
 
 int main(int argc, char** argv) {
@@ -502,6 +536,7 @@ int main(int argc, char** argv) {
   RUN(KvChecksum, ScalarChainEqualsBatch);
   RUN(FileChecksum, Crc32cGenerator);
   RUN(BlockProtection, DataBlockMatchesProtectKV);
+  RUN(Perf, BlockChecksumTime);
   printf("%d checks, %d failures\n", g_checks, g_fail);
   return g_fail ? 1 : 0;
 }
