@@ -59,10 +59,7 @@ constexpr uint32_t kLdsLowEnd = kLdsQuarter + 512;  // 34816
 // the join of two chains (a 32-byte nibble map per round) costs more than
 // the latency it hides (headline 0.786 vs 0.774, SST 0.657 vs 0.648, WAL
 // 0.711 vs 0.700; four chains: 73.1 vs 76.5 %).
-#ifndef MCK_CRC_CHAINS
-#define MCK_CRC_CHAINS 1
-#endif
-constexpr int kCrcChains = MCK_CRC_CHAINS;
+constexpr int kCrcChains = 1;
 static_assert(kCrcChains == 1 || kCrcChains == 2 || kCrcChains == 4, "chains");
 constexpr uint32_t kLdsStep = 65536;
 constexpr uint32_t kLdsUnshift = 131072;
@@ -331,17 +328,14 @@ __device__ __forceinline__ void quad_transpose(Chunk& c, int q) {
     for (int j = 0; j < 4; j++) reinterpret_cast<uint32_t*>(&c.v[j])[d] = w[j];
   }
 }
-// Row variant (MCK_CRC_ROWT, the default): lane l = 16 k + c loads the 16 B
+// Row variant (kCrcRowT, the default): lane l = 16 k + c loads the 16 B
 // at 1024 j + 64 c + 16 k -- each instruction still reads the round's 1 KiB
 // j whole, in a permuted lane order -- and a 4 x 4 transpose over (row k,
 // register j) made of two v_permlane16_swap and two v_permlane32_swap per
 // 32-bit component (4 instructions, each moving two registers, instead of
 // 16 DPP moves and selects) leaves lane l holding the 64-byte chunk l: the
 // chunk layout itself, no virtual lanes.
-#ifndef MCK_CRC_ROWT
-#define MCK_CRC_ROWT 1
-#endif
-constexpr bool kCrcRowT = MCK_CRC_ROWT;
+constexpr bool kCrcRowT = true;
 __device__ __forceinline__ Chunk crc_load_chunk_rt(const CrcSpan& sp, int r, int plane) {
   const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 64ull * (plane & 15) + 16ull * (plane >> 4);
   Chunk c;
@@ -848,14 +842,6 @@ __device__ __forceinline__ RowSpan row_span_sel(bool a, const RowSpan& x, const 
 // pieces wholly before a0 read the zero piece `zp` instead, so they need no
 // masking (and lanes before the owner hash zeros); only the piece at a0
 // keeps ptr - a0 < 16 bytes of another span to mask (row_round).
-// MCK_ROW_LOAD_ZERO=1 (timing experiments only, wrong output): every piece
-// reads the zero piece.
-#ifndef MCK_PROLOGUE_ONLY
-#define MCK_PROLOGUE_ONLY 0
-#endif
-#ifndef MCK_ROW_LOAD_ZERO
-#define MCK_ROW_LOAD_ZERO 0
-#endif
 template <int W, int P = 4>
 __device__ __forceinline__ ChunkN<P> row_load_chunk(const RowSpan& sp, int r, uint32_t c, uint64_t zp) {
   constexpr uint64_t Q = 16u * P;
@@ -866,7 +852,7 @@ __device__ __forceinline__ ChunkN<P> row_load_chunk(const RowSpan& sp, int r, ui
   ChunkN<P> ch;
 #pragma unroll
   for (int j = 0; j < P; j++) {
-    const uint64_t a = rel < -16 * j || MCK_ROW_LOAD_ZERO ? zp : b + 16ull * j;
+    const uint64_t a = rel < -16 * j ? zp : b + 16ull * j;
     ch.v[j] = span_load16<false>(a);
   }
   return ch;

@@ -225,13 +225,10 @@ __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin
 // pieces and plans fit 128 VGPRs), 4 for the block / WAL / blob ops, whose
 // two prefetched epilogue inputs per plan would spill at 8 (A/B: 4300-B
 // Value blocks 0.599 at 8 vs 0.585 at 4; the SST verify mix spilled 80 B
-// per lane at 8 and lost 20 %).  -DMCK_UNIT_SLOTS=4|8 forces one (A/B).
-#ifndef MCK_UNIT_SLOTS
-#define MCK_UNIT_SLOTS 0
-#endif
+// per lane at 8 and lost 20 %).
 template <class Op>
 constexpr uint32_t unit_slots_of() {
-  return MCK_UNIT_SLOTS ? MCK_UNIT_SLOTS : sizeof(typename Op::Pre) <= 4 ? 8u : 4u;
+  return sizeof(typename Op::Pre) <= 4 ? 8u : 4u;
 }
 // flags: 8 bits each, bit j = slot j
 constexpr uint32_t kUFirst = 1u, kUHead = 1u << 8, kUTail = 1u << 16, kUEnd = 1u << 24;
@@ -546,9 +543,6 @@ __device__ __forceinline__ void crc_auto_units_driver(const Op& op, uint32_t fir
   // interleaved under the test hook) -- every driver works on the same one
   const RowShare sh = row_share<BLK>(first, count);
   if (sh.n == 0) return;  // workgroup-uniform (the row feed would read an unstaged slot 0)
-#if MCK_PROLOGUE_ONLY == 2  // timing experiments only (wrong output): an empty kernel
-  return;
-#endif
   int mode = force;
   bool lpt = force == 1;
   if (!mode) {

@@ -227,10 +227,6 @@ std::atomic<int> g_crc_force{0}, g_crc_interleaved{0};
 int crc_auto_force() { return g_crc_force.load(std::memory_order_relaxed); }
 bool crc_auto_blocked() { return g_crc_interleaved.load(std::memory_order_relaxed) == 0; }
 
-#ifndef MCK_GRID_MULT
-#define MCK_GRID_MULT 1
-#endif
-constexpr uint32_t kGridMult = MCK_GRID_MULT;
 
 template <class Op>
 int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
@@ -241,14 +237,14 @@ int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int n
   // one 16-wave workgroup per CU; each stages its share's descriptors in
   // LDS, so a batch runs in launches of at most ncu * kRowDescCache spans,
   // split evenly (no short last launch)
-  const uint32_t cap = kGridMult * (uint32_t)ncu * kRowDescCache;
+  const uint32_t cap = (uint32_t)ncu * kRowDescCache;
   const uint32_t nl = (count + cap - 1) / cap;
   const uint32_t per = (uint32_t)(((uint64_t)count + nl - 1) / nl);
   for (uint32_t first = 0; first < count; first += per) {
     const uint32_t n = std::min(per, count - first);
     // (>= 4 spans per workgroup: a batch of a few thousand large spans -- one
     // 64 MiB SST file -- still fills every CU)
-    const uint32_t grid = std::min<uint32_t>(kGridMult * ncu, (n + 3) / 4);
+    const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (n + 3) / 4);
     if (blk)
       hipLaunchKernelGGL((k_crc_auto<Op, T, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n,
                          crc_auto_force());
@@ -328,7 +324,7 @@ int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform) {
   if (rc) return rc;
   if (!uniform) {
     // one workgroup per CU, spans dealt by LDS tickets
-    const uint32_t grid = std::min<uint32_t>(kGridMult * (uint32_t)ncu, (count + 3) / 4);
+    const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + 3) / 4);
     hipLaunchKernelGGL((k_xxh3_wave<Op>), dim3(grid), dim3(kX3WaveThreads), 0, st, op, count);
   } else {
     // 16 rows (spans) per 256-thread workgroup
@@ -712,13 +708,10 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, 
   }
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
-#ifndef MCK_WAL_T
-#define MCK_WAL_T 1
-#endif
-  if (int rc = ensure_lds(k_wal_verify<MCK_WAL_T>, dev)) return rc;
+  if (int rc = ensure_lds(k_wal_verify<true>, dev)) return rc;
   const uint32_t nblocks = (uint32_t)nb64;
   const uint32_t grid = std::min<uint32_t>(ncu, (nblocks + 15) / 16);
-  hipLaunchKernelGGL(k_wal_verify<MCK_WAL_T>, dim3(grid), dim3(1024), kCrcLdsBytes,
+  hipLaunchKernelGGL(k_wal_verify<true>, dim3(grid), dim3(1024), kCrcLdsBytes,
                      reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(wal), nbytes, log_number,
                      reinterpret_cast<WalResult*>(results), nblocks);
   MCK_HIP(hipGetLastError());
@@ -755,7 +748,7 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
   if (int rc = ensure_lds(k_wal_write_il, dev)) return rc;
-  const uint32_t cap = kGridMult * (uint32_t)ncu * kRowDescCache;
+  const uint32_t cap = (uint32_t)ncu * kRowDescCache;
   const uint32_t nl = (nfrags + cap - 1) / cap;
   const uint32_t per = (uint32_t)(((uint64_t)nfrags + nl - 1) / nl);
   for (uint32_t first = 0; first < nfrags; first += per) {

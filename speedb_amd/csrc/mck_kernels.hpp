@@ -242,10 +242,7 @@ __global__ __launch_bounds__(256) void k_xxh3(Op op, uint32_t count) {
   xxh3_rows_driver(op, count);
 }
 // Wave driver workgroup: 16 waves, one workgroup per CU.
-#ifndef MCK_X3W_THREADS
-#define MCK_X3W_THREADS 1024
-#endif
-constexpr int kX3WaveThreads = MCK_X3W_THREADS;
+constexpr int kX3WaveThreads = 1024;
 static_assert(kX3WaveThreads / 64 <= kX3MaxWaves, "X3Lds holds a parked-sum buffer per wave");
 template <class Op>
 __global__ __launch_bounds__(kX3WaveThreads) void k_xxh3_wave(Op op, uint32_t count) {
@@ -503,7 +500,8 @@ struct WalFrag {  // = mck_wal_fragment
 //   * at the span's last round: the < 16 payload bytes before the first and
 //     after the last full output piece, byte by byte, and the trailer padding
 //     + header ([masked CRC][len][type][log number]) -- the CRC is known then.
-// Stores with nothing to write are exec-masked (MCK_WAL_SINK above).  The
+// Stores with nothing to write are exec-masked (round 2 measured sinks for
+// them: slower).  The
 // payload is read from HBM once.
 // LDS: the row image; fragments' dst_off at kLdsWalAux, over the un-shift
 // tables k >= 16, which this kernel never reads (typed init: no per-span

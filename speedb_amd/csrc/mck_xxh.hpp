@@ -417,16 +417,13 @@ __device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t 
 
 // PREVIEW = XXPH3 (Hash64 with `seed`), else XXH3_64bits v0.8.1 (seed 0).
 //
-// Epilogues are batched (MCK_X3_STASH, default on): a row's finished span
+// Epilogues are batched: a row's finished span
 // parks (index, hash) in lane `slot` of the row, and every 16 spans the 16
 // lanes run op.finish together -- its epilogue loads (op.pre) included --
 // instead of lane 0 running one finish (and every iteration carrying the
 // span's epilogue inputs in registers) per span.  For the per-KV protection
 // epilogue (key, op type and seqno hashes) that is most of a ~1 KiB span's
 // non-data VALU work.
-#ifndef MCK_X3_STASH
-#define MCK_X3_STASH 1
-#endif
 template <class Op, bool PREVIEW = false>
 __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, uint64_t seed = 0) {
   const X3Row X = x3_row(seed);
@@ -437,11 +434,9 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
   X3Span rs{reinterpret_cast<uint64_t>(op.base()), 0, 0, 0, 0, 0, false};
   bool act = x3_next_long<Op, PREVIEW>(op, first, count, stride, X, rs);
   uint64_t a0 = X.i0, a1 = X.i1;
-#if MCK_X3_STASH
   uint32_t slot = 0, si = 0;
   uint64_t shv = 0;
   bool sv = false;
-#endif
   // the raw last dword (d[3].w) of each lane's previous segment: lane 15's is
   // the dword before the row's next segment (e0 below)
   uint32_t pw = 0;
@@ -489,10 +484,6 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
       e0 = gload4(act && seg - sh >= idle ? seg - sh : idle);
     }
     const uint32_t el = gload4(act ? (full ? seg - sh + 4 : lst - shl) : idle);
-#if !MCK_X3_STASH
-    // the span's epilogue inputs travel with its data (see BlockPre / KvPre)
-    const typename Op::Pre e = op.pre(rs.i, rs.ptr, rs.len);
-#endif
     rd_fix_row(d, e0, X.j, sel);
     const uint32_t pl = dpp32<kDppQuadShr1>(dl.w);  // unconditional: see x3w_fold
     dl = rd_fix(dl, X.q ? pl : el, rd_sel(shl));
@@ -519,7 +510,6 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
       }
       const uint64_t m = quad_sum(mul128_fold64(a0 ^ X.km0, a1 ^ X.km1));
       const uint64_t h = PREVIEW ? xxph3_avalanche(rs.len * P64_1 + m) : xxh3_avalanche(rs.len * P64_1 + m);
-#if MCK_X3_STASH
       if ((uint32_t)X.j == slot) {
         si = rs.i;
         shv = h;
@@ -530,17 +520,12 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
         sv = false;
         slot = 0;
       }
-#else
-      if (X.j == 0) op.finish(rs.i, h, e);
-#endif
       act = x3_next_long<Op, PREVIEW>(op, rs.i + stride, count, stride, X, rs);
       a0 = X.i0;
       a1 = X.i1;
     }
   }
-#if MCK_X3_STASH
   if (sv) op.finish(si, shv);
-#endif
 }
 
 // ---- XXH3 / XXPH3, one WAVE per span ---------------------------------------
@@ -799,10 +784,7 @@ __device__ __forceinline__ void x3w_full_round(const X3WSpan& sp, uint32_t k, co
 // Pieces are handed out in order, so the piece a wave waits for is held by
 // a wave that started earlier and never waits on a later one: the oldest
 // unfinished piece always runs, and every wave of the workgroup is resident.
-#ifndef MCK_X3_PIECE_ROUNDS
-#define MCK_X3_PIECE_ROUNDS 4
-#endif
-constexpr uint32_t kX3PieceRounds = MCK_X3_PIECE_ROUNDS;
+constexpr uint32_t kX3PieceRounds = 4;
 constexpr uint32_t kX3MaxWaves = 16;
 
 template <bool PREVIEW>
