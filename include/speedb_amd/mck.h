@@ -315,6 +315,10 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes,
 /* Reader::UpdateRecordedTimestampSize (db/log_reader.cc:594-616) */
 #define MCK_WAL_R_TS_ZERO_SIZE 13
 #define MCK_WAL_R_TS_CF_UPDATE 14
+/* ReadRecord's kSetCompressionType case (db/log_reader.cc:167-188) */
+#define MCK_WAL_R_COMPRESSION_MULTIPLE 15
+#define MCK_WAL_R_COMPRESSION_NOT_FIRST 16
+#define MCK_WAL_R_COMPRESSION_DECODE 17
 /* "unknown record type %u" of header[6] read as a (signed) char: types
  * >= 128 print as 4294967xxx, as in the reference */
 #define MCK_WAL_R_UNKNOWN_TYPE_BASE 256 /* + the record type byte */
@@ -346,6 +350,21 @@ typedef struct mck_wal_read_out {
   uint64_t nreports;
   uint64_t dropped_bytes;     /* sum of the reported bytes                 */
   uint64_t end_offset;        /* where ReadRecord returned false           */
+  /* WAL compression (a kSetCompressionType record, db/log_writer.cc
+   * AddCompressionTypeRecord): 0 = none, else the record's CompressionType
+   * (kZSTD = 7).  From that record on, every physical record's payload is a
+   * chunk of ONE streaming-compressed stream: `frags` then hold the
+   * compressed chunks of each returned record, and the reader's
+   * StreamingUncompress is fed every chunk in `stream` order (also chunks of
+   * records later dropped, as ReadPhysicalRecord does, :534-571): stream[k]
+   * .dst_off = the index in `frags` of that chunk, or ~0 when its record was
+   * not returned.  Decompression, its errors (kBadRecord) and the XXH3
+   * record checksum over the decompressed bytes are the caller's. */
+  uint32_t compression_type;
+  uint32_t reserved;
+  mck_wal_fragment* stream;
+  uint64_t stream_cap;
+  uint64_t nstream;
 } mck_wal_read_out;
 
 /* log::Reader (checksum = true, no WAL compression) reading a whole WAL
@@ -356,8 +375,10 @@ typedef struct mck_wal_read_out {
  * image (the device's verdict on every physical record); NULL trusts every
  * CRC.  Returns the logical records (as fragments of one contiguous buffer,
  * for mck_wal_gather_batch) and every corruption the reader would report,
- * with the bytes it drops.  A kSetCompressionType record (compressed WAL):
- * MCK_ENOTSUP.  Results that do not belong to the image: MCK_EINVAL. */
+ * with the bytes it drops.  A compressed WAL (kSetCompressionType record) is
+ * walked and CRC-verified the same way; its records come back as compressed
+ * chunks (see mck_wal_read_out.compression_type).  Results that do not
+ * belong to the image: MCK_EINVAL. */
 int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t log_number,
                          int recovery_mode,
                          const mck_wal_block_result* verified,

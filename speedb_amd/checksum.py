@@ -604,7 +604,9 @@ class mck_wal_read_out(ctypes.Structure):
                 ("rec_file_offsets", ctypes.c_void_p), ("rec_cap", ctypes.c_uint64),
                 ("nrecords", ctypes.c_uint64), ("records_bytes", ctypes.c_uint64),
                 ("reports", ctypes.c_void_p), ("report_cap", ctypes.c_uint64), ("nreports", ctypes.c_uint64),
-                ("dropped_bytes", ctypes.c_uint64), ("end_offset", ctypes.c_uint64)]
+                ("dropped_bytes", ctypes.c_uint64), ("end_offset", ctypes.c_uint64),
+                ("compression_type", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("stream", ctypes.c_void_p), ("stream_cap", ctypes.c_uint64), ("nstream", ctypes.c_uint64)]
 
 
 class WalReadPlan(NamedTuple):
@@ -619,6 +621,9 @@ class WalReadPlan(NamedTuple):
     dropped_bytes: int       # ReportCollector::dropped_bytes_
     message: str             # ReportCollector::message_ ("Corruption: ..." appended)
     end_offset: int
+    compression_type: int = 0  # WAL compression (kSetCompressionType; kZSTD = 7), 0 = none
+    stream: list = []        # compressed logs: [(file offset, length, index in frags or -1)]
+                             # of every chunk fed to the reader's StreamingUncompress
 
 
 def wal_read_records(wal: bytes, log_number: int = 0,
@@ -643,14 +648,20 @@ def wal_read_records(wal: bytes, log_number: int = 0,
     lens = np.zeros(max(o.nrecords, 1), dtype=np.uint32)
     foffs = np.zeros(max(o.nrecords, 1), dtype=np.uint64)
     reps = (mck_wal_report * max(o.nreports, 1))()
+    strm = (mck_wal_fragment * max(o.nstream, 1))()
     o2 = mck_wal_read_out(ctypes.addressof(frags), o.nfrags, 0, offs.ctypes.data, lens.ctypes.data,
                           foffs.ctypes.data, o.nrecords, 0, 0, ctypes.addressof(reps), o.nreports)
+    o2.stream = ctypes.addressof(strm)
+    o2.stream_cap = o.nstream
     check(lib.mck_wal_read_records(buf, len(buf), log_number & 0xFFFFFFFF, int(recovery_mode), vp,
                                    ctypes.addressof(o2)), "mck_wal_read_records")
     reports = [(r.offset, r.bytes, lib.mck_wal_reason_string(r.reason).decode()) for r in reps[:o2.nreports]]
+    stream = [(f.src_off, f.length, -1 if f.dst_off == 0xFFFFFFFFFFFFFFFF else f.dst_off)
+              for f in strm[:o2.nstream]]
     return WalReadPlan(frags, o2.nfrags, offs[:o2.nrecords], lens[:o2.nrecords], foffs[:o2.nrecords],
                        o2.records_bytes, reports, o2.dropped_bytes,
-                       "".join("Corruption: " + r[2] for r in reports), o2.end_offset)
+                       "".join("Corruption: " + r[2] for r in reports), o2.end_offset,
+                       o2.compression_type, stream)
 
 
 class WalRecovery(NamedTuple):
@@ -658,11 +669,13 @@ class WalRecovery(NamedTuple):
     rec_offsets: object
     rec_lengths: object
     rec_file_offsets: object
-    record_checksums: object  # numpy uint64 XXH3_64bits of every record
+    record_checksums: object  # numpy uint64 XXH3_64bits of every record (None: compressed log)
     blocks: object           # device per-block verify results (or None)
     reports: list
     dropped_bytes: int
     message: str
+    compression_type: int = 0  # compressed WAL: records are compressed chunks (see WalReadPlan)
+    stream: list = []
 
     def Records(self):
         """The records as bytes (what ReadRecord's *record holds, in order)."""
@@ -703,14 +716,18 @@ def WalRecover(wal: bytes, log_number: int = 0,
             check(lib.mck_wal_gather_batch(img.data_ptr(), d_frags.data_ptr(), nf, out.data_ptr(), _stream(st)),
                   "mck_wal_gather_batch")
         offs, lens = plan.rec_offsets, plan.rec_lengths
-        if len(offs):
+        if plan.compression_type:
+            # compressed chunks: the record checksum is XXH3 over the
+            # DECOMPRESSED bytes (db/log_reader.cc:537-571), the caller's
+            x3 = None
+        elif len(offs):
             sp = Spans(out, len(offs), offsets=torch.from_numpy(offs.astype(np.int64)).to(dev),
                        lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
             x3 = xxh3_64_batch(sp, stream=st).cpu().numpy().view(np.uint64)
         else:
             x3 = np.zeros(0, np.uint64)
     return WalRecovery(out[:nbytes], offs, lens, plan.rec_file_offsets, x3, blocks, plan.reports,
-                       plan.dropped_bytes, plan.message)
+                       plan.dropped_bytes, plan.message, plan.compression_type, plan.stream)
 
 
 def WalReadRecords(wal: bytes, log_number: int = 0, device=None, stream=None):

@@ -213,9 +213,11 @@ struct WalReader {
       *frag_len = length;
       buf_off += hs + length;
       buf_size -= hs + length;
+      read_ok = true;  // (a type byte may equal one of the error codes above)
       return (int)type;
     }
   }
+  bool read_ok = false;  // the last read_physical returned a record
 };
 
 }  // namespace
@@ -237,6 +239,9 @@ extern "C" const char* mck_wal_reason_string(int reason) {
     case MCK_WAL_R_TS_ZERO_SIZE: return "User-defined timestamp size record contains zero timestamp size.";
     case MCK_WAL_R_TS_CF_UPDATE:
       return "User-defined timestamp size record contains update to recorded column family.";
+    case MCK_WAL_R_COMPRESSION_MULTIPLE: return "read multiple SetCompressionType records";
+    case MCK_WAL_R_COMPRESSION_NOT_FIRST: return "SetCompressionType not the first record";
+    case MCK_WAL_R_COMPRESSION_DECODE: return "could not decode SetCompressionType record";
     default:
       if (reason >= MCK_WAL_R_UNKNOWN_TYPE_BASE && reason < MCK_WAL_R_UNKNOWN_TYPE_BASE + 256) {
         static thread_local char buf[40];
@@ -269,23 +274,35 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
   uint64_t cur_file = 0;        // file offset of its first physical record
   size_t cur_first_frag = 0;    // its first fragment in fr
   bool in_fragmented_record = false;
+  // WAL compression: the chunks fed to StreamingUncompress, in order, and per
+  // fragment of fr the stream entry it came from
+  uint32_t compression = 0;
+  bool compression_read = false;
+  std::vector<mck_wal_fragment> stream;
+  std::vector<uint64_t> fr_sidx;
+  auto feed = [&](uint64_t off, uint32_t len, uint32_t type) {
+    if (compression) stream.push_back(mck_wal_fragment{off, ~0ull, len, (uint8_t)type, 0, 0});
+  };
   auto scratch_size = [&] { return dst - cur_start; };
   auto scratch_clear = [&] {  // scratch->clear(): its fragments are dropped
     fr.resize(cur_first_frag);
+    fr_sidx.resize(cur_first_frag);
     dst = cur_start;
+  };
+  auto scratch_append = [&](uint64_t off, uint32_t len, uint8_t type) {
+    fr.push_back(mck_wal_fragment{off, dst, len, type, 0, 0});
+    fr_sidx.push_back(compression ? stream.size() - 1 : ~0ull);  // the chunk just fed
+    dst += len;
   };
   auto scratch_assign = [&](uint64_t off, uint32_t len, uint8_t type, uint64_t file_off) {
     scratch_clear();
     cur_first_frag = fr.size();
     cur_file = file_off;
-    fr.push_back(mck_wal_fragment{off, dst, len, type, 0, 0});
-    dst += len;
-  };
-  auto scratch_append = [&](uint64_t off, uint32_t len, uint8_t type) {
-    fr.push_back(mck_wal_fragment{off, dst, len, type, 0, 0});
-    dst += len;
+    scratch_append(off, len, type);
   };
   auto emit = [&] {  // ReadRecord returns *record = scratch
+    for (size_t k = cur_first_frag; k < fr.size(); k++)
+      if (fr_sidx[k] != ~0ull) stream[fr_sidx[k]].dst_off = k;
     roff.push_back(cur_start);
     rlen.push_back((uint32_t)(dst - cur_start));
     rfile.push_back(cur_file);
@@ -302,8 +319,14 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
       const uint64_t phys = R.end_of_buffer_offset - R.buf_size;
       uint64_t drop_size = 0, foff = 0;
       uint32_t flen = 0;
+      R.read_ok = false;
       const int t = R.read_physical(&foff, &flen, &drop_size);
       if (R.err) break;
+      // ReadPhysicalRecord feeds every record it returns (but the
+      // compression and timestamp-size records) to the uncompressor
+      if (R.read_ok && t != (int)kSetCompressionType && t != (int)kUserDefinedTimestampSizeType &&
+          t != (int)kRecyclableUserDefinedTimestampSizeType)
+        feed(foff, flen, (uint32_t)t);
       if (t == 1 || t == 5) {  // kFullType
         if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_PARTIAL_WITHOUT_END_1);
         scratch_assign(foff, flen, (uint8_t)t, phys);
@@ -326,11 +349,23 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
           emit();
           break;
         }
-      } else if (t == (int)kSetCompressionType) {
-        // WAL compression (wal_compression != kNoCompression): the records
-        // that follow are compressed streams, outside this engine
-        mck_internal_set_error("WAL compression (kSetCompressionType record) is not supported");
-        return MCK_ENOTSUP;
+      } else if (t == (int)kSetCompressionType) {  // :167-188
+        if (compression_read) R.report(phys, flen, MCK_WAL_R_COMPRESSION_MULTIPLE);
+        if (R.first_record_read) R.report(phys, flen, MCK_WAL_R_COMPRESSION_NOT_FIRST);
+        cur_file = phys;
+        scratch_clear();
+        // CompressionTypeRecord::DecodeFrom (util/compression.h:1710-1725):
+        // LE32, a streaming-capable type (kNoCompression or kZSTD)
+        const uint8_t* p = R.d + foff;
+        const uint32_t ct = flen >= 4 ? (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) |
+                                            ((uint32_t)p[3] << 24)
+                                      : 0xFFFFFFFFu;
+        if (ct != 0 && ct != 7) {
+          R.report(phys, flen, MCK_WAL_R_COMPRESSION_DECODE);
+        } else {
+          compression_read = true;   // InitCompression (:590-600)
+          compression = ct;          // kNoCompression: no uncompressor
+        }
       } else if (t == (int)kUserDefinedTimestampSizeType || t == (int)kRecyclableUserDefinedTimestampSizeType) {
         if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_TS_INTERSPERSED);
         // prospective_record_offset = last_record_offset_ = this record's
@@ -425,6 +460,15 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
   if (out->reports) {
     const size_t n = std::min<size_t>(out->report_cap, R.reports.size());
     if (n) memcpy(out->reports, R.reports.data(), n * sizeof(mck_wal_report));
+  }
+  out->compression_type = compression;
+  out->nstream = stream.size();
+  if (out->stream) {
+    if (out->stream_cap < stream.size()) {
+      mck_internal_set_error("stream capacity too small");
+      return MCK_EINVAL;
+    }
+    if (!stream.empty()) memcpy(out->stream, stream.data(), stream.size() * sizeof(mck_wal_fragment));
   }
   return MCK_OK;
 }
