@@ -105,13 +105,31 @@ def VerifyChecksum(image: bytes, file_name: str = "", stream=None, device=None,
     if rc == MCK_ECORRUPT:
         return Status.Corruption(_err())
     check(rc, "mck_sst_verify_footer")
+    return VerifyBlocks(image, blocks, f.checksum_type, f.base_context_checksum, file_name, stream, device,
+                        per_block)
+
+
+def VerifyBlocks(image, blocks, checksum_type: int, base_context_checksum: int = 0, file_name: str = "",
+                 stream=None, device=None, per_block: Optional[list] = None) -> Status:
+    """The lower-level form of VerifyChecksum: the caller names the blocks
+    (``blocks``: (offset, size[, kind]) handles, as its own IndexBlockIter /
+    metaindex walk found them) and every one is verified in one GPU batch,
+    compressed or not -- the checksum covers the stored (compressed) bytes
+    and the type byte.  This is the path for tables whose index or meta
+    blocks are compressed (enable_index_compression defaults to true,
+    include/rocksdb/table.h:541), which list_blocks cannot parse."""
+    import torch
+    blocks = [b if isinstance(b, SstBlock) else SstBlock(int(b[0]), int(b[1]), b[2] if len(b) > 2 else "block")
+              for b in blocks]
+    if not blocks:
+        return Status.OK()
     dev = torch.device("cuda") if device is None else device
     img = torch.frombuffer(bytearray(bytes(image) + bytes(64)), dtype=torch.uint8).to(dev)
     offs = torch.tensor([b.offset for b in blocks], dtype=torch.int64, device=dev)
     lens = torch.tensor([b.size for b in blocks], dtype=torch.int32, device=dev)
     sp = Spans(img, len(blocks), offsets=offs, lengths=lens)
-    ct = ChecksumType(f.checksum_type)
-    mm, comp, stored, _ = sst_verify_batch(ct, sp, base_context_checksum=f.base_context_checksum,
+    ct = ChecksumType(checksum_type)
+    mm, comp, stored, _ = sst_verify_batch(ct, sp, base_context_checksum=base_context_checksum,
                                            stream=stream)
     mm = mm.cpu().numpy()
     comp = comp.cpu().numpy().view(np.uint32)
@@ -123,7 +141,7 @@ def VerifyChecksum(image: bytes, file_name: str = "", stream=None, device=None,
             s_v, c_v = int(stored[i]), int(comp[i])
             if ct == ChecksumType.kCRC32c:  # reader_common.cc:51-55: unmask for people
                 s_v, c_v = crc32c.Unmask(s_v), crc32c.Unmask(c_v)
-            ctx = "(context removed)" if f.base_context_checksum else ""
+            ctx = "(context removed)" if base_context_checksum else ""
             st = Status.Corruption(f"block checksum mismatch: stored{ctx} = {s_v}, computed = {c_v}, "
                                    f"type = {int(ct)}  in {file_name} offset {b.offset} size {b.size}")
             if first.ok():
@@ -133,4 +151,4 @@ def VerifyChecksum(image: bytes, file_name: str = "", stream=None, device=None,
     return first
 
 
-__all__ = ["list_blocks", "decode_footer", "VerifyChecksum", "SstBlock", "SstError", "BLOCK_KINDS"]
+__all__ = ["list_blocks", "decode_footer", "VerifyChecksum", "VerifyBlocks", "SstBlock", "SstError", "BLOCK_KINDS"]

@@ -164,7 +164,8 @@ def index_block(handles: List[Tuple[int, int]], keys: List[bytes], delta: bool,
 def write_sst(oracle, *, seed: int = 1, n_data: int = 40, checksum_type: int = 1,
               format_version: int = 5, index_type: int = 0, delta: Optional[bool] = None,
               base_context_checksum: int = 0x5EED1234, partition_size: int = 8,
-              meta: Tuple[str, ...] = ("filter", "range_del"), data_sizes=(1000, 9000)) -> Tuple[bytes, Layout]:
+              meta: Tuple[str, ...] = ("filter", "range_del"), data_sizes=(1000, 9000),
+              index_comp: int = 0) -> Tuple[bytes, Layout]:
     """An SST image: n_data data blocks of random payload sizes (index keys
     with shared prefixes), the meta blocks named in ``meta`` ("filter",
     "partitioned_filter", "range_del", "compression_dict"), the index
@@ -196,11 +197,14 @@ def write_sst(oracle, *, seed: int = 1, n_data: int = 40, checksum_type: int = 1
         parts = []
         for p in range(0, n_data, partition_size):
             blk = index_block(handles[p:p + partition_size], keys[p:p + partition_size], delta, 4)
-            parts.append((w.write_block(blk, "index_partition"), keys[min(p + partition_size, n_data) - 1]))
+            parts.append((w.write_block(blk, "index_partition", index_comp), keys[min(p + partition_size, n_data) - 1]))
         top = index_block([h for h, _ in parts], [k for _, k in parts], delta, 2)
-        index_h = w.write_block(top, "index")
+        index_h = w.write_block(top, "index", index_comp)
     else:
-        index_h = w.write_block(index_block(handles, keys, delta, 4, fk), "index")
+        # index_comp != 0: the index block's trailer names a compression
+        # type (enable_index_compression); its bytes stay opaque here (no
+        # compressor in this image) -- the checksum covers them as stored
+        index_h = w.write_block(index_block(handles, keys, delta, 4, fk), "index", index_comp)
     if "compression_dict" in meta:
         metas[b"rocksdb.compression_dict"] = w.write_block(bytes(rnd.getrandbits(8) for _ in range(200)),
                                                             "compression_dict")

@@ -135,3 +135,45 @@ def test_verify_sst_footer_checksum(gpu, oracle):
     bad[-53 + 1 + 16 + 3] ^= 0x40  # inside the 16 unchecked reserved bytes
     st = sst.VerifyChecksum(bytes(bad))
     assert st.IsCorruption() and "checksum mismatch" in st.message and "Footer at" in st.message
+
+
+@pytest.mark.parametrize("index_type", [0, 2])
+def test_compressed_index_is_not_parsed(oracle, index_type):
+    """An index block with a compression type (enable_index_compression, on
+    by default -- include/rocksdb/table.h:541) cannot be read by the host
+    lister (no decompressor): NotSupported, never a wrong block list."""
+    from speedb_amd import sst
+    img, _ = write_sst(oracle, format_version=5, index_type=index_type, n_data=20, index_comp=1)
+    with pytest.raises(sst.SstError) as e:
+        sst.list_blocks(img)
+    assert e.value.rc == sst.MCK_ENOTSUP and e.value.status.code == "Not implemented"
+    assert "compressed" in str(e.value)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fv,index_type", [(5, 0), (6, 2)])
+def test_compressed_index_low_level_verify(gpu, oracle, fv, index_type):
+    """The documented path for such tables: the reader's
+    own IndexBlockIter / metaindex walk names the blocks, one GPU batch
+    verifies all of them -- the compressed index blocks included (the
+    checksum covers the stored bytes and the type byte)."""
+    import speedb_amd as S
+    from speedb_amd import sst
+    img, layout = write_sst(oracle, format_version=fv, index_type=index_type, n_data=30, index_comp=1,
+                            meta=("filter", "range_del"))
+    handles = sorted(layout.blocks)
+    per = []
+    st = sst.VerifyBlocks(img, handles, 1, 0x5EED1234 if fv >= 6 else 0, "000007.sst", per_block=per)
+    assert st.ok(), st.ToString()
+    assert len(per) == len(handles) and all(s.ok() for _, s in per)
+    assert any(k == "index" for _, _, k in handles)
+    # a flipped byte in the compressed index block and in one data block
+    bad = bytearray(img)
+    idx = [h for h in handles if h[2] == "index"][0]
+    dat = [h for h in handles if h[2] == "data"][7]
+    bad[idx[0] + 3] ^= 0x10
+    bad[dat[0] + dat[1]] ^= 0x01  # the type byte
+    per = []
+    st = sst.VerifyBlocks(bytes(bad), handles, 1, 0x5EED1234 if fv >= 6 else 0, "000007.sst", per_block=per)
+    assert st.IsCorruption() and "block checksum mismatch" in st.ToString()
+    assert sorted(b.offset for b, s in per if not s.ok()) == sorted([idx[0], dat[0]])
