@@ -228,19 +228,19 @@ __device__ __forceinline__ void crc_bh_stage(const Op& op, const UShare& sh, uin
 // kind 2: round r of a body piece (rounds rhi down to rlo, wave-uniform);
 // kind 1: round q of a head batch (row values; R = the batch's rounds);
 // kind 0: nothing left.
-struct BhUnit {
+struct BhUnit {  // 64-bit fields first, no bools: copied whole, it must stay in registers
+  uint64_t ba1;         // body: the span's 16-aligned end
+  uint64_t hptr;        // head: the span's first byte (per row)
   int32_t kind;
   // body piece (wave-uniform)
   uint32_t bt;          // window slot
   int32_t r, rlo, rhi;  // current / last / first round of the piece (from the span end)
-  uint64_t ba1;
   uint32_t bkt;
   uint32_t binj;        // ~init at lane 0 of round rhi (h = 0, the span's first piece), else 0
   uint32_t bparts;      // the span's parts (1: finish at once)
   // head batch (per row; the rest of the head's geometry is derived, bh_hgeo)
   uint32_t ht;          // window slot
-  bool hlive;
-  uint64_t hptr;        // the span's first byte
+  uint32_t hlive;       // the row has a head in this batch
   uint32_t hn;          // the SPAN's bytes
   int32_t hrounds;      // 512-byte rounds of the head
   uint32_t hinj;        // ~init, un-shifted by (hptr & 15): injected at the piece holding hptr
@@ -258,7 +258,7 @@ __device__ __forceinline__ BhUnit bh_none() {
   u.binj = 0;
   u.bparts = 1;
   u.ht = 0;
-  u.hlive = false;
+  u.hlive = 0;
   u.hptr = 0;
   u.hn = 0;
   u.hrounds = 0;
@@ -301,7 +301,7 @@ __device__ __forceinline__ BhUnit bh_take(const Op& op, uint64_t base, int kind,
   if (k < hb) {  // head batch: row `lane / 8` takes head 8 k + row of the list
     u.kind = 1;
     const uint32_t e = 8 * k + (lane >> 3);
-    u.hlive = e < nheads;
+    u.hlive = e < nheads ? 1u : 0u;
     u.ht = *lds_p32(kBLdsHlist + 4 * (u.hlive ? e : 8 * k));
     const uint4 d = bh_desc(u.ht);
     const BhGeo x = bh_geo(base, d);

@@ -69,6 +69,14 @@ int ensure_lds(K kern, int dev) {
   static std::atomic<uint64_t> done{0};
   const uint64_t bit = 1ull << dev;
   if (done.load(std::memory_order_acquire) & bit) return MCK_OK;
+  // the LDS images are addressed from 0: a kernel with static LDS (the
+  // compiler promoting private arrays) would read shifted tables
+  hipFuncAttributes fa;
+  MCK_HIP(hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(kern)));
+  if (fa.sharedSizeBytes != 0) {
+    set_err("a CRC kernel has %zu B of static LDS; its image must start at 0", (size_t)fa.sharedSizeBytes);
+    return MCK_EHIP;
+  }
   MCK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)kCrcLdsBytes));
   done.fetch_or(bit, std::memory_order_acq_rel);

@@ -223,6 +223,11 @@ __global__ __launch_bounds__(1024) void k_crc_auto(Op op, uint32_t first, uint32
 // ragged batches on the body/head driver alone (mck_crc_bh.hpp)
 template <class Op, bool T>
 __global__ __launch_bounds__(1024) void k_crc_bh(Op op, uint32_t first, uint32_t count) {
+  // declared (though addressed absolutely, from 0): without it the compiler
+  // sees an LDS budget and promotes private arrays into static LDS, which
+  // would shift the dynamic image
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  asm volatile("" ::"v"((uint32_t)(size_t)lds));
   const RowShare sh = row_share<true>(first, count);
   if (sh.n == 0) return;
   crc_bh_driver<Op, T>(op, sh, &g_crc_tables);
