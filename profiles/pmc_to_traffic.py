@@ -73,6 +73,17 @@ def main():
         raise SystemExit("no counter rows for " + kernel)
     rd = 2 * 1024 * sum(fetch) / len(fetch)
     wr = 1024 * sum(write) / len(write)
+    whole_step = "(whole step" in kernel
+    if whole_step:
+        # alg bytes per STEP of several kernels (blockkv: layout, scans,
+        # protect, long-value sweep): every dispatch of the step's kernels,
+        # summed, over the steps the run made (= dispatches of the first
+        # kernel, launched once per step)
+        steps_f = len(per_launch(os.path.join(d, "pmc_fetch", "pmc_counter_collection.csv"), names[:1], "FETCH_SIZE"))
+        steps_w = len(per_launch(os.path.join(d, "pmc_write", "pmc_counter_collection.csv"), names[:1], "WRITE_SIZE"))
+        rd = 2 * 1024 * sum(fetch) / max(steps_f, 1)
+        wr = 1024 * sum(write) / max(steps_w, 1)
+        timed_ns = None
     if overlapped:
         m = re.search(r"\((\d+) launch\(es\) per step", kernel)
         # launches per step: stated in the label, else the dispatch count over
@@ -91,8 +102,9 @@ def main():
         "bench_kernel_avg_ms": line["roofline"]["kernel_avg_ms"],
         "source": os.path.relpath(d),
         "method": "FETCH_SIZE(KiB)*1024*2 (gfx950 16B/lane read correction) + WRITE_SIZE(KiB)*1024, "
-                  "averaged over the dominant kernel's dispatches; separate --pmc passes with "
-                  "--kernel-trace only",
+                  + ("summed over every kernel of a step, per step" if whole_step else
+                     "averaged over the dominant kernel's dispatches")
+                  + "; separate --pmc passes with --kernel-trace only",
     }
     dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"traffic_{workload}.json")
     with open(dst, "w") as f:
