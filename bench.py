@@ -138,7 +138,7 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0,
                    help="0 = the CPUs this process may use (cgroup quota / affinity)")
     p.add_argument("--no-verify", action="store_true")
-    p.add_argument("--crc-driver", choices=["auto", "wave", "rows16", "rows8", "units", "rows4", "rows1", "bh"], default="auto",
+    p.add_argument("--crc-driver", choices=["auto", "rows16", "rows8", "rows4", "rows1", "bh"], default="auto",
                    help="force the ragged CRC driver for every workgroup (A/B measurements; the engine's "
                         "test hook mck_test_set_crc_driver)")
     p.add_argument("--crc-order", choices=["blocked", "interleaved"], default="blocked",
@@ -251,18 +251,12 @@ def cpu_baseline(args, kind, block, sample, gpu_results):
     }
 
 
-def _auto(op):
-    """k_crc_auto's instantiation name for op (contiguous span ranges)."""
-    return f"mck::k_crc_auto<{op}, true, true>"
-
-
-def _launches(count, dev):
-    """Suffix for a k_crc_auto batch the engine splits into launches of at
-    most ncu * 1528 spans (its LDS descriptor cache): the bench times the
-    whole step, profiles/pmc_to_traffic.py then sums the launches."""
-    import torch
-    nl = -(-count // (torch.cuda.get_device_properties(dev).multi_processor_count * 1528))
-    return f" ({nl} launch(es) per step, timed as the step)" if nl > 1 else ""
+def _ragged(op, mean_len):
+    """The kernel that does a ragged CRC batch's work: k_crc_bh (body/head
+    driver) for spans averaging more than 2.5 KiB, k_crc_auto (row drivers)
+    otherwise -- both are launched, once each, and the other exits at once;
+    the HIP-event kernel time covers both."""
+    return f"mck::k_crc_bh<{op}, true>" if mean_len > 2560 else f"mck::k_crc_auto<{op}, true, true>"
 
 
 def C_wal_verify(im, nblocks, stream):
@@ -301,8 +295,8 @@ def make_workload(args, dev, rank, world):
         if args.workload == "crc32c":
             w.step = lambda: S.crc32c_batch(spans, out=out32, stream=stream)
             # 16-byte-multiple blocks: the whole-round uniform kernel; any
-            # other size (a 4300-B SST block): the ragged path's unit stream
-            w.kernel = CRC_UNIFORM_FULL if block % 4096 == 0 else _auto("mck::OpCrcValue") + _launches(count, dev)
+            # other size (a 4300-B SST block): the ragged path
+            w.kernel = CRC_UNIFORM_FULL if block % 4096 == 0 else _ragged("mck::OpCrcValue", block)
             w.alg_bytes = count * (block + 4)
         else:
             w.step = lambda: S.xxh3_64_batch(spans, out=out64, stream=stream)
@@ -345,7 +339,7 @@ def make_workload(args, dev, rank, world):
             stream.wait_event(join)
         w.step = step
         w.launches = len(imgs)
-        w.kernel = " + ".join({int(S.ChecksumType.kCRC32c): _auto("mck::OpCrcBlock<2>"),
+        w.kernel = " + ".join({int(S.ChecksumType.kCRC32c): _ragged("mck::OpCrcBlock<2>", 1 << 20),
                                int(S.ChecksumType.kXXH3): "mck::k_xxh3_wave<mck::OpX3Block<2> >"}[int(t)]
                               for t in types)
         w.span_bytes = sum(im.payload_bytes + im.count for im in imgs)  # payload + type byte
@@ -464,12 +458,12 @@ def make_workload(args, dev, rank, world):
         if args.workload == "walrec":
             types = torch.from_numpy(rng.choice([1, 2, 3, 4], size=count).astype(np.uint8)).to(dev)
             w.step = lambda: S.wal_record_crc_batch(sp, types, 7, out=out, stream=stream)
-            w.kernel = _auto("mck::OpCrcWal") + _launches(count, dev)
+            w.kernel = _ragged("mck::OpCrcWal", float(lens.mean()))
             w.desc = (f"WAL record CRCs (EmitPhysicalRecord, db/log_writer.cc:263-311): {count} records of "
                       f"{args.span_min}-{args.span_max} B per GPU at any byte offset, mck_wal_record_crc_batch")
         else:
             w.step = lambda: S.crc32c_batch(sp, out=out, stream=stream)
-            w.kernel = _auto("mck::OpCrcValue") + _launches(count, dev)
+            w.kernel = _ragged("mck::OpCrcValue", float(lens.mean()))
             w.desc = (f"crc32c_batch over {count} ragged spans of {args.span_min}-{args.span_max} B per GPU "
                       "(explicit offsets/lengths)")
         w.span_bytes = int(lens.sum())
@@ -545,7 +539,7 @@ def make_workload(args, dev, rank, world):
         def step():
             S.blob.record_batch(False, img, offs, lens, status=status, stream=stream)
         w.step = step
-        w.kernel = _auto("mck::OpBlobRecord<false>") + _launches(n, dev)
+        w.kernel = _ragged("mck::OpBlobRecord<false>", 4112)
         w.span_bytes = n * rec
         w.alg_bytes = n * (rec + 8 + 4 + 1)
         w.desc = (f"blob file verify: {n} records per GPU ({kb} B key, {vb} B value), header CRC + blob CRC "
@@ -677,7 +671,7 @@ def make_workload(args, dev, rank, world):
                 1, hbuf.data_ptr(), None, None, block, block, count, 0, ndev, 256 << 20,
                 out.ctypes.data, None, ctypes.byref(secs)), "mck_host_batch_checksum")
         w.step = step
-        w.kernel = _auto("mck::OpCrcValue") + " (H2D/D2H overlapped)"
+        w.kernel = _ragged("mck::OpCrcValue", 4300) + " (H2D/D2H overlapped)"
         w.span_bytes = count * block
         w.alg_bytes = count * (block + 4 + 8 + 4)
         per = count // max(1, ndev)
@@ -929,7 +923,7 @@ def main():
 
     from speedb_amd import _lib, shard
     if args.crc_driver != "auto" or args.crc_order != "blocked":
-        drv = {"auto": 0, "wave": 1, "rows16": 2, "rows8": 3, "units": 4, "rows4": 5, "rows1": 6, "bh": 7}[args.crc_driver]
+        drv = {"auto": 0, "rows16": 2, "rows8": 3, "rows4": 5, "rows1": 6, "bh": 7}[args.crc_driver]
         _lib.check(_lib.lib.mck_test_set_crc_driver(drv, 1 if args.crc_order == "interleaved" else 0),
                    "mck_test_set_crc_driver")
     w = make_workload(args, dev, rank, world)

@@ -818,13 +818,14 @@ int mck_get_perf_level(void);
  * batches); reset != 0 zeroes it (PerfContext::Reset). */
 int mck_perf_context_get(mck_perf_context* out, int reset);
 
-/* TEST HOOK (parity tests only; never needed in production): ragged CRC
- * batches choose their driver per workgroup from the share's mean span
- * length, so a mixed parity batch may exercise only one driver.  driver:
- * 0 = by length (the default), 1 = 4 KiB-round wave driver, 2 = 16-lane
- * rows, 3 = 8-lane rows, 4 = unit stream, 5 = 4-lane rows, 6 = one lane per
- * span; interleaved != 0 deals spans to
- * workgroups round-robin instead of in contiguous ranges.  Process-wide. */
+/* TEST HOOK (parity tests only; never needed in production): a ragged CRC
+ * batch runs each workgroup's share on the row drivers or the body/head
+ * driver, chosen from a sample of its lengths, so a mixed parity batch may
+ * exercise only one.  driver: 0 = by length (the default), 2 = 16-lane rows,
+ * 3 = 8-lane rows, 5 = 4-lane rows, 6 = one lane per span, 7 = the
+ * body/head driver (1 and 4, the retired wave driver and unit stream, are
+ * refused); interleaved != 0 deals spans to workgroups round-robin (row
+ * drivers only) instead of in contiguous ranges.  Process-wide. */
 int mck_test_set_crc_driver(int driver, int interleaved);
 
 #ifdef __cplusplus

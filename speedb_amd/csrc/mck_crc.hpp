@@ -539,70 +539,10 @@ __device__ __forceinline__ uint32_t crc_extend_byte(uint32_t crc, uint8_t b) {
 __device__ __forceinline__ uint32_t crc_mask(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
 
 
-struct SpanDesc {
-  uint64_t off;
-  uint64_t len;
-  uint32_t init;
-};
-
 typedef __attribute__((address_space(3))) uint32_t lds_u32_t;
 typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
 __device__ __forceinline__ lds_u32_t* lds_p32(uint32_t off) { return reinterpret_cast<lds_u32_t*>(static_cast<size_t>(off)); }
 __device__ __forceinline__ lds_u64_t* lds_p64(uint32_t off) { return reinterpret_cast<lds_u64_t*>(static_cast<size_t>(off)); }
-
-template <class Op, class Feed, bool T = false>
-__device__ __forceinline__ void crc_drive(const Op& op, Feed& f, const CrcLane& L) {
-  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  uint32_t i;
-  SpanDesc d;
-  if (!f.first(op, L, &i, &d)) return;
-  CrcSpan sp = crc_span(reinterpret_cast<const uint8_t*>(base + d.off), d.len, d.init);
-  int r = sp.rounds - 1;
-  Chunk cur = crc_load_chunk<T>(sp, r, L);
-  // the epilogue inputs of the span being loaded travel with its chunks
-  typename Op::Pre pcur = op.pre(i, sp.ptr, sp.end - sp.ptr);
-  uint32_t s = 0;
-  for (;;) {
-    uint32_t ni = i;
-    int nr = r - 1;
-    CrcSpan nsp = sp;
-    bool more = true;
-    if (nr < 0) {
-      SpanDesc nd;
-      more = f.next(op, L, &ni, &nd);
-      if (more) {
-        nsp = crc_span(reinterpret_cast<const uint8_t*>(base + nd.off), nd.len, nd.init);
-        nr = nsp.rounds - 1;
-      }
-    }
-    // unconditional (see crc_load_chunk); after the last round it re-reads
-    // the current chunk, which is never used
-    const CrcSpan& lsp = more ? nsp : sp;
-    const Chunk nxt = crc_load_chunk<T>(lsp, more ? nr : r, L);
-    const typename Op::Pre pnxt = op.pre(more ? ni : i, lsp.ptr, lsp.end - lsp.ptr);
-    if (T && !(sp.mini && r == sp.rounds - 1)) row_transpose(cur);  // wave-uniform
-    s = crc_round(s, cur, sp, r, L);
-    if (r == 0) op.finish(i, crc_finish(s, sp, L), pcur, (threadIdx.x & 63) == 0);
-    if (!more) break;
-    i = ni;
-    r = nr;
-    sp = nsp;
-    cur = nxt;
-    pcur = pnxt;
-  }
-}
-
-// crc_drive: the persistent, software-pipelined wave driver -- each wave
-// walks (span, round) pairs of the spans its feed hands it (FeedRowCache,
-// below); the next pair's chunk is loaded before the current one is hashed.
-// Op supplies the spans and consumes the results:
-//   const uint8_t* Op::base(), uint64_t Op::off(i), uint64_t Op::len(i),
-//   uint32_t Op::init_crc(i)                    (per lane, i < count)
-//   Op::Pre Op::pre(i, ptr, len)   epilogue inputs, loaded with the chunks
-//   void Op::finish(i, crc, pre, writer)  (all lanes call it; the lanes
-//                                  with writer set store: lane 0 of the wave
-//                                  here, lane 0 of each row in the row driver)
-// T: row-transposed loads (crc_load_chunk<true>, row_transpose).
 
 // ---------------------------------------------------------------------------
 // Uniform batches: every span has the same 16-byte-multiple length and a
@@ -953,21 +893,15 @@ __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, co
   return sp.n == 0 ? sp.init : ~p;
 }
 
-// Descriptor feed of the row driver: workgroup b owns spans first + b + G t
-// (t < its share, interleaved as in FeedLds), staged in LDS once as 16-byte
-// records {off, len, key}; a row takes the next one with an LDS ticket when
-// its span ends, one span ahead, so the chunk loads of a new span never wait
-// for a descriptor load (every load in the loop is a data load).  The host
-// splits batches whose share exceeds kRowDescCache into several launches.
-
-
-// Also sums the share's span bytes into the u64 at kLdsRowTotal (zeroed
-// here; valid after the next __syncthreads + the atomics).
+// Descriptor feed of the row driver: a workgroup's share is staged in LDS,
+// a window of at most kRowDescCache spans at a time, as 16-byte records
+// {off, len, key}; a row takes the next one with an LDS ticket when its span
+// ends, one span ahead, so the chunk loads of a new span never wait for a
+// descriptor load (every load in the loop is a data load).
+// The staging also sums the window's span bytes into the u64 at
+// kLdsRowTotal (zeroed here; valid after the next __syncthreads + the
+// atomics): the row width is chosen from its mean.
 constexpr uint32_t kLdsRowTotal = kLdsRowTicket + 8;  // u64
-// ... and the bytes the wave driver's 4 KiB rounds would cover (each span
-// rounded up to 4 KiB: a partial round costs it about as much as a full one)
-constexpr uint32_t kLdsRowWaveTotal = kLdsRowTicket + 16;  // u64
-constexpr uint32_t kLdsRowLongs = kLdsRowTicket + 24;      // u32: spans of >= 8 KiB
 // A workgroup's share of spans [first, first + count): span first + b + G t
 // (interleaved: the grid sweeps the batch front to back together) or, BLK,
 // the contiguous range [count b / G, count (b + 1) / G) (neighbouring spans
@@ -986,77 +920,26 @@ __device__ __forceinline__ RowShare row_share(uint32_t first, uint32_t count) {
   return {first + b, G, (count - b + G - 1) / G};
 }
 
-// Longest-first order for the wave driver (lpt): a wave hashes its span
-// alone, at about 1/16 of the CU's rate while the others run, so a 64 KiB
-// span taken last keeps the workgroup busy ~30 us after the rest is done
-// (the SST mix's per-launch tail).  Slots are staged by length class, long
-// first; the slot's share position rides in the high bits of the offset word
-// (offsets < 2^53), read back by FeedRowCache.
-constexpr int kLptClasses = 4;
-constexpr uint32_t kLdsLptCount = kLdsRowTicket + 32;   // [4] u32
-constexpr uint32_t kLdsLptCursor = kLdsRowTicket + 48;  // [4] u32
-constexpr uint32_t kLptSlotShift = 21;
-static_assert(kRowDescCache <= (1u << (32 - kLptSlotShift)), "slot bits");
-static_assert(kLdsLptCursor + 16 <= kLdsRowMaskHead, "lpt counters");
-__device__ __forceinline__ uint32_t lpt_class(uint32_t len) {
-  return len >= 49152 ? 0u : len >= 24576 ? 1u : len >= 8192 ? 2u : 3u;
-}
-
 template <class Op>
-__device__ __forceinline__ void row_desc_stage(const Op& op, const RowShare& sh, bool total, bool lpt = false) {
+__device__ __forceinline__ void row_desc_stage(const Op& op, const RowShare& sh, bool total) {
   const uint32_t n = sh.n;
-  if (lpt) {  // workgroup-uniform: count the classes first
-    if (threadIdx.x < 2 * kLptClasses) *lds_p32(kLdsLptCount + 4 * threadIdx.x) = 0;  // counts, cursors
-    __syncthreads();
-    for (uint32_t t = threadIdx.x; t < n; t += blockDim.x)
-      __hip_atomic_fetch_add(lds_p32(kLdsLptCount + 4 * lpt_class((uint32_t)op.len(sh.idx(t)))), 1u,
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    __syncthreads();
-  }
-  uint64_t sum = 0, wsum = 0;
-  uint32_t longs = 0;  // spans of >= 8 KiB (longest-first order matters only with them)
+  uint64_t sum = 0;
   for (uint32_t t = threadIdx.x; t < n; t += blockDim.x) {
     const uint32_t i = sh.idx(t);
     const uint64_t off = op.off(i);
     const uint32_t len = (uint32_t)op.len(i);
     sum += len;
-    longs += lpt_class(len) < 3 ? 1u : 0u;
-    // the bytes the wave driver's 4 KiB rounds would cover: the span's
-    // 16-byte-aligned extent rounded up to 4 KiB (a 4096-B span off the
-    // 16-byte grid takes two rounds)
-    wsum += (((((off + reinterpret_cast<uint64_t>(op.base())) & 15u) + len + 15) & ~15ull) + 4095) & ~4095ull;
-    span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, op.init_key(i)};
-    uint32_t pos = t;
-    if (lpt) {
-      const uint32_t c = lpt_class(len);
-      uint32_t below = 0;
-#pragma unroll
-      for (uint32_t k = 0; k < kLptClasses - 1; k++) below += k < c ? *lds_p32(kLdsLptCount + 4 * k) : 0u;
-      pos = below + __hip_atomic_fetch_add(lds_p32(kLdsLptCursor + 4 * c), 1u, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_WORKGROUP);
-      d.y |= t << kLptSlotShift;
-    }
-    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsRowDesc + 16 * pos)) = d;
+    const span_u32x4 d = {(uint32_t)off, (uint32_t)(off >> 32), len, op.init_key(i)};
+    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsRowDesc + 16 * t)) = d;
   }
   if (threadIdx.x == 0) *lds_p32(kLdsRowTicket) = 0;
   if (total) {
     // wave sums, then one LDS atomic per wave (after a barrier zeroes them)
-    for (int m = 32; m >= 1; m >>= 1) {
-      sum += __shfl_xor(sum, m, 64);
-      wsum += __shfl_xor(wsum, m, 64);
-      longs += (uint32_t)__shfl_xor((int)longs, m, 64);
-    }
-    if (threadIdx.x == 0) {
-      *lds_p64(kLdsRowTotal) = 0;
-      *lds_p64(kLdsRowWaveTotal) = 0;
-      *lds_p32(kLdsRowLongs) = 0;
-    }
+    for (int m = 32; m >= 1; m >>= 1) sum += __shfl_xor(sum, m, 64);
+    if (threadIdx.x == 0) *lds_p64(kLdsRowTotal) = 0;
     __syncthreads();
-    if ((threadIdx.x & 63) == 0) {
+    if ((threadIdx.x & 63) == 0)
       __hip_atomic_fetch_add(lds_p64(kLdsRowTotal), sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      __hip_atomic_fetch_add(lds_p64(kLdsRowWaveTotal), wsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (longs) __hip_atomic_fetch_add(lds_p32(kLdsRowLongs), longs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
   }
 }
 
@@ -1082,9 +965,9 @@ __device__ __forceinline__ uint4 row_desc(uint32_t t, uint32_t share) {
 // tables; ends with a barrier.
 template <class Op>
 __device__ __forceinline__ void crc_rows_prologue(const Op& op, const RowShare& sh, uint8_t* lds,
-                                                  const CrcTables* __restrict__ g, bool total, bool lpt = false) {
+                                                  const CrcTables* __restrict__ g, bool total) {
   crc_fill_rows(lds, g);
-  row_desc_stage<Op>(op, sh, total, lpt);
+  row_desc_stage<Op>(op, sh, total);
   __syncthreads();
   row_init_tables(op);
   __syncthreads();
@@ -1151,67 +1034,69 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, const RowShare& sh, 
   }
 }
 
-// The wave driver (crc_drive) fed from the row descriptor cache: one
-// ticket per wave; lpt: the slots were staged longest first (row_desc_stage).
+// ---------------------------------------------------------------------------
+// Ragged batches: two kernels over the whole batch, same grid, same
+// contiguous shares -- k_crc_auto (the row drivers, below) and k_crc_bh (the
+// body/head driver, mck_crc_bh.hpp) -- and every workgroup takes its share
+// in exactly one of them: the row drivers when the share's spans average at
+// most kAutoLongMin bytes, else the body/head driver.  The choice is made
+// from a fixed sample of the share's lengths (crc_share_long), the same
+// deterministic answer in both kernels.  (The host cannot choose: ragged
+// lengths live on the device.)
+constexpr uint32_t kAutoLongMin = 2560;    // mean span bytes
+constexpr uint32_t kAutoRows1Max = 80;     // one lane per span below ~80 B
+constexpr uint32_t kAutoRows8Max = 640;    // 8-lane rows up to 640 B, 16-lane rows above
 template <class Op>
-struct FeedRowCache {
-  RowShare sh;
-  int kind;
-  bool lpt;
-  __device__ bool take(uint32_t* span, SpanDesc* d) {
-    const uint32_t t = __builtin_amdgcn_readfirstlane(lds_ticket(lds_p32(kLdsRowTicket)));
-    const uint32_t share = sh.n;
-    if (t >= share) return false;
-    const uint4 v = row_desc(t, share);
-    const uint32_t hi = lpt ? v.y & ((1u << kLptSlotShift) - 1) : v.y;
-    *span = sh.idx(lpt ? v.y >> kLptSlotShift : t);
-    d->off = ((uint64_t)hi << 32) | v.x;
-    d->len = v.z;
-    d->init = kind == kInitArray ? v.w : *lds_p32(kLdsRowInit + 4 * (kind == kInitTyped ? (v.w & 15u) : 0u));
-    return true;
-  }
-  __device__ bool first(const Op&, const CrcLane&, uint32_t* span, SpanDesc* d) { return take(span, d); }
-  __device__ bool next(const Op&, const CrcLane&, uint32_t* span, SpanDesc* d) { return take(span, d); }
-};
+__device__ __forceinline__ bool crc_share_long(const Op& op, const RowShare& sh) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t m = sh.n < 64 ? sh.n : 64u;  // spans k n / m, k < m
+  uint64_t len = 0;
+  if (lane < m) len = op.len(sh.idx((uint32_t)((uint64_t)lane * sh.n / m)));
+  for (int d = 32; d >= 1; d >>= 1) len += __shfl_xor(len, d, 64);
+  return len > (uint64_t)kAutoLongMin * m;
+}
 
-// Ragged batches, driver chosen per workgroup from its share's mean span
-// length (the host cannot see device-resident lengths): 8-lane rows for
-// short spans, 16-lane rows for spans up to a few KiB, the wave driver
-// above that.  force: 0 = by length, 1 = wave, 2 = rows16, 3 = rows8,
-// 5 = rows4, 6 = one lane per span.
-// (Superseded for long spans by crc_auto_units_driver, mck_crc_units.hpp.)
-constexpr uint32_t kAutoRows8Max = 640;    // mean span bytes
-constexpr uint32_t kAutoRows16Max = 2560;
-constexpr uint32_t kAutoRows16WasteMax = 8192;  // mean span bytes, with > 25 % of the wave rounds empty
-// The drivers over a staged share (crc_rows_prologue done): force = the
-// driver chosen, else by the staging's totals.
-template <class Op, bool T>
-__device__ __forceinline__ void crc_auto_dispatch(const Op& op, const RowShare& sh, const CrcTables* __restrict__ g,
-                                                  int force, bool lpt) {
-  const uint32_t share = sh.n;
-  const uint64_t total = *lds_p64(kLdsRowTotal);
-  const uint64_t mean = total / (share ? share : 1);
-  // spans of a few KiB that leave the wave driver's last 4 KiB round mostly
-  // empty (blob records of 16 + 4096 B: 1 full + 1 nearly empty round) go
-  // to 16-lane rows as well (1 KiB rounds): blob verify 0.460 -> 0.559
-  const bool ragged4k = mean <= kAutoRows16WasteMax && 4 * *lds_p64(kLdsRowWaveTotal) > 5 * total;
-  const int mode = force                    ? force
-                   : mean <= kAutoRows8Max  ? 3
-                   : mean <= kAutoRows16Max ? 2
-                   : ragged4k               ? 2
-                                            : 1;
-  if (mode == 6) {
-    crc_rows_loop<Op, 1>(op, sh, g);
-  } else if (mode == 5) {
-    crc_rows_loop<Op, 4>(op, sh, g);
-  } else if (mode == 3) {
-    crc_rows_loop<Op, 8>(op, sh, g);
-  } else if (mode == 2) {
-    crc_rows_loop<Op, 16>(op, sh, g);
-  } else {
-    FeedRowCache<Op> f{sh, op.init_kind(), lpt};
-    crc_drive<Op, FeedRowCache<Op>, T>(op, f, crc_lane());
+// The row drivers over a share, in windows of at most kRowDescCache spans
+// (one launch per batch; the table image is filled once).  The width is
+// chosen once per share, from its first window's mean span: one lane per
+// span below ~80 B (20-100 B: 0.16-0.19 vs 0.09 of peak on 8-lane rows,
+// whose 512-B rounds are mostly padding there), 8-lane rows up to 640 B,
+// 16-lane rows above.  (The window loop sits inside each width's branch: a
+// loop around all four widths kept every width's lane constants live and
+// spilled 76-132 B per lane.)  force: 0 = by length, 2 = rows16, 3 = rows8,
+// 5 = rows4, 6 = one lane per span (test hook).
+template <class Op, int W>
+__device__ __forceinline__ void crc_rows_windows_w(const Op& op, const RowShare& share, uint32_t nwin,
+                                                   const CrcTables* __restrict__ g) {
+  const uint32_t n = share.n;
+  for (uint32_t wi = 0; wi < nwin; wi++) {
+    const uint32_t w0 = (uint32_t)((uint64_t)n * wi / nwin), w1 = (uint32_t)((uint64_t)n * (wi + 1) / nwin);
+    const RowShare sh{share.start + share.stride * w0, share.stride, w1 - w0};
+    if (wi) {  // window 0 was staged by the caller
+      __syncthreads();  // every row is done with the previous window's slots
+      row_desc_stage<Op>(op, sh, false);
+      __syncthreads();
+    }
+    crc_rows_loop<Op, W>(op, sh, g);
   }
+}
+template <class Op>
+__device__ __forceinline__ void crc_rows_windows(const Op& op, const RowShare& share, uint8_t* lds,
+                                                 const CrcTables* __restrict__ g, int force) {
+  const uint32_t n = share.n;
+  const uint32_t nwin = (n + kRowDescCache - 1) / kRowDescCache;
+  const RowShare sh0{share.start, share.stride, (uint32_t)((uint64_t)n / nwin)};
+  crc_rows_prologue<Op>(op, sh0, lds, g, true);
+  const uint64_t mean = *lds_p64(kLdsRowTotal) / sh0.n;
+  const int mode = force ? force : mean <= kAutoRows1Max ? 6 : mean <= kAutoRows8Max ? 3 : 2;
+  if (mode == 6)
+    crc_rows_windows_w<Op, 1>(op, share, nwin, g);
+  else if (mode == 5)
+    crc_rows_windows_w<Op, 4>(op, share, nwin, g);
+  else if (mode == 3)
+    crc_rows_windows_w<Op, 8>(op, share, nwin, g);
+  else
+    crc_rows_windows_w<Op, 16>(op, share, nwin, g);
 }
 
 }  // namespace mck

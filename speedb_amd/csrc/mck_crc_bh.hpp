@@ -54,9 +54,16 @@
 //   [64K, 128K)     the 4-byte step tables (kLdsStep, CrcLane)
 //   [128K, 160K)    the window's descriptors, accumulators, piece prefix
 #pragma once
-#include "mck_crc_units.hpp"
+#include "mck_crc.hpp"
 
 namespace mck {
+
+// A window of a share: slot t is span start + stride t.
+struct UShare {
+  uint32_t start, stride;
+  __device__ uint32_t idx(uint32_t t) const { return start + stride * t; }
+};
+__device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 constexpr uint32_t kBNC = 1024;                          // spans per window (<= kCrcBlock)
 constexpr uint32_t kBLdsRowGap = kLdsGap + 512;          // zshift(., 64 * 7): 8-lane rows

@@ -225,53 +225,17 @@ SpanSrc to_src(const mck_spans* s) {
 // 64 KiB 74.7 -> 83.4 %).
 constexpr bool kCrcGenericT = true;
 
-// Ragged batches run on k_crc_auto, which picks the driver per workgroup
-// from the mean length of its share (crc_auto_units_driver: 8- or 16-lane
-// rows, the unit stream) over contiguous span ranges per workgroup.  Tests
-// force one driver / the interleaved order through mck_test_set_crc_driver
-// (the per-workgroup choice by length means a mixed parity batch might
-// exercise only one); production code never calls it.
+// Ragged batches: k_crc_auto (row drivers) and k_crc_bh (body/head driver)
+// are both launched over the whole batch with the same grid and contiguous
+// shares; each workgroup works in exactly one of them, chosen on the device
+// from a sample of its share's lengths (crc_share_long: the host cannot see
+// device-resident lengths).  One launch each, whatever the batch size (both
+// walk their shares in LDS windows).  Tests force one driver / the
+// interleaved order through mck_test_set_crc_driver; production code never
+// calls it.
 std::atomic<int> g_crc_force{0}, g_crc_interleaved{0};
 int crc_auto_force() { return g_crc_force.load(std::memory_order_relaxed); }
 bool crc_auto_blocked() { return g_crc_interleaved.load(std::memory_order_relaxed) == 0; }
-
-
-template <class Op>
-int launch_crc_auto(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
-  constexpr bool T = kCrcGenericT;
-  const bool blk = crc_auto_blocked();
-  int rc = blk ? ensure_lds(k_crc_auto<Op, T, true>, dev) : ensure_lds(k_crc_auto<Op, T>, dev);
-  if (rc) return rc;
-  // one 16-wave workgroup per CU; each stages its share's descriptors in
-  // LDS, so a batch runs in launches of at most ncu * kRowDescCache spans,
-  // split evenly (no short last launch)
-  const uint32_t cap = (uint32_t)ncu * kRowDescCache;
-  const uint32_t nl = (count + cap - 1) / cap;
-  const uint32_t per = (uint32_t)(((uint64_t)count + nl - 1) / nl);
-  for (uint32_t first = 0; first < count; first += per) {
-    const uint32_t n = std::min(per, count - first);
-    // (>= 4 spans per workgroup: a batch of a few thousand large spans -- one
-    // 64 MiB SST file -- still fills every CU)
-    const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (n + 3) / 4);
-    if (blk)
-      hipLaunchKernelGGL((k_crc_auto<Op, T, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n,
-                         crc_auto_force());
-    else
-      hipLaunchKernelGGL((k_crc_auto<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n, crc_auto_force());
-    MCK_HIP(hipGetLastError());
-  }
-  return MCK_OK;
-}
-
-template <class Op>
-int launch_crc_bh(const Op& op, uint32_t count, hipStream_t st, int dev, int ncu) {
-  constexpr bool T = kCrcGenericT;
-  if (int rc = ensure_lds(k_crc_bh<Op, T>, dev)) return rc;
-  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + 3) / 4);
-  hipLaunchKernelGGL((k_crc_bh<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count);
-  MCK_HIP(hipGetLastError());
-  return MCK_OK;
-}
 
 template <class Op>
 int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
@@ -279,8 +243,28 @@ int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
   int dev, ncu;
   int rc = current_device(&dev, &ncu);
   if (rc) return rc;
-  if (crc_auto_force() == 7) return launch_crc_bh(op, count, st, dev, ncu);
-  return launch_crc_auto(op, count, st, dev, ncu);
+  constexpr bool T = kCrcGenericT;
+  const int force = crc_auto_force();
+  const bool blk = crc_auto_blocked();
+  // (>= 4 spans per workgroup: a batch of a few thousand large spans -- one
+  // 64 MiB SST file -- still fills every CU)
+  const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + 3) / 4);
+  if (force != 7) {  // the row drivers (under the interleaved hook: every share)
+    const int af = blk ? force : (force ? force : 8);
+    rc = blk ? ensure_lds(k_crc_auto<Op, T, true>, dev) : ensure_lds(k_crc_auto<Op, T>, dev);
+    if (rc) return rc;
+    if (blk)
+      hipLaunchKernelGGL((k_crc_auto<Op, T, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count, af);
+    else
+      hipLaunchKernelGGL((k_crc_auto<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count, af);
+    MCK_HIP(hipGetLastError());
+  }
+  if (blk && (force == 0 || force == 7)) {  // the body/head driver
+    if ((rc = ensure_lds(k_crc_bh<Op, T>, dev))) return rc;
+    hipLaunchKernelGGL((k_crc_bh<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count, force);
+    MCK_HIP(hipGetLastError());
+  }
+  return MCK_OK;
 }
 
 // Uniform batch fast path: geometry precomputed here (crc_uniform_driver).
@@ -1470,8 +1454,10 @@ int mck_perf_context_get(mck_perf_context* out, int reset) {
 
 int mck_test_set_crc_driver(int driver, int interleaved) {
   t_err[0] = 0;
-  if (driver < 0 || driver > 7) {
-    set_err("driver must be 0..7");
+  // 1 (the 4 KiB-round wave driver) and 4 (the unit stream) were retired
+  // in round 4 by the body/head driver (7)
+  if (driver < 0 || driver > 7 || driver == 1 || driver == 4) {
+    set_err("driver must be 0, 2, 3, 5, 6 or 7");
     return MCK_EINVAL;
   }
   g_crc_force.store(driver, std::memory_order_relaxed);

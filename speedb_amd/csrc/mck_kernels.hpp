@@ -7,7 +7,6 @@
 #include <stdint.h>
 
 #include "mck_crc.hpp"
-#include "mck_crc_units.hpp"
 #include "mck_crc_bh.hpp"
 #include "mck_xxh.hpp"
 
@@ -213,16 +212,23 @@ struct OpCrcBlock {
   }
 };
 
-// ragged batches: driver chosen per workgroup (crc_auto_units_driver)
+// Ragged batches: k_crc_auto and k_crc_bh are launched over the same batch
+// with the same grid; each workgroup takes its share in one of them
+// (crc_share_long, mck_crc.hpp).
+// k_crc_auto, force: 0 = short shares only, 2/3/5/6 = every share on that
+// row width, 8 = every share, width by length (the interleaved test order).
 template <class Op, bool T, bool BLK = false>
 __global__ __launch_bounds__(1024) void k_crc_auto(Op op, uint32_t first, uint32_t count, int force) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_auto_units_driver<Op, T, BLK>(op, first, count, lds, &g_crc_tables, force);
+  const RowShare sh = row_share<BLK>(first, count);
+  if (sh.n == 0) return;  // workgroup-uniform
+  if (force == 0 && crc_share_long(op, sh)) return;  // k_crc_bh's
+  crc_rows_windows<Op>(op, sh, lds, &g_crc_tables, force == 8 ? 0 : force);
 }
 
-// ragged batches on the body/head driver alone (mck_crc_bh.hpp)
+// k_crc_bh, force: 0 = long shares only, 7 = every share.
 template <class Op, bool T>
-__global__ __launch_bounds__(1024) void k_crc_bh(Op op, uint32_t first, uint32_t count) {
+__global__ __launch_bounds__(1024) void k_crc_bh(Op op, uint32_t first, uint32_t count, int force) {
   // declared (though addressed absolutely, from 0): without it the compiler
   // sees an LDS budget and promotes private arrays into static LDS, which
   // would shift the dynamic image
@@ -230,6 +236,7 @@ __global__ __launch_bounds__(1024) void k_crc_bh(Op op, uint32_t first, uint32_t
   asm volatile("" ::"v"((uint32_t)(size_t)lds));
   const RowShare sh = row_share<true>(first, count);
   if (sh.n == 0) return;
+  if (force == 0 && !crc_share_long(op, sh)) return;  // k_crc_auto's
   crc_bh_driver<Op, T>(op, sh, &g_crc_tables);
 }
 

@@ -24,9 +24,8 @@ constexpr int kMaxUnshift = 64;                                 // k in [0,64)
 // bytes apart between rounds.
 constexpr int kRowWidths = 3;  // W = 4 << k
 constexpr int row_gap_bytes(int k) { return (4 << k) * kChunkBytes - kChunkBytes; }
-// Unit-stream driver: a span shared by several waves' streams has each
-// portion's state moved to the span end by zshift(1024 m), m < 2^22 units
-// (spans < 4 GiB).
+// Body/head driver: a span's head and body pieces are moved to its end by
+// zshift(4096 m), m <= 2^20 (spans < 4 GiB): pow1k entries 2..22.
 constexpr int kPowBits = 23;
 
 struct alignas(16) CrcTables {
@@ -47,12 +46,8 @@ struct alignas(16) CrcTables {
   // lane c holds pieces c + 16 j of a 1280-byte round, j = 0..4)
   uint32_t lane_final16[8][16][16];  // zshift(v << 4n, 4 + 16 (15 - c))
   uint32_t gap244[4][256];           // zshift(v << 8t, 244): piece to piece
-  // unit-stream driver (mck_crc_units.hpp): lane l holds the 16-byte piece
-  // 16 l of every 1 KiB unit of a span, units anchored at the span's
-  // 16-aligned end
-  uint32_t gap1012[4][256];           // zshift(v << 8t, 4 + 1008): piece to the lane's next piece
-  uint32_t ulane_final[8][16][64];    // zshift(v << 4n, 4 + 16 (63 - l)): to the unit's end
-  uint32_t pow1k[kPowBits][8][16];    // zshift(v << 4n, 1024 * 2^b): stream portions to the span end
+  // body/head driver (mck_crc_bh.hpp): a span's parts moved to its end
+  uint32_t pow1k[kPowBits][8][16];    // zshift(v << 4n, 1024 * 2^b)
 };
 
 // ---- host-side GF(2) helpers (also used by the host shims) ----------------
@@ -124,16 +119,6 @@ inline void build_crc_tables(CrcTables* t) {
     const uint32_t k = gf_xpow8n(244);
     for (int b = 0; b < 4; b++)
       for (int v = 0; v < 256; v++) t->gap244[b][v] = gf_mul((uint32_t)v << (8 * b), k);
-  }
-  {
-    const uint32_t k = gf_xpow8n(1012);
-    for (int b = 0; b < 4; b++)
-      for (int v = 0; v < 256; v++) t->gap1012[b][v] = gf_mul((uint32_t)v << (8 * b), k);
-  }
-  for (int l = 0; l < 64; l++) {
-    const uint32_t k = gf_xpow8n(4u + 16u * (63 - l));
-    for (int n = 0; n < 8; n++)
-      for (int v = 0; v < 16; v++) t->ulane_final[n][v][l] = gf_mul((uint32_t)v << (4 * n), k);
   }
   for (int b = 0; b < kPowBits; b++) {
     const uint32_t k = gf_xpow8n(1024ull << b);

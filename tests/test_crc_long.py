@@ -1,17 +1,16 @@
-"""The unit-stream CRC driver (mck_crc_units.hpp) against the oracle.
+"""The body/head CRC driver (mck_crc_bh.hpp, k_crc_bh) against the oracle.
 
-k_crc_auto sends a workgroup whose share has a mean span above 2.5 KiB to
-the unit stream: 1 KiB units anchored at each span's 16-aligned end, the
-window's units cut into one equal stream per wave, four units per wave
-iteration across span boundaries; a span cut by stream boundaries is
-joined through an LDS accumulator (portions moved to the span end by
-zshift(1024 m)).  The cases below are the shapes that stress it: SST data
-blocks (4096 + 0..255 bytes + the type byte, never 16-aligned), uniform
-non-aligned strides, every span length around the unit / iteration
-boundaries, long spans (shared by many streams, portions finishing on
-different waves), runs of empty spans, non-zero Extend inits.  The unit
-stream forced on every generic CRC test (short spans, WAL, blob) and these
-tests with the interleaved span order: test_crc_rows.py
+A workgroup whose share averages more than 2.5 KiB per span takes it on the
+body/head driver: each span's whole 4 KiB rounds (ending at its 16-aligned
+end) in pieces of at most four rounds, its head (the rest, or the whole of
+a short span) on 8-lane rows eight heads at a time, the parts joined in an
+LDS accumulator (moved to the span end by zshift(4096 m)).  The cases below
+are the shapes that stress it: SST data blocks (4096 + 0..255 bytes + the
+type byte, never 16-aligned), uniform non-aligned strides, every span length
+around the round / piece / head-batch boundaries, long spans (many pieces
+finishing on different waves), runs of empty spans, many windows, non-zero
+Extend inits.  The driver forced on every generic CRC test (short spans,
+WAL, blob) and these tests with the row drivers: test_crc_rows.py
 test_auto_kernel_forced_drivers_subprocess.  Bit-exact throughout."""
 import random
 import struct
@@ -45,7 +44,7 @@ def _spans(torch, S, dev, offs, lens):
                    lengths=torch.tensor(lens, dtype=torch.int32, device="cuda"))
 
 
-def test_units_sst_block_shapes(gpu, oracle):
+def test_long_sst_block_shapes(gpu, oracle):
     """40K spans of 4096 + 0..255 (+1) bytes at every alignment: the 5-unit
     blocks whose last unit shares a wave iteration with the next block."""
     import speedb_amd as S
@@ -69,9 +68,9 @@ def test_units_sst_block_shapes(gpu, oracle):
 
 
 @pytest.mark.parametrize("stride", [4300, 4101, 5000, 8193])
-def test_units_uniform_unaligned_stride(gpu, oracle, stride):
+def test_long_uniform_unaligned_stride(gpu, oracle, stride):
     """Uniform batches whose length is not a 16-byte multiple (implicit
-    offsets i * stride): the unit stream, not the aligned uniform kernel."""
+    offsets i * stride): the body/head driver, not the aligned uniform kernel."""
     import speedb_amd as S
     torch = gpu
     count = 30_000
@@ -82,10 +81,10 @@ def test_units_uniform_unaligned_stride(gpu, oracle, stride):
         assert got[i] == oracle.Value(host[i * stride:(i + 1) * stride]), i
 
 
-def test_units_boundary_lengths(gpu, oracle):
+def test_long_boundary_lengths(gpu, oracle):
     """Lengths around the 1 KiB unit, the 4-unit iteration and multiples of
     16 units, at every start alignment, mixed with 3-8 KiB spans so the
-    workgroups choose the unit stream."""
+    workgroups choose the body/head driver."""
     import speedb_amd as S
     torch = gpu
     rnd = random.Random(11)
@@ -107,7 +106,7 @@ def test_units_boundary_lengths(gpu, oracle):
         assert ext[i] == oracle.Extend(inits[i], d), (i, o, n)
 
 
-def test_units_long_spans_split(gpu, oracle):
+def test_long_long_spans_split(gpu, oracle):
     """Spans of 25 units to 4 MiB (a 4 MiB span is longer than a whole
     window's stream: shared by all 16 waves), empty spans and short spans in
     between."""
@@ -129,7 +128,7 @@ def test_units_long_spans_split(gpu, oracle):
         assert ext[i] == oracle.Extend(inits[i], d), (i, o, n)
 
 
-def test_units_runs_of_empty_spans(gpu, oracle):
+def test_long_runs_of_empty_spans(gpu, oracle):
     """Runs of 0..200 empty spans between 3-9 KiB spans: a stream's lookahead
     over the units' prefix passes more than 63 empty spans at once."""
     import speedb_amd as S
@@ -151,7 +150,7 @@ def test_units_runs_of_empty_spans(gpu, oracle):
         assert ext[i] == oracle.Extend(inits[i], d), (i, o, n)
 
 
-def test_units_many_windows(gpu, oracle):
+def test_long_many_windows(gpu, oracle):
     """More spans per workgroup than one LDS descriptor window (832): the
     share is processed in several windows, and in several launches."""
     import speedb_amd as S
@@ -172,10 +171,10 @@ def test_units_many_windows(gpu, oracle):
 
 
 @pytest.mark.parametrize("ctype", [1, 4])
-def test_units_sst_verify_mix(gpu, oracle, ctype):
+def test_long_sst_verify_mix(gpu, oracle, ctype):
     """VerifyBlockChecksum over a compaction mix of 4/16/64 KiB blocks with
     jitter (64 KiB blocks cut by stream boundaries: the epilogue runs on
-    whichever wave finishes the last portion -- the CRC unit stream, and for
+    whichever wave finishes the last part -- the CRC body/head driver, and for
     kXXH3 the wave driver's pieces), context checksums, then flipped bytes."""
     import speedb_amd as S
     torch = gpu

@@ -1,11 +1,10 @@
 """The ragged-batch CRC drivers against the oracle.  A ragged batch runs on
-k_crc_auto, which picks per workgroup (from its share's mean span length)
-8- or 16-lane rows (one row per span, mck_crc.hpp crc_rows_loop) or the unit
-stream (mck_crc_units.hpp).  Every driver -- and the round-2 wave driver
-still reachable through the test hook -- is also forced for every workgroup
-in a child process over the generic-op parity tests
-(mck_test_set_crc_driver, set by tests/conftest.py from
-SPEEDB_AMD_TEST_CRC_DRIVER / _ORDER)."""
+two kernels over the same shares: k_crc_auto (one lane, 4-, 8- or 16-lane
+rows per span, mck_crc.hpp crc_rows_loop, for shares of short spans) and
+k_crc_bh (the body/head driver, mck_crc_bh.hpp, for the rest).  Every
+driver is also forced for every workgroup in a child process over the
+generic-op parity tests (mck_test_set_crc_driver, set by tests/conftest.py
+from SPEEDB_AMD_TEST_CRC_DRIVER / _ORDER)."""
 import os
 import random
 import subprocess
@@ -61,7 +60,7 @@ def _forced(env):
         "test_crc32c_known_answers_on_device", "test_builtin_checksum_batch", "test_sst_verify_large_static_feed",
         "test_checksum_schemas_on_device", "test_scalar_shims", "test_crc32c_long_vs_oracle")]
     tests += [os.path.join(HERE, "test_blob_file.py"), os.path.join(HERE, "test_sst_file.py"),
-              os.path.join(HERE, "test_crc_units.py")]
+              os.path.join(HERE, "test_crc_long.py")]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-m", "gpu", "-p", "no:cacheprovider",
                         "-k", "not subprocess"] + tests,
                        env=dict(os.environ, **env), cwd=os.path.dirname(HERE), capture_output=True, text=True,
@@ -70,7 +69,7 @@ def _forced(env):
     assert " passed" in r.stdout
 
 
-@pytest.mark.parametrize("mode", ["wave", "rows16", "rows8", "rows4", "rows1", "units", "bh", "interleaved"])
+@pytest.mark.parametrize("mode", ["rows16", "rows8", "rows4", "rows1", "bh", "interleaved"])
 def test_auto_kernel_forced_drivers_subprocess(gpu, mode):
     """k_crc_auto with each driver forced for every workgroup (its choice is
     by mean length, so a parity test of mixed lengths may exercise only one):
