@@ -630,6 +630,20 @@ constexpr uint32_t kBlkKeyBuf = 128;  // bytes of LDS key buffer per thread
 // per 16-lane row, 16-byte loads), XORs the value hash into enc[k] (protect)
 // or compares partial ^ value hash with the stored bytes (verify).
 constexpr uint32_t kBlkLong = 241;
+// Encode(n) bytes of key k in a kv_checksum array: one load of n bytes when
+// the array is aligned to n, byte loads otherwise.
+__device__ __forceinline__ uint64_t blk_load_prot(const uint8_t* a, uint64_t k, uint32_t n) {
+  const uint64_t at = reinterpret_cast<uint64_t>(a) + k * n;
+  if ((at & (n - 1)) == 0) {  // n = 1, 2, 4, 8
+    if (n == 8) return *reinterpret_cast<gbl_u64u_t*>(at);
+    if (n == 4) return *reinterpret_cast<gbl_u32u_t*>(at);
+    if (n == 2) return *reinterpret_cast<__attribute__((address_space(1))) const uint16_t*>(at);
+    return *reinterpret_cast<gbl_u8_t*>(at);
+  }
+  uint64_t s = 0;
+  for (uint32_t c = 0; c < n; c++) s |= (uint64_t)*reinterpret_cast<gbl_u8_t*>(at + c) << (8 * c);
+  return s;
+}
 // 17..128-byte values are hashed by lane octets (xp_mid_octets)
 template <int KIND, bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t count, const uint64_t* key_base,
@@ -652,28 +666,68 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
   uint8_t* const gkey = active ? arena + ldg_u64(arena_base, b) : arena;
   bool global_key = false;
   const GblRd rd{active ? blocks.ptr(b) : nullptr};
-  const uint32_t ro = active ? rd_header(rd, blocks.len(b)).ro : 0;  // the layout pass validated the block
+  const uint32_t n = active ? (uint32_t)blocks.len(b) : 0;  // the layout pass validated the block (< 4 GiB)
+  const uint32_t ro = active ? rd_header(rd, n).ro : 0;
   const uint64_t oklo = sec64(16 * (int)(lane & 7)) + kSeedV, okhi = sec64(16 * (int)(lane & 7) + 8) - kSeedV;
+  // 8-byte protection into an aligned array: entries are stored in pairs
+  const bool p8 = !VERIFY && prot_bytes == 8 && (reinterpret_cast<uint64_t>(enc) & 7) == 0;
+  uint64_t pend = 0;  // p8: the lane's even entry, stored with the odd one after it
   uint32_t p = 0, idx = 0;
-  uint32_t u = active ? rd.u32(0) : 0;  // the next entry's first dword, one entry ahead
+  // The next entry's first 16 bytes, one entry ahead: its header and, on
+  // DecodeEntry's fast path, its key delta's first 13 bytes -- ONE divergent
+  // load per entry where the header dword and two key-delta loads were three
+  // (a load whose 64 lanes read 64 blocks is what bounds this kernel: the
+  // texture addresser).  uok = false: the 16 bytes would
+  // leave the block, the entry is read field by field.
+  uint4 U = make_uint4(0, 0, 0, 0);
+  bool uok = false;
+  if (active) {
+    uok = n >= 16;
+    if (uok) U = vload16_any(reinterpret_cast<uint64_t>(rd.p));
+  }
   while (__any(active)) {
     uint32_t sh = 0, ns = 0, q = 0, v = 0, vl = 0;
     uint64_t hv = 0;
     uint32_t kw[4];
     bool vmid = false;
     if (active) {
-      rd_entry_pre<KIND>(rd, p, ro, u, &sh, &ns, &q, &v, &vl);
-      // prefetch: the following entry's header travels with this entry's
-      // key and value loads (one dependent round trip per entry, not two)
-      if (v + vl < ro) u = rd.u32(v + vl);
-      // this entry's loads, all issued before any is waited for: the key
-      // delta's first 16 bytes (8 bytes at q are always inside the block: the
-      // 4-byte restart array + 4-byte footer at least), as two 8-byte loads
-      const uint64_t k01 = rd.u64(q), k23 = rd.u64(ns > 8 ? q + 8 : q);
-      kw[0] = (uint32_t)k01;
-      kw[1] = (uint32_t)(k01 >> 32);
-      kw[2] = (uint32_t)k23;
-      kw[3] = (uint32_t)(k23 >> 32);
+      const uint4 Uc = U;
+      bool fast = false;
+      if (KIND != kBlkIndexDelta && KIND != kBlkIndexDeltaFk && uok && (Uc.x & 0x808080u) == 0) {
+        // block.cc:45-50: shared, non_shared, value length one byte each
+        const uint32_t kk = (Uc.x >> 8) & 255u, xx = (Uc.x >> 16) & 255u;
+        if (p <= ro && ro - p >= 3 && ro - (p + 3) >= kk + xx) {
+          sh = Uc.x & 255u;
+          ns = kk;
+          q = p + 3;
+          v = q + kk;
+          vl = xx;
+          fast = true;
+        }
+      }
+      if (!fast) rd_entry<KIND>(rd, p, ro, &sh, &ns, &q, &v, &vl);
+      const uint32_t pn = v + vl;
+      if (pn < ro) {
+        uok = pn + 16 <= n;
+        if (uok) U = vload16_any(reinterpret_cast<uint64_t>(rd.p + pn));
+      }
+      // the key delta's first 16 bytes: bytes 3..18 of the entry on the fast
+      // path (the dword at p + 16 only when non_shared > 13: then it lies
+      // before the value); otherwise two 8-byte loads at q (8 bytes at q are
+      // always inside the block: the restart array + footer follow)
+      if (fast) {
+        const uint32_t e = ns > 13 ? rd.u32(p + 16) : 0u;
+        kw[0] = __builtin_amdgcn_alignbyte(Uc.y, Uc.x, 3);
+        kw[1] = __builtin_amdgcn_alignbyte(Uc.z, Uc.y, 3);
+        kw[2] = __builtin_amdgcn_alignbyte(Uc.w, Uc.z, 3);
+        kw[3] = __builtin_amdgcn_alignbyte(e, Uc.w, 3);
+      } else {
+        const uint64_t k01 = rd.u64(q), k23 = rd.u64(ns > 8 ? q + 8 : q);
+        kw[0] = (uint32_t)k01;
+        kw[1] = (uint32_t)(k01 >> 32);
+        kw[2] = (uint32_t)k23;
+        kw[3] = (uint32_t)(k23 >> 32);
+      }
       vmid = vl > 16 && vl <= 128;
     }
     {
@@ -714,13 +768,22 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
         if constexpr (VERIFY) long_part[k] = hv;
       }
       if constexpr (!VERIFY) {
-        if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0))
-          reinterpret_cast<uint64_t*>(enc)[k] = hv;
-        else
+        if (p8) {
+          // entries idx - 1, idx as one 16-byte store when idx is odd (half
+          // the divergent stores); a block's last even entry alone
+          if (idx & 1) {
+            *reinterpret_cast<__attribute__((address_space(1))) span_u32x4*>(
+                reinterpret_cast<uint64_t>(enc) + 8 * (k - 1)) =
+                span_u32x4{(uint32_t)pend, (uint32_t)(pend >> 32), (uint32_t)hv, (uint32_t)(hv >> 32)};
+          } else if (v + vl >= ro) {
+            reinterpret_cast<uint64_t*>(enc)[k] = hv;
+          }
+          pend = hv;
+        } else {
           for (uint32_t c = 0; c < prot_bytes; c++) enc[k * prot_bytes + c] = (uint8_t)(hv >> (8 * c));
+        }
       } else if (!lng) {
-        uint64_t sv = 0;
-        for (uint32_t c = 0; c < prot_bytes; c++) sv |= (uint64_t)blk_u8(stored + k * prot_bytes + c) << (8 * c);
+        const uint64_t sv = blk_load_prot(stored, k, prot_bytes);
         const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
         const bool bad = sv != (hv & keep);
         mismatch[k] = bad;
@@ -791,8 +854,7 @@ __global__ __launch_bounds__(256) void k_block_long(const uint64_t* key_base, ui
           for (uint32_t b = 0; b < prot_bytes; b++) enc[k * prot_bytes + b] ^= (uint8_t)(hv >> (8 * b));
         }
       } else {
-        uint64_t sv = 0;
-        for (uint32_t b = 0; b < prot_bytes; b++) sv |= (uint64_t)blk_u8(stored + k * prot_bytes + b) << (8 * b);
+        const uint64_t sv = blk_load_prot(stored, k, prot_bytes);
         const bool bad = sv != ((part ^ hv) & keep);
         mismatch[k] = bad;
         if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);

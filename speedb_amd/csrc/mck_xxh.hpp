@@ -724,19 +724,27 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
 // x3w_round_c: the round's four segment sums C_g (row 0's lanes hold segments
 // 4k .. 4k + 3 in order, for their accumulator pair q); x3w_full_round
 // chains them into the accumulators.
-template <bool PREVIEW>
-__device__ __forceinline__ void x3w_round_c(const X3WSpan& sp, uint32_t k, const X3Row& X, uint64_t (&C0)[4],
-                                            uint64_t (&C1)[4]) {
+struct X3RoundLoads {
+  uint4 d[4];
+  uint32_t e0;  // the dword before the row's segment (byte-misaligned spans)
+};
+__device__ __forceinline__ X3RoundLoads x3w_round_load(const X3WSpan& sp, uint32_t k, const X3Row& X) {
+  X3RoundLoads R;
   const uint32_t sh = rd_shift(sp.ptr);
   const uint64_t seg = sp.ptr + 1024ull * (4 * k + X.row);
   const uint64_t a = seg + 64 * X.st4 + 16 * X.q - sh + 4;
-  uint4 d[4];
 #pragma unroll
-  for (int m = 0; m < 4; m++) d[m] = gload16u(a + 256 * m);
-  if (sp.ptr & 3) {  // wave-uniform
-    const uint32_t e0 = gload4(seg - sh);
-    rd_fix_row(d, e0, X.j, rd_sel(sh));
-  }
+  for (int m = 0; m < 4; m++) R.d[m] = gload16u(a + 256 * m);
+  // (rd_shift is 4, not 0, for a dword-aligned span: seg - 4 could lie
+  // before the buffer)
+  R.e0 = (sp.ptr & 3) ? gload4(seg - sh) : 0u;  // wave-uniform
+  return R;
+}
+template <bool PREVIEW>
+__device__ __forceinline__ void x3w_round_sums(const X3WSpan& sp, X3RoundLoads R, const X3Row& X,
+                                               uint64_t (&C0)[4], uint64_t (&C1)[4]) {
+  uint4(&d)[4] = R.d;
+  if (sp.ptr & 3) rd_fix_row(d, R.e0, X.j, rd_sel(rd_shift(sp.ptr)));  // wave-uniform
   uint64_t c0 = 0, c1 = 0;
 #pragma unroll
   for (int m = 0; m < 4; m++) {
@@ -755,6 +763,11 @@ __device__ __forceinline__ void x3w_round_c(const X3WSpan& sp, uint32_t k, const
   C1[1] = e1;
   C1[2] = xl32_64(c1);
   C1[3] = xl32_64(e1);
+}
+template <bool PREVIEW>
+__device__ __forceinline__ void x3w_round_c(const X3WSpan& sp, uint32_t k, const X3Row& X, uint64_t (&C0)[4],
+                                            uint64_t (&C1)[4]) {
+  x3w_round_sums<PREVIEW>(sp, x3w_round_load(sp, k, X), X, C0, C1);
 }
 template <bool PREVIEW>
 __device__ __forceinline__ void x3w_full_round(const X3WSpan& sp, uint32_t k, const X3Row& X, uint64_t& a0,
@@ -838,6 +851,9 @@ struct X3FeedPieces {
 };
 
 // Park the piece's segment sums (rounds k0 .. ke - 1) in the wave's buffer.
+// (Round 4 measured round k + 1's loads issued before round k is summed --
+// two rounds in flight per wave, 127 VGPRs: SST XXH3 image 0.682 -> 0.600,
+// same box; the other waves of the CU already cover the round trip.)
 template <bool PREVIEW>
 __device__ __forceinline__ void x3p_park(const X3WSpan& sp, uint32_t k0, uint32_t ke, const X3Row& X,
                                          ulonglong2 (*cs)[4]) {

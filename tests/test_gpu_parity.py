@@ -594,6 +594,28 @@ def test_xxh3_long_spans_in_pieces(gpu, oracle):
         assert got[i] == oracle.XXH3(host[o:o + n]), (i, o, n)
 
 
+@pytest.mark.parametrize("where", ["front", "middle", "back"])
+def test_empty_workgroup_shares(gpu, oracle, where):
+    """Batches whose bytes sit almost all in one span: the XXH3 wave driver's
+    byte-balanced shares (share_by_bytes) leave most workgroups an EMPTY
+    range, and the CRC kernels' count shares give the long span's workgroup
+    all the work -- both hashes must still cover every span exactly once."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(61)
+    small = [rnd.randrange(0, 400) for _ in range(300)]
+    big = 8 << 20
+    pos = {"front": 0, "middle": 150, "back": 300}[where]
+    lens = small[:pos] + [big] + small[pos:]
+    host, dev, offs, lens = make_batch(torch, 61, lens)
+    sp = spans(torch, S, dev, offs, lens)
+    got_x = u64(S.xxh3_64_batch(sp))
+    got_c = u32(S.crc32c_batch(sp))
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert got_x[i] == oracle.XXH3(host[o:o + n]), ("xxh3", i, o, n)
+        assert got_c[i] == oracle.Value(host[o:o + n]), ("crc", i, o, n)
+
+
 # ---- long spans / whole-file checksum (SURVEY.md 8f row 2) -----------------
 
 LONG_SIZES = [0, 1, 15, 16, 4095, 4096, 65535, 65536, 65537, 131072, 3 * 65536 + 5,
