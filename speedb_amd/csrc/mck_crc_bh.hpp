@@ -231,49 +231,35 @@ __device__ __forceinline__ void crc_bh_stage(const Op& op, const UShare& sh, uin
   __syncthreads();
 }
 
-// ---- one unit of work ---------------------------------------------------------
-// kind 2: round r of a body piece (rounds rhi down to rlo, wave-uniform);
-// kind 1: round q of a head batch (row values; R = the batch's rounds);
-// kind 0: nothing left.
-struct BhUnit {  // 64-bit fields first, no bools: copied whole, it must stay in registers
-  uint64_t ba1;         // body: the span's 16-aligned end
-  uint64_t hptr;        // head: the span's first byte (per row)
-  int32_t kind;
-  // body piece (wave-uniform)
-  uint32_t bt;          // window slot
-  int32_t r, rlo, rhi;  // current / last / first round of the piece (from the span end)
-  uint32_t bkt;
-  uint32_t binj;        // ~init at lane 0 of round rhi (h = 0, the span's first piece), else 0
-  uint32_t bparts;      // the span's parts (1: finish at once)
-  // head batch (per row; the rest of the head's geometry is derived, bh_hgeo)
-  uint32_t ht;          // window slot
-  uint32_t hlive;       // the row has a head in this batch
-  uint32_t hn;          // the SPAN's bytes
-  int32_t hrounds;      // 512-byte rounds of the head
-  uint32_t hinj;        // ~init, un-shifted by (hptr & 15): injected at the piece holding hptr
-  int32_t q, R;
-};
+// ---- units of work --------------------------------------------------------------
+// Tickets [0, HB) are head batches, the rest body pieces.  A wave runs two
+// loops, each with one unit loaded ahead of the one it folds: its head
+// batches, then -- from the first body ticket it draws, whose loads the head
+// loop's last iteration already issued -- its body pieces.  (One loop over
+// both kinds kept both kinds' state and branches live in every iteration:
+// ~60 more VALU and ~200 SALU per unit, SQ counters profiles/r4/prof1.)
 
-// 0: no unit
-__device__ __forceinline__ BhUnit bh_none() {
-  BhUnit u;
-  u.kind = 0;
-  u.bt = 0;
-  u.r = u.rlo = u.rhi = 0;
-  u.ba1 = 0;
-  u.bkt = 0;
-  u.binj = 0;
-  u.bparts = 1;
-  u.ht = 0;
-  u.hlive = 0;
-  u.hptr = 0;
-  u.hn = 0;
-  u.hrounds = 0;
-  u.hinj = 0;
-  u.q = 0;
-  u.R = 0;
-  return u;
-}
+// A head batch round: head 8 k + row of the list on 8-lane row `lane / 8`
+// (row values).
+struct BhHeadU {
+  uint64_t hptr;    // the span's first byte
+  uint32_t ht;      // window slot
+  uint32_t hlive;   // the row has a head in this batch
+  uint32_t hn;      // the SPAN's bytes
+  uint32_t hinj;    // ~init, un-shifted by (hptr & 15): injected at the piece holding hptr
+  int32_t hrounds;  // 512-byte rounds of the head
+  int32_t q, R;     // the batch's round / rounds (wave-uniform)
+};
+// A body piece: rounds rhi down to rlo of span slot bt (wave-uniform).
+struct BhBodyU {
+  uint64_t ba1;     // the span's 16-aligned end
+  uint32_t bt;
+  int32_t r, rlo, rhi;
+  uint32_t bkt;
+  uint32_t binj;    // ~init at lane 0 of round rhi (h = 0, the span's first piece), else 0
+  uint32_t bparts;  // the span's parts (1: finish at once)
+  uint32_t live;    // 0: no piece left
+};
 
 // A head's geometry: [ptr, a1 - kt) with a1 16-aligned -- the whole span
 // (F = 0) or the h bytes before its body -- in 512-byte rounds anchored at
@@ -299,97 +285,109 @@ __device__ __forceinline__ BhHead bh_hgeo(uint64_t ptr, uint32_t n, int32_t roun
   return x;
 }
 
-template <class Op>
-__device__ __forceinline__ BhUnit bh_take(const Op& op, uint64_t base, int kind, uint32_t nheads, uint32_t npieces,
-                                          uint32_t& tc, uint32_t lane) {
-  BhUnit u = bh_none();
-  const uint32_t k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
-  const uint32_t hb = (nheads + 7) >> 3;
-  if (k < hb) {  // head batch: row `lane / 8` takes head 8 k + row of the list
-    u.kind = 1;
-    const uint32_t e = 8 * k + (lane >> 3);
-    u.hlive = e < nheads ? 1u : 0u;
-    u.ht = *lds_p32(kBLdsHlist + 4 * (u.hlive ? e : 8 * k));
-    const uint4 d = bh_desc(u.ht);
-    const BhGeo x = bh_geo(base, d);
-    u.hptr = x.ptr;
-    u.hn = x.n;
-    // the head: the whole span (F = 0) or the h bytes before the body
-    const uint32_t cover = x.F ? x.h : (uint32_t)(x.a1 - x.ptr);  // > 0
-    u.hrounds = (int32_t)((cover + 511) >> 9);
-    const uint32_t hk = (uint32_t)x.ptr & 15u;  // = the owner's hb % 16 (chunks are 16-aligned)
-    u.hinj = kind == kInitArray ? crc_nibmap(kBLdsUnshift + hk * 512, ~d.w)
-                                : *lds_p32(kBLdsInj + 4 * ((kind == kInitTyped ? (d.w & 15u) * 16 : 0u) + hk));
-    uint32_t m = u.hlive ? (uint32_t)u.hrounds : 0u, R = 0;
+// Head batch k (< HB).
+__device__ __forceinline__ BhHeadU bh_head_of(uint32_t k, uint64_t base, int kind, uint32_t nheads, uint32_t lane) {
+  BhHeadU u;
+  const uint32_t e = 8 * k + (lane >> 3);
+  u.hlive = e < nheads ? 1u : 0u;
+  u.ht = *lds_p32(kBLdsHlist + 4 * (u.hlive ? e : 8 * k));
+  const uint4 d = bh_desc(u.ht);
+  const BhGeo x = bh_geo(base, d);
+  u.hptr = x.ptr;
+  u.hn = x.n;
+  // the head: the whole span (F = 0) or the h bytes before the body
+  const uint32_t cover = x.F ? x.h : (uint32_t)(x.a1 - x.ptr);  // > 0
+  u.hrounds = (int32_t)((cover + 511) >> 9);
+  const uint32_t hk = (uint32_t)x.ptr & 15u;  // = the owner's hb % 16 (chunks are 16-aligned)
+  u.hinj = kind == kInitArray ? crc_nibmap(kBLdsUnshift + hk * 512, ~d.w)
+                              : *lds_p32(kBLdsInj + 4 * ((kind == kInitTyped ? (d.w & 15u) * 16 : 0u) + hk));
+  uint32_t m = u.hlive ? (uint32_t)u.hrounds : 0u, R = 0;
 #pragma unroll
-    for (uint32_t rw = 0; rw < 8; rw++) R = max(R, readlane_u32(m, 8 * rw));
-    u.R = (int32_t)R;
-    u.q = 0;
-  } else if (k - hb < npieces) {  // body piece k - hb
-    u.kind = 2;
-    const uint32_t q = k - hb;
-    uint32_t v = bh_bpre(tc + 1 + lane);
-    uint32_t c0 = (uint32_t)__popcll(__ballot(v <= q));
-    while (c0 == 64) {
-      tc += 64;
-      v = bh_bpre(tc + 1 + lane);
-      c0 = (uint32_t)__popcll(__ballot(v <= q));
-    }
-    tc += c0;
-    u.bt = tc;
-    const uint4 d = bh_desc(tc);
-    const uint4 ds = make_uint4(rfl(d.x), rfl(d.y), rfl(d.z), rfl(d.w));
-    const BhGeo x = bh_geo(base, ds);
-    const uint32_t P = (x.F + 3) >> 2;
-    const uint32_t j = P - 1 - (q - rfl(bh_bpre(tc)));  // pieces in address order
-    u.rlo = (int32_t)(4 * j);
-    u.rhi = (int32_t)min(4 * j + 3, x.F - 1);
-    u.r = u.rhi;
-    u.ba1 = x.a1;
-    u.bkt = x.kt;
-    const bool first = j == P - 1 && x.h == 0;  // the span starts at this piece's first round
-    u.binj = first ? ~bh_init_of(kind, ds.w, *lds_p32(kBLdsInit + 4 * (ds.w & 15u))) : 0u;
-    u.bparts = P + (x.h != 0 ? 1u : 0u);
-  }
+  for (uint32_t rw = 0; rw < 8; rw++) R = max(R, readlane_u32(m, 8 * rw));
+  u.R = (int32_t)R;
+  u.q = 0;
   return u;
 }
 
-// The unit's loads (always 4 x 16 B per lane, so the waits stay exact).
-// Body: the row-transposed layout of the round (crc_load_chunk_rt), non-
-// temporal; head: lane c of a row the 64-byte chunk c of its round (the
-// pieces wholly before the head and idle rows read the zero piece).
-__device__ __forceinline__ Chunk bh_load(const BhUnit& u, uint32_t lane, uint64_t zp) {
-  Chunk ch;
-  if (u.kind == 2) {
-    const uint64_t b = u.ba1 - (uint64_t)kRoundBytes * (uint32_t)(u.r + 1) + 64ull * (lane & 15) + 16ull * (lane >> 4);
-#pragma unroll
-    for (int j = 0; j < 4; j++) ch.v[j] = span_load16<true>(b + 1024ull * j);
-  } else {
-    const uint32_t c = lane & 7;
-    const BhHead x = bh_hgeo(u.hptr, u.hn, u.hrounds);
-    const int32_t rr = u.hrounds - 1 - u.q;
-    const bool act = u.hlive && rr >= 0;
-    const uint64_t b = x.a1 - 512ull * (uint32_t)(rr + 1) + 64ull * c;
-    const int32_t rel = rr == u.hrounds - 1 ? (int32_t)((uint32_t)b - (uint32_t)x.a0) : 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) ch.v[j] = span_load16<false>((!act || rel < -16 * j) ? zp : b + 16ull * j);
+// Body piece q (q >= npieces: none); tc = the wave's search cursor (pieces
+// are drawn in increasing order, so the search only moves forward).
+__device__ __forceinline__ BhBodyU bh_body_of(uint32_t q, uint32_t npieces, uint64_t base, int kind, uint32_t& tc,
+                                              uint32_t lane) {
+  BhBodyU u;
+  u.live = q < npieces ? 1u : 0u;
+  u.bt = 0;
+  u.r = u.rlo = u.rhi = 0;
+  u.ba1 = 0;
+  u.bkt = 0;
+  u.binj = 0;
+  u.bparts = 1;
+  if (!u.live) return u;
+  uint32_t v = bh_bpre(tc + 1 + lane);
+  uint32_t c0 = (uint32_t)__popcll(__ballot(v <= q));
+  while (c0 == 64) {
+    tc += 64;
+    v = bh_bpre(tc + 1 + lane);
+    c0 = (uint32_t)__popcll(__ballot(v <= q));
   }
+  tc += c0;
+  u.bt = tc;
+  const uint4 d = bh_desc(tc);
+  const uint4 ds = make_uint4(rfl(d.x), rfl(d.y), rfl(d.z), rfl(d.w));
+  const BhGeo x = bh_geo(base, ds);
+  const uint32_t P = (x.F + 3) >> 2;
+  const uint32_t j = P - 1 - (q - rfl(bh_bpre(tc)));  // pieces in address order
+  u.rlo = (int32_t)(4 * j);
+  u.rhi = (int32_t)min(4 * j + 3, x.F - 1);
+  u.r = u.rhi;
+  u.ba1 = x.a1;
+  u.bkt = x.kt;
+  const bool first = j == P - 1 && x.h == 0;  // the span starts at this piece's first round
+  u.binj = first ? ~bh_init_of(kind, ds.w, *lds_p32(kBLdsInit + 4 * (ds.w & 15u))) : 0u;
+  u.bparts = P + (x.h != 0 ? 1u : 0u);
+  return u;
+}
+
+// Round r of a body piece: the row-transposed layout (crc_load_chunk_rt),
+// non-temporal; no piece left: the zero piece.
+__device__ __forceinline__ Chunk bh_load_body(const BhBodyU& u, uint32_t lane, uint64_t zp) {
+  Chunk ch;
+  const uint64_t b = u.ba1 - (uint64_t)kRoundBytes * (uint32_t)(u.r + 1) + 64ull * (lane & 15) + 16ull * (lane >> 4);
+#pragma unroll
+  for (int j = 0; j < 4; j++) ch.v[j] = span_load16<true>(u.live ? b + 1024ull * j : zp);
+  return ch;
+}
+// Round q of a head batch: lane c of a row the 64-byte chunk c of its
+// round (the pieces wholly before the head and idle rows read the zero
+// piece).
+__device__ __forceinline__ Chunk bh_load_head(const BhHeadU& u, uint32_t lane, uint64_t zp) {
+  Chunk ch;
+  const uint32_t c = lane & 7;
+  const BhHead x = bh_hgeo(u.hptr, u.hn, u.hrounds);
+  const int32_t rr = u.hrounds - 1 - u.q;
+  const bool act = u.hlive && rr >= 0;
+  const uint64_t b = x.a1 - 512ull * (uint32_t)(rr + 1) + 64ull * c;
+  const int32_t rel = rr == u.hrounds - 1 ? (int32_t)((uint32_t)b - (uint32_t)x.a0) : 0;
+#pragma unroll
+  for (int j = 0; j < 4; j++) ch.v[j] = span_load16<false>((!act || rel < -16 * j) ? zp : b + 16ull * j);
   return ch;
 }
 
-// Epilogue inputs of the unit's span(s): every part of a span loads the
-// span's own (Op::pre depends on the span only), so whichever part finishes
-// it has them.  Vector loads: the body's arguments are wave-uniform.
+// Epilogue inputs of a span: every part loads its span's own (Op::pre
+// depends on the span only), so whichever part finishes it has them.
+// Vector loads: a body's arguments are wave-uniform, and uniform loads
+// compile to scalar ones, which drop the low address bits.
 template <class Op>
-__device__ __forceinline__ typename Op::Pre bh_pre(const Op& op, bool body, uint32_t bt, uint32_t ht, uint64_t hptr,
-                                                   uint32_t hn, const UShare& sh, uint64_t base) {
-  const uint32_t t = body ? bt : ht;
-  const uint4 d = bh_desc(bt);
-  uint64_t ptr = body ? base + (((uint64_t)d.y << 32) | d.x) : hptr;
-  const uint32_t n = body ? d.z : hn;
-  uint32_t i = sh.idx(t);
+__device__ __forceinline__ typename Op::Pre bh_pre_body(const Op& op, const BhBodyU& u, const UShare& sh,
+                                                        uint64_t base) {
+  const uint4 d = bh_desc(u.bt);
+  uint64_t ptr = base + (((uint64_t)d.y << 32) | d.x);
+  uint32_t i = sh.idx(u.bt);
   asm volatile("" : "+v"(i), "+v"(ptr));
-  return op.pre(i, ptr, n);
+  return op.pre(i, ptr, d.z);
+}
+template <class Op>
+__device__ __forceinline__ typename Op::Pre bh_pre_head(const Op& op, const BhHeadU& u, const UShare& sh) {
+  return op.pre(sh.idx(u.ht), u.hptr, u.hn);
 }
 
 __device__ __forceinline__ uint32_t bh_unshift(uint32_t k, uint32_t s) { return crc_nibmap(kBLdsUnshift + k * 512, s); }
@@ -412,8 +410,8 @@ __device__ __forceinline__ uint32_t bh_pow_v(uint32_t p, uint32_t m) {
 
 // A body piece ends: p = its pure state at the piece end (wave-uniform).
 template <class Op>
-__device__ __forceinline__ void bh_body_end(const Op& op, const BhUnit& u, uint32_t p, const typename Op::Pre& pre,
-                                            const UShare& sh, uint64_t base, uint32_t lane) {
+__device__ __forceinline__ void bh_body_end(const Op& op, const BhBodyU& u, uint32_t p, const typename Op::Pre& pre,
+                                            const UShare& sh, uint32_t lane) {
   p = bh_pow_u(p, (uint32_t)u.rlo);  // the piece end is 4096 rlo bytes before a1
   if (u.bparts != 1) {
     uint32_t left = 0;
@@ -433,7 +431,7 @@ __device__ __forceinline__ void bh_body_end(const Op& op, const BhUnit& u, uint3
 // Head rows end (fin: the row's head ends in this round): p = the pure state
 // at the head end, in every lane of the row.
 template <class Op>
-__device__ __forceinline__ void bh_head_end(const Op& op, const BhUnit& u, uint32_t p, bool fin,
+__device__ __forceinline__ void bh_head_end(const Op& op, const BhHeadU& u, uint32_t p, bool fin,
                                             const typename Op::Pre& pre, const UShare& sh, uint32_t lane) {
   const bool lead = (lane & 7) == 0;
   const uint32_t F = (uint32_t)((((u.hptr + u.hn + 15) & ~15ull) - u.hptr) >> 12);
@@ -465,7 +463,7 @@ __device__ __forceinline__ void bh_head_end(const Op& op, const BhUnit& u, uint3
 }
 
 // One 512-byte round of the head batch (row values; q wave-uniform).
-__device__ __forceinline__ uint32_t bh_head_round(uint32_t s, Chunk ch, const BhUnit& u, uint32_t c, const CrcLane& L) {
+__device__ __forceinline__ uint32_t bh_head_round(uint32_t s, Chunk ch, const BhHeadU& u, uint32_t c, const CrcLane& L) {
   const BhHead hg = bh_hgeo(u.hptr, u.hn, u.hrounds);
   const int32_t rr = u.hrounds - 1 - u.q;
   const bool first = u.q == 0;  // every live row starts its head in the batch's first round
@@ -499,7 +497,7 @@ __device__ __forceinline__ uint32_t bh_head_round(uint32_t s, Chunk ch, const Bh
 }
 
 // One 4 KiB round of a body piece (chunk already row-transposed).
-__device__ __forceinline__ uint32_t bh_body_round(uint32_t s, Chunk ch, const BhUnit& u, uint32_t lane,
+__device__ __forceinline__ uint32_t bh_body_round(uint32_t s, Chunk ch, const BhBodyU& u, uint32_t lane,
                                                   const CrcLane& L) {
   const bool first = u.r == u.rhi;
   uint32_t x = first ? (lane == 0 ? u.binj : 0u) : crc_nibmap(kLdsGap, s);
@@ -519,42 +517,62 @@ __device__ __forceinline__ void crc_bh_window(const Op& op, const UShare& sh, ui
   const uint32_t lf4 = (56u + c) << 2;  // 8-lane rows: lane-final column 64 - 8 + c
   const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
   const uint32_t nheads = *lds_p32(kBLdsCtl + 4), npieces = *lds_p32(kBLdsCtl + 8);
+  const uint32_t HB = (nheads + 7) >> 3;
   typedef typename Op::Pre Pre;
   uint32_t tc = 0;
-  BhUnit u = bh_take(op, base, kind, nheads, npieces, tc, lane);
-  if (u.kind == 0) return;
-  Chunk cur = bh_load(u, lane, zp);
-  Pre pcur = bh_pre(op, u.kind == 2, u.bt, u.ht, u.hptr, u.hn, sh, base);
-  uint32_t s = 0;
-  for (;;) {
-    BhUnit nu;
-    if (u.kind == 2 && u.r > u.rlo) {
-      nu = u;
-      nu.r = u.r - 1;
-    } else if (u.kind == 1 && u.q + 1 < u.R) {
-      nu = u;
-      nu.q = u.q + 1;
-    } else {
-      nu = bh_take(op, base, kind, nheads, npieces, tc, lane);
-    }
-    // unconditional: the next unit's loads (the zero piece when none is left)
-    const Chunk nxt = bh_load(nu, lane, zp);
-    const bool nb = nu.kind ? nu.kind == 2 : u.kind == 2;
-    const Pre pnxt = bh_pre(op, nb, nu.kind ? nu.bt : u.bt, nu.kind ? nu.ht : u.ht, nu.kind ? nu.hptr : u.hptr,
-                            nu.kind ? nu.hn : u.hn, sh, base);
-    if (u.kind == 2) {
-      if (T) row_transpose(cur);
-      s = bh_body_round(s, cur, u, lane, L);
-      if (u.r == u.rlo) bh_body_end(op, u, wave_xor32(crc_lane_final(s, L)), pcur, sh, base, lane);
-    } else {
-      s = bh_head_round(s, cur, u, c, L);
+  uint32_t k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
+  if (k < HB) {
+    // ---- head batches ----
+    BhHeadU u = bh_head_of(k, base, kind, nheads, lane);
+    Chunk cur = bh_load_head(u, lane, zp);
+    Pre pcur = bh_pre_head(op, u, sh);
+    uint32_t hs = 0;  // the rows' states (a head's state carries over its rounds)
+    for (;;) {
+      BhHeadU nu = u;
+      bool nh = true;
+      if (u.q + 1 < u.R) {
+        nu.q = u.q + 1;
+      } else {
+        k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
+        nh = k < HB;
+        if (nh) nu = bh_head_of(k, base, kind, nheads, lane);
+        nu.hlive = nh ? nu.hlive : 0u;  // the last iteration loads the zero piece
+      }
+      const Chunk nxt = bh_load_head(nu, lane, zp);
+      const Pre pnxt = bh_pre_head(op, nu, sh);
+      hs = bh_head_round(hs, cur, u, c, L);
       const bool fin = u.hlive && u.hrounds - 1 - u.q == 0;
-      if (wave_any(fin)) bh_head_end(op, u, row_xor32<8>(crc_lane_final4(s, lf4)), fin, pcur, sh, lane);
+      if (wave_any(fin)) bh_head_end(op, u, row_xor32<8>(crc_lane_final4(hs, lf4)), fin, pcur, sh, lane);
+      if (!nh) break;
+      u = nu;
+      cur = nxt;
+      pcur = pnxt;
     }
-    if (nu.kind == 0) break;
-    u = nu;
-    cur = nxt;
-    pcur = pnxt;
+  }
+  // (ticket k >= HB: the wave's first body piece; its loads were not issued
+  // ahead -- one round trip per wave and window)
+  BhBodyU b = bh_body_of(k - HB, npieces, base, kind, tc, lane);
+  Chunk bcur = bh_load_body(b, lane, zp);
+  Pre bpre = bh_pre_body(op, b, sh, base);
+  // ---- body pieces ----
+  uint32_t s = 0;
+  while (b.live) {
+    BhBodyU nb = b;
+    if (b.r > b.rlo) {
+      nb.r = b.r - 1;
+    } else {
+      k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
+      nb = bh_body_of(k - HB, npieces, base, kind, tc, lane);
+    }
+    const Chunk nxt = bh_load_body(nb, lane, zp);
+    const Pre pnxt = b.r > b.rlo ? bpre : bh_pre_body(op, nb, sh, base);
+    Chunk cur = bcur;
+    if (T) row_transpose(cur);
+    s = bh_body_round(s, cur, b, lane, L);
+    if (b.r == b.rlo) bh_body_end(op, b, wave_xor32(crc_lane_final(s, L)), bpre, sh, lane);
+    b = nb;
+    bcur = nxt;
+    bpre = pnxt;
   }
 }
 
