@@ -24,10 +24,11 @@
 //   * pieces run on the wave driver's round (row-transposed non-temporal
 //     loads, 4 KiB in flight per wave, the 4032-byte gap map between rounds,
 //     the per-lane final shift and the wave XOR at the piece end);
-//   * heads run EIGHT AT A TIME, one per 8-lane row, on the row driver's
-//     round (512-byte rounds of 64-byte lane chunks anchored at the head's
-//     end, lanes before the head load the zero piece): one iteration per 8
-//     heads of <= 512 bytes instead of one per head;
+//   * heads run 16 or 64 AT A TIME, one per 4-lane row or per lane, on the
+//     row driver's round (256- or 64-byte rounds of 64-byte lane chunks
+//     anchored at the head's end, lanes before the head load the zero
+//     piece): one iteration per 16 heads of <= 256 bytes instead of one per
+//     head;
 //   * each part XORs its state, moved to a1 by zshift(4096 m) (nibble maps
 //     of 4096 * 2^b in LDS, one per set bit of m), into the span's LDS
 //     accumulator and decrements its part counter; the part that brings it
@@ -48,7 +49,7 @@
 // LDS image (160 KiB):
 //   [0, 32K)        per-lane final shift (kLdsFinal, as the wave driver)
 //   [32K, +512)     gap map 4032 (kLdsGap)
-//   then            8-lane row gap map (448 B), head / tail byte masks,
+//   then            row gap maps (W = 4, 8, 16), head / tail byte masks,
 //                   init injection tables, control words, zshift(4096 * 2^b)
 //                   maps, un-shift maps k < 16, the window's head list
 //   [64K, 128K)     the 4-byte step tables (kLdsStep, CrcLane)
@@ -66,15 +67,16 @@ struct UShare {
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 constexpr uint32_t kBNC = 1024;                          // spans per window (<= kCrcBlock)
-constexpr uint32_t kBLdsRowGap = kLdsGap + 512;          // zshift(., 64 * 7): 8-lane rows
-constexpr uint32_t kBLdsMaskHead = kBLdsRowGap + 512;    // [16] x 16 B: keep bytes >= h
+constexpr uint32_t kBLdsRowGap = kLdsGap + 512;          // [3] zshift(., 64 (W - 1)): W = 4, 8, 16-lane rows
+constexpr uint32_t kBLdsMaskHead = kBLdsRowGap + 1536;   // [16] x 16 B: keep bytes >= h
 constexpr uint32_t kBLdsMaskTail = kBLdsMaskHead + 256;  // [16] x 16 B: keep the first 16 - k
 constexpr uint32_t kBLdsInj = kBLdsMaskTail + 256;       // [16 types][16 k]: unshift(~init_t, k)
 constexpr uint32_t kBLdsInit = kBLdsInj + 1024;          // [16] init_t
-constexpr uint32_t kBLdsCtl = kBLdsInit + 64;            // ticket, nheads, npieces; wave sums
-constexpr uint32_t kBLdsWsum = kBLdsCtl + 16;            // u64 x 16 waves
+constexpr uint32_t kBLdsCtl = kBLdsInit + 64;            // ticket, nheads, npieces, head row width
+constexpr uint32_t kBLdsWsum = kBLdsCtl + 16;            // u64 x 16 waves: the scans' wave totals
+constexpr uint32_t kBLdsWsum2 = kBLdsWsum + 128;         // u64 x 16 waves: head bytes / heads
 constexpr uint32_t kBPowBits = 21;                       // 4096 * 2^b, b <= 20 (spans < 4 GiB)
-constexpr uint32_t kBLdsPow = kBLdsCtl + 256;            // [21][8][16]
+constexpr uint32_t kBLdsPow = kBLdsCtl + 512;            // [21][8][16]
 constexpr uint32_t kBLdsUnshift = kBLdsPow + kBPowBits * 512;  // [16][8][16]
 constexpr uint32_t kBLdsHlist = kBLdsUnshift + 16 * 512;       // u32 x kBNC
 static_assert(kBLdsHlist + 4 * kBNC <= kLdsStep, "BH low image overlaps the step tables");
@@ -107,8 +109,8 @@ __device__ __forceinline__ void crc_bh_fill(const Op& op, const CrcTables* __res
     const int i = (int)t + kCrcBlock * k;
     l[k] = lo[i < kLow ? i : 0];
   }
-  // row gap (32 slots), pow maps (b + 2 of pow1k: 672 slots), un-shift k < 16 (512)
-  const uint4 rg = reinterpret_cast<const uint4*>(&g->gap_row[1][0][0])[t < 32 ? t : 0];
+  // row gaps (96 slots), pow maps (b + 2 of pow1k: 672 slots), un-shift k < 16 (512)
+  const uint4 rg = reinterpret_cast<const uint4*>(&g->gap_row[0][0][0])[t < 96 ? t : 0];
   const uint4 pw = reinterpret_cast<const uint4*>(&g->pow1k[2][0][0])[t < kBPowBits * 32 ? t : 0];
   const uint4 us = reinterpret_cast<const uint4*>(&g->unshift[0][0][0])[t < 512 ? t : 0];
 #pragma unroll
@@ -125,7 +127,7 @@ __device__ __forceinline__ void crc_bh_fill(const Op& op, const CrcTables* __res
           span_u32x4{l[k].x, l[k].y, l[k].z, l[k].w};
   }
   typedef __attribute__((address_space(3))) span_u32x4 lds_u32x4_t;
-  if (t < 32) *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsRowGap + 16 * t)) = span_u32x4{rg.x, rg.y, rg.z, rg.w};
+  if (t < 96) *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsRowGap + 16 * t)) = span_u32x4{rg.x, rg.y, rg.z, rg.w};
   if (t < kBPowBits * 32)
     *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsPow + 16 * t)) = span_u32x4{pw.x, pw.y, pw.z, pw.w};
   if (t < 512) *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsUnshift + 16 * t)) = span_u32x4{us.x, us.y, us.z, us.w};
@@ -173,14 +175,27 @@ __device__ __forceinline__ BhGeo bh_geo(uint64_t base, const uint4& d) {
   return x;
 }
 
+// Head rows: W lanes per head, 64 W-byte rounds, 64 / W heads per batch
+// round.  A window takes one lane per head (64 heads a round) when 1.25x its
+// mean head fits 64 bytes -- blob records' 16-31-byte heads -- and 4-lane
+// rows (256-byte rounds, 16 heads) otherwise -- SST blocks' 0-272-byte
+// heads.  The head list puts the heads that fit one round before the
+// longer ones, so a batch of short heads is one round.  (8- and 16-lane
+// variants as well made the kernel spill: each width is a copy of the head
+// loop.)
+__device__ __forceinline__ uint32_t bh_head_w(uint32_t hbytes, uint32_t nheads) {
+  return 5ull * hbytes <= 256ull * nheads ? 1u : 4u;  // 1.25 x mean <= 64  <=>  5 sum <= 256 n
+}
+
 // Stage window slots [0, wn) = spans sh.idx(t): descriptors, accumulators
-// {0, parts}, the head list and the pieces' exclusive prefix (padded for the
-// ballot search); empty spans finish here (Extend(init, "") = init).  Ends
-// with a barrier; the totals are at kBLdsCtl + 4 / + 8.
+// {0, parts}, the head list (heads of one W-row round first) and the
+// pieces' exclusive prefix (padded for the ballot search); empty spans
+// finish here (Extend(init, "") = init).  Ends with a barrier; the totals
+// and W are at kBLdsCtl + 4 / + 8 / + 12.
 template <class Op>
 __device__ __forceinline__ void crc_bh_stage(const Op& op, const UShare& sh, uint32_t wn, uint64_t base, int kind) {
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6, nw = blockDim.x >> 6;
-  uint32_t hh = 0, P = 0;
+  uint32_t hh = 0, P = 0, hc = 0;
   if (t < wn) {
     const uint32_t i = sh.idx(t);
     const uint64_t off = op.off(i);
@@ -195,12 +210,26 @@ __device__ __forceinline__ void crc_bh_stage(const Op& op, const UShare& sh, uin
       op.finish(i, init, op.pre(i, x.ptr, 0), true);
     } else {
       hh = (x.F == 0 || x.h != 0) ? 1u : 0u;
+      hc = x.F ? x.h : (uint32_t)(x.a1 - x.ptr);  // the head's cover (when hh)
       P = (x.F + 3) >> 2;
     }
     *lds_p64(kBLdsAcc + 8 * t) = (uint64_t)(P + hh) << 32;
   }
-  // exclusive scans of (heads, pieces), packed: heads < 2^16 per window
-  const uint64_t v = ((uint64_t)P << 16) | hh;
+  // the window's head bytes and heads -> W
+  uint64_t hs = hh ? ((uint64_t)hc << 16) | 1u : 0ull;  // heads < 2^16, bytes < 2^40
+#pragma unroll
+  for (int dd = 32; dd >= 1; dd >>= 1)
+    hs += ((uint64_t)(uint32_t)__shfl_xor((int)(uint32_t)(hs >> 32), dd, 64) << 32) |
+          (uint32_t)__shfl_xor((int)(uint32_t)hs, dd, 64);
+  if (lane == 0) *lds_p64(kBLdsWsum2 + 8 * w) = hs;
+  __syncthreads();
+  uint64_t htot = 0;
+  for (uint32_t q = 0; q < nw; q++) htot += *lds_p64(kBLdsWsum2 + 8 * q);
+  const uint32_t W = bh_head_w((uint32_t)(htot >> 16), (uint32_t)(htot & 0xFFFFu));
+  const uint32_t one = hh && hc <= 64u * W ? 1u : 0u;  // the head fits one round
+  // exclusive scans of (pieces, long heads, one-round heads), packed:
+  // heads < 2^16 per window, pieces < 2^32
+  const uint64_t v = ((uint64_t)P << 32) | ((uint64_t)(hh - one) << 16) | one;
   uint64_t x = v;
 #pragma unroll
   for (int dd = 1; dd < 64; dd <<= 1) {
@@ -217,16 +246,18 @@ __device__ __forceinline__ void crc_bh_stage(const Op& op, const UShare& sh, uin
     tot += ws;
   }
   const uint64_t ex = below + x - v;
+  const uint32_t n1 = (uint32_t)(tot & 0xFFFFu), nl = (uint32_t)((tot >> 16) & 0xFFFFu);
   if (t < wn) {
-    *lds_p32(kBLdsBpre + 4 * t) = (uint32_t)(ex >> 16);
-    if (hh) *lds_p32(kBLdsHlist + 4 * (uint32_t)(ex & 0xFFFFu)) = t;
+    *lds_p32(kBLdsBpre + 4 * t) = (uint32_t)(ex >> 32);
+    if (hh) *lds_p32(kBLdsHlist + 4 * (one ? (uint32_t)(ex & 0xFFFFu) : n1 + (uint32_t)((ex >> 16) & 0xFFFFu))) = t;
   }
-  const uint32_t nheads = (uint32_t)(tot & 0xFFFFu), npieces = (uint32_t)(tot >> 16);
+  const uint32_t nheads = n1 + nl, npieces = (uint32_t)(tot >> 32);
   if (t <= 64) *lds_p32(kBLdsBpre + 4 * (wn + t)) = t ? 0xFFFFFFFFu : npieces;
   if (t == 0) {
     *lds_p32(kBLdsCtl) = 0;  // ticket
     *lds_p32(kBLdsCtl + 4) = nheads;
     *lds_p32(kBLdsCtl + 8) = npieces;
+    *lds_p32(kBLdsCtl + 12) = W;
   }
   __syncthreads();
 }
@@ -239,15 +270,15 @@ __device__ __forceinline__ void crc_bh_stage(const Op& op, const UShare& sh, uin
 // both kinds kept both kinds' state and branches live in every iteration:
 // ~60 more VALU and ~200 SALU per unit, SQ counters profiles/r4/prof1.)
 
-// A head batch round: head 8 k + row of the list on 8-lane row `lane / 8`
-// (row values).
+// A head batch round: head (64 / W) k + row of the list on W-lane row
+// `lane / W` (row values).
 struct BhHeadU {
   uint64_t hptr;    // the span's first byte
   uint32_t ht;      // window slot
   uint32_t hlive;   // the row has a head in this batch
   uint32_t hn;      // the SPAN's bytes
   uint32_t hinj;    // ~init, un-shifted by (hptr & 15): injected at the piece holding hptr
-  int32_t hrounds;  // 512-byte rounds of the head
+  int32_t hrounds;  // 64 W-byte rounds of the head
   int32_t q, R;     // the batch's round / rounds (wave-uniform)
 };
 // A body piece: rounds rhi down to rlo of span slot bt (wave-uniform).
@@ -262,7 +293,7 @@ struct BhBodyU {
 };
 
 // A head's geometry: [ptr, a1 - kt) with a1 16-aligned -- the whole span
-// (F = 0) or the h bytes before its body -- in 512-byte rounds anchored at
+// (F = 0) or the h bytes before its body -- in 64 W-byte rounds anchored at
 // a1; `owner` = the row lane whose first-round chunk holds ptr, hb = ptr -
 // that chunk's start.
 struct BhHead {
@@ -271,6 +302,7 @@ struct BhHead {
   int32_t owner;
   uint32_t hb;
 };
+template <int W>
 __device__ __forceinline__ BhHead bh_hgeo(uint64_t ptr, uint32_t n, int32_t rounds) {
   BhHead x;
   x.a0 = ptr & ~15ull;
@@ -279,32 +311,35 @@ __device__ __forceinline__ BhHead bh_hgeo(uint64_t ptr, uint32_t n, int32_t roun
   x.a1 = a1 - ((uint64_t)x.F << 12);
   x.kt = x.F ? 0u : (uint32_t)(a1 - (ptr + n));
   x.cover = (uint32_t)(x.a1 - ptr);
-  const uint32_t lead = 512u * (uint32_t)rounds - x.cover;
+  const uint32_t lead = 64u * W * (uint32_t)rounds - x.cover;
   x.owner = (int32_t)(lead >> 6);
   x.hb = lead & 63u;
   return x;
 }
 
-// Head batch k (< HB).
+// Head batch k (< HB): head (64 / W) k + row of the list on W-lane row
+// `lane / W`.
+template <int W>
 __device__ __forceinline__ BhHeadU bh_head_of(uint32_t k, uint64_t base, int kind, uint32_t nheads, uint32_t lane) {
   BhHeadU u;
-  const uint32_t e = 8 * k + (lane >> 3);
+  constexpr uint32_t NB = 64 / W;
+  const uint32_t e = NB * k + lane / W;
   u.hlive = e < nheads ? 1u : 0u;
-  u.ht = *lds_p32(kBLdsHlist + 4 * (u.hlive ? e : 8 * k));
+  u.ht = *lds_p32(kBLdsHlist + 4 * (u.hlive ? e : NB * k));
   const uint4 d = bh_desc(u.ht);
   const BhGeo x = bh_geo(base, d);
   u.hptr = x.ptr;
   u.hn = x.n;
   // the head: the whole span (F = 0) or the h bytes before the body
   const uint32_t cover = x.F ? x.h : (uint32_t)(x.a1 - x.ptr);  // > 0
-  u.hrounds = (int32_t)((cover + 511) >> 9);
+  u.hrounds = (int32_t)((cover + 64 * W - 1) / (64 * W));
   const uint32_t hk = (uint32_t)x.ptr & 15u;  // = the owner's hb % 16 (chunks are 16-aligned)
   u.hinj = kind == kInitArray ? crc_nibmap(kBLdsUnshift + hk * 512, ~d.w)
                               : *lds_p32(kBLdsInj + 4 * ((kind == kInitTyped ? (d.w & 15u) * 16 : 0u) + hk));
-  uint32_t m = u.hlive ? (uint32_t)u.hrounds : 0u, R = 0;
+  uint32_t R = u.hlive ? (uint32_t)u.hrounds : 0u;  // the batch's rounds: the wave max
 #pragma unroll
-  for (uint32_t rw = 0; rw < 8; rw++) R = max(R, readlane_u32(m, 8 * rw));
-  u.R = (int32_t)R;
+  for (int dd = 32; dd >= 1; dd >>= 1) R = max(R, (uint32_t)__shfl_xor((int)R, dd, 64));
+  u.R = (int32_t)rfl(R);
   u.q = 0;
   return u;
 }
@@ -359,13 +394,14 @@ __device__ __forceinline__ Chunk bh_load_body(const BhBodyU& u, uint32_t lane, u
 // Round q of a head batch: lane c of a row the 64-byte chunk c of its
 // round (the pieces wholly before the head and idle rows read the zero
 // piece).
+template <int W>
 __device__ __forceinline__ Chunk bh_load_head(const BhHeadU& u, uint32_t lane, uint64_t zp) {
   Chunk ch;
-  const uint32_t c = lane & 7;
-  const BhHead x = bh_hgeo(u.hptr, u.hn, u.hrounds);
+  const uint32_t c = lane & (W - 1);
+  const BhHead x = bh_hgeo<W>(u.hptr, u.hn, u.hrounds);
   const int32_t rr = u.hrounds - 1 - u.q;
   const bool act = u.hlive && rr >= 0;
-  const uint64_t b = x.a1 - 512ull * (uint32_t)(rr + 1) + 64ull * c;
+  const uint64_t b = x.a1 - 64ull * W * (uint32_t)(rr + 1) + 64ull * c;
   const int32_t rel = rr == u.hrounds - 1 ? (int32_t)((uint32_t)b - (uint32_t)x.a0) : 0;
 #pragma unroll
   for (int j = 0; j < 4; j++) ch.v[j] = span_load16<false>((!act || rel < -16 * j) ? zp : b + 16ull * j);
@@ -430,10 +466,10 @@ __device__ __forceinline__ void bh_body_end(const Op& op, const BhBodyU& u, uint
 
 // Head rows end (fin: the row's head ends in this round): p = the pure state
 // at the head end, in every lane of the row.
-template <class Op>
-__device__ __forceinline__ void bh_head_end(const Op& op, const BhHeadU& u, uint32_t p, bool fin,
-                                            const typename Op::Pre& pre, const UShare& sh, uint32_t lane) {
-  const bool lead = (lane & 7) == 0;
+template <int W, class Op>
+__device__ __forceinline__ void bh_head_end(const Op& op, const BhHeadU& u, uint32_t p, bool fin, const UShare& sh,
+                                            uint32_t lane) {
+  const bool lead = (lane & (W - 1)) == 0;
   const uint32_t F = (uint32_t)((((u.hptr + u.hn + 15) & ~15ull) - u.hptr) >> 12);
   const bool direct = F == 0;  // the head is the whole span
   bool done = fin && direct;
@@ -448,29 +484,34 @@ __device__ __forceinline__ void bh_head_end(const Op& op, const BhHeadU& u, uint
                                     __HIP_MEMORY_SCOPE_WORKGROUP);
       if (left == 1) p = __hip_atomic_load(lds_p32(kBLdsAcc + 8 * u.ht), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    // the row leader's values to its row
-    const int src = (int)((lane & ~7u) << 2);
-    left = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)left);
-    const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)p);
-    p = part ? pl : p;
+    if constexpr (W > 1) {  // the row leader's values to its row
+      const int src = (int)((lane & ~(uint32_t)(W - 1)) << 2);
+      left = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)left);
+      const uint32_t pl = (uint32_t)__builtin_amdgcn_ds_bpermute(src, (int)p);
+      p = part ? pl : p;
+    }
     done = done || (part && left == 1);
   }
   if (!wave_any(done)) return;
   const uint32_t kt = (uint32_t)(0u - (uint32_t)(u.hptr + u.hn)) & 15u;
   const uint32_t x = bh_unshift(kt, p);
   p = kt ? x : p;
-  op.finish(sh.idx(u.ht), ~p, pre, done && lead);
+  // the epilogue inputs only now: heads run before the bodies, so a head
+  // finishes its span mostly when it IS the span (no prefetch registers
+  // through the head loop)
+  op.finish(sh.idx(u.ht), ~p, bh_pre_head(op, u, sh), done && lead);
 }
 
-// One 512-byte round of the head batch (row values; q wave-uniform).
+// One 64 W-byte round of the head batch (row values; q wave-uniform).
+template <int W>
 __device__ __forceinline__ uint32_t bh_head_round(uint32_t s, Chunk ch, const BhHeadU& u, uint32_t c, const CrcLane& L) {
-  const BhHead hg = bh_hgeo(u.hptr, u.hn, u.hrounds);
+  const BhHead hg = bh_hgeo<W>(u.hptr, u.hn, u.hrounds);
   const int32_t rr = u.hrounds - 1 - u.q;
   const bool first = u.q == 0;  // every live row starts its head in the batch's first round
   const bool own = (int32_t)c == hg.owner;
   const uint32_t h0 = (uint32_t)u.hptr & 15u;
   const uint4 mh = lds_u32x4(kBLdsMaskHead + 16 * h0);
-  const uint4 mt = lds_u32x4(kBLdsMaskTail + 16 * ((rr == 0 && c == 7) ? hg.kt : 0u));
+  const uint4 mt = lds_u32x4(kBLdsMaskTail + 16 * ((rr == 0 && c == W - 1) ? hg.kt : 0u));
   const uint32_t pa = (first && own) ? hg.hb >> 4 : 4u;
   uint32_t sels[4];
 #pragma unroll
@@ -483,7 +524,11 @@ __device__ __forceinline__ uint32_t bh_head_round(uint32_t s, Chunk ch, const Bh
     ch.v[j].w = __builtin_amdgcn_bitop3_b32(ch.v[j].w, mh.w, sel, 0xD0);
   }
   and4(ch.v[3], mt);
-  const uint32_t gap = first ? 0u : crc_nibmap(kBLdsRowGap, s);
+  // a lane's next chunk is 64 W bytes on: zshift(., 64 (W - 1)) after its
+  // own 64 (W = 1: adjacent, the state carries over)
+  uint32_t gap = s;
+  if constexpr (W > 1) gap = crc_nibmap(kBLdsRowGap + 512u * (W == 4 ? 0u : W == 8 ? 1u : 2u), s);
+  gap = first ? 0u : gap;
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&ch.v[0]);
   const uint32_t inj = u.hinj;
   uint32_t x = gap ^ w[0] ^ (sels[0] & inj);
@@ -509,45 +554,58 @@ __device__ __forceinline__ uint32_t bh_body_round(uint32_t s, Chunk ch, const Bh
   return x;
 }
 
+// The wave's head batches, from its first ticket k (< HB); returns the first
+// ticket past them.
+template <int W, class Op>
+__device__ __forceinline__ uint32_t crc_bh_heads(const Op& op, const UShare& sh, uint64_t base, uint64_t zp, uint32_t k,
+                                                 uint32_t HB, uint32_t nheads, const CrcLane& L) {
+  const int kind = op.init_kind();
+  const uint32_t lane = threadIdx.x & 63, c = lane & (W - 1);
+  const uint32_t lf4 = (64u - W + c) << 2;  // lane-final column 64 - W + c: zshift(., 64 (W - 1 - c))
+  BhHeadU u = bh_head_of<W>(k, base, kind, nheads, lane);
+  Chunk cur = bh_load_head<W>(u, lane, zp);
+  uint32_t hs = 0;  // the rows' states (a head's state carries over its rounds)
+  for (;;) {
+    BhHeadU nu = u;
+    bool nh = true;
+    if (u.q + 1 < u.R) {
+      nu.q = u.q + 1;
+    } else {
+      k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
+      nh = k < HB;
+      if (nh) nu = bh_head_of<W>(k, base, kind, nheads, lane);
+      nu.hlive = nh ? nu.hlive : 0u;  // the last iteration loads the zero piece
+    }
+    const Chunk nxt = bh_load_head<W>(nu, lane, zp);
+    hs = bh_head_round<W>(hs, cur, u, c, L);
+    const bool fin = u.hlive && u.hrounds - 1 - u.q == 0;
+    if (wave_any(fin)) {
+      uint32_t p = hs;  // W = 1: the lane's state is its head's
+      if constexpr (W > 1) p = row_xor32<W>(crc_lane_final4(hs, lf4));
+      bh_head_end<W>(op, u, p, fin, sh, lane);
+    }
+    if (!nh) return k;
+    u = nu;
+    cur = nxt;
+  }
+}
+
 template <class Op, bool T>
 __device__ __forceinline__ void crc_bh_window(const Op& op, const UShare& sh, uint64_t base, const CrcTables* __restrict__ g) {
   const int kind = op.init_kind();
   const CrcLane L = crc_lane();
-  const uint32_t lane = threadIdx.x & 63, c = lane & 7;
-  const uint32_t lf4 = (56u + c) << 2;  // 8-lane rows: lane-final column 64 - 8 + c
+  const uint32_t lane = threadIdx.x & 63;
   const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
-  const uint32_t nheads = *lds_p32(kBLdsCtl + 4), npieces = *lds_p32(kBLdsCtl + 8);
-  const uint32_t HB = (nheads + 7) >> 3;
+  const uint32_t nheads = *lds_p32(kBLdsCtl + 4), npieces = *lds_p32(kBLdsCtl + 8), W = *lds_p32(kBLdsCtl + 12);
+  const uint32_t HB = (nheads + 64 / W - 1) / (64 / W);
   typedef typename Op::Pre Pre;
   uint32_t tc = 0;
   uint32_t k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
-  if (k < HB) {
-    // ---- head batches ----
-    BhHeadU u = bh_head_of(k, base, kind, nheads, lane);
-    Chunk cur = bh_load_head(u, lane, zp);
-    Pre pcur = bh_pre_head(op, u, sh);
-    uint32_t hs = 0;  // the rows' states (a head's state carries over its rounds)
-    for (;;) {
-      BhHeadU nu = u;
-      bool nh = true;
-      if (u.q + 1 < u.R) {
-        nu.q = u.q + 1;
-      } else {
-        k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
-        nh = k < HB;
-        if (nh) nu = bh_head_of(k, base, kind, nheads, lane);
-        nu.hlive = nh ? nu.hlive : 0u;  // the last iteration loads the zero piece
-      }
-      const Chunk nxt = bh_load_head(nu, lane, zp);
-      const Pre pnxt = bh_pre_head(op, nu, sh);
-      hs = bh_head_round(hs, cur, u, c, L);
-      const bool fin = u.hlive && u.hrounds - 1 - u.q == 0;
-      if (wave_any(fin)) bh_head_end(op, u, row_xor32<8>(crc_lane_final4(hs, lf4)), fin, pcur, sh, lane);
-      if (!nh) break;
-      u = nu;
-      cur = nxt;
-      pcur = pnxt;
-    }
+  if (k < HB) {  // head batches (W wave-uniform)
+    if (W == 1)
+      k = crc_bh_heads<1>(op, sh, base, zp, k, HB, nheads, L);
+    else
+      k = crc_bh_heads<4>(op, sh, base, zp, k, HB, nheads, L);
   }
   // (ticket k >= HB: the wave's first body piece; its loads were not issued
   // ahead -- one round trip per wave and window)
