@@ -252,11 +252,11 @@ def cpu_baseline(args, kind, block, sample, gpu_results):
 
 
 def _ragged(op, mean_len):
-    """The kernel that does a ragged CRC batch's work: k_crc_bh (body/head
-    driver) for spans averaging more than 2.5 KiB, k_crc_auto (row drivers)
-    otherwise -- both are launched, once each, and the other exits at once;
-    the HIP-event kernel time covers both."""
-    return f"mck::k_crc_bh<{op}, true>" if mean_len > 2560 else f"mck::k_crc_auto<{op}, true, true>"
+    """The kernel that does a ragged CRC batch's work: k_crc_ragged, one
+    launch; its workgroups run the body/head driver for spans averaging more
+    than 2.5 KiB, the row drivers otherwise (mean_len: the label once named
+    the kernel per driver)."""
+    return f"mck::k_crc_ragged<{op}, true, true>"
 
 
 def C_wal_verify(im, nblocks, stream):

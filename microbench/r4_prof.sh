@@ -13,12 +13,15 @@ declare -A ARGS=(
   [r16k]="--workload ragged --span-min 16384 --span-max 65536 --span-bytes $((4 << 30))"
   [sstc]="--workload sst --sst-types crc32c"
   [blob]="--workload blob"
+  [r4096]="--workload ragged --span-min 4096 --span-max 4096 --span-bytes $((4 << 30))"
+  [walrec]="--workload walrec"
+  [u4300]="--workload crc32c --block-bytes 4300 --blocks 1000000"
 )
 PA="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
 PB="SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SMEM"
 PC="TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE"
 for wl in ${PROF_WL:-r4100 r16k}; do
-  for v in r3base new; do
+  for v in ${PROF_VARIANTS:-r3base new}; do
     if [ $v = r3base ]; then E="SPEEDB_AMD_LIB=$V/r3base.so"; else E="-u SPEEDB_AMD_LIB"; fi
     d=$O/${wl}_$v
     mkdir -p $d

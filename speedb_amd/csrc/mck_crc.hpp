@@ -1035,16 +1035,15 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, const RowShare& sh, 
 }
 
 // ---------------------------------------------------------------------------
-// Ragged batches: two kernels over the whole batch, same grid, same
-// contiguous shares -- k_crc_auto (the row drivers, below) and k_crc_bh (the
-// body/head driver, mck_crc_bh.hpp) -- and every workgroup takes its share
-// in exactly one of them: the row drivers when the share's spans average at
-// most kAutoLongMin bytes, else the body/head driver.  The choice is made
-// from a fixed sample of the share's lengths (crc_share_long), the same
-// deterministic answer in both kernels.  (The host cannot choose: ragged
+// Ragged batches: one kernel over the whole batch (k_crc_ragged), contiguous
+// shares, and every workgroup runs its share on the row drivers (below) when
+// the share's spans average at most kAutoLongMin bytes, else on the
+// body/head driver (mck_crc_bh.hpp).  The choice is made from a fixed sample
+// of the share's lengths (crc_share_long).  (The host cannot choose: ragged
 // lengths live on the device.)
 constexpr uint32_t kAutoLongMin = 2560;    // mean span bytes
 constexpr uint32_t kAutoRows1Max = 80;     // one lane per span below ~80 B
+constexpr uint32_t kAutoRows4Max = 384;    // 4-lane rows up to 384 B
 constexpr uint32_t kAutoRows8Max = 640;    // 8-lane rows up to 640 B, 16-lane rows above
 template <class Op>
 __device__ __forceinline__ bool crc_share_long(const Op& op, const RowShare& sh) {
@@ -1060,8 +1059,9 @@ __device__ __forceinline__ bool crc_share_long(const Op& op, const RowShare& sh)
 // (one launch per batch; the table image is filled once).  The width is
 // chosen once per share, from its first window's mean span: one lane per
 // span below ~80 B (20-100 B: 0.16-0.19 vs 0.09 of peak on 8-lane rows,
-// whose 512-B rounds are mostly padding there), 8-lane rows up to 640 B,
-// 16-lane rows above.  (The window loop sits inside each width's branch: a
+// whose 512-B rounds are mostly padding there), 4-lane rows up to 384 B
+// (100-300-B spans 0.365 vs 0.345 on 8-lane rows; 300-700 B 0.427 vs 0.444,
+// profiles/r4/rows), 8-lane rows up to 640 B, 16-lane rows above.  (The window loop sits inside each width's branch: a
 // loop around all four widths kept every width's lane constants live and
 // spilled 76-132 B per lane.)  force: 0 = by length, 2 = rows16, 3 = rows8,
 // 5 = rows4, 6 = one lane per span (test hook).
@@ -1088,7 +1088,11 @@ __device__ __forceinline__ void crc_rows_windows(const Op& op, const RowShare& s
   const RowShare sh0{share.start, share.stride, (uint32_t)((uint64_t)n / nwin)};
   crc_rows_prologue<Op>(op, sh0, lds, g, true);
   const uint64_t mean = *lds_p64(kLdsRowTotal) / sh0.n;
-  const int mode = force ? force : mean <= kAutoRows1Max ? 6 : mean <= kAutoRows8Max ? 3 : 2;
+  const int mode = force ? force
+                         : mean <= kAutoRows1Max ? 6
+                         : mean <= kAutoRows4Max ? 5
+                         : mean <= kAutoRows8Max ? 3
+                                                 : 2;
   if (mode == 6)
     crc_rows_windows_w<Op, 1>(op, share, nwin, g);
   else if (mode == 5)

@@ -16,9 +16,9 @@
 // a1, HEAD = the h = cover % 4096 bytes before them (the whole span when
 // F = 0).  CRC-32C is linear (util/crc32c.cc:1221-1266, Crc32cCombine): the
 // span's pure state at a1 is
-//     zshift(head state, 4096 F)  ^  XOR_j zshift(piece j state, 16384 j)
-// where the body is cut into PIECES of at most 4 rounds anchored at a1
-// (piece j = rounds 4j .. 4j + 3 counted from the end).  ~init is injected
+//     zshift(head state, 4096 F)  ^  XOR_j zshift(piece j state, 4096 R j)
+// where the body is cut into PIECES of at most R = kBhPieceRounds rounds
+// anchored at a1 (piece j = rounds R j .. R j + R - 1 counted from the end).  ~init is injected
 // at ptr (in the head; in the body's first round when h = 0) and the < 16
 // bytes past the end are masked and un-shifted at the end, as in crc_drive.
 //   * pieces run on the wave driver's round (row-transposed non-temporal
@@ -67,6 +67,7 @@ struct UShare {
 __device__ __forceinline__ uint32_t rfl(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
 
 constexpr uint32_t kBNC = 1024;                          // spans per window (<= kCrcBlock)
+constexpr uint32_t kBhPieceRounds = 4;                   // 4 KiB rounds per body piece
 constexpr uint32_t kBLdsRowGap = kLdsGap + 512;          // [3] zshift(., 64 (W - 1)): W = 4, 8, 16-lane rows
 constexpr uint32_t kBLdsMaskHead = kBLdsRowGap + 1536;   // [16] x 16 B: keep bytes >= h
 constexpr uint32_t kBLdsMaskTail = kBLdsMaskHead + 256;  // [16] x 16 B: keep the first 16 - k
@@ -211,7 +212,7 @@ __device__ __forceinline__ void crc_bh_stage(const Op& op, const UShare& sh, uin
     } else {
       hh = (x.F == 0 || x.h != 0) ? 1u : 0u;
       hc = x.F ? x.h : (uint32_t)(x.a1 - x.ptr);  // the head's cover (when hh)
-      P = (x.F + 3) >> 2;
+      P = (x.F + kBhPieceRounds - 1) / kBhPieceRounds;
     }
     *lds_p64(kBLdsAcc + 8 * t) = (uint64_t)(P + hh) << 32;
   }
@@ -369,10 +370,10 @@ __device__ __forceinline__ BhBodyU bh_body_of(uint32_t q, uint32_t npieces, uint
   const uint4 d = bh_desc(tc);
   const uint4 ds = make_uint4(rfl(d.x), rfl(d.y), rfl(d.z), rfl(d.w));
   const BhGeo x = bh_geo(base, ds);
-  const uint32_t P = (x.F + 3) >> 2;
+  const uint32_t P = (x.F + kBhPieceRounds - 1) / kBhPieceRounds;
   const uint32_t j = P - 1 - (q - rfl(bh_bpre(tc)));  // pieces in address order
-  u.rlo = (int32_t)(4 * j);
-  u.rhi = (int32_t)min(4 * j + 3, x.F - 1);
+  u.rlo = (int32_t)(kBhPieceRounds * j);
+  u.rhi = (int32_t)min(kBhPieceRounds * j + kBhPieceRounds - 1, x.F - 1);
   u.r = u.rhi;
   u.ba1 = x.a1;
   u.bkt = x.kt;
@@ -554,6 +555,50 @@ __device__ __forceinline__ uint32_t bh_body_round(uint32_t s, Chunk ch, const Bh
   return x;
 }
 
+// ---- the body loop ----------------------------------------------------------------
+template <class Op>
+struct BhCtx {
+  const Op& op;
+  const UShare& sh;
+  uint64_t base, zp;
+  uint32_t HB, npieces;
+  int kind;
+  uint32_t lane;
+  const CrcLane& L;
+};
+// The unit after b: its next round, or the next piece drawn (none after none).
+template <class Op>
+__device__ __forceinline__ BhBodyU bh_next_body(const BhCtx<Op>& x, uint32_t& tc, const BhBodyU& b) {
+  BhBodyU n = b;
+  if (!b.live) return n;  // wave-uniform
+  if (b.r > b.rlo) {
+    n.r = b.r - 1;
+    return n;
+  }
+  const uint32_t k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
+  return bh_body_of(k - x.HB, x.npieces, x.base, x.kind, tc, x.lane);
+}
+// n's epilogue inputs: b's when n is b's next round
+template <class Op>
+__device__ __forceinline__ typename Op::Pre bh_pre_next(const BhCtx<Op>& x, const BhBodyU& b, const BhBodyU& n,
+                                                        const typename Op::Pre& pb) {
+  if (b.live && b.r > b.rlo) return pb;  // wave-uniform
+  return bh_pre_body(x.op, n, x.sh, x.base);
+}
+// Fold round A (loaded); issue B = next(A).  Returns B.live.
+template <class Op, bool T>
+__device__ __forceinline__ bool bh_body_step(const BhCtx<Op>& x, uint32_t& tc, const BhBodyU& bA, BhBodyU& bB,
+                                             const Chunk& cA, Chunk& cB, const typename Op::Pre& pA,
+                                             typename Op::Pre& pB, uint32_t& s) {
+  bB = bh_next_body(x, tc, bA);
+  cB = bh_load_body(bB, x.lane, x.zp);
+  pB = bh_pre_next(x, bA, bB, pA);
+  Chunk cur = cA;
+  if (T) row_transpose(cur);
+  s = bh_body_round(s, cur, bA, x.lane, x.L);
+  if (bA.r == bA.rlo) bh_body_end(x.op, bA, wave_xor32(crc_lane_final(s, x.L)), pA, x.sh, x.lane);
+  return bB.live != 0;
+}
 // The wave's head batches, from its first ticket k (< HB); returns the first
 // ticket past them.
 template <int W, class Op>
@@ -607,30 +652,25 @@ __device__ __forceinline__ void crc_bh_window(const Op& op, const UShare& sh, ui
     else
       k = crc_bh_heads<4>(op, sh, base, zp, k, HB, nheads, L);
   }
+  // ---- body pieces ----
   // (ticket k >= HB: the wave's first body piece; its loads were not issued
   // ahead -- one round trip per wave and window)
-  BhBodyU b = bh_body_of(k - HB, npieces, base, kind, tc, lane);
-  Chunk bcur = bh_load_body(b, lane, zp);
-  Pre bpre = bh_pre_body(op, b, sh, base);
-  // ---- body pieces ----
+  const BhCtx<Op> x{op, sh, base, zp, HB, npieces, kind, lane, L};
+  BhBodyU b0 = bh_body_of(k - HB, npieces, base, kind, tc, lane);
+  if (!b0.live) return;
+  Chunk c0 = bh_load_body(b0, lane, zp);
+  Pre p0 = bh_pre_body(op, b0, sh, base);
   uint32_t s = 0;
-  while (b.live) {
-    BhBodyU nb = b;
-    if (b.r > b.rlo) {
-      nb.r = b.r - 1;
-    } else {
-      k = rfl(lds_ticket(lds_p32(kBLdsCtl)));
-      nb = bh_body_of(k - HB, npieces, base, kind, tc, lane);
-    }
-    const Chunk nxt = bh_load_body(nb, lane, zp);
-    const Pre pnxt = b.r > b.rlo ? bpre : bh_pre_body(op, nb, sh, base);
-    Chunk cur = bcur;
-    if (T) row_transpose(cur);
-    s = bh_body_round(s, cur, b, lane, L);
-    if (b.r == b.rlo) bh_body_end(op, b, wave_xor32(crc_lane_final(s, L)), bpre, sh, lane);
-    b = nb;
-    bcur = nxt;
-    bpre = pnxt;
+  // the loop unrolled twice: the loaded round and the one in flight swap
+  // register names instead of 16 v_mov per round (ragged 4096-B spans 0.775
+  // -> 0.828, 4100-4400 B 0.679 -> 0.715, same box; two rounds in flight per
+  // wave, unrolled three times, measured the same: 0.828 / 0.719)
+  BhBodyU b1;
+  Chunk c1;
+  Pre p1;
+  for (;;) {
+    if (!bh_body_step<Op, T>(x, tc, b0, b1, c0, c1, p0, p1, s)) break;
+    if (!bh_body_step<Op, T>(x, tc, b1, b0, c1, c0, p1, p0, s)) break;
   }
 }
 

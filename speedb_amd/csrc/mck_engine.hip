@@ -225,14 +225,15 @@ SpanSrc to_src(const mck_spans* s) {
 // 64 KiB 74.7 -> 83.4 %).
 constexpr bool kCrcGenericT = true;
 
-// Ragged batches: k_crc_auto (row drivers) and k_crc_bh (body/head driver)
-// are both launched over the whole batch with the same grid and contiguous
-// shares; each workgroup works in exactly one of them, chosen on the device
-// from a sample of its share's lengths (crc_share_long: the host cannot see
-// device-resident lengths).  One launch each, whatever the batch size (both
-// walk their shares in LDS windows).  Tests force one driver / the
-// interleaved order through mck_test_set_crc_driver; production code never
-// calls it.
+// Ragged batches: one launch of k_crc_ragged over the whole batch; each
+// workgroup runs its contiguous share on the row drivers or the body/head
+// driver, chosen on the device from a sample of the share's lengths
+// (crc_share_long: the host cannot see device-resident lengths).  Both walk
+// their shares in LDS windows, so one launch serves any batch size.  (Round
+// 4 first launched the two drivers as two kernels over the same shares: the
+// one with nothing to do still cost ~5 us per batch, 2.5 % of a 1 GiB SST
+// image.)  Tests force one driver / the interleaved order through
+// mck_test_set_crc_driver; production code never calls it.
 std::atomic<int> g_crc_force{0}, g_crc_interleaved{0};
 int crc_auto_force() { return g_crc_force.load(std::memory_order_relaxed); }
 bool crc_auto_blocked() { return g_crc_interleaved.load(std::memory_order_relaxed) == 0; }
@@ -249,21 +250,15 @@ int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
   // (>= 4 spans per workgroup: a batch of a few thousand large spans -- one
   // 64 MiB SST file -- still fills every CU)
   const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + 3) / 4);
-  if (force != 7) {  // the row drivers (under the interleaved hook: every share)
-    const int af = blk ? force : (force ? force : 8);
-    rc = blk ? ensure_lds(k_crc_auto<Op, T, true>, dev) : ensure_lds(k_crc_auto<Op, T>, dev);
-    if (rc) return rc;
-    if (blk)
-      hipLaunchKernelGGL((k_crc_auto<Op, T, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count, af);
-    else
-      hipLaunchKernelGGL((k_crc_auto<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count, af);
-    MCK_HIP(hipGetLastError());
+  if (blk) {
+    if ((rc = ensure_lds(k_crc_ragged<Op, T, true>, dev))) return rc;
+    hipLaunchKernelGGL((k_crc_ragged<Op, T, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count, force);
+  } else {  // the interleaved order (test hook): row drivers only
+    if ((rc = ensure_lds(k_crc_ragged<Op, T, false>, dev))) return rc;
+    hipLaunchKernelGGL((k_crc_ragged<Op, T, false>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count,
+                       force == 7 ? 7 : (force ? force : 8));
   }
-  if (blk && (force == 0 || force == 7)) {  // the body/head driver
-    if ((rc = ensure_lds(k_crc_bh<Op, T>, dev))) return rc;
-    hipLaunchKernelGGL((k_crc_bh<Op, T>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count, force);
-    MCK_HIP(hipGetLastError());
-  }
+  MCK_HIP(hipGetLastError());
   return MCK_OK;
 }
 

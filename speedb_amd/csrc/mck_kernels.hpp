@@ -212,32 +212,21 @@ struct OpCrcBlock {
   }
 };
 
-// Ragged batches: k_crc_auto and k_crc_bh are launched over the same batch
-// with the same grid; each workgroup takes its share in one of them
-// (crc_share_long, mck_crc.hpp).
-// k_crc_auto, force: 0 = short shares only, 2/3/5/6 = every share on that
-// row width, 8 = every share, width by length (the interleaved test order).
-template <class Op, bool T, bool BLK = false>
-__global__ __launch_bounds__(1024) void k_crc_auto(Op op, uint32_t first, uint32_t count, int force) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const RowShare sh = row_share<BLK>(first, count);
-  if (sh.n == 0) return;  // workgroup-uniform
-  if (force == 0 && crc_share_long(op, sh)) return;  // k_crc_bh's
-  crc_rows_windows<Op>(op, sh, lds, &g_crc_tables, force == 8 ? 0 : force);
-}
-
-// k_crc_bh, force: 0 = long shares only, 7 = every share.
-template <class Op, bool T>
-__global__ __launch_bounds__(1024) void k_crc_bh(Op op, uint32_t first, uint32_t count, int force) {
-  // declared (though addressed absolutely, from 0): without it the compiler
-  // sees an LDS budget and promotes private arrays into static LDS, which
-  // would shift the dynamic image
+// Ragged batches in ONE launch: each workgroup runs its share on the
+// body/head driver or the row drivers (crc_share_long).  force: 0 = by
+// length, 7 = body/head for every share, 2/3/5/6 = that row width for every
+// share, 8 = row drivers, width by length (the interleaved test order).
+template <class Op, bool T, bool BLK = true>
+__global__ __launch_bounds__(1024) void k_crc_ragged(Op op, uint32_t first, uint32_t count, int force) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   asm volatile("" ::"v"((uint32_t)(size_t)lds));
-  const RowShare sh = row_share<true>(first, count);
-  if (sh.n == 0) return;
-  if (force == 0 && !crc_share_long(op, sh)) return;  // k_crc_auto's
-  crc_bh_driver<Op, T>(op, sh, &g_crc_tables);
+  const RowShare sh = row_share<BLK>(first, count);
+  if (sh.n == 0) return;  // workgroup-uniform
+  const bool bh = force == 7 || (force == 0 && BLK && crc_share_long(op, sh));
+  if (bh)
+    crc_bh_driver<Op, T>(op, sh, &g_crc_tables);
+  else
+    crc_rows_windows<Op>(op, sh, lds, &g_crc_tables, force == 8 ? 0 : force);
 }
 
 // uniform batches (see CrcUniform)

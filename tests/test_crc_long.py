@@ -1,9 +1,10 @@
-"""The body/head CRC driver (mck_crc_bh.hpp, k_crc_bh) against the oracle.
+"""The body/head CRC driver (mck_crc_bh.hpp, in k_crc_ragged) against the oracle.
 
 A workgroup whose share averages more than 2.5 KiB per span takes it on the
 body/head driver: each span's whole 4 KiB rounds (ending at its 16-aligned
 end) in pieces of at most four rounds, its head (the rest, or the whole of
-a short span) on 8-lane rows eight heads at a time, the parts joined in an
+a short span) on 4-lane rows 16 heads at a time (one lane per head when
+the window's heads are short), the parts joined in an
 LDS accumulator (moved to the span end by zshift(4096 m)).  The cases below
 are the shapes that stress it: SST data blocks (4096 + 0..255 bytes + the
 type byte, never 16-aligned), uniform non-aligned strides, every span length

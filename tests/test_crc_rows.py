@@ -1,7 +1,8 @@
-"""The ragged-batch CRC drivers against the oracle.  A ragged batch runs on
-two kernels over the same shares: k_crc_auto (one lane, 4-, 8- or 16-lane
-rows per span, mck_crc.hpp crc_rows_loop, for shares of short spans) and
-k_crc_bh (the body/head driver, mck_crc_bh.hpp, for the rest).  Every
+"""The ragged-batch CRC drivers against the oracle.  A ragged batch is one
+launch of k_crc_ragged; each workgroup runs its share on the row drivers
+(one lane, 4-, 8- or 16-lane rows per span, mck_crc.hpp crc_rows_loop, for
+shares of short spans) or the body/head driver (mck_crc_bh.hpp, the rest).
+Every
 driver is also forced for every workgroup in a child process over the
 generic-op parity tests (mck_test_set_crc_driver, set by tests/conftest.py
 from SPEEDB_AMD_TEST_CRC_DRIVER / _ORDER)."""
@@ -71,7 +72,7 @@ def _forced(env):
 
 @pytest.mark.parametrize("mode", ["rows16", "rows8", "rows4", "rows1", "bh", "interleaved"])
 def test_auto_kernel_forced_drivers_subprocess(gpu, mode):
-    """k_crc_auto with each driver forced for every workgroup (its choice is
+    """k_crc_ragged with each driver forced for every workgroup (its choice is
     by mean length, so a parity test of mixed lengths may exercise only one):
     short spans, 0-byte spans, WAL / blob / SST ops on every driver; and the
     interleaved span order instead of contiguous ranges."""

@@ -627,6 +627,33 @@ def test_compressed_wal_corruption_and_drops(oracle):
     _stream_ok(plan2, img2)
 
 
+def test_compressed_recyclable_log_bad_crc_goes_on(oracle):
+    """A recyclable compressed log starts with kSetCompressionType under the
+    legacy 7-byte header, so ReadPhysicalRecord never sets recycled_
+    (log_reader.cc:472-476: only a recyclable type at file offset 0 does) and
+    a bad CRC under kTolerateCorruptedTailRecords does NOT end the log
+    (:290-295): the rest of the block is dropped and reported, reading goes
+    on.  (The same corruption in an uncompressed recyclable log ends it.)"""
+    import speedb_amd as S
+    L = _compressed_log(oracle, True)
+    chunks = [big_string(str(i), 700 + 37 * i) for i in range(200)]
+    for c in chunks:
+        L.write(c)
+    bad_at = L.w.records[-50][0]
+    img = bytearray(L.w.buf)
+    img[bad_at + K_RECYCLABLE_HEADER + 1] ^= 1
+    img = bytes(img)
+    ver = np.array(wal_expected_blocks(img, LOG, oracle), dtype=np.int64).astype(np.int32)
+    plan = S.wal_read_records(img, LOG, kTolerate, ver)
+    got = _records(plan, img)
+    i = next(j for j, (a, b) in enumerate(zip(got, chunks)) if a != b)
+    k = chunks.index(got[i])
+    assert k > i and got[:i] == chunks[:i] and got[i:] == chunks[k:]
+    # the drop, then the dropped record's later fragments in the next block
+    assert [r[2] for r in plan.reports][0] == "checksum mismatch"
+    assert all(r[2] == "checksum mismatch" or r[2].startswith("missing start") for r in plan.reports)
+
+
 def test_compression_record_reports(oracle):
     """ReadRecord's kSetCompressionType checks (log_reader.cc:167-188)."""
     import speedb_amd as S
@@ -676,6 +703,14 @@ def test_compressed_wal_recover_on_device(gpu, oracle):
     r = S.WalRecover(bytes(img), LOG, kTolerate)
     assert r.compression_type == kZSTD and r.record_checksums is None
     got = r.Records()
-    assert got == chunks[:len(got)] and len(got) < len(chunks)  # recyclable: the bad CRC ends the log
+    # the log's first record is kSetCompressionType, written with the legacy
+    # header (log_writer.cc EmitPhysicalRecord), so the reader never sets
+    # recycled_ (log_reader.cc:472-476, only a recyclable type at offset 0
+    # does): the bad CRC drops the rest of its block, is reported, and the
+    # walk goes on -- unlike an uncompressed recyclable log, where it ends
+    i = next(j for j, (a, b) in enumerate(zip(got, chunks)) if a != b)
+    k = chunks.index(got[i])
+    assert k > i and got[:i] == chunks[:i] and got[i:] == chunks[k:]
+    assert any("checksum mismatch" in rep[2] for rep in r.reports), r.reports
     want = wal_expected_blocks(bytes(img), LOG, oracle)
     assert [tuple(int(x) for x in b) for b in r.blocks.cpu().numpy()] == [tuple(b) for b in want]
