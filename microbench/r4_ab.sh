@@ -18,6 +18,8 @@ declare -A ARGS=(
   [sstc]="--workload sst --sst-types crc32c"
   [sstx]="--workload sst --sst-types xxh3"
   [sst]="--workload sst"
+  [sst2]="--workload sst --sst-streams 2"
+  [r300]="--workload ragged --span-min 300 --span-max 700"
   [blob]="--workload blob"
   [walrec]="--workload walrec"
   [r100]="--workload ragged --span-min 100 --span-max 300"

@@ -424,15 +424,11 @@ __device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t 
 // span's epilogue inputs in registers) per span.  For the per-KV protection
 // epilogue (key, op type and seqno hashes) that is most of a ~1 KiB span's
 // non-data VALU work.
-template <class Op, bool PREVIEW = false>
-__device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, uint64_t seed = 0) {
-  const X3Row X = x3_row(seed);
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint32_t stride = gridDim.x * wpb * 4;  // rows in the grid
-  const uint32_t first = (blockIdx.x * wpb + (threadIdx.x >> 6)) * 4 + X.row;
-  // idle rows keep loading from a valid address: the batch's base
-  X3Span rs{reinterpret_cast<uint64_t>(op.base()), 0, 0, 0, 0, 0, false};
-  bool act = x3_next_long<Op, PREVIEW>(op, first, count, stride, X, rs);
+// The row loop: each row walks its span segment by segment; next_span(rs)
+// moves a row whose span ended to its next long one (false: none left).
+template <class Op, bool PREVIEW, class Next>
+__device__ __forceinline__ void xxh3_rows_loop(const Op& op, const X3Row& X, X3Span& rs, bool act,
+                                               Next&& next_span) {
   uint64_t a0 = X.i0, a1 = X.i1;
   uint32_t slot = 0, si = 0;
   uint64_t shv = 0;
@@ -520,13 +516,28 @@ __device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, u
         sv = false;
         slot = 0;
       }
-      act = x3_next_long<Op, PREVIEW>(op, rs.i + stride, count, stride, X, rs);
+      act = next_span(rs);
       a0 = X.i0;
       a1 = X.i1;
     }
   }
   if (sv) op.finish(si, shv);
 }
+
+template <class Op, bool PREVIEW = false>
+__device__ __forceinline__ void xxh3_rows_driver(const Op& op, uint32_t count, uint64_t seed = 0) {
+  const X3Row X = x3_row(seed);
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint32_t stride = gridDim.x * wpb * 4;  // rows in the grid
+  const uint32_t first = (blockIdx.x * wpb + (threadIdx.x >> 6)) * 4 + X.row;
+  // idle rows keep loading from a valid address: the batch's base
+  X3Span rs{reinterpret_cast<uint64_t>(op.base()), 0, 0, 0, 0, 0, false};
+  const bool act = x3_next_long<Op, PREVIEW>(op, first, count, stride, X, rs);
+  xxh3_rows_loop<Op, PREVIEW>(op, X, rs, act, [&](X3Span& r) {
+    return x3_next_long<Op, PREVIEW>(op, r.i + stride, count, stride, X, r);
+  });
+}
+
 
 // ---- XXH3 / XXPH3, one WAVE per span ---------------------------------------
 // For batches of KiB-sized blocks (SST): spans are dealt to waves like the
@@ -974,6 +985,10 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
         op.finish(wb + stride * t, PREVIEW ? xxph3_short(p, len, seed) : xxh3_short(p, len));
       }
     }
+    // (Round 4 measured spans of one piece -- <= 4 rounds, the SST mix's 4
+    // and 16 KiB blocks -- on 16-lane rows first, segment by segment as
+    // xxh3_rows_driver, one scramble per segment and row: SST XXH3 image
+    // 0.613 vs 0.666 on the wave units, same box; not kept.)
     X3FeedPieces f{&s, wn, wb, stride, 0, base};
     xxh3_piece_loop<Op, PREVIEW>(op, f, X);
   }
