@@ -653,11 +653,144 @@ __device__ __forceinline__ uint4 dpp_u32x4(const uint4& v) {
 constexpr int kDppRowRor15 = 0x12F;  // lane j of a row <- lane j + 1 (mod 16)
 constexpr int kDppRowRor1x = 0x121;  // lane j of a row <- lane j - 1 (mod 16)
 
+// A row's place in the writer's share: fragment slot i, its geometry sp
+// (record type / trailer padding in key, header offset in the output dst),
+// round r; the next ticket nt (descriptor nd, header offset ndst).
+struct WalIlState {
+  RowSpan sp;
+  uint4 nd;
+  uint64_t dst, ndst;
+  uint32_t key, i, nt, live;
+  int32_t r;
+};
+struct WalIlCtx {
+  const OpWalWrite& op;
+  const RowShare& sh;
+  uint64_t base, obase, zp;
+  uint32_t share, c, lf4, carry_slot;
+  const CrcLane& L;
+};
+constexpr int kWalW = 16, kWalNP = 5;
+constexpr int kWalHdr = 2;  // padding + header bytes per lane (pad + hs <= 21)
+
+// One iteration: the output of (A's fragment, round A.r) from the round's own
+// registers (ca, masked in place), its CRC round, and B -- the row's next
+// round or its next fragment's first -- set up and loaded into cb.  x = the
+// lane's CRC state at its next piece.  Returns whether any row goes on.
+__device__ __forceinline__ bool wal_il_step(const WalIlCtx& X, const WalIlState& A, ChunkN<kWalNP>& ca,
+                                            WalIlState& B, ChunkN<kWalNP>& cb, uint32_t& x) {
+  constexpr int W = kWalW, NP = kWalNP;
+  const uint32_t c = X.c;
+  const bool live = A.live != 0;
+  const RowSpan& sp = A.sp;
+  const int r = A.r;
+  const bool last = r == 0;
+  const bool firstr = r == sp.rounds - 1;
+  const bool fin = live && last;
+
+  // ---- the output of this (span, round), from the round's own registers ----
+  const uint32_t type = A.key & 0xFF, pad = (A.key >> 8) & 0xFF;
+  const uint32_t hs = ((type >= 5 && type <= 8) || type == 11) ? 11u : 7u;
+  const uint64_t P = X.obase + A.dst + hs;  // payload in the output
+  const uint64_t ps = sp.ptr;               // payload in the source
+  const uint64_t delta = P - ps;            // (mod 2^64)
+  const uint32_t e = (uint32_t)(0ull - delta) & 15u;
+  const uint32_t q2 = e & 8u, q1 = e & 4u, be = e & 3u;
+  il_mask(ca, sp, r, c);
+  // output piece c + 16 j takes source bytes [x0 + 256 j, + 16), x0 = the
+  // round's window start + e + 16 c; whole pieces of the payload only
+  // (rel = offset in the payload, 32-bit: fragments are < 4 GiB)
+  const uint32_t win = (uint32_t)(sp.a1 - ps) - 1280u * (uint32_t)(r + 1);  // window start - ps
+  const int32_t rel0 = (int32_t)(win + e + 16u * c);
+  const int32_t lim = (int32_t)sp.n - 16;
+  const uint64_t oa0 = P + (uint64_t)(int64_t)rel0;  // output address of piece c
+  uint4 rj = dpp_u32x4<kDppRowRor15>(ca.v[0]);  // lane c + 1's piece j
+#pragma unroll
+  for (int j = 0; j < NP; j++) {
+    const uint4 rn = j + 1 < NP ? dpp_u32x4<kDppRowRor15>(ca.v[j + 1]) : rj;
+    const int32_t rel = rel0 + 256 * j;
+    const bool ok = live && rel >= 0 && rel <= lim && !(j == NP - 1 && c == 15 && e != 0);
+    const uint4 nb = (j < NP - 1 && c == 15) ? rn : rj;
+    const uint4 o = il_align(ca.v[j], nb, q2, q1, be);
+    if (ok) st16(oa0 + 256ull * j, o);
+    rj = rn;
+    // one piece at a time (the scheduler would otherwise hoist every
+    // piece's DPP moves and selects and spill)
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  {  // the piece that straddles the previous round and this one: lane 15's
+     // piece 4 of that round waits in the row's LDS slot
+    const int32_t relm = (int32_t)(win + e) - 16;
+    const bool okm = live && !firstr && e != 0 && c == 0 && relm >= 0 && relm <= lim;
+    if (wave_any(okm)) {
+      const uint4 cm = lds_u32x4(X.carry_slot);
+      const uint4 o = il_align(cm, ca.v[0], q2, q1, be);
+      if (okm) st16(P + (uint64_t)(int64_t)relm, o);
+    }
+  }
+  if (c == 15) {
+    const span_u32x4 cv = {ca.v[NP - 1].x, ca.v[NP - 1].y, ca.v[NP - 1].z, ca.v[NP - 1].w};
+    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(X.carry_slot)) = cv;
+  }
+  {  // the < 16 payload bytes before the first and after the last full output piece
+    const uint64_t h16 = (P + 15) & ~15ull;
+    const uint64_t t16 = (P + sp.n) & ~15ull;
+    const uint64_t hb_end = h16 < P + sp.n ? h16 : P + sp.n;
+    const uint64_t tb_beg = t16 > hb_end ? t16 : hb_end;
+    const uint64_t oh = P + c, ot = tb_beg + c;
+    const bool okh = fin && oh < hb_end, okt = fin && ot < P + sp.n;
+    const uint32_t bh = *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : X.zp);
+    const uint32_t bt = *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : X.zp);
+    if (okh) st_u8(oh, bh);
+    if (okt) st_u8(ot, bt);
+  }
+
+  // ---- next unit (as crc_rows_step) ----
+  const bool go = live && (!last || A.nt < X.share);
+  const RowSpan nsp = row_span<W, NP>(X.base + (((uint64_t)A.nd.y << 32) | A.nd.x), A.nd.z, A.nd.w, kInitTyped);
+  const bool sw = go && last;
+  B.sp = row_span_sel(sw, nsp, sp);
+  B.r = go ? (last ? nsp.rounds - 1 : r - 1) : r;
+  B.i = sw ? X.sh.idx(A.nt) : A.i;
+  cb = il_load(B.sp, B.r, c, X.zp);
+
+  x = il_round(firstr ? 0u : x, ca, sp, r, c, X.L);
+  uint32_t crc = 0;
+  if (wave_any(fin)) crc = crc_mask(row_finish4<W>(x, sp, X.lf4));
+  if (wave_any(live && !last)) x = il_gap(x, 0u);  // to the lane's piece in the next round
+  if (fin && c == 0) st_u32(reinterpret_cast<uint64_t>(X.op.crcs + A.i), crc);
+  // trailer padding + header: bytes c + 16 m of [dst - pad, dst + hs)
+  const uint64_t hstart = X.obase + A.dst - pad;
+#pragma unroll
+  for (int m = 0; m < kWalHdr; m++) {
+    const uint32_t b = c + (uint32_t)W * m;
+    const bool okb = fin && b < pad + hs;
+    const uint32_t val = b < pad ? 0u : wal_hdr_byte(b - pad, crc, sp.n, type, X.op.log_number);
+    if (okb) st_u8(hstart + b, val);
+  }
+
+  // ---- advance ----
+  B.nt = A.nt;
+  B.nd = A.nd;
+  B.ndst = A.ndst;
+  if (wave_any(sw)) {
+    const uint32_t tk = row_ticket<W>(sw);
+    if (sw) {
+      B.nt = tk;
+      B.nd = row_desc(tk, X.share);
+      B.ndst = *lds_p64(kLdsWalAux + 8 * (tk < X.share ? tk : 0));
+    }
+  }
+  B.key = sw ? A.nd.w : A.key;
+  B.dst = sw ? A.ndst : A.dst;
+  B.live = go ? 1u : 0u;
+  return wave_any(go);
+}
+
 __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
                                              const CrcTables* __restrict__ g) {
   constexpr bool BLK = true;  // contiguous fragment ranges per workgroup
-  constexpr int W = 16, NP = 5;
-  constexpr int kHdr = 2;  // padding + header bytes per lane (pad + hs <= 21)
+  constexpr int W = kWalW, NP = kWalNP;
   const RowShare sh = row_share<BLK>(first, count);
   crc_rows_prologue<OpWalWrite>(op, sh, lds, g, false);
   // fragments' dst_off, staged like the descriptors (row_desc_stage order)
@@ -675,135 +808,31 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
   __syncthreads();
   const CrcLane L = crc_lane();
   const uint32_t c = threadIdx.x & (W - 1);
-  const uint32_t lf4 = c << 2;
   const uint32_t share = sh.n;
-  const uint64_t base = reinterpret_cast<uint64_t>(op.src);
-  const uint64_t obase = reinterpret_cast<uint64_t>(op.out);
-  const uint64_t zp = reinterpret_cast<uint64_t>(&g->zero16[0]);
-  uint32_t t = row_ticket<W>(true);
-  bool live = t < share;
-  uint4 d = row_desc(t, share);
-  uint64_t dst = *lds_p64(kLdsWalAux + 8 * (t < share ? t : 0));
-  uint32_t i = sh.idx(live ? t : 0);
-  RowSpan sp = row_span<W, NP>(base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kInitTyped);
-  uint32_t key = d.w;
-  int r = sp.rounds - 1;
-  ChunkN<NP> cur = il_load(sp, r, c, zp);
-  uint32_t nt = row_ticket<W>(true);
-  uint4 nd = row_desc(nt, share);
-  uint64_t ndst = *lds_p64(kLdsWalAux + 8 * (nt < share ? nt : 0));
-  uint32_t x = 0;  // the lane's CRC state at its next piece
   // the row's LDS slot for the previous round's straddling piece
-  const uint32_t carry_slot = kLdsWalCarry + 16u * (threadIdx.x >> 4);
+  const WalIlCtx X{op, sh, reinterpret_cast<uint64_t>(op.src), reinterpret_cast<uint64_t>(op.out),
+                   reinterpret_cast<uint64_t>(&g->zero16[0]), share, c, c << 2, kLdsWalCarry + 16u * (threadIdx.x >> 4), L};
+  WalIlState A;
+  const uint32_t t = row_ticket<W>(true);
+  A.live = t < share ? 1u : 0u;
+  const uint4 d = row_desc(t, share);
+  A.dst = *lds_p64(kLdsWalAux + 8 * (t < share ? t : 0));
+  A.i = sh.idx(A.live ? t : 0);
+  A.sp = row_span<W, NP>(X.base + (((uint64_t)d.y << 32) | d.x), d.z, d.w, kInitTyped);
+  A.key = d.w;
+  A.r = A.sp.rounds - 1;
+  ChunkN<NP> ca = il_load(A.sp, A.r, c, X.zp);
+  A.nt = row_ticket<W>(true);
+  A.nd = row_desc(A.nt, share);
+  A.ndst = *lds_p64(kLdsWalAux + 8 * (A.nt < share ? A.nt : 0));
+  uint32_t x = 0;  // the lane's CRC state at its next piece
+  // unrolled twice: the rounds' chunks and states swap register names
+  // instead of 20 v_mov per round
+  WalIlState B;
+  ChunkN<NP> cb;
   for (;;) {
-    const bool last = r == 0;
-    const bool firstr = r == sp.rounds - 1;
-    const bool fin = live && last;
-
-    // ---- the output of this (span, round), from the round's own registers ----
-    const uint32_t type = key & 0xFF, pad = (key >> 8) & 0xFF;
-    const uint32_t hs = ((type >= 5 && type <= 8) || type == 11) ? 11u : 7u;
-    const uint64_t P = obase + dst + hs;             // payload in the output
-    const uint64_t ps = sp.ptr;  // payload in the source
-    const uint64_t delta = P - ps;                   // (mod 2^64)
-    const uint32_t e = (uint32_t)(0ull - delta) & 15u;
-    const uint32_t q2 = e & 8u, q1 = e & 4u, be = e & 3u;
-    il_mask(cur, sp, r, c);
-    // output piece c + 16 j takes source bytes [x0 + 256 j, + 16), x0 = the
-    // round's window start + e + 16 c; whole pieces of the payload only
-    // (rel = offset in the payload, 32-bit: fragments are < 4 GiB)
-    const uint32_t win = (uint32_t)(sp.a1 - ps) - 1280u * (uint32_t)(r + 1);  // window start - ps
-    const int32_t rel0 = (int32_t)(win + e + 16u * c);
-    const int32_t lim = (int32_t)sp.n - 16;
-    const uint64_t oa0 = P + (uint64_t)(int64_t)rel0;  // output address of piece c
-    uint4 rj = dpp_u32x4<kDppRowRor15>(cur.v[0]);  // lane c + 1's piece j
-#pragma unroll
-    for (int j = 0; j < NP; j++) {
-      const uint4 rn = j + 1 < NP ? dpp_u32x4<kDppRowRor15>(cur.v[j + 1]) : rj;
-      const int32_t rel = rel0 + 256 * j;
-      const bool ok = live && rel >= 0 && rel <= lim && !(j == NP - 1 && c == 15 && e != 0);
-      const uint4 nb = (j < NP - 1 && c == 15) ? rn : rj;
-      const uint4 o = il_align(cur.v[j], nb, q2, q1, be);
-      if (ok) st16(oa0 + 256ull * j, o);
-      rj = rn;
-      // one piece at a time (the scheduler would otherwise hoist every
-      // piece's DPP moves and selects and spill)
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    {  // the piece that straddles the previous round and this one: lane 15's
-       // piece 4 of that round waits in the row's LDS slot
-      const int32_t relm = (int32_t)(win + e) - 16;
-      const bool okm = live && !firstr && e != 0 && c == 0 && relm >= 0 && relm <= lim;
-      if (wave_any(okm)) {
-        const uint4 cm = lds_u32x4(carry_slot);
-        const uint4 o = il_align(cm, cur.v[0], q2, q1, be);
-        if (okm) st16(P + (uint64_t)(int64_t)relm, o);
-      }
-    }
-    if (c == 15) {
-      const span_u32x4 cv = {cur.v[NP - 1].x, cur.v[NP - 1].y, cur.v[NP - 1].z, cur.v[NP - 1].w};
-      *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(carry_slot)) = cv;
-    }
-    {  // the < 16 payload bytes before the first and after the last full output piece
-      const uint64_t h16 = (P + 15) & ~15ull;
-      const uint64_t t16 = (P + sp.n) & ~15ull;
-      const uint64_t hb_end = h16 < P + sp.n ? h16 : P + sp.n;
-      const uint64_t tb_beg = t16 > hb_end ? t16 : hb_end;
-      const uint64_t oh = P + c, ot = tb_beg + c;
-      const bool okh = fin && oh < hb_end, okt = fin && ot < P + sp.n;
-      const uint32_t bh = *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : zp);
-      const uint32_t bt = *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : zp);
-      if (okh) st_u8(oh, bh);
-      if (okt) st_u8(ot, bt);
-    }
-
-    // ---- next unit (as crc_rows_loop) ----
-    const bool go = live && (!last || nt < share);
-    const RowSpan nsp = row_span<W, NP>(base + (((uint64_t)nd.y << 32) | nd.x), nd.z, nd.w, kInitTyped);
-    const bool sw = go && last;
-    const RowSpan lsp = row_span_sel(sw, nsp, sp);
-    const int lr = go ? (last ? nsp.rounds - 1 : r - 1) : r;
-    const uint32_t li = sw ? sh.idx(nt) : i;
-    const ChunkN<NP> nxt = il_load(lsp, lr, c, zp);
-
-    x = il_round(firstr ? 0u : x, cur, sp, r, c, L);
-    uint32_t crc = 0;
-    if (wave_any(fin)) crc = crc_mask(row_finish4<W>(x, sp, lf4));
-    if (wave_any(live && !last)) x = il_gap(x, 0u);  // to the lane's piece in the next round
-    if (fin && c == 0) st_u32(reinterpret_cast<uint64_t>(op.crcs + i), crc);
-    // trailer padding + header: bytes c + 16 m of [dst - pad, dst + hs)
-    const uint64_t hstart = obase + dst - pad;
-#pragma unroll
-    for (int m = 0; m < kHdr; m++) {
-      const uint32_t b = c + (uint32_t)W * m;
-      const bool okb = fin && b < pad + hs;
-      const uint32_t val = b < pad ? 0u : wal_hdr_byte(b - pad, crc, sp.n, type, op.log_number);
-      if (okb) st_u8(hstart + b, val);
-    }
-
-    // ---- advance ----
-    uint32_t nnt = nt;
-    uint4 nnd = nd;
-    uint64_t nndst = ndst;
-    if (wave_any(sw)) {
-      const uint32_t tk = row_ticket<W>(sw);
-      if (sw) {
-        nnt = tk;
-        nnd = row_desc(tk, share);
-        nndst = *lds_p64(kLdsWalAux + 8 * (tk < share ? tk : 0));
-      }
-    }
-    if (!wave_any(go)) break;
-    key = sw ? nd.w : key;
-    dst = sw ? ndst : dst;
-    live = go;
-    i = li;
-    nt = nnt;
-    nd = nnd;
-    ndst = nndst;
-    sp = lsp;
-    r = lr;
-    cur = nxt;
+    if (!wal_il_step(X, A, ca, B, cb, x)) break;
+    if (!wal_il_step(X, B, cb, A, ca, x)) break;
   }
 }
 
