@@ -18,6 +18,9 @@ declare -A ARGS=(
   [u4300]="--workload crc32c --block-bytes 4300 --blocks 1000000"
   [sstx]="--workload sst --sst-types xxh3"
   [x4k]="--workload xxh3"
+  [kv100]="--workload blockkv --kv-value-bytes 100"
+  [kv1000]="--workload blockkv --kv-value-bytes 1000"
+  [walwrite]="--workload walwrite"
 )
 PA="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY"
 PB="SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_INSTS_SMEM"

@@ -800,7 +800,10 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
 // keys [64 c, 64 c + 64) for c = w, w + W, ... (one coalesced read of 64
 // lengths; a chunk without long values costs nothing more), its long values
 // four at a time, one per 16-lane row (xp_row_long: every load instruction
-// reads 128 contiguous bytes of each of four neighbouring values).
+// reads 128 contiguous bytes of each of four neighbouring values).  (Round 4
+// measured values under 1 KiB with the last stripe's load issued with the
+// others, one or two values per row and round: 1000-B values 0.3371 / 0.3375
+// vs 0.3374 -- the sweep is not bound by its round trips per wave.)
 template <bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_long(const uint64_t* key_base, uint32_t nblocks,
                                                     const uint64_t* long_off, const uint32_t* long_len,
