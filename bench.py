@@ -616,7 +616,7 @@ def make_workload(args, dev, rank, world):
                                                     rint.data_ptr(), nkeys, work.data_ptr(), out.data_ptr(), stream.cuda_stream),
                        "mck_block_kv_protect_batch")
         w.step = step
-        w.kernel = ("k_block_layout_t + k_blk_scan + k_block_kv_t + k_block_long "
+        w.kernel = ("k_block_layout_t + k_blk_scan + k_block_kv_t + k_block_long_rows "
                     "(whole step, incl. the totals readback)")
         w.span_bytes = db.block_bytes
         # what the step must move: every block read once, the kv_checksum

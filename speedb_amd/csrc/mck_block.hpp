@@ -16,8 +16,8 @@
 //   k_block_kv_t      walks again, reassembling every key in a per-thread
 //                     LDS buffer: ProtectKV(key, value).Encode(prot_bytes)
 //                     for every entry, values over 240 B left to
-//   k_block_long      the long-value list in key order, XXPH3 by 16-lane
-//                     rows (mck_kernels.hpp OpBlkLong)
+//   k_block_long_rows the long-value list in key order, XXPH3 on the XXH3
+//                     row loop (16-lane rows, 16-byte loads)
 //
 // Entry k of a block lands at key index key_base[block] + k, in the order the
 // reference's SeekToFirst/Next loop generates them (:1116-1123).
@@ -619,13 +619,15 @@ constexpr uint32_t kBlkKeyBuf = 128;  // bytes of LDS key buffer per thread
 // walk (round 3): a lane's long value would be read with 8-byte loads from
 // 64 different blocks per instruction, or, four at a time by 16-lane rows
 // (round 2), serialise the bandwidth-bound hashing behind the latency-bound
-// walk in one wave.  The walk writes the entry's hash WITHOUT the value's
+// walk in one wave.  (Round 3 swept the list with a wave per 64 keys and 8-byte
+// loads per lane, k_block_long: 1000-B values 0.335 of peak; the row loop
+// below, 0.362.)  The walk writes the entry's hash WITHOUT the value's
 // (ProtectKV XORs the per-field hashes, and the Encode truncation commutes
 // with XOR) and records the value in a LONG-VALUE LIST indexed by the key
 // index k -- so the list is in memory order (keys follow blocks, entries
 // follow each other) and needs no scan: long_len[k] = value length (0: no
 // long value; the host zeroes the array), long_off[k] = value address,
-// and, to verify, long_part[k] = the partial hash.  k_block_long then
+// and, to verify, long_part[k] = the partial hash.  k_block_long_rows then
 // sweeps the key range front to back with the XXPH3 row driver (one value
 // per 16-lane row, 16-byte loads), XORs the value hash into enc[k] (protect)
 // or compares partial ^ value hash with the stored bytes (verify).
@@ -648,7 +650,8 @@ __device__ __forceinline__ uint64_t blk_load_prot(const uint8_t* a, uint64_t k, 
 template <int KIND, bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t count, const uint64_t* key_base,
                                                     const uint64_t* arena_base, uint8_t* arena, uint64_t* long_off,
-                                                    uint32_t* long_len, uint64_t* long_part, uint32_t prot_bytes,
+                                                    uint32_t* long_len, uint64_t K_total, uint64_t* long_part,
+                                                    uint32_t prot_bytes,
                                                     uint8_t* enc, const uint8_t* stored, uint8_t* mismatch,
                                                     uint32_t* mismatch_count) {
   // + 20 B: dword reads and the 16-byte delta write past the key end; an odd
@@ -681,6 +684,7 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
   // leave the block, the entry is read field by field.
   uint4 U = make_uint4(0, 0, 0, 0);
   bool uok = false;
+  bool any_long = false;  // this lane recorded a long value
   if (active) {
     uok = n >= 16;
     if (uok) U = vload16_any(reinterpret_cast<uint64_t>(rd.p));
@@ -760,9 +764,10 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
       }
       if (!vmid && !lng) hv ^= xp_short(rd, v, vl, kSeedV);  // <= 16 or 129..240 bytes
     }
+    any_long |= lng;
     if (active) {
       const uint64_t k = k0 + idx;
-      if (lng) {  // to the long-value list; k_block_long completes the entry
+      if (lng) {  // to the long-value list; k_block_long_rows completes the entry
         long_off[k] = reinterpret_cast<uint64_t>(rd.p) + v;
         long_len[k] = vl;
         if constexpr (VERIFY) long_part[k] = hv;
@@ -794,76 +799,10 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
       active = p < ro;
     }
   }
-}
-
-// The long-value list (see k_block_kv_t), swept front to back: wave w takes
-// keys [64 c, 64 c + 64) for c = w, w + W, ... (one coalesced read of 64
-// lengths; a chunk without long values costs nothing more), its long values
-// four at a time, one per 16-lane row (xp_row_long: every load instruction
-// reads 128 contiguous bytes of each of four neighbouring values).  (Round 4
-// measured values under 1 KiB with the last stripe's load issued with the
-// others, one or two values per row and round: 1000-B values 0.3371 / 0.3375
-// vs 0.3374 -- the sweep is not bound by its round trips per wave.)
-template <bool VERIFY>
-__global__ __launch_bounds__(256) void k_block_long(const uint64_t* key_base, uint32_t nblocks,
-                                                    const uint64_t* long_off, const uint32_t* long_len,
-                                                    const uint64_t* long_part, uint32_t prot_bytes, uint8_t* enc,
-                                                    const uint8_t* stored, uint8_t* mismatch,
-                                                    uint32_t* mismatch_count) {
-  __shared__ uint64_t s_sec[24];  // XXPH3_initCustomSecret(kSeedV) as u64 words
-  if (threadIdx.x < 24) s_sec[threadIdx.x] = csec64(8 * (int)threadIdx.x, kSeedV);
-  __syncthreads();
-  const uint32_t lane = threadIdx.x & 63, l8 = lane & 7;
-  const uint64_t klast = csec64(121 + 8 * (int)l8, kSeedV);
-  const uint64_t km = csec64((l8 & 1) ? 19 + 16 * (int)(l8 >> 1) : 11 + 16 * (int)(l8 >> 1), kSeedV);
-  const uint64_t K = ldg_u64(key_base, nblocks);  // keys of the batch
-  const uint64_t wpb = blockDim.x >> 6;
-  const uint64_t nw = gridDim.x * wpb, w = blockIdx.x * wpb + (threadIdx.x >> 6);
-  const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
-  for (uint64_t c = 64 * w; c < K; c += 64 * nw) {
-    const uint64_t k = c + lane;
-    const uint32_t vl = k < K ? long_len[k] : 0u;
-    uint64_t longs = __ballot(vl != 0);
-    if (!longs) continue;  // wave-uniform
-    const uint64_t va = vl ? long_off[k] : 0;
-    const uint64_t part = VERIFY && vl ? long_part[k] : 0;
-    uint64_t hv = 0;
-    while (longs) {
-      uint32_t js[4] = {64, 64, 64, 64};
-#pragma unroll
-      for (int m = 0; m < 4; m++)
-        if (longs) {
-          js[m] = (uint32_t)__builtin_ctzll(longs);
-          longs &= longs - 1;
-        }
-      const uint32_t row = lane >> 4;
-      const uint32_t src = row == 0 ? js[0] : row == 1 ? js[1] : row == 2 ? js[2] : js[3];
-      const uint32_t srcl = src < 64 ? src : 0u;
-      const uint64_t va_r = __shfl(va, (int)srcl, 64);
-      const uint32_t vl_r = (uint32_t)__shfl((int)vl, (int)srcl, 64);
-      uint64_t h2 = 0;
-      if (src < 64) h2 = xp_row_long(GblRd{reinterpret_cast<const uint8_t*>(va_r)}, 0, vl_r, s_sec, klast, km, lane);
-#pragma unroll
-      for (int m = 0; m < 4; m++) {
-        const uint64_t hm = __shfl(h2, 16 * m, 64);
-        if (lane == js[m]) hv = hm;
-      }
-    }
-    if (vl) {
-      if constexpr (!VERIFY) {  // enc[k] holds Encode(partial): XOR the value's hash in
-        if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0)) {
-          reinterpret_cast<uint64_t*>(enc)[k] ^= hv;
-        } else {
-          for (uint32_t b = 0; b < prot_bytes; b++) enc[k * prot_bytes + b] ^= (uint8_t)(hv >> (8 * b));
-        }
-      } else {
-        const uint64_t sv = blk_load_prot(stored, k, prot_bytes);
-        const bool bad = sv != ((part ^ hv) & keep);
-        mismatch[k] = bad;
-        if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
-      }
-    }
-  }
+  // one flag store per wave (every writer stores 1; an atomic per step on
+  // one address serialised the walk: 1000-B values 0.363 -> 0.274): the
+  // long-value sweep exits at once when no value was recorded
+  if (__ballot(any_long) && lane == 0) long_len[K_total] = 1u;
 }
 
 __global__ __launch_bounds__(64) void k_dbg_xp(const uint8_t* d, uint32_t len, uint64_t seed, uint64_t* out) {
@@ -888,6 +827,84 @@ __global__ __launch_bounds__(64) void k_dbg_xp(const uint8_t* d, uint32_t len, u
     out[2] = c;
   }
   if ((lane & 15) == 0) out[3 + (lane >> 4)] = r;
+}
+
+// The long-value list on the XXH3 row driver (round 4): each 16-lane row
+// walks key chunks [16 c, 16 c + 16), c = its row id, + rows in the grid,
+// ... (one coalesced read of 16 lengths per row; a chunk without long
+// values costs nothing more) and hashes the chunk's long values one after
+// another with xxh3_rows_loop (XXPH3 preview rules, seed kSeedV): 16-byte
+// dword-aligned loads, one KiB per row per iteration, one scramble per
+// segment and row -- where k_block_long's wave-wide sweep read 8 bytes per
+// lane per load.  op.finish XORs the value's hash into enc[k] (protect) or
+// compares partial ^ hash with the stored bytes (verify).
+template <bool VERIFY>
+struct OpBlkLongRows {
+  const uint64_t* long_off;
+  const uint32_t* long_len;  // [K]; [K] = long values recorded by the walk
+  const uint64_t* long_part;
+  uint32_t prot_bytes;
+  uint8_t* enc;
+  const uint8_t* stored;
+  uint8_t* mismatch;
+  uint32_t* mismatch_count;
+  __device__ void finish(uint32_t k, uint64_t hv) const {
+    if constexpr (!VERIFY) {  // enc[k] holds Encode(partial): XOR the value's hash in
+      if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0)) {
+        reinterpret_cast<uint64_t*>(enc)[k] ^= hv;
+      } else {
+        for (uint32_t b = 0; b < prot_bytes; b++) enc[(uint64_t)k * prot_bytes + b] ^= (uint8_t)(hv >> (8 * b));
+      }
+    } else {
+      const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
+      const uint64_t sv = blk_load_prot(stored, k, prot_bytes);
+      const bool bad = sv != ((long_part[k] ^ hv) & keep);
+      mismatch[k] = bad;
+      if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
+    }
+  }
+};
+template <bool VERIFY>
+__global__ __launch_bounds__(256) void k_block_long_rows(OpBlkLongRows<VERIFY> op, const uint64_t* key_base,
+                                                         uint32_t nblocks) {
+  const uint64_t K = ldg_u64(key_base, nblocks);  // keys of the batch (< 2^32: the host checks)
+  if (op.long_len[K] == 0) return;  // no long value in the batch (the walk counted them)
+  const X3Row X = x3_row(kSeedV);
+  const uint32_t wpb = blockDim.x >> 6;
+  const uint64_t rows = (uint64_t)gridDim.x * wpb * 4;
+  uint64_t c = ((uint64_t)blockIdx.x * wpb + (threadIdx.x >> 6)) * 4 + X.row;  // the row's chunk
+  uint32_t mask = 0, mylen = 0;  // the chunk's long values (row bits) / this lane's key's length
+  uint64_t myoff = 0;
+  bool have = false;
+  // idle rows load from a valid address (the list itself)
+  X3Span rs{reinterpret_cast<uint64_t>(op.long_off), 0, 0, 0, 0, 0, false};
+  auto next = [&](X3Span& r) -> bool {
+    for (;;) {
+      if (mask) {  // row-uniform
+        const uint32_t b = (uint32_t)__builtin_ctz(mask);
+        mask &= mask - 1;
+        const int src = (int)(((uint32_t)X.lane & ~15u) + b);
+        r.ptr = (uint64_t)__shfl((long long)myoff, src, 64);
+        r.len = (uint32_t)__shfl((int)mylen, src, 64);
+        // XXPH3 util/xxph3.h:1516-1543 (len > 240)
+        r.nb = (uint32_t)(r.len / 1024);
+        r.nst = (uint32_t)((r.len - 1024ull * r.nb) / 64);
+        r.tail = (r.len & 63) != 0;
+        r.g = 0;
+        r.i = (uint32_t)(16 * c + b);
+        return true;
+      }
+      if (have) c += rows;
+      have = true;
+      if (16 * c >= K) return false;
+      const uint64_t k = 16 * c + (uint32_t)X.j;
+      mylen = k < K ? op.long_len[k] : 0u;
+      myoff = mylen ? op.long_off[k] : 0ull;
+      mask = (uint32_t)(__ballot(mylen != 0) >> (16 * X.row)) & 0xFFFFu;
+    }
+  };
+  const bool act = next(rs);
+  xxh3_rows_loop<OpBlkLongRows<VERIFY>, true>(op, X, rs, act, next);
 }
 
 // ---- exclusive scan of two u64 arrays (key counts, key bytes) --------------

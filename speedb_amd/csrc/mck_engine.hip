@@ -433,13 +433,14 @@ template <int KIND>
 struct BlkKvT {
   template <class... A>
   static void go(dim3, hipStream_t st, bool verify, SpanSrc s, uint32_t n, const uint64_t* kb, const uint64_t* ab,
-                 uint8_t* arena, uint64_t* long_off, uint32_t* long_len, uint64_t* long_part, A... rest) {
+                 uint8_t* arena, uint64_t* long_off, uint32_t* long_len, uint64_t nkeys, uint64_t* long_part,
+                 A... rest) {
     if (verify)
       hipLaunchKernelGGL((k_block_kv_t<KIND, true>), dim3((n + 255) / 256), dim3(256), 0, st, s, n, kb, ab, arena,
-                         long_off, long_len, long_part, rest...);
+                         long_off, long_len, nkeys, long_part, rest...);
     else
       hipLaunchKernelGGL((k_block_kv_t<KIND, false>), dim3((n + 255) / 256), dim3(256), 0, st, s, n, kb, ab, arena,
-                         long_off, long_len, long_part, rest...);
+                         long_off, long_len, nkeys, long_part, rest...);
   }
 };
 template <template <int> class K, class... A>
@@ -463,8 +464,8 @@ int launch_blk(int kind, uint32_t count, hipStream_t st, A... args) {
 
 uint64_t blk_tiles(uint32_t count) { return ((uint64_t)count + kBlkScanTile - 1) / kBlkScanTile; }
 
-// work area: [long_off u64 K][long_part u64 K][long_len u32 K][4 B x K spare] [key arena]
-// (the long-value list of k_block_kv_t / k_block_long, indexed by key)
+// work area: [long_off u64 K][long_part u64 K][long_len u32 K][u32: long values recorded][spare] [key arena]
+// (the long-value list of k_block_kv_t / k_block_long_rows, indexed by key)
 struct BlkWork {
   uint64_t *long_off, *long_part;
   uint32_t* long_len;
@@ -498,22 +499,33 @@ int blk_kv(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_
     return MCK_EINVAL;
   }
   if (!total_keys || !blocks->count) return MCK_OK;
+  if (total_keys > 0xFFFFFFFFull) {
+    set_err("more than 2^32 - 1 keys in one batch (%llu)", (unsigned long long)total_keys);
+    return MCK_EINVAL;
+  }
   const BlkWork w = blk_work(work, total_keys);
   const bool verify = stored != nullptr;
-  MCK_HIP(hipMemsetAsync(w.long_len, 0, 4 * total_keys, st));  // no long value unless the walk records one
+  // no long value unless the walk records one; [total_keys] counts them
+  MCK_HIP(hipMemsetAsync(w.long_len, 0, 4 * total_keys + 4, st));
   if (int rc = launch_blk<BlkKvT>(kind, blocks->count, st, verify, to_src(blocks), blocks->count, key_base,
-                                  arena_base, w.arena, w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored,
+                                  arena_base, w.arena, w.long_off, w.long_len, total_keys, w.long_part, prot_bytes,
+                                  enc, stored,
                                   mismatch, mismatch_count))
     return rc;
   int ncu;
   if (int rc = current_device(nullptr, &ncu)) return rc;
-  const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)ncu * 16, (total_keys + 255) / 256);
+  // 16 keys per row chunk; rows = 16 per workgroup of 256
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)ncu * 8, (total_keys + 255) / 256);
   if (verify)
-    hipLaunchKernelGGL(k_block_long<true>, dim3(grid), dim3(256), 0, st, key_base, blocks->count, w.long_off,
-                       w.long_len, w.long_part, prot_bytes, enc, stored, mismatch, mismatch_count);
+    hipLaunchKernelGGL(k_block_long_rows<true>, dim3(grid), dim3(256), 0, st,
+                       OpBlkLongRows<true>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
+                                           mismatch_count},
+                       key_base, blocks->count);
   else
-    hipLaunchKernelGGL(k_block_long<false>, dim3(grid), dim3(256), 0, st, key_base, blocks->count, w.long_off,
-                       w.long_len, w.long_part, prot_bytes, enc, stored, mismatch, mismatch_count);
+    hipLaunchKernelGGL(k_block_long_rows<false>, dim3(grid), dim3(256), 0, st,
+                       OpBlkLongRows<false>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
+                                            mismatch_count},
+                       key_base, blocks->count);
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }
