@@ -326,25 +326,6 @@ __device__ __forceinline__ uint64_t xp_mid_fold(const uint64_t (&d)[16], uint32_
   return xxph3_avalanche(acc);
 }
 
-// 64-bit sum over the 8 lanes of each lane octet (DPP: quad swaps, then the
-// half-row mirror), in every lane of the octet.
-__device__ __forceinline__ uint64_t oct_sum_u64(uint64_t v) {
-  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-#define MCK_OCT_STEP(CTRL)                                                              \
-  {                                                                                     \
-    const uint32_t xl = (uint32_t)__builtin_amdgcn_mov_dpp((int)lo, CTRL, 0xF, 0xF, false); \
-    const uint32_t xh = (uint32_t)__builtin_amdgcn_mov_dpp((int)hi, CTRL, 0xF, 0xF, false); \
-    const uint64_t s = ((uint64_t)hi << 32 | lo) + ((uint64_t)xh << 32 | xl);              \
-    lo = (uint32_t)s;                                                                   \
-    hi = (uint32_t)(s >> 32);                                                           \
-  }
-  MCK_OCT_STEP(0xB1)   // quad_perm [1,0,3,2]
-  MCK_OCT_STEP(0x4E)   // quad_perm [2,3,0,1]
-  MCK_OCT_STEP(0x141)  // row_half_mirror
-#undef MCK_OCT_STEP
-  return (uint64_t)hi << 32 | lo;
-}
-
 // 17..128-byte values of a wave's lanes hashed by lane octets (all 64 lanes
 // call it; `mine`: this lane has such a value, at global address va).  In
 // step j octet g hashes the value of lane 8 g + j, its lane 8 g + t loading
@@ -352,8 +333,8 @@ __device__ __forceinline__ uint64_t oct_sum_u64(uint64_t v) {
 // eight contiguous <= 128-byte windows, where a per-lane hash's reads 64
 // scattered pieces -- the per-lane walk is bound by the texture addresser
 // (TA busy ~95 % of the protect kernel, ~64 lanes' worth of cycles per
-// divergent load).  The octet sums its terms with DPP; lane 8 g + j keeps the
-// hash of its own value.  klo / khi: sec64(16 t) + seed, sec64(16 t + 8) - seed.
+// divergent load).  The octet sums its terms with DPP (reduce-scatter: lane
+// 8 g + j ends with the sum for its own value).  klo / khi: sec64(16 t) + seed, sec64(16 t + 8) - seed.
 __device__ __forceinline__ uint64_t xp_mid_octets(uint64_t va, uint32_t vl, bool mine, uint64_t klo, uint64_t khi,
                                                   uint32_t lane) {
   const uint32_t t = lane & 7, gb = lane & ~7u;
@@ -373,17 +354,33 @@ __device__ __forceinline__ uint64_t xp_mid_octets(uint64_t va, uint32_t vl, bool
     d[j] = *reinterpret_cast<__attribute__((address_space(1))) const span_u32x4*>(addr);
     lens[j] = lm;
   }
-  uint64_t res = 0;
+  uint64_t m[8];  // this lane's term for value j (piece t of it)
 #pragma unroll
   for (int j = 0; j < 8; j++) {
     const uint64_t lo = (uint64_t)d[j].y << 32 | d[j].x, hi = (uint64_t)d[j].w << 32 | d[j].z;
-    const uint64_t m = mul128_fold64(lo ^ klo, hi ^ khi);
+    const uint64_t mm = mul128_fold64(lo ^ klo, hi ^ khi);
     const uint32_t pairs = (lens[j] + 31) / 32;
-    const uint64_t sum = oct_sum_u64((t >> 1) < pairs ? m : 0ull);
-    const uint64_t h = xxph3_avalanche((uint64_t)lens[j] * P64_1 + sum);
-    res = t == (uint32_t)j ? h : res;
+    m[j] = (t >> 1) < pairs ? mm : 0ull;
   }
-  return res;
+  // Reduce-scatter over the octet: lane t ends with the sum over the octet
+  // of value t's terms (its own value), in three exchange steps -- bit 2 of
+  // the value index with the half-row mirror partner (7 - t), then bit 1
+  // (lane ^ 2) and bit 0 (lane ^ 1) -- 7 exchanged values instead of eight
+  // 3-step octet sums, and one avalanche per lane instead of eight.
+  uint64_t r1[4], r2[2];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint64_t keep = (t & 4) ? m[4 + q] : m[q], send = (t & 4) ? m[q] : m[4 + q];
+    r1[q] = keep + dpp64<0x141>(send);  // row_half_mirror
+  }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint64_t keep = (t & 2) ? r1[2 + q] : r1[q], send = (t & 2) ? r1[q] : r1[2 + q];
+    r2[q] = keep + dpp64<0x4E>(send);  // quad_perm [2,3,0,1]: lane ^ 2
+  }
+  const uint64_t keep = (t & 1) ? r2[1] : r2[0], send = (t & 1) ? r2[0] : r2[1];
+  const uint64_t sum = keep + dpp64<0xB1>(send);  // quad_perm [1,0,3,2]: lane ^ 1
+  return xxph3_avalanche((uint64_t)lm_own * P64_1 + sum);
 }
 
 // one lane, any length (keys)
@@ -748,9 +745,19 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
       // IterKey::TrimAppend: only the non-shared bytes change
       if (!global_key) {
         // the delta's first 16 bytes from kw (written whole: bytes past the
-        // key are never read as key), the rest (rare) in dword loads
-#pragma unroll
-        for (int c = 0; c < 16; c++) lkey[sh + c] = (uint8_t)(kw[c >> 2] >> (8 * (c & 3)));
+        // key are never read as key) as five aligned dwords, the first merged
+        // with the shared prefix bytes below sh (16 byte stores were 16 LDS
+        // instructions per entry); the rest (rare) in dword loads
+        {
+          uint32_t* kd = s_key[threadIdx.x] + (sh >> 2);
+          const uint32_t s4 = sh & 3u, sb = 4u - s4;  // alignbyte uses sb & 3: s4 = 0 is the plain copy
+          const uint32_t prev = s4 ? kd[0] << (8 * sb) : 0u;  // the prefix bytes, at the top
+          kd[0] = s4 ? __builtin_amdgcn_alignbyte(kw[0], prev, sb) : kw[0];
+          kd[1] = s4 ? __builtin_amdgcn_alignbyte(kw[1], kw[0], sb) : kw[1];
+          kd[2] = s4 ? __builtin_amdgcn_alignbyte(kw[2], kw[1], sb) : kw[2];
+          kd[3] = s4 ? __builtin_amdgcn_alignbyte(kw[3], kw[2], sb) : kw[3];
+          kd[4] = __builtin_amdgcn_alignbyte(0u, kw[3], sb);  // (s4 = 0: past the 16 bytes, never read)
+        }
         for (uint32_t i = sh + 16; i < kl; i += 4) {
           const uint32_t w = rd.u32(q + i - sh);
           for (uint32_t c = 0; c < 4 && i + c < kl; c++) lkey[i + c] = (uint8_t)(w >> (8 * c));
