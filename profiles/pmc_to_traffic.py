@@ -92,11 +92,21 @@ def main():
         rd, wr = rd * per_step, wr * per_step
         timed_ns = None
     alg = line["roofline"]["alg_bytes_per_launch"]
+    # a step of passes over a resident image whose last pass is partial (the
+    # WAL replay: 10M blocks = 4 x 2,097,152 + 1,611,392): the counters
+    # average the actual dispatches, alg_bytes_per_launch is a full pass --
+    # compare like with like, and report the traffic per full pass
+    c = line["config"]
+    scale = 1.0
+    if all(k in c for k in ("blocks_per_gpu", "passes", "resident_blocks")):
+        scale = c["blocks_per_gpu"] / (c["passes"] * c["resident_blocks"])
+    rd, wr = rd / scale, wr / scale
     out = {
         "workload": workload, "kernel": kernel, "config": cfg,
         "hbm_bytes_per_launch": int(rd + wr),
         "read_bytes_per_launch": int(rd), "write_bytes_per_launch": int(wr),
         "alg_bytes_per_launch": alg, "traffic_over_alg": round((rd + wr) / alg, 4),
+        "dispatch_scale": round(scale, 6),
         "rocprof_avg_kernel_ns": round(avg_ns / max(calls, 1), 1), "rocprof_calls": calls,
         "rocprof_timed_window_avg_kernel_ns": None if timed_ns is None else round(timed_ns, 1),
         "bench_kernel_avg_ms": line["roofline"]["kernel_avg_ms"],
@@ -104,7 +114,8 @@ def main():
         "method": "FETCH_SIZE(KiB)*1024*2 (gfx950 16B/lane read correction) + WRITE_SIZE(KiB)*1024, "
                   + ("summed over every kernel of a step, per step" if whole_step else
                      "averaged over the dominant kernel's dispatches")
-                  + "; separate --pmc passes with --kernel-trace only",
+                  + "; separate --pmc passes with --kernel-trace only"
+                  + ("; per full resident pass (dispatch_scale = mean dispatch / full pass)" if scale != 1.0 else ""),
     }
     dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"traffic_{workload}.json")
     with open(dst, "w") as f:
