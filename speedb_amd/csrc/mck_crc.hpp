@@ -212,10 +212,10 @@ __device__ __forceinline__ uint32_t crc_lane_final(uint32_t s, const CrcLane& L)
 // 16-lane row (xor 1, xor 2, half-mirror, mirror), then the 4 row totals are
 // read out with v_readlane.  No LDS traffic.
 __device__ __forceinline__ uint32_t wave_xor32(uint32_t v) {
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true);  // row_mirror
   return (uint32_t)__builtin_amdgcn_readlane((int)v, 0) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 16) ^
          (uint32_t)__builtin_amdgcn_readlane((int)v, 32) ^ (uint32_t)__builtin_amdgcn_readlane((int)v, 48);
 }
@@ -312,7 +312,7 @@ template <int M, int CTRL>
 __device__ __forceinline__ void quad_xstep(uint32_t (&w)[4], int q) {
   uint32_t x[4];
 #pragma unroll
-  for (int j = 0; j < 4; j++) x[j] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)w[j ^ M], CTRL, 0xF, 0xF, false);
+  for (int j = 0; j < 4; j++) x[j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)w[j ^ M], CTRL, 0xF, 0xF, true);
 #pragma unroll
   for (int j = 0; j < 4; j++) w[j] = ((q ^ j) & M) ? x[j] : w[j];
 }
@@ -862,10 +862,10 @@ __device__ __forceinline__ uint32_t row_round(uint32_t s, ChunkN<P> ch, const Ro
 // XOR over the W lanes of each row, in every lane of the row (DPP).
 template <int W>
 __device__ __forceinline__ uint32_t row_xor32(uint32_t v) {
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
-  v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);  // quad_perm [2,3,0,1]
-  if (W >= 8) v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  if (W >= 16) v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, true);  // quad_perm [1,0,3,2]
+  v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, true);  // quad_perm [2,3,0,1]
+  if (W >= 8) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+  if (W >= 16) v ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x140, 0xF, 0xF, true);  // row_mirror
   return v;
 }
 

@@ -644,10 +644,10 @@ __device__ __forceinline__ uint4 il_align(const uint4& lo, const uint4& hi, uint
 template <int CTRL>
 __device__ __forceinline__ uint4 dpp_u32x4(const uint4& v) {
   uint4 r;
-  r.x = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, CTRL, 0xF, 0xF, false);
-  r.y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.y, CTRL, 0xF, 0xF, false);
-  r.z = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.z, CTRL, 0xF, 0xF, false);
-  r.w = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.w, CTRL, 0xF, 0xF, false);
+  r.x = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.x, CTRL, 0xF, 0xF, true);
+  r.y = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.y, CTRL, 0xF, 0xF, true);
+  r.z = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.z, CTRL, 0xF, 0xF, true);
+  r.w = (uint32_t)__builtin_amdgcn_mov_dpp((int)v.w, CTRL, 0xF, 0xF, true);
   return r;
 }
 constexpr int kDppRowRor15 = 0x12F;  // lane j of a row <- lane j + 1 (mod 16)

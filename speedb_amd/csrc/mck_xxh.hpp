@@ -266,8 +266,8 @@ __device__ __forceinline__ uint64_t xxph3_any(const uint8_t* in, uint64_t len, u
 // 64-bit DPP move (both halves with the same control)
 template <int CTRL>
 __device__ __forceinline__ uint64_t dpp64(uint64_t v) {
-  const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, false);
-  const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, CTRL, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, true);
   return ((uint64_t)hi << 32) | lo;
 }
 // sum over the 4 lanes of a row with the same (lane & 3): row_ror 4, 8
@@ -317,7 +317,7 @@ __device__ __forceinline__ uint4 rd_fix(const uint4& u, uint32_t d0, uint32_t se
 // call operands to branches, and the move would then read masked lanes)
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp32(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
 }
 constexpr int kDppRowRor1 = 0x121;   // lane j of a row <- lane j - 1 (mod 16)
 constexpr int kDppWaveShr1 = 0x138;  // lane l <- lane l - 1
@@ -344,7 +344,11 @@ struct X3Row {
   uint64_t i0, i1;        // XXH3_INIT_ACC
   uint64_t ko0, ko1;      // wave layout, lone partial segment: stripe lane>>2, pair q
   uint64_t seed;          // XXPH3 seed (0 for XXH3)
-  int lane, row, j, q, st4;
+  // wave layout: rows 0-1 carry accumulator 2q of the chain, rows 2-3
+  // accumulator 2q + 1 (role = lane >> 5), so a scramble instruction
+  // advances both accumulators of a pair at once
+  uint64_t ksw, iw;       // the role's scramble secret and initial value
+  int lane, row, j, q, st4, role;
 };
 __device__ __forceinline__ X3Row x3_row(uint64_t seed) {
   X3Row X;
@@ -371,6 +375,9 @@ __device__ __forceinline__ X3Row x3_row(uint64_t seed) {
   // INIT_ACC = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1}
   X.i0 = X.q == 0 ? (uint64_t)P32_3 : X.q == 1 ? P64_2 : X.q == 2 ? P64_4 : P64_5;
   X.i1 = X.q == 0 ? P64_1 : X.q == 1 ? P64_3 : X.q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+  X.role = X.lane >> 5;
+  X.ksw = X.role ? X.ks1 : X.ks0;
+  X.iw = X.role ? X.i1 : X.i0;
   return X;
 }
 
@@ -643,12 +650,15 @@ __device__ __forceinline__ X3WLoads x3w_load(const X3WSpan& sp, uint32_t k, cons
   return L;
 }
 
-// Fold unit k of the span into (a0, a1); after the last unit, merge, finish
-// and reset the accumulators.
+// Fold unit k of the span into the lane's accumulator a (accumulator 2q in
+// rows 0-1, 2q + 1 in rows 2-3: X.role); after the last unit, merge, finish
+// and reset it.  tx: the wave's 1 KiB LDS buffer (free: the parked sums are
+// chained).
 template <class Op, bool PREVIEW>
 __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32_t k, X3WLoads L,
-                                         const X3Row& X, uint64_t& a0, uint64_t& a1, const typename Op::Pre& e) {
+                                         const X3Row& X, uint64_t& a, const typename Op::Pre& e, uint64_t* tx) {
   const uint32_t sel = rd_sel(rd_shift(sp.ptr));
+  const bool r1 = X.role != 0;
   if (k < sp.rounds) {  // wave-uniform
     const uint32_t g = 4 * k + X.row;
     if (sp.ptr & 3) rd_fix_row(L.d, L.e0, X.j, sel);  // wave-uniform: dword-aligned spans need no fix
@@ -664,22 +674,27 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
     }
     c0 = row_sum_st4(c0);
     c1 = row_sum_st4(c1);
-    // row 0 gathers the four rows' sums in segment order: rows 0, 1
-    // (lane ^ 16), 2 (lane ^ 32), 3 (lane ^ 48); only row 0's accumulators
-    // are used
-    const uint64_t e0 = xl16_64(c0), e1 = xl16_64(c1);
-    const uint64_t C0[4] = {c0, e0, xl32_64(c0), xl32_64(e0)};
-    const uint64_t C1[4] = {c1, e1, xl32_64(c1), xl32_64(e1)};
+    // Rows 0 (role 0) and 2 (role 1) gather the four rows' sums of their
+    // accumulator in segment order, through LDS (tx[role][q][row]: one
+    // 8-byte store per row and accumulator, two 16-byte reads -- the
+    // v_permlane16/32 transposes cost ~30 VALU a unit); rows 1 and 3 compute
+    // an unused chain.
+    if (X.st4 == 0) {
+      tx[4 * X.q + X.row] = c0;
+      tx[64 + 4 * X.q + X.row] = c1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    const ulonglong2* tr = reinterpret_cast<const ulonglong2*>(tx + 64 * X.role + 4 * X.q);
+    const ulonglong2 t01 = tr[0], t23 = tr[1];
+    const uint64_t T[4] = {t01.x, t01.y, t23.x, t23.y};
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const uint32_t gr = 4 * k + r;
       if (gr > sp.nb) break;  // wave-uniform
-      a0 += C0[r];
-      a1 += C1[r];
-      if (gr < sp.nb) {
-        a0 = xxh3_scramble(a0, X.ks0);
-        a1 = xxh3_scramble(a1, X.ks1);
-      }
+      a += T[r];
+      if (gr < sp.nb) a = xxh3_scramble(a, X.ksw);
     }
   }
   if (k + 1 < sp.units) return;  // wave-uniform
@@ -699,8 +714,9 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
     c1 = row_sum_st4(c1);
     c0 += xl16_64(c0);
     c1 += xl16_64(c1);
-    a0 += c0 + xl32_64(c0);
-    a1 += c1 + xl32_64(c1);
+    c0 += xl32_64(c0);  // the wave's sum, in every lane
+    c1 += xl32_64(c1);
+    a += r1 ? c1 : c0;
   }
   uint4 dl = L.dl;
   if ((sp.ptr + sp.len) & 3) {  // wave-uniform: the last stripe's own alignment
@@ -708,15 +724,16 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
     dl = rd_fix(L.dl, X.q ? pl : L.el, rd_sel(rd_shift(sp.ptr + sp.len - 64)));
   }
   const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
-  if (sp.tail) {
-    a0 += (PREVIEW ? l0 : l1) + mul32to64(l0 ^ X.kl0);
-    a1 += (PREVIEW ? l1 : l0) + mul32to64(l1 ^ X.kl1);
+  if (sp.tail) {  // the role's word and secret
+    const uint64_t lw = r1 ? l1 : l0, lo = r1 ? l0 : l1;
+    a += (PREVIEW ? lw : lo) + mul32to64(lw ^ (r1 ? X.kl1 : X.kl0));
   }
-  const uint64_t m = quad_sum(mul128_fold64(a0 ^ X.km0, a1 ^ X.km1));
+  // row 0's lanes take accumulator 2q + 1 from row 2 (lane ^ 32)
+  const uint64_t b = xl32_64(a);
+  const uint64_t m = quad_sum(mul128_fold64(a ^ X.km0, b ^ X.km1));
   const uint64_t h = PREVIEW ? xxph3_avalanche(sp.len * P64_1 + m) : xxh3_avalanche(sp.len * P64_1 + m);
   if (X.lane == 0) op.finish(sp.i, h, e);
-  a0 = X.i0;
-  a1 = X.i1;
+  a = X.iw;
 }
 
 // Every unit issues all its loads -- the four round loads, the lone partial
@@ -732,9 +749,8 @@ __device__ __forceinline__ void x3w_fold(const Op& op, const X3WSpan& sp, uint32
 // addresses, no per-stripe masks, no lone-segment / last-stripe / epilogue
 // loads: four 16-byte loads at one base + 256 B immediates (+ the dword
 // before the row's segment when the span is byte-misaligned) and the fold.
-// x3w_round_c: the round's four segment sums C_g (row 0's lanes hold segments
-// 4k .. 4k + 3 in order, for their accumulator pair q); x3w_full_round
-// chains them into the accumulators.
+// x3w_round_sums: the round's segment sums (row r's lanes: segment 4k + r,
+// their accumulator pair q).
 struct X3RoundLoads {
   uint4 d[4];
   uint32_t e0;  // the dword before the row's segment (byte-misaligned spans)
@@ -752,44 +768,20 @@ __device__ __forceinline__ X3RoundLoads x3w_round_load(const X3WSpan& sp, uint32
   return R;
 }
 template <bool PREVIEW>
-__device__ __forceinline__ void x3w_round_sums(const X3WSpan& sp, X3RoundLoads R, const X3Row& X,
-                                               uint64_t (&C0)[4], uint64_t (&C1)[4]) {
+__device__ __forceinline__ void x3w_round_sums(const X3WSpan& sp, X3RoundLoads R, const X3Row& X, uint64_t& c0,
+                                               uint64_t& c1) {
   uint4(&d)[4] = R.d;
   if (sp.ptr & 3) rd_fix_row(d, R.e0, X.j, rd_sel(rd_shift(sp.ptr)));  // wave-uniform
-  uint64_t c0 = 0, c1 = 0;
+  c0 = 0;
+  c1 = 0;
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const uint64_t d0 = ((uint64_t)d[m].y << 32) | d[m].x, d1 = ((uint64_t)d[m].w << 32) | d[m].z;
     c0 += (PREVIEW ? d0 : d1) + mul32to64(d0 ^ X.k0[m]);
     c1 += (PREVIEW ? d1 : d0) + mul32to64(d1 ^ X.k1[m]);
   }
-  c0 = row_sum_st4(c0);
+  c0 = row_sum_st4(c0);  // segment 4k + row's sums, in every lane of the row
   c1 = row_sum_st4(c1);
-  const uint64_t e0 = xl16_64(c0), e1 = xl16_64(c1);
-  C0[0] = c0;
-  C0[1] = e0;
-  C0[2] = xl32_64(c0);
-  C0[3] = xl32_64(e0);
-  C1[0] = c1;
-  C1[1] = e1;
-  C1[2] = xl32_64(c1);
-  C1[3] = xl32_64(e1);
-}
-template <bool PREVIEW>
-__device__ __forceinline__ void x3w_round_c(const X3WSpan& sp, uint32_t k, const X3Row& X, uint64_t (&C0)[4],
-                                            uint64_t (&C1)[4]) {
-  x3w_round_sums<PREVIEW>(sp, x3w_round_load(sp, k, X), X, C0, C1);
-}
-template <bool PREVIEW>
-__device__ __forceinline__ void x3w_full_round(const X3WSpan& sp, uint32_t k, const X3Row& X, uint64_t& a0,
-                                               uint64_t& a1) {
-  uint64_t C0[4], C1[4];
-  x3w_round_c<PREVIEW>(sp, k, X, C0, C1);
-#pragma unroll
-  for (int r = 0; r < 4; r++) {
-    a0 = xxh3_scramble(a0 + C0[r], X.ks0);
-    a1 = xxh3_scramble(a1 + C1[r], X.ks1);
-  }
 }
 
 // ---- long spans in pieces (round 3) -----------------------------------------
@@ -869,38 +861,35 @@ template <bool PREVIEW>
 __device__ __forceinline__ void x3p_park(const X3WSpan& sp, uint32_t k0, uint32_t ke, const X3Row& X,
                                          ulonglong2 (*cs)[4]) {
   for (uint32_t k = k0; k < ke; k++) {
-    uint64_t C0[4], C1[4];
-    x3w_round_c<PREVIEW>(sp, k, X, C0, C1);
-    if (X.lane < 4) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) cs[4 * (k - k0) + r][X.q] = make_ulonglong2(C0[r], C1[r]);
-    }
+    uint64_t c0, c1;
+    x3w_round_sums<PREVIEW>(sp, x3w_round_load(sp, k, X), X, c0, c1);
+    // each row parks its own segment's sums (lanes st4 = 0 of the row)
+    if (X.st4 == 0) cs[4 * (k - k0) + X.row][X.q] = make_ulonglong2(c0, c1);
   }
 }
 // Wait for piece p - 1 of span t, then chain the parked segments.
 __device__ __forceinline__ void x3p_chain(X3Lds* s, uint32_t t, uint32_t p, uint32_t segs, const X3Row& X,
-                                          ulonglong2 (*cs)[4], uint64_t& a0, uint64_t& a1) {
+                                          ulonglong2 (*cs)[4], uint64_t& a) {
   if (p) {
     while (__builtin_amdgcn_readfirstlane(
                __hip_atomic_load(&s->done[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) != p)
       __builtin_amdgcn_s_sleep(1);
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    const ulonglong2 a = s->acc[t][X.q];
-    a0 = a.x;
-    a1 = a.y;
+    const ulonglong2 v = s->acc[t][X.q];
+    a = X.role ? v.y : v.x;
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");  // the parked sums to the other lanes
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
   for (uint32_t g = 0; g < segs; g++) {
     const ulonglong2 c = cs[g][X.q];
-    a0 = xxh3_scramble(a0 + c.x, X.ks0);
-    a1 = xxh3_scramble(a1 + c.y, X.ks1);
+    a = xxh3_scramble(a + (X.role ? c.y : c.x), X.ksw);
   }
 }
-__device__ __forceinline__ void x3p_publish(X3Lds* s, uint32_t t, uint32_t p, const X3Row& X, uint64_t a0,
-                                            uint64_t a1) {
-  if (X.lane < 4) s->acc[t][X.q] = make_ulonglong2(a0, a1);
+__device__ __forceinline__ void x3p_publish(X3Lds* s, uint32_t t, uint32_t p, const X3Row& X, uint64_t a) {
+  // accumulator 2q from row 0 (lanes 0-3), 2q + 1 from row 2 (lanes 32-35)
+  if (X.lane < 4) s->acc[t][X.q].x = a;
+  if (X.lane >= 32 && X.lane < 36) s->acc[t][X.q].y = a;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   if (X.lane == 0) __hip_atomic_store(&s->done[t], p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
@@ -911,7 +900,7 @@ __device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, c
   X3Piece pc;
   while (f.template next<PREVIEW>(pc)) {
     const X3WSpan& cur = pc.sp;
-    uint64_t a0 = X.i0, a1 = X.i1;
+    uint64_t a = X.iw;
     // a whole span (np = 1) is its own last piece: the same code
     const uint32_t kl = cur.units - 1;  // the last unit
     const uint32_t k0 = pc.p * kX3PieceRounds;
@@ -919,14 +908,14 @@ __device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, c
     const uint32_t ke = last ? kl : k0 + kX3PieceRounds;
     x3p_park<PREVIEW>(cur, k0, ke, X, cs);
     if (!last) {
-      x3p_chain(f.s, pc.t, pc.p, 4 * kX3PieceRounds, X, cs, a0, a1);
-      x3p_publish(f.s, pc.t, pc.p, X, a0, a1);
+      x3p_chain(f.s, pc.t, pc.p, 4 * kX3PieceRounds, X, cs, a);
+      x3p_publish(f.s, pc.t, pc.p, X, a);
       continue;
     }
     const X3WLoads L = x3w_load(cur, kl, X);
     const typename Op::Pre e = op.pre(cur.i, cur.ptr, cur.len);
-    x3p_chain(f.s, pc.t, pc.p, 4 * (kl - k0), X, cs, a0, a1);
-    x3w_fold<Op, PREVIEW>(op, cur, kl, L, X, a0, a1, e);
+    x3p_chain(f.s, pc.t, pc.p, 4 * (kl - k0), X, cs, a);
+    x3w_fold<Op, PREVIEW>(op, cur, kl, L, X, a, e, reinterpret_cast<uint64_t*>(cs));
   }
 }
 
