@@ -128,6 +128,8 @@ def parse():
     p.add_argument("--kvs", type=int, default=1 << 22, help="KVs per GPU (kv)")
     p.add_argument("--kv-value-bytes", type=int, default=1000, help="value bytes (blockkv)")
     p.add_argument("--kv-prot-bytes", type=int, default=8, help="protection_bytes_per_key (blockkv)")
+    p.add_argument("--kv-two-pass", action="store_true",
+                   help="blockkv: the layout + protect pair (host readback between) instead of the one-pass call")
     p.add_argument("--span-min", type=int, default=100, help="smallest span (walrec, ragged)")
     p.add_argument("--span-max", type=int, default=1100, help="largest span (walrec, ragged)")
     p.add_argument("--span-bytes", type=int, default=1 << 30, help="span bytes per GPU (walrec, ragged)")
@@ -597,27 +599,42 @@ def make_workload(args, dev, rank, world):
         nkeys = int(db.keys_per_block.sum())
         kbytes = sum(len(k) for e in db.entries for k, _ in e) * (n // db.distinct) + sum(
             len(k) for e in db.entries[:n % db.distinct] for k, _ in e)
-        work = torch.empty(int(L.mck_block_kv_work_bytes(nkeys, kbytes)), dtype=torch.uint8, device=dev)
-        out = torch.empty(nkeys * pb, dtype=torch.uint8, device=dev)
-        tot = torch.empty(2, dtype=torch.int64, pin_memory=True)
         sp = db.spans.c()
+        if args.kv_two_pass:
+            work = torch.empty(int(L.mck_block_kv_work_bytes(nkeys, kbytes)), dtype=torch.uint8, device=dev)
+            out = torch.empty(nkeys * pb, dtype=torch.uint8, device=dev)
+            tot = torch.empty(2, dtype=torch.int64, pin_memory=True)
 
-        def step():
-            _lib.check(L.mck_block_kv_layout_batch(0, ctypes.byref(sp), kbase.data_ptr(), abase.data_ptr(),
-                                                   rint.data_ptr(),
-                                                   status.data_ptr(), scratch.data_ptr(), stream.cuda_stream),
-                       "mck_block_kv_layout_batch")
-            # the totals size the work area: one 16-byte readback per batch
-            tot[0].copy_(kbase[n], non_blocking=True)
-            tot[1].copy_(abase[n], non_blocking=True)
-            stream.synchronize()
-            assert int(tot[0]) == nkeys and int(tot[1]) == kbytes
-            _lib.check(L.mck_block_kv_protect_batch(0, ctypes.byref(sp), pb, kbase.data_ptr(), abase.data_ptr(),
-                                                    rint.data_ptr(), nkeys, work.data_ptr(), out.data_ptr(), stream.cuda_stream),
-                       "mck_block_kv_protect_batch")
+            def step():
+                _lib.check(L.mck_block_kv_layout_batch(0, ctypes.byref(sp), kbase.data_ptr(), abase.data_ptr(),
+                                                       rint.data_ptr(),
+                                                       status.data_ptr(), scratch.data_ptr(), stream.cuda_stream),
+                           "mck_block_kv_layout_batch")
+                # the totals size the work area: one 16-byte readback per batch
+                tot[0].copy_(kbase[n], non_blocking=True)
+                tot[1].copy_(abase[n], non_blocking=True)
+                stream.synchronize()
+                assert int(tot[0]) == nkeys and int(tot[1]) == kbytes
+                _lib.check(L.mck_block_kv_protect_batch(0, ctypes.byref(sp), pb, kbase.data_ptr(), abase.data_ptr(),
+                                                        rint.data_ptr(), nkeys, work.data_ptr(), out.data_ptr(),
+                                                        stream.cuda_stream),
+                           "mck_block_kv_protect_batch")
+            w.kernel = ("k_block_layout_t + k_blk_scan + k_block_kv_t + k_block_long_rows "
+                        "(whole step, incl. the totals readback)")
+        else:
+            # one pass: slots sized to the batch's largest block (entries)
+            slot_cap = int(db.keys_per_block.max())
+            work = torch.empty(int(L.mck_block_kv_blocks_work_bytes(n, slot_cap, 0)), dtype=torch.uint8, device=dev)
+            out = torch.empty(n * slot_cap * pb, dtype=torch.uint8, device=dev)
+
+            def step():
+                _lib.check(L.mck_block_kv_protect_blocks_batch(0, ctypes.byref(sp), pb, slot_cap, 0, kbase.data_ptr(),
+                                                               abase.data_ptr(), rint.data_ptr(), status.data_ptr(),
+                                                               work.data_ptr(), out.data_ptr(), stream.cuda_stream),
+                           "mck_block_kv_protect_blocks_batch")
+            w.kernel = ("k_block_kv_walk + k_blk_scan + k_block_kv_flush + k_block_long_rows "
+                        "(whole step: mck_block_kv_protect_blocks_batch)")
         w.step = step
-        w.kernel = ("k_block_layout_t + k_blk_scan + k_block_kv_t + k_block_long_rows "
-                    "(whole step, incl. the totals readback)")
         w.span_bytes = db.block_bytes
         # what the step must move: every block read once, the kv_checksum
         # array written (+ 8 B offset, 4 B length per block in, 8 B key base
@@ -628,7 +645,8 @@ def make_workload(args, dev, rank, world):
                   f"restart interval 16, {len(db.entries[0][0][0])} B internal keys, {args.kv_value_bytes} B "
                   f"values, {nkeys} entries), protection_bytes_per_key {pb}: "
                   "Block::InitializeDataBlockProtectionInfo (SURVEY.md 8f row 4)")
-        w.cfg = {"blocks_per_gpu": n, "entries": nkeys, "value_bytes": args.kv_value_bytes, "prot_bytes": pb}
+        w.cfg = {"blocks_per_gpu": n, "entries": nkeys, "value_bytes": args.kv_value_bytes, "prot_bytes": pb,
+                 "path": "two-pass" if args.kv_two_pass else "one-pass"}
 
         def check():
             # sampled entries == ProtectKV composed from scalar NPHash64 calls

@@ -562,6 +562,10 @@ int mck_handoff_checksum_batch(const mck_spans* pieces, uint32_t* out,
                                     fewer or more than block_restart_interval
                                     entries): the reference only asserts these
                                     and its output is undefined there          */
+#define MCK_BLOCK_SLOT_OVERFLOW 4 /* one-pass entry points only: more than
+                                     slot_cap entries, or a key longer than
+                                     128 bytes and arena_cap; protect the
+                                     block with the two-pass pair instead     */
 
 /* Scratch for mck_block_kv_layout_batch (device bytes). */
 uint64_t mck_block_kv_scratch_bytes(uint32_t count);
@@ -602,6 +606,36 @@ int mck_block_kv_verify_batch(int kind, const mck_spans* blocks,
                               const uint8_t* stored,
                               uint8_t* mismatch, uint32_t* mismatch_count,
                               mck_stream_t stream);
+
+/* One pass (layout + protection in one walk of every block, no host
+ * round trip): the outputs of mck_block_kv_layout_batch (key_base,
+ * arena_base, restart_interval, status) and of mck_block_kv_protect_batch
+ * (out, laid out by key_base) from one call.  Every block's entries are
+ * parked in `slot_cap` 16-byte slots of the work area until the key index is
+ * known; keys over 128 bytes use an `arena_cap`-byte slice per block.  A
+ * block that does not fit gets MCK_BLOCK_SLOT_OVERFLOW and no keys.
+ * out: count * slot_cap * prot_bytes bytes (room for any outcome; the
+ * first key_base[count] * prot_bytes are written). */
+uint64_t mck_block_kv_blocks_work_bytes(uint32_t count, uint32_t slot_cap,
+                                        uint32_t arena_cap);
+int mck_block_kv_protect_blocks_batch(int kind, const mck_spans* blocks,
+                                      uint32_t prot_bytes, uint32_t slot_cap,
+                                      uint32_t arena_cap, uint64_t* key_base,
+                                      uint64_t* arena_base,
+                                      uint32_t* restart_interval,
+                                      int32_t* status, void* work,
+                                      uint8_t* out, mck_stream_t stream);
+/* ... and the read-side check in one pass: mismatch[key] as
+ * mck_block_kv_verify_batch (mismatch: count * slot_cap bytes). */
+int mck_block_kv_verify_blocks_batch(int kind, const mck_spans* blocks,
+                                     uint32_t prot_bytes, uint32_t slot_cap,
+                                     uint32_t arena_cap, uint64_t* key_base,
+                                     uint64_t* arena_base,
+                                     uint32_t* restart_interval,
+                                     int32_t* status, void* work,
+                                     const uint8_t* stored, uint8_t* mismatch,
+                                     uint32_t* mismatch_count,
+                                     mck_stream_t stream);
 
 /* ---- SST files: whole-file verification ------------- */
 

@@ -105,6 +105,13 @@ SIGNATURES = [
     ("mck_block_kv_verify_batch", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, vp, vp, vp, ctypes.c_uint64, vp, vp, vp,
       vp, vp]),
+    ("mck_block_kv_blocks_work_bytes", ctypes.c_uint64, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32]),
+    ("mck_block_kv_protect_blocks_batch", ctypes.c_int,
+     [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp,
+      vp, vp, vp]),
+    ("mck_block_kv_verify_blocks_batch", ctypes.c_int,
+     [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp,
+      vp, vp, vp, vp, vp]),
     ("mck_sst_decode_footer", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
     ("mck_sst_list_blocks", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
     ("mck_sst_verify_footer", ctypes.c_int, [vp, vp]),

@@ -35,6 +35,13 @@ class BlockStatus(enum.IntEnum):
     kBadContents = 1
     kBadEntry = 2
     kBadRestarts = 3
+    kSlotOverflow = 4  # one-pass entry points only: the block goes to the two-pass pair
+
+
+# one-pass defaults: entries parked per block, arena bytes per block for keys
+# over 128 bytes (a batch with a block beyond either runs the two-pass pair)
+DEFAULT_SLOT_CAP = 64
+DEFAULT_ARENA_CAP = 0
 
 
 _MESSAGES = {
@@ -59,6 +66,8 @@ class BlockProtection:
     total_key_bytes: int
     work: object              # uint8 work area (device), reused by verify
     kv_checksum: object       # uint8 [total_keys * protection_bytes_per_key] (device)
+    slot_cap: int = 0         # > 0: built by the one-pass entry point (verify uses it too)
+    arena_cap: int = 0
 
     def block_status(self, i: int) -> Status:
         st = BlockStatus(int(self.status[i]))
@@ -93,10 +102,51 @@ def _work(total_keys: int, total_key_bytes: int, device):
     return torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
 
 
-def InitializeBlockProtectionInfo(kind: int, blocks: Spans, protection_bytes_per_key: int,
-                                  stream=None) -> BlockProtection:
-    """Per-KV checksums of every entry of every block in ``blocks``."""
+def _blocks_outputs(blocks: Spans, slot_cap: int, arena_cap: int):
     torch = _torch()
+    dev = blocks.base.device
+    n = blocks.count
+    key_base = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    arena_base = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    interval = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    nbytes = int(lib.mck_block_kv_blocks_work_bytes(n, slot_cap, arena_cap))
+    work = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=dev)
+    return key_base, arena_base, status, interval, work
+
+
+def InitializeBlockProtectionInfoOnePass(kind: int, blocks: Spans, protection_bytes_per_key: int,
+                                         slot_cap: int = DEFAULT_SLOT_CAP, arena_cap: int = DEFAULT_ARENA_CAP,
+                                         stream=None) -> BlockProtection:
+    """mck_block_kv_protect_blocks_batch: layout and protection in one walk
+    of every block.  Blocks beyond ``slot_cap`` entries (or with a key over
+    128 bytes and ``arena_cap``) come back kSlotOverflow with no keys."""
+    torch = _torch()
+    n = blocks.count
+    key_base, arena_base, status, interval, work = _blocks_outputs(blocks, slot_cap, arena_cap)
+    out = torch.empty(max(n * slot_cap * protection_bytes_per_key, 1), dtype=torch.uint8, device=blocks.base.device)
+    s = blocks.c()
+    check(lib.mck_block_kv_protect_blocks_batch(int(kind), ctypes.byref(s), protection_bytes_per_key, slot_cap,
+                                                arena_cap, key_base.data_ptr(), arena_base.data_ptr(),
+                                                interval.data_ptr(), status.data_ptr(), work.data_ptr(),
+                                                out.data_ptr(), _stream(stream)),
+          "mck_block_kv_protect_blocks_batch")
+    totals = torch.stack([key_base[n], arena_base[n]]).cpu()
+    nk, nkb = int(totals[0]), int(totals[1])
+    return BlockProtection(BlockKind(kind), protection_bytes_per_key, key_base, arena_base, status[:n],
+                           interval[:n], nk, nkb, work, out[:nk * protection_bytes_per_key], slot_cap, arena_cap)
+
+
+def InitializeBlockProtectionInfo(kind: int, blocks: Spans, protection_bytes_per_key: int,
+                                  stream=None, one_pass: bool = True) -> BlockProtection:
+    """Per-KV checksums of every entry of every block in ``blocks``: the
+    one-pass entry point, or the two-pass pair when a block does not fit its
+    slots (or ``one_pass`` is False)."""
+    torch = _torch()
+    if one_pass and blocks.count:
+        prot = InitializeBlockProtectionInfoOnePass(kind, blocks, protection_bytes_per_key, stream=stream)
+        if not bool((prot.status == int(BlockStatus.kSlotOverflow)).any().item()):
+            return prot
     key_base, arena_base, status, interval, nk, nkb = _layout(kind, blocks, stream)
     work = _work(nk, nkb, blocks.base.device)
     out = torch.empty(max(nk * protection_bytes_per_key, 1), dtype=torch.uint8, device=blocks.base.device)
@@ -136,9 +186,20 @@ def VerifyBlockProtectionInfo(blocks: Spans, prot: BlockProtection, stored=None,
     torch = _torch()
     dev = blocks.base.device
     stored = prot.kv_checksum if stored is None else stored
-    mismatch = torch.empty(max(prot.total_keys, 1), dtype=torch.uint8, device=dev)
     count = torch.zeros(1, dtype=torch.int32, device=dev)
     s = blocks.c()
+    if prot.slot_cap:  # one pass: the walk again, compared instead of stored
+        n = blocks.count
+        key_base, arena_base, status, interval, work = _blocks_outputs(blocks, prot.slot_cap, prot.arena_cap)
+        mismatch = torch.empty(max(n * prot.slot_cap, 1), dtype=torch.uint8, device=dev)
+        check(lib.mck_block_kv_verify_blocks_batch(int(prot.kind), ctypes.byref(s), prot.protection_bytes_per_key,
+                                                   prot.slot_cap, prot.arena_cap, key_base.data_ptr(),
+                                                   arena_base.data_ptr(), interval.data_ptr(), status.data_ptr(),
+                                                   work.data_ptr(), stored.data_ptr(), mismatch.data_ptr(),
+                                                   count.data_ptr(), _stream(stream)),
+              "mck_block_kv_verify_blocks_batch")
+        return mismatch[:prot.total_keys], count
+    mismatch = torch.empty(max(prot.total_keys, 1), dtype=torch.uint8, device=dev)
     check(lib.mck_block_kv_verify_batch(int(prot.kind), ctypes.byref(s), prot.protection_bytes_per_key,
                                         prot.key_base.data_ptr(), prot.arena_base.data_ptr(),
                                         prot.restart_interval.data_ptr(), prot.total_keys,

@@ -812,6 +812,303 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
   if (__ballot(any_long) && lane == 0) long_len[K_total] = 1u;
 }
 
+// ---- one pass (round 4): layout and protection in the same walk ------------
+// The two-pass pair above reads every block twice: k_block_layout_t's walk
+// touches every 128-byte line (one entry header per ~line at 100-byte
+// values) only to count entries for the key index, then k_block_kv_t walks
+// again -- 100-B values: 4.2 + 8.3 GB of HBM reads for a 4.3 GB image, the
+// layout pass a third of the step.  k_block_kv_walk does the layout checks
+// and the hashing in ONE walk and parks every entry's hash (without a long
+// value's) in a per-block SLOT (slot_cap entries per block, rounded up to
+// even: 8 bytes each, stored in 16-byte pairs as k_block_kv_t's output) and
+// a long value's offset/length beside it; the scan of the counts gives the
+// key index, and k_block_kv_flush moves the slots to the kv_checksum array
+// (coalesced: a thread per slot pair).  A block with more than slot_cap
+// entries, or a key longer than the LDS buffer and arena_cap, gets
+// MCK_BLOCK_SLOT_OVERFLOW and no keys; the caller protects it with the
+// two-pass pair.
+constexpr int kBlkSlotOverflow = 4;
+
+// Entry e of block b: slot_h[b * stride + e] = the hash without the long
+// value's; slot_m[...] = (value offset in block << 32 | length), written for
+// long values only; bit e of the block's long mask (blk_long, stride / 32
+// words per block, rounded up) marks them.
+__host__ __device__ __forceinline__ uint32_t blk_slot_stride(uint32_t slot_cap) { return (slot_cap + 1) & ~1u; }
+__host__ __device__ __forceinline__ uint32_t blk_long_words(uint32_t slot_cap) {
+  return (blk_slot_stride(slot_cap) + 31) / 32;
+}
+
+template <int KIND>
+__global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t count, uint32_t slot_cap,
+                                                       uint8_t* arena, uint32_t arena_cap, uint64_t* slot_h,
+                                                       uint64_t* slot_m, uint32_t* blk_long, uint64_t* key_cnt,
+                                                       uint64_t* key_bytes, uint32_t* interval_out,
+                                                       int32_t* status, uint32_t* long_flag) {
+  __shared__ uint32_t s_key[256][kBlkKeyBuf / 4 + 5];  // as k_block_kv_t
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  uint8_t* const lkey = reinterpret_cast<uint8_t*>(s_key[threadIdx.x]);
+  const bool in = b < count;
+  const GblRd rd{in ? blocks.ptr(b) : nullptr};
+  const uint64_t n64 = in ? blocks.len(b) : 0;
+  // ---- the block's header and restart array: blk_seq_walk's checks
+  int st = kBlkOk;
+  BlkHdr h{0, 0, false};
+  bool active = false;
+  if (in) {
+    h = rd_header(rd, n64);
+    if (!h.ok) {
+      st = kBlkBadContents;
+    } else if (h.nr != 0) {
+      // four restart words per round trip (a loop of dependent-exit loads
+      // was one round trip per restart point)
+      uint32_t prev = 0;
+      for (uint32_t r0 = 0; r0 < h.nr && st == kBlkOk; r0 += 4) {
+        uint32_t x[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) x[j] = r0 + j < h.nr ? rd.u32(h.ro + 4 * (r0 + j)) : 0u;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          const uint32_t r = r0 + j;
+          if (r < h.nr && st == kBlkOk && (r == 0 ? (h.ro != 0 && x[j] != 0) : (x[j] <= prev || x[j] >= h.ro)))
+            st = kBlkBadRestarts;
+          prev = x[j];
+        }
+      }
+      if (st == kBlkOk && h.ro == 0 && h.nr != 1) st = kBlkBadRestarts;
+      active = st == kBlkOk && h.ro != 0;
+    }
+  }
+  const uint32_t n = (uint32_t)n64, ro = h.ro, nr = h.nr;
+  uint8_t* const gkey = arena + (uint64_t)(in ? b : 0) * arena_cap;
+  bool global_key = false;
+  const uint64_t oklo = sec64(16 * (int)(lane & 7)) + kSeedV, okhi = sec64(16 * (int)(lane & 7) + 8) - kSeedV;
+  const uint64_t sbase = (uint64_t)(in ? b : 0) * blk_slot_stride(slot_cap);
+  uint64_t pend = 0;  // the lane's even entry, stored with the odd one after it
+  uint32_t lmask = 0;  // long entries of the current 32
+  uint32_t* const lwords = blk_long + (uint64_t)(in ? b : 0) * blk_long_words(slot_cap);
+  uint32_t p = 0, idx = 0, interval = 0, in_cur = 0, r = 0, kl = 0;
+  // restart point r and, loaded one restart ahead, r + 1
+  uint32_t next = active ? rd.u32(ro) : 0u;
+  uint32_t nextn = active && nr > 1 ? rd.u32(ro + 4) : 0xFFFFFFFFu;
+  uint64_t kbytes = 0;
+  // the next entry's first 16 bytes, one entry ahead (k_block_kv_t)
+  uint4 U = make_uint4(0, 0, 0, 0);
+  bool uok = false;
+  bool any_long = false;
+  if (active) {
+    uok = n >= 16;
+    if (uok) U = vload16_any(reinterpret_cast<uint64_t>(rd.p));
+  }
+  while (__any(active)) {
+    uint32_t sh = 0, ns = 0, q = 0, v = 0, vl = 0;
+    uint32_t kw[4] = {0, 0, 0, 0};
+    bool vmid = false;
+    if (active) {
+      // block.cc:1091-1132 with the restart checks of blk_seq_walk
+      int err = kBlkOk;
+      if (r < nr && p > next) err = kBlkBadRestarts;  // a restart point inside an entry
+      const bool at_restart = r < nr && p == next;
+      if (err == kBlkOk && at_restart) {
+        if (r == 1)
+          interval = in_cur;
+        else if (r > 1 && in_cur != interval)
+          err = kBlkBadRestarts;
+        in_cur = 0;
+        r++;
+        next = nextn;
+        nextn = r + 1 < nr ? rd.u32(ro + 4 * (r + 1)) : 0xFFFFFFFFu;
+      }
+      const uint4 Uc = U;
+      bool fast = false;
+      if (err == kBlkOk) {
+        if (KIND != kBlkIndexDelta && KIND != kBlkIndexDeltaFk && uok && (Uc.x & 0x808080u) == 0) {
+          const uint32_t kk = (Uc.x >> 8) & 255u, xx = (Uc.x >> 16) & 255u;
+          if (p <= ro && ro - p >= 3 && ro - (p + 3) >= kk + xx) {
+            sh = Uc.x & 255u;
+            ns = kk;
+            q = p + 3;
+            v = q + kk;
+            vl = xx;
+            fast = true;
+          }
+        }
+        if (!fast && !rd_entry<KIND>(rd, p, ro, &sh, &ns, &q, &v, &vl)) err = kBlkBadEntry;
+      }
+      if (err == kBlkOk && at_restart && sh != 0) err = r == 1 ? kBlkBadEntry : kBlkBadRestarts;
+      if (err == kBlkOk && kl < sh) err = kBlkBadEntry;
+      if (err == kBlkOk && idx >= slot_cap) err = kBlkSlotOverflow;
+      if (err == kBlkOk && !global_key && sh + ns > kBlkKeyBuf && sh + ns > arena_cap) err = kBlkSlotOverflow;
+      if (err == kBlkOk && global_key && sh + ns > arena_cap) err = kBlkSlotOverflow;
+      if (err != kBlkOk) {
+        st = err;
+        active = false;
+      } else {
+        const uint32_t pn = v + vl;
+        if (pn < ro) {
+          uok = pn + 16 <= n;
+          if (uok) U = vload16_any(reinterpret_cast<uint64_t>(rd.p + pn));
+        }
+        if (fast) {
+          const uint32_t e = ns > 13 ? rd.u32(p + 16) : 0u;
+          kw[0] = __builtin_amdgcn_alignbyte(Uc.y, Uc.x, 3);
+          kw[1] = __builtin_amdgcn_alignbyte(Uc.z, Uc.y, 3);
+          kw[2] = __builtin_amdgcn_alignbyte(Uc.w, Uc.z, 3);
+          kw[3] = __builtin_amdgcn_alignbyte(e, Uc.w, 3);
+        } else {
+          const uint64_t k01 = rd.u64(q), k23 = rd.u64(ns > 8 ? q + 8 : q);
+          kw[0] = (uint32_t)k01;
+          kw[1] = (uint32_t)(k01 >> 32);
+          kw[2] = (uint32_t)k23;
+          kw[3] = (uint32_t)(k23 >> 32);
+        }
+        vmid = vl > 16 && vl <= 128;
+      }
+    }
+    uint64_t hv;
+    {
+      const uint64_t hm = xp_mid_octets(reinterpret_cast<uint64_t>(rd.p) + v, vl, vmid, oklo, okhi, lane);
+      hv = vmid ? hm : 0ull;
+    }
+    const bool lng = active && vl >= kBlkLong;
+    if (active) {
+      const uint32_t kn = sh + ns;
+      if (!global_key && kn > kBlkKeyBuf) {  // rare: move the prefix to the block's arena slot
+        for (uint32_t i = 0; i < sh; i++) gkey[i] = lkey[i];
+        global_key = true;
+      }
+      if (!global_key) {  // IterKey::TrimAppend in the LDS buffer (k_block_kv_t)
+        {
+          uint32_t* kd = s_key[threadIdx.x] + (sh >> 2);
+          const uint32_t s4 = sh & 3u, sb = 4u - s4;
+          const uint32_t prev = s4 ? kd[0] << (8 * sb) : 0u;
+          kd[0] = s4 ? __builtin_amdgcn_alignbyte(kw[0], prev, sb) : kw[0];
+          kd[1] = s4 ? __builtin_amdgcn_alignbyte(kw[1], kw[0], sb) : kw[1];
+          kd[2] = s4 ? __builtin_amdgcn_alignbyte(kw[2], kw[1], sb) : kw[2];
+          kd[3] = s4 ? __builtin_amdgcn_alignbyte(kw[3], kw[2], sb) : kw[3];
+          kd[4] = __builtin_amdgcn_alignbyte(0u, kw[3], sb);
+        }
+        for (uint32_t i = sh + 16; i < kn; i += 4) {
+          const uint32_t w = rd.u32(q + i - sh);
+          for (uint32_t c = 0; c < 4 && i + c < kn; c++) lkey[i + c] = (uint8_t)(w >> (8 * c));
+        }
+        const LdsRd kr{s_key[threadIdx.x], 0};
+        hv ^= xp_short(kr, 0, kn, kSeedK);
+      } else {
+        for (uint32_t i = sh; i < kn; i++) gkey[i] = (uint8_t)rd.u8(q + i - sh);
+        __threadfence_block();
+        hv ^= xp_lane(GblRd{gkey}, 0, kn, kSeedK);
+      }
+      if (!vmid && !lng) hv ^= xp_short(rd, v, vl, kSeedV);  // <= 16 or 129..240 bytes
+      if (idx & 1)  // entries idx - 1, idx as one 16-byte store (half the divergent stores)
+        *reinterpret_cast<__attribute__((address_space(1))) span_u32x4*>(
+            reinterpret_cast<uint64_t>(slot_h + sbase + idx - 1)) =
+            span_u32x4{(uint32_t)pend, (uint32_t)(pend >> 32), (uint32_t)hv, (uint32_t)(hv >> 32)};
+      else if (v + vl >= ro)  // the block's last entry, even
+        slot_h[sbase + idx] = hv;
+      pend = hv;
+      if (lng) {
+        slot_m[sbase + idx] = (uint64_t)v << 32 | vl;
+        lmask |= 1u << (idx & 31);
+      }
+      if ((idx & 31) == 31 || v + vl >= ro) {
+        lwords[idx >> 5] = lmask;
+        lmask = 0;
+      }
+      kl = kn;
+      kbytes += kn;
+      idx++;
+      in_cur++;
+      p = v + vl;
+      active = p < ro;
+    }
+    any_long |= lng;
+  }
+  if (in) {
+    if (st == kBlkOk && nr != 0 && ro != 0 && r != nr) st = kBlkBadRestarts;
+    const bool ok = st == kBlkOk;
+    key_cnt[b] = ok ? idx : 0;
+    key_bytes[b] = ok ? kbytes : 0;
+    interval_out[b] = ok && nr > 1 ? interval : 0;
+    status[b] = st;
+  }
+  if (__ballot(any_long) && lane == 0) *long_flag = 1u;
+}
+
+// Slots -> the kv_checksum array (protect) or the mismatch flags (verify),
+// and the long-value list k_block_long_rows sweeps (long_len[k] for every
+// key): thread t moves slot pair t of the flattened slot array, 4 pairs per
+// thread (a wave per block ran into the dispatcher: 0.27 ms at 1M blocks).
+template <bool VERIFY>
+__device__ __forceinline__ void blk_flush_one(SpanSrc blocks, uint32_t stride, uint32_t j, const uint64_t* slot_h,
+                                              const uint64_t* slot_m, const uint32_t* blk_long,
+                                              const uint64_t* key_base, uint32_t prot_bytes, bool p8, uint8_t* enc,
+                                              const uint8_t* stored, uint8_t* mismatch, uint32_t* mismatch_count,
+                                              uint64_t* long_off, uint32_t* long_len, uint64_t* long_part) {
+  const uint32_t hs = stride >> 1;
+  const uint32_t b = j / hs, i = 2 * (j - b * hs);
+  const uint64_t k0 = ldg_u64(key_base, b), cnt = ldg_u64(key_base, b + 1) - k0;
+  if (i >= cnt) return;
+  const uint64_t s0 = (uint64_t)b * stride + i;
+  const bool two = i + 1 < cnt;
+  uint64_t h[2];
+  if (two) {
+    const span_u32x4 v = *reinterpret_cast<__attribute__((address_space(1))) const span_u32x4*>(
+        reinterpret_cast<uint64_t>(slot_h + s0));
+    h[0] = (uint64_t)v.y << 32 | v.x;
+    h[1] = (uint64_t)v.w << 32 | v.z;
+  } else {
+    h[0] = slot_h[s0];
+    h[1] = 0;
+  }
+  // i is even: entries i, i + 1 share a mask word
+  const uint32_t lm = (ldg_u32(blk_long, b * blk_long_words(stride) + (i >> 5)) >> (i & 31)) & 3u;
+  const uint64_t base = lm ? reinterpret_cast<uint64_t>(blocks.ptr(b)) : 0;
+#pragma unroll
+  for (int e = 0; e < 2; e++) {
+    if (e == 1 && !two) break;
+    const uint64_t k = k0 + i + e;
+    const uint64_t m = (lm >> e) & 1u ? slot_m[s0 + e] : 0ull;  // (unwritten for short values)
+    const uint32_t vl = (uint32_t)m;
+    long_len[k] = vl;
+    if (vl) {
+      long_off[k] = base + (m >> 32);
+      if constexpr (VERIFY) long_part[k] = h[e];
+    }
+    if constexpr (!VERIFY) {
+      if (p8)
+        reinterpret_cast<uint64_t*>(enc)[k] = h[e];
+      else
+        for (uint32_t c = 0; c < prot_bytes; c++) enc[k * prot_bytes + c] = (uint8_t)(h[e] >> (8 * c));
+    } else if (!vl) {
+      const uint64_t sv = blk_load_prot(stored, k, prot_bytes);
+      const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
+      const bool bad = sv != (h[e] & keep);
+      mismatch[k] = bad;
+      if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
+    }
+  }
+}
+template <bool VERIFY>
+__global__ __launch_bounds__(256) void k_block_kv_flush(SpanSrc blocks, uint32_t npairs, uint32_t stride,
+                                                        const uint64_t* slot_h, const uint64_t* slot_m,
+                                                        const uint32_t* blk_long, const uint64_t* key_base,
+                                                        uint32_t prot_bytes, uint8_t* enc, const uint8_t* stored,
+                                                        uint8_t* mismatch, uint32_t* mismatch_count,
+                                                        uint64_t* long_off, uint32_t* long_len,
+                                                        uint64_t* long_part) {
+  const bool p8 = prot_bytes == 8 && (reinterpret_cast<uint64_t>(enc) & 7) == 0;
+  const uint32_t g = gridDim.x * blockDim.x;
+  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+#pragma unroll
+  for (uint32_t u = 0; u < 4; u++) {
+    const uint64_t j = t + (uint64_t)u * g;
+    if (j < npairs)
+      blk_flush_one<VERIFY>(blocks, stride, (uint32_t)j, slot_h, slot_m, blk_long, key_base, prot_bytes, p8, enc,
+                            stored, mismatch, mismatch_count, long_off, long_len, long_part);
+  }
+}
+
 __global__ __launch_bounds__(64) void k_dbg_xp(const uint8_t* d, uint32_t len, uint64_t seed, uint64_t* out) {
   __shared__ uint32_t slot[kBlkSlotWords];
   const uint32_t lane = threadIdx.x & 63;
@@ -848,13 +1145,14 @@ __global__ __launch_bounds__(64) void k_dbg_xp(const uint8_t* d, uint32_t len, u
 template <bool VERIFY>
 struct OpBlkLongRows {
   const uint64_t* long_off;
-  const uint32_t* long_len;  // [K]; [K] = long values recorded by the walk
+  const uint32_t* long_len;  // [K]
   const uint64_t* long_part;
   uint32_t prot_bytes;
   uint8_t* enc;
   const uint8_t* stored;
   uint8_t* mismatch;
   uint32_t* mismatch_count;
+  const uint32_t* any_long;  // nonzero: the walk recorded a long value
   __device__ void finish(uint32_t k, uint64_t hv) const {
     if constexpr (!VERIFY) {  // enc[k] holds Encode(partial): XOR the value's hash in
       if (prot_bytes == 8 && ((reinterpret_cast<uint64_t>(enc) & 7) == 0)) {
@@ -875,7 +1173,7 @@ template <bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_long_rows(OpBlkLongRows<VERIFY> op, const uint64_t* key_base,
                                                          uint32_t nblocks) {
   const uint64_t K = ldg_u64(key_base, nblocks);  // keys of the batch (< 2^32: the host checks)
-  if (op.long_len[K] == 0) return;  // no long value in the batch (the walk counted them)
+  if (*op.any_long == 0) return;  // no long value in the batch
   const X3Row X = x3_row(kSeedV);
   const uint32_t wpb = blockDim.x >> 6;
   const uint64_t rows = (uint64_t)gridDim.x * wpb * 4;

@@ -423,10 +423,17 @@ int stage_in(const void* data, size_t n, uint8_t** d_data, void** d_out, size_t 
 template <template <int> class K, class... A>
 int launch_blk(int kind, uint32_t count, hipStream_t st, A... args);
 
+// Dynamic LDS that caps the walks at two workgroups (8 waves) per CU:
+// fewer blocks in flight per CU keep each walk's lines in L2 between its
+// header, key and value reads (100-B values, round 4: the kv walk fetched
+// 2.7x its image at 4 workgroups per CU, 1.9x at 2, and ran 15 % faster;
+// the layout walk 1.2x -> 1.0x, 9 % faster).
+constexpr size_t kBlkLayoutLdsPad = 56 * 1024;
+constexpr size_t kBlkWalkLdsPad = 17 * 1024;  // + the walks' 37 KiB key buffers
 template <int KIND>
 struct BlkLayoutT {
   static void go(dim3, hipStream_t st, SpanSrc s, uint32_t n, uint64_t* a, uint64_t* b, uint32_t* ri, int32_t* stt) {
-    hipLaunchKernelGGL(k_block_layout_t<KIND>, dim3((n + 255) / 256), dim3(256), 0, st, s, n, a, b, ri, stt);
+    hipLaunchKernelGGL(k_block_layout_t<KIND>, dim3((n + 255) / 256), dim3(256), kBlkLayoutLdsPad, st, s, n, a, b, ri, stt);
   }
 };
 template <int KIND>
@@ -436,10 +443,10 @@ struct BlkKvT {
                  uint8_t* arena, uint64_t* long_off, uint32_t* long_len, uint64_t nkeys, uint64_t* long_part,
                  A... rest) {
     if (verify)
-      hipLaunchKernelGGL((k_block_kv_t<KIND, true>), dim3((n + 255) / 256), dim3(256), 0, st, s, n, kb, ab, arena,
+      hipLaunchKernelGGL((k_block_kv_t<KIND, true>), dim3((n + 255) / 256), dim3(256), kBlkWalkLdsPad, st, s, n, kb, ab, arena,
                          long_off, long_len, nkeys, long_part, rest...);
     else
-      hipLaunchKernelGGL((k_block_kv_t<KIND, false>), dim3((n + 255) / 256), dim3(256), 0, st, s, n, kb, ab, arena,
+      hipLaunchKernelGGL((k_block_kv_t<KIND, false>), dim3((n + 255) / 256), dim3(256), kBlkWalkLdsPad, st, s, n, kb, ab, arena,
                          long_off, long_len, nkeys, long_part, rest...);
   }
 };
@@ -519,13 +526,136 @@ int blk_kv(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_
   if (verify)
     hipLaunchKernelGGL(k_block_long_rows<true>, dim3(grid), dim3(256), 0, st,
                        OpBlkLongRows<true>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
-                                           mismatch_count},
+                                           mismatch_count, w.long_len + total_keys},
                        key_base, blocks->count);
   else
     hipLaunchKernelGGL(k_block_long_rows<false>, dim3(grid), dim3(256), 0, st,
                        OpBlkLongRows<false>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
-                                            mismatch_count},
+                                            mismatch_count, w.long_len + total_keys},
                        key_base, blocks->count);
+  MCK_HIP(hipGetLastError());
+  return MCK_OK;
+}
+
+// ---- one pass: k_block_kv_walk + scan + k_block_kv_flush + long values -----
+template <int KIND>
+struct BlkWalkT {
+  template <class... A>
+  static void go(dim3, hipStream_t st, uint32_t n, size_t lds_pad, A... args) {
+    hipLaunchKernelGGL(k_block_kv_walk<KIND>, dim3((n + 255) / 256), dim3(256), lds_pad, st, args...);
+  }
+};
+static_assert(kBlkSlotOverflow == MCK_BLOCK_SLOT_OVERFLOW, "status codes");
+
+// work: [scan tiles][flag u32, pad to 256][slot_h, slot_m: u64 x count x stride][long masks]
+//       [long_off u64 x K][long_part u64 x K][long_len u32 x K][arena count x arena_cap], K = count x slot_cap
+struct BlkBlocksWork {
+  uint64_t* tsum;
+  uint32_t* flag;
+  uint64_t *slot_h, *slot_m;
+  uint32_t* blk_long;
+  uint64_t *long_off, *long_part;
+  uint32_t* long_len;
+  uint8_t* arena;
+  uint64_t bytes;
+};
+BlkBlocksWork blk_blocks_work(void* work, uint32_t count, uint32_t slot_cap, uint32_t arena_cap) {
+  auto up = [](uint64_t x) { return (x + 255) & ~255ull; };
+  const uint64_t K = (uint64_t)count * slot_cap;
+  uint8_t* w = static_cast<uint8_t*>(work);
+  BlkBlocksWork r{};
+  uint64_t o = 0;
+  r.tsum = reinterpret_cast<uint64_t*>(w + o);
+  o += up(16 * blk_tiles(count) + 64);
+  r.flag = reinterpret_cast<uint32_t*>(w + o);
+  o += 256;
+  const uint64_t S = (uint64_t)count * blk_slot_stride(slot_cap);
+  r.slot_h = reinterpret_cast<uint64_t*>(w + o);
+  o += up(8 * S);
+  r.slot_m = reinterpret_cast<uint64_t*>(w + o);
+  o += up(8 * S);
+  r.blk_long = reinterpret_cast<uint32_t*>(w + o);
+  o += up(4ull * count * blk_long_words(slot_cap));
+  r.long_off = reinterpret_cast<uint64_t*>(w + o);
+  o += up(8 * K);
+  r.long_part = reinterpret_cast<uint64_t*>(w + o);
+  o += up(8 * K);
+  r.long_len = reinterpret_cast<uint32_t*>(w + o);
+  o += up(4 * K + 4);
+  r.arena = w + o;
+  o += up((uint64_t)count * arena_cap + 16);
+  r.bytes = o;
+  return r;
+}
+
+int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32_t slot_cap, uint32_t arena_cap,
+                  uint64_t* key_base, uint64_t* arena_base, uint32_t* restart_interval, int32_t* status, void* work,
+                  uint8_t* enc, const uint8_t* stored, uint8_t* mismatch, uint32_t* mismatch_count,
+                  hipStream_t st) {
+  if (int rc = check_spans(blocks)) return rc;
+  if (kind < MCK_BLOCK_DATA || kind > MCK_BLOCK_META) {
+    set_err("unknown block kind %d", kind);
+    return MCK_EINVAL;
+  }
+  if (prot_bytes != 1 && prot_bytes != 2 && prot_bytes != 4 && prot_bytes != 8) {
+    set_err("protection_bytes_per_key must be 1, 2, 4 or 8 (got %u)", prot_bytes);
+    return MCK_EINVAL;
+  }
+  stat_batch(blocks->count, known_bytes(blocks));
+  if (!key_base || !arena_base) {
+    set_err("key_base/arena_base is NULL");
+    return MCK_EINVAL;
+  }
+  const uint32_t n = blocks->count;
+  if (!n) {
+    MCK_HIP(hipMemsetAsync(key_base, 0, 8, st));
+    MCK_HIP(hipMemsetAsync(arena_base, 0, 8, st));
+    return MCK_OK;
+  }
+  if (!restart_interval || !status || !work || (!enc && !stored) || (stored && !mismatch)) {
+    set_err("restart_interval/status/work/out is NULL");
+    return MCK_EINVAL;
+  }
+  if (slot_cap == 0 || (uint64_t)n * blk_slot_stride(slot_cap) > 0xFFFFFFFFull) {
+    set_err("slot_cap must be >= 1 with count * slot_cap < 2^32 (got %u x %u)", n, slot_cap);
+    return MCK_EINVAL;
+  }
+  const BlkBlocksWork w = blk_blocks_work(work, n, slot_cap, arena_cap);
+  MCK_HIP(hipMemsetAsync(w.flag, 0, 4, st));
+  if (int rc = launch_blk<BlkWalkT>(kind, n, st, n, kBlkWalkLdsPad, to_src(blocks), n, slot_cap, w.arena, arena_cap,
+                                    w.slot_h, w.slot_m, w.blk_long, key_base, arena_base, restart_interval, status,
+                                    w.flag))
+    return rc;
+  const uint32_t tiles = (uint32_t)blk_tiles(n);
+  hipLaunchKernelGGL(k_blk_scan_tiles, dim3(tiles), dim3(kBlkScanThreads), 0, st, key_base, arena_base, n, w.tsum);
+  hipLaunchKernelGGL(k_blk_scan_top, dim3(1), dim3(kBlkScanThreads), 0, st, w.tsum, tiles, key_base, arena_base, n);
+  hipLaunchKernelGGL(k_blk_scan_apply, dim3(tiles), dim3(kBlkScanThreads), 0, st, key_base, arena_base, n, w.tsum);
+  int ncu;
+  if (int rc = current_device(nullptr, &ncu)) return rc;
+  const uint32_t stride = blk_slot_stride(slot_cap);
+  const uint32_t npairs = n * (stride / 2);
+  const uint32_t fgrid = (uint32_t)(((uint64_t)npairs + 4 * 256 - 1) / (4 * 256));  // 4 pairs per thread
+  const bool verify = stored != nullptr;
+  if (verify)
+    hipLaunchKernelGGL(k_block_kv_flush<true>, dim3(fgrid), dim3(256), 0, st, to_src(blocks), npairs, stride,
+                       w.slot_h, w.slot_m, w.blk_long, key_base, prot_bytes, enc, stored, mismatch, mismatch_count,
+                       w.long_off, w.long_len, w.long_part);
+  else
+    hipLaunchKernelGGL(k_block_kv_flush<false>, dim3(fgrid), dim3(256), 0, st, to_src(blocks), npairs, stride,
+                       w.slot_h, w.slot_m, w.blk_long, key_base, prot_bytes, enc, stored, mismatch, mismatch_count,
+                       w.long_off, w.long_len, w.long_part);
+  const uint64_t K = (uint64_t)n * slot_cap;  // bound; the sweep reads the total from key_base[n]
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)ncu * 8, (K + 255) / 256);
+  if (verify)
+    hipLaunchKernelGGL(k_block_long_rows<true>, dim3(grid), dim3(256), 0, st,
+                       OpBlkLongRows<true>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
+                                           mismatch_count, w.flag},
+                       key_base, n);
+  else
+    hipLaunchKernelGGL(k_block_long_rows<false>, dim3(grid), dim3(256), 0, st,
+                       OpBlkLongRows<false>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
+                                            mismatch_count, w.flag},
+                       key_base, n);
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }
@@ -1089,6 +1219,32 @@ int mck_block_kv_verify_batch(int kind, const mck_spans* blocks, uint32_t prot_b
   }
   return blk_kv(kind, blocks, prot_bytes, key_base, arena_base, restart_interval, total_keys, work, nullptr, stored,
                 mismatch, mismatch_count, reinterpret_cast<hipStream_t>(stream));
+}
+
+uint64_t mck_block_kv_blocks_work_bytes(uint32_t count, uint32_t slot_cap, uint32_t arena_cap) {
+  return blk_blocks_work(nullptr, count, slot_cap, arena_cap).bytes;
+}
+
+int mck_block_kv_protect_blocks_batch(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32_t slot_cap,
+                                      uint32_t arena_cap, uint64_t* key_base, uint64_t* arena_base,
+                                      uint32_t* restart_interval, int32_t* status, void* work, uint8_t* out,
+                                      mck_stream_t stream) {
+  t_err[0] = 0;
+  return blk_kv_blocks(kind, blocks, prot_bytes, slot_cap, arena_cap, key_base, arena_base, restart_interval, status,
+                       work, out, nullptr, nullptr, nullptr, reinterpret_cast<hipStream_t>(stream));
+}
+
+int mck_block_kv_verify_blocks_batch(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32_t slot_cap,
+                                     uint32_t arena_cap, uint64_t* key_base, uint64_t* arena_base,
+                                     uint32_t* restart_interval, int32_t* status, void* work, const uint8_t* stored,
+                                     uint8_t* mismatch, uint32_t* mismatch_count, mck_stream_t stream) {
+  t_err[0] = 0;
+  if (!stored) {
+    set_err("stored is NULL");
+    return MCK_EINVAL;
+  }
+  return blk_kv_blocks(kind, blocks, prot_bytes, slot_cap, arena_cap, key_base, arena_base, restart_interval, status,
+                       work, nullptr, stored, mismatch, mismatch_count, reinterpret_cast<hipStream_t>(stream));
 }
 
 // Internal test hook (not part of mck.h): XXPH3 of one device span by the

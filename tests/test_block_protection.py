@@ -313,6 +313,80 @@ def test_block_protection_many_blocks_property(gpu, oracle):
 
 
 @pytest.mark.gpu
+def test_block_protection_one_pass_vs_oracle(gpu, oracle):
+    """mck_block_kv_protect_blocks_batch (layout checks and hashing in one
+    walk, entries parked in per-block slots) with room for every block of the
+    corpus -- 300-entry blocks, 100..400-byte keys in the per-block arena --
+    equals the oracle block by block (status, checksums, restart interval),
+    and its key_base / arena_base equal the two-pass layout's."""
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    rnd = random.Random(23)
+    cases = corpus(rnd)
+    for kind in (DATA, INDEX, INDEX_DELTA, INDEX_DELTA_FK, META):
+        sel = [c for c in cases if c[0] == kind or (kind == DATA and c[0] not in (INDEX, INDEX_DELTA,
+                                                                                   INDEX_DELTA_FK, META))]
+        blocks = [c[1] for c in sel]
+        base, offs, lens = _pack(torch, blocks, rnd)
+        spans = speedb_amd.Spans(base, len(blocks), offs, lens)
+        for p in (1, 2, 4, 8):
+            prot = B.InitializeBlockProtectionInfoOnePass(kind, spans, p, slot_cap=320, arena_cap=4096)
+            two = B.InitializeBlockProtectionInfo(kind, spans, p, one_pass=False)
+            torch.cuda.synchronize()
+            kb = prot.key_base.cpu().tolist()
+            sts = prot.status.cpu().tolist()
+            ris = prot.restart_interval.cpu().tolist()
+            allck = prot.kv_checksum.cpu().numpy().tobytes()
+            for i, blk in enumerate(blocks):
+                ost, ock, ori = oracle.BlockKvProtect(kind, blk, p)
+                assert sts[i] == ost, (kind, i, sts[i], ost)
+                assert allck[kb[i] * p:kb[i + 1] * p] == ock, (kind, i)
+                assert ris[i] == ori, (kind, i)
+            assert kb == two.key_base.cpu().tolist()
+            assert prot.arena_base.cpu().tolist() == two.arena_base.cpu().tolist()
+            assert prot.total_keys == two.total_keys
+
+
+@pytest.mark.gpu
+def test_block_protection_one_pass_overflow(gpu, oracle):
+    """Blocks with more entries than slot_cap, or a key over 128 bytes and
+    arena_cap, come back MCK_BLOCK_SLOT_OVERFLOW with no keys while their
+    neighbours are protected; InitializeBlockProtectionInfo then runs the
+    two-pass pair for the batch and matches the oracle everywhere."""
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    rnd = random.Random(29)
+    small = [build_block(data_block(rnd, rnd.randrange(1, 16), 4), 4) for _ in range(40)]
+    big = build_block(data_block(rnd, 40, 4), 4)
+    longk = build_block(data_block(rnd, 6, 2, klo=130, khi=200), 2)
+    blocks = small[:20] + [big] + small[20:] + [longk]
+    base, offs, lens = _pack(torch, blocks, rnd)
+    spans = speedb_amd.Spans(base, len(blocks), offs, lens)
+    prot = B.InitializeBlockProtectionInfoOnePass(DATA, spans, 8, slot_cap=16, arena_cap=0)
+    sts = prot.status.cpu().tolist()
+    assert sts[20] == B.BlockStatus.kSlotOverflow and sts[-1] == B.BlockStatus.kSlotOverflow
+    kb = prot.key_base.cpu().tolist()
+    ck = prot.kv_checksum.cpu().numpy().tobytes()
+    for i, blk in enumerate(blocks):
+        if i in (20, len(blocks) - 1):
+            assert kb[i + 1] == kb[i]
+            continue
+        assert sts[i] == OK
+        assert ck[kb[i] * 8:kb[i + 1] * 8] == oracle.BlockKvProtect(DATA, blk, 8)[1], i
+    # the long key fits once the arena slice holds it
+    prot = B.InitializeBlockProtectionInfoOnePass(DATA, spans, 8, slot_cap=64, arena_cap=256)
+    assert prot.status.cpu().tolist() == [OK] * len(blocks)
+    full = B.InitializeDataBlockProtectionInfo(spans, 8)
+    kb = full.key_base.cpu().tolist()
+    ck = full.kv_checksum.cpu().numpy().tobytes()
+    assert full.slot_cap == 0  # the fallback ran
+    for i, blk in enumerate(blocks):
+        assert ck[kb[i] * 8:kb[i + 1] * 8] == oracle.BlockKvProtect(DATA, blk, 8)[1], i
+
+
+@pytest.mark.gpu
 def test_block_protection_empty_and_all_bad(gpu):
     import speedb_amd
     from speedb_amd import block as B
@@ -336,6 +410,13 @@ def test_block_protection_abi_errors():
     assert lib.mck_block_kv_protect_batch(9, ctypes.byref(s), 4, None, None, None, 0, None, None, None) == -1
     assert lib.mck_block_kv_scratch_bytes(5000) >= 16 * 3
     assert lib.mck_block_kv_work_bytes(10, 100) >= 10 * 24 + 100
+    assert lib.mck_block_kv_protect_blocks_batch(0, ctypes.byref(s), 3, 64, 0, None, None, None, None, None,
+                                                 None, None) == -1
+    assert lib.mck_block_kv_protect_blocks_batch(9, ctypes.byref(s), 8, 64, 0, None, None, None, None, None,
+                                                 None, None) == -1
+    assert lib.mck_block_kv_verify_blocks_batch(0, ctypes.byref(s), 8, 64, 0, None, None, None, None, None,
+                                                None, None, None, None) == -1
+    assert lib.mck_block_kv_blocks_work_bytes(10, 64, 32) >= 10 * 64 * 36 + 10 * 32
 
 
 @pytest.mark.gpu
