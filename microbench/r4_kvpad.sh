@@ -1,5 +1,7 @@
 #!/bin/bash
 # EXPERIMENT: block KV walk occupancy (LDS padding) vs time
+# (historical: the MCK_PAD_* hooks this sweep set were replaced by the fixed
+# kBlkLayoutLdsPad / kBlkWalkLdsPad in mck_engine.hip; results in profiles/r4/blockkv_occupancy)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
