@@ -857,7 +857,9 @@ int mck_perf_context_get(mck_perf_context* out, int reset);
  * driver, chosen from a sample of its lengths, so a mixed parity batch may
  * exercise only one.  driver: 0 = by length (the default), 2 = 16-lane rows,
  * 3 = 8-lane rows, 5 = 4-lane rows, 6 = one lane per span, 7 = the
- * body/head driver (1 and 4, the retired wave driver and unit stream, are
+ * body/head driver, 9 = a wave per span wherever a workgroup's share allows
+ * it (<= 16 spans of <= 16 KiB; by default only batches of <= 64 spans take
+ * it) (1 and 4, the retired wave driver and unit stream, and 8 are
  * refused); interleaved != 0 deals spans to workgroups round-robin (row
  * drivers only) instead of in contiguous ranges.  Process-wide. */
 int mck_test_set_crc_driver(int driver, int interleaved);

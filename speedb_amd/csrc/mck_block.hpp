@@ -1044,7 +1044,8 @@ __device__ __forceinline__ void blk_flush_one(SpanSrc blocks, uint32_t stride, u
                                               const uint64_t* slot_m, const uint32_t* blk_long,
                                               const uint64_t* key_base, uint32_t prot_bytes, bool p8, uint8_t* enc,
                                               const uint8_t* stored, uint8_t* mismatch, uint32_t* mismatch_count,
-                                              uint64_t* long_off, uint32_t* long_len, uint64_t* long_part) {
+                                              uint64_t* long_off, uint32_t* long_len, uint64_t* long_part,
+                                              bool batch_long) {
   const uint32_t hs = stride >> 1;
   const uint32_t b = j / hs, i = 2 * (j - b * hs);
   const uint64_t k0 = ldg_u64(key_base, b), cnt = ldg_u64(key_base, b + 1) - k0;
@@ -1070,7 +1071,7 @@ __device__ __forceinline__ void blk_flush_one(SpanSrc blocks, uint32_t stride, u
     const uint64_t k = k0 + i + e;
     const uint64_t m = (lm >> e) & 1u ? slot_m[s0 + e] : 0ull;  // (unwritten for short values)
     const uint32_t vl = (uint32_t)m;
-    long_len[k] = vl;
+    if (batch_long) long_len[k] = vl;  // (no long value in the batch: the sweep exits on the flag)
     if (vl) {
       long_off[k] = base + (m >> 32);
       if constexpr (VERIFY) long_part[k] = h[e];
@@ -1096,8 +1097,9 @@ __global__ __launch_bounds__(256) void k_block_kv_flush(SpanSrc blocks, uint32_t
                                                         uint32_t prot_bytes, uint8_t* enc, const uint8_t* stored,
                                                         uint8_t* mismatch, uint32_t* mismatch_count,
                                                         uint64_t* long_off, uint32_t* long_len,
-                                                        uint64_t* long_part) {
+                                                        uint64_t* long_part, const uint32_t* long_flag) {
   const bool p8 = prot_bytes == 8 && (reinterpret_cast<uint64_t>(enc) & 7) == 0;
+  const bool batch_long = *long_flag != 0;
   const uint32_t g = gridDim.x * blockDim.x;
   const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 #pragma unroll
@@ -1105,7 +1107,7 @@ __global__ __launch_bounds__(256) void k_block_kv_flush(SpanSrc blocks, uint32_t
     const uint64_t j = t + (uint64_t)u * g;
     if (j < npairs)
       blk_flush_one<VERIFY>(blocks, stride, (uint32_t)j, slot_h, slot_m, blk_long, key_base, prot_bytes, p8, enc,
-                            stored, mismatch, mismatch_count, long_off, long_len, long_part);
+                            stored, mismatch, mismatch_count, long_off, long_len, long_part, batch_long);
   }
 }
 

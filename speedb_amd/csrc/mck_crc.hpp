@@ -251,6 +251,10 @@ struct CrcSpan {
 
 constexpr uint32_t kMiniBytes = 1024;  // 64 lanes x 16 bytes
 
+// INJ = false leaves the init state un-un-shifted (no LDS read: the
+// geometry, and so the first loads, before the table fill); crc_span_inj
+// completes it.
+template <bool INJ = true>
 __device__ __forceinline__ CrcSpan crc_span(const uint8_t* p, uint64_t n, uint32_t init_crc) {
   CrcSpan s;
   s.ptr = reinterpret_cast<uint64_t>(p);
@@ -270,7 +274,7 @@ __device__ __forceinline__ CrcSpan crc_span(const uint8_t* p, uint64_t n, uint32
     s.owner_m = (int32_t)(lead >> 4);
     s.hb_m = lead & 15u;
     s.inj_m = ~init_crc;
-    if (s.hb_m) s.inj_m = crc_unshift(s.hb_m, s.inj_m);  // wave-uniform branch
+    if (INJ && s.hb_m) s.inj_m = crc_unshift(s.hb_m, s.inj_m);  // wave-uniform branch
     // the first full round starts exactly at the mini round's end
     s.owner = 0;
     s.hb = 0;
@@ -285,8 +289,12 @@ __device__ __forceinline__ CrcSpan crc_span(const uint8_t* p, uint64_t n, uint32
   s.owner = s.empty ? 64 : (int32_t)(lead >> 6);
   s.hb = lead & 63u;
   s.inj = ~init_crc;
-  if (s.hb) s.inj = crc_unshift(s.hb, s.inj);  // wave-uniform branch
+  if (INJ && s.hb) s.inj = crc_unshift(s.hb, s.inj);  // wave-uniform branch
   return s;
+}
+__device__ __forceinline__ void crc_span_inj(CrcSpan& s) {
+  if (s.mini && s.hb_m) s.inj_m = crc_unshift(s.hb_m, s.inj_m);  // wave-uniform branches
+  if (!s.mini && s.hb) s.inj = crc_unshift(s.hb, s.inj);
 }
 
 // ---- transposed loads -------------------------------------------------------

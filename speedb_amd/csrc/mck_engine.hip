@@ -250,9 +250,14 @@ int launch_crc(const Op& op, uint32_t count, hipStream_t st) {
   // (>= 4 spans per workgroup: a batch of a few thousand large spans -- one
   // 64 MiB SST file -- still fills every CU)
   const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + 3) / 4);
-  if (blk) {
+  if (blk && ((count <= kSmallBatch && force == 0) || force == 9)) {  // a wave per span (latency)
+    if ((rc = ensure_lds(k_crc_ragged<Op, T, true, true>, dev))) return rc;
+    hipLaunchKernelGGL((k_crc_ragged<Op, T, true, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count,
+                       force);
+  } else if (blk) {
     if ((rc = ensure_lds(k_crc_ragged<Op, T, true>, dev))) return rc;
-    hipLaunchKernelGGL((k_crc_ragged<Op, T, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count, force);
+    hipLaunchKernelGGL((k_crc_ragged<Op, T, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count,
+                       force == 9 ? 0 : force);
   } else {  // the interleaved order (test hook): row drivers only
     if ((rc = ensure_lds(k_crc_ragged<Op, T, false>, dev))) return rc;
     hipLaunchKernelGGL((k_crc_ragged<Op, T, false>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, count,
@@ -639,11 +644,11 @@ int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32
   if (verify)
     hipLaunchKernelGGL(k_block_kv_flush<true>, dim3(fgrid), dim3(256), 0, st, to_src(blocks), npairs, stride,
                        w.slot_h, w.slot_m, w.blk_long, key_base, prot_bytes, enc, stored, mismatch, mismatch_count,
-                       w.long_off, w.long_len, w.long_part);
+                       w.long_off, w.long_len, w.long_part, w.flag);
   else
     hipLaunchKernelGGL(k_block_kv_flush<false>, dim3(fgrid), dim3(256), 0, st, to_src(blocks), npairs, stride,
                        w.slot_h, w.slot_m, w.blk_long, key_base, prot_bytes, enc, stored, mismatch, mismatch_count,
-                       w.long_off, w.long_len, w.long_part);
+                       w.long_off, w.long_len, w.long_part, w.flag);
   const uint64_t K = (uint64_t)n * slot_cap;  // bound; the sweep reads the total from key_base[n]
   const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)ncu * 8, (K + 255) / 256);
   if (verify)
@@ -1618,9 +1623,10 @@ int mck_perf_context_get(mck_perf_context* out, int reset) {
 int mck_test_set_crc_driver(int driver, int interleaved) {
   t_err[0] = 0;
   // 1 (the 4 KiB-round wave driver) and 4 (the unit stream) were retired
-  // in round 4 by the body/head driver (7)
-  if (driver < 0 || driver > 7 || driver == 1 || driver == 4) {
-    set_err("driver must be 0, 2, 3, 5, 6 or 7");
+  // in round 4 by the body/head driver (7); 9 = the small-batch wave-per-span
+  // path wherever it applies
+  if (driver < 0 || driver > 9 || driver == 1 || driver == 4 || driver == 8) {
+    set_err("driver must be 0, 2, 3, 5, 6, 7 or 9");
     return MCK_EINVAL;
   }
   g_crc_force.store(driver, std::memory_order_relaxed);

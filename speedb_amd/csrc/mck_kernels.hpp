@@ -212,21 +212,78 @@ struct OpCrcBlock {
   }
 };
 
+
+// ---- small batches: one wave per span --------------------------------------
+// A batch of a few short spans (a MultiGet's <= 32 blocks,
+// RetrieveMultipleBlocks) is latency, not bandwidth: the row and body/head
+// drivers' descriptor staging, init tables, span scans and barriers are a
+// chain of dependent round trips before the first data load.  For at most
+// kSmallBatch spans of at most kSmallSpanMax bytes each workgroup instead
+// gives every span of its share (<= 16 here) a wave: descriptor and epilogue
+// loads issued with the table fill, the first round's loads before its
+// stores, then the wave driver's rounds (crc_round), the finish.  Its own instance of k_crc_ragged
+// (SMALL): one more path in the bandwidth instance spilled the blob and
+// index-block ops' registers.
+constexpr uint32_t kSmallBatch = 64, kSmallSpanMax = 16384;
+template <class Op>
+__device__ __forceinline__ bool crc_share_small(const Op& op, const RowShare& sh) {
+  if (sh.n > 16) return false;  // workgroup-uniform
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t len = lane < sh.n ? op.len(sh.idx(lane)) : 0;
+  return !wave_any(len > kSmallSpanMax);  // (every wave reads the same lengths)
+}
+template <class Op>
+__device__ __forceinline__ void crc_small_share(const Op& op, const RowShare& sh, uint8_t* lds,
+                                                const CrcTables* __restrict__ g) {
+  const uint32_t w = threadIdx.x >> 6;
+  // table loads and the span's descriptor in flight together; the first
+  // round's loads (they need the descriptor) before the table stores (the
+  // init state's un-shift reads the tables: after them)
+  CrcFill f;
+  crc_fill_load<true>(f, g);
+  const uint32_t i = sh.idx(w < sh.n ? w : 0);
+  const uint64_t ptr = reinterpret_cast<uint64_t>(op.base()) + op.off(i);
+  const uint64_t n = op.len(i);
+  const typename Op::Pre e = op.pre(i, ptr, n);
+  const CrcLane L = crc_lane();
+  CrcSpan sp = crc_span<false>(reinterpret_cast<const uint8_t*>(ptr), n, op.init_crc(i));
+  Chunk cur = crc_load_chunk<false>(sp, sp.rounds - 1, L);
+  crc_fill_store<true>(f, lds);
+  __syncthreads();
+  if (w >= sh.n) return;  // wave-uniform
+  crc_span_inj(sp);
+  uint32_t s = 0;
+  for (int r = sp.rounds - 1; r >= 0; r--) {  // next round's loads issued first
+    const Chunk nxt = crc_load_chunk<false>(sp, r > 0 ? r - 1 : 0, L);
+    s = crc_round(s, cur, sp, r, L);
+    cur = nxt;
+  }
+  op.finish(i, crc_finish(s, sp, L), e, (threadIdx.x & 63) == 0);
+}
+
 // Ragged batches in ONE launch: each workgroup runs its share on the
-// body/head driver or the row drivers (crc_share_long).  force: 0 = by
-// length, 7 = body/head for every share, 2/3/5/6 = that row width for every
-// share, 8 = row drivers, width by length (the interleaved test order).
-template <class Op, bool T, bool BLK = true>
+// body/head driver or the row drivers (crc_share_long), or, in a small batch,
+// a wave per span (crc_share_small).  force: 0 = by length, 7 = body/head for
+// every share, 2/3/5/6 = that row width for every share, 8 = row drivers,
+// width by length (the interleaved test order), 9 = a wave per span wherever
+// crc_share_small allows it (SMALL instances).
+template <class Op, bool T, bool BLK = true, bool SMALL = false>
 __global__ __launch_bounds__(1024) void k_crc_ragged(Op op, uint32_t first, uint32_t count, int force) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   asm volatile("" ::"v"((uint32_t)(size_t)lds));
   const RowShare sh = row_share<BLK>(first, count);
   if (sh.n == 0) return;  // workgroup-uniform
+  if constexpr (SMALL) {
+    if ((force == 0 || force == 9) && crc_share_small(op, sh)) {
+      crc_small_share(op, sh, lds, &g_crc_tables);
+      return;
+    }
+  }
   const bool bh = force == 7 || (force == 0 && BLK && crc_share_long(op, sh));
   if (bh)
     crc_bh_driver<Op, T>(op, sh, &g_crc_tables);
   else
-    crc_rows_windows<Op>(op, sh, lds, &g_crc_tables, force == 8 ? 0 : force);
+    crc_rows_windows<Op>(op, sh, lds, &g_crc_tables, force == 8 || force == 9 ? 0 : force);
 }
 
 // uniform batches (see CrcUniform)
@@ -1040,20 +1097,6 @@ struct WalResult {
   uint32_t bytes_ok;
 };
 
-// T: row-transposed loads for the full rounds (crc_load_chunk<true>).
-template <bool T>
-__device__ __forceinline__ uint32_t crc_span_wave(const uint8_t* p, uint64_t n, uint32_t init, const CrcLane& L) {
-  const CrcSpan sp = crc_span(p, n, init);
-  uint32_t s = 0;
-  Chunk cur = crc_load_chunk<T>(sp, sp.rounds - 1, L);
-  for (int r = sp.rounds - 1; r >= 0; r--) {
-    const Chunk nxt = crc_load_chunk<T>(sp, r > 0 ? r - 1 : 0, L);
-    if (T && !(sp.mini && r == sp.rounds - 1)) row_transpose(cur);  // wave-uniform
-    s = crc_round(s, cur, sp, r, L);
-    cur = nxt;
-  }
-  return crc_finish(s, sp, L);
-}
 
 // The block's first header comes from a 16-byte vector load issued while
 // the previous block is hashed (one memory round trip per 32 KiB block

@@ -23,7 +23,7 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 
 # Child pytest processes of the forced-driver tests set these; the engine
 # itself reads no environment (mck_test_set_crc_driver is its test hook).
-CRC_DRIVERS = {"rows16": 2, "rows8": 3, "rows4": 5, "rows1": 6, "bh": 7}
+CRC_DRIVERS = {"rows16": 2, "rows8": 3, "rows4": 5, "rows1": 6, "bh": 7, "small": 9}
 
 
 def pytest_configure(config):

@@ -70,12 +70,14 @@ def _forced(env):
     assert " passed" in r.stdout
 
 
-@pytest.mark.parametrize("mode", ["rows16", "rows8", "rows4", "rows1", "bh", "interleaved"])
+@pytest.mark.parametrize("mode", ["rows16", "rows8", "rows4", "rows1", "bh", "small", "interleaved"])
 def test_auto_kernel_forced_drivers_subprocess(gpu, mode):
     """k_crc_ragged with each driver forced for every workgroup (its choice is
     by mean length, so a parity test of mixed lengths may exercise only one):
     short spans, 0-byte spans, WAL / blob / SST ops on every driver; and the
-    interleaved span order instead of contiguous ranges."""
+    interleaved span order instead of contiguous ranges.  "small": the
+    wave-per-span path for every share it accepts (<= 16 spans of <= 16 KiB),
+    in batches of any size -- by default only batches of <= 64 spans."""
     if os.environ.get("SPEEDB_AMD_TEST_CRC_DRIVER") or os.environ.get("SPEEDB_AMD_TEST_CRC_ORDER"):
         pytest.skip("already running a forced driver")
     _forced({"SPEEDB_AMD_TEST_CRC_ORDER": "interleaved"} if mode == "interleaved"
