@@ -257,8 +257,9 @@ def _ragged(op, mean_len):
     """The kernel that does a ragged CRC batch's work: k_crc_ragged, one
     launch; its workgroups run the body/head driver for spans averaging more
     than 2.5 KiB, the row drivers otherwise (mean_len: the label once named
-    the kernel per driver)."""
-    return f"mck::k_crc_ragged<{op}, true, true>"
+    the kernel per driver; the 4th template argument is the small-batch
+    instance's flag, false for every batch of more than 64 spans)."""
+    return f"mck::k_crc_ragged<{op}, true, true, false>"
 
 
 def C_wal_verify(im, nblocks, stream):
