@@ -387,6 +387,50 @@ def test_block_protection_one_pass_overflow(gpu, oracle):
 
 
 @pytest.mark.gpu
+def test_block_protection_one_pass_equals_two_pass_many(gpu):
+    """Property at scale: 3000 blocks (short and long values, long keys,
+    corrupt blocks, every 7th block 64 bytes of garbage) -- the one-pass
+    entry point (room for every block) and the two-pass pair agree on every
+    status, restart interval, key base and checksum byte, and one-pass
+    verify flags exactly the entries whose stored bytes were flipped."""
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    rnd = random.Random(41)
+    blocks = []
+    for i in range(3000):
+        if i % 7 == 3:
+            blocks.append(bytes(rnd.getrandbits(8) for _ in range(64)))
+            continue
+        n = rnd.randrange(1, 40)
+        ri = rnd.choice((1, 2, 4, 16))
+        if i % 11 == 5:
+            e = data_block(rnd, n, ri, 200, 1500)
+        elif i % 13 == 6:
+            e = data_block(rnd, rnd.randrange(1, 8), ri, 0, 60, klo=130, khi=300)
+        else:
+            e = data_block(rnd, n, ri, 0, 130)
+        blocks.append(build_block(e, ri))
+    base, offs, lens = _pack(torch, blocks, rnd)
+    spans = speedb_amd.Spans(base, len(blocks), offs, lens)
+    for p in (2, 8):
+        one = B.InitializeBlockProtectionInfoOnePass(DATA, spans, p, slot_cap=64, arena_cap=512)
+        two = B.InitializeBlockProtectionInfo(DATA, spans, p, one_pass=False)
+        assert one.status.cpu().tolist() == two.status.cpu().tolist()
+        assert one.restart_interval.cpu().tolist() == two.restart_interval.cpu().tolist()
+        assert one.key_base.cpu().tolist() == two.key_base.cpu().tolist()
+        assert one.arena_base.cpu().tolist() == two.arena_base.cpu().tolist()
+        assert torch.equal(one.kv_checksum, two.kv_checksum)
+        stored = one.kv_checksum.clone()
+        bad = sorted(rnd.sample(range(one.total_keys), 50))
+        for k in bad:
+            stored[p * k + rnd.randrange(p)] ^= 1 << rnd.randrange(8)
+        mism, cnt = B.VerifyBlockProtectionInfo(spans, one, stored)
+        assert int(cnt.item()) == len(bad)
+        assert torch.nonzero(mism).flatten().cpu().tolist() == bad
+
+
+@pytest.mark.gpu
 def test_block_protection_empty_and_all_bad(gpu):
     import speedb_amd
     from speedb_amd import block as B
