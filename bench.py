@@ -507,12 +507,10 @@ def make_workload(args, dev, rank, world):
         w.step = step
         w.launches = 1
         w.span_bytes = int(lens.sum())
-        # the one-pass writer k_wal_write_il in launches of <= ncu * 1528
-        # fragments, timed together as the step; it reads the payload and the
-        # 24 B descriptor once, writes the stream and the 4 B CRC
-        cap = torch.cuda.get_device_properties(dev).multi_processor_count * 1528
-        nl = -(-nf // cap)
-        w.kernel = f"mck::k_wal_write_il ({nl} launch(es) per step, timed as the step)"
+        # the one-pass writer k_wal_write_il, one launch per group commit
+        # (round 4; workgroups walk their ranges in LDS windows); it reads the
+        # payload and the 24 B descriptor once, writes the stream and the 4 B CRC
+        w.kernel = "mck::k_wal_write_il (1 launch(es) per step, timed as the step)"
         w.alg_bytes = int(lens.sum()) + nbytes + nf * (24 + 4)
         w.desc = (f"device WAL writer: group commit of {len(lens)} records of 1000-1100 B per GPU "
                   f"(README 1 KB values) -> {nf} physical records, {nbytes} B of log stream "

@@ -857,8 +857,8 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, 
 // driver's loop (16-lane rows, 80-byte lane chunks of interleaved 16-byte
 // pieces, one ~1 KB fragment per 1280-byte round) CRCs every fragment and,
 // from the same registers, writes the log stream; contiguous fragment ranges
-// per workgroup.  Launches hold at most ncu * kRowDescCache fragments (its
-// LDS descriptor / dst_off tables).  (Round 2 measured the alternatives --
+// per workgroup, in LDS windows of kRowDescCache (one launch per batch).
+// (Round 2 measured the alternatives --
 // two kernels overlapped in pieces on a side stream, 8-lane rows, 64-byte
 // chunks, re-reading copies, interleaved order -- and kept this one; they
 // were removed from the library in round 3.)
@@ -882,15 +882,10 @@ int mck_wal_write_batch(const void* src, const mck_wal_fragment* frags, uint32_t
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
   if (int rc = ensure_lds(k_wal_write_il, dev)) return rc;
-  const uint32_t cap = (uint32_t)ncu * kRowDescCache;
-  const uint32_t nl = (nfrags + cap - 1) / cap;
-  const uint32_t per = (uint32_t)(((uint64_t)nfrags + nl - 1) / nl);
-  for (uint32_t first = 0; first < nfrags; first += per) {
-    const uint32_t n = std::min(per, nfrags - first);
-    const uint32_t grid = std::min<uint32_t>(ncu, (n + 63) / 64);
-    hipLaunchKernelGGL(k_wal_write_il, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, first, n);
-    MCK_HIP(hipGetLastError());
-  }
+  // one launch: each workgroup walks its range in LDS windows (wal_write_il)
+  const uint32_t grid = std::min<uint32_t>(ncu, (nfrags + 63) / 64);
+  hipLaunchKernelGGL(k_wal_write_il, dim3(grid), dim3(1024), kCrcLdsBytes, st, op, 0u, nfrags);
+  MCK_HIP(hipGetLastError());
   return MCK_OK;
 }
 

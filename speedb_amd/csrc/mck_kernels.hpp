@@ -844,26 +844,15 @@ __device__ __forceinline__ bool wal_il_step(const WalIlCtx& X, const WalIlState&
   return wave_any(go);
 }
 
-__device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
-                                             const CrcTables* __restrict__ g) {
-  constexpr bool BLK = true;  // contiguous fragment ranges per workgroup
-  constexpr int W = kWalW, NP = kWalNP;
-  const RowShare sh = row_share<BLK>(first, count);
-  crc_rows_prologue<OpWalWrite>(op, sh, lds, g, false);
-  // fragments' dst_off, staged like the descriptors (row_desc_stage order)
+// fragments' dst_off, staged like the descriptors (row_desc_stage order)
+__device__ __forceinline__ void wal_stage_dst(const OpWalWrite& op, const RowShare& sh) {
   for (uint32_t t = threadIdx.x; t < sh.n; t += blockDim.x) *lds_p64(kLdsWalAux + 8 * t) = op.frags[sh.idx(t)].dst_off;
-  {  // lane-final map over lane-final columns 0-15, the piece-to-piece byte table
-    const uint32_t t = threadIdx.x;
-    if (t < 512) {
-      const uint4 x = reinterpret_cast<const uint4*>(&g->lane_final16[0][0][0])[t];
-      *reinterpret_cast<uint4*>(lds + kLdsFinal + 256 * (t >> 2) + 16 * (t & 3)) = x;
-    } else if (t < 768) {
-      const uint4 x = reinterpret_cast<const uint4*>(&g->gap244[0][0])[t - 512];
-      *reinterpret_cast<uint4*>(lds + kLdsWalGap244 + 16 * (t - 512)) = x;
-    }
-  }
-  __syncthreads();
-  const CrcLane L = crc_lane();
+}
+
+// The row loop over one window of <= kRowDescCache fragments (staged).
+__device__ __forceinline__ void wal_write_window(const OpWalWrite& op, const RowShare& sh, const CrcLane& L,
+                                                 const CrcTables* __restrict__ g) {
+  constexpr int W = kWalW, NP = kWalNP;
   const uint32_t c = threadIdx.x & (W - 1);
   const uint32_t share = sh.n;
   // the row's LDS slot for the previous round's straddling piece
@@ -890,6 +879,47 @@ __device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t firs
   for (;;) {
     if (!wal_il_step(X, A, ca, B, cb, x)) break;
     if (!wal_il_step(X, B, cb, A, ca, x)) break;
+  }
+}
+
+// A workgroup's contiguous fragment range in windows of <= kRowDescCache
+// (its LDS descriptor and dst_off tables): one launch serves any group
+// commit (round 4; launches of <= ncu * kRowDescCache fragments each paid
+// the launch's ramp and drain, 6 per 2M-record step).
+__device__ __forceinline__ void wal_write_il(const OpWalWrite& op, uint32_t first, uint32_t count, uint8_t* lds,
+                                             const CrcTables* __restrict__ g) {
+  constexpr bool BLK = true;  // contiguous fragment ranges per workgroup
+  const RowShare share = row_share<BLK>(first, count);
+  const uint32_t nwin = (share.n + kRowDescCache - 1) / kRowDescCache;
+  if (nwin == 0) return;  // workgroup-uniform
+  auto win = [&](uint32_t wi) {
+    const uint32_t w0 = (uint32_t)((uint64_t)share.n * wi / nwin), w1 = (uint32_t)((uint64_t)share.n * (wi + 1) / nwin);
+    return RowShare{share.start + share.stride * w0, share.stride, w1 - w0};
+  };
+  const RowShare sh0 = win(0);
+  crc_rows_prologue<OpWalWrite>(op, sh0, lds, g, false);
+  wal_stage_dst(op, sh0);
+  {  // lane-final map over lane-final columns 0-15, the piece-to-piece byte table
+    const uint32_t t = threadIdx.x;
+    if (t < 512) {
+      const uint4 x = reinterpret_cast<const uint4*>(&g->lane_final16[0][0][0])[t];
+      *reinterpret_cast<uint4*>(lds + kLdsFinal + 256 * (t >> 2) + 16 * (t & 3)) = x;
+    } else if (t < 768) {
+      const uint4 x = reinterpret_cast<const uint4*>(&g->gap244[0][0])[t - 512];
+      *reinterpret_cast<uint4*>(lds + kLdsWalGap244 + 16 * (t - 512)) = x;
+    }
+  }
+  __syncthreads();
+  const CrcLane L = crc_lane();
+  for (uint32_t wi = 0; wi < nwin; wi++) {
+    const RowShare sh = win(wi);
+    if (wi) {
+      __syncthreads();  // every row is done with the previous window's slots
+      row_desc_stage<OpWalWrite>(op, sh, false);
+      wal_stage_dst(op, sh);
+      __syncthreads();
+    }
+    wal_write_window(op, sh, L, g);
   }
 }
 
