@@ -4,7 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-O=gpurun_out/final
+O=gpurun_out/${1:-final}
 mkdir -p $O
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/gpu_tests.log 2>&1 || { tail -40 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
