@@ -893,8 +893,17 @@ __device__ __forceinline__ uint32_t row_finish4(uint32_t s, const RowSpan& sp, u
 
 // The span's CRC (Extend semantics) in every lane of its row; Lf = the lane
 // constants with lane4 = (64 - W + c) * 4 (shift by 64 (W - 1 - c)).
+// 4-lane rows: the shift and the un-shift as one map (CrcTables::rowfin4,
+// copied over the lane-final tables by crc_rows_windows_w<.., 4>): 8 lookups
+// per finish instead of 16, and no un-shift branch.
+constexpr uint32_t kLdsRowFin4 = kLdsFinal;
 template <int W>
 __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, const CrcLane& Lf) {
+  if constexpr (W == 4) {
+    const uint32_t c = (Lf.lane4 >> 2) - 60u;  // Lf.lane4 = (64 - W + c) * 4
+    const uint32_t p = row_xor32<4>(crc_nibmap(kLdsRowFin4 + ((c * 16u + sp.kt) << 9), s));
+    return sp.n == 0 ? sp.init : ~p;
+  }
   uint32_t p = s;  // W = 1: the lane's state is the span's (no shift, no row XOR)
   if constexpr (W > 1) p = row_xor32<W>(crc_lane_final(s, Lf));
   if (wave_any(sp.kt != 0)) p = crc_unshift(sp.kt, p);
@@ -1106,6 +1115,17 @@ template <class Op, int W>
 __device__ __forceinline__ void crc_rows_windows_w(const Op& op, const RowShare& share, uint32_t nwin,
                                                    const CrcTables* __restrict__ g) {
   const uint32_t n = share.n;
+  if constexpr (W == 4) {  // the combined finish maps over the (unused) lane-final tables
+    static_assert(sizeof(g->rowfin4) == 32768 && kLdsRowFin4 + 32768 <= kLdsGap, "rowfin4 fits the lane-final area");
+    const uint4* src = reinterpret_cast<const uint4*>(&g->rowfin4[0][0][0][0]);
+    const uint4 a = src[threadIdx.x], b = src[threadIdx.x + kCrcBlock];  // 2 x 16 B per thread
+    __syncthreads();  // (no reader of the lane-final tables in this mode; the barrier orders the fill)
+    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsRowFin4 + 16 * threadIdx.x)) =
+        span_u32x4{a.x, a.y, a.z, a.w};
+    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(
+        static_cast<size_t>(kLdsRowFin4 + 16 * (threadIdx.x + kCrcBlock))) = span_u32x4{b.x, b.y, b.z, b.w};
+    __syncthreads();
+  }
   for (uint32_t wi = 0; wi < nwin; wi++) {
     const uint32_t w0 = (uint32_t)((uint64_t)n * wi / nwin), w1 = (uint32_t)((uint64_t)n * (wi + 1) / nwin);
     const RowShare sh{share.start + share.stride * w0, share.stride, w1 - w0};
