@@ -42,6 +42,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "mck_common.hpp"
 #include "mck_tables.hpp"
 
@@ -893,15 +895,43 @@ __device__ __forceinline__ uint32_t row_finish4(uint32_t s, const RowSpan& sp, u
 
 // The span's CRC (Extend semantics) in every lane of its row; Lf = the lane
 // constants with lane4 = (64 - W + c) * 4 (shift by 64 (W - 1 - c)).
-// 4-lane rows: the shift and the un-shift as one map (CrcTables::rowfin4,
-// copied over the lane-final tables by crc_rows_windows_w<.., 4>): 8 lookups
-// per finish instead of 16, and no un-shift branch.
+// 4- and 8-lane rows: the shift and the un-shift as one map
+// (CrcTables::rowfin4 / rowfin8, copied by crc_rows_windows_w): 8 lookups
+// per finish instead of 16, and no un-shift branch.  rowfin4 (32 KiB) goes
+// over the lane-final tables, which no row mode but 16-lane rows reads;
+// rowfin8 (64 KiB) over those and the un-shift tables, so only for ops
+// that never un-shift an init at run time (no per-span init array: the init
+// injection tables are built before the copy).
 constexpr uint32_t kLdsRowFin4 = kLdsFinal;
+template <class Op, class = void>
+struct op_array_init : std::false_type {};
+template <class Op>
+struct op_array_init<Op, std::void_t<decltype(Op::kArrayInit)>> : std::bool_constant<Op::kArrayInit> {};
+template <class Op>
+constexpr bool kRowFin8 = !op_array_init<Op>::value;
+// The combined map of (lane c, kt) applied to s: 8 nibble lookups in the
+// lane-minor layout [kt][n][v][c]; W = 8 splits it by kt over the two 32 KiB
+// halves (kt < 8: the lane-final area, else the un-shift area).
 template <int W>
+__device__ __forceinline__ uint32_t row_finmap(uint32_t s, uint32_t c, uint32_t kt) {
+  constexpr uint32_t kMap = 8 * 16 * W * 4;  // bytes per kt
+  const uint32_t base = W == 4 ? kLdsFinal + kt * kMap
+                               : (kt < 8 ? kLdsFinal : kLdsUnshift) + (kt & 7u) * kMap;
+  uint32_t x[8];
+#pragma unroll
+  for (int n = 0; n < 8; n++) x[n] = lds_u32(base + ((uint32_t)n * 16u + ((s >> (4 * n)) & 15u)) * (W * 4) + 4 * c);
+  return xor3(xor3(x[0], x[1], x[2]), xor3(x[3], x[4], x[5]), x[6] ^ x[7]);
+}
+template <int W, bool FIN8 = false>
 __device__ __forceinline__ uint32_t row_finish(uint32_t s, const RowSpan& sp, const CrcLane& Lf) {
   if constexpr (W == 4) {
     const uint32_t c = (Lf.lane4 >> 2) - 60u;  // Lf.lane4 = (64 - W + c) * 4
-    const uint32_t p = row_xor32<4>(crc_nibmap(kLdsRowFin4 + ((c * 16u + sp.kt) << 9), s));
+    const uint32_t p = row_xor32<4>(row_finmap<4>(s, c, sp.kt));
+    return sp.n == 0 ? sp.init : ~p;
+  }
+  if constexpr (W == 8 && FIN8) {
+    const uint32_t c = (Lf.lane4 >> 2) - 56u;
+    const uint32_t p = row_xor32<8>(row_finmap<8>(s, c, sp.kt));
     return sp.n == 0 ? sp.init : ~p;
   }
   uint32_t p = s;  // W = 1: the lane's state is the span's (no shift, no row XOR)
@@ -1040,7 +1070,8 @@ __device__ __forceinline__ bool crc_rows_step(const RowCtx<Op>& x, const RowStat
   }
   B.live = go ? 1u : 0u;
   s = row_round<W>(s, ca, A.sp, A.r, x.c, x.L);
-  if (wave_any(live && last)) x.op.finish(A.i, row_finish<W>(s, A.sp, x.Lf), pa, live && last && x.c == 0);
+  if (wave_any(live && last))
+    x.op.finish(A.i, row_finish<W, kRowFin8<Op>>(s, A.sp, x.Lf), pa, live && last && x.c == 0);
   return wave_any(go);
 }
 
@@ -1115,15 +1146,22 @@ template <class Op, int W>
 __device__ __forceinline__ void crc_rows_windows_w(const Op& op, const RowShare& share, uint32_t nwin,
                                                    const CrcTables* __restrict__ g) {
   const uint32_t n = share.n;
-  if constexpr (W == 4) {  // the combined finish maps over the (unused) lane-final tables
+  if constexpr (W == 4 || (W == 8 && kRowFin8<Op>)) {  // the combined finish maps (row_finish)
     static_assert(sizeof(g->rowfin4) == 32768 && kLdsRowFin4 + 32768 <= kLdsGap, "rowfin4 fits the lane-final area");
-    const uint4* src = reinterpret_cast<const uint4*>(&g->rowfin4[0][0][0][0]);
-    const uint4 a = src[threadIdx.x], b = src[threadIdx.x + kCrcBlock];  // 2 x 16 B per thread
-    __syncthreads();  // (no reader of the lane-final tables in this mode; the barrier orders the fill)
-    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsRowFin4 + 16 * threadIdx.x)) =
-        span_u32x4{a.x, a.y, a.z, a.w};
-    *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(
-        static_cast<size_t>(kLdsRowFin4 + 16 * (threadIdx.x + kCrcBlock))) = span_u32x4{b.x, b.y, b.z, b.w};
+    static_assert(sizeof(g->rowfin8) == 65536 && kLdsUnshift + 32768 <= kCrcLdsBytes, "rowfin8 halves fit");
+    const uint4* src = reinterpret_cast<const uint4*>(W == 4 ? &g->rowfin4[0][0][0][0] : &g->rowfin8[0][0][0][0]);
+    constexpr int kPer = W == 4 ? 2 : 4;  // 16-byte slots per thread
+    uint4 v[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; k++) v[k] = src[threadIdx.x + kCrcBlock * k];
+    __syncthreads();  // every reader of the tables overwritten here is done (the init tables are built)
+#pragma unroll
+    for (int k = 0; k < kPer; k++) {
+      const uint32_t slot = threadIdx.x + kCrcBlock * k;  // 2048 slots = 32 KiB per half
+      const uint32_t off = slot < 2048 ? kLdsFinal + 16 * slot : kLdsUnshift + 16 * (slot - 2048);
+      *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(off)) =
+          span_u32x4{v[k].x, v[k].y, v[k].z, v[k].w};
+    }
     __syncthreads();
   }
   for (uint32_t wi = 0; wi < nwin; wi++) {

@@ -149,6 +149,7 @@ struct OpCrcValue {
   uint32_t flags;
   uint32_t* out;
   typedef NoPre Pre;
+  static constexpr bool kArrayInit = true;  // per-span inits: the row loop un-shifts them (no rowfin8)
   __device__ const uint8_t* base() const { return s.base; }
   __device__ uint64_t off(uint32_t i) const { return s.off(i); }
   __device__ uint64_t len(uint32_t i) const { return s.len(i); }

@@ -48,10 +48,12 @@ struct alignas(16) CrcTables {
   uint32_t gap244[4][256];           // zshift(v << 8t, 244): piece to piece
   // body/head driver (mck_crc_bh.hpp): a span's parts moved to its end
   uint32_t pow1k[kPowBits][8][16];    // zshift(v << 4n, 1024 * 2^b)
-  // 4-lane rows' finish (round 4): lane c's shift to the row's end and the
-  // un-shift of the kt trailing zero bytes as ONE map, a shift by
-  // 64 (3 - c) - kt bytes (an un-shift for c = 3)
-  uint32_t rowfin4[4][16][8][16];
+  // 4- / 8-lane rows' finish (round 4): lane c's shift to the row's end and
+  // the un-shift of the kt trailing zero bytes as ONE map, a shift by
+  // 64 (W - 1 - c) - kt bytes (an un-shift for c = W - 1); lane-minor, as
+  // lane_final, so the lanes of a row read neighbouring LDS banks
+  uint32_t rowfin4[16][8][16][4];  // [kt][n][v][c]
+  uint32_t rowfin8[16][8][16][8];
 };
 
 // ---- host-side GF(2) helpers (also used by the host shims) ----------------
@@ -136,21 +138,22 @@ inline void build_crc_tables(CrcTables* t) {
         for (int i = 0; i < 8 * k; i++) x = gf_unmulx(x);
         t->unshift[k][n][v] = x;
       }
-  for (int c = 0; c < 4; c++)
-    for (int kt = 0; kt < 16; kt++) {
-      const int d = kChunkBytes * (3 - c) - kt;  // bytes; < 0 only for c = 3
-      const uint32_t k = d >= 0 ? gf_xpow8n((uint64_t)d) : 0u;
+  // rowfin4 / rowfin8: lane c of a W-lane row, kt trailing bytes: a shift
+  // by 64 (W - 1 - c) - kt bytes (< 0, an un-shift, only for c = W - 1)
+  auto rowfin = [&](int W, int c, int kt, int n, int v) {
+    const int d = kChunkBytes * (W - 1 - c) - kt;
+    uint32_t x = (uint32_t)v << (4 * n);
+    if (d >= 0) return gf_mul(x, gf_xpow8n((uint64_t)d));
+    for (int i = 0; i < -8 * d; i++) x = gf_unmulx(x);
+    return x;
+  };
+  for (int c = 0; c < 8; c++)
+    for (int kt = 0; kt < 16; kt++)
       for (int n = 0; n < 8; n++)
         for (int v = 0; v < 16; v++) {
-          uint32_t x = (uint32_t)v << (4 * n);
-          if (d >= 0) {
-            x = gf_mul(x, k);
-          } else {
-            for (int i = 0; i < -8 * d; i++) x = gf_unmulx(x);
-          }
-          t->rowfin4[c][kt][n][v] = x;
+          if (c < 4) t->rowfin4[kt][n][v][c] = rowfin(4, c, kt, n, v);
+          t->rowfin8[kt][n][v][c] = rowfin(8, c, kt, n, v);
         }
-    }
 }
 
 }  // namespace mck
