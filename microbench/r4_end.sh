@@ -7,7 +7,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 export PYTHONUNBUFFERED=1 TMPDIR=/tmp
-tag=r4end
+tag=${R4_TAG:-r4end}
 O=gpurun_out/bench_$tag
 mkdir -p $O
 B="timeout -k 10 240 python -u bench.py"
