@@ -299,7 +299,7 @@ def make_workload(args, dev, rank, world):
             w.step = lambda: S.crc32c_batch(spans, out=out32, stream=stream)
             # 16-byte-multiple blocks: the whole-round uniform kernel; any
             # other size (a 4300-B SST block): the ragged path
-            w.kernel = CRC_UNIFORM_FULL if block % 4096 == 0 else _ragged("mck::OpCrcValue", block)
+            w.kernel = CRC_UNIFORM_FULL if block % 4096 == 0 else _ragged("mck::OpCrcValueZ", block)
             w.alg_bytes = count * (block + 4)
         else:
             w.step = lambda: S.xxh3_64_batch(spans, out=out64, stream=stream)
@@ -466,7 +466,7 @@ def make_workload(args, dev, rank, world):
                       f"{args.span_min}-{args.span_max} B per GPU at any byte offset, mck_wal_record_crc_batch")
         else:
             w.step = lambda: S.crc32c_batch(sp, out=out, stream=stream)
-            w.kernel = _ragged("mck::OpCrcValue", float(lens.mean()))
+            w.kernel = _ragged("mck::OpCrcValueZ", float(lens.mean()))
             w.desc = (f"crc32c_batch over {count} ragged spans of {args.span_min}-{args.span_max} B per GPU "
                       "(explicit offsets/lengths)")
         w.span_bytes = int(lens.sum())
@@ -688,7 +688,7 @@ def make_workload(args, dev, rank, world):
                 1, hbuf.data_ptr(), None, None, block, block, count, 0, ndev, 256 << 20,
                 out.ctypes.data, None, ctypes.byref(secs)), "mck_host_batch_checksum")
         w.step = step
-        w.kernel = _ragged("mck::OpCrcValue", 4300) + " (H2D/D2H overlapped)"
+        w.kernel = _ragged("mck::OpCrcValueZ", 4300) + " (H2D/D2H overlapped)"
         w.span_bytes = count * block
         w.alg_bytes = count * (block + 4 + 8 + 4)
         per = count // max(1, ndev)

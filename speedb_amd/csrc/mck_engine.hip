@@ -715,6 +715,8 @@ int mck_crc32c_batch(const mck_spans* spans, const uint32_t* init_crcs, uint32_t
   const OpCrcValue op{to_src(spans), init_crcs, flags & MCK_F_MASK, out};
   if (!init_crcs && is_uniform_aligned(spans))
     return launch_crc_uniform(op, spans, reinterpret_cast<hipStream_t>(stream));
+  if (!init_crcs)  // (no init array: OpCrcValueZ takes the rows' combined finish maps)
+    return launch_crc(OpCrcValueZ{op}, spans->count, reinterpret_cast<hipStream_t>(stream));
   return launch_crc(op, spans->count, reinterpret_cast<hipStream_t>(stream));
 }
 

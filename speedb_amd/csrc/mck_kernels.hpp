@@ -164,6 +164,15 @@ struct OpCrcValue {
   }
 };
 
+// OpCrcValue without per-span inits (Value, init 0): the 8-lane rows'
+// combined finish maps apply (kRowFin8: no init un-shift at run time)
+struct OpCrcValueZ : OpCrcValue {
+  static constexpr bool kArrayInit = false;
+  __device__ int init_kind() const { return kInitZero; }
+  __device__ uint32_t init_key(uint32_t) const { return 0u; }
+  __device__ uint32_t init_crc(uint32_t) const { return 0u; }
+};
+
 // WAL write side: init = Value(type byte [+ LE32 log number])
 struct WalTypeCrcs {
   uint32_t v[16];
