@@ -27,6 +27,7 @@ declare -A ARGS=(
   [kv100]="--workload blockkv --kv-value-bytes 100"
   [kv1000]="--workload blockkv --kv-value-bytes 1000"
   [walwrite]="--workload walwrite"
+  [wal]="--workload wal"
 )
 B="timeout -k 10 180 python -u bench.py --cpu-seconds 0 --steps 20 --warmup 20"
 V=$PWD/microbench/_variants
