@@ -106,6 +106,8 @@ def parse():
     # 0.77 -> 0.90 -> 0.76 ms per launch at 1M x 4 KiB): run the workload
     # untimed for this long before the warmup steps, whatever W is
     p.add_argument("--settle-ms", type=float, default=250.0)
+    p.add_argument("--engine-lib", default=None,
+                   help="time an alternative build of the engine (A/B runs); the line records its path + sha256")
     p.add_argument("--workload", choices=["crc32c", "xxh3", "sst", "wal", "host", "kv", "file", "walwrite", "blob", "shim", "blockkv",
                             "walrec", "ragged", "latency"], default="crc32c")
     p.add_argument("--blocks", type=int, default=1 << 20)
@@ -306,8 +308,8 @@ def make_workload(args, dev, rank, world):
             w.kernel = "mck::k_xxh3<mck::OpX3Value>"
             w.alg_bytes = count * (block + 8)
         w.span_bytes = count * block
-        w.desc = (f"{args.workload} over {count} x {block} B random blocks per GPU, device-resident "
-                  "(BASELINE.json configs[1])")
+        w.desc = (f"{args.workload} over {count} x {block} B random blocks per GPU, device-resident" +
+                  (" (BASELINE.json configs[1])" if block == 4096 and args.blocks == 1 << 20 else ""))
         w.cfg = {"blocks_per_gpu": count, "block_bytes": block}
 
         def check():
@@ -346,13 +348,15 @@ def make_workload(args, dev, rank, world):
                                int(S.ChecksumType.kXXH3): "mck::k_xxh3_wave<mck::OpX3Block<2> >"}[int(t)]
                               for t in types)
         w.span_bytes = sum(im.payload_bytes + im.count for im in imgs)  # payload + type byte
-        # per launch: span bytes + 4 B stored + 8 B offset + 4 B length + 8 B
-        # file offset in, 1 B flag + 4 + 4 B out
-        w.alg_bytes = sum(im.payload_bytes + im.count * (1 + 4 + 8 + 4 + 8 + 1 + 4 + 4)
+        # per launch, SURVEY.md 8(d): span bytes (payload + type byte) + the
+        # 4 B stored checksum read + the outputs written (1 B mismatch flag,
+        # 4 B computed, 4 B stored); descriptors are not counted
+        w.alg_bytes = sum(im.payload_bytes + im.count * (1 + 4 + 1 + 4 + 4)
                           for im in imgs) / len(imgs)
         w.desc = ("VerifyBlockChecksum over a compaction-shaped run of 4/16/64 KiB (+0..255 B) SST "
                   f"blocks, {args.sst_bytes >> 20} MiB per image, format_version 6 context "
-                  "checksums; one kCRC32c + one kXXH3 image per step (BASELINE.json configs[2])")
+                  "checksums; " + ("one kCRC32c + one kXXH3 image per step" if len(imgs) == 2 else "one image per step") +
+                  (" (BASELINE.json configs[2])" if len(imgs) == 2 and args.sst_bytes == 1 << 30 else ""))
         w.cfg = {"blocks_per_gpu": sum(im.count for im in imgs), "image_bytes": args.sst_bytes,
                  "checksum_types": [S.ChecksumType(int(t)).name for t in types]}
         if side is not None:
@@ -911,6 +915,9 @@ def check_world(requested, world_env) -> int:
 
 def main():
     args = parse()
+    if args.engine_lib:  # the only way a bench run loads another engine build (speedb_amd/_lib.py)
+        os.environ["SPEEDB_AMD_LIB"] = os.path.abspath(args.engine_lib)
+        os.environ["SPEEDB_AMD_AB"] = "1"
     if args.workload == "shim":
         return shim_latency(args)
     if args.workload == "latency":
@@ -1012,6 +1019,7 @@ def main():
             "config": dict({"workload": w.desc, "parallelism": f"partitioned x{world} (no collective)"},
                            **w.cfg),
             "roofline": roof, "cpu_baseline": cpu, "verified": verified,
+            "engine": _lib.lib_identity(),
         }
         if getattr(w, "device_only", None):
             line["device_only"] = w.device_only

@@ -50,6 +50,8 @@ class Status {
   bool IsCorruption() const { return code_ == kCorruption; }
   bool IsInvalidArgument() const { return code_ == kInvalidArgument; }
   bool IsNotSupported() const { return code_ == kNotSupported; }
+  bool IsIOError() const { return code_ == kIOError; }
+  const std::string& message() const { return msg_; }
   std::string ToString() const {
     switch (code_) {
       case kOk:

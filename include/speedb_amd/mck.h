@@ -332,8 +332,13 @@ typedef struct mck_wal_report {
 } mck_wal_report;
 
 /* Outputs of mck_wal_read_records.  Every array pointer may be NULL (counts
- * only); the *_cap fields give the array sizes. */
+ * only); the *_cap fields give the array sizes.  Zero-initialise the struct
+ * and set struct_size = sizeof(mck_wal_read_out): the library writes no field
+ * past struct_size, and a caller whose struct ends before the compression
+ * fields (MCK_WAL_READ_OUT_V1_SIZE) gets MCK_ENOTSUP for a compressed WAL
+ * instead of a write past its struct. */
 typedef struct mck_wal_read_out {
+  uint64_t struct_size;       /* sizeof(mck_wal_read_out) of the caller    */
   mck_wal_fragment* frags;    /* payload fragments of the returned records */
   uint64_t frag_cap;
   uint64_t nfrags;
@@ -366,6 +371,8 @@ typedef struct mck_wal_read_out {
   uint64_t stream_cap;
   uint64_t nstream;
 } mck_wal_read_out;
+/* struct_size of the layout without the compression fields */
+#define MCK_WAL_READ_OUT_V1_SIZE 120
 
 /* log::Reader (checksum = true, no WAL compression) reading a whole WAL
  * image in HOST memory: ReadRecord (db/log_reader.cc:69-321) called until it
@@ -625,12 +632,21 @@ int mck_block_kv_protect_blocks_batch(int kind, const mck_spans* blocks,
                                       uint32_t* restart_interval,
                                       int32_t* status, void* work,
                                       uint8_t* out, mck_stream_t stream);
-/* ... and the read-side check in one pass: mismatch[key] as
- * mck_block_kv_verify_batch (mismatch: count * slot_cap bytes). */
+/* ... and the read-side check in one pass.  key_base / total_keys are the
+ * PROTECT-time key index (key_base[count + 1], device; total_keys =
+ * key_base[count], at most count * slot_cap): `stored` and `mismatch` are laid
+ * out by it, as the iterators index kv_checksum_ by the entry's position in
+ * its own block (block.h:623).  mismatch: total_keys bytes.  status / restart
+ * interval: the walk's.  A block whose walk now fails, or gives another entry
+ * count than key_base, has every one of its keys flagged (the iterator's
+ * CorruptionError, block.h:559-565) and no other block's keys move.  A block
+ * with status MCK_BLOCK_SLOT_OVERFLOW is not verified (its keys are left
+ * unflagged): re-verify the batch with mck_block_kv_verify_batch. */
 int mck_block_kv_verify_blocks_batch(int kind, const mck_spans* blocks,
                                      uint32_t prot_bytes, uint32_t slot_cap,
-                                     uint32_t arena_cap, uint64_t* key_base,
-                                     uint64_t* arena_base,
+                                     uint32_t arena_cap,
+                                     const uint64_t* key_base,
+                                     uint64_t total_keys,
                                      uint32_t* restart_interval,
                                      int32_t* status, void* work,
                                      const uint8_t* stored, uint8_t* mismatch,

@@ -34,7 +34,7 @@ V=$PWD/microbench/_variants
 for v in ${AB_VARIANTS:-r3base new}; do
   for wl in ${AB_WL:-r4100 r16k sstc blob}; do
     if [ $v = new ]; then env -u SPEEDB_AMD_LIB $B ${ARGS[$wl]} > $O/${wl}_$v.json || exit 1
-    else env SPEEDB_AMD_LIB=$V/$v.so $B ${ARGS[$wl]} > $O/${wl}_$v.json || exit 1; fi
+    else env SPEEDB_AMD_AB=1 SPEEDB_AMD_LIB=$V/$v.so $B ${ARGS[$wl]} > $O/${wl}_$v.json || exit 1; fi
   done
 done
 for f in $O/*.json; do echo "$f $(python3 -c "import json,sys; d=json.load(open('$f')); print(d['value'], d['roofline']['frac'], d['roofline'].get('kernel_avg_ms'), d.get('verified'))")"; done

@@ -8,7 +8,7 @@ export PYTHONUNBUFFERED=1 TMPDIR=/tmp
 B="timeout -k 10 180 python -u bench.py --cpu-seconds 0 --steps 20 --warmup 20"
 V=$PWD/microbench/_variants
 for v in r3base wsum; do
-  P="env SPEEDB_AMD_LIB=$V/$v.so"
+  P="env SPEEDB_AMD_AB=1 SPEEDB_AMD_LIB=$V/$v.so"
   $P $B --workload sst > $O/sst_$v.json || exit 1
   $P $B --workload sst --sst-types crc32c > $O/sstc_$v.json || exit 1
   $P $B --workload sst --sst-types xxh3 > $O/sstx_$v.json || exit 1

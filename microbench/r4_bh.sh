@@ -13,7 +13,7 @@ tail -2 $O/tests.log
 B="timeout -k 10 180 python -u bench.py --cpu-seconds 0 --steps 20 --warmup 20"
 V=$PWD/microbench/_variants
 for v in r3base new; do
-  if [ $v = r3base ]; then P="env SPEEDB_AMD_LIB=$V/r3base.so"; else P=""; fi
+  if [ $v = r3base ]; then P="env SPEEDB_AMD_AB=1 SPEEDB_AMD_LIB=$V/r3base.so"; else P=""; fi
   $P $B --workload crc32c --block-bytes 4300 --blocks 1000000 > $O/u4300_$v.json || exit 1
   $P $B --workload ragged --span-min 4100 --span-max 4400 --span-bytes $((4<<30)) > $O/r4100_$v.json || exit 1
   $P $B --workload ragged --span-min 4096 --span-max 4096 --span-bytes $((4<<30)) > $O/r4096_$v.json || exit 1

@@ -27,7 +27,7 @@ PB="SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_I
 PC="TA_TA_BUSY_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE"
 for wl in ${PROF_WL:-r4100 r16k}; do
   for v in ${PROF_VARIANTS:-r3base new}; do
-    if [ $v = r3base ]; then E="SPEEDB_AMD_LIB=$V/r3base.so"; else E="-u SPEEDB_AMD_LIB"; fi
+    if [ $v = r3base ]; then E="SPEEDB_AMD_AB=1 SPEEDB_AMD_LIB=$V/r3base.so"; else E="-u SPEEDB_AMD_LIB"; fi
     d=$O/${wl}_$v
     mkdir -p $d
     B="python3 bench.py ${ARGS[$wl]} --cpu-seconds 0 --no-verify --steps 5 --warmup 3"

@@ -7,7 +7,7 @@ timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -1 $out/t.log
 for i in 1 2; do
   for v in new old; do
-    if [ $v = old ]; then export SPEEDB_AMD_LIB=$PWD/$B; else unset SPEEDB_AMD_LIB; fi
+    if [ $v = old ]; then export SPEEDB_AMD_AB=1 SPEEDB_AMD_LIB=$PWD/$B; else unset SPEEDB_AMD_LIB; fi
     timeout -k 10 120 python bench.py --workload sst --sst-types xxh3 --no-verify > $out/x3_$v$i.json 2>/dev/null || exit 1
     timeout -k 10 120 python bench.py --workload sst --no-verify > $out/sst_$v$i.json 2>/dev/null || exit 1
   done

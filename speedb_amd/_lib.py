@@ -7,12 +7,23 @@ library is missing, importing this module raises.
 from __future__ import annotations
 
 import ctypes
+import hashlib
 import os
+import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# SPEEDB_AMD_LIB: an alternative build of the same engine (A/B experiments
-# under microbench/); the default is the in-tree library.
-LIB_PATH = os.environ.get("SPEEDB_AMD_LIB") or os.path.join(_HERE, "libspeedb_amd.so")
+DEFAULT_LIB_PATH = os.path.join(_HERE, "libspeedb_amd.so")
+# An alternative build of the same engine (A/B experiments under microbench/,
+# `bench.py --engine-lib PATH`) is loaded only when BOTH SPEEDB_AMD_LIB names
+# it and SPEEDB_AMD_AB=1 says so: a stray SPEEDB_AMD_LIB in a production
+# environment is refused instead of silently swapping the engine.
+_OVERRIDE = os.environ.get("SPEEDB_AMD_LIB")
+AB_MODE = os.environ.get("SPEEDB_AMD_AB") == "1"
+if _OVERRIDE and not AB_MODE:
+    raise ImportError(
+        f"speedb_amd: SPEEDB_AMD_LIB={_OVERRIDE} is set without SPEEDB_AMD_AB=1; an alternative engine "
+        "build is loaded only for explicit A/B runs (bench.py --engine-lib PATH)")
+LIB_PATH = _OVERRIDE if _OVERRIDE else DEFAULT_LIB_PATH
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
@@ -21,6 +32,17 @@ if not os.path.exists(LIB_PATH):
         "There is no CPU fallback.")
 
 lib = ctypes.CDLL(LIB_PATH)
+
+
+def lib_identity() -> dict:
+    """Path and sha256 of the engine this process loaded (recorded in every
+    bench line, so a number names the exact .so it timed)."""
+    h = hashlib.sha256()
+    with open(LIB_PATH, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return {"path": os.path.relpath(LIB_PATH, os.path.dirname(_HERE)) if LIB_PATH.startswith(os.path.dirname(_HERE))
+            else LIB_PATH, "sha256": h.hexdigest(), "override": bool(_OVERRIDE)}
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -110,8 +132,8 @@ SIGNATURES = [
      [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp,
       vp, vp, vp]),
     ("mck_block_kv_verify_blocks_batch", ctypes.c_int,
-     [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp, vp,
-      vp, vp, vp, vp, vp]),
+     [ctypes.c_int, ctypes.POINTER(mck_spans), ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, vp,
+      ctypes.c_uint64, vp, vp, vp, vp, vp, vp, vp]),
     ("mck_sst_decode_footer", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
     ("mck_sst_list_blocks", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
     ("mck_sst_verify_footer", ctypes.c_int, [vp, vp]),
@@ -152,17 +174,21 @@ SIGNATURES = [
     ("mck_perf_context_get", ctypes.c_int, [vp, ctypes.c_int]),
 ]
 
+MISSING_SYMBOLS = []
 for _name, _res, _args in SIGNATURES:
     try:
         _f = getattr(lib, _name)
     except AttributeError:
         # an older build loaded for an A/B timing run may lack newer entry
-        # points; the in-tree library must export every one
-        if "SPEEDB_AMD_LIB" in os.environ:
+        # points (named on stderr); the in-tree library must export every one
+        if _OVERRIDE:
+            MISSING_SYMBOLS.append(_name)
             continue
         raise
     _f.restype = _res
     _f.argtypes = _args
+if MISSING_SYMBOLS:
+    print(f"speedb_amd: A/B engine {LIB_PATH} lacks {', '.join(MISSING_SYMBOLS)}", file=sys.stderr)
 
 
 class MckError(RuntimeError):

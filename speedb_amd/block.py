@@ -179,45 +179,63 @@ def InitializeMetaIndexBlockProtectionInfo(blocks: Spans, protection_bytes_per_k
     return InitializeBlockProtectionInfo(BlockKind.kMetaIndex, blocks, protection_bytes_per_key, stream)
 
 
-def VerifyBlockProtectionInfo(blocks: Spans, prot: BlockProtection, stored=None, stream=None):
+def VerifyBlockProtectionInfo(blocks: Spans, prot: BlockProtection, stored=None, stream=None,
+                              return_status: bool = False):
     """Check every entry against ``stored`` (default: prot.kv_checksum, as
     read back from the block cache).  Returns (mismatch uint8 [total_keys],
-    mismatch_count int32[1])."""
+    mismatch_count int32[1]) laid out by ``prot.key_base`` -- the protect-time
+    index, as the iterators index kv_checksum_ (block.h:623) -- and, with
+    ``return_status``, the walk's per-block status (int32 [count] device; None
+    for the two-pass verify, which has none).
+
+    A block that no longer walks (bad header, entry or restart array) or now
+    holds another number of entries has ALL of its keys flagged -- the
+    iterator's CorruptionError (block.h:559-565) -- and no other block's keys
+    move.  A block the one-pass walk cannot park (kSlotOverflow) sends the
+    whole batch to the two-pass verify."""
     torch = _torch()
     dev = blocks.base.device
     stored = prot.kv_checksum if stored is None else stored
     count = torch.zeros(1, dtype=torch.int32, device=dev)
+    mismatch = torch.empty(max(prot.total_keys, 1), dtype=torch.uint8, device=dev)
     s = blocks.c()
-    if prot.slot_cap:  # one pass: the walk again, compared instead of stored
-        n = blocks.count
-        key_base, arena_base, status, interval, work = _blocks_outputs(blocks, prot.slot_cap, prot.arena_cap)
-        mismatch = torch.empty(max(n * prot.slot_cap, 1), dtype=torch.uint8, device=dev)
+    n = blocks.count
+    if prot.slot_cap and prot.total_keys <= n * prot.slot_cap:  # one pass: the walk again, compared
+        _, _, status, interval, work = _blocks_outputs(blocks, prot.slot_cap, prot.arena_cap)
         check(lib.mck_block_kv_verify_blocks_batch(int(prot.kind), ctypes.byref(s), prot.protection_bytes_per_key,
-                                                   prot.slot_cap, prot.arena_cap, key_base.data_ptr(),
-                                                   arena_base.data_ptr(), interval.data_ptr(), status.data_ptr(),
+                                                   prot.slot_cap, prot.arena_cap, prot.key_base.data_ptr(),
+                                                   prot.total_keys, interval.data_ptr(), status.data_ptr(),
                                                    work.data_ptr(), stored.data_ptr(), mismatch.data_ptr(),
                                                    count.data_ptr(), _stream(stream)),
               "mck_block_kv_verify_blocks_batch")
-        return mismatch[:prot.total_keys], count
-    mismatch = torch.empty(max(prot.total_keys, 1), dtype=torch.uint8, device=dev)
+        if not bool((status[:n] == int(BlockStatus.kSlotOverflow)).any().item()):
+            out = (mismatch[:prot.total_keys], count)
+            return out + (status[:n],) if return_status else out
+        count.zero_()  # a block outgrew its slots: the two-pass verify decides the batch
+    work = _work(prot.total_keys, prot.total_key_bytes, dev)
     check(lib.mck_block_kv_verify_batch(int(prot.kind), ctypes.byref(s), prot.protection_bytes_per_key,
                                         prot.key_base.data_ptr(), prot.arena_base.data_ptr(),
                                         prot.restart_interval.data_ptr(), prot.total_keys,
-                                        prot.work.data_ptr(), stored.data_ptr(), mismatch.data_ptr(),
+                                        work.data_ptr(), stored.data_ptr(), mismatch.data_ptr(),
                                         count.data_ptr(), _stream(stream)), "mck_block_kv_verify_batch")
-    return mismatch[:prot.total_keys], count
+    out = (mismatch[:prot.total_keys], count)
+    return out + (None,) if return_status else out
 
 
-def PerKVChecksumStatus(prot: BlockProtection, mismatch, entry_offsets: Optional[list] = None) -> list:
+def PerKVChecksumStatus(prot: BlockProtection, mismatch, entry_offsets: Optional[list] = None,
+                        status=None) -> list:
     """(block, Status) for every block holding a mismatching entry, with the
     reference's message (block.h:567-574): the first bad entry's index and,
     when ``entry_offsets`` (per block, the entries' byte offsets) is given,
-    its offset."""
+    its offset.  With ``status`` (VerifyBlockProtectionInfo's walk status), a
+    block that no longer walks reports its layout error instead ("bad entry
+    in block", block.h:559-565)."""
     torch = _torch()
     bad = torch.nonzero(mismatch).flatten().cpu().tolist()
     if not bad:
         return []
     kb = prot.key_base.cpu().tolist()
+    st = status.cpu().tolist() if status is not None else None
     out, seen = [], set()
     import bisect
     for k in bad:
@@ -225,6 +243,9 @@ def PerKVChecksumStatus(prot: BlockProtection, mismatch, entry_offsets: Optional
         if i in seen:
             continue
         seen.add(i)
+        if st is not None and st[i] not in (int(BlockStatus.kOk), int(BlockStatus.kSlotOverflow)):
+            out.append((i, Status.Corruption(_MESSAGES[BlockStatus(st[i])])))
+            continue
         e = k - kb[i]
         off = entry_offsets[i][e] if entry_offsets is not None else "?"
         out.append((i, Status.Corruption("Corrupted block entry: per key-value checksum verification failed."

@@ -599,7 +599,8 @@ class mck_wal_report(ctypes.Structure):
 
 
 class mck_wal_read_out(ctypes.Structure):
-    _fields_ = [("frags", ctypes.c_void_p), ("frag_cap", ctypes.c_uint64), ("nfrags", ctypes.c_uint64),
+    _fields_ = [("struct_size", ctypes.c_uint64),
+                ("frags", ctypes.c_void_p), ("frag_cap", ctypes.c_uint64), ("nfrags", ctypes.c_uint64),
                 ("rec_offsets", ctypes.c_void_p), ("rec_lengths", ctypes.c_void_p),
                 ("rec_file_offsets", ctypes.c_void_p), ("rec_cap", ctypes.c_uint64),
                 ("nrecords", ctypes.c_uint64), ("records_bytes", ctypes.c_uint64),
@@ -640,6 +641,7 @@ def wal_read_records(wal: bytes, log_number: int = 0,
         v = verified.cpu().numpy() if hasattr(verified, "cpu") else np.asarray(verified)
         ver = np.ascontiguousarray(v.astype(np.int32).reshape(-1, 4))
     o = mck_wal_read_out()
+    o.struct_size = ctypes.sizeof(mck_wal_read_out)
     vp = ver.ctypes.data if ver is not None else None
     check(lib.mck_wal_read_records(buf, len(buf), log_number & 0xFFFFFFFF, int(recovery_mode), vp,
                                    ctypes.addressof(o)), "mck_wal_read_records")
@@ -649,7 +651,7 @@ def wal_read_records(wal: bytes, log_number: int = 0,
     foffs = np.zeros(max(o.nrecords, 1), dtype=np.uint64)
     reps = (mck_wal_report * max(o.nreports, 1))()
     strm = (mck_wal_fragment * max(o.nstream, 1))()
-    o2 = mck_wal_read_out(ctypes.addressof(frags), o.nfrags, 0, offs.ctypes.data, lens.ctypes.data,
+    o2 = mck_wal_read_out(ctypes.sizeof(mck_wal_read_out), ctypes.addressof(frags), o.nfrags, 0, offs.ctypes.data, lens.ctypes.data,
                           foffs.ctypes.data, o.nrecords, 0, 0, ctypes.addressof(reps), o.nreports)
     o2.stream = ctypes.addressof(strm)
     o2.stream_cap = o.nstream
@@ -872,10 +874,16 @@ class FragmentBufferedReader:
 
     def ReadRecord(self) -> Optional[bytes]:
         nf, nb, lro = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        supplied = set()
         while True:
             rc = lib.mck_wal_tail_read_record(self._h, ctypes.byref(nf), ctypes.byref(nb), ctypes.byref(lro))
             if rc != MCK_EAGAIN:
                 break
+            off = ctypes.c_uint64()
+            lib.mck_wal_tail_pending_verify(self._h, ctypes.byref(off), None)
+            if off.value in supplied:  # the verdict added did not decide it: never spin
+                raise RuntimeError(f"WAL tail reader: the verdict for offset {off.value} did not resolve it")
+            supplied.add(off.value)
             self._supply_verdict()
         if rc < 0:
             check(rc, "mck_wal_tail_read_record")

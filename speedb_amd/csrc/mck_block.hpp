@@ -656,18 +656,40 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
   __shared__ uint32_t s_key[256][kBlkKeyBuf / 4 + 5];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  uint64_t k0 = 0;
+  uint64_t k0 = 0, cnt = 0, aslice = 0;
   bool active = false;
   if (b < count) {
     k0 = ldg_u64(key_base, b);
-    active = ldg_u64(key_base, b + 1) != k0;  // no keys (or a bad block): idle
+    cnt = ldg_u64(key_base, b + 1) - k0;
+    active = cnt != 0 && k0 <= K_total && cnt <= K_total - k0;  // no keys (or a bad block): idle
   }
   uint8_t* const lkey = reinterpret_cast<uint8_t*>(s_key[threadIdx.x]);
   uint8_t* const gkey = active ? arena + ldg_u64(arena_base, b) : arena;
+  if (active) aslice = ldg_u64(arena_base, b + 1) - ldg_u64(arena_base, b);
   bool global_key = false;
   const GblRd rd{active ? blocks.ptr(b) : nullptr};
-  const uint32_t n = active ? (uint32_t)blocks.len(b) : 0;  // the layout pass validated the block (< 4 GiB)
-  const uint32_t ro = active ? rd_header(rd, n).ro : 0;
+  const uint64_t n64 = active ? blocks.len(b) : 0;
+  const uint32_t n = (uint32_t)n64;
+  // Protect: the layout pass validated the block.  Verify: the block may
+  // have changed since it was protected, so the walk trusts nothing -- a bad
+  // header or entry, more or fewer entries than key_base gives the block, a
+  // shared prefix longer than the previous key or a key longer than the
+  // block's arena slice makes the block BAD: every one of its protect-time
+  // keys is flagged and nothing outside [k0, k0 + cnt) is touched (the
+  // iterator's CorruptionError, block.h:559-565).
+  bool bad = false;
+  uint32_t nbad = 0, kprev = 0;
+  uint32_t ro = 0;
+  if (active) {
+    const BlkHdr h = rd_header(rd, n64);
+    ro = h.ro;
+    if constexpr (VERIFY) {
+      if (!h.ok || h.ro == 0) {
+        bad = true;
+        active = false;
+      }
+    }
+  }
   const uint64_t oklo = sec64(16 * (int)(lane & 7)) + kSeedV, okhi = sec64(16 * (int)(lane & 7) + 8) - kSeedV;
   // 8-byte protection into an aligned array: entries are stored in pairs
   const bool p8 = !VERIFY && prot_bytes == 8 && (reinterpret_cast<uint64_t>(enc) & 7) == 0;
@@ -706,9 +728,17 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
           fast = true;
         }
       }
-      if (!fast) rd_entry<KIND>(rd, p, ro, &sh, &ns, &q, &v, &vl);
+      const bool dec = fast || rd_entry<KIND>(rd, p, ro, &sh, &ns, &q, &v, &vl);
+      if constexpr (VERIFY) {
+        if (!dec || idx >= cnt || sh > kprev ||
+            (sh + ns > kBlkKeyBuf && (uint64_t)sh + ns > aslice)) {
+          bad = true;
+          active = false;
+          sh = ns = q = v = vl = 0;
+        }
+      }
       const uint32_t pn = v + vl;
-      if (pn < ro) {
+      if (active && pn < ro) {
         uok = pn + 16 <= n;
         if (uok) U = vload16_any(reinterpret_cast<uint64_t>(rd.p + pn));
       }
@@ -797,13 +827,25 @@ __global__ __launch_bounds__(256) void k_block_kv_t(SpanSrc blocks, uint32_t cou
       } else if (!lng) {
         const uint64_t sv = blk_load_prot(stored, k, prot_bytes);
         const uint64_t keep = prot_bytes >= 8 ? ~0ull : ((1ull << (8 * prot_bytes)) - 1);
-        const bool bad = sv != (hv & keep);
-        mismatch[k] = bad;
-        if (bad && mismatch_count) atomicAdd(mismatch_count, 1u);
+        const bool miss = sv != (hv & keep);
+        mismatch[k] = miss;
+        nbad += miss;
+        if (miss && mismatch_count) atomicAdd(mismatch_count, 1u);
       }
       idx++;
+      kprev = sh + ns;
       p = v + vl;
       active = p < ro;
+    }
+  }
+  if constexpr (VERIFY) {
+    if (b < count && cnt != 0 && !bad && idx != cnt && k0 <= K_total && cnt <= K_total - k0) bad = true;
+    if (bad) {  // rare: flag the whole block, drop its long values from the sweep
+      for (uint64_t k = k0; k < k0 + cnt; k++) {
+        mismatch[k] = 1;
+        long_len[k] = 0;
+      }
+      if (mismatch_count && cnt > nbad) atomicAdd(mismatch_count, (uint32_t)(cnt - nbad));
     }
   }
   // one flag store per wave (every writer stores 1; an atomic per step on
@@ -1042,14 +1084,23 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
 template <bool VERIFY>
 __device__ __forceinline__ void blk_flush_one(SpanSrc blocks, uint32_t stride, uint32_t j, const uint64_t* slot_h,
                                               const uint64_t* slot_m, const uint32_t* blk_long,
-                                              const uint64_t* key_base, uint32_t prot_bytes, bool p8, uint8_t* enc,
+                                              const uint64_t* key_base, const uint64_t* prot_base, uint64_t kcap,
+                                              uint32_t prot_bytes, bool p8, uint8_t* enc,
                                               const uint8_t* stored, uint8_t* mismatch, uint32_t* mismatch_count,
                                               uint64_t* long_off, uint32_t* long_len, uint64_t* long_part,
                                               bool batch_long) {
   const uint32_t hs = stride >> 1;
   const uint32_t b = j / hs, i = 2 * (j - b * hs);
-  const uint64_t k0 = ldg_u64(key_base, b), cnt = ldg_u64(key_base, b + 1) - k0;
+  uint64_t k0 = ldg_u64(key_base, b);
+  const uint64_t cnt = ldg_u64(key_base, b + 1) - k0;
   if (i >= cnt) return;
+  if constexpr (VERIFY) {
+    // keys are the PROTECT-time ones (block.h:623: kv_checksum_ + n *
+    // cur_entry_idx_ within the block's own array); a block whose entry
+    // count changed is k_block_kv_verify_bad's
+    k0 = ldg_u64(prot_base, b);
+    if (ldg_u64(prot_base, b + 1) - k0 != cnt || k0 > kcap || cnt > kcap - k0) return;
+  }
   const uint64_t s0 = (uint64_t)b * stride + i;
   const bool two = i + 1 < cnt;
   uint64_t h[2];
@@ -1094,6 +1145,7 @@ template <bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_kv_flush(SpanSrc blocks, uint32_t npairs, uint32_t stride,
                                                         const uint64_t* slot_h, const uint64_t* slot_m,
                                                         const uint32_t* blk_long, const uint64_t* key_base,
+                                                        const uint64_t* prot_base, uint64_t kcap,
                                                         uint32_t prot_bytes, uint8_t* enc, const uint8_t* stored,
                                                         uint8_t* mismatch, uint32_t* mismatch_count,
                                                         uint64_t* long_off, uint32_t* long_len,
@@ -1106,9 +1158,36 @@ __global__ __launch_bounds__(256) void k_block_kv_flush(SpanSrc blocks, uint32_t
   for (uint32_t u = 0; u < 4; u++) {
     const uint64_t j = t + (uint64_t)u * g;
     if (j < npairs)
-      blk_flush_one<VERIFY>(blocks, stride, (uint32_t)j, slot_h, slot_m, blk_long, key_base, prot_bytes, p8, enc,
-                            stored, mismatch, mismatch_count, long_off, long_len, long_part, batch_long);
+      blk_flush_one<VERIFY>(blocks, stride, (uint32_t)j, slot_h, slot_m, blk_long, key_base, prot_base, kcap,
+                            prot_bytes, p8, enc, stored, mismatch, mismatch_count, long_off, long_len, long_part,
+                            batch_long);
   }
+}
+
+// One-pass verify, blocks whose walk now gives another entry count than
+// protect did (a corrupt header, entry or restart array; walk failures count
+// 0): every protect-time key of the block is flagged and leaves the long-value
+// sweep, no other block's keys move.  A block the walk could not park
+// (kBlkSlotOverflow) is not verified: its keys stay unflagged and the caller
+// re-verifies the batch with the two-pass pair (status says which).
+__global__ __launch_bounds__(256) void k_block_kv_verify_bad(uint32_t count, const uint64_t* walk_base,
+                                                             const uint64_t* prot_base, const int32_t* status,
+                                                             uint64_t kcap, uint8_t* mismatch,
+                                                             uint32_t* mismatch_count, uint32_t* long_len,
+                                                             const uint32_t* long_flag) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= count) return;
+  const uint64_t k0 = ldg_u64(prot_base, b), cp = ldg_u64(prot_base, b + 1) - k0;
+  const uint64_t cw = ldg_u64(walk_base, b + 1) - ldg_u64(walk_base, b);
+  if (cp == cw || k0 >= kcap) return;
+  const uint64_t k1 = cp > kcap - k0 ? kcap : k0 + cp;
+  const bool flag = status[b] != kBlkSlotOverflow;
+  const bool batch_long = *long_flag != 0;
+  for (uint64_t k = k0; k < k1; k++) {
+    mismatch[k] = flag;
+    if (batch_long) long_len[k] = 0;
+  }
+  if (flag && mismatch_count) atomicAdd(mismatch_count, (uint32_t)(k1 - k0));
 }
 
 __global__ __launch_bounds__(64) void k_dbg_xp(const uint8_t* d, uint32_t len, uint64_t seed, uint64_t* out) {
@@ -1173,8 +1252,9 @@ struct OpBlkLongRows {
 };
 template <bool VERIFY>
 __global__ __launch_bounds__(256) void k_block_long_rows(OpBlkLongRows<VERIFY> op, const uint64_t* key_base,
-                                                         uint32_t nblocks) {
-  const uint64_t K = ldg_u64(key_base, nblocks);  // keys of the batch (< 2^32: the host checks)
+                                                         uint32_t nblocks, uint64_t kcap) {
+  // keys of the batch (< 2^32: the host checks), never past the list's room
+  const uint64_t K = min(ldg_u64(key_base, nblocks), kcap);
   if (*op.any_long == 0) return;  // no long value in the batch
   const X3Row X = x3_row(kSeedV);
   const uint32_t wpb = blockDim.x >> 6;

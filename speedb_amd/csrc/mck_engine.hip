@@ -532,12 +532,12 @@ int blk_kv(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_
     hipLaunchKernelGGL(k_block_long_rows<true>, dim3(grid), dim3(256), 0, st,
                        OpBlkLongRows<true>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
                                            mismatch_count, w.long_len + total_keys},
-                       key_base, blocks->count);
+                       key_base, blocks->count, total_keys);
   else
     hipLaunchKernelGGL(k_block_long_rows<false>, dim3(grid), dim3(256), 0, st,
                        OpBlkLongRows<false>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
                                             mismatch_count, w.long_len + total_keys},
-                       key_base, blocks->count);
+                       key_base, blocks->count, total_keys);
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }
@@ -553,7 +553,8 @@ struct BlkWalkT {
 static_assert(kBlkSlotOverflow == MCK_BLOCK_SLOT_OVERFLOW, "status codes");
 
 // work: [scan tiles][flag u32, pad to 256][slot_h, slot_m: u64 x count x stride][long masks]
-//       [long_off u64 x K][long_part u64 x K][long_len u32 x K][arena count x arena_cap], K = count x slot_cap
+//       [long_off u64 x K][long_part u64 x K][long_len u32 x K][arena count x arena_cap]
+//       [walk key_base, walk arena_base: u64 x (count + 1) each; verify only], K = count x slot_cap
 struct BlkBlocksWork {
   uint64_t* tsum;
   uint32_t* flag;
@@ -562,6 +563,7 @@ struct BlkBlocksWork {
   uint64_t *long_off, *long_part;
   uint32_t* long_len;
   uint8_t* arena;
+  uint64_t *walk_kb, *walk_ab;
   uint64_t bytes;
 };
 BlkBlocksWork blk_blocks_work(void* work, uint32_t count, uint32_t slot_cap, uint32_t arena_cap) {
@@ -589,14 +591,22 @@ BlkBlocksWork blk_blocks_work(void* work, uint32_t count, uint32_t slot_cap, uin
   o += up(4 * K + 4);
   r.arena = w + o;
   o += up((uint64_t)count * arena_cap + 16);
+  r.walk_kb = reinterpret_cast<uint64_t*>(w + o);
+  o += up(8ull * (count + 1));
+  r.walk_ab = reinterpret_cast<uint64_t*>(w + o);
+  o += up(8ull * (count + 1));
   r.bytes = o;
   return r;
 }
 
+// Protect (prot_base == nullptr): key_base / arena_base are the caller's
+// outputs.  Verify: prot_base / total_keys are the protect-time key index
+// (what `stored` and `mismatch` are laid out by); the walk's own index goes
+// to the work area and only decides which blocks still match it.
 int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32_t slot_cap, uint32_t arena_cap,
-                  uint64_t* key_base, uint64_t* arena_base, uint32_t* restart_interval, int32_t* status, void* work,
-                  uint8_t* enc, const uint8_t* stored, uint8_t* mismatch, uint32_t* mismatch_count,
-                  hipStream_t st) {
+                  uint64_t* key_base, uint64_t* arena_base, const uint64_t* prot_base, uint64_t total_keys,
+                  uint32_t* restart_interval, int32_t* status, void* work, uint8_t* enc, const uint8_t* stored,
+                  uint8_t* mismatch, uint32_t* mismatch_count, hipStream_t st) {
   if (int rc = check_spans(blocks)) return rc;
   if (kind < MCK_BLOCK_DATA || kind > MCK_BLOCK_META) {
     set_err("unknown block kind %d", kind);
@@ -607,17 +617,20 @@ int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32
     return MCK_EINVAL;
   }
   stat_batch(blocks->count, known_bytes(blocks));
-  if (!key_base || !arena_base) {
-    set_err("key_base/arena_base is NULL");
+  const bool verify = stored != nullptr;
+  if (verify ? !prot_base : (!key_base || !arena_base)) {
+    set_err(verify ? "key_base (protect-time) is NULL" : "key_base/arena_base is NULL");
     return MCK_EINVAL;
   }
   const uint32_t n = blocks->count;
   if (!n) {
-    MCK_HIP(hipMemsetAsync(key_base, 0, 8, st));
-    MCK_HIP(hipMemsetAsync(arena_base, 0, 8, st));
+    if (!verify) {
+      MCK_HIP(hipMemsetAsync(key_base, 0, 8, st));
+      MCK_HIP(hipMemsetAsync(arena_base, 0, 8, st));
+    }
     return MCK_OK;
   }
-  if (!restart_interval || !status || !work || (!enc && !stored) || (stored && !mismatch)) {
+  if (!restart_interval || !status || !work || (!enc && !stored) || (verify && total_keys && !mismatch)) {
     set_err("restart_interval/status/work/out is NULL");
     return MCK_EINVAL;
   }
@@ -625,42 +638,52 @@ int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32
     set_err("slot_cap must be >= 1 with count * slot_cap < 2^32 (got %u x %u)", n, slot_cap);
     return MCK_EINVAL;
   }
+  const uint64_t K = (uint64_t)n * slot_cap;  // room of the long-value list
+  if (verify && total_keys > K) {
+    set_err("total_keys %llu exceeds count * slot_cap = %llu: verify this batch with "
+            "mck_block_kv_verify_batch", (unsigned long long)total_keys, (unsigned long long)K);
+    return MCK_EINVAL;
+  }
   const BlkBlocksWork w = blk_blocks_work(work, n, slot_cap, arena_cap);
+  uint64_t* const kb = verify ? w.walk_kb : key_base;
+  uint64_t* const ab = verify ? w.walk_ab : arena_base;
   MCK_HIP(hipMemsetAsync(w.flag, 0, 4, st));
   if (int rc = launch_blk<BlkWalkT>(kind, n, st, n, kBlkWalkLdsPad, to_src(blocks), n, slot_cap, w.arena, arena_cap,
-                                    w.slot_h, w.slot_m, w.blk_long, key_base, arena_base, restart_interval, status,
-                                    w.flag))
+                                    w.slot_h, w.slot_m, w.blk_long, kb, ab, restart_interval, status, w.flag))
     return rc;
   const uint32_t tiles = (uint32_t)blk_tiles(n);
-  hipLaunchKernelGGL(k_blk_scan_tiles, dim3(tiles), dim3(kBlkScanThreads), 0, st, key_base, arena_base, n, w.tsum);
-  hipLaunchKernelGGL(k_blk_scan_top, dim3(1), dim3(kBlkScanThreads), 0, st, w.tsum, tiles, key_base, arena_base, n);
-  hipLaunchKernelGGL(k_blk_scan_apply, dim3(tiles), dim3(kBlkScanThreads), 0, st, key_base, arena_base, n, w.tsum);
+  hipLaunchKernelGGL(k_blk_scan_tiles, dim3(tiles), dim3(kBlkScanThreads), 0, st, kb, ab, n, w.tsum);
+  hipLaunchKernelGGL(k_blk_scan_top, dim3(1), dim3(kBlkScanThreads), 0, st, w.tsum, tiles, kb, ab, n);
+  hipLaunchKernelGGL(k_blk_scan_apply, dim3(tiles), dim3(kBlkScanThreads), 0, st, kb, ab, n, w.tsum);
   int ncu;
   if (int rc = current_device(nullptr, &ncu)) return rc;
   const uint32_t stride = blk_slot_stride(slot_cap);
   const uint32_t npairs = n * (stride / 2);
   const uint32_t fgrid = (uint32_t)(((uint64_t)npairs + 4 * 256 - 1) / (4 * 256));  // 4 pairs per thread
-  const bool verify = stored != nullptr;
-  if (verify)
+  const uint64_t kcap = verify ? total_keys : K;
+  const uint64_t* const kidx = verify ? prot_base : kb;  // the index the outputs are laid out by
+  if (verify) {
+    hipLaunchKernelGGL(k_block_kv_verify_bad, dim3((n + 255) / 256), dim3(256), 0, st, n, kb, prot_base, status,
+                       kcap, mismatch, mismatch_count, w.long_len, w.flag);
     hipLaunchKernelGGL(k_block_kv_flush<true>, dim3(fgrid), dim3(256), 0, st, to_src(blocks), npairs, stride,
-                       w.slot_h, w.slot_m, w.blk_long, key_base, prot_bytes, enc, stored, mismatch, mismatch_count,
-                       w.long_off, w.long_len, w.long_part, w.flag);
-  else
+                       w.slot_h, w.slot_m, w.blk_long, kb, prot_base, kcap, prot_bytes, enc, stored, mismatch,
+                       mismatch_count, w.long_off, w.long_len, w.long_part, w.flag);
+  } else {
     hipLaunchKernelGGL(k_block_kv_flush<false>, dim3(fgrid), dim3(256), 0, st, to_src(blocks), npairs, stride,
-                       w.slot_h, w.slot_m, w.blk_long, key_base, prot_bytes, enc, stored, mismatch, mismatch_count,
-                       w.long_off, w.long_len, w.long_part, w.flag);
-  const uint64_t K = (uint64_t)n * slot_cap;  // bound; the sweep reads the total from key_base[n]
+                       w.slot_h, w.slot_m, w.blk_long, kb, kb, kcap, prot_bytes, enc, stored, mismatch,
+                       mismatch_count, w.long_off, w.long_len, w.long_part, w.flag);
+  }
   const uint32_t grid = (uint32_t)std::min<uint64_t>((uint64_t)ncu * 8, (K + 255) / 256);
   if (verify)
     hipLaunchKernelGGL(k_block_long_rows<true>, dim3(grid), dim3(256), 0, st,
                        OpBlkLongRows<true>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
                                            mismatch_count, w.flag},
-                       key_base, n);
+                       kidx, n, kcap);
   else
     hipLaunchKernelGGL(k_block_long_rows<false>, dim3(grid), dim3(256), 0, st,
                        OpBlkLongRows<false>{w.long_off, w.long_len, w.long_part, prot_bytes, enc, stored, mismatch,
                                             mismatch_count, w.flag},
-                       key_base, n);
+                       kidx, n, kcap);
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }
@@ -1232,12 +1255,13 @@ int mck_block_kv_protect_blocks_batch(int kind, const mck_spans* blocks, uint32_
                                       uint32_t* restart_interval, int32_t* status, void* work, uint8_t* out,
                                       mck_stream_t stream) {
   t_err[0] = 0;
-  return blk_kv_blocks(kind, blocks, prot_bytes, slot_cap, arena_cap, key_base, arena_base, restart_interval, status,
-                       work, out, nullptr, nullptr, nullptr, reinterpret_cast<hipStream_t>(stream));
+  return blk_kv_blocks(kind, blocks, prot_bytes, slot_cap, arena_cap, key_base, arena_base, nullptr, 0,
+                       restart_interval, status, work, out, nullptr, nullptr, nullptr,
+                       reinterpret_cast<hipStream_t>(stream));
 }
 
 int mck_block_kv_verify_blocks_batch(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32_t slot_cap,
-                                     uint32_t arena_cap, uint64_t* key_base, uint64_t* arena_base,
+                                     uint32_t arena_cap, const uint64_t* key_base, uint64_t total_keys,
                                      uint32_t* restart_interval, int32_t* status, void* work, const uint8_t* stored,
                                      uint8_t* mismatch, uint32_t* mismatch_count, mck_stream_t stream) {
   t_err[0] = 0;
@@ -1245,8 +1269,9 @@ int mck_block_kv_verify_blocks_batch(int kind, const mck_spans* blocks, uint32_t
     set_err("stored is NULL");
     return MCK_EINVAL;
   }
-  return blk_kv_blocks(kind, blocks, prot_bytes, slot_cap, arena_cap, key_base, arena_base, restart_interval, status,
-                       work, nullptr, stored, mismatch, mismatch_count, reinterpret_cast<hipStream_t>(stream));
+  return blk_kv_blocks(kind, blocks, prot_bytes, slot_cap, arena_cap, nullptr, nullptr, key_base, total_keys,
+                       restart_interval, status, work, nullptr, stored, mismatch, mismatch_count,
+                       reinterpret_cast<hipStream_t>(stream));
 }
 
 // Internal test hook (not part of mck.h): XXPH3 of one device span by the

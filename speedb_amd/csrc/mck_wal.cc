@@ -2,6 +2,7 @@
 // fragmentation log::Writer::AddRecord performs (db/log_writer.cc:79-175),
 // on sizes only.  The bytes are written on the device by
 // mck_wal_write_batch (mck_engine.hip).
+#include <stddef.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -260,6 +261,12 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
     mck_internal_set_error("wal / out is NULL");
     return MCK_EINVAL;
   }
+  static_assert(offsetof(mck_wal_read_out, compression_type) == MCK_WAL_READ_OUT_V1_SIZE, "v1 layout");
+  if (out->struct_size < MCK_WAL_READ_OUT_V1_SIZE) {
+    mck_internal_set_error("mck_wal_read_out.struct_size not set (sizeof(mck_wal_read_out))");
+    return MCK_EINVAL;
+  }
+  const bool has_stream = out->struct_size >= sizeof(mck_wal_read_out);
   if (recovery_mode < MCK_WAL_kTolerateCorruptedTailRecords || recovery_mode > MCK_WAL_kSkipAnyCorruptedRecords) {
     mck_internal_set_error("unknown WALRecoveryMode");
     return MCK_EINVAL;
@@ -433,6 +440,10 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
     return R.err;
   }
   scratch_clear();
+  if (compression && !has_stream) {
+    mck_internal_set_error("compressed WAL: mck_wal_read_out.struct_size has no room for the compression fields");
+    return MCK_ENOTSUP;
+  }
   out->nfrags = fr.size();
   out->nrecords = roff.size();
   out->records_bytes = dst;
@@ -461,6 +472,7 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
     const size_t n = std::min<size_t>(out->report_cap, R.reports.size());
     if (n) memcpy(out->reports, R.reports.data(), n * sizeof(mck_wal_report));
   }
+  if (!has_stream) return MCK_OK;
   out->compression_type = compression;
   out->nstream = stream.size();
   if (out->stream) {
@@ -481,6 +493,7 @@ extern "C" int mck_wal_list_records(const void* wal, uint64_t nbytes, uint32_t l
                                     uint64_t* records_bytes) {
   mck_wal_read_out o;
   memset(&o, 0, sizeof o);
+  o.struct_size = sizeof o;
   o.frags = frags;
   o.frag_cap = frag_cap;
   o.rec_offsets = rec_offsets;
@@ -846,6 +859,21 @@ extern "C" int mck_wal_tail_add_verdict(mck_wal_tail* r, uint64_t file_offset, c
   }
   if (file_offset >= r->avail) {
     mck_internal_set_error("verdict offset past the image");
+    return MCK_EINVAL;
+  }
+  // only the verdict mck_wal_tail_pending_verify asked for, and only one that
+  // decides the pending record (its CRC holds past it, or fails AT it): any
+  // other would leave the reader asking for the same verdict forever
+  char msg[160];
+  if (r->need_from == ~0ull || file_offset != r->need_from) {
+    snprintf(msg, sizeof msg, "no verdict pending at offset %llu", (unsigned long long)file_offset);
+    mck_internal_set_error(msg);
+    return MCK_EINVAL;
+  }
+  if (res->stop_offset == 0 && res->status != MCK_WAL_BAD_CHECKSUM) {
+    snprintf(msg, sizeof msg, "verdict at %llu makes no progress (stop_offset 0, status %d)",
+             (unsigned long long)file_offset, (int)res->status);
+    mck_internal_set_error(msg);
     return MCK_EINVAL;
   }
   r->sub.push_back(mck_wal_tail::SubVerdict{file_offset, *res});

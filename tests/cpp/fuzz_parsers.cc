@@ -73,6 +73,7 @@ static void run_wal(const uint8_t* d, uint64_t n) {
       for (uint32_t ln : {0u, 123u}) {
         mck_wal_read_out o;
         memset(&o, 0, sizeof o);
+        o.struct_size = sizeof o;
         if (mck_wal_read_records(d, n, ln, mode, v ? ok.data() : nullptr, &o) != MCK_OK) continue;
         std::vector<mck_wal_fragment> fr(o.nfrags ? o.nfrags : 1);
         std::vector<uint64_t> ro(o.nrecords ? o.nrecords : 1), rf(ro.size());

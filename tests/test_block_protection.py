@@ -430,6 +430,125 @@ def test_block_protection_one_pass_equals_two_pass_many(gpu):
         assert torch.nonzero(mism).flatten().cpu().tolist() == bad
 
 
+def _corrupt_cases(rnd, blocks):
+    """Block-data corruptions: (block index, new bytes, whole)
+    -- whole: the block no longer walks to its protect-time entry count, so
+    every one of its keys must be flagged."""
+    out = []
+    mid, last = len(blocks) // 2, len(blocks) - 1
+    # num_restarts far past the block: the constructor's error marker
+    b = bytearray(blocks[mid])
+    b[-4:] = struct.pack("<I", 0x7000)
+    out.append((mid, bytes(b), True))
+    # shared != 0 at the first entry (a restart point)
+    b = bytearray(blocks[last])
+    b[0] = 3
+    out.append((last, bytes(b), True))
+    # a restart offset moved into the middle of an entry (one-pass walk:
+    # bad restarts; either way the key count or layout changes)
+    b = bytearray(blocks[mid + 1])
+    nr = struct.unpack("<I", b[-4:])[0]
+    if nr > 1:
+        ro = len(b) - 4 * (nr + 1)
+        r1 = struct.unpack("<I", b[ro + 4:ro + 8])[0]
+        b[ro + 4:ro + 8] = struct.pack("<I", r1 + 1)
+        out.append((mid + 1, bytes(b), None))
+    # a value byte of entry 0 (blocks[3] is built with restart interval 1
+    # and one-byte varints: its value starts at 3 + key length): only that
+    # entry's checksum changes
+    b = bytearray(blocks[3])
+    b[3 + b[1]] ^= 0x40
+    out.append((3, bytes(b), False))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [2, 8])
+def test_block_protection_verify_corrupt_block_data(gpu, p):
+    """Verify after the BLOCK DATA changed (not only the stored bytes): a
+    corrupt header, a bad first entry or a moved restart point in a middle
+    block and in the last block.  Both verify entry points index `stored` by
+    the protect-time key_base (block.h:623); a block that no longer walks to
+    its protect-time entry count has all of its keys flagged, and no key of
+    another block is -- the one-pass walk used to re-derive key_base and shift
+    every later block (and read `stored` past its end).  The C calls run with
+    4 KiB guard bands around `stored` and `mismatch`."""
+    import ctypes
+    import speedb_amd
+    from speedb_amd import block as B
+    from speedb_amd._lib import lib
+    torch = gpu
+    rnd = random.Random(91 + p)
+    blocks = []
+    for i in range(200):
+        n = rnd.randrange(8, 40)
+        ri = rnd.choice((2, 4, 16))
+        e = data_block(rnd, n, ri, 200, 700) if i % 9 == 4 else data_block(rnd, n, ri, 0, 120)
+        blocks.append(build_block(e, ri))
+    blocks[3] = build_block(data_block(rnd, 10, 1, 5, 100), 1)
+    for idx, nb, whole in _corrupt_cases(rnd, blocks):
+        good_base, offs, lens = _pack(torch, blocks, random.Random(1))
+        spans = speedb_amd.Spans(good_base, len(blocks), offs, lens)
+        for one_pass in (True, False):
+            prot = B.InitializeBlockProtectionInfo(DATA, spans, p, one_pass=one_pass)
+            assert prot.status.cpu().tolist() == [OK] * len(blocks)
+            kb = prot.key_base.cpu().tolist()
+            bad_blocks = list(blocks)
+            bad_blocks[idx] = nb
+            base2, offs2, lens2 = _pack(torch, bad_blocks, random.Random(1))
+            assert torch.equal(offs2, offs) and torch.equal(lens2, lens)
+            spans2 = speedb_amd.Spans(base2, len(blocks), offs2, lens2)
+            mism, cnt, st = B.VerifyBlockProtectionInfo(spans2, prot, return_status=True)
+            flagged = torch.nonzero(mism).flatten().cpu().tolist()
+            own = list(range(kb[idx], kb[idx + 1]))
+            assert set(flagged) <= set(own), (idx, one_pass)
+            assert int(cnt.item()) == len(flagged)
+            w = whole
+            if w is None:  # a moved restart point: the sequential two-pass walk never reads it
+                w = True if one_pass else None
+            if w is not None:
+                assert flagged
+            if w is True:
+                assert flagged == own
+            elif w is False:
+                assert flagged == [kb[idx]]
+            if one_pass and w:
+                assert st is not None and int(st[idx].item()) != OK
+                msgs = B.PerKVChecksumStatus(prot, mism, status=st)
+                assert [m[0] for m in msgs] == [idx] and "per key-value" not in msgs[0][1].message
+            # the C entry points with guard bands around stored / mismatch
+            G = 4096
+            K = prot.total_keys
+            sbuf = torch.full((G + K * p + G,), 0xA5, dtype=torch.uint8, device="cuda")
+            sbuf[G:G + K * p] = prot.kv_checksum
+            mbuf = torch.full((G + K + G,), 0x5A, dtype=torch.uint8, device="cuda")
+            c32 = torch.zeros(1, dtype=torch.int32, device="cuda")
+            s = spans2.c()
+            if one_pass:
+                n = len(blocks)
+                status = torch.empty(n, dtype=torch.int32, device="cuda")
+                ri = torch.empty(n, dtype=torch.int32, device="cuda")
+                work = torch.empty(int(lib.mck_block_kv_blocks_work_bytes(n, prot.slot_cap, prot.arena_cap)),
+                                   dtype=torch.uint8, device="cuda")
+                rc = lib.mck_block_kv_verify_blocks_batch(
+                    DATA, ctypes.byref(s), p, prot.slot_cap, prot.arena_cap, prot.key_base.data_ptr(), K,
+                    ri.data_ptr(), status.data_ptr(), work.data_ptr(), sbuf[G:].data_ptr(), mbuf[G:].data_ptr(),
+                    c32.data_ptr(), None)
+            else:
+                work = torch.empty(int(lib.mck_block_kv_work_bytes(K, prot.total_key_bytes)), dtype=torch.uint8,
+                                   device="cuda")
+                rc = lib.mck_block_kv_verify_batch(
+                    DATA, ctypes.byref(s), p, prot.key_base.data_ptr(), prot.arena_base.data_ptr(),
+                    prot.restart_interval.data_ptr(), K, work.data_ptr(), sbuf[G:].data_ptr(),
+                    mbuf[G:].data_ptr(), c32.data_ptr(), None)
+            assert rc == 0
+            torch.cuda.synchronize()
+            assert bool((sbuf[:G] == 0xA5).all()) and bool((sbuf[G + K * p:] == 0xA5).all())
+            assert bool((mbuf[:G] == 0x5A).all()) and bool((mbuf[G + K:] == 0x5A).all())
+            assert torch.nonzero(mbuf[G:G + K]).flatten().cpu().tolist() == flagged
+            assert int(c32.item()) == len(flagged)
+
+
 @pytest.mark.gpu
 def test_block_protection_empty_and_all_bad(gpu):
     import speedb_amd
@@ -458,7 +577,7 @@ def test_block_protection_abi_errors():
                                                  None, None) == -1
     assert lib.mck_block_kv_protect_blocks_batch(9, ctypes.byref(s), 8, 64, 0, None, None, None, None, None,
                                                  None, None) == -1
-    assert lib.mck_block_kv_verify_blocks_batch(0, ctypes.byref(s), 8, 64, 0, None, None, None, None, None,
+    assert lib.mck_block_kv_verify_blocks_batch(0, ctypes.byref(s), 8, 64, 0, None, 0, None, None, None,
                                                 None, None, None, None) == -1
     assert lib.mck_block_kv_blocks_work_bytes(10, 64, 32) >= 10 * 64 * 36 + 10 * 32
 

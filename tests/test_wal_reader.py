@@ -591,6 +591,42 @@ def test_compressed_wal_walk(oracle, recycle):
     _stream_ok(plan, img)
 
 
+def test_read_out_struct_size(oracle):
+    """mck_wal_read_out carries its caller's struct_size: 0 is
+    refused, and a caller built against the layout without the compression
+    fields gets MCK_ENOTSUP for a compressed WAL, with nothing written past
+    its struct; an uncompressed WAL reads the same with either size."""
+    import ctypes
+    from speedb_amd import checksum as C
+    from speedb_amd._lib import lib
+    L = _compressed_log(oracle, False)
+    for c in (b"foo", b"bar" * 100):
+        L.write(c)
+    img = bytes(L.w.buf)
+
+    class Guarded(ctypes.Structure):
+        _fields_ = [("o", C.mck_wal_read_out), ("guard", ctypes.c_uint64 * 8)]
+
+    g = Guarded()
+    assert lib.mck_wal_read_records(img, len(img), LOG, kTolerate, None, ctypes.addressof(g.o)) == -1
+    g.o.struct_size = 120  # MCK_WAL_READ_OUT_V1_SIZE
+    # the v1 struct ends at compression_type: fill everything past it
+    ctypes.memset(ctypes.addressof(g) + 120, 0xCD, ctypes.sizeof(g) - 120)
+    rc = lib.mck_wal_read_records(img, len(img), LOG, kTolerate, None, ctypes.addressof(g.o))
+    assert rc == -6 and "compression" in lib.mck_last_error().decode()  # MCK_ENOTSUP
+    assert bytes((ctypes.c_uint8 * (ctypes.sizeof(g) - 120)).from_address(ctypes.addressof(g) + 120)) == \
+        b"\xcd" * (ctypes.sizeof(g) - 120)
+    w = WalWriter(oracle, LOG)
+    for c in (b"foo", b"bar" * 100):
+        w.add_record(c)
+    plain = bytes(w.buf)
+    for size in (120, ctypes.sizeof(C.mck_wal_read_out)):
+        o = C.mck_wal_read_out()
+        o.struct_size = size
+        assert lib.mck_wal_read_records(plain, len(plain), LOG, kTolerate, None, ctypes.addressof(o)) == 0
+        assert o.nrecords == 2
+
+
 def test_compressed_wal_corruption_and_drops(oracle):
     """A chunk whose CRC fails is dropped BEFORE the uncompressor (not in the
     stream); a first fragment whose record never completes WAS fed (in the
