@@ -868,6 +868,13 @@ int mck_get_perf_level(void);
  * batches); reset != 0 zeroes it (PerfContext::Reset). */
 int mck_perf_context_get(mck_perf_context* out, int reset);
 
+/* Test hook: k > 0 makes mck_host_batch_checksum see k "devices" that are all
+ * device 0, each with its own staging, streams and host thread, so the
+ * ndev > 1 branch (per-device threads, concurrent first use, result
+ * concatenation) runs on a one-GPU box; 0 restores the real devices.  Frees
+ * the cached host pipelines.  Never used by production code. */
+int mck_test_set_virtual_devices(int k);
+
 /* TEST HOOK (parity tests only; never needed in production): a ragged CRC
  * batch runs each workgroup's share on the row drivers or the body/head
  * driver, chosen from a sample of its lengths, so a mixed parity batch may

@@ -1,0 +1,40 @@
+#!/bin/bash
+# round 5 (copy of r4_ab.sh): parity of the ragged CRC paths, then a same-box A/B of chosen
+# workloads against the round-3 library.
+#   $1 = output tag; AB_WL = workloads (names below); AB_TESTS = test files
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+O=gpurun_out/${1:-r4ab}
+mkdir -p $O
+export PYTHONUNBUFFERED=1 TMPDIR=/tmp
+T="timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread"
+$T ${AB_TESTS:-tests/test_crc_long.py tests/test_crc_rows.py tests/test_sst_file.py tests/test_blob_file.py} > $O/tests.log 2>&1 || { tail -60 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+declare -A ARGS=(
+  [u4300]="--workload crc32c --block-bytes 4300 --blocks 1000000"
+  [r4100]="--workload ragged --span-min 4100 --span-max 4400 --span-bytes $((4 << 30))"
+  [r4096]="--workload ragged --span-min 4096 --span-max 4096 --span-bytes $((4 << 30))"
+  [r16k]="--workload ragged --span-min 16384 --span-max 65536 --span-bytes $((4 << 30))"
+  [sstc]="--workload sst --sst-types crc32c"
+  [sstx]="--workload sst --sst-types xxh3"
+  [sst]="--workload sst"
+  [sst2]="--workload sst --sst-streams 2"
+  [r300]="--workload ragged --span-min 300 --span-max 700"
+  [blob]="--workload blob"
+  [walrec]="--workload walrec"
+  [r100]="--workload ragged --span-min 100 --span-max 300"
+  [r512]="--workload ragged --span-min 512 --span-max 512"
+  [kv100]="--workload blockkv --kv-value-bytes 100"
+  [kv1000]="--workload blockkv --kv-value-bytes 1000"
+  [walwrite]="--workload walwrite"
+  [wal]="--workload wal"
+)
+B="timeout -k 10 180 python -u bench.py --cpu-seconds 0 --steps 20 --warmup 20"
+V=$PWD/microbench/_variants
+for v in ${AB_VARIANTS:-r3base new}; do
+  for wl in ${AB_WL:-r4100 r16k sstc blob}; do
+    if [ $v = new ]; then env -u SPEEDB_AMD_LIB $B ${ARGS[$wl]} > $O/${wl}_$v.json || exit 1
+    else env SPEEDB_AMD_AB=1 SPEEDB_AMD_LIB=$V/$v.so $B ${ARGS[$wl]} > $O/${wl}_$v.json || exit 1; fi
+  done
+done
+for f in $O/*.json; do echo "$f $(python3 -c "import json,sys; d=json.load(open('$f')); print(d['value'], d['roofline']['frac'], d['roofline'].get('kernel_avg_ms'), d.get('verified'))")"; done

@@ -79,62 +79,85 @@ __device__ __forceinline__ uint32_t lds_ticket(P ctr) {
 }
 
 // Byte-balanced contiguous shares of a ragged batch [first, first + count)
-// over the grid.  Workgroup b's boundary is the first span whose offset
-// reaches b/G of the batch's offset range, searched over S = min(count, 8192)
-// evenly spaced samples of the offsets (span k * count / S, one load per
-// thread per 1024 samples); "the first sample at or past a target" is
-// monotone in the target for ANY offsets, so the shares always partition the
-// batch, and they are balanced to ~count/S spans when the offsets grow with
-// the bytes (an SST or blob file image).  Each boundary is clamped to within
-// `slack` spans of the count-balanced one (the row drivers' descriptor cache
-// bounds a share's spans).  Count-balanced shares hand the SST verify mix's
-// workgroups up to 1.2x the mean bytes (their end times spread 165-209 us
-// over a 1 GiB image).  scratch: 2 x u32 in LDS.  Workgroup-uniform; has
-// barriers.
-template <class F>
-__device__ __forceinline__ uint32_t k_or_count(uint32_t k, uint32_t S, uint32_t count, const F& idx) {
-  return k >= S ? count : idx(k);
-}
+// over the grid.  Workgroup b's boundary j (j = b for its first span, b + 1
+// for its end) is the first span whose offset reaches o0 + range * j / G
+// (o0, o0 + range: the first and last span's offsets), found by a sampled
+// search: each level samples the current index range at 512 evenly spaced
+// points (one load per thread, half the workgroup per boundary), the first
+// sample at or past the target narrows the range to the gap before it, and a
+// range of <= 512 spans is scanned whole -- two levels (two load round
+// trips) up to 262,144 spans, three up to 2^27.  "The first sample at or past
+// a target" is monotone in the target for ANY offsets, level by level, so the
+// shares always partition the batch; they are exact byte balance when the
+// offsets grow with the bytes (an SST or blob file image).  Each boundary is
+// clamped to within `slack` spans of the count-balanced one.  (Round 4 took
+// 8192 samples per workgroup, eight dependent loads per thread: 13.5 us
+// before the first unit of a 1 GiB SST image, round-5 stamps; count-balanced
+// CRC shares of that image hold 3.0-4.9 MiB and their end times track the
+// bytes, correlation 0.98.)  scratch: 12 x u32 in LDS.  Workgroup-uniform;
+// has barriers; blockDim.x = 1024.
 template <class Op, class P>
 __device__ __forceinline__ void share_by_bytes(const Op& op, uint32_t first, uint32_t count, uint32_t slack,
                                                P scratch, uint32_t* lo, uint32_t* hi) {
   const uint32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t clo = (uint32_t)((uint64_t)count * b / G), chi = (uint32_t)((uint64_t)count * (b + 1) / G);
-  constexpr uint32_t kS = 8192;  // 2^13
-  const uint32_t S = count < kS ? count : kS;
-  if (S == 0 || G == 1) {
+  if (count <= 1 || G == 1) {
     *lo = clo;
     *hi = chi;
     return;
   }
-  if (threadIdx.x < 2) scratch[threadIdx.x] = S;
-  __syncthreads();
+  constexpr uint32_t kS = 512;  // samples per boundary and level
+  uint32_t nlev = 1;
+  for (uint32_t c = count; c > kS; c = c / kS + 1) nlev++;
+  const uint32_t tgt = threadIdx.x >= kS ? 1u : 0u, t = threadIdx.x & (kS - 1);
+  if (threadIdx.x < 2 * nlev) scratch[threadIdx.x] = 0xFFFFFFFFu;
   const uint64_t o0 = op.off(first), oL = op.off(first + count - 1);
   const uint64_t range = oL > o0 ? oL - o0 : 0;
-  const uint64_t tb = o0 + range * b / G, te = o0 + range * (b + 1) / G;
-  uint32_t kb = S, ke = S;
-  // sample k is span k * count / S: k itself when S = count, else (S = 2^13)
-  // a shift (no 64-bit division per sample)
-  for (uint32_t k = threadIdx.x; k < S; k += blockDim.x) {
-    const uint32_t i = S == count ? k : (uint32_t)(((uint64_t)k * count) >> 13);
-    const uint64_t o = op.off(first + i);
-    kb = (o >= tb && k < kb) ? k : kb;
-    ke = (o >= te && k < ke) ? k : ke;
-  }
-  if (kb < S) __hip_atomic_fetch_min(&scratch[0], kb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (ke < S) __hip_atomic_fetch_min(&scratch[1], ke, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  const uint32_t j = b + tgt;
+  // o0 + range * j / G without a 128-bit product
+  const uint64_t T = o0 + (range / G) * j + (range % G) * j / G;
+  uint32_t L = 0, R = count, res = j == 0 ? 0u : count;
+  bool done = j == 0 || j == G;
   __syncthreads();
-  kb = scratch[0];
-  ke = scratch[1];
+  for (uint32_t lev = 0; lev < nlev; lev++) {
+    const uint32_t n = R - L;
+    const bool whole = n <= kS;
+    const uint32_t p = whole ? L + t : L + (uint32_t)((uint64_t)n * t / kS);
+    const bool flag = !done && (!whole || t < n) && op.off(first + p) >= T;
+    const uint64_t m = __ballot(flag);
+    if ((threadIdx.x & 63) == 0 && m)
+      __hip_atomic_fetch_min(&scratch[2 * lev + tgt], (t & ~63u) + (uint32_t)__builtin_ctzll(m), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+    if (done) continue;
+    const uint32_t tf = scratch[2 * lev + tgt];  // first sample at or past T (~0: none)
+    if (whole) {
+      res = tf < n ? L + tf : R;
+      done = true;
+    } else if (tf == 0) {
+      res = L;
+      done = true;
+    } else {
+      const uint32_t tl = tf > kS ? kS : tf;  // none: the gap after the last sample
+      const uint32_t nL = L + (uint32_t)((uint64_t)n * (tl - 1) / kS) + 1;
+      const uint32_t nR = tf > kS ? R : L + (uint32_t)((uint64_t)n * tf / kS);
+      L = nL;
+      R = nR;
+      if (L >= R) {
+        res = R;
+        done = true;
+      }
+    }
+  }
+  const uint32_t cc = tgt ? chi : clo;
+  const uint32_t a = cc > slack ? cc - slack : 0u;
+  const uint64_t z = (uint64_t)cc + slack < count ? (uint64_t)cc + slack : count;
+  res = res < a ? a : res > z ? (uint32_t)z : res;
+  if (t == 0) scratch[2 * nlev + tgt] = res;
+  __syncthreads();
+  *lo = scratch[2 * nlev];
+  *hi = scratch[2 * nlev + 1];
   __syncthreads();  // the scratch may be reused
-  const auto clampb = [&](uint32_t x, uint32_t c) {
-    const uint32_t a = c > slack ? c - slack : 0u;
-    const uint64_t z = (uint64_t)c + slack < count ? (uint64_t)c + slack : count;
-    return x < a ? a : x > z ? (uint32_t)z : x;
-  };
-  const auto idx = [&](uint32_t k) { return S == count ? k : (uint32_t)(((uint64_t)k * count) >> 13); };
-  *lo = b == 0 ? 0u : clampb(k_or_count(kb, S, count, idx), clo);
-  *hi = b + 1 == G ? count : clampb(k_or_count(ke, S, count, idx), chi);
 }
 
 }  // namespace mck

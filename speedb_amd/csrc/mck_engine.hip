@@ -1412,7 +1412,9 @@ static int host_pipe_reserve(HostPipe& p, size_t cap, uint32_t max_spans) {
 // stream, so the H2D copy of one chunk overlaps the kernel of the previous
 // one; results come back D2H into pinned memory and are copied out when the
 // slot is reused.  Every exit path leaves no copy in flight.
-static int run_device_share(int dev, const HostJob& J, uint32_t lo, uint32_t hi) {
+// `pipe` picks the staging (g_host[pipe]); it is the device itself, except
+// under mck_test_set_virtual_devices, where pipes 0..k-1 all run on device 0.
+static int run_device_share(int dev, int pipe, const HostJob& J, uint32_t lo, uint32_t hi) {
   NoStat nostat;
   MCK_HIP(hipSetDevice(dev));
   if (lo >= hi) return MCK_OK;
@@ -1422,7 +1424,7 @@ static int run_device_share(int dev, const HostJob& J, uint32_t lo, uint32_t hi)
   size_t cap = J.chunk_bytes;
   for (uint32_t i = lo; i < hi; i++) cap = std::max<size_t>(cap, (size_t)J.len(i) + 32);
   const uint32_t max_spans = (uint32_t)std::min<uint64_t>(hi - lo, 1u << 20);
-  HostPipe& P = g_host[dev];
+  HostPipe& P = g_host[pipe];
   std::lock_guard<std::mutex> lock(P.mu);
   if ((rc = host_pipe_reserve(P, cap, max_spans))) return rc;
   const size_t res_sz = J.kind == MCK_kXXH3 ? 8 : 4;
@@ -1493,6 +1495,11 @@ static int run_device_share(int dev, const HostJob& J, uint32_t lo, uint32_t hi)
   return MCK_OK;
 }
 
+// Test hook (mck_test_set_virtual_devices): k > 0 makes mck_host_batch_checksum
+// see k devices, all of them device 0, each with its own staging, streams and
+// host thread -- the ndev > 1 branch on a one-GPU box.
+std::atomic<int> g_virtual_devs{0};
+
 }  // namespace
 
 int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* host_offsets,
@@ -1514,6 +1521,8 @@ int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* hos
     set_err("no HIP device");
     return MCK_ENODEV;
   }
+  const int virt = g_virtual_devs.load(std::memory_order_relaxed);
+  if (virt > 0) have = virt;
   int prev = 0;
   (void)hipGetDevice(&prev);
   // ndev <= 0: only the calling thread's current device (one process per
@@ -1544,14 +1553,17 @@ int mck_host_batch_checksum(int kind, const void* host_base, const uint64_t* hos
             flags & MCK_F_MASK, chunk_bytes, out32, out64};
   std::vector<int> rcs(ndev, 0);
   std::vector<std::string> errs(ndev);
+  // (virtual devices: pipe d on device 0; ndev <= 0 keeps the caller's device)
+  const auto phys = [&](int d) { return virt > 0 && ndev > 1 ? 0 : devs[d]; };
+  const auto pipe = [&](int d) { return virt > 0 && ndev > 1 ? d : devs[d]; };
   if (ndev == 1) {
-    rcs[0] = run_device_share(devs[0], J, first[0], first[1]);
+    rcs[0] = run_device_share(phys(0), pipe(0), J, first[0], first[1]);
     if (rcs[0]) errs[0] = t_err;
   } else {
     std::vector<std::thread> th;
     for (int d = 0; d < ndev; d++)
       th.emplace_back([&, d] {
-        rcs[d] = run_device_share(devs[d], J, first[d], first[d + 1]);
+        rcs[d] = run_device_share(phys(d), pipe(d), J, first[d], first[d + 1]);
         if (rcs[d]) errs[d] = t_err;
       });
     for (auto& t : th) t.join();
@@ -1659,14 +1671,28 @@ int mck_test_set_crc_driver(int driver, int interleaved) {
 void mck_host_pipeline_release(void) {
   int prev = 0;
   (void)hipGetDevice(&prev);
+  const bool virt = g_virtual_devs.load(std::memory_order_relaxed) > 0;
   for (int d = 0; d < kMaxDev; d++) {
     HostPipe& P = g_host[d];
     std::lock_guard<std::mutex> lock(P.mu);
     if (!P.slot[0].st && !P.cap) continue;
-    if (hipSetDevice(d) != hipSuccess) continue;
+    // (pipes of virtual devices live on device 0)
+    if (hipSetDevice(virt ? 0 : d) != hipSuccess) continue;
     host_pipe_free(P);
   }
   (void)hipSetDevice(prev);
+}
+
+int mck_test_set_virtual_devices(int k) {
+  t_err[0] = 0;
+  if (k < 0 || k > kMaxDev) {
+    set_err("virtual devices must be 0..%d", kMaxDev);
+    return MCK_EINVAL;
+  }
+  // pipes built for real devices must not be reused under the other mapping
+  mck_host_pipeline_release();
+  g_virtual_devs.store(k, std::memory_order_relaxed);
+  return MCK_OK;
 }
 
 }  // extern "C"

@@ -201,6 +201,7 @@ struct OpCrcWal {
 // stored LE32 follows it
 template <int MODE>
 struct OpCrcBlock {
+  static constexpr bool kByteShares = true;  // blocks of a file image, in file order
   BlockArgs a;
   typedef BlockPre Pre;
   __device__ const uint8_t* base() const { return a.s.base; }
@@ -277,11 +278,28 @@ __device__ __forceinline__ void crc_small_share(const Op& op, const RowShare& sh
 // every share, 2/3/5/6 = that row width for every share, 8 = row drivers,
 // width by length (the interleaved test order), 9 = a wave per span wherever
 // crc_share_small allows it (SMALL instances).
+// Ops over the spans of one file image in file order (SST blocks, blob
+// records) take byte-balanced shares (share_by_bytes) in large batches:
+// count-balanced shares of the SST mix differ by up to 1.6x in bytes, and the
+// launch ends with the fullest one.
+template <class Op, class = void>
+struct ByteShares : std::false_type {};
+template <class Op>
+struct ByteShares<Op, std::void_t<decltype(Op::kByteShares)>> : std::integral_constant<bool, Op::kByteShares> {};
+constexpr uint32_t kByteSharesMin = 64;  // spans per workgroup (a small batch keeps count shares: latency)
+
 template <class Op, bool T, bool BLK = true, bool SMALL = false>
 __global__ __launch_bounds__(1024) void k_crc_ragged(Op op, uint32_t first, uint32_t count, int force) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   asm volatile("" ::"v"((uint32_t)(size_t)lds));
-  const RowShare sh = row_share<BLK>(first, count);
+  RowShare sh = row_share<BLK>(first, count);
+  if constexpr (BLK && ByteShares<Op>::value) {
+    if (count >= kByteSharesMin * gridDim.x) {  // workgroup-uniform
+      uint32_t lo, hi;
+      share_by_bytes(op, first, count, count / gridDim.x, lds_p32(kBLdsWsum), &lo, &hi);
+      sh = RowShare{first + lo, 1u, hi - lo};
+    }
+  }
   if (sh.n == 0) return;  // workgroup-uniform
   if constexpr (SMALL) {
     if ((force == 0 || force == 9) && crc_share_small(op, sh)) {
@@ -1039,6 +1057,7 @@ __device__ __forceinline__ uint32_t blob_header_crc(const BlobPre& e) {
 }
 template <bool WRITE>
 struct OpBlobRecord {
+  static constexpr bool kByteShares = true;  // records in file order
   const uint8_t* file;
   const uint64_t* rec_off;   // record header offsets in the file
   const uint32_t* blob_len;  // key_size + value_size

@@ -115,3 +115,41 @@ def test_host_errors(gpu):
     assert L.mck_host_batch_checksum(4, buf, None, None, 16, 16, 4, 0, 0, 0, out, None, None) == -1  # no out64
     # empty batch: nothing to do
     assert L.mck_host_batch_checksum(1, None, None, None, 0, 0, 0, 0, 0, 0, None, None, None) == 0
+
+
+@pytest.mark.parametrize("k", [2, 4, 8])
+def test_host_virtual_devices(gpu, oracle, k):
+    """The ndev > 1 branch of mck_host_batch_checksum -- one host thread,
+    staging and stream pair per device, concurrent first use, the byte-balanced
+    device split (mck_partition_spans) and the result concatenation -- run on
+    a one-GPU box through mck_test_set_virtual_devices(k): k "devices" that
+    are all device 0.  Ragged spans (CRC32C and XXH3) and 4300-B pinned blocks
+    against the oracle; more devices than that is refused."""
+    import speedb_amd as S
+    from speedb_amd import _lib
+    torch = gpu
+    L = _lib.lib
+    assert L.mck_test_set_virtual_devices(k) == 0
+    try:
+        lens = LENS * 6
+        random.Random(10 + k).shuffle(lens)
+        host, offs = ragged(10 + k, lens)
+        buf = np.frombuffer(host, dtype=np.uint8)
+        got, _ = S.host_batch_checksum(S.ChecksumType.kCRC32c, buf, offs, lens, ndev=k, chunk_bytes=96 << 10)
+        assert got.tolist() == [oracle.Value(host[o:o + n]) for o, n in zip(offs, lens)]
+        gx, _ = S.host_batch_checksum(S.ChecksumType.kXXH3, buf, offs, lens, ndev=k, chunk_bytes=160 << 10)
+        assert gx.tolist() == [oracle.XXH3(host[o:o + n]) for o, n in zip(offs, lens)]
+        block, count = 4300, 2000
+        hb = splitmix_bytes(20 + k, block * count + 64)
+        pinned = torch.empty(len(hb), dtype=torch.uint8, pin_memory=True)
+        pinned.copy_(torch.frombuffer(bytearray(hb), dtype=torch.uint8))
+        got, _ = S.host_batch_checksum(S.ChecksumType.kCRC32c, pinned, stride=block, length=block, count=count,
+                                       ndev=k, mask=True, chunk_bytes=1 << 20)
+        assert got.tolist() == [oracle.Mask(oracle.Value(hb[i * block:(i + 1) * block])) for i in range(count)]
+        # fewer spans than devices: empty shares
+        got, _ = S.host_batch_checksum(S.ChecksumType.kCRC32c, buf, offs[:1], lens[:1], ndev=k)
+        assert got.tolist() == [oracle.Value(host[offs[0]:offs[0] + lens[0]])]
+        assert L.mck_host_batch_checksum(1, buf.ctypes.data, None, None, 16, 16, 4, 0, k + 1, 0,
+                                         (ctypes.c_uint32 * 4)(), None, None) == -3  # MCK_ENODEV
+    finally:
+        assert L.mck_test_set_virtual_devices(0) == 0
