@@ -20,12 +20,12 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "microbench", "_variants", "stamps.so")
 
 STAMP_DECL = r"""
-__device__ unsigned long long g_stamps[2][2048][6];
+__device__ unsigned long long g_stamps[3][2048][16];
 __device__ __forceinline__ void stamp(int k, int p) {
   if (threadIdx.x == 0 && blockIdx.x < 2048) g_stamps[k][blockIdx.x][p] = wall_clock64();
 }
 __device__ __forceinline__ void stamp_id(int k) {
-  if (threadIdx.x == 0 && blockIdx.x < 2048) g_stamps[k][blockIdx.x][4] = __smid();
+  if (threadIdx.x == 0 && blockIdx.x < 2048) g_stamps[k][blockIdx.x][k == 2 ? 15 : 4] = __smid();
 }
 """
 
@@ -40,10 +40,15 @@ PATCHES = [
      "    crc_bh_stage(op, sh, w1 - w0, base, kind);\n    if (wi == 0) stamp(0, 2);", 1),
     ("mck_kernels.hpp", "  xxh3_wave_driver<Op, false>(op, count, 0);",
      "  stamp(1, 0); stamp_id(1); xxh3_wave_driver<Op, false>(op, count, 0); __syncthreads(); stamp(1, 3);", 1),
-    ("mck_xxh.hpp", "  share_by_bytes(op, 0u, count, 0xFFFFFFFFu, &s.wsum[0], &lo, &hi);",
-     "  share_by_bytes(op, 0u, count, 0xFFFFFFFFu, &s.wsum[0], &lo, &hi);\n  stamp(1, 1);", 1),
+    ("mck_xxh.hpp", "  const uint32_t start = lo, stride = 1, n = hi - lo;",
+     "  stamp(1, 1);\n  const uint32_t start = lo, stride = 1, n = hi - lo;", 1),
     ("mck_xxh.hpp", "    X3FeedPieces f{&s, wn, wb, stride, 0, base};",
      "    if (w0 == 0) stamp(1, 2);\n    X3FeedPieces f{&s, wn, wb, stride, 0, base};", 1),
+    ("mck_kernels.hpp", "    crc_rows_windows<Op>(op, sh, lds, &g_crc_tables, force == 8 || force == 9 ? 0 : force);",
+     "  { stamp(2, 0); stamp_id(2); crc_rows_windows<Op>(op, sh, lds, &g_crc_tables, force == 8 || force == 9 ? 0 : force);"
+     " __syncthreads(); stamp(2, 14); }", 1),
+    ("mck_crc.hpp", "    crc_rows_loop<Op, W>(op, sh, g);\n  }",
+     "    if (wi < 13) stamp(2, 1 + wi);\n    crc_rows_loop<Op, W>(op, sh, g);\n  }", 1),
     ("mck_engine.hip", "}  // extern \"C\"",
      "int mck_dbg_stamps(void* host) {\n  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mck::g_stamps), sizeof(mck::g_stamps)) == hipSuccess ? 0 : -2;\n}\n"
      "}  // extern \"C\"", 1),
@@ -93,7 +98,7 @@ def run(gib):
         im.verify()
         e1.record()
         torch.cuda.synchronize()
-        buf = np.zeros((2, 2048, 6), dtype=np.uint64)
+        buf = np.zeros((3, 2048, 16), dtype=np.uint64)
         assert f(buf.ctypes.data) == 0
         k = 0 if t == S.ChecksumType.kCRC32c else 1
         a = buf[k].astype(np.int64)
@@ -126,8 +131,60 @@ def run(gib):
         torch.cuda.empty_cache()
 
 
+def run_rows():
+    """The row driver on the WAL-record shape (bench.py --workload walrec):
+    per-workgroup window starts."""
+    os.environ["SPEEDB_AMD_AB"] = "1"
+    os.environ["SPEEDB_AMD_LIB"] = OUT
+    sys.path.insert(0, REPO)
+    import ctypes
+    import numpy as np
+    import torch
+    import speedb_amd as S
+    from speedb_amd import _lib
+    from speedb_amd import workloads as W
+    dev = torch.device("cuda", 0)
+    f = _lib.lib.mck_dbg_stamps
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_void_p]
+    rng = np.random.default_rng(800)
+    n = int((1 << 30) // 600)
+    lens = rng.integers(100, 1101, size=n).astype(np.int64)
+    step = lens + 7 + rng.integers(0, 8, size=n)
+    offs = np.zeros(n, dtype=np.int64)
+    offs[1:] = np.cumsum(step)[:-1]
+    data = W.rand_bytes(int(offs[-1] + lens[-1]) + 64, dev, 801)
+    sp = S.Spans(data, n, offsets=torch.from_numpy(offs).to(dev), lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
+    types = torch.from_numpy(rng.choice([1, 2, 3, 4], size=n).astype(np.uint8)).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    for _ in range(40):
+        S.wal_record_crc_batch(sp, types, 7, out=out)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    S.wal_record_crc_batch(sp, types, 7, out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    buf = np.zeros((3, 2048, 16), dtype=np.uint64)
+    assert f(buf.ctypes.data) == 0
+    a = buf[2].astype(np.int64)
+    a = a[a[:, 14] > 0]
+    t0 = a[:, 0].min()
+    pct = lambda x: " ".join(f"{np.percentile(x, q):7.1f}" for q in (0, 10, 50, 90, 100))
+    print(f"== walrec rows: {len(a)} workgroups, {n} spans, event {e0.elapsed_time(e1) * 1e3:.1f} us")
+    print(f"  entry        : {pct((a[:, 0] - t0) / 100)}")
+    for w in range(13):
+        col = a[:, 1 + w]
+        if (col > 0).sum() < len(a) // 2:
+            break
+        print(f"  window {w:2d} go: {pct((col[col > 0] - t0) / 100)}")
+    print(f"  end          : {pct((a[:, 14] - t0) / 100)}")
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "build":
         build()
+    elif sys.argv[1] == "rows":
+        run_rows()
     else:
         run(float(sys.argv[2]) if len(sys.argv) > 2 else 1.0)

@@ -96,9 +96,13 @@ __device__ __forceinline__ uint32_t lds_ticket(P ctr) {
 // CRC shares of that image hold 3.0-4.9 MiB and their end times track the
 // bytes, correlation 0.98.)  scratch: 12 x u32 in LDS.  Workgroup-uniform;
 // has barriers; blockDim.x = 1024.
-template <class Op, class P>
+// prefetch(i): a load of span i's descriptors whose value is discarded --
+// issued for the count-balanced share's first spans with the first level's
+// samples, so the window staging that follows finds them in the cache (the
+// SST images' staging waited 6-9 us on them, round-5 stamps).
+template <class Op, class P, class F>
 __device__ __forceinline__ void share_by_bytes(const Op& op, uint32_t first, uint32_t count, uint32_t slack,
-                                               P scratch, uint32_t* lo, uint32_t* hi) {
+                                               P scratch, uint32_t* lo, uint32_t* hi, const F& prefetch) {
   const uint32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t clo = (uint32_t)((uint64_t)count * b / G), chi = (uint32_t)((uint64_t)count * (b + 1) / G);
   if (count <= 1 || G == 1) {
@@ -111,19 +115,26 @@ __device__ __forceinline__ void share_by_bytes(const Op& op, uint32_t first, uin
   for (uint32_t c = count; c > kS; c = c / kS + 1) nlev++;
   const uint32_t tgt = threadIdx.x >= kS ? 1u : 0u, t = threadIdx.x & (kS - 1);
   if (threadIdx.x < 2 * nlev) scratch[threadIdx.x] = 0xFFFFFFFFu;
+  // (a barrier waits for every load in flight: the scratch is set up before
+  // the first loads, so the range ends, the first level's samples -- their
+  // positions do not depend on the target -- and the prefetch share one
+  // round trip)
+  __syncthreads();
   const uint64_t o0 = op.off(first), oL = op.off(first + count - 1);
+  const uint32_t p0 = count > kS ? (uint32_t)((uint64_t)count * t / kS) : t;  // level 0's sample
+  const uint64_t s0 = count > kS || t < count ? op.off(first + p0) : 0ull;
+  const uint32_t pf = clo + threadIdx.x < count ? prefetch(first + clo + threadIdx.x) : 0u;
   const uint64_t range = oL > o0 ? oL - o0 : 0;
   const uint32_t j = b + tgt;
   // o0 + range * j / G without a 128-bit product
   const uint64_t T = o0 + (range / G) * j + (range % G) * j / G;
   uint32_t L = 0, R = count, res = j == 0 ? 0u : count;
   bool done = j == 0 || j == G;
-  __syncthreads();
   for (uint32_t lev = 0; lev < nlev; lev++) {
     const uint32_t n = R - L;
     const bool whole = n <= kS;
     const uint32_t p = whole ? L + t : L + (uint32_t)((uint64_t)n * t / kS);
-    const bool flag = !done && (!whole || t < n) && op.off(first + p) >= T;
+    const bool flag = !done && (!whole || t < n) && (lev == 0 ? s0 : op.off(first + p)) >= T;
     const uint64_t m = __ballot(flag);
     if ((threadIdx.x & 63) == 0 && m)
       __hip_atomic_fetch_min(&scratch[2 * lev + tgt], (t & ~63u) + (uint32_t)__builtin_ctzll(m), __ATOMIC_RELAXED,
@@ -154,6 +165,7 @@ __device__ __forceinline__ void share_by_bytes(const Op& op, uint32_t first, uin
   const uint64_t z = (uint64_t)cc + slack < count ? (uint64_t)cc + slack : count;
   res = res < a ? a : res > z ? (uint32_t)z : res;
   if (t == 0) scratch[2 * nlev + tgt] = res;
+  asm volatile("" ::"v"(pf));  // (the prefetch's value, never used)
   __syncthreads();
   *lo = scratch[2 * nlev];
   *hi = scratch[2 * nlev + 1];

@@ -296,7 +296,8 @@ __global__ __launch_bounds__(1024) void k_crc_ragged(Op op, uint32_t first, uint
   if constexpr (BLK && ByteShares<Op>::value) {
     if (count >= kByteSharesMin * gridDim.x) {  // workgroup-uniform
       uint32_t lo, hi;
-      share_by_bytes(op, first, count, count / gridDim.x, lds_p32(kBLdsWsum), &lo, &hi);
+      share_by_bytes(op, first, count, count / gridDim.x, lds_p32(kBLdsWsum), &lo, &hi,
+                     [&](uint32_t i) { return (uint32_t)op.off(i) ^ (uint32_t)op.len(i); });
       sh = RowShare{first + lo, 1u, hi - lo};
     }
   }

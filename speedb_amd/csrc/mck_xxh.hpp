@@ -926,7 +926,8 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
   __shared__ X3Lds s;
   const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
   uint32_t lo, hi;
-  share_by_bytes(op, 0u, count, 0xFFFFFFFFu, &s.wsum[0], &lo, &hi);
+  share_by_bytes(op, 0u, count, 0xFFFFFFFFu, &s.wsum[0], &lo, &hi,
+                 [&](uint32_t i) { return (uint32_t)op.off(i) ^ (uint32_t)op.hlen(i); });
   const uint32_t start = lo, stride = 1, n = hi - lo;
   const X3Row X = x3_row(seed);
   for (uint32_t w0 = 0; w0 < n; w0 += kX3DescCache) {
@@ -943,7 +944,8 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
     uint32_t carry = 0;
     for (uint32_t c0 = 0; c0 < wn; c0 += blockDim.x) {
       const uint32_t t = c0 + threadIdx.x;
-      const uint32_t v = t < wn ? x3w_pieces<PREVIEW>(op.hlen(wb + stride * t)) : 0;
+      // (the length this thread staged above: no second global read)
+      const uint32_t v = t < wn ? x3w_pieces<PREVIEW>(s.len[t]) : 0;
       uint32_t x = v;
 #pragma unroll
       for (int d = 1; d < 64; d <<= 1) {
