@@ -20,7 +20,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(REPO, "microbench", "_variants", "stamps.so")
 
 STAMP_DECL = r"""
-__device__ unsigned long long g_stamps[3][2048][16];
+__device__ unsigned long long g_stamps[3][2048][32];
 __device__ __forceinline__ void stamp(int k, int p) {
   if (threadIdx.x == 0 && blockIdx.x < 2048) g_stamps[k][blockIdx.x][p] = wall_clock64();
 }
@@ -49,6 +49,18 @@ PATCHES = [
      " __syncthreads(); stamp(2, 14); }", 1),
     ("mck_crc.hpp", "    crc_rows_loop<Op, W>(op, sh, g);\n  }",
      "    if (wi < 13) stamp(2, 1 + wi);\n    crc_rows_loop<Op, W>(op, sh, g);\n  }", 1),
+    ("mck_crc_bh.hpp", "    *lds_p64(kBLdsAcc + 8 * t) = (uint64_t)(P + hh) << 32;\n  }",
+     "    *lds_p64(kBLdsAcc + 8 * t) = (uint64_t)(P + hh) << 32;\n  }\n  if (sh.start == blockIdx.x || true) stamp(0, 5);", 1),
+    ("mck_crc_bh.hpp", "  const uint32_t W = bh_head_w((uint32_t)(htot >> 16), (uint32_t)(htot & 0xFFFFu));",
+     "  stamp(0, 6);\n  const uint32_t W = bh_head_w((uint32_t)(htot >> 16), (uint32_t)(htot & 0xFFFFu));", 1),
+    ("mck_crc_bh.hpp", "  const uint64_t ex = below + x - v;",
+     "  stamp(0, 7);\n  const uint64_t ex = below + x - v;", 1),
+    ("mck_xxh.hpp", "    if (threadIdx.x == 0) s.ctr = 0;\n    // pieces per span",
+     "    if (threadIdx.x == 0) s.ctr = 0;\n    if (w0 == 0) stamp(1, 5);\n    // pieces per span", 1),
+    ("mck_xxh.hpp", "    if (threadIdx.x == 0) s.pre[wn] = carry;\n    __syncthreads();",
+     "    if (threadIdx.x == 0) s.pre[wn] = carry;\n    if (w0 == 0) stamp(1, 6);\n    __syncthreads();\n    if (w0 == 0) stamp(1, 7);", 1),
+    ("mck_crc.hpp", "      __syncthreads();  // every row is done with the previous window's slots\n      row_desc_stage<Op>(op, sh, false);",
+     "      __syncthreads();  // every row is done with the previous window's slots\n      if (wi < 13) stamp(2, 16 + wi);\n      row_desc_stage<Op>(op, sh, false);", 1),
     ("mck_engine.hip", "}  // extern \"C\"",
      "int mck_dbg_stamps(void* host) {\n  return hipMemcpyFromSymbol(host, HIP_SYMBOL(mck::g_stamps), sizeof(mck::g_stamps)) == hipSuccess ? 0 : -2;\n}\n"
      "}  // extern \"C\"", 1),
@@ -98,7 +110,7 @@ def run(gib):
         im.verify()
         e1.record()
         torch.cuda.synchronize()
-        buf = np.zeros((3, 2048, 16), dtype=np.uint64)
+        buf = np.zeros((3, 2048, 32), dtype=np.uint64)
         assert f(buf.ctypes.data) == 0
         k = 0 if t == S.ChecksumType.kCRC32c else 1
         a = buf[k].astype(np.int64)
@@ -112,6 +124,9 @@ def run(gib):
             print(f"  {nm:12s} p0/10/50/90/100: {pct(rel[:, i])}")
         print(f"  P1-P0: {pct(rel[:, 1] - rel[:, 0])}   P2-P1: {pct(rel[:, 2] - rel[:, 1])}   "
               f"P3-P2: {pct(rel[:, 3] - rel[:, 2])}")
+        fine = (a[:, 5:8] - t0) / 100.0
+        for i, nm in enumerate(("S5", "S6", "S7")):
+            print(f"  {nm} - P1     : {pct(fine[:, i] - rel[:, 1])}")
         ends = rel[:, 3]
         order = np.argsort(ends)
         print("  slowest 8 (wg, cu id, P2, end):", [(int(i), int(a[i, 4]), round(rel[i, 2], 1), round(ends[i], 1))
@@ -165,7 +180,7 @@ def run_rows():
     S.wal_record_crc_batch(sp, types, 7, out=out)
     e1.record()
     torch.cuda.synchronize()
-    buf = np.zeros((3, 2048, 16), dtype=np.uint64)
+    buf = np.zeros((3, 2048, 32), dtype=np.uint64)
     assert f(buf.ctypes.data) == 0
     a = buf[2].astype(np.int64)
     a = a[a[:, 14] > 0]
@@ -179,6 +194,13 @@ def run_rows():
             break
         print(f"  window {w:2d} go: {pct((col[col > 0] - t0) / 100)}")
     print(f"  end          : {pct((a[:, 14] - t0) / 100)}")
+    for w in range(1, 13):
+        d = a[:, 16 + w]
+        g = a[:, 1 + w]
+        ok = (d > 0) & (g > 0)
+        if ok.sum() < len(a) // 2:
+            break
+        print(f"  window {w:2d} staging (go - drained): {pct((g[ok] - d[ok]) / 100)}")
 
 
 if __name__ == "__main__":

@@ -880,6 +880,80 @@ __host__ __device__ __forceinline__ uint32_t blk_long_words(uint32_t slot_cap) {
   return (blk_slot_stride(slot_cap) + 31) / 32;
 }
 
+// ---- entry windows (round 5) ----------------------------------------------
+// The walk's divergent loads -- each entry's 16-byte head (U), its key's
+// fifth dword and eight octet value loads per 64 entries -- are what bound it
+// (the texture addresser, TA_BUSY 91 %).  Since an entry's
+// start p is known one entry ahead, the octet loads fetch the whole ENTRY
+// window [p, p + 128) instead: in step j lane 8 g + t loads bytes [16 t,
+// 16 t + 16) of lane 8 g + j's window (one load instruction: eight
+// contiguous 128-byte windows), the pieces are parked in the lanes' LDS rows
+// at the next iteration's start, and each lane then reads its head, key and
+// (17..128-byte) value pieces from its own row -- no per-lane global load
+// for an entry that fits the window and the block.  Rows are 36 dwords
+// (144 B: 16-byte aligned, conflict-free b128 stores; 16 B of pad for the
+// unaligned reads at the row end).
+constexpr uint32_t kBlkWin = 128, kBlkWinRow = 36;
+__device__ __forceinline__ uint4 lds_row_u4(const uint32_t* w, uint32_t o) {  // 16 bytes at byte o
+  const uint32_t i = o >> 2, sb = o & 3u;
+  const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2], d3 = w[i + 3], d4 = w[i + 4];
+  return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, sb), __builtin_amdgcn_alignbyte(d2, d1, sb),
+                    __builtin_amdgcn_alignbyte(d3, d2, sb), __builtin_amdgcn_alignbyte(d4, d3, sb));
+}
+// Octet step loads: W[j] = piece (lane & 7) of the window at address a of
+// lane (lane & ~7) + j, or the zero page where that lane has none.
+__device__ __forceinline__ void blk_win_load(uint4 (&W)[8], uint64_t a, bool have, uint32_t lane, uint64_t zp) {
+  const uint32_t t = lane & 7, gb = lane & ~7u;
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const uint64_t aj = __shfl(a, (int)gb + j, 64);
+    const bool hj = __shfl((int)have, (int)gb + j, 64) != 0;
+    W[j] = span_load16<false>(hj ? aj + 16u * t : zp);
+  }
+}
+// ... parked in the rows: piece t of lane (gb + j)'s window -> row gb + j.
+__device__ __forceinline__ void blk_win_store(uint32_t (*rows)[kBlkWinRow], const uint4 (&W)[8], uint32_t tid) {
+  const uint32_t t = tid & 7, g0 = tid & ~7u;
+#pragma unroll
+  for (int j = 0; j < 8; j++)
+    *reinterpret_cast<uint4*>(&rows[g0 + j][4 * t]) = W[j];
+}
+// xp_mid_octets over the lanes' windows: value j = bytes [vo, vo + vl) of
+// lane (gb + j)'s row (17 <= vl <= 128, vo + vl <= 128).
+__device__ __forceinline__ uint64_t xp_mid_octets_win(const uint32_t (*rows)[kBlkWinRow], uint32_t vo, uint32_t vl,
+                                                      bool mine, uint64_t klo, uint64_t khi, uint32_t tid) {
+  const uint32_t lane = tid & 63, t = lane & 7, g0 = tid & ~7u, gb = lane & ~7u;
+  const uint32_t lm_own = mine ? vl : 0u;
+  uint64_t m[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) {
+    const int src = (int)gb + j;
+    const uint32_t o = (uint32_t)__shfl((int)vo, src, 64);
+    const uint32_t lm = (uint32_t)__shfl((int)lm_own, src, 64);
+    const int last = (int)lm - 16;
+    int off = (t & 1) ? last - 16 * (int)(t >> 1) : 16 * (int)(t >> 1);
+    off = off < 0 ? 0 : off > last ? last : off;
+    const uint4 d = lds_row_u4(rows[g0 + j], lm ? o + (uint32_t)off : 0u);
+    const uint64_t lo = (uint64_t)d.y << 32 | d.x, hi = (uint64_t)d.w << 32 | d.z;
+    const uint64_t mm = mul128_fold64(lo ^ klo, hi ^ khi);
+    m[j] = (t >> 1) < (lm + 31) / 32 ? mm : 0ull;
+  }
+  uint64_t r1[4], r2[2];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const uint64_t keep = (t & 4) ? m[4 + q] : m[q], send = (t & 4) ? m[q] : m[4 + q];
+    r1[q] = keep + dpp64<0x141>(send);
+  }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const uint64_t keep = (t & 2) ? r1[2 + q] : r1[q], send = (t & 2) ? r1[q] : r1[2 + q];
+    r2[q] = keep + dpp64<0x4E>(send);
+  }
+  const uint64_t keep = (t & 1) ? r2[1] : r2[0], send = (t & 1) ? r2[0] : r2[1];
+  const uint64_t sum = keep + dpp64<0xB1>(send);
+  return xxph3_avalanche((uint64_t)lm_own * P64_1 + sum);
+}
+
 template <int KIND>
 __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t count, uint32_t slot_cap,
                                                        uint8_t* arena, uint32_t arena_cap, uint64_t* slot_h,
@@ -887,11 +961,14 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
                                                        uint64_t* key_bytes, uint32_t* interval_out,
                                                        int32_t* status, uint32_t* long_flag) {
   __shared__ uint32_t s_key[256][kBlkKeyBuf / 4 + 5];  // as k_block_kv_t
+  __shared__ __attribute__((aligned(16))) uint32_t s_win[256][kBlkWinRow];  // the entry windows
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
   uint8_t* const lkey = reinterpret_cast<uint8_t*>(s_key[threadIdx.x]);
   const bool in = b < count;
   const GblRd rd{in ? blocks.ptr(b) : nullptr};
+  const LdsRd wr{s_win[threadIdx.x], 0};  // this lane's window (entry-relative offsets)
+  const uint64_t zp = reinterpret_cast<uint64_t>(&g_zero16[0]);
   const uint64_t n64 = in ? blocks.len(b) : 0;
   // ---- the block's header and restart array: blk_seq_walk's checks
   int st = kBlkOk;
@@ -934,18 +1011,31 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
   uint32_t next = active ? rd.u32(ro) : 0u;
   uint32_t nextn = active && nr > 1 ? rd.u32(ro + 4) : 0xFFFFFFFFu;
   uint64_t kbytes = 0;
-  // the next entry's first 16 bytes, one entry ahead (k_block_kv_t)
+  // the next entry, one entry ahead: its window (octet loads, wnx) when
+  // [p, p + 128) lies in the block, else its first 16 bytes (U, uok)
   uint4 U = make_uint4(0, 0, 0, 0);
-  bool uok = false;
+  uint4 Wn[8];
+  bool uok = false, wnx = false;
   bool any_long = false;
   if (active) {
-    uok = n >= 16;
+    wnx = n >= kBlkWin;
+    uok = !wnx && n >= 16;
     if (uok) U = vload16_any(reinterpret_cast<uint64_t>(rd.p));
   }
+  blk_win_load(Wn, reinterpret_cast<uint64_t>(rd.p), wnx, lane, zp);
   while (__any(active)) {
     uint32_t sh = 0, ns = 0, q = 0, v = 0, vl = 0;
     uint32_t kw[4] = {0, 0, 0, 0};
     bool vmid = false;
+    // this iteration's windows into the rows (their loads were issued one
+    // entry ago)
+    const bool wok = wnx;
+    if (__any(wok)) {
+      blk_win_store(s_win, Wn, threadIdx.x);
+      wave_lds_sync();
+    }
+    wnx = false;
+    uint32_t pn = 0;  // the next entry (wnx)
     if (active) {
       // block.cc:1091-1132 with the restart checks of blk_seq_walk
       int err = kBlkOk;
@@ -961,10 +1051,10 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
         next = nextn;
         nextn = r + 1 < nr ? rd.u32(ro + 4 * (r + 1)) : 0xFFFFFFFFu;
       }
-      const uint4 Uc = U;
+      const uint4 Uc = wok ? lds_row_u4(s_win[threadIdx.x], 0) : U;
       bool fast = false;
       if (err == kBlkOk) {
-        if (KIND != kBlkIndexDelta && KIND != kBlkIndexDeltaFk && uok && (Uc.x & 0x808080u) == 0) {
+        if (KIND != kBlkIndexDelta && KIND != kBlkIndexDeltaFk && (uok || wok) && (Uc.x & 0x808080u) == 0) {
           const uint32_t kk = (Uc.x >> 8) & 255u, xx = (Uc.x >> 16) & 255u;
           if (p <= ro && ro - p >= 3 && ro - (p + 3) >= kk + xx) {
             sh = Uc.x & 255u;
@@ -986,13 +1076,18 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
         st = err;
         active = false;
       } else {
-        const uint32_t pn = v + vl;
+        pn = v + vl;
+        uok = false;
         if (pn < ro) {
-          uok = pn + 16 <= n;
+          // a window only while entries fit one (the next is likely the
+          // size of this one): a 1000-byte value's entry would fetch 112
+          // bytes it never uses, where its 16-byte head is all the walk needs
+          wnx = pn + kBlkWin <= n && pn - p <= kBlkWin;
+          uok = !wnx && pn + 16 <= n;
           if (uok) U = vload16_any(reinterpret_cast<uint64_t>(rd.p + pn));
         }
         if (fast) {
-          const uint32_t e = ns > 13 ? rd.u32(p + 16) : 0u;
+          const uint32_t e = ns > 13 ? (wok ? s_win[threadIdx.x][4] : rd.u32(p + 16)) : 0u;
           kw[0] = __builtin_amdgcn_alignbyte(Uc.y, Uc.x, 3);
           kw[1] = __builtin_amdgcn_alignbyte(Uc.z, Uc.y, 3);
           kw[2] = __builtin_amdgcn_alignbyte(Uc.w, Uc.z, 3);
@@ -1007,10 +1102,18 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
         vmid = vl > 16 && vl <= 128;
       }
     }
-    uint64_t hv;
-    {
-      const uint64_t hm = xp_mid_octets(reinterpret_cast<uint64_t>(rd.p) + v, vl, vmid, oklo, okhi, lane);
-      hv = vmid ? hm : 0ull;
+    // the next entries' windows: in flight while this entry is hashed
+    if (__any(wnx)) blk_win_load(Wn, reinterpret_cast<uint64_t>(rd.p) + pn, wnx, lane, zp);
+    // the entry lies in its window: key and value bytes from the row
+    const bool inwin = active && wok && v + vl <= p + kBlkWin;
+    uint64_t hv = 0;
+    if (__any(vmid && inwin)) {
+      const uint64_t hm = xp_mid_octets_win(s_win, v - p, vl, vmid && inwin, oklo, okhi, threadIdx.x);
+      hv = vmid && inwin ? hm : hv;
+    }
+    if (__any(vmid && !inwin)) {
+      const uint64_t hm = xp_mid_octets(reinterpret_cast<uint64_t>(rd.p) + v, vl, vmid && !inwin, oklo, okhi, lane);
+      hv = vmid && !inwin ? hm : hv;
     }
     const bool lng = active && vl >= kBlkLong;
     if (active) {
@@ -1031,7 +1134,7 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
           kd[4] = __builtin_amdgcn_alignbyte(0u, kw[3], sb);
         }
         for (uint32_t i = sh + 16; i < kn; i += 4) {
-          const uint32_t w = rd.u32(q + i - sh);
+          const uint32_t w = inwin ? wr.u32(q - p + i - sh) : rd.u32(q + i - sh);
           for (uint32_t c = 0; c < 4 && i + c < kn; c++) lkey[i + c] = (uint8_t)(w >> (8 * c));
         }
         const LdsRd kr{s_key[threadIdx.x], 0};
@@ -1041,7 +1144,12 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
         __threadfence_block();
         hv ^= xp_lane(GblRd{gkey}, 0, kn, kSeedK);
       }
-      if (!vmid && !lng) hv ^= xp_short(rd, v, vl, kSeedV);  // <= 16 or 129..240 bytes
+      if (!vmid && !lng) {  // <= 16 or 129..240 bytes
+        if (inwin)
+          hv ^= xp_short(wr, v - p, vl, kSeedV);
+        else
+          hv ^= xp_short(rd, v, vl, kSeedV);
+      }
       if (idx & 1)  // entries idx - 1, idx as one 16-byte store (half the divergent stores)
         *reinterpret_cast<__attribute__((address_space(1))) span_u32x4*>(
             reinterpret_cast<uint64_t>(slot_h + sbase + idx - 1)) =

@@ -648,7 +648,9 @@ int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32
   uint64_t* const kb = verify ? w.walk_kb : key_base;
   uint64_t* const ab = verify ? w.walk_ab : arena_base;
   MCK_HIP(hipMemsetAsync(w.flag, 0, 4, st));
-  if (int rc = launch_blk<BlkWalkT>(kind, n, st, n, kBlkWalkLdsPad, to_src(blocks), n, slot_cap, w.arena, arena_cap,
+  // (the walk's key buffers + entry windows, 73 KiB static, already hold it
+  // at two workgroups per CU: no pad)
+  if (int rc = launch_blk<BlkWalkT>(kind, n, st, n, 0, to_src(blocks), n, slot_cap, w.arena, arena_cap,
                                     w.slot_h, w.slot_m, w.blk_long, kb, ab, restart_interval, status, w.flag))
     return rc;
   const uint32_t tiles = (uint32_t)blk_tiles(n);

@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <chrono>
 #include <random>
+#include <string>
 #include <vector>
 
 #include "speedb_amd/mck.h"
@@ -63,6 +64,10 @@ static std::vector<double> timed(F f, int reps) {
 
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 2000;
+  // "spin": the host spins in hipStreamSynchronize instead of sleeping
+  // (hipDeviceScheduleSpin, set before the context exists)
+  const bool spin = argc > 2 && std::string(argv[2]) == "spin";
+  if (spin) CK(hipSetDeviceFlags(hipDeviceScheduleSpin));
   hipStream_t st;
   CK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   const mck_stream_t ms = reinterpret_cast<mck_stream_t>(st);
@@ -75,7 +80,22 @@ int main(int argc, char** argv) {
                              if (hipStreamSynchronize(st) != hipSuccess) bad = true;
                            },
                            reps));
-  printf("{\"harness\": \"tests/cpp/latency_verify.hip\", \"reps\": %d, \"floor_us\": %.2f, \"rows\": [", reps, fl.p50);
+  // the same empty launch, device time between two events
+  hipEvent_t f0, f1;
+  CK(hipEventCreate(&f0));
+  CK(hipEventCreate(&f1));
+  std::vector<double> ft(200);
+  for (auto& x : ft) {
+    CK(hipEventRecord(f0, st));
+    hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st);
+    CK(hipEventRecord(f1, st));
+    CK(hipEventSynchronize(f1));
+    float m = 0;
+    CK(hipEventElapsedTime(&m, f0, f1));
+    x = m * 1e3;
+  }
+  printf("{\"harness\": \"tests/cpp/latency_verify.hip\", \"sync\": \"%s\", \"reps\": %d, \"floor_us\": %.2f, "
+         "\"floor_kernel_us\": %.2f, \"rows\": [", spin ? "spin" : "default", reps, fl.p50, stat(ft).p50);
   std::mt19937_64 rng(1);
   const int sizes[] = {1, 8, 32, 64, 256};
   for (int si = 0; si < 5; si++) {

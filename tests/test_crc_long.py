@@ -206,3 +206,57 @@ def test_long_sst_verify_mix(gpu, oracle, ctype):
     assert int(cnt.item()) == len(bad)
 
 
+
+
+@pytest.mark.parametrize("ctype", [1, 4])
+@pytest.mark.parametrize("order", ["file", "shuffled", "reversed"])
+def test_byte_shares_partition_any_order(gpu, oracle, ctype, order):
+    """Byte-balanced workgroup shares (share_by_bytes: the sampled multi-level
+    search; k_crc_ragged for SST blocks, k_xxh3_wave) must partition every
+    batch -- each span verified exactly once -- whatever the offsets' order:
+    file order (exact byte balance), shuffled and reversed (the search is
+    only monotone then, the clamp to count shares bounds the imbalance).
+    30,000 blocks (> 64 per workgroup, so the byte shares are on), outputs
+    pre-filled with sentinels so a span no workgroup visited shows."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(900 + ctype)
+    n = 30000
+    sizes = [rnd.choice([rnd.randrange(200, 3000)] * 19 + [65536 + rnd.randrange(0, 256)]) for _ in range(n)]
+    offs, pos = [], 0
+    for ln in sizes:
+        offs.append(pos)
+        pos += ln + 5 + rnd.randrange(0, 3)
+    host = bytearray(splitmix_bytes(31 + ctype, pos + 64))
+    dev = torch.frombuffer(host, dtype=torch.uint8).to("cuda")
+    perm = list(range(n))
+    if order == "shuffled":
+        rnd.shuffle(perm)
+    elif order == "reversed":
+        perm.reverse()
+    po = [offs[i] for i in perm]
+    pl = [sizes[i] for i in perm]
+    sp = _spans(torch, S, dev, po, pl)
+    ct = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    tr = S.sst_trailer_batch(ctype, sp, ct)
+    # seal every block on the device: [type 0][LE32 trailer]
+    pos_t = torch.tensor(po, dtype=torch.int64, device="cuda") + torch.tensor(pl, dtype=torch.int64, device="cuda")
+    trailer = torch.zeros((n, 5), dtype=torch.uint8, device="cuda")
+    trailer[:, 1:] = tr.view(torch.uint8).view(n, 4)
+    dev[(pos_t.unsqueeze(1) + torch.arange(5, device="cuda")).flatten()] = trailer.flatten()
+    # the trailers of a sample against the oracle
+    img = bytes(dev.cpu().numpy().tobytes())
+    for k in rnd.sample(range(n), 200):
+        o, ln = po[k], pl[k]
+        assert oracle.BuiltinLast(ctype, img[o:o + ln], 0) == _u32(tr[k:k + 1])[0], (order, k)
+    mm = torch.full((n,), 0xAB, dtype=torch.uint8, device="cuda")
+    comp = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    stored = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    mm, comp, stored, cnt = S.sst_verify_batch(ctype, sp, outs=(mm, comp, stored))
+    assert int(cnt.item()) == 0 and int((mm != 0).sum().item()) == 0, order
+    assert torch.equal(comp, stored) and torch.equal(comp, tr)
+    bad = sorted(rnd.sample(range(n), 40))
+    for k in bad:
+        dev[po[k] + rnd.randrange(0, pl[k])] ^= 0x08
+    mm, comp, stored, cnt = S.sst_verify_batch(ctype, sp)
+    assert torch.nonzero(mm).flatten().cpu().tolist() == bad and int(cnt.item()) == len(bad)
