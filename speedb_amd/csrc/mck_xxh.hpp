@@ -31,7 +31,7 @@ constexpr uint32_t P32_1 = 0x9E3779B1u, P32_2 = 0x85EBCA77u, P32_3 = 0xC2B2AE3Du
                    P32_4 = 0x27D4EB2Fu, P32_5 = 0x165667B1u;
 
 // XXH3_kSecret, util/xxhash.h:3661-3674 (192 bytes)
-__constant__ const uint8_t kXxh3Secret[192] = {
+constexpr uint8_t kXxh3SecretBytes[192] = {
     0xb8, 0xfe, 0x6c, 0x39, 0x23, 0xa4, 0x4b, 0xbe, 0x7c, 0x01, 0x81, 0x2c, 0xf7, 0x21, 0xad, 0x1c,
     0xde, 0xd4, 0x6d, 0xe9, 0x83, 0x90, 0x97, 0xdb, 0x72, 0x40, 0xa4, 0xa4, 0xb7, 0xb3, 0x67, 0x1f,
     0xcb, 0x79, 0xe6, 0x4e, 0xcc, 0xc0, 0xe5, 0x78, 0x82, 0x5a, 0xd0, 0x7d, 0xcc, 0xff, 0x72, 0x21,
@@ -45,28 +45,41 @@ __constant__ const uint8_t kXxh3Secret[192] = {
     0x2b, 0x16, 0xbe, 0x58, 0x7d, 0x47, 0xa1, 0xfc, 0x8f, 0xf8, 0xb8, 0xd1, 0x7a, 0xd0, 0x31, 0xce,
     0x45, 0xcb, 0x3a, 0x8f, 0x95, 0x16, 0x04, 0x28, 0xaf, 0xd7, 0xfb, 0xca, 0xbb, 0x4b, 0x40, 0x7e,
 };
+// ... as 24 little-endian 8-byte words (+ one zero word): a secret word at a
+// per-lane byte offset is two aligned 8-byte loads and a funnel shift (the
+// byte-wise read was up to 16 byte loads per word: the XXH3 wave driver's
+// per-lane constants alone were ~100 loads per lane in its prologue)
+struct X3SecretWords {
+  uint64_t w[25];
+};
+constexpr X3SecretWords x3_secret_words() {
+  X3SecretWords r{};
+  for (int i = 0; i < 24; i++) {
+    uint64_t v = 0;
+    for (int b = 7; b >= 0; b--) v = (v << 8) | kXxh3SecretBytes[8 * i + b];
+    r.w[i] = v;
+  }
+  r.w[24] = 0;
+  return r;
+}
+__constant__ const X3SecretWords kXxh3SecretW = x3_secret_words();
 
 __device__ __forceinline__ uint64_t sec64(int off) {
-  uint64_t v = 0;
-#pragma unroll
-  for (int b = 7; b >= 0; b--) v = (v << 8) | kXxh3Secret[off + b];
-  return v;
+  const int w = off >> 3, sh = (off & 7) * 8;
+  const uint64_t lo = kXxh3SecretW.w[w];
+  if (sh == 0) return lo;
+  return (lo >> sh) | (kXxh3SecretW.w[w + 1] << (64 - sh));
 }
-__device__ __forceinline__ uint32_t sec32(int off) {
-  uint32_t v = 0;
-#pragma unroll
-  for (int b = 3; b >= 0; b--) v = (v << 8) | kXxh3Secret[off + b];
-  return v;
-}
+__device__ __forceinline__ uint32_t sec32(int off) { return (uint32_t)sec64(off); }
 // 8 bytes at byte offset `off` of the seeded secret of
 // XXPH3_initCustomSecret (util/xxph3.h:1613-1624): 8-byte word w of the
 // default secret gets +seed (w even) or -seed (w odd).  seed 0 = the default
 // secret, so XXH3 v0.8.1 uses the same accessor.
 __device__ __forceinline__ uint64_t csec64(int off, uint64_t seed) {
   const int w = off >> 3, sh = (off & 7) * 8;
-  const uint64_t lo = sec64(8 * w) + ((w & 1) ? 0 - seed : seed);
+  const uint64_t lo = kXxh3SecretW.w[w] + ((w & 1) ? 0 - seed : seed);
   if (sh == 0) return lo;
-  const uint64_t hi = sec64(8 * w + 8) + (((w + 1) & 1) ? 0 - seed : seed);
+  const uint64_t hi = kXxh3SecretW.w[w + 1] + (((w + 1) & 1) ? 0 - seed : seed);
   return (lo >> sh) | (hi << (64 - sh));
 }
 

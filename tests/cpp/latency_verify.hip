@@ -142,6 +142,26 @@ int main(int argc, char** argv) {
       if (hipStreamSynchronize(st) != hipSuccess) rc = 1;
     };
     const Stat s = stat(timed(call, reps));
+    // host time to ENQUEUE one call (no sync; 64 calls, then one sync):
+    // the API's own CPU cost, next to an empty kernel's launch
+    const auto enq = [&](auto one) {
+      std::vector<double> v(50);
+      for (auto& x : v) {
+        (void)hipStreamSynchronize(st);
+        const auto a = std::chrono::steady_clock::now();
+        for (int r = 0; r < 64; r++) one();
+        x = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - a).count() / 64;
+      }
+      (void)hipStreamSynchronize(st);
+      return stat(v).p50;
+    };
+    double enq_us = 0, enq_empty_us = 0;
+    {
+      const auto r = enq([&] { (void)mck_sst_verify_batch(MCK_kCRC32c, &sp, nullptr, 0, d_mm, nullptr, nullptr, nullptr, ms); });
+      enq_us = r;
+      const auto r2 = enq([&] { hipLaunchKernelGGL(k_empty, dim3(1), dim3(64), 0, st); });
+      enq_empty_us = r2;
+    }
     // device time of the verify alone
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
@@ -175,8 +195,9 @@ int main(int argc, char** argv) {
     for (uint32_t i = 0; i < n; i++) ok = ok && mm[i] == (i == victim ? 1 : 0);
     ok = ok && cnt == 1;
     printf("%s{\"blocks\": %u, \"bytes\": %llu, \"device_us\": %.2f, \"p10_us\": %.2f, \"p90_us\": %.2f, "
-           "\"kernel_us\": %.2f, \"ok\": %s}",
-           si ? ", " : "", n, (unsigned long long)(pos - 5ull * n), s.p50, s.p10, s.p90, k.p50, ok ? "true" : "false");
+           "\"kernel_us\": %.2f, \"enqueue_us\": %.2f, \"enqueue_empty_us\": %.2f, \"ok\": %s}",
+           si ? ", " : "", n, (unsigned long long)(pos - 5ull * n), s.p50, s.p10, s.p90, k.p50, enq_us, enq_empty_us,
+           ok ? "true" : "false");
     bad = bad || !ok;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
