@@ -100,14 +100,21 @@ __device__ __forceinline__ uint32_t lds_ticket(P ctr) {
 // issued for the count-balanced share's first spans with the first level's
 // samples, so the window staging that follows finds them in the cache (the
 // SST images' staging waited 6-9 us on them, round-5 stamps).
-template <class Op, class P, class F>
+// overlap(): the caller's own prologue work (its loads ride along with the
+// first level's round trip); called exactly once on every path.
+struct NoOverlap {
+  __device__ void operator()() const {}
+};
+template <class Op, class P, class F, class O = NoOverlap>
 __device__ __forceinline__ void share_by_bytes(const Op& op, uint32_t first, uint32_t count, uint32_t slack,
-                                               P scratch, uint32_t* lo, uint32_t* hi, const F& prefetch) {
+                                               P scratch, uint32_t* lo, uint32_t* hi, const F& prefetch,
+                                               const O& overlap = O{}) {
   const uint32_t G = gridDim.x, b = blockIdx.x;
   const uint32_t clo = (uint32_t)((uint64_t)count * b / G), chi = (uint32_t)((uint64_t)count * (b + 1) / G);
   if (count <= 1 || G == 1) {
     *lo = clo;
     *hi = chi;
+    overlap();
     return;
   }
   constexpr uint32_t kS = 512;  // samples per boundary and level
@@ -124,6 +131,7 @@ __device__ __forceinline__ void share_by_bytes(const Op& op, uint32_t first, uin
   const uint32_t p0 = count > kS ? (uint32_t)((uint64_t)count * t / kS) : t;  // level 0's sample
   const uint64_t s0 = count > kS || t < count ? op.off(first + p0) : 0ull;
   const uint32_t pf = clo + threadIdx.x < count ? prefetch(first + clo + threadIdx.x) : 0u;
+  overlap();
   const uint64_t range = oL > o0 ? oL - o0 : 0;
   const uint32_t j = b + tgt;
   // o0 + range * j / G without a 128-bit product

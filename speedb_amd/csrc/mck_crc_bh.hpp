@@ -93,45 +93,54 @@ __device__ __forceinline__ uint32_t bh_init_of(int kind, uint32_t key, uint32_t 
 }
 
 // ---- LDS fill: tables from the device copy, then the computed ones -------------
-template <class Op>
-__device__ __forceinline__ void crc_bh_fill(const Op& op, const CrcTables* __restrict__ g) {
-  const uint32_t t = threadIdx.x;
-  constexpr int kLow = (int)(kLdsGap + 512) / 16;  // lane_final + gap: 2080 slots
+// Split in two: the loads (bh_fill_load, registers) and the stores + the
+// computed tables (bh_fill_store), so a caller can issue the loads with its
+// own first memory round trip (k_crc_ragged: the byte-share search).
+struct BhFill {
   uint32_t st[4];
+  uint4 l[3];
+  uint4 rg, pw, us;
+};
+constexpr int kBhFillLow = (int)(kLdsGap + 512) / 16;  // lane_final + gap: 2080 slots
+__device__ __forceinline__ void bh_fill_load(BhFill& f, const CrcTables* __restrict__ g) {
+  const uint32_t t = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
     const uint32_t i = t + kCrcBlock * k;
-    st[k] = g->step[(i >> 2) & 3][i >> 4];
+    f.st[k] = g->step[(i >> 2) & 3][i >> 4];
   }
   const uint4* lo = reinterpret_cast<const uint4*>(&g->lane_final[0][0][0]);
-  uint4 l[3];
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const int i = (int)t + kCrcBlock * k;
-    l[k] = lo[i < kLow ? i : 0];
+    f.l[k] = lo[i < kBhFillLow ? i : 0];
   }
   // row gaps (96 slots), pow maps (b + 2 of pow1k: 672 slots), un-shift k < 16 (512)
-  const uint4 rg = reinterpret_cast<const uint4*>(&g->gap_row[0][0][0])[t < 96 ? t : 0];
-  const uint4 pw = reinterpret_cast<const uint4*>(&g->pow1k[2][0][0])[t < kBPowBits * 32 ? t : 0];
-  const uint4 us = reinterpret_cast<const uint4*>(&g->unshift[0][0][0])[t < 512 ? t : 0];
+  f.rg = reinterpret_cast<const uint4*>(&g->gap_row[0][0][0])[t < 96 ? t : 0];
+  f.pw = reinterpret_cast<const uint4*>(&g->pow1k[2][0][0])[t < kBPowBits * 32 ? t : 0];
+  f.us = reinterpret_cast<const uint4*>(&g->unshift[0][0][0])[t < 512 ? t : 0];
+}
+template <class Op>
+__device__ __forceinline__ void bh_fill_store(const Op& op, const BhFill& f) {
+  const uint32_t t = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 4; k++) {
-    const uint32_t x = st[k];
+    const uint32_t x = f.st[k];
     *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(
         static_cast<size_t>(kLdsStep + 16 * (t + kCrcBlock * k))) = span_u32x4{x, x, x, x};
   }
 #pragma unroll
   for (int k = 0; k < 3; k++) {
     const int i = (int)t + kCrcBlock * k;
-    if (i < kLow)
+    if (i < kBhFillLow)
       *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(16 * i)) =
-          span_u32x4{l[k].x, l[k].y, l[k].z, l[k].w};
+          span_u32x4{f.l[k].x, f.l[k].y, f.l[k].z, f.l[k].w};
   }
   typedef __attribute__((address_space(3))) span_u32x4 lds_u32x4_t;
-  if (t < 96) *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsRowGap + 16 * t)) = span_u32x4{rg.x, rg.y, rg.z, rg.w};
+  if (t < 96) *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsRowGap + 16 * t)) = span_u32x4{f.rg.x, f.rg.y, f.rg.z, f.rg.w};
   if (t < kBPowBits * 32)
-    *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsPow + 16 * t)) = span_u32x4{pw.x, pw.y, pw.z, pw.w};
-  if (t < 512) *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsUnshift + 16 * t)) = span_u32x4{us.x, us.y, us.z, us.w};
+    *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsPow + 16 * t)) = span_u32x4{f.pw.x, f.pw.y, f.pw.z, f.pw.w};
+  if (t < 512) *reinterpret_cast<lds_u32x4_t*>(static_cast<size_t>(kBLdsUnshift + 16 * t)) = span_u32x4{f.us.x, f.us.y, f.us.z, f.us.w};
   if (t < 128) {  // byte masks of a 16-byte piece
     const int h = (int)(t >> 2) & 15, k = (int)(t & 3);
     if (t < 64) {  // keep bytes >= h
@@ -677,8 +686,13 @@ __device__ __forceinline__ void crc_bh_window(const Op& op, const UShare& sh, ui
 // A workgroup's share [start, start + n) (contiguous), in windows of at most
 // kBNC spans, as even as the share allows.
 template <class Op, bool T>
-__device__ __forceinline__ void crc_bh_driver(const Op& op, const RowShare& share, const CrcTables* __restrict__ g) {
-  crc_bh_fill(op, g);
+__device__ __forceinline__ void crc_bh_driver(const Op& op, const RowShare& share, const CrcTables* __restrict__ g,
+                                              bool filled = false) {
+  if (!filled) {  // (k_crc_ragged fills the image itself when it searched byte shares)
+    BhFill f;
+    bh_fill_load(f, g);
+    bh_fill_store(op, f);
+  }
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   const int kind = op.init_kind();
   const uint32_t n = share.n;

@@ -293,12 +293,20 @@ __global__ __launch_bounds__(1024) void k_crc_ragged(Op op, uint32_t first, uint
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   asm volatile("" ::"v"((uint32_t)(size_t)lds));
   RowShare sh = row_share<BLK>(first, count);
+  bool filled = false;  // the body/head image is in LDS
   if constexpr (BLK && ByteShares<Op>::value) {
     if (count >= kByteSharesMin * gridDim.x) {  // workgroup-uniform
+      // the body/head table loads ride along with the search's first round
+      // trip and are stored right after it (the row drivers, should a share
+      // take them, fill their own image over it)
+      BhFill fill;
       uint32_t lo, hi;
       share_by_bytes(op, first, count, count / gridDim.x, lds_p32(kBLdsWsum), &lo, &hi,
-                     [&](uint32_t i) { return (uint32_t)op.off(i) ^ (uint32_t)op.len(i); });
+                     [&](uint32_t i) { return (uint32_t)op.off(i) ^ (uint32_t)op.len(i); },
+                     [&] { bh_fill_load(fill, &g_crc_tables); });
+      bh_fill_store(op, fill);
       sh = RowShare{first + lo, 1u, hi - lo};
+      filled = true;
     }
   }
   if (sh.n == 0) return;  // workgroup-uniform
@@ -310,7 +318,7 @@ __global__ __launch_bounds__(1024) void k_crc_ragged(Op op, uint32_t first, uint
   }
   const bool bh = force == 7 || (force == 0 && BLK && crc_share_long(op, sh));
   if (bh)
-    crc_bh_driver<Op, T>(op, sh, &g_crc_tables);
+    crc_bh_driver<Op, T>(op, sh, &g_crc_tables, filled);
   else
     crc_rows_windows<Op>(op, sh, lds, &g_crc_tables, force == 8 || force == 9 ? 0 : force);
 }

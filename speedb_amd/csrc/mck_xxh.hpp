@@ -939,10 +939,14 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
   __shared__ X3Lds s;
   const uint32_t lane = threadIdx.x & 63, wpb = blockDim.x >> 6, wid = threadIdx.x >> 6;
   uint32_t lo, hi;
+  // the per-lane constants' loads ride along with the search's first round
+  // trip (their ~1.2 us came after the 5 us search: round-5 LDS stamps,
+  // microbench/r5_stamps_x3.py)
+  X3Row X;
   share_by_bytes(op, 0u, count, 0xFFFFFFFFu, &s.wsum[0], &lo, &hi,
-                 [&](uint32_t i) { return (uint32_t)op.off(i) ^ (uint32_t)op.hlen(i); });
+                 [&](uint32_t i) { return (uint32_t)op.off(i) ^ (uint32_t)op.hlen(i); },
+                 [&] { X = x3_row(seed); });
   const uint32_t start = lo, stride = 1, n = hi - lo;
-  const X3Row X = x3_row(seed);
   for (uint32_t w0 = 0; w0 < n; w0 += kX3DescCache) {
     const uint32_t wn = n - w0 < kX3DescCache ? n - w0 : kX3DescCache;
     const uint32_t wb = start + stride * w0;  // span of window slot t: wb + stride t
