@@ -126,6 +126,8 @@ def parse():
                    help="largest resident WAL image per GPU (wal); a bigger share is verified in passes")
     p.add_argument("--file-bytes", type=int, default=4 << 30, help="file image bytes per GPU (file)")
     p.add_argument("--wal-records", type=int, default=2 << 20, help="logical records per GPU (walwrite)")
+    p.add_argument("--wal-len-min", type=int, default=1000, help="smallest record payload (walwrite)")
+    p.add_argument("--wal-len-max", type=int, default=1100, help="largest record payload (walwrite)")
     p.add_argument("--blob-records", type=int, default=1 << 20, help="blob records per GPU (blob)")
     p.add_argument("--kvs", type=int, default=1 << 22, help="KVs per GPU (kv)")
     p.add_argument("--kv-value-bytes", type=int, default=1000, help="value bytes (blockkv)")
@@ -495,7 +497,7 @@ def make_workload(args, dev, rank, world):
         w.check = check
     elif args.workload == "walwrite":
         rng = np.random.default_rng(600 + rank)
-        lens = rng.integers(1000, 1101, size=args.wal_records).astype(np.uint32)
+        lens = rng.integers(args.wal_len_min, args.wal_len_max + 1, size=args.wal_records).astype(np.uint32)
         offs = np.zeros(len(lens), dtype=np.uint64)
         offs[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
         src = W.rand_bytes(int(lens.sum()) + 64, dev, 601 + rank)
@@ -516,7 +518,8 @@ def make_workload(args, dev, rank, world):
         # payload and the 24 B descriptor once, writes the stream and the 4 B CRC
         w.kernel = "mck::k_wal_write_il (1 launch(es) per step, timed as the step)"
         w.alg_bytes = int(lens.sum()) + nbytes + nf * (24 + 4)
-        w.desc = (f"device WAL writer: group commit of {len(lens)} records of 1000-1100 B per GPU "
+        w.desc = (f"device WAL writer: group commit of {len(lens)} records of "
+                  f"{args.wal_len_min}-{args.wal_len_max} B per GPU "
                   f"(README 1 KB values) -> {nf} physical records, {nbytes} B of log stream "
                   "(log::Writer::AddRecord + EmitPhysicalRecord, SURVEY.md 8f row 3)")
         w.cfg = {"records_per_gpu": len(lens), "fragments": nf, "stream_bytes": nbytes}

@@ -782,15 +782,53 @@ __device__ __forceinline__ bool wal_il_step(const WalIlCtx& X, const WalIlState&
   const bool firstr = r == sp.rounds - 1;
   const bool fin = live && last;
 
-  // ---- the output of this (span, round), from the round's own registers ----
   const uint32_t type = A.key & 0xFF, pad = (A.key >> 8) & 0xFF;
+  il_mask(ca, sp, r, c);
+
+  // ---- next unit (as crc_rows_step), its load in flight over the CRC round ----
+  const bool go = live && (!last || A.nt < X.share);
+  const RowSpan nsp = row_span<W, NP>(X.base + (((uint64_t)A.nd.y << 32) | A.nd.x), A.nd.z, A.nd.w, kInitTyped);
+  const bool sw = go && last;
+  B.sp = row_span_sel(sw, nsp, sp);
+  B.r = go ? (last ? nsp.rounds - 1 : r - 1) : r;
+  B.i = sw ? X.sh.idx(A.nt) : A.i;
+  cb = il_load(B.sp, B.r, c, X.zp);
+
+  x = il_round(firstr ? 0u : x, ca, sp, r, c, X.L);
+  uint32_t crc = 0;
+  if (wave_any(fin)) crc = crc_mask(row_finish4<W>(x, sp, X.lf4));
+  if (wave_any(live && !last)) x = il_gap(x, 0u);  // to the lane's piece in the next round
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---- the output of this (span, round), from the round's own registers ----
+  // Every store of the round -- payload pieces, the edge bytes, the header
+  // once the CRC is known -- issues here, back to back: a 128-B line the
+  // round writes in parts is then complete before L2 writes it back (stores
+  // split around the CRC round measured 1.09-1.15x the stream's bytes).
   const uint32_t hs = ((type >= 5 && type <= 8) || type == 11) ? 11u : 7u;
   const uint64_t P = X.obase + A.dst + hs;  // payload in the output
+  // the < 16 payload bytes before the first and after the last full output
+  // piece (lane c: head byte c, tail byte c), loaded first (L2 hits: the
+  // round just read them), stored after the pieces
+  uint32_t bh = 0, bt = 0, ebt = 0;  // head byte c, tail byte c, the tail byte's offset
+  bool okh = false, okt = false;
+  if (wave_any(fin)) {
+    const uint32_t Pl = (uint32_t)P;  // payload start mod 2^32
+    const uint32_t hb = (16u - (Pl & 15u)) & 15u;  // bytes before the first aligned piece
+    const uint32_t hb_end = hb < sp.n ? hb : sp.n;
+    const uint32_t tb = (Pl + sp.n) & 15u;
+    const uint32_t tb_beg = sp.n - tb > hb_end ? sp.n - tb : hb_end;
+    okh = fin && c < hb_end;
+    ebt = tb_beg + c;
+    okt = fin && ebt < sp.n;
+    bh = *reinterpret_cast<gbl_u8_t*>(okh ? sp.ptr + c : X.zp);
+    bt = *reinterpret_cast<gbl_u8_t*>(okt ? sp.ptr + ebt : X.zp);
+  }
+
   const uint64_t ps = sp.ptr;               // payload in the source
   const uint64_t delta = P - ps;            // (mod 2^64)
   const uint32_t e = (uint32_t)(0ull - delta) & 15u;
   const uint32_t q2 = e & 8u, q1 = e & 4u, be = e & 3u;
-  il_mask(ca, sp, r, c);
   // output piece c + 16 j takes source bytes [x0 + 256 j, + 16), x0 = the
   // round's window start + e + 16 c; whole pieces of the payload only
   // (rel = offset in the payload, 32-bit: fragments are < 4 GiB)
@@ -798,6 +836,16 @@ __device__ __forceinline__ bool wal_il_step(const WalIlCtx& X, const WalIlState&
   const int32_t rel0 = (int32_t)(win + e + 16u * c);
   const int32_t lim = (int32_t)sp.n - 16;
   const uint64_t oa0 = P + (uint64_t)(int64_t)rel0;  // output address of piece c
+  {  // the piece that straddles the previous round and this one: lane 15's
+     // piece 4 of that round waits in the row's LDS slot
+    const int32_t relm = (int32_t)(win + e) - 16;
+    const bool okm = live && !firstr && e != 0 && c == 0 && relm >= 0 && relm <= lim;
+    if (wave_any(okm)) {
+      const uint4 cm = lds_u32x4(X.carry_slot);
+      const uint4 o = il_align(cm, ca.v[0], q2, q1, be);
+      if (okm) st16(P + (uint64_t)(int64_t)relm, o);
+    }
+  }
   uint4 rj = dpp_u32x4<kDppRowRor15>(ca.v[0]);  // lane c + 1's piece j
 #pragma unroll
   for (int j = 0; j < NP; j++) {
@@ -812,46 +860,15 @@ __device__ __forceinline__ bool wal_il_step(const WalIlCtx& X, const WalIlState&
     // piece's DPP moves and selects and spill)
     __builtin_amdgcn_sched_barrier(0);
   }
-  {  // the piece that straddles the previous round and this one: lane 15's
-     // piece 4 of that round waits in the row's LDS slot
-    const int32_t relm = (int32_t)(win + e) - 16;
-    const bool okm = live && !firstr && e != 0 && c == 0 && relm >= 0 && relm <= lim;
-    if (wave_any(okm)) {
-      const uint4 cm = lds_u32x4(X.carry_slot);
-      const uint4 o = il_align(cm, ca.v[0], q2, q1, be);
-      if (okm) st16(P + (uint64_t)(int64_t)relm, o);
-    }
-  }
   if (c == 15) {
     const span_u32x4 cv = {ca.v[NP - 1].x, ca.v[NP - 1].y, ca.v[NP - 1].z, ca.v[NP - 1].w};
     *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(X.carry_slot)) = cv;
   }
   {  // the < 16 payload bytes before the first and after the last full output piece
-    const uint64_t h16 = (P + 15) & ~15ull;
-    const uint64_t t16 = (P + sp.n) & ~15ull;
-    const uint64_t hb_end = h16 < P + sp.n ? h16 : P + sp.n;
-    const uint64_t tb_beg = t16 > hb_end ? t16 : hb_end;
-    const uint64_t oh = P + c, ot = tb_beg + c;
-    const bool okh = fin && oh < hb_end, okt = fin && ot < P + sp.n;
-    const uint32_t bh = *reinterpret_cast<gbl_u8_t*>(okh ? ps + c : X.zp);
-    const uint32_t bt = *reinterpret_cast<gbl_u8_t*>(okt ? ps + (ot - P) : X.zp);
+    const uint64_t oh = P + c, ot = P + ebt;
     if (okh) st_u8(oh, bh);
     if (okt) st_u8(ot, bt);
   }
-
-  // ---- next unit (as crc_rows_step) ----
-  const bool go = live && (!last || A.nt < X.share);
-  const RowSpan nsp = row_span<W, NP>(X.base + (((uint64_t)A.nd.y << 32) | A.nd.x), A.nd.z, A.nd.w, kInitTyped);
-  const bool sw = go && last;
-  B.sp = row_span_sel(sw, nsp, sp);
-  B.r = go ? (last ? nsp.rounds - 1 : r - 1) : r;
-  B.i = sw ? X.sh.idx(A.nt) : A.i;
-  cb = il_load(B.sp, B.r, c, X.zp);
-
-  x = il_round(firstr ? 0u : x, ca, sp, r, c, X.L);
-  uint32_t crc = 0;
-  if (wave_any(fin)) crc = crc_mask(row_finish4<W>(x, sp, X.lf4));
-  if (wave_any(live && !last)) x = il_gap(x, 0u);  // to the lane's piece in the next round
   if (fin && c == 0) st_u32(reinterpret_cast<uint64_t>(X.op.crcs + A.i), crc);
   // trailer padding + header: bytes c + 16 m of [dst - pad, dst + hs)
   const uint64_t hstart = X.obase + A.dst - pad;
