@@ -34,6 +34,8 @@ case "${1:-1}" in
   for wl in wal walwrite blob blockkv kv xxh3 file; do
     bash profiles/run_profile.sh $tag $wl || exit 1
   done
+  bash profiles/run_profile.sh ${tag}_100 blockkv --kv-value-bytes 100 || exit 1
+  PROFILE_SQ=1 bash profiles/run_profile.sh ${tag}_r100 ragged --span-min 100 --span-max 300 || exit 1
   # WAL verify FETCH calibration: the bench image reads every byte once
   # (one kFullType record per 32 KiB block); request counts beside FETCH_SIZE
   d=gpurun_out/prof_${tag}_wal

@@ -1,10 +1,10 @@
 #!/usr/bin/env python3
 """Copy one round's GPU-box profile output into the tracked profiles/ tree.
 
-  python profiles/collect.py <tag>
+  python profiles/collect.py <tag> [<dest, default tag>]
 
-gpurun_out/bench_<tag>/<wl>.json     -> profiles/<tag>/bench_<wl>.json
-gpurun_out/prof_<tag>_<wl>/          -> profiles/<tag>/<wl>/
+gpurun_out/bench_<tag>/<wl>.json     -> profiles/<dest>/bench_<wl>.json
+gpurun_out/prof_<tag>_<wl>/          -> profiles/<dest>/<wl>/
     trace/trace_kernel_stats.csv, trace/trace_domain_stats.csv (as is)
     trace/trace_kernel_trace.csv     -> trace_mck_kernels.csv (engine kernels only)
     pmc_*/pmc_counter_collection.csv -> pmc_fetch_mck.csv / pmc_write_mck.csv
@@ -43,7 +43,8 @@ def filter_csv(src, dst, keep_cols=None):
 
 def main():
     tag = sys.argv[1]
-    dst_root = os.path.join(HERE, tag)
+    dest = sys.argv[2] if len(sys.argv) > 2 else tag
+    dst_root = os.path.join(HERE, dest)
     os.makedirs(dst_root, exist_ok=True)
     bdir = os.path.join(OUT, f"bench_{tag}")
     if os.path.isdir(bdir):
@@ -81,7 +82,7 @@ def main():
         if os.path.exists(t):
             with open(t) as f:
                 tr = json.load(f)
-            tr["source"] = f"profiles/{tag}/{wl} (rocprofv3 run of profiles/run_profile.sh {tag} {wl})"
+            tr["source"] = f"profiles/{dest}/{wl} (rocprofv3 run of profiles/run_profile.sh {tag} {wl})"
             for p in (os.path.join(dst, "traffic.json"), os.path.join(HERE, f"traffic_{wl}.json")):
                 with open(p, "w") as f:
                     json.dump(tr, f, indent=1)
