@@ -28,6 +28,8 @@ declare -A ARGS=(
   [kv1000]="--workload blockkv --kv-value-bytes 1000"
   [walwrite]="--workload walwrite"
   [wal]="--workload wal"
+  [crc]="--workload crc32c"
+  [file]="--workload file"
 )
 B="timeout -k 10 180 python -u bench.py --cpu-seconds 0 --steps 20 --warmup 20"
 V=$PWD/microbench/_variants
