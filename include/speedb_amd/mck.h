@@ -713,6 +713,47 @@ int mck_sst_list_blocks(const void* file, uint64_t file_size,
                         mck_sst_footer* footer, mck_sst_block* blocks,
                         uint64_t cap, uint64_t* nblocks);
 
+/* A compressed block's contents, supplied by the caller: called by
+ * mck_sst_list_blocks_uncompress for every block the lister must read (index,
+ * index partitions, filter partition index, metaindex, properties) whose
+ * trailer names a compression type -- enable_index_compression is on by
+ * default (include/rocksdb/table.h:541).  raw / raw_size = the stored payload
+ * (the 5-byte trailer excluded), block_offset = its handle offset.  On MCK_OK
+ * *out / *out_size are the uncompressed contents, valid until the listing call
+ * returns (the callback's owner keeps them).  The reference-side callback is
+ * UncompressBlockData (table/format.h:412) with the table's dictionary
+ * (integration/rocksdb_adapters.h UncompressWithReference).  Any other return
+ * value fails the listing with that code. */
+typedef int (*mck_sst_uncompress_fn)(void* ctx, uint8_t compression_type,
+                                     uint64_t block_offset, const void* raw,
+                                     uint64_t raw_size, const void** out,
+                                     uint64_t* out_size);
+
+/* mck_sst_list_blocks for tables with compressed index / meta blocks: each is
+ * uncompressed by `uncompress` (NULL = MCK_ENOTSUP, as mck_sst_list_blocks)
+ * and then parsed as usual (table/block_based/block_based_table_reader.cc:
+ * 2336-2412 reads the index through the block cache, i.e. uncompressed).
+ * The listed handles, sizes and kinds are those of the stored blocks, which
+ * is what mck_sst_verify_batch checks. */
+int mck_sst_list_blocks_uncompress(const void* file, uint64_t file_size,
+                                   mck_sst_uncompress_fn uncompress, void* ctx,
+                                   mck_sst_footer* footer, mck_sst_block* blocks,
+                                   uint64_t cap, uint64_t* nblocks);
+
+/* The block handles ONE uncompressed index block lists, for a reader that
+ * already holds the index contents (IndexBlockIter, table/block_based/
+ * block.cc: every entry's value is an IndexValue -- a full BlockHandle, or
+ * with value_delta_encoded and shared != 0 the varsigned size delta after the
+ * previous handle -- followed, for index_type 3 (kBinarySearchWithFirstKey),
+ * by the length-prefixed first key).  Every output handle gets `kind`
+ * (MCK_SST_BLOCK_DATA for a single-level index or a partition,
+ * MCK_SST_BLOCK_INDEX_PARTITION for a two-level index's top level).  out =
+ * NULL queries the count (*n). */
+int mck_sst_index_handles(const void* contents, uint64_t size,
+                          int value_delta_encoded, uint32_t index_type,
+                          int kind, mck_sst_block* out, uint64_t cap,
+                          uint64_t* n);
+
 /* table/format.cc:405-440: check the format_version 6 footer checksum of the
  * 53 footer bytes (host memory); 0 for older formats / kNoChecksum.  The
  * blocks themselves are verified with ONE mck_sst_verify_batch over the

@@ -136,6 +136,9 @@ SIGNATURES = [
       ctypes.c_uint64, vp, vp, vp, vp, vp, vp, vp]),
     ("mck_sst_decode_footer", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint64, vp]),
     ("mck_sst_list_blocks", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, ctypes.c_uint64, vp]),
+    ("mck_sst_list_blocks_uncompress", ctypes.c_int, [vp, ctypes.c_uint64, vp, vp, vp, vp, ctypes.c_uint64, vp]),
+    ("mck_sst_index_handles", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_int, ctypes.c_uint32, ctypes.c_int, vp,
+                                             ctypes.c_uint64, vp]),
     ("mck_sst_verify_footer", ctypes.c_int, [vp, vp]),
     ("mck_wal_plan", ctypes.c_int,
      [vp, vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, vp, ctypes.c_uint64, vp, vp, vp]),

@@ -19,8 +19,10 @@
 //                                             block_based_table_factory.cc:1141-1143
 //   VerifyChecksum / VerifyChecksumInBlocks / VerifyChecksumInMetaBlocks
 //                                             table/block_based/block_based_table_reader.cc:2336-2500
-// Compressed index / meta blocks cannot be parsed here (no decompressor in
-// this engine): they are reported as MCK_ENOTSUP.
+// Compressed index / meta blocks are not decompressed here (the codecs are
+// the reference's): mck_sst_list_blocks reports them as MCK_ENOTSUP, and
+// mck_sst_list_blocks_uncompress hands each to the caller's callback (the
+// reference's UncompressBlockData) and parses what it returns.
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -101,18 +103,31 @@ struct Entry {
 
 class File {
  public:
-  File(const uint8_t* d, uint64_t n) : d_(d), n_(n) {}
+  File(const uint8_t* d, uint64_t n, mck_sst_uncompress_fn fn = nullptr, void* ctx = nullptr)
+      : d_(d), n_(n), fn_(fn), ctx_(ctx) {}
 
-  // The payload of block `h` (trailer follows).  Compressed blocks cannot be
-  // parsed here.
+  // The contents of block `h` (trailer follows): the stored payload, or for
+  // a compressed block what the caller's uncompress callback returns.
   int payload(const Handle& h, const char* what, Slice* out) const {
     if (h.offset > n_ || h.size > n_ - h.offset || n_ - h.offset - h.size < kBlockTrailerSize)
       return fail(MCK_ECORRUPT, "%s block handle (offset %llu, size %llu) is past the end of the file (%llu bytes)",
                   what, (unsigned long long)h.offset, (unsigned long long)h.size, (unsigned long long)n_);
     const uint8_t type = d_[h.offset + h.size];
-    if (type != 0)
-      return fail(MCK_ENOTSUP, "%s block at offset %llu is compressed (type %u): cannot be parsed on the host", what,
-                  (unsigned long long)h.offset, type);
+    if (type != 0) {
+      if (!fn_)
+        return fail(MCK_ENOTSUP, "%s block at offset %llu is compressed (type %u): cannot be parsed on the host", what,
+                    (unsigned long long)h.offset, type);
+      const void* u = nullptr;
+      uint64_t un = 0;
+      const int rc = fn_(ctx_, type, h.offset, d_ + h.offset, h.size, &u, &un);
+      if (rc != MCK_OK)
+        return fail(rc, "%s block at offset %llu: uncompress callback failed (type %u, rc %d)", what,
+                    (unsigned long long)h.offset, type, rc);
+      if (!u && un) return fail(MCK_EINVAL, "%s block at offset %llu: uncompress callback returned NULL", what,
+                                (unsigned long long)h.offset);
+      *out = Slice{static_cast<const uint8_t*>(u), un};
+      return MCK_OK;
+    }
     *out = Slice{d_ + h.offset, h.size};
     return MCK_OK;
   }
@@ -204,6 +219,8 @@ class File {
 
   const uint8_t* d_;
   uint64_t n_;
+  mck_sst_uncompress_fn fn_;
+  void* ctx_;
 };
 
 bool starts_with(const std::string& s, const char* p) { return s.compare(0, strlen(p), p) == 0; }
@@ -283,12 +300,35 @@ int mck_sst_decode_footer(const void* tail, uint64_t tail_len, uint64_t tail_off
 
 int mck_sst_list_blocks(const void* file, uint64_t file_size, mck_sst_footer* footer, mck_sst_block* blocks,
                         uint64_t cap, uint64_t* nblocks) {
+  return mck_sst_list_blocks_uncompress(file, file_size, nullptr, nullptr, footer, blocks, cap, nblocks);
+}
+
+int mck_sst_index_handles(const void* contents, uint64_t size, int value_delta_encoded, uint32_t index_type, int kind,
+                          mck_sst_block* out, uint64_t cap, uint64_t* n) {
+  mck_internal_set_error("");
+  if ((!contents && size) || !n) return fail(MCK_EINVAL, "NULL argument");
+  if (index_type > 3) return fail(MCK_EINVAL, "index_type %u is not a block-based table index type", index_type);
+  std::vector<Handle> hs;
+  if (int rc = File::index_handles(Slice{static_cast<const uint8_t*>(contents), size}, value_delta_encoded != 0,
+                                   index_type == 3, "index", &hs))
+    return rc;
+  *n = hs.size();
+  if (out) {
+    if (cap < hs.size())
+      return fail(MCK_EINVAL, "capacity %llu < %llu", (unsigned long long)cap, (unsigned long long)hs.size());
+    for (size_t i = 0; i < hs.size(); i++) out[i] = mck_sst_block{hs[i].offset, hs[i].size, kind, 0};
+  }
+  return MCK_OK;
+}
+
+int mck_sst_list_blocks_uncompress(const void* file, uint64_t file_size, mck_sst_uncompress_fn uncompress, void* ctx,
+                                   mck_sst_footer* footer, mck_sst_block* blocks, uint64_t cap, uint64_t* nblocks) {
   mck_internal_set_error("");
   if (!file || !footer || !nblocks) return fail(MCK_EINVAL, "NULL argument");
   const uint8_t* d = static_cast<const uint8_t*>(file);
   const uint64_t tail = file_size < kNewVersionsEncodedLength ? file_size : kNewVersionsEncodedLength;
   if (int rc = mck_sst_decode_footer(d + file_size - tail, tail, file_size - tail, footer)) return rc;
-  File F(d, file_size);
+  File F(d, file_size, uncompress, ctx);
   std::vector<mck_sst_block> out;
   auto add = [&](uint64_t off, uint64_t size, int kind) { out.push_back(mck_sst_block{off, size, kind, 0}); };
 

@@ -71,33 +71,83 @@ def decode_footer(image: bytes) -> mck_sst_footer:
     return f
 
 
-def list_blocks(image: bytes) -> Tuple[mck_sst_footer, List[SstBlock]]:
+# int (*)(void* ctx, uint8_t type, uint64_t offset, const void* raw, uint64_t
+#        raw_size, const void** out, uint64_t* out_size)  (mck_sst_uncompress_fn)
+UNCOMPRESS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint8, ctypes.c_uint64, ctypes.c_void_p,
+                                 ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64))
+
+
+def list_blocks(image: bytes, uncompress=None) -> Tuple[mck_sst_footer, List[SstBlock]]:
     """Every checksummed block of the SST image (host bytes), in
     VerifyChecksum order: metaindex, meta blocks, index (+ partitions), data,
-    filter partitions."""
+    filter partitions.  ``uncompress(type, offset, raw: bytes) -> bytes``
+    supplies the contents of compressed index / meta blocks
+    (mck_sst_list_blocks_uncompress; the reference's UncompressBlockData in a
+    real integration); without it such a table raises MCK_ENOTSUP.  An
+    exception in the callback fails the listing (MCK_ECORRUPT)."""
     buf = bytes(image)
+    held = []  # the uncompressed blocks, alive until the call returns
+
+    def cb(_ctx, ctype, off, raw, raw_size, out, out_size):
+        try:
+            data = bytes(uncompress(int(ctype), int(off), ctypes.string_at(raw, raw_size)))
+        except Exception:  # the listing reports it; never unwind through C
+            return MCK_ECORRUPT
+        b = ctypes.create_string_buffer(data, max(len(data), 1))
+        held.append(b)
+        out[0] = ctypes.cast(b, ctypes.c_void_p)
+        out_size[0] = len(data)
+        return 0
+
+    fn = UNCOMPRESS_FN(cb) if uncompress is not None else None  # (kept alive for the calls)
+    fnp = ctypes.cast(fn, ctypes.c_void_p) if fn is not None else None
+
+    def call(arr, cap, f, n):
+        held.clear()
+        return lib.mck_sst_list_blocks_uncompress(buf, len(buf), fnp, None, ctypes.addressof(f), arr, cap,
+                                                  ctypes.addressof(n))
+
     f = mck_sst_footer()
     n = ctypes.c_uint64()
-    rc = lib.mck_sst_list_blocks(buf, len(buf), ctypes.addressof(f), None, 0, ctypes.addressof(n))
+    rc = call(None, 0, f, n)
     if rc:
         raise SstError(rc, _err())
     arr = (mck_sst_block * max(n.value, 1))()
-    rc = lib.mck_sst_list_blocks(buf, len(buf), ctypes.addressof(f), ctypes.addressof(arr), n.value,
-                                 ctypes.addressof(n))
+    rc = call(ctypes.addressof(arr), n.value, f, n)
     if rc:
         raise SstError(rc, _err())
     return f, [SstBlock(int(b.offset), int(b.size), BLOCK_KINDS.get(b.kind, str(b.kind)))
                for b in arr[:n.value]]
 
 
+def index_handles(contents: bytes, value_delta_encoded: bool, index_type: int = 0,
+                  kind: str = "data") -> List[SstBlock]:
+    """The handles one uncompressed index block lists (mck_sst_index_handles),
+    for a reader that already holds its contents."""
+    kinds = {v: k for k, v in BLOCK_KINDS.items()}
+    buf = bytes(contents)
+    n = ctypes.c_uint64()
+    rc = lib.mck_sst_index_handles(buf, len(buf), int(bool(value_delta_encoded)), index_type, kinds[kind], None, 0,
+                                   ctypes.addressof(n))
+    if rc:
+        raise SstError(rc, _err())
+    arr = (mck_sst_block * max(n.value, 1))()
+    rc = lib.mck_sst_index_handles(buf, len(buf), int(bool(value_delta_encoded)), index_type, kinds[kind],
+                                   ctypes.addressof(arr), n.value, ctypes.addressof(n))
+    if rc:
+        raise SstError(rc, _err())
+    return [SstBlock(int(b.offset), int(b.size), BLOCK_KINDS.get(b.kind, str(b.kind))) for b in arr[:n.value]]
+
+
 def VerifyChecksum(image: bytes, file_name: str = "", stream=None, device=None,
-                   per_block: Optional[list] = None) -> Status:
+                   per_block: Optional[list] = None, uncompress=None) -> Status:
     """BlockBasedTable::VerifyChecksum of a whole SST image: parse on the
     host, one batched GPU verify of every block.  ``per_block`` (a list)
-    receives (SstBlock, Status) for every block."""
+    receives (SstBlock, Status) for every block; ``uncompress`` as in
+    list_blocks (compressed index / meta blocks)."""
     import torch
     try:
-        f, blocks = list_blocks(image)
+        f, blocks = list_blocks(image, uncompress)
     except SstError as e:
         return e.status
     tail = bytes(image[f.footer_offset:f.footer_offset + 53])
@@ -151,4 +201,4 @@ def VerifyBlocks(image, blocks, checksum_type: int, base_context_checksum: int =
     return first
 
 
-__all__ = ["list_blocks", "decode_footer", "VerifyChecksum", "VerifyBlocks", "SstBlock", "SstError", "BLOCK_KINDS"]
+__all__ = ["list_blocks", "index_handles", "decode_footer", "VerifyChecksum", "VerifyBlocks", "SstBlock", "SstError", "BLOCK_KINDS"]

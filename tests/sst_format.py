@@ -161,6 +161,32 @@ def index_block(handles: List[Tuple[int, int]], keys: List[bytes], delta: bool,
     return build_block(entries, restart_interval, deltas if delta else None)
 
 
+def zlib_block(contents: bytes) -> bytes:
+    """A block as the reference's Zlib_Compress stores it for
+    format_version >= 2 (util/compression.h: compress_format_version 2 =
+    varint32 uncompressed length, then a raw deflate stream; window_bits
+    -14 by default, CompressionOptions)."""
+    import zlib
+    c = zlib.compressobj(6, zlib.DEFLATED, -14)
+    return varint(len(contents)) + c.compress(contents) + c.flush()
+
+
+def zlib_unblock(raw: bytes) -> bytes:
+    """The inverse (UncompressBlockData's kZlibCompression case)."""
+    import zlib
+    n, k, shift = 0, 0, 0
+    while True:
+        b = raw[k]
+        n |= (b & 127) << shift
+        k += 1
+        shift += 7
+        if not b & 128:
+            break
+    out = zlib.decompress(raw[k:], -15)
+    assert len(out) == n
+    return out
+
+
 def write_sst(oracle, *, seed: int = 1, n_data: int = 40, checksum_type: int = 1,
               format_version: int = 5, index_type: int = 0, delta: Optional[bool] = None,
               base_context_checksum: int = 0x5EED1234, partition_size: int = 8,
@@ -170,7 +196,10 @@ def write_sst(oracle, *, seed: int = 1, n_data: int = 40, checksum_type: int = 1
     with shared prefixes), the meta blocks named in ``meta`` ("filter",
     "partitioned_filter", "range_del", "compression_dict"), the index
     (index_type 0 binary search, 1 hash, 2 two-level partitioned, 3 binary
-    search with first key), properties, metaindex and footer."""
+    search with first key), properties, metaindex and footer.  index_comp:
+    the compression type in the index blocks' trailers -- 2 (kZlibCompression)
+    stores them really compressed (zlib_block), any other nonzero type keeps
+    the bytes as they are (opaque to a reader without that codec)."""
     rnd = random.Random(seed)
     if delta is None:
         delta = format_version >= 4
@@ -193,18 +222,22 @@ def write_sst(oracle, *, seed: int = 1, n_data: int = 40, checksum_type: int = 1
         metas[b"partitionedfilter.rocksdb.BuiltinBloomFilter"] = w.write_block(fidx, "filter_partition_index")
     # index (Finish: WriteIndexBlock after the filter)
     fk = first_keys if index_type == 3 else None
+
+    def comp(b: bytes) -> bytes:
+        return zlib_block(b) if index_comp == 2 else b
     if index_type == 2:
         parts = []
         for p in range(0, n_data, partition_size):
             blk = index_block(handles[p:p + partition_size], keys[p:p + partition_size], delta, 4)
-            parts.append((w.write_block(blk, "index_partition", index_comp), keys[min(p + partition_size, n_data) - 1]))
+            parts.append((w.write_block(comp(blk), "index_partition", index_comp),
+                          keys[min(p + partition_size, n_data) - 1]))
         top = index_block([h for h, _ in parts], [k for _, k in parts], delta, 2)
-        index_h = w.write_block(top, "index", index_comp)
+        index_h = w.write_block(comp(top), "index", index_comp)
     else:
         # index_comp != 0: the index block's trailer names a compression
         # type (enable_index_compression); its bytes stay opaque here (no
         # compressor in this image) -- the checksum covers them as stored
-        index_h = w.write_block(index_block(handles, keys, delta, 4, fk), "index", index_comp)
+        index_h = w.write_block(comp(index_block(handles, keys, delta, 4, fk)), "index", index_comp)
     if "compression_dict" in meta:
         metas[b"rocksdb.compression_dict"] = w.write_block(bytes(rnd.getrandbits(8) for _ in range(200)),
                                                             "compression_dict")

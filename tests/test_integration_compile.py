@@ -26,6 +26,10 @@ int main() {
   std::vector<ROCKSDB_NAMESPACE::BlockHandle> hs;
   std::vector<ROCKSDB_NAMESPACE::Status> st;
   (void)A::VerifyBlockChecksums(footer, nullptr, 0, hs, "f", &st);
+  A::UncompressCtx uc{nullptr, 6};
+  mck_sst_footer sf{};
+  uint64_t n = 0;
+  (void)mck_sst_list_blocks_uncompress(nullptr, 0, &A::UncompressWithReference, &uc, &sf, nullptr, 0, &n);
   return g ? 0 : 1;
 }
 """

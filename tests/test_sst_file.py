@@ -150,6 +150,103 @@ def test_compressed_index_is_not_parsed(oracle, index_type):
     assert "compressed" in str(e.value)
 
 
+@pytest.mark.parametrize("fv,it,delta", [(2, 0, False), (5, 0, True), (5, 2, True), (6, 2, True), (6, 3, False),
+                                         (4, 1, True)])
+def test_compressed_index_listed_through_callback(oracle, fv, it, delta):
+    """Tables with zlib-compressed index blocks (and, two-level, compressed
+    partitions): mck_sst_list_blocks_uncompress hands every compressed block
+    the lister reads to the caller's callback -- here the inverse of the
+    reference's Zlib_Compress format; in an integration its
+    UncompressBlockData -- and lists exactly the blocks the writer wrote,
+    with their STORED (compressed) handles."""
+    from sst_format import zlib_unblock
+    from speedb_amd import sst
+    img, layout = write_sst(oracle, seed=fv * 13 + it, format_version=fv, index_type=it, delta=delta, n_data=33,
+                            index_comp=2, meta=("filter", "range_del"))
+    with pytest.raises(sst.SstError) as e:  # no callback: as before
+        sst.list_blocks(img)
+    assert e.value.rc == sst.MCK_ENOTSUP
+    seen = []
+
+    def unz(t, off, raw):
+        assert t == 2
+        seen.append(off)
+        return zlib_unblock(raw)
+
+    f, blocks = sst.list_blocks(img, uncompress=unz)
+    assert _kinds(blocks) == sorted(layout.blocks)
+    assert f.index_type == it and bool(f.index_value_is_delta_encoded) == delta
+    idx = sorted(o for o, _, k in layout.blocks if k in ("index", "index_partition"))
+    # every compressed index block, once per pass (list_blocks: count, then list)
+    assert sorted(set(seen)) == idx and len(seen) == 2 * len(idx)
+
+
+def test_compressed_index_callback_errors(oracle):
+    """A failing callback (an exception in Python; any non-OK return in C)
+    fails the listing with the callback's code, naming the block."""
+    from speedb_amd import sst
+    img, layout = write_sst(oracle, format_version=5, index_type=2, n_data=20, index_comp=2)
+
+    def bad(t, off, raw):
+        raise ValueError("codec missing")
+
+    with pytest.raises(sst.SstError) as e:
+        sst.list_blocks(img, uncompress=bad)
+    assert e.value.rc == sst.MCK_ECORRUPT and "uncompress callback failed" in str(e.value)
+    # garbage "uncompressed" contents are parsed and rejected as a bad index
+    with pytest.raises(sst.SstError) as e:
+        sst.list_blocks(img, uncompress=lambda t, off, raw: b"\xff" * 7)
+    assert e.value.rc == sst.MCK_ECORRUPT
+
+
+@pytest.mark.parametrize("delta,it", [(False, 0), (True, 0), (True, 3), (False, 3)])
+def test_index_handles_of_one_block(delta, it):
+    """mck_sst_index_handles: the handles an already-uncompressed index block
+    lists (IndexBlockIter), full or delta-encoded values, with first keys."""
+    from sst_format import index_block
+    from speedb_amd import sst
+    rnd = random.Random(7)
+    hs, off = [], 0
+    for _ in range(70):
+        n = rnd.randrange(100, 9000)
+        hs.append((off, n))
+        off += n + 5
+    keys = [b"k%06d" % (3 * i + 1) for i in range(len(hs))]
+    fks = [b"k%06d" % (3 * i) for i in range(len(hs))] if it == 3 else None
+    blk = index_block(hs, keys, delta, 4, fks)
+    got = sst.index_handles(blk, delta, it, "data")
+    assert [(b.offset, b.size, b.kind) for b in got] == [(o, n, "data") for o, n in hs]
+    top = sst.index_handles(blk, delta, it, "index_partition")
+    assert all(b.kind == "index_partition" for b in top)
+    with pytest.raises(sst.SstError):
+        sst.index_handles(blk[:-9], delta, it)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fv,index_type", [(5, 2), (6, 0)])
+def test_compressed_index_whole_file_verify(gpu, oracle, fv, index_type):
+    """VerifyChecksum of a table with zlib-compressed index blocks: listed
+    through the callback, every block (the compressed ones included)
+    verified in one GPU batch; a flipped byte in a compressed partition is
+    flagged at exactly that block."""
+    from sst_format import zlib_unblock
+    from speedb_amd import sst
+    img, layout = write_sst(oracle, format_version=fv, index_type=index_type, n_data=40, index_comp=2)
+    unz = lambda t, off, raw: zlib_unblock(raw)  # noqa: E731
+    per = []
+    st = sst.VerifyChecksum(img, "000011.sst", per_block=per, uncompress=unz)
+    assert st.ok(), st.ToString()
+    assert sorted((b.offset, b.size, b.kind) for b, _ in per) == sorted(layout.blocks)
+    tgt = [h for h in sorted(layout.blocks) if h[2] == ("index_partition" if index_type == 2 else "index")][-1]
+    bad = bytearray(img)
+    bad[tgt[0] + tgt[1]] ^= 0x40  # the stored trailer's type byte: the checksum covers it
+    per = []
+    st = sst.VerifyChecksum(bytes(bad), "000011.sst", per_block=per,
+                            uncompress=lambda t, off, raw: zlib_unblock(raw) if t == 2 else
+                            (_ for _ in ()).throw(ValueError(t)))
+    assert not st.ok()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fv,index_type", [(5, 0), (6, 2)])
 def test_compressed_index_low_level_verify(gpu, oracle, fv, index_type):
