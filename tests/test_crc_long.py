@@ -209,6 +209,47 @@ def test_long_sst_verify_mix(gpu, oracle, ctype):
 
 
 @pytest.mark.parametrize("ctype", [1, 4])
+def test_sst_mix_oracle_at_scale(gpu, oracle, ctype):
+    """configs[2]'s shape at scale: ~256 MiB of 4/16/64 KiB + jitter blocks
+    at byte offsets (a compaction's input), every trailer sealed by the
+    ORACLE (the reference's BuiltinChecksumWithLastByte + context modifier,
+    not the engine's write kernel), then one verify batch: no block may
+    mismatch and every computed checksum must equal the oracle's stored one
+    -- bit-exact parity over ~18K blocks, 10x the mix test above."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(4242 + ctype)
+    sizes, total = [], 0
+    while total < (256 << 20):
+        n = rnd.choice([4096] * 6 + [16384] * 3 + [65536]) + rnd.randrange(0, 256)
+        sizes.append(n)
+        total += n
+    pool = splitmix_bytes(7000 + ctype, total)
+    comps = [rnd.choice([0, 1, 7]) for _ in sizes]
+    base_ctx, file_start = 0x1234ABCD, 4096 + 13
+    img = bytearray()
+    offs, pos = [], 0
+    want = []
+    for n, ct in zip(sizes, comps):
+        p = pool[pos:pos + n]
+        pos += n
+        off = len(img)
+        raw = oracle.BuiltinLast(ctype, p, ct)
+        ck = (raw + oracle.ContextModifier(base_ctx, file_start + off)) & 0xFFFFFFFF
+        offs.append(off)
+        want.append(raw)  # computed = the builtin checksum, context removed (format.h:119)
+        img += p + bytes([ct]) + struct.pack("<I", ck)
+    dev = torch.frombuffer(img + bytes(64), dtype=torch.uint8).to("cuda")
+    sp = _spans(torch, S, dev, offs, sizes)
+    foff = torch.tensor([file_start + o for o in offs], dtype=torch.int64, device="cuda")
+    mm, comp, stored, cnt = S.sst_verify_batch(ctype, sp, file_offsets=foff, base_context_checksum=base_ctx)
+    assert int(cnt.item()) == 0 and int(mm.sum().item()) == 0
+    comp = _u32(comp)
+    bad = [i for i in range(len(sizes)) if int(comp[i]) != want[i]]
+    assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("ctype", [1, 4])
 @pytest.mark.parametrize("order", ["file", "shuffled", "reversed"])
 def test_byte_shares_partition_any_order(gpu, oracle, ctype, order):
     """Byte-balanced workgroup shares (share_by_bytes: the sampled multi-level
