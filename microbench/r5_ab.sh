@@ -28,6 +28,8 @@ declare -A ARGS=(
   [kv1000]="--workload blockkv --kv-value-bytes 1000"
   [walwrite]="--workload walwrite"
   [wal]="--workload wal"
+  [r200]="--workload ragged --span-min 200 --span-max 500"
+  [r150]="--workload ragged --span-min 150 --span-max 400"
   [crc]="--workload crc32c"
   [file]="--workload file"
 )

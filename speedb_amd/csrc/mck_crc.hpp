@@ -1120,7 +1120,7 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, const RowShare& sh, 
 // lengths live on the device.)
 constexpr uint32_t kAutoLongMin = 2560;    // mean span bytes
 constexpr uint32_t kAutoRows1Max = 80;     // one lane per span below ~80 B
-constexpr uint32_t kAutoRows4Max = 384;    // 4-lane rows up to 384 B
+constexpr uint32_t kAutoRows4Max = 240;    // 4-lane rows up to 240 B
 constexpr uint32_t kAutoRows8Max = 640;    // 8-lane rows up to 640 B, 16-lane rows above
 template <class Op>
 __device__ __forceinline__ bool crc_share_long(const Op& op, const RowShare& sh) {
@@ -1136,9 +1136,14 @@ __device__ __forceinline__ bool crc_share_long(const Op& op, const RowShare& sh)
 // (one launch per batch; the table image is filled once).  The width is
 // chosen once per share, from its first window's mean span: one lane per
 // span below ~80 B (20-100 B: 0.16-0.19 vs 0.09 of peak on 8-lane rows,
-// whose 512-B rounds are mostly padding there), 4-lane rows up to 384 B
-// (100-300-B spans 0.365 vs 0.345 on 8-lane rows; 300-700 B 0.427 vs 0.444,
-// profiles/r4/rows), 8-lane rows up to 640 B, 16-lane rows above.  (The window loop sits inside each width's branch: a
+// whose 512-B rounds are mostly padding there), 4-lane rows up to 240 B,
+// 8-lane rows up to 640 B, 16-lane rows above.  Round 5's sweep with every
+// width forced (microbench/rows_width.py, profiles/r5/rows_width/): 4-lane
+// rows win at a 200-B mean (100-300 B: 0.421 vs 0.386) but 8-lane rows from
+// ~275 B on (150-400 B 0.489 vs 0.450, 250-350 B 0.511 vs 0.454, 200-500 B
+// 0.555 vs 0.458: round 4's 384-B bound was too high); 8 vs 16 lanes
+// depends on the spread around a 600-700-B mean (400-800 B: 16 lanes 0.534
+// vs 0.519; 100-1100 B WAL records: 8 lanes 0.511 vs 0.492).  (The window loop sits inside each width's branch: a
 // loop around all four widths kept every width's lane constants live and
 // spilled 76-132 B per lane.)  force: 0 = by length, 2 = rows16, 3 = rows8,
 // 5 = rows4, 6 = one lane per span (test hook).
