@@ -30,6 +30,9 @@ declare -A ARGS=(
   [wal]="--workload wal"
   [r200]="--workload ragged --span-min 200 --span-max 500"
   [r150]="--workload ragged --span-min 150 --span-max 400"
+  [r2k]="--workload ragged --span-min 2000 --span-max 3000"
+  [r3k]="--workload ragged --span-min 2500 --span-max 3500"
+  [r4k]="--workload ragged --span-min 3500 --span-max 4500"
   [crc]="--workload crc32c"
   [file]="--workload file"
 )

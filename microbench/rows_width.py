@@ -2,7 +2,7 @@
 byte offsets, 100-300-B spans, 300-700-B spans): the same batch with every
 share forced to one row width through the engine's test hook
 (mck_test_set_crc_driver: 6 = one lane per span, 5 = 4-lane rows, 3 = 8-lane,
-2 = 16-lane, 0 = the by-length choice), kernel time from HIP events, best of 20.  Prints one JSON
+2 = 16-lane, 7 = the body/head driver, 0 = the by-length choice), kernel time from HIP events, best of 20.  Prints one JSON
 line per shape: fraction of 8 TB/s per width (same accounting as bench.py:
 span bytes + 16 B descriptor/output per span, +1 type byte for WAL records).
 
@@ -69,7 +69,7 @@ def main():
             fn()
         torch.cuda.synchronize()
         for rep in range(2):  # two passes; the best of each width
-            for name, drv in (("auto", 0), ("rows1", 6), ("rows4", 5), ("rows8", 3), ("rows16", 2)):
+            for name, drv in (("auto", 0), ("rows1", 6), ("rows4", 5), ("rows8", 3), ("rows16", 2), ("bh", 7)):
                 _lib.check(_lib.lib.mck_test_set_crc_driver(drv, 0), "mck_test_set_crc_driver")
                 ms = timed(fn)
                 got = out.clone()

@@ -1114,11 +1114,16 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, const RowShare& sh, 
 // ---------------------------------------------------------------------------
 // Ragged batches: one kernel over the whole batch (k_crc_ragged), contiguous
 // shares, and every workgroup runs its share on the row drivers (below) when
-// the share's spans average at most kAutoLongMin bytes, else on the
+// the share's spans average less than kAutoLongMin bytes, else on the
 // body/head driver (mck_crc_bh.hpp).  The choice is made from a fixed sample
 // of the share's lengths (crc_share_long).  (The host cannot choose: ragged
-// lengths live on the device.)
-constexpr uint32_t kAutoLongMin = 2560;    // mean span bytes
+// lengths live on the device.)  4096: below one whole 4 KiB round a span is
+// all head to the body/head driver, whose heads run on 4-lane rows -- spans
+// of 2000-4000 B measured 0.44-0.45 there against 0.59-0.64 on 16-lane rows,
+// while from 4 KiB + jitter on the body/head driver wins (4100-4400 B 0.739
+// vs 0.576, 4096 B 0.819 vs 0.642; microbench/rows_width.py,
+// profiles/r5/rows_width/sweep3.txt, sweep4.txt; round 4's bound was 2560).
+constexpr uint32_t kAutoLongMin = 4096;    // mean span bytes
 constexpr uint32_t kAutoRows1Max = 80;     // one lane per span below ~80 B
 constexpr uint32_t kAutoRows4Max = 240;    // 4-lane rows up to 240 B
 constexpr uint32_t kAutoRows8Max = 640;    // 8-lane rows up to 640 B, 16-lane rows above
@@ -1129,7 +1134,7 @@ __device__ __forceinline__ bool crc_share_long(const Op& op, const RowShare& sh)
   uint64_t len = 0;
   if (lane < m) len = op.len(sh.idx((uint32_t)((uint64_t)lane * sh.n / m)));
   for (int d = 32; d >= 1; d >>= 1) len += __shfl_xor(len, d, 64);
-  return len > (uint64_t)kAutoLongMin * m;
+  return len >= (uint64_t)kAutoLongMin * m;
 }
 
 // The row drivers over a share, in windows of at most kRowDescCache spans
