@@ -927,6 +927,10 @@ int mck_test_set_virtual_devices(int k);
  * refused); interleaved != 0 deals spans to workgroups round-robin (row
  * drivers only) instead of in contiguous ranges.  Process-wide. */
 int mck_test_set_crc_driver(int driver, int interleaved);
+/* Test hook: the XXH3 driver for every batch -- 0 = by batch shape (rows for
+ * uniform batches, a wave per span for ragged ones), 1 = a wave per span,
+ * 2 = 16-lane rows.  Production code never calls it. */
+int mck_test_set_xxh3_driver(int driver);
 
 #ifdef __cplusplus
 }

@@ -172,6 +172,7 @@ SIGNATURES = [
     ("mck_host_pipeline_release", None, []),
     ("mck_statistics_get", ctypes.c_int, [vp, ctypes.c_int]),
     ("mck_test_set_crc_driver", ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+    ("mck_test_set_xxh3_driver", ctypes.c_int, [ctypes.c_int]),
     ("mck_test_set_virtual_devices", ctypes.c_int, [ctypes.c_int]),
     ("mck_set_perf_level", ctypes.c_int, [ctypes.c_int]),
     ("mck_get_perf_level", ctypes.c_int, []),

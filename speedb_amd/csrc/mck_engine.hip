@@ -324,12 +324,17 @@ bool is_uniform_aligned(const mck_spans* s) {
 // row gets the same work; measured 5495 vs 4849 GiB/s at 1M x 4 KiB),
 // one wave per span for ragged batches (a long span is not serialised on one
 // row and waves balance better: SST verify mix 3287 vs 2752 GiB/s).
+// (test hook: mck_test_set_xxh3_driver -- 1 = the wave driver, 2 = rows,
+// for any batch; production code never calls it)
+std::atomic<int> g_x3_force{0};
 template <class Op>
 int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform) {
   if (!count) return MCK_OK;
   int ncu;
   int rc = current_device(nullptr, &ncu);
   if (rc) return rc;
+  const int force = g_x3_force.load(std::memory_order_relaxed);
+  if (force) uniform = force == 2;
   if (!uniform) {
     // one workgroup per CU, spans dealt by LDS tickets
     const uint32_t grid = std::min<uint32_t>((uint32_t)ncu, (count + 3) / 4);
@@ -1670,6 +1675,16 @@ int mck_perf_context_get(mck_perf_context* out, int reset) {
   out->block_checksum_batches = t_perf.batches;
   if (reset) t_perf.time_ns = t_perf.count = t_perf.batches = 0;
   return rc;
+}
+
+int mck_test_set_xxh3_driver(int driver) {
+  t_err[0] = 0;
+  if (driver < 0 || driver > 2) {
+    set_err("driver must be 0 (by batch shape), 1 (wave per span) or 2 (16-lane rows)");
+    return MCK_EINVAL;
+  }
+  g_x3_force.store(driver, std::memory_order_relaxed);
+  return MCK_OK;
 }
 
 int mck_test_set_crc_driver(int driver, int interleaved) {

@@ -408,7 +408,8 @@ struct X3Span {
 // on the row's first lane on the way).  Op: base(), off(i), hlen(i),
 // finish(i, h) (called by lane j == 0 of the row).  Returns false when the
 // row has no spans left.
-template <class Op, bool PREVIEW>
+// (SKIP_SHORT: the caller already hashed the short spans, one per lane)
+template <class Op, bool PREVIEW, bool SKIP_SHORT = false>
 __device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t count, uint32_t stride,
                                              const X3Row& X, X3Span& rs) {
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
@@ -427,7 +428,7 @@ __device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t 
       rs.i = i;
       return true;
     }
-    if (X.j == 0) {
+    if (!SKIP_SHORT && X.j == 0) {
       const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr);
       op.finish(i, PREVIEW ? xxph3_short(p, len, X.seed) : xxh3_short(p, len));
     }
@@ -932,6 +933,24 @@ __device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, c
   }
 }
 
+// Shares of spans that average 256 B - 2.5 KiB run on 16-lane rows inside
+// the wave kernel (xxh3_rows_loop, as k_xxh3): the wave units' 4 KiB rounds
+// are mostly padding there -- ragged 300-700 B 0.407 vs 0.153 of peak,
+// 500-1500 B 0.456 vs 0.275, 1000-3000 B 0.554 vs 0.464; from ~3 KiB the
+// wave units win (2000-4000 B 0.636 vs 0.590, SST-sized 4 KiB + jitter
+// 0.733 vs 0.628; microbench/x3_width.py, profiles/r5/x3_width/).  Chosen
+// per workgroup from a sample of its share's lengths, as crc_share_long.
+constexpr uint32_t kX3RowsMin = 256, kX3RowsMax = 2560;  // mean span bytes
+template <class Op>
+__device__ __forceinline__ bool x3_share_rows(const Op& op, uint32_t lo, uint32_t hi) {
+  const uint32_t n = hi - lo, lane = threadIdx.x & 63;
+  const uint32_t m = n < 64 ? n : 64u;
+  uint64_t len = 0;
+  if (lane < m) len = op.hlen(lo + (uint32_t)((uint64_t)lane * n / m));
+  for (int d = 32; d >= 1; d >>= 1) len += __shfl_xor(len, d, 64);
+  return m != 0 && len >= (uint64_t)kX3RowsMin * m && len < (uint64_t)kX3RowsMax * m;
+}
+
 // Workgroup b's share: a byte-balanced contiguous range (share_by_bytes),
 // staged in windows of kX3DescCache spans, long spans in pieces.
 template <class Op, bool PREVIEW>
@@ -946,6 +965,24 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
   share_by_bytes(op, 0u, count, 0xFFFFFFFFu, &s.wsum[0], &lo, &hi,
                  [&](uint32_t i) { return (uint32_t)op.off(i) ^ (uint32_t)op.hlen(i); },
                  [&] { X = x3_row(seed); });
+  if (x3_share_rows(op, lo, hi)) {  // workgroup-uniform
+    const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {  // short spans, one per lane
+      const uint64_t len = op.hlen(i);
+      if (len <= 240) {
+        const uint8_t* p = reinterpret_cast<const uint8_t*>(base + op.off(i));
+        op.finish(i, PREVIEW ? xxph3_short(p, len, seed) : xxh3_short(p, len));
+      }
+    }
+    const uint32_t rows = wpb * 4, row = wid * 4 + (uint32_t)X.row;
+    // idle rows keep loading from a valid address: the batch's base
+    X3Span rs{base, 0, 0, 0, 0, 0, false};
+    const bool act = x3_next_long<Op, PREVIEW, true>(op, lo + row, hi, rows, X, rs);
+    xxh3_rows_loop<Op, PREVIEW>(op, X, rs, act, [&](X3Span& r) {
+      return x3_next_long<Op, PREVIEW, true>(op, r.i + rows, hi, rows, X, r);
+    });
+    return;
+  }
   const uint32_t start = lo, stride = 1, n = hi - lo;
   for (uint32_t w0 = 0; w0 < n; w0 += kX3DescCache) {
     const uint32_t wn = n - w0 < kX3DescCache ? n - w0 : kX3DescCache;

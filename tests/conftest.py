@@ -22,7 +22,8 @@ GOLDEN = os.path.join(REPO, "tests", "golden")
 
 
 # Child pytest processes of the forced-driver tests set these; the engine
-# itself reads no environment (mck_test_set_crc_driver is its test hook).
+# itself reads no environment (mck_test_set_crc_driver / mck_test_set_xxh3_driver
+# are its test hooks).
 CRC_DRIVERS = {"rows16": 2, "rows8": 3, "rows4": 5, "rows1": 6, "bh": 7, "small": 9}
 
 
@@ -31,7 +32,8 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
     drv = os.environ.get("SPEEDB_AMD_TEST_CRC_DRIVER")
     order = os.environ.get("SPEEDB_AMD_TEST_CRC_ORDER")
-    if drv or order:
+    x3 = os.environ.get("SPEEDB_AMD_TEST_X3_DRIVER")
+    if drv or order or x3:
         import sys
         if REPO not in sys.path:
             sys.path.insert(0, REPO)
@@ -43,6 +45,7 @@ def pytest_configure(config):
         from speedb_amd import _lib
         _lib.check(_lib.lib.mck_test_set_crc_driver(CRC_DRIVERS.get(drv, 0), 1 if order == "interleaved" else 0),
                    "mck_test_set_crc_driver")
+        _lib.check(_lib.lib.mck_test_set_xxh3_driver({"wave": 1, "rows": 2}.get(x3, 0)), "mck_test_set_xxh3_driver")
 
 
 def _bind(lib, prefix):

@@ -70,15 +70,21 @@ def _forced(env):
     assert " passed" in r.stdout
 
 
-@pytest.mark.parametrize("mode", ["rows16", "rows8", "rows4", "rows1", "bh", "small", "interleaved"])
+@pytest.mark.parametrize("mode", ["rows16", "rows8", "rows4", "rows1", "bh", "small", "interleaved", "x3rows",
+                                  "x3wave"])
 def test_auto_kernel_forced_drivers_subprocess(gpu, mode):
     """k_crc_ragged with each driver forced for every workgroup (its choice is
     by mean length, so a parity test of mixed lengths may exercise only one):
     short spans, 0-byte spans, WAL / blob / SST ops on every driver; and the
     interleaved span order instead of contiguous ranges.  "small": the
     wave-per-span path for every share it accepts (<= 16 spans of <= 16 KiB),
-    in batches of any size -- by default only batches of <= 64 spans."""
-    if os.environ.get("SPEEDB_AMD_TEST_CRC_DRIVER") or os.environ.get("SPEEDB_AMD_TEST_CRC_ORDER"):
+    in batches of any size -- by default only batches of <= 64 spans.
+    "x3rows" / "x3wave": every XXH3 batch (ragged or uniform) on the 16-lane
+    rows kernel / the wave kernel (which itself takes rows for shares of
+    256 B - 2.5 KiB spans)."""
+    if (os.environ.get("SPEEDB_AMD_TEST_CRC_DRIVER") or os.environ.get("SPEEDB_AMD_TEST_CRC_ORDER")
+            or os.environ.get("SPEEDB_AMD_TEST_X3_DRIVER")):
         pytest.skip("already running a forced driver")
     _forced({"SPEEDB_AMD_TEST_CRC_ORDER": "interleaved"} if mode == "interleaved"
+            else {"SPEEDB_AMD_TEST_X3_DRIVER": mode[2:]} if mode.startswith("x3")
             else {"SPEEDB_AMD_TEST_CRC_DRIVER": mode})
