@@ -33,6 +33,10 @@ declare -A ARGS=(
   [r2k]="--workload ragged --span-min 2000 --span-max 3000"
   [r3k]="--workload ragged --span-min 2500 --span-max 3500"
   [r4k]="--workload ragged --span-min 3500 --span-max 4500"
+  [x3u]="--workload xxh3"
+  [x3u16k]="--workload xxh3 --block-bytes 16384 --blocks 65536"
+  [x3u64k]="--workload xxh3 --block-bytes 65536 --blocks 16384"
+  [x3u2k]="--workload xxh3 --block-bytes 2048 --blocks 524288"
   [crc]="--workload crc32c"
   [file]="--workload file"
 )

@@ -320,19 +320,29 @@ bool is_uniform_aligned(const mck_spans* s) {
          (reinterpret_cast<uintptr_t>(s->base) & 15u) == 0;
 }
 
-// XXH3 driver choice: one 16-lane row per span for uniform batches (every
-// row gets the same work; measured 5495 vs 4849 GiB/s at 1M x 4 KiB),
-// one wave per span for ragged batches (a long span is not serialised on one
-// row and waves balance better: SST verify mix 3287 vs 2752 GiB/s).
+// XXH3 driver choice: one 16-lane row per span for uniform batches of short
+// spans (every row gets the same work; round 1 measured 5495 vs 4849 GiB/s
+// at 1M x 4 KiB, before the wave kernel's byte-balanced shares and prologue
+// overlap -- it now wins from ~3 KiB, below), one wave per span for ragged
+// batches (a long span is not serialised on one row and waves balance
+// better: SST verify mix 3287 vs 2752 GiB/s; the wave kernel itself runs
+// rows for shares of 256 B - 2.5 KiB spans).
 // (test hook: mck_test_set_xxh3_driver -- 1 = the wave driver, 2 = rows,
 // for any batch; production code never calls it)
 std::atomic<int> g_x3_force{0};
+// Uniform batches of spans of >= kX3UniformWaveMin bytes go to the wave
+// kernel too (round 5, microbench/x3_width.py u:<len>, profiles/r5/x3_width/
+// uniform.txt: 4 KiB 0.827 vs 0.761 on rows, 16 KiB 0.801 vs 0.685; 1-2 KiB
+// stay on rows, 0.774-0.815 vs 0.721-0.768).
+constexpr uint32_t kX3UniformWaveMin = 3072;
 template <class Op>
-int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform) {
+int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform, uint32_t uniform_len = 0) {
   if (!count) return MCK_OK;
   int ncu;
   int rc = current_device(nullptr, &ncu);
   if (rc) return rc;
+  // (small batches keep the rows kernel: no share search in their latency)
+  if (uniform && uniform_len >= kX3UniformWaveMin && count >= 16u * (uint32_t)ncu) uniform = false;
   const int force = g_x3_force.load(std::memory_order_relaxed);
   if (force) uniform = force == 2;
   if (!uniform) {
@@ -378,7 +388,7 @@ int launch_block(int type, const BlockArgs& a, uint32_t count, hipStream_t st, i
     case MCK_kCRC32c:
       return launch_crc(OpCrcBlock<MODE>{a}, count, st, dev, ncu);
     case MCK_kXXH3:
-      return launch_xxh3(OpX3Block<MODE>{a}, count, st, a.s.lengths == nullptr);
+      return launch_xxh3(OpX3Block<MODE>{a}, count, st, a.s.lengths == nullptr, a.s.length);
     case MCK_kxxHash:
       return launch_legacy(OpLegacyBlock<false, MODE>{a}, count, st);
     case MCK_kxxHash64:
@@ -781,7 +791,7 @@ int mck_xxh3_64_batch(const mck_spans* spans, uint64_t* out, mck_stream_t stream
     return MCK_EINVAL;
   }
   return launch_xxh3(OpX3Value{to_src(spans), out}, spans->count, reinterpret_cast<hipStream_t>(stream),
-                     spans->lengths == nullptr);
+                     spans->lengths == nullptr, spans->length);
 }
 
 int mck_xxh32_batch(const mck_spans* spans, uint32_t seed, uint32_t* out, mck_stream_t stream) {
