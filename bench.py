@@ -160,7 +160,6 @@ def parse():
 
 
 # whole-round uniform CRC kernel (row-transposed, non-temporal loads)
-CRC_UNIFORM_FULL = "mck::k_crc_uniform<mck::OpCrcValue, true, true>"
 
 
 def _cpu_quota():
@@ -258,9 +257,10 @@ def cpu_baseline(args, kind, block, sample, gpu_results):
 
 
 def _ragged(op, mean_len):
-    """The kernel that does a ragged CRC batch's work: k_crc_ragged, one
-    launch; its workgroups run the body/head driver for spans averaging more
-    than 2.5 KiB, the row drivers otherwise (mean_len: the label once named
+    """The kernel that does a ragged (or, since round 5, uniform) CRC
+    batch's work: k_crc_ragged, one launch; its workgroups run the body/head
+    driver for spans averaging 4 KiB or more, the row drivers otherwise
+    (mean_len: the label once named
     the kernel per driver; the 4th template argument is the small-batch
     instance's flag, false for every batch of more than 64 spans)."""
     return f"mck::k_crc_ragged<{op}, true, true, false>"
@@ -301,13 +301,17 @@ def make_workload(args, dev, rank, world):
         out64 = torch.empty(count, dtype=torch.int64, device=dev)
         if args.workload == "crc32c":
             w.step = lambda: S.crc32c_batch(spans, out=out32, stream=stream)
-            # 16-byte-multiple blocks: the whole-round uniform kernel; any
-            # other size (a 4300-B SST block): the ragged path
-            w.kernel = CRC_UNIFORM_FULL if block % 4096 == 0 else _ragged("mck::OpCrcValueZ", block)
+            # every block size on the ragged kernel (round 5 retired the
+            # uniform-batch kernel: the body/head and row drivers were faster)
+            w.kernel = _ragged("mck::OpCrcValueZ", block)
             w.alg_bytes = count * (block + 4)
         else:
             w.step = lambda: S.xxh3_64_batch(spans, out=out64, stream=stream)
-            w.kernel = "mck::k_xxh3<mck::OpX3Value>"
+            # uniform batches of >= 3 KiB spans (and >= 16 per CU) run on the
+            # wave kernel since round 5 (mck_engine.hip kX3UniformWaveMin)
+            ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+            w.kernel = ("mck::k_xxh3_wave<mck::OpX3Value>" if block >= 3072 and count >= 16 * ncu
+                        else "mck::k_xxh3<mck::OpX3Value>")
             w.alg_bytes = count * (block + 8)
         w.span_bytes = count * block
         w.desc = (f"{args.workload} over {count} x {block} B random blocks per GPU, device-resident" +
@@ -430,7 +434,8 @@ def make_workload(args, dev, rank, world):
             if world > 1:  # the one real exchange: (crc, length) per rank
                 res["crc"] = shard.combine_span_crcs(out, nbytes, dev)
         w.step = step
-        w.kernel = CRC_UNIFORM_FULL
+        # 64 KiB pieces on k_crc_ragged (body/head), then k_crc_combine
+        w.kernel = _ragged("mck::OpCrcValueZ", 65536)
         w.span_bytes = nbytes
         w.alg_bytes = (nbytes // 65536) * (65536 + 4)
         w.desc = (f"whole-file CRC32C (FileChecksumGenCrc32c, util/file_checksum_helper.h) of a "

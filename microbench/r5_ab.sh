@@ -37,6 +37,13 @@ declare -A ARGS=(
   [x3u16k]="--workload xxh3 --block-bytes 16384 --blocks 65536"
   [x3u64k]="--workload xxh3 --block-bytes 65536 --blocks 16384"
   [x3u2k]="--workload xxh3 --block-bytes 2048 --blocks 524288"
+  [cu512]="--workload crc32c --block-bytes 512 --blocks 2097152"
+  [cu1k]="--workload crc32c --block-bytes 1024 --blocks 1048576"
+  [cu2k]="--workload crc32c --block-bytes 2048 --blocks 524288"
+  [cu16k]="--workload crc32c --block-bytes 16384 --blocks 65536"
+  [r512u]="--workload ragged --span-min 512 --span-max 512"
+  [r1ku]="--workload ragged --span-min 1024 --span-max 1024"
+  [r2ku]="--workload ragged --span-min 2048 --span-max 2048"
   [crc]="--workload crc32c"
   [file]="--workload file"
 )

@@ -554,91 +554,11 @@ typedef __attribute__((address_space(3))) uint64_t lds_u64_t;
 __device__ __forceinline__ lds_u32_t* lds_p32(uint32_t off) { return reinterpret_cast<lds_u32_t*>(static_cast<size_t>(off)); }
 __device__ __forceinline__ lds_u64_t* lds_p64(uint32_t off) { return reinterpret_cast<lds_u64_t*>(static_cast<size_t>(off)); }
 
-// ---------------------------------------------------------------------------
-// Uniform batches: every span has the same 16-byte-multiple length and a
-// 16-byte-aligned start (base + i * stride).  All span geometry is then
-// batch-constant and precomputed on the host; FULL = length is a multiple of
-// the 4 KiB round (owner 0, nothing to zero or clamp).
-struct CrcUniform {
-  uint64_t stride;
-  uint32_t length;
-  int32_t rounds;
-  int32_t owner;
-  uint32_t hb;
-  uint32_t inj;  // unshift(~0, hb): Value's init state at the owner's chunk start
-};
-
-template <bool FULL>
-__device__ __forceinline__ CrcSpan crc_uniform_span(uint64_t base, uint32_t i, const CrcUniform& U) {
-  CrcSpan sp;
-  sp.ptr = base + (uint64_t)i * U.stride;
-  sp.a0 = sp.ptr;
-  sp.a1 = sp.ptr + U.length;
-  sp.end = sp.a1;
-  sp.rounds = U.rounds;
-  sp.owner = FULL ? 0 : U.owner;
-  sp.hb = FULL ? 0u : U.hb;
-  sp.kt = 0;
-  sp.inj = FULL ? 0xFFFFFFFFu : U.inj;
-  sp.init_crc = 0;
-  sp.empty = false;
-  sp.mini = 0;
-  sp.owner_m = 64;
-  sp.hb_m = 0;
-  sp.inj_m = 0;
-  return sp;
-}
-
-// TLAYOUT: transposed loads (FULL batches only).
-template <class Op, bool FULL, bool TLAYOUT = false>
-__device__ __forceinline__ void crc_uniform_driver(const Op& op, const CrcUniform& U, uint32_t count, uint8_t* lds,
-                                                   const CrcTables* __restrict__ g) {
-  static_assert(FULL || !TLAYOUT, "transposed loads need whole rounds");
-  // table loads, then this wave's first span loads, then the LDS stores:
-  // the first round's HBM latency overlaps the fill (uniform spans never
-  // un-shift, so those tables are not loaded)
-  CrcFill fill;
-  crc_fill_load<false>(fill, g);
-  const CrcLane L = TLAYOUT && !kCrcRowT ? crc_lane_t() : crc_lane();
-  const int plane = (int)(threadIdx.x & 63);
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-  const uint32_t nwaves = gridDim.x * wpb;
-  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-  uint32_t i = wave < count ? wave : 0;
-  CrcSpan sp = crc_uniform_span<FULL>(base, i, U);
-  int r = sp.rounds - 1;
-  Chunk cur = !TLAYOUT ? crc_load_chunk(sp, r, L) : kCrcRowT ? crc_load_chunk_rt(sp, r, plane)
-                                                             : crc_load_chunk_t(sp, r, plane);
-  crc_fill_store<false>(fill, lds);
-  __syncthreads();
-  if (wave >= count) return;
-  uint32_t s = 0;
-  for (;;) {
-    uint32_t ni = i;
-    int nr = r - 1;
-    CrcSpan nsp = sp;
-    bool more = true;
-    if (nr < 0) {
-      ni = i + nwaves;
-      more = ni < count;
-      nsp = crc_uniform_span<FULL>(base, more ? ni : i, U);
-      nr = U.rounds - 1;
-    }
-    const Chunk nxt = !TLAYOUT  ? crc_load_chunk(more ? nsp : sp, more ? nr : r, L)
-                      : kCrcRowT ? crc_load_chunk_rt(more ? nsp : sp, more ? nr : r, plane)
-                                 : crc_load_chunk_t(more ? nsp : sp, more ? nr : r, plane);
-    if (TLAYOUT && kCrcRowT) row_transpose(cur);
-    if (TLAYOUT && !kCrcRowT) quad_transpose(cur, plane & 3);
-    s = crc_round(s, cur, sp, r, L);
-    if (r == 0) op.finish(i, crc_finish(s, sp, L), typename Op::Pre{}, (threadIdx.x & 63) == 0);
-    if (!more) break;
-    i = ni;
-    r = nr;
-    sp = nsp;
-    cur = nxt;
-  }
-}
+// (Round 5 retired the uniform-batch driver, crc_uniform_driver /
+// k_crc_uniform: uniform batches run on k_crc_ragged like any other, whose
+// body/head and row drivers measured faster at every length -- 4 KiB
+// blocks 0.784 -> 0.805 of peak, whole-file 64 KiB pieces 0.787 -> 0.815,
+// 512 B 0.157 -> 0.596; profiles/r5/uniform_retired/.)
 
 // ---------------------------------------------------------------------------
 // Row driver: one 16-lane ROW per span, four spans per wave.

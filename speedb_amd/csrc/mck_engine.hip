@@ -283,42 +283,6 @@ int launch_crc(const Op& op, uint32_t count, hipStream_t st, int dev = -1, int n
   return MCK_OK;
 }
 
-// Uniform batch fast path: geometry precomputed here (crc_uniform_driver).
-template <class Op>
-int launch_crc_uniform(const Op& op, const mck_spans* sp, hipStream_t st) {
-  const uint32_t count = sp->count;
-  if (!count) return MCK_OK;
-  int dev, ncu;
-  int rc = current_device(&dev, &ncu);
-  if (rc) return rc;
-  CrcUniform U;
-  U.stride = sp->stride;
-  U.length = sp->length;
-  U.rounds = (int32_t)((sp->length + kRoundBytes - 1) / kRoundBytes);
-  const uint32_t lead = (uint32_t)U.rounds * kRoundBytes - sp->length;
-  U.owner = (int32_t)(lead >> 6);
-  U.hb = lead & 63u;
-  uint32_t inj = 0xFFFFFFFFu;
-  for (uint32_t b = 0; b < 8 * U.hb; b++) inj = gf_unmulx(inj);
-  U.inj = inj;
-  const uint32_t grid = std::min<uint32_t>(ncu, (count + 15) / 16);
-  if (U.owner == 0 && U.hb == 0) {  // whole 4 KiB rounds: row-transposed, non-temporal loads
-    rc = ensure_lds(k_crc_uniform<Op, true, true>, dev);
-    if (rc) return rc;
-    hipLaunchKernelGGL((k_crc_uniform<Op, true, true>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, U, count);
-  } else {
-    rc = ensure_lds(k_crc_uniform<Op, false>, dev);
-    if (rc) return rc;
-    hipLaunchKernelGGL((k_crc_uniform<Op, false>), dim3(grid), dim3(1024), kCrcLdsBytes, st, op, U, count);
-  }
-  MCK_HIP(hipGetLastError());
-  return MCK_OK;
-}
-
-bool is_uniform_aligned(const mck_spans* s) {
-  return !s->offsets && !s->lengths && s->length > 0 && (s->length & 15u) == 0 && (s->stride & 15u) == 0 &&
-         (reinterpret_cast<uintptr_t>(s->base) & 15u) == 0;
-}
 
 // XXH3 driver choice: one 16-lane row per span for uniform batches of short
 // spans (every row gets the same work; round 1 measured 5495 vs 4849 GiB/s
@@ -769,8 +733,8 @@ int mck_crc32c_batch(const mck_spans* spans, const uint32_t* init_crcs, uint32_t
     return MCK_EINVAL;
   }
   const OpCrcValue op{to_src(spans), init_crcs, flags & MCK_F_MASK, out};
-  if (!init_crcs && is_uniform_aligned(spans))
-    return launch_crc_uniform(op, spans, reinterpret_cast<hipStream_t>(stream));
+  // uniform batches too: k_crc_ragged reads off(i) = i * stride (round 5
+  // retired the uniform-batch kernel, slower at every length)
   if (!init_crcs)  // (no init array: OpCrcValueZ takes the rows' combined finish maps)
     return launch_crc(OpCrcValueZ{op}, spans->count, reinterpret_cast<hipStream_t>(stream));
   return launch_crc(op, spans->count, reinterpret_cast<hipStream_t>(stream));

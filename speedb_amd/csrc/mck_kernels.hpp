@@ -323,12 +323,6 @@ __global__ __launch_bounds__(1024) void k_crc_ragged(Op op, uint32_t first, uint
     crc_rows_windows<Op>(op, sh, lds, &g_crc_tables, force == 8 || force == 9 ? 0 : force);
 }
 
-// uniform batches (see CrcUniform)
-template <class Op, bool FULL, bool TLAYOUT = false>
-__global__ __launch_bounds__(1024) void k_crc_uniform(Op op, CrcUniform U, uint32_t count) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_uniform_driver<Op, FULL, TLAYOUT>(op, U, count, lds, &g_crc_tables);
-}
 
 // ============================ XXH3 ========================================
 // one span per 16-lane row (xxh3_rows_driver) or per wave (xxh3_wave_driver)

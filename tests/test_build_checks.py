@@ -27,7 +27,6 @@ def test_engine_lds_image_kernels_have_no_static_lds():
 _PROBE = r"""
 #include <hip/hip_runtime.h>
 namespace mck {
-__global__ void k_crc_uniform(int* o) { extern __shared__ int d[]; d[threadIdx.x] = 1; o[0] = d[1]; }
 __global__ void k_crc_ragged(int* o, int i) {
   // a private array the compiler promotes to static LDS (what round 4 hit)
   __shared__ int promoted[256];
