@@ -44,6 +44,13 @@ declare -A ARGS=(
   [r512u]="--workload ragged --span-min 512 --span-max 512"
   [r1ku]="--workload ragged --span-min 1024 --span-max 1024"
   [r2ku]="--workload ragged --span-min 2048 --span-max 2048"
+  [r57]="--workload ragged --span-min 500 --span-max 700"
+  [r49]="--workload ragged --span-min 400 --span-max 900"
+  [r113]="--workload ragged --span-min 100 --span-max 1300"
+  [r48]="--workload ragged --span-min 400 --span-max 800"
+  [r38]="--workload ragged --span-min 300 --span-max 800"
+  [w39]="--workload walrec --span-min 300 --span-max 900"
+  [r611]="--workload ragged --span-min 600 --span-max 1100"
   [crc]="--workload crc32c"
   [file]="--workload file"
 )
