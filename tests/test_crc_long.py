@@ -249,6 +249,52 @@ def test_sst_mix_oracle_at_scale(gpu, oracle, ctype):
     assert not bad, bad[:10]
 
 
+@pytest.mark.parametrize("lo,hi", [(241, 700), (300, 700), (1000, 3000), (2400, 2700), (100, 5000)])
+def test_xxh3_ragged_rows_in_wave_kernel(gpu, oracle, lo, hi):
+    """XXH3 over ragged batches whose shares average 256 B - 2.5 KiB run on
+    16-lane rows inside the wave kernel (x3_share_rows, round 5); around and
+    across the bounds, every span's XXH3_64bits against the oracle, spans at
+    byte offsets, some short (<= 240 B) ones mixed in for the wide shape."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(lo * 7 + hi)
+    n = 12000
+    lens = [rnd.randrange(lo, hi + 1) for _ in range(n)]
+    offs, pos = [], 0
+    for ln in lens:
+        offs.append(pos)
+        pos += ln + rnd.randrange(0, 9)
+    host = splitmix_bytes(lo + hi, pos + 64)
+    dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda")
+    sp = _spans(torch, S, dev, offs, lens)
+    got = S.xxh3_64_batch(sp).cpu().numpy().view(np.uint64)
+    bad = [i for i in range(n) if int(got[i]) != oracle.XXH3(host[offs[i]:offs[i] + lens[i]])]
+    assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("length", [3072, 16384])
+def test_xxh3_uniform_long_spans_on_wave_kernel(gpu, oracle, length):
+    """Uniform XXH3 batches of >= 3 KiB spans (and >= 16 per CU) run on the
+    wave kernel since round 5 (kX3UniformWaveMin): every span against the
+    oracle, and the same batch on the rows kernel (test hook) agrees."""
+    import speedb_amd as S
+    from speedb_amd import _lib
+    torch = gpu
+    n = 16 * torch.cuda.get_device_properties(0).multi_processor_count + 17
+    host = splitmix_bytes(length, n * length)
+    dev = torch.frombuffer(bytearray(host + bytes(64)), dtype=torch.uint8).to("cuda")
+    sp = S.Spans.uniform(dev, length, n)
+    got = S.xxh3_64_batch(sp).cpu().numpy().view(np.uint64)
+    bad = [i for i in range(n) if int(got[i]) != oracle.XXH3(host[i * length:(i + 1) * length])]
+    assert not bad, bad[:10]
+    try:
+        _lib.check(_lib.lib.mck_test_set_xxh3_driver(2), "mck_test_set_xxh3_driver")
+        rows = S.xxh3_64_batch(sp).cpu().numpy().view(np.uint64)
+    finally:
+        _lib.check(_lib.lib.mck_test_set_xxh3_driver(0), "mck_test_set_xxh3_driver")
+    assert (rows == got).all()
+
+
 @pytest.mark.parametrize("ctype", [1, 4])
 @pytest.mark.parametrize("order", ["file", "shuffled", "reversed"])
 def test_byte_shares_partition_any_order(gpu, oracle, ctype, order):
