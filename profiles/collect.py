@@ -7,8 +7,8 @@ gpurun_out/bench_<tag>/<wl>.json     -> profiles/<dest>/bench_<wl>.json
 gpurun_out/prof_<tag>_<wl>/          -> profiles/<dest>/<wl>/
     trace/trace_kernel_stats.csv, trace/trace_domain_stats.csv (as is)
     trace/trace_kernel_trace.csv     -> trace_mck_kernels.csv (engine kernels only)
-    pmc_*/pmc_counter_collection.csv -> pmc_fetch_mck.csv / pmc_write_mck.csv
-                                        (engine kernels only)
+    pmc_*/pmc_counter_collection.csv -> pmc_fetch_mck.csv / pmc_write_mck.csv /
+                                        pmc_sq_mck.csv (engine kernels only)
     bench_trace.txt                  -> bench_under_rocprof.json
     traffic.json                     -> traffic.json (+ profiles/traffic_<wl>.json)
 """
@@ -70,7 +70,7 @@ def main():
             filter_csv(kt, os.path.join(dst, "trace_mck_kernels.csv"),
                        ["Dispatch_Id", "Kernel_Name", "Grid_Size", "Workgroup_Size", "LDS_Block_Size",
                         "VGPR_Count", "SGPR_Count", "Start_Timestamp", "End_Timestamp"])
-        for kind in ("fetch", "write"):
+        for kind in ("fetch", "write", "sq"):
             p = os.path.join(src, f"pmc_{kind}", "pmc_counter_collection.csv")
             if os.path.exists(p):
                 filter_csv(p, os.path.join(dst, f"pmc_{kind}_mck.csv"))
