@@ -305,47 +305,17 @@ __device__ __forceinline__ void crc_span_inj(CrcSpan& s) {
 // 4 GiB, 16 waves/CU, one round prefetched) reads 6.05 TB/s that way,
 // 6.13 TB/s when each instruction reads 1 KiB contiguous, and 6.90 TB/s
 // contiguous with non-temporal loads (the chunk layout with nt: 3.82).  So
-// lane l = 4a + q loads the 16 B at 1024 j + 16 l of the round (j = 0..3,
-// nt), and a 4 x 4 transpose of 16-byte pieces inside each lane quad (two
-// DPP xor-steps) hands lane l the 64-byte chunk 16 q + a.  The CRC algebra
-// is unchanged, under that "virtual lane" (crc_lane_t).
-__device__ __forceinline__ Chunk crc_load_chunk_t(const CrcSpan& sp, int r, int plane) {
-  const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 16ull * plane;
-  Chunk c;
-#pragma unroll
-  for (int j = 0; j < 4; j++) c.v[j] = span_load16<true>(b + 1024ull * j);
-  return c;
-}
-// one xor-step of the quad transpose on one 32-bit component: register j
-// takes register j ^ M of lane q ^ M where bit M of q differs from bit M of j
-template <int M, int CTRL>
-__device__ __forceinline__ void quad_xstep(uint32_t (&w)[4], int q) {
-  uint32_t x[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++) x[j] = (uint32_t)__builtin_amdgcn_mov_dpp((int)w[j ^ M], CTRL, 0xF, 0xF, true);
-#pragma unroll
-  for (int j = 0; j < 4; j++) w[j] = ((q ^ j) & M) ? x[j] : w[j];
-}
-__device__ __forceinline__ void quad_transpose(Chunk& c, int q) {
-#pragma unroll
-  for (int d = 0; d < 4; d++) {
-    uint32_t w[4];
-#pragma unroll
-    for (int j = 0; j < 4; j++) w[j] = reinterpret_cast<const uint32_t*>(&c.v[j])[d];
-    quad_xstep<2, 0x4E>(w, q);  // quad_perm [2,3,0,1]
-    quad_xstep<1, 0xB1>(w, q);  // quad_perm [1,0,3,2]
-#pragma unroll
-    for (int j = 0; j < 4; j++) reinterpret_cast<uint32_t*>(&c.v[j])[d] = w[j];
-  }
-}
-// Row variant (kCrcRowT, the default): lane l = 16 k + c loads the 16 B
-// at 1024 j + 64 c + 16 k -- each instruction still reads the round's 1 KiB
-// j whole, in a permuted lane order -- and a 4 x 4 transpose over (row k,
-// register j) made of two v_permlane16_swap and two v_permlane32_swap per
-// 32-bit component (4 instructions, each moving two registers, instead of
-// 16 DPP moves and selects) leaves lane l holding the 64-byte chunk l: the
-// chunk layout itself, no virtual lanes.
-constexpr bool kCrcRowT = true;
+// every 16-byte load instruction reads one whole contiguous KiB of the round
+// (non-temporal), and a transpose inside the wave hands each lane its chunk.
+// (Round 5 dropped the lane-quad variant with virtual lanes -- crc_lane_t,
+// quad_transpose -- which only the retired uniform-batch kernel could select.)
+// Lane l = 16 k + c loads the 16 B at 1024 j + 64 c + 16 k -- each
+// instruction reads the round's 1 KiB j whole, in a permuted lane order --
+// and a 4 x 4 transpose over (row k, register j) made of two
+// v_permlane16_swap and two v_permlane32_swap per 32-bit component (4
+// instructions, each moving two registers, instead of 16 DPP moves and
+// selects) leaves lane l holding the 64-byte chunk l: the chunk layout
+// itself, no virtual lanes.
 __device__ __forceinline__ Chunk crc_load_chunk_rt(const CrcSpan& sp, int r, int plane) {
   const uint64_t b = sp.a1 - (uint64_t)kRoundBytes * (r + 1) + 64ull * (plane & 15) + 16ull * (plane >> 4);
   Chunk c;
@@ -377,15 +347,6 @@ __device__ __forceinline__ void row_transpose(Chunk& c) {
     for (int j = 0; j < 4; j++) reinterpret_cast<uint32_t*>(&c.v[j])[d] = w[j];
   }
 }
-// CrcLane for the transposed layout: table copies by the physical lane (the
-// bank pattern), positions by the virtual lane 16 (l & 3) + (l >> 2).
-__device__ __forceinline__ CrcLane crc_lane_t() {
-  CrcLane L = crc_lane();
-  L.lane = 16 * (L.lane & 3) + (L.lane >> 2);
-  L.lane4 = (uint32_t)L.lane << 2;
-  return L;
-}
-
 __device__ __forceinline__ uint64_t crc_chunk_base(const CrcSpan& sp, int r, const CrcLane& L) {
   return sp.a1 - (uint64_t)kRoundBytes * (r + 1) + (uint64_t)L.lane * kChunkBytes;
 }
@@ -394,8 +355,8 @@ __device__ __forceinline__ uint64_t crc_chunk_base(const CrcSpan& sp, int r, con
 // an exec-masked branch turns later waits into vmcnt(0) and kills the
 // prefetch).  In the first round, pieces below a0 read a0 instead (their
 // data is discarded); only the address computation is branched, uniformly.
-// T = transposed loads (see crc_load_chunk_t): full rounds read 1 KiB
-// contiguous per instruction, non-temporal; quad_transpose() before
+// T = transposed loads (see crc_load_chunk_rt): full rounds read 1 KiB
+// contiguous per instruction, non-temporal; row_transpose() before
 // crc_round turns them into chunks.
 template <bool T = false>
 __device__ __forceinline__ Chunk crc_load_chunk(const CrcSpan& sp, int r, const CrcLane& L) {
