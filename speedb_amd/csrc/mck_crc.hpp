@@ -982,13 +982,23 @@ __device__ __forceinline__ void crc_rows_loop(const Op& op, const RowShare& sh, 
   uint32_t s = 0;
   // unrolled twice: the two iterations' chunks, spans and epilogue inputs
   // swap register names instead of being copied every round (the body/head
-  // driver's body loop measured +7 % for the same change)
+  // driver's body loop measured +7 % for the same change).  The loop's
+  // breaks merge at its header, where the compiler then drains every load in
+  // flight once per iteration (vmcnt(0)): that drain turned out to pace the
+  // loads well -- with none, 16-lane rows of 1 KiB spans measured 0.649 ->
+  // 0.559 of peak, one per step 0.616; 8-lane rows gain 1-2 % with one per
+  // four steps (200-500-B spans 0.538 -> 0.549), 16-lane rows lose 5-8 %
+  // (profiles/r5/rows_pace/).
   RowState B;
   Chunk cb;
   typename Op::Pre pb;
   for (;;) {
     if (!crc_rows_step<Op, W>(x, A, ca, pa, B, cb, pb, s)) break;
     if (!crc_rows_step<Op, W>(x, B, cb, pb, A, ca, pa, s)) break;
+    if constexpr (W == 8) {
+      if (!crc_rows_step<Op, W>(x, A, ca, pa, B, cb, pb, s)) break;
+      if (!crc_rows_step<Op, W>(x, B, cb, pb, A, ca, pa, s)) break;
+    }
   }
 }
 
