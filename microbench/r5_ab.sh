@@ -36,6 +36,13 @@ declare -A ARGS=(
   [x3u]="--workload xxh3"
   [x3u16k]="--workload xxh3 --block-bytes 16384 --blocks 65536"
   [x3u64k]="--workload xxh3 --block-bytes 65536 --blocks 16384"
+  [x3u1k]="--workload xxh3 --block-bytes 1024 --blocks 1048576"
+  [x3u1000]="--workload xxh3 --block-bytes 1000 --blocks 1048576"
+  [kv]="--workload kv"
+  [x3u1040]="--workload xxh3 --block-bytes 1040 --blocks 1048576"
+  [x3u1032]="--workload xxh3 --block-bytes 1032 --blocks 1048576"
+  [x3u1028]="--workload xxh3 --block-bytes 1028 --blocks 1048576"
+  [x3u1088]="--workload xxh3 --block-bytes 1088 --blocks 1048576"
   [x3u2k]="--workload xxh3 --block-bytes 2048 --blocks 524288"
   [cu512]="--workload crc32c --block-bytes 512 --blocks 2097152"
   [cu1k]="--workload crc32c --block-bytes 1024 --blocks 1048576"
