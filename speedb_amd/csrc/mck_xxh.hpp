@@ -447,9 +447,9 @@ __device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t 
 // non-data VALU work.
 // The row loop: each row walks its span segment by segment; next_span(rs)
 // moves a row whose span ended to its next long one (false: none left).
-template <class Op, bool PREVIEW, class Next>
-__device__ __forceinline__ void xxh3_rows_loop(const Op& op, const X3Row& X, X3Span& rs, bool act,
-                                               Next&& next_span) {
+template <class Op, bool PREVIEW, bool NT, class Next>
+__device__ __forceinline__ void xxh3_rows_loop_p(const Op& op, const X3Row& X, X3Span& rs, bool act,
+                                                 Next&& next_span) {
   uint64_t a0 = X.i0, a1 = X.i1;
   uint32_t slot = 0, si = 0;
   uint64_t shv = 0;
@@ -469,11 +469,8 @@ __device__ __forceinline__ void xxh3_rows_loop(const Op& op, const X3Row& X, X3S
     uint4 d[4];
     bool ok[4];
 #pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t st = (uint32_t)(X.st4 + 4 * k);
-      ok[k] = act && (full || st < rs.nst);
-      d[k] = gload16u(ok[k] ? seg + 64 * st + 16 * X.q - sh + 4 : idle);
-    }
+    for (int k = 0; k < 4; k++) ok[k] = act && (full || (uint32_t)(X.st4 + 4 * k) < rs.nst);
+    const uint64_t sb = seg + 64 * X.st4 + 16 * X.q - sh + 4;  // + 256 k
     const uint64_t lst = rs.ptr + rs.len - 64;  // last stripe: its own byte offset
     const uint32_t shl = rd_shift(lst);
     // the last stripe is used only in the span's last segment: before that
@@ -481,8 +478,10 @@ __device__ __forceinline__ void xxh3_rows_loop(const Op& op, const X3Row& X, X3S
     // first stripe, whose line this iteration fetches anyway -- re-reading
     // the span's last 64 bytes in every segment cost ~6 % extra HBM reads
     // at 4 KiB (PMC traffic 1.09x, non-temporal loads do not keep the line)
-    const uint64_t lsa = full ? seg + 16 * X.q - sh + 4 : lst + 16 * X.q - shl + 4;
-    uint4 dl = gload16u(act ? lsa : idle);
+    const uint64_t lsa = act ? (full ? seg + 16 * X.q - sh + 4 : lst + 16 * X.q - shl + 4) : idle;
+#pragma unroll
+    for (int k = 0; k < 4; k++) d[k] = span_load16<NT>(ok[k] ? sb + 256 * k : idle);
+    uint4 dl = span_load16<NT>(lsa);
     // the dword before the segment: loaded only at the span's first segment;
     // later it is the previous segment's last dword, already in lane 15's
     // registers -- re-reading it fetched that line again (non-temporal loads
@@ -543,6 +542,22 @@ __device__ __forceinline__ void xxh3_rows_loop(const Op& op, const X3Row& X, X3S
     }
   }
   if (sv) op.finish(si, shv);
+}
+// Non-temporal loads only for waves whose first spans are all 16-byte
+// aligned: a misaligned segment's 256-byte chunks share their boundary lines
+// with the next chunk's load instruction, which non-temporal loads do not
+// keep (1000-byte spans at 8-byte alignment: 0.621 of peak with
+// non-temporal loads, 0.705 without; aligned 1 KiB spans 0.760 with, 0.712
+// without -- profiles/r5/x3_align/).  Chosen once per wave from the rows'
+// first spans (a per-iteration choice would need both load sets in the
+// loop, and the compiler merges them into one without the policy).
+template <class Op, bool PREVIEW, class Next>
+__device__ __forceinline__ void xxh3_rows_loop(const Op& op, const X3Row& X, X3Span& rs, bool act,
+                                               Next&& next_span) {
+  if (!__any(act && ((uint32_t)rs.ptr & 15u) != 0))  // wave-uniform
+    xxh3_rows_loop_p<Op, PREVIEW, true>(op, X, rs, act, next_span);
+  else
+    xxh3_rows_loop_p<Op, PREVIEW, false>(op, X, rs, act, next_span);
 }
 
 template <class Op, bool PREVIEW = false>
