@@ -295,6 +295,38 @@ def test_xxh3_uniform_long_spans_on_wave_kernel(gpu, oracle, length):
     assert (rows == got).all()
 
 
+@pytest.mark.parametrize("length", [1000, 1024, 1032, 1040, 2056])
+def test_xxh3_rows_load_policy_by_alignment(gpu, oracle, length):
+    """The XXH3 / XXPH3 row loop runs one of two instances per wave --
+    non-temporal loads when every row's first span is 16-byte aligned, the
+    default policy otherwise (xxh3_rows_loop, round 5): uniform batches whose
+    spans are all aligned (1024), alternate (1000, 2056: 8-byte steps) or
+    mostly misaligned (1032, 1040), on the rows kernel, against the oracle;
+    and per-KV protection of values at the same stride (XXPH3, kind 2)."""
+    import speedb_amd as S
+    torch = gpu
+    n = 3000
+    host = splitmix_bytes(length + 5, n * length)
+    dev = torch.frombuffer(bytearray(host + bytes(64)), dtype=torch.uint8).to("cuda")
+    sp = S.Spans.uniform(dev, length, n)
+    got = S.xxh3_64_batch(sp).cpu().numpy().view(np.uint64)
+    bad = [i for i in range(n) if int(got[i]) != oracle.XXH3(host[i * length:(i + 1) * length])]
+    assert not bad, bad[:10]
+    kb = 16
+    keys = splitmix_bytes(length + 6, n * kb)
+    kd = torch.frombuffer(bytearray(keys + bytes(64)), dtype=torch.uint8).to("cuda")
+    ks = S.Spans.uniform(kd, kb, n)
+    ops = [(7 * i) % 256 for i in range(n)]
+    ex = [(0x9E3779B97F4A7C15 * (i + 3)) & (2 ** 64 - 1) for i in range(n)]
+    dops = torch.tensor(ops, dtype=torch.uint8, device="cuda")
+    dex = torch.tensor(np.array(ex, dtype=np.uint64).view(np.int64), device="cuda")
+    kv = S.kv_protect_batch(2, ks, sp, dops, dex).cpu().numpy().view(np.uint64)
+    bad = [i for i in range(0, n, 7)
+           if int(kv[i]) != oracle.KvProtect(2, keys[i * kb:(i + 1) * kb], host[i * length:(i + 1) * length],
+                                             ops[i], ex[i])]
+    assert not bad, bad[:10]
+
+
 @pytest.mark.parametrize("ctype", [1, 4])
 @pytest.mark.parametrize("order", ["file", "shuffled", "reversed"])
 def test_byte_shares_partition_any_order(gpu, oracle, ctype, order):
