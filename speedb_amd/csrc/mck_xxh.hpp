@@ -489,20 +489,28 @@ __device__ __forceinline__ void xxh3_rows_loop_p(const Op& op, const X3Row& X, X
     // (XXH3 only: the XXPH3 users -- per-KV protection, ~1 KiB spans of one
     // segment -- would pay the register for nothing: OpKvProtect<true> went
     // from 128 to 130 VGPRs, 4 -> 3 waves per SIMD, -6 %)
-    uint32_t e0;
+    uint32_t e0p = 0;
     if constexpr (!PREVIEW) {
-      const uint32_t e0l = gload4(act && rs.g == 0 && seg - sh >= idle ? seg - sh : act ? seg - sh + 4 : idle);
-      const uint32_t w3 = d[3].w;
-      const uint32_t e0p = dpp32<kDppRowRor1>(pw);  // lane 0 of the row (the one user) <- lane 15
-      e0 = rs.g ? e0p : e0l;
-      pw = w3;
-    } else {
-      e0 = gload4(act && seg - sh >= idle ? seg - sh : idle);
+      e0p = dpp32<kDppRowRor1>(pw);  // lane 0 of the row (the one user) <- lane 15
+      pw = d[3].w;
     }
-    const uint32_t el = gload4(act ? (full ? seg - sh + 4 : lst - shl) : idle);
-    rd_fix_row(d, e0, X.j, sel);
-    const uint32_t pl = dpp32<kDppQuadShr1>(dl.w);  // unconditional: see x3w_fold
-    dl = rd_fix(dl, X.q ? pl : el, rd_sel(shl));
+    // Realignment only while some active row's span (or its last stripe)
+    // is not dword-aligned (wave-uniform branch): for an aligned one rd_fix
+    // is the identity, and its two dword loads, 20 v_perm and 5 DPP moves
+    // per iteration are skipped (profiles/r5/x3_align/).
+    if (__any(act && (((uint32_t)rs.ptr | (uint32_t)rs.len) & 3u) != 0)) {
+      uint32_t e0;
+      if constexpr (!PREVIEW) {
+        const uint32_t e0l = gload4(act && rs.g == 0 && seg - sh >= idle ? seg - sh : act ? seg - sh + 4 : idle);
+        e0 = rs.g ? e0p : e0l;
+      } else {
+        e0 = gload4(act && seg - sh >= idle ? seg - sh : idle);
+      }
+      const uint32_t el = gload4(act ? (full ? seg - sh + 4 : lst - shl) : idle);
+      rd_fix_row(d, e0, X.j, sel);
+      const uint32_t pl = dpp32<kDppQuadShr1>(dl.w);  // unconditional in the branch: see x3w_fold
+      dl = rd_fix(dl, X.q ? pl : el, rd_sel(shl));
+    }
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll
     for (int k = 0; k < 4; k++) {
