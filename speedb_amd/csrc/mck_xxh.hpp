@@ -478,7 +478,13 @@ __device__ __forceinline__ void xxh3_rows_loop_p(const Op& op, const X3Row& X, X
     // first stripe, whose line this iteration fetches anyway -- re-reading
     // the span's last 64 bytes in every segment cost ~6 % extra HBM reads
     // at 4 KiB (PMC traffic 1.09x, non-temporal loads do not keep the line)
-    const uint64_t lsa = act ? (full ? seg + 16 * X.q - sh + 4 : lst + 16 * X.q - shl + 4) : idle;
+    // a last segment holding no stripe (len just past a segment multiple)
+    // is finished in the iteration of the full segment before it: the last
+    // stripe is loaded here and merged after the scramble (one iteration
+    // per span instead of two at 1025-1088 bytes)
+    const bool fin = full && rs.g + 1 == rs.nb && rs.nst == 0;
+    const bool lastseg = !full || fin;
+    const uint64_t lsa = act ? (lastseg ? lst + 16 * X.q - shl + 4 : seg + 16 * X.q - sh + 4) : idle;
 #pragma unroll
     for (int k = 0; k < 4; k++) d[k] = span_load16<NT>(ok[k] ? sb + 256 * k : idle);
     uint4 dl = span_load16<NT>(lsa);
@@ -506,7 +512,7 @@ __device__ __forceinline__ void xxh3_rows_loop_p(const Op& op, const X3Row& X, X
       } else {
         e0 = gload4(act && seg - sh >= idle ? seg - sh : idle);
       }
-      const uint32_t el = gload4(act ? (full ? seg - sh + 4 : lst - shl) : idle);
+      const uint32_t el = gload4(act ? (lastseg ? lst - shl : seg - sh + 4) : idle);
       rd_fix_row(d, e0, X.j, sel);
       const uint32_t pl = dpp32<kDppQuadShr1>(dl.w);  // unconditional in the branch: see x3w_fold
       dl = rd_fix(dl, X.q ? pl : el, rd_sel(shl));
@@ -526,7 +532,8 @@ __device__ __forceinline__ void xxh3_rows_loop_p(const Op& op, const X3Row& X, X
       a0 = xxh3_scramble(a0, X.ks0);
       a1 = xxh3_scramble(a1, X.ks1);
       rs.g++;
-    } else if (act) {  // last, partial segment done: last stripe, merge, next span
+    }
+    if (act && lastseg) {  // last (partial) segment done: last stripe, merge, next span
       const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
       if (rs.tail) {
         a0 += (PREVIEW ? l0 : l1) + mul32to64(l0 ^ X.kl0);

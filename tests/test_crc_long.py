@@ -295,14 +295,17 @@ def test_xxh3_uniform_long_spans_on_wave_kernel(gpu, oracle, length):
     assert (rows == got).all()
 
 
-@pytest.mark.parametrize("length", [1000, 1024, 1032, 1040, 2056])
+@pytest.mark.parametrize("length", [1000, 1024, 1025, 1032, 1040, 1088, 2048, 2056])
 def test_xxh3_rows_load_policy_by_alignment(gpu, oracle, length):
     """The XXH3 / XXPH3 row loop runs one of two instances per wave --
     non-temporal loads when every row's first span is 16-byte aligned, the
     default policy otherwise (xxh3_rows_loop, round 5): uniform batches whose
-    spans are all aligned (1024), alternate (1000, 2056: 8-byte steps) or
-    mostly misaligned (1032, 1040), on the rows kernel, against the oracle;
-    and per-KV protection of values at the same stride (XXPH3, kind 2)."""
+    spans are all aligned (1024, 2048), alternate (1000, 2056: 8-byte steps)
+    or mostly misaligned (1025, 1032, 1040, 1088), on the rows kernel,
+    against the oracle; and per-KV protection of values at the same stride
+    (XXPH3, kind 2).  1025-1088 and 2056 (XXH3) and 1024, 1040, 1088, 2048,
+    2056 (XXPH3) end in a segment with no stripe, finished in the iteration
+    of the full segment before it."""
     import speedb_amd as S
     torch = gpu
     n = 3000
