@@ -402,6 +402,10 @@ struct X3Span {
   uint32_t g;    // segment being processed
   uint32_t i;    // span index
   bool tail;     // last stripe at len - 64 (XXPH3: only if len % 64)
+  // XXH3: the descriptor of span pi (hlen, off), loaded when span i started
+  // (x3_next_long)
+  uint64_t pl = 0, po = 0;
+  uint32_t pi = ~0u;
 };
 
 // Advance the row to its next long span (hashing short ones -- n <= 240 --
@@ -414,9 +418,20 @@ __device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t 
                                              const X3Row& X, X3Span& rs) {
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   for (; i < count; i += stride) {
-    const uint64_t len = op.hlen(i);
-    const uint64_t ptr = base + op.off(i);
+    // XXH3 (ragged batches: a descriptor is two dependent loads before the
+    // span's data loads): the next span's descriptor was loaded when this
+    // one started, so it arrives while the span is hashed.  (Not for XXPH3:
+    // per-KV protection's verify op sits at 128 VGPRs, 4 waves per SIMD.)
+    const bool pf = !PREVIEW && i == rs.pi;
+    const uint64_t len = pf ? rs.pl : op.hlen(i);
+    const uint64_t ptr = base + (pf ? rs.po : op.off(i));
     if (len > 240) {
+      if constexpr (!PREVIEW) {
+        const uint32_t ni = i + stride, pj = ni < count ? ni : i;  // (unconditional loads)
+        rs.pi = ni;
+        rs.pl = op.hlen(pj);
+        rs.po = op.off(pj);
+      }
       rs.ptr = ptr;
       rs.len = len;
       // XXH3 util/xxhash.h:5141-5171; XXPH3 util/xxph3.h:1516-1543
