@@ -703,9 +703,14 @@ __device__ __forceinline__ X3WLoads x3w_load(const X3WSpan& sp, uint32_t k, cons
   L.v = gload16u(okl ? lone + 16 * X.lane - sh + 4 : idle);
   const uint32_t shl = rd_shift(lst);  // the last stripe's own byte offset
   L.dl = gload16u(last ? lst + 16 * X.q - shl + 4 : idle);
-  L.e0 = gload4(x3w_ok(sp, k, g, 0) && g ? seg - sh : idle);
-  L.ev = gload4(okl && sp.nb ? lone - sh : idle);
-  L.el = gload4(last ? lst - shl : idle);
+  // the realignment dwords only for a span that needs them (x3w_fold skips
+  // rd_fix for dword-aligned spans and last stripes; wave-uniform branch)
+  L.e0 = L.ev = L.el = 0;
+  if (((uint32_t)sp.ptr | (uint32_t)sp.len) & 3u) {
+    L.e0 = gload4(x3w_ok(sp, k, g, 0) && g ? seg - sh : idle);
+    L.ev = gload4(okl && sp.nb ? lone - sh : idle);
+    L.el = gload4(last ? lst - shl : idle);
+  }
   return L;
 }
 
