@@ -290,6 +290,27 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes,
                          uint32_t log_number, mck_wal_block_result* results,
                          mck_stream_t stream);
 
+/* WAL recovery's device pass (db/log_reader.cc:69-584 with a record_checksum,
+ * as DBImpl::RecoverLogFiles asks for it, db/db_impl/db_impl_open.cc:1217-1221):
+ * ONE read of the image gives mck_wal_verify_batch's per-block results AND
+ * the XXH3_64bits of every single-fragment record -- kFullType /
+ * kRecyclableFullType, whose record_checksum ReadRecord computes over the
+ * fragment in place (:107-110) -- in walk order per block: the k-th
+ * full-type record of block b (counting every full-type record the block's
+ * walk passes, before its stop) goes to record_hashes[base_b + k] if k <
+ * cap_b, with
+ *   base_b = slot_base[b], cap_b = slot_base[b + 1] - slot_base[b]
+ *            (slot_base: device array [nblocks + 1], e.g. the prefix sum of
+ *            the full records per block of a host plan -- mck_wal_recover),
+ *   or, slot_base NULL: base_b = b * slots_per_block, cap_b = slots_per_block.
+ * record_hashes NULL: the CRC verify alone.  Multi-fragment records
+ * (kFirst..kLast) are not hashed here (their bytes are not contiguous):
+ * mck_wal_gather_batch + mck_xxh3_64_batch. */
+int mck_wal_recover_batch(const void* wal, uint64_t nbytes, uint32_t log_number,
+                          mck_wal_block_result* results, const uint64_t* slot_base,
+                          uint32_t slots_per_block, uint64_t* record_hashes,
+                          mck_stream_t stream);
+
 /* ---- log::Reader, the whole log (db/log_reader.cc:69-584) ----------------- */
 
 /* WALRecoveryMode (include/rocksdb/options.h) */
@@ -336,7 +357,9 @@ typedef struct mck_wal_report {
  * and set struct_size = sizeof(mck_wal_read_out): the library writes no field
  * past struct_size, and a caller whose struct ends before the compression
  * fields (MCK_WAL_READ_OUT_V1_SIZE) gets MCK_ENOTSUP for a compressed WAL
- * instead of a write past its struct. */
+ * instead of a write past its struct.  Any other struct_size (e.g. a caller
+ * built before struct_size became the first field, whose frags pointer sits
+ * there) is refused with MCK_EINVAL, nothing written. */
 typedef struct mck_wal_read_out {
   uint64_t struct_size;       /* sizeof(mck_wal_read_out) of the caller    */
   mck_wal_fragment* frags;    /* payload fragments of the returned records */
@@ -390,6 +413,49 @@ int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t log_number,
                          int recovery_mode,
                          const mck_wal_block_result* verified,
                          mck_wal_read_out* out);
+
+/* ---- WAL recovery with record checksums, one device pass ------------------ */
+/* DBImpl::RecoverLogFiles' read loop (db/db_impl/db_impl_open.cc:1204-1221):
+ * log::Reader::ReadRecord(&record, &scratch, mode, &record_checksum) until it
+ * returns false, over a whole WAL image, with every CRC32C (ReadPhysicalRecord,
+ * db/log_reader.cc:512-525) and every record's XXH3_64bits record_checksum
+ * (:107-110 one fragment, :128-158 streamed over fragments) computed on the
+ * device in ONE read of the image (mck_wal_recover_batch); multi-fragment
+ * records are gathered and hashed in the same stream.  wal_host: the image in
+ * host memory (the reader's header walk, as the reference reads it from the
+ * file); wal_dev: the same nbytes in device memory (readable 16 bytes past
+ * nbytes).  Synchronous: returns after the results are on the host.  The
+ * result holds what mck_wal_read_records returns for the same image and mode
+ * (records, fragments, reports, drops) plus the checksums.
+ * *out: free with mck_wal_recovery_free. */
+typedef struct mck_wal_recovery mck_wal_recovery;
+int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64_t nbytes,
+                    uint32_t log_number, int recovery_mode, mck_stream_t stream,
+                    mck_wal_recovery** out);
+/* The walk's records, fragments and reports, exactly as mck_wal_read_records
+ * fills `out` (same capacity rules: call with NULL arrays for the counts). */
+int mck_wal_recovery_read_out(const mck_wal_recovery* r, mck_wal_read_out* out);
+/* record_checksum (XXH3_64bits) of every returned record, in order
+ * (cap >= nrecords).  MCK_ENOTSUP for a compressed WAL: there the reference
+ * hashes the DECOMPRESSED record (db/log_reader.cc:537-571), the caller's. */
+int mck_wal_recovery_checksums(const mck_wal_recovery* r, uint64_t* checksums,
+                               uint64_t cap);
+typedef struct mck_wal_recovery_info {
+  uint64_t nrecords;
+  uint64_t in_place;        /* one-fragment records hashed by the recover pass  */
+  uint64_t gathered;        /* multi-fragment records (gather + XXH3 batch)     */
+  uint64_t gathered_bytes;  /* their bytes                                      */
+  uint32_t host_walks;      /* 1, or 2 when a CRC failed (walk over verdicts)    */
+  uint32_t has_checksums;   /* 0: compressed WAL                                 */
+  double walk_seconds;      /* host header walks                                 */
+  double device_seconds;    /* device pass(es): launch to results on the host    */
+} mck_wal_recovery_info;
+int mck_wal_recovery_get_info(const mck_wal_recovery* r, mck_wal_recovery_info* info);
+/* The device pass's per-block results (as mck_wal_verify_batch's), host copy;
+ * cap >= ceil(nbytes / 32768). */
+int mck_wal_recovery_block_results(const mck_wal_recovery* r, mck_wal_block_result* results,
+                                   uint64_t cap);
+void mck_wal_recovery_free(mck_wal_recovery* r);
 
 /* Text of a MCK_WAL_R_* reason ("checksum mismatch", "unknown record type
  * 101", ...); Status::Corruption(reason).ToString() is "Corruption: " + it. */

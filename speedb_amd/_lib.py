@@ -149,6 +149,15 @@ SIGNATURES = [
     ("mck_wal_gather_batch", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp]),
     ("mck_wal_read_records", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, vp, vp]),
     ("mck_wal_reason_string", ctypes.c_char_p, [ctypes.c_int]),
+    ("mck_wal_recover_batch", ctypes.c_int,
+     [vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp]),
+    ("mck_wal_recover", ctypes.c_int,
+     [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, vp, vp]),
+    ("mck_wal_recovery_read_out", ctypes.c_int, [vp, vp]),
+    ("mck_wal_recovery_checksums", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
+    ("mck_wal_recovery_get_info", ctypes.c_int, [vp, vp]),
+    ("mck_wal_recovery_block_results", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
+    ("mck_wal_recovery_free", None, [vp]),
     ("mck_wal_tail_create", ctypes.c_int, [ctypes.c_uint32, vp]),
     ("mck_wal_tail_destroy", None, [vp]),
     ("mck_wal_tail_set_image", ctypes.c_int, [vp, vp, ctypes.c_uint64, vp]),

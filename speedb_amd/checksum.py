@@ -346,6 +346,28 @@ def wal_verify_batch(wal, nbytes: Optional[int] = None, log_number: int = 0, str
     return res
 
 
+def wal_recover_batch(wal, nbytes: Optional[int] = None, log_number: int = 0, slot_base=None,
+                      slots_per_block: int = 0, hashes=None, stream=None, out=None):
+    """mck_wal_recover_batch: the per-block verify results (as
+    wal_verify_batch) and, in the same read, the XXH3_64bits of every
+    full-type record: record k of block b at hashes[slot_base[b] + k] (k <
+    slot_base[b + 1] - slot_base[b]) or, without slot_base, at
+    hashes[b * slots_per_block + k].  Returns (results, hashes)."""
+    torch = _torch()
+    if nbytes is None:
+        nbytes = wal.numel()
+    nblocks = (nbytes + 32767) // 32768
+    res = out if out is not None else torch.empty((nblocks, 4), dtype=torch.int32, device=wal.device)
+    if hashes is None and (slot_base is not None or slots_per_block):
+        n = int(slot_base[-1].item()) if slot_base is not None else nblocks * slots_per_block
+        hashes = torch.zeros(max(n, 1), dtype=torch.int64, device=wal.device)
+    check(lib.mck_wal_recover_batch(wal.data_ptr(), nbytes, log_number & 0xFFFFFFFF, res.data_ptr(),
+                                    slot_base.data_ptr() if slot_base is not None else None, slots_per_block,
+                                    hashes.data_ptr() if hashes is not None else None, _stream(stream)),
+          "mck_wal_recover_batch")
+    return res, hashes
+
+
 def np_hash64_batch(spans: Spans, seed: int = 0, out=None, stream=None):
     """out[i] = NPHash64(span i, seed) (int64 tensor of the u64 bit patterns)."""
     torch = _torch()
@@ -666,70 +688,117 @@ def wal_read_records(wal: bytes, log_number: int = 0,
                        o2.compression_type, stream)
 
 
+class mck_wal_recovery_info(ctypes.Structure):
+    _fields_ = [("nrecords", ctypes.c_uint64), ("in_place", ctypes.c_uint64), ("gathered", ctypes.c_uint64),
+                ("gathered_bytes", ctypes.c_uint64), ("host_walks", ctypes.c_uint32),
+                ("has_checksums", ctypes.c_uint32), ("walk_seconds", ctypes.c_double),
+                ("device_seconds", ctypes.c_double)]
+
+
 class WalRecovery(NamedTuple):
-    records: object          # device uint8 tensor: every record, back to back
-    rec_offsets: object
+    records: object          # device uint8 tensor of every record back to back (gather=True), else None
+    rec_offsets: object      # numpy uint64: record r in that (contiguous) record buffer
     rec_lengths: object
     rec_file_offsets: object
     record_checksums: object  # numpy uint64 XXH3_64bits of every record (None: compressed log)
-    blocks: object           # device per-block verify results (or None)
+    blocks: object           # per-block device verdicts (mck_wal_block_result as int32 [nblocks, 4])
     reports: list
     dropped_bytes: int
     message: str
     compression_type: int = 0  # compressed WAL: records are compressed chunks (see WalReadPlan)
     stream: list = []
+    frags: object = None     # ctypes array of mck_wal_fragment (src_off in the image, dst_off in the buffer)
+    nfrags: int = 0
+    image: bytes = b""       # the host image (Records() reassembles from it)
+    info: object = None      # mck_wal_recovery_info
 
     def Records(self):
         """The records as bytes (what ReadRecord's *record holds, in order)."""
-        host = bytes(self.records.cpu().numpy().tobytes())
-        return [host[int(o):int(o) + int(n)] for o, n in zip(self.rec_offsets, self.rec_lengths)]
+        if self.records is not None:
+            host = bytes(self.records.cpu().numpy().tobytes())
+            return [host[int(o):int(o) + int(n)] for o, n in zip(self.rec_offsets, self.rec_lengths)]
+        buf = bytearray(sum(int(n) for n in self.rec_lengths) + 1)
+        for f in self.frags[:self.nfrags]:
+            buf[f.dst_off:f.dst_off + f.length] = self.image[f.src_off:f.src_off + f.length]
+        return [bytes(buf[int(o):int(o) + int(n)]) for o, n in zip(self.rec_offsets, self.rec_lengths)]
 
 
 def WalRecover(wal: bytes, log_number: int = 0,
                recovery_mode: int = WALRecoveryMode.kTolerateCorruptedTailRecords,
-               device=None, stream=None, checksum: bool = True) -> WalRecovery:
-    """WAL recovery with the checksum work on the device:
-      1. mck_wal_verify_batch -- every physical record's CRC32C, per 32 KiB
-         block (ReadPhysicalRecord's check);
-      2. mck_wal_read_records -- ReadRecord's walk on the host over those
-         verdicts: records, drops and corruption reports of the given
-         WALRecoveryMode;
-      3. mck_wal_gather_batch + mck_xxh3_64_batch -- the records reassembled
-         into one device buffer and their record_checksum (XXH3_64bits)."""
+               device=None, stream=None, checksum: bool = True, gather: bool = False,
+               wal_dev=None) -> WalRecovery:
+    """DBImpl::RecoverLogFiles' reader loop (db/db_impl/db_impl_open.cc
+    :1204-1221: ReadRecord(&record, &scratch, mode, &record_checksum) until
+    false) through ONE entry point, mck_wal_recover: every physical record's
+    CRC32C and every single-fragment record's XXH3 record_checksum in one
+    device pass over the image (mck_wal_recover_batch), multi-fragment
+    records gathered and hashed on the same stream, the reader's walk on the
+    host over the verdicts (records, drops and reports of the given
+    WALRecoveryMode).  ``wal_dev``: the image already in device memory (a
+    uint8 tensor of at least len(wal) + 16 bytes); else it is uploaded.
+    ``gather``: also reassemble the records into one device buffer
+    (``records``).  ``checksum=False``: the host walk alone, every CRC
+    trusted (mck_wal_read_records without verdicts)."""
     import numpy as np
     torch = _torch()
     dev = torch.device("cuda") if device is None else device
     st = stream if stream is not None else torch.cuda.current_stream(dev)
     wal = bytes(wal)
-    # uploads, kernels and readbacks all on `st`: inside the context every
-    # torch op (.to, zeros, .cpu) is queued on it, and .cpu() waits for it --
-    # the host walk never reads verdicts the kernel has not written
+    if not checksum:
+        plan = wal_read_records(wal, log_number, recovery_mode, None)
+        return WalRecovery(None, plan.rec_offsets, plan.rec_lengths, plan.rec_file_offsets, None, None,
+                           plan.reports, plan.dropped_bytes, plan.message, plan.compression_type, plan.stream,
+                           plan.frags, plan.nfrags, wal, None)
     with torch.cuda.stream(st):
-        img = torch.frombuffer(bytearray(wal + bytes(64)), dtype=torch.uint8).to(dev)
-        blocks = wal_verify_batch(img, len(wal), log_number, stream=st) if (len(wal) and checksum) else None
-        if blocks is not None:
-            st.synchronize()
-        plan = wal_read_records(wal, log_number, recovery_mode, blocks)
-        nbytes, nf = plan.records_bytes, plan.nfrags
-        out = torch.zeros(nbytes + 64, dtype=torch.uint8, device=dev)
-        if nf:
-            d_frags = torch.frombuffer(bytearray(bytes(plan.frags)[:nf * ctypes.sizeof(mck_wal_fragment)]),
-                                       dtype=torch.uint8).to(dev)
-            check(lib.mck_wal_gather_batch(img.data_ptr(), d_frags.data_ptr(), nf, out.data_ptr(), _stream(st)),
-                  "mck_wal_gather_batch")
-        offs, lens = plan.rec_offsets, plan.rec_lengths
-        if plan.compression_type:
-            # compressed chunks: the record checksum is XXH3 over the
-            # DECOMPRESSED bytes (db/log_reader.cc:537-571), the caller's
+        img = wal_dev if wal_dev is not None else \
+            torch.frombuffer(bytearray(wal + bytes(64)), dtype=torch.uint8).to(dev)
+        h = ctypes.c_void_p()
+        check(lib.mck_wal_recover(wal, img.data_ptr(), len(wal), log_number & 0xFFFFFFFF, int(recovery_mode),
+                                  _stream(st), ctypes.byref(h)), "mck_wal_recover")
+        try:
+            o = mck_wal_read_out()
+            o.struct_size = ctypes.sizeof(mck_wal_read_out)
+            check(lib.mck_wal_recovery_read_out(h, ctypes.addressof(o)), "mck_wal_recovery_read_out")
+            frags = (mck_wal_fragment * max(o.nfrags, 1))()
+            offs = np.zeros(max(o.nrecords, 1), dtype=np.uint64)
+            lens = np.zeros(max(o.nrecords, 1), dtype=np.uint32)
+            foffs = np.zeros(max(o.nrecords, 1), dtype=np.uint64)
+            reps = (mck_wal_report * max(o.nreports, 1))()
+            strm = (mck_wal_fragment * max(o.nstream, 1))()
+            o2 = mck_wal_read_out(ctypes.sizeof(mck_wal_read_out), ctypes.addressof(frags), o.nfrags, 0,
+                                  offs.ctypes.data, lens.ctypes.data, foffs.ctypes.data, o.nrecords, 0, 0,
+                                  ctypes.addressof(reps), o.nreports)
+            o2.stream = ctypes.addressof(strm)
+            o2.stream_cap = o.nstream
+            check(lib.mck_wal_recovery_read_out(h, ctypes.addressof(o2)), "mck_wal_recovery_read_out")
+            info = mck_wal_recovery_info()
+            check(lib.mck_wal_recovery_get_info(h, ctypes.addressof(info)), "mck_wal_recovery_get_info")
             x3 = None
-        elif len(offs):
-            sp = Spans(out, len(offs), offsets=torch.from_numpy(offs.astype(np.int64)).to(dev),
-                       lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
-            x3 = xxh3_64_batch(sp, stream=st).cpu().numpy().view(np.uint64)
-        else:
-            x3 = np.zeros(0, np.uint64)
-    return WalRecovery(out[:nbytes], offs, lens, plan.rec_file_offsets, x3, blocks, plan.reports,
-                       plan.dropped_bytes, plan.message, plan.compression_type, plan.stream)
+            if info.has_checksums:
+                x3 = np.zeros(max(o2.nrecords, 1), dtype=np.uint64)
+                check(lib.mck_wal_recovery_checksums(h, x3.ctypes.data, len(x3)), "mck_wal_recovery_checksums")
+                x3 = x3[:o2.nrecords]
+            nblocks = (len(wal) + 32767) // 32768
+            blk = np.zeros((max(nblocks, 1), 4), dtype=np.int32)
+            check(lib.mck_wal_recovery_block_results(h, blk.ctypes.data, nblocks), "mck_wal_recovery_block_results")
+        finally:
+            lib.mck_wal_recovery_free(h)
+        reports = [(r.offset, r.bytes, lib.mck_wal_reason_string(r.reason).decode()) for r in reps[:o2.nreports]]
+        stream_l = [(f.src_off, f.length, -1 if f.dst_off == 0xFFFFFFFFFFFFFFFF else f.dst_off)
+                    for f in strm[:o2.nstream]]
+        out = None
+        if gather:
+            out = torch.zeros(o2.records_bytes + 64, dtype=torch.uint8, device=dev)
+            if o2.nfrags:
+                d_frags = torch.frombuffer(bytearray(bytes(frags)[:o2.nfrags * ctypes.sizeof(mck_wal_fragment)]),
+                                           dtype=torch.uint8).to(dev)
+                check(lib.mck_wal_gather_batch(img.data_ptr(), d_frags.data_ptr(), o2.nfrags, out.data_ptr(),
+                                               _stream(st)), "mck_wal_gather_batch")
+            out = out[:o2.records_bytes]
+        blocks = torch.from_numpy(blk[:nblocks]) if nblocks else None
+    return WalRecovery(out, offs[:o2.nrecords], lens[:o2.nrecords], foffs[:o2.nrecords], x3, blocks, reports,
+                       o2.dropped_bytes, "".join("Corruption: " + r[2] for r in reports), o2.compression_type,
+                       stream_l, frags, o2.nfrags, wal, info)
 
 
 def WalReadRecords(wal: bytes, log_number: int = 0, device=None, stream=None):
@@ -738,7 +807,7 @@ def WalReadRecords(wal: bytes, log_number: int = 0, device=None, stream=None):
     checksum; the physical records' CRCs per 32 KiB block.  Returns (records
     uint8 tensor, offsets, lengths, xxh3 uint64 numpy, per-block verify
     results).  See WalRecover for the reports and other recovery modes."""
-    r = WalRecover(wal, log_number, device=device, stream=stream)
+    r = WalRecover(wal, log_number, device=device, stream=stream, gather=True)
     return r.records, r.rec_offsets, r.rec_lengths, r.record_checksums, r.blocks
 
 
@@ -937,7 +1006,7 @@ class FragmentBufferedReader:
 
 __all__ += ["wal_plan", "WalBatchWriter", "mck_wal_fragment", "wal_list_records", "WalReadRecords",
             "WALRecoveryMode", "wal_read_records", "WalReadPlan", "WalRecover", "WalRecovery",
-            "FragmentBufferedReader"]
+            "FragmentBufferedReader", "wal_recover_batch", "mck_wal_recovery_info"]
 
 
 # ---------------------------------------------------------------------------

@@ -305,6 +305,10 @@ __global__ __launch_bounds__(1024) void k_crc_ragged(Op op, uint32_t first, uint
                      [&](uint32_t i) { return (uint32_t)op.off(i) ^ (uint32_t)op.len(i); },
                      [&] { bh_fill_load(fill, &g_crc_tables); });
       bh_fill_store(op, fill);
+      // every wave's image stores (the injection tables, which read the
+      // un-shift tables) land before anything reuses those LDS bytes: the
+      // row drivers' prologue writes its row-gap maps and descriptors there
+      __syncthreads();
       sh = RowShare{first + lo, 1u, hi - lo};
       filled = true;
     }
@@ -811,7 +815,9 @@ __device__ __forceinline__ bool wal_il_step(const WalIlCtx& X, const WalIlState&
     const uint32_t hb = (16u - (Pl & 15u)) & 15u;  // bytes before the first aligned piece
     const uint32_t hb_end = hb < sp.n ? hb : sp.n;
     const uint32_t tb = (Pl + sp.n) & 15u;
-    const uint32_t tb_beg = sp.n - tb > hb_end ? sp.n - tb : hb_end;
+    // (sp.n < tb: a payload inside one 16-byte granule -- its head bytes
+    // cover it, no tail bytes; no unsigned wraparound)
+    const uint32_t tb_beg = (sp.n >= tb && sp.n - tb > hb_end) ? sp.n - tb : hb_end;
     okh = fin && c < hb_end;
     ebt = tb_beg + c;
     okt = fin && ebt < sp.n;

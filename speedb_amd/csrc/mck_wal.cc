@@ -12,6 +12,7 @@
 
 #include "../../include/speedb_amd/mck.h"
 #include "mck_internal.h"
+#include "mck_walk.h"
 
 namespace {
 // db/log_format.h:22-45
@@ -210,6 +211,15 @@ struct WalReader {
         buf_size = 0;
         return kBadRecordChecksum;
       }
+      if (type == 1 || type == 5) {  // a full-type record: its slot in the block (mck_wal_recover)
+        const uint64_t blk = buf_off / MCK_WAL_kBlockSize;
+        if (blk != full_blk) {
+          full_blk = blk;
+          full_k = 0;
+        }
+        last_full_k = full_k++;
+        if (full_counts) (*full_counts)[blk]++;
+      }
       *frag_off = buf_off + hs;
       *frag_len = length;
       buf_off += hs + length;
@@ -219,6 +229,12 @@ struct WalReader {
     }
   }
   bool read_ok = false;  // the last read_physical returned a record
+  // full-type records (kFullType / kRecyclableFullType) returned per block, in
+  // walk order: the device's recover pass hashes them in the same order
+  // (k_wal_recover), so record k of block b is slot (b, k)
+  uint64_t full_blk = ~0ull;
+  uint32_t full_k = 0, last_full_k = 0;
+  std::vector<uint32_t>* full_counts = nullptr;  // per block (optional)
 };
 
 }  // namespace
@@ -254,28 +270,21 @@ extern "C" const char* mck_wal_reason_string(int reason) {
   }
 }
 
-extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t log_number, int recovery_mode,
-                                    const mck_wal_block_result* verified, mck_wal_read_out* out) {
-  mck_internal_set_error("");
-  if ((!wal && nbytes) || !out) {
-    mck_internal_set_error("wal / out is NULL");
-    return MCK_EINVAL;
+namespace mck_walk {
+// log::Reader (checksum = true) reading the whole image: ReadRecord until it
+// returns false, over the device's verdicts (NULL = trust every CRC).
+int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recovery_mode,
+             const mck_wal_block_result* verified, bool count_full, WalWalk& W) {
+  WalReader R{d, nbytes, log_number, recovery_mode, verified};
+  if (count_full) {
+    W.full_counts.assign((nbytes + MCK_WAL_kBlockSize - 1) / MCK_WAL_kBlockSize, 0u);
+    R.full_counts = &W.full_counts;
   }
-  static_assert(offsetof(mck_wal_read_out, compression_type) == MCK_WAL_READ_OUT_V1_SIZE, "v1 layout");
-  if (out->struct_size < MCK_WAL_READ_OUT_V1_SIZE) {
-    mck_internal_set_error("mck_wal_read_out.struct_size not set (sizeof(mck_wal_read_out))");
-    return MCK_EINVAL;
-  }
-  const bool has_stream = out->struct_size >= sizeof(mck_wal_read_out);
-  if (recovery_mode < MCK_WAL_kTolerateCorruptedTailRecords || recovery_mode > MCK_WAL_kSkipAnyCorruptedRecords) {
-    mck_internal_set_error("unknown WALRecoveryMode");
-    return MCK_EINVAL;
-  }
-  WalReader R{static_cast<const uint8_t*>(wal), nbytes, log_number, recovery_mode, verified};
   TsRecorder ts;
-  std::vector<mck_wal_fragment> fr;
-  std::vector<uint64_t> roff, rfile;
-  std::vector<uint32_t> rlen;
+  std::vector<mck_wal_fragment>& fr = W.fr;
+  std::vector<uint64_t>& roff = W.roff;
+  std::vector<uint64_t>& rfile = W.rfile;
+  std::vector<uint32_t>& rlen = W.rlen;
   uint64_t dst = 0;             // end of the reassembled buffer
   uint64_t cur_start = 0;       // dst offset of scratch (the record being assembled)
   uint64_t cur_file = 0;        // file offset of its first physical record
@@ -285,7 +294,7 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
   // fragment of fr the stream entry it came from
   uint32_t compression = 0;
   bool compression_read = false;
-  std::vector<mck_wal_fragment> stream;
+  std::vector<mck_wal_fragment>& stream = W.stream;
   std::vector<uint64_t> fr_sidx;
   auto feed = [&](uint64_t off, uint32_t len, uint32_t type) {
     if (compression) stream.push_back(mck_wal_fragment{off, ~0ull, len, (uint8_t)type, 0, 0});
@@ -307,12 +316,15 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
     cur_file = file_off;
     scratch_append(off, len, type);
   };
-  auto emit = [&] {  // ReadRecord returns *record = scratch
-    for (size_t k = cur_first_frag; k < fr.size(); k++)
-      if (fr_sidx[k] != ~0ull) stream[fr_sidx[k]].dst_off = k;
+  auto emit = [&](uint64_t blk, uint32_t k) {  // ReadRecord returns *record = scratch
+    for (size_t j = cur_first_frag; j < fr.size(); j++)
+      if (fr_sidx[j] != ~0ull) stream[fr_sidx[j]].dst_off = j;
     roff.push_back(cur_start);
     rlen.push_back((uint32_t)(dst - cur_start));
     rfile.push_back(cur_file);
+    W.rblk.push_back(blk);
+    W.rk.push_back(k);
+    W.rfrag.push_back(cur_first_frag);
     cur_start = dst;
     cur_first_frag = fr.size();
     R.first_record_read = true;
@@ -337,7 +349,7 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
       if (t == 1 || t == 5) {  // kFullType
         if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_PARTIAL_WITHOUT_END_1);
         scratch_assign(foff, flen, (uint8_t)t, phys);
-        emit();
+        emit(R.full_blk, R.last_full_k);
         break;
       } else if (t == 2 || t == 6) {  // kFirstType
         if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_PARTIAL_WITHOUT_END_2);
@@ -353,7 +365,7 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
           R.report(phys, flen, MCK_WAL_R_MISSING_START_2);
         } else {
           scratch_append(foff, flen, (uint8_t)t);
-          emit();
+          emit(~0ull, 0u);
           break;
         }
       } else if (t == (int)kSetCompressionType) {  // :167-188
@@ -435,54 +447,97 @@ extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t l
       }
     }
   }
-  if (R.err) {
-    mck_internal_set_error("verify results do not match the WAL image (a record the device did not reach)");
-    return R.err;
-  }
+  if (R.err) return R.err;
   scratch_clear();
-  if (compression && !has_stream) {
+  W.rfrag.push_back(fr.size());
+  W.records_bytes = dst;
+  W.reports = std::move(R.reports);
+  W.dropped = R.dropped;
+  W.end_offset = R.end_of_buffer_offset - R.buf_size;
+  W.compression = compression;
+  return MCK_OK;
+}
+
+// mck_wal_read_out (caller arrays, *_cap sizes) from a walk
+int wal_copy_out(const WalWalk& W, mck_wal_read_out* out) {
+  const bool has_stream = out->struct_size >= sizeof(mck_wal_read_out);
+  if (W.compression && !has_stream) {
     mck_internal_set_error("compressed WAL: mck_wal_read_out.struct_size has no room for the compression fields");
     return MCK_ENOTSUP;
   }
-  out->nfrags = fr.size();
-  out->nrecords = roff.size();
-  out->records_bytes = dst;
-  out->nreports = R.reports.size();
-  out->dropped_bytes = R.dropped;
-  out->end_offset = R.end_of_buffer_offset - R.buf_size;
+  out->nfrags = W.fr.size();
+  out->nrecords = W.roff.size();
+  out->records_bytes = W.records_bytes;
+  out->nreports = W.reports.size();
+  out->dropped_bytes = W.dropped;
+  out->end_offset = W.end_offset;
   if (out->frags) {
-    if (out->frag_cap < fr.size()) {
+    if (out->frag_cap < W.fr.size()) {
       mck_internal_set_error("frags capacity too small");
       return MCK_EINVAL;
     }
-    if (!fr.empty()) memcpy(out->frags, fr.data(), fr.size() * sizeof(mck_wal_fragment));
+    if (!W.fr.empty()) memcpy(out->frags, W.fr.data(), W.fr.size() * sizeof(mck_wal_fragment));
   }
   if (out->rec_offsets || out->rec_lengths || out->rec_file_offsets) {
-    if (out->rec_cap < roff.size()) {
+    if (out->rec_cap < W.roff.size()) {
       mck_internal_set_error("records capacity too small");
       return MCK_EINVAL;
     }
-    if (!roff.empty()) {
-      if (out->rec_offsets) memcpy(out->rec_offsets, roff.data(), roff.size() * 8);
-      if (out->rec_lengths) memcpy(out->rec_lengths, rlen.data(), rlen.size() * 4);
-      if (out->rec_file_offsets) memcpy(out->rec_file_offsets, rfile.data(), rfile.size() * 8);
+    if (!W.roff.empty()) {
+      if (out->rec_offsets) memcpy(out->rec_offsets, W.roff.data(), W.roff.size() * 8);
+      if (out->rec_lengths) memcpy(out->rec_lengths, W.rlen.data(), W.rlen.size() * 4);
+      if (out->rec_file_offsets) memcpy(out->rec_file_offsets, W.rfile.data(), W.rfile.size() * 8);
     }
   }
   if (out->reports) {
-    const size_t n = std::min<size_t>(out->report_cap, R.reports.size());
-    if (n) memcpy(out->reports, R.reports.data(), n * sizeof(mck_wal_report));
+    const size_t n = std::min<size_t>(out->report_cap, W.reports.size());
+    if (n) memcpy(out->reports, W.reports.data(), n * sizeof(mck_wal_report));
   }
   if (!has_stream) return MCK_OK;
-  out->compression_type = compression;
-  out->nstream = stream.size();
+  out->compression_type = W.compression;
+  out->nstream = W.stream.size();
   if (out->stream) {
-    if (out->stream_cap < stream.size()) {
+    if (out->stream_cap < W.stream.size()) {
       mck_internal_set_error("stream capacity too small");
       return MCK_EINVAL;
     }
-    if (!stream.empty()) memcpy(out->stream, stream.data(), stream.size() * sizeof(mck_wal_fragment));
+    if (!W.stream.empty()) memcpy(out->stream, W.stream.data(), W.stream.size() * sizeof(mck_wal_fragment));
   }
   return MCK_OK;
+}
+
+int check_read_args(const void* wal, uint64_t nbytes, int recovery_mode, const mck_wal_read_out* out) {
+  if ((!wal && nbytes) || !out) {
+    mck_internal_set_error("wal / out is NULL");
+    return MCK_EINVAL;
+  }
+  static_assert(offsetof(mck_wal_read_out, compression_type) == MCK_WAL_READ_OUT_V1_SIZE, "v1 layout");
+  if (out->struct_size != MCK_WAL_READ_OUT_V1_SIZE && out->struct_size != sizeof(mck_wal_read_out)) {
+    // a struct of another (older or unknown) layout -- e.g. one built before
+    // struct_size became the first field -- is refused, never written
+    mck_internal_set_error("mck_wal_read_out.struct_size is neither MCK_WAL_READ_OUT_V1_SIZE nor sizeof(mck_wal_read_out)");
+    return MCK_EINVAL;
+  }
+  if (recovery_mode < MCK_WAL_kTolerateCorruptedTailRecords || recovery_mode > MCK_WAL_kSkipAnyCorruptedRecords) {
+    mck_internal_set_error("unknown WALRecoveryMode");
+    return MCK_EINVAL;
+  }
+  return MCK_OK;
+}
+}  // namespace mck_walk
+
+using namespace mck_walk;
+
+extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t log_number, int recovery_mode,
+                                    const mck_wal_block_result* verified, mck_wal_read_out* out) {
+  mck_internal_set_error("");
+  if (int rc = check_read_args(wal, nbytes, recovery_mode, out)) return rc;
+  WalWalk W;
+  if (int rc = wal_walk(static_cast<const uint8_t*>(wal), nbytes, log_number, recovery_mode, verified, false, W)) {
+    mck_internal_set_error("verify results do not match the WAL image (a record the device did not reach)");
+    return rc;
+  }
+  return wal_copy_out(W, out);
 }
 
 // The reassembly plan alone: mck_wal_read_records without CRCs, in the

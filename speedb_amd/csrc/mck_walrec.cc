@@ -1,0 +1,318 @@
+// mck_walrec.cc -- mck_wal_recover: WAL recovery with the record checksums,
+// the checksum work in ONE device pass (mck_wal_recover_batch,
+// mck_walrec.hpp), the reader's walk on the host (mck_walk.h).
+#include <hip/hip_runtime_api.h>
+#include <string.h>
+
+#include <chrono>
+#include <new>
+#include <vector>
+
+#include "../../include/speedb_amd/mck.h"
+#include "mck_internal.h"
+#include "mck_walk.h"
+
+using namespace mck_walk;
+
+// ---------------------------------------------------------------------------
+// WAL recovery with the record checksums (db/db_impl/db_impl_open.cc:1204-1221:
+// ReadRecord(&record, &scratch, mode, &record_checksum) until false), the
+// checksum work in ONE device pass over the image:
+//   1. plan: the host walk trusting every CRC, counting the full-type records
+//      of every block -> dense slots (prefix sum) and the multi-fragment
+//      records;
+//   2. device: mck_wal_recover_batch (every physical record's CRC32C + the
+//      XXH3 of every full-type record in place, into its slot) and, on the same
+//      stream, mck_wal_gather_batch + mck_xxh3_64_batch for the multi-fragment
+//      records only; one readback;
+//   3. if a CRC failed (a block stopped with MCK_WAL_BAD_CHECKSUM), the walk
+//      again over the verdicts (records, drops and reports as the reference's
+//      reader sees them), and its multi-fragment records hashed again.
+// Without a failure the plan IS the reader's walk: the verdicts only change
+// the walk where a checksum fails.
+// ---------------------------------------------------------------------------
+struct mck_wal_recovery {
+  WalWalk W;
+  std::vector<uint64_t> checksums;
+  std::vector<mck_wal_block_result> blocks;  // the device's per-block verdicts
+  mck_wal_recovery_info info{};
+};
+
+namespace {
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Device scratch of one recover call (one allocation, freed in order on the
+// stream).
+struct DevArena {
+  hipStream_t st;
+  char* base = nullptr;
+  size_t used = 0, cap = 0;
+  ~DevArena() {
+    if (base) (void)hipFreeAsync(base, st);
+  }
+  int reserve(size_t bytes) {
+    cap = bytes ? bytes : 16;
+    if (hipMallocAsync(reinterpret_cast<void**>(&base), cap, st) != hipSuccess) {
+      base = nullptr;
+      mck_internal_set_error("hipMallocAsync failed (recover scratch)");
+      return MCK_ENOMEM;
+    }
+    return MCK_OK;
+  }
+  template <class T>
+  T* take(size_t n) {  // 256-byte aligned pieces (the gather output needs 16)
+    T* p = reinterpret_cast<T*>(base + used);
+    used += (n * sizeof(T) + 255) & ~size_t(255);
+    return p;
+  }
+  static size_t need(size_t n, size_t sz) { return (n * sz + 255) & ~size_t(255); }
+};
+
+// The multi-fragment records of a walk: their fragments re-based into one
+// contiguous gather buffer, and each record's (offset, length) in it.
+struct MultiPlan {
+  std::vector<size_t> recs;  // record indices in the walk
+  std::vector<mck_wal_fragment> frags;
+  std::vector<uint64_t> offs;
+  std::vector<uint32_t> lens;
+  uint64_t bytes = 0;
+};
+MultiPlan multi_plan(const WalWalk& W) {
+  MultiPlan M;
+  for (size_t r = 0; r < W.roff.size(); r++) {
+    if (W.rblk[r] != ~0ull) continue;  // one fragment: hashed in place
+    M.recs.push_back(r);
+    M.offs.push_back(M.bytes);
+    M.lens.push_back(W.rlen[r]);
+    for (uint64_t j = W.rfrag[r]; j < W.rfrag[r + 1]; j++) {
+      mck_wal_fragment f = W.fr[j];
+      f.dst_off = M.bytes + (f.dst_off - W.roff[r]);
+      M.frags.push_back(f);
+    }
+    M.bytes += (W.rlen[r] + 15) & ~uint64_t(15);  // 16-aligned records
+  }
+  return M;
+}
+
+// Launch the gather + XXH3 of a multi plan on the stream (results at d_out).
+int launch_multi(const void* wal_dev, const MultiPlan& M, DevArena& A, uint64_t** d_out, hipStream_t st) {
+  *d_out = nullptr;
+  if (M.recs.empty()) return MCK_OK;
+  mck_wal_fragment* d_fr = A.take<mck_wal_fragment>(M.frags.size());
+  uint64_t* d_offs = A.take<uint64_t>(M.offs.size());
+  uint32_t* d_lens = A.take<uint32_t>(M.lens.size());
+  uint8_t* d_buf = A.take<uint8_t>(M.bytes + 64);
+  *d_out = A.take<uint64_t>(M.recs.size());
+  if (hipMemcpyAsync(d_fr, M.frags.data(), M.frags.size() * sizeof(mck_wal_fragment), hipMemcpyHostToDevice, st) ||
+      hipMemcpyAsync(d_offs, M.offs.data(), M.offs.size() * 8, hipMemcpyHostToDevice, st) ||
+      hipMemcpyAsync(d_lens, M.lens.data(), M.lens.size() * 4, hipMemcpyHostToDevice, st)) {
+    mck_internal_set_error("hipMemcpyAsync failed (multi-fragment plan)");
+    return MCK_EHIP;
+  }
+  mck_stream_t s = reinterpret_cast<mck_stream_t>(st);
+  if (!M.frags.empty())
+    if (int rc = mck_wal_gather_batch(wal_dev, d_fr, (uint32_t)M.frags.size(), d_buf, s)) return rc;
+  const mck_spans sp{d_buf, d_offs, d_lens, 0, 0, (uint32_t)M.recs.size()};
+  return mck_xxh3_64_batch(&sp, *d_out, s);
+}
+size_t multi_bytes(const MultiPlan& M) {
+  if (M.recs.empty()) return 0;
+  return DevArena::need(M.frags.size(), sizeof(mck_wal_fragment)) + DevArena::need(M.offs.size(), 8) +
+         DevArena::need(M.lens.size(), 4) + DevArena::need(M.bytes + 64, 1) + DevArena::need(M.recs.size(), 8);
+}
+}  // namespace
+
+extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64_t nbytes, uint32_t log_number,
+                               int recovery_mode, mck_stream_t stream, mck_wal_recovery** out) {
+  mck_internal_set_error("");
+  if (!out || (nbytes && (!wal_host || !wal_dev))) {
+    mck_internal_set_error("wal_host / wal_dev / out is NULL");
+    return MCK_EINVAL;
+  }
+  *out = nullptr;
+  if (recovery_mode < MCK_WAL_kTolerateCorruptedTailRecords || recovery_mode > MCK_WAL_kSkipAnyCorruptedRecords) {
+    mck_internal_set_error("unknown WALRecoveryMode");
+    return MCK_EINVAL;
+  }
+  const uint64_t nblocks = (nbytes + MCK_WAL_kBlockSize - 1) / MCK_WAL_kBlockSize;
+  if (nblocks > 0xFFFFFFFFull) {
+    mck_internal_set_error("WAL image too large");
+    return MCK_EINVAL;
+  }
+  mck_wal_recovery* R = new (std::nothrow) mck_wal_recovery();
+  if (!R) {
+    mck_internal_set_error("out of memory");
+    return MCK_ENOMEM;
+  }
+  const uint8_t* d = static_cast<const uint8_t*>(wal_host);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  double t0 = now_s();
+  // 1. the plan
+  WalWalk plan;
+  if (int rc = wal_walk(d, nbytes, log_number, recovery_mode, nullptr, true, plan)) {
+    delete R;
+    return rc;
+  }
+  std::vector<uint64_t> base(nblocks + 1, 0);
+  for (uint64_t b = 0; b < nblocks; b++) base[b + 1] = base[b] + plan.full_counts[b];
+  const uint64_t nfull = base[nblocks];
+  const MultiPlan M = plan.compression ? MultiPlan{} : multi_plan(plan);
+  R->info.walk_seconds = now_s() - t0;
+  R->info.host_walks = 1;
+  // 2. the device pass (+ the multi-fragment records), one readback
+  t0 = now_s();
+  std::vector<mck_wal_block_result> res(nblocks);
+  std::vector<uint64_t> hashes(nfull), mhash(M.recs.size());
+  int rc = MCK_OK;
+  {
+    DevArena A{st};
+    const size_t need = DevArena::need(nblocks, sizeof(mck_wal_block_result)) + DevArena::need(nblocks + 1, 8) +
+                        DevArena::need(nfull, 8) + multi_bytes(M);
+    if (nblocks && !(rc = A.reserve(need))) {
+      auto* d_res = A.take<mck_wal_block_result>(nblocks);
+      auto* d_base = A.take<uint64_t>(nblocks + 1);
+      auto* d_hash = A.take<uint64_t>(nfull);
+      uint64_t* d_mh = nullptr;
+      if (hipMemcpyAsync(d_base, base.data(), (nblocks + 1) * 8, hipMemcpyHostToDevice, st)) {
+        mck_internal_set_error("hipMemcpyAsync failed (slot bases)");
+        rc = MCK_EHIP;
+      }
+      if (!rc)
+        rc = mck_wal_recover_batch(wal_dev, nbytes, log_number, d_res, d_base, 0, nfull ? d_hash : nullptr, stream);
+      if (!rc) rc = launch_multi(wal_dev, M, A, &d_mh, st);
+      if (!rc && (hipMemcpyAsync(res.data(), d_res, nblocks * sizeof(mck_wal_block_result), hipMemcpyDeviceToHost, st) ||
+                  (nfull && hipMemcpyAsync(hashes.data(), d_hash, nfull * 8, hipMemcpyDeviceToHost, st)) ||
+                  (d_mh && hipMemcpyAsync(mhash.data(), d_mh, mhash.size() * 8, hipMemcpyDeviceToHost, st)))) {
+        mck_internal_set_error("hipMemcpyAsync failed (recover results)");
+        rc = MCK_EHIP;
+      }
+    }
+    if (!rc && hipStreamSynchronize(st)) {
+      mck_internal_set_error("hipStreamSynchronize failed (recover)");
+      rc = MCK_EHIP;
+    }
+  }
+  R->info.device_seconds = now_s() - t0;
+  if (rc) {
+    delete R;
+    return rc;
+  }
+  // 3. a failed checksum changes the walk: walk again over the verdicts
+  bool bad = false;
+  for (uint64_t b = 0; b < nblocks && !bad; b++) bad = res[b].status == MCK_WAL_BAD_CHECKSUM;
+  WalWalk& W = R->W;
+  const MultiPlan* MP = &M;
+  MultiPlan M2;
+  std::vector<uint64_t> mhash2;
+  if (!bad) {
+    W = std::move(plan);
+  } else {
+    t0 = now_s();
+    rc = wal_walk(d, nbytes, log_number, recovery_mode, res.data(), false, W);
+    R->info.walk_seconds += now_s() - t0;
+    R->info.host_walks = 2;
+    if (rc) {
+      mck_internal_set_error("verify results do not match the WAL image (a record the device did not reach)");
+      delete R;
+      return rc;
+    }
+    if (!W.compression) {
+      M2 = multi_plan(W);
+      mhash2.resize(M2.recs.size());
+      t0 = now_s();
+      if (!M2.recs.empty()) {
+        DevArena A{st};
+        uint64_t* d_mh = nullptr;
+        if (!(rc = A.reserve(multi_bytes(M2)))) rc = launch_multi(wal_dev, M2, A, &d_mh, st);
+        if (!rc && (hipMemcpyAsync(mhash2.data(), d_mh, mhash2.size() * 8, hipMemcpyDeviceToHost, st) ||
+                    hipStreamSynchronize(st))) {
+          mck_internal_set_error("recover: multi-fragment readback failed");
+          rc = MCK_EHIP;
+        }
+      }
+      R->info.device_seconds += now_s() - t0;
+      if (rc) {
+        delete R;
+        return rc;
+      }
+      MP = &M2;
+    }
+  }
+  const std::vector<uint64_t>& mh = bad ? mhash2 : mhash;
+  R->blocks = std::move(res);
+  // 4. every record's checksum
+  const size_t nr = W.roff.size();
+  R->info.nrecords = nr;
+  R->info.has_checksums = W.compression ? 0u : 1u;
+  if (!W.compression) {
+    R->checksums.assign(nr, 0);
+    for (size_t r = 0; r < nr; r++) {
+      if (W.rblk[r] == ~0ull) continue;
+      const uint64_t b = W.rblk[r];
+      if (W.rk[r] >= base[b + 1] - base[b]) {  // cannot happen: the plan counted every one
+        mck_internal_set_error("recover: a full record outside its block's slots");
+        delete R;
+        return MCK_EINVAL;
+      }
+      R->checksums[r] = hashes[base[b] + W.rk[r]];
+      R->info.in_place++;
+    }
+    for (size_t j = 0; j < MP->recs.size(); j++) R->checksums[MP->recs[j]] = mh[j];
+    R->info.gathered = MP->recs.size();
+    R->info.gathered_bytes = 0;
+    for (uint32_t n : MP->lens) R->info.gathered_bytes += n;
+  }
+  *out = R;
+  return MCK_OK;
+}
+
+extern "C" int mck_wal_recovery_read_out(const mck_wal_recovery* r, mck_wal_read_out* out) {
+  mck_internal_set_error("");
+  if (!r) {
+    mck_internal_set_error("recovery is NULL");
+    return MCK_EINVAL;
+  }
+  if (int rc = check_read_args(nullptr, 0, MCK_WAL_kTolerateCorruptedTailRecords, out)) return rc;
+  return wal_copy_out(r->W, out);
+}
+
+extern "C" int mck_wal_recovery_checksums(const mck_wal_recovery* r, uint64_t* checksums, uint64_t cap) {
+  mck_internal_set_error("");
+  if (!r) {
+    mck_internal_set_error("recovery is NULL");
+    return MCK_EINVAL;
+  }
+  if (!r->info.has_checksums) {
+    mck_internal_set_error("compressed WAL: the record checksums are over the decompressed records (the caller's)");
+    return MCK_ENOTSUP;
+  }
+  if (r->checksums.empty()) return MCK_OK;
+  if (!checksums || cap < r->checksums.size()) {
+    mck_internal_set_error("checksums capacity too small");
+    return MCK_EINVAL;
+  }
+  memcpy(checksums, r->checksums.data(), r->checksums.size() * 8);
+  return MCK_OK;
+}
+
+extern "C" int mck_wal_recovery_get_info(const mck_wal_recovery* r, mck_wal_recovery_info* info) {
+  if (!r || !info) return MCK_EINVAL;
+  *info = r->info;
+  return MCK_OK;
+}
+
+extern "C" int mck_wal_recovery_block_results(const mck_wal_recovery* r, mck_wal_block_result* results,
+                                              uint64_t cap) {
+  mck_internal_set_error("");
+  if (!r || (!results && !r->blocks.empty()) || cap < r->blocks.size()) {
+    mck_internal_set_error("recovery / results is NULL or the capacity is too small");
+    return MCK_EINVAL;
+  }
+  if (!r->blocks.empty()) memcpy(results, r->blocks.data(), r->blocks.size() * sizeof(mck_wal_block_result));
+  return MCK_OK;
+}
+
+extern "C" void mck_wal_recovery_free(mck_wal_recovery* r) { delete r; }
+

@@ -686,6 +686,9 @@ __device__ __forceinline__ bool x3w_ok(const X3WSpan& sp, uint32_t k, uint32_t g
 }
 // (dword-aligned loads, realigned in x3w_fold: see rd_fix; loads without
 // work read the span's first dwords)
+// (NT = false: the default cache policy, for a fused kernel that re-reads
+// bytes another load of the same wave just brought into L2)
+template <bool NT = true>
 __device__ __forceinline__ X3WLoads x3w_load(const X3WSpan& sp, uint32_t k, const X3Row& X) {
   X3WLoads L;
   const uint32_t g = 4 * k + X.row;
@@ -695,14 +698,14 @@ __device__ __forceinline__ X3WLoads x3w_load(const X3WSpan& sp, uint32_t k, cons
 #pragma unroll
   for (int m = 0; m < 4; m++) {
     const uint32_t st = (uint32_t)(X.st4 + 4 * m);
-    L.d[m] = gload16u(x3w_ok(sp, k, g, st) ? seg + 64 * st + 16 * X.q - sh + 4 : idle);
+    L.d[m] = span_load16<NT>(x3w_ok(sp, k, g, st) ? seg + 64 * st + 16 * X.q - sh + 4 : idle);
   }
   const bool last = k + 1 == sp.units;
   const bool okl = last && sp.lone && (uint32_t)(X.lane >> 2) < sp.nst;
   const uint64_t lone = sp.ptr + 1024ull * sp.nb, lst = sp.ptr + sp.len - 64;
-  L.v = gload16u(okl ? lone + 16 * X.lane - sh + 4 : idle);
+  L.v = span_load16<NT>(okl ? lone + 16 * X.lane - sh + 4 : idle);
   const uint32_t shl = rd_shift(lst);  // the last stripe's own byte offset
-  L.dl = gload16u(last ? lst + 16 * X.q - shl + 4 : idle);
+  L.dl = span_load16<NT>(last ? lst + 16 * X.q - shl + 4 : idle);
   // the realignment dwords only for a span that needs them (x3w_fold skips
   // rd_fix for dword-aligned spans and last stripes; wave-uniform branch)
   L.e0 = L.ev = L.el = 0;
@@ -819,13 +822,14 @@ struct X3RoundLoads {
   uint4 d[4];
   uint32_t e0;  // the dword before the row's segment (byte-misaligned spans)
 };
+template <bool NT = true>
 __device__ __forceinline__ X3RoundLoads x3w_round_load(const X3WSpan& sp, uint32_t k, const X3Row& X) {
   X3RoundLoads R;
   const uint32_t sh = rd_shift(sp.ptr);
   const uint64_t seg = sp.ptr + 1024ull * (4 * k + X.row);
   const uint64_t a = seg + 64 * X.st4 + 16 * X.q - sh + 4;
 #pragma unroll
-  for (int m = 0; m < 4; m++) R.d[m] = gload16u(a + 256 * m);
+  for (int m = 0; m < 4; m++) R.d[m] = span_load16<NT>(a + 256 * m);
   // (rd_shift is 4, not 0, for a dword-aligned span: seg - 4 could lie
   // before the buffer)
   R.e0 = (sp.ptr & 3) ? gload4(seg - sh) : 0u;  // wave-uniform

@@ -36,6 +36,7 @@ __global__ void k_crc_ragged(int* o, int i) {
 }
 __global__ void k_wal_write_il(int* o) { o[0] = 2; }
 __global__ void k_wal_verify(int* o) { o[0] = 3; }
+__global__ void k_wal_recover(int* o) { o[0] = 4; }
 }
 extern "C" void probe_launch(int* o) { hipLaunchKernelGGL(mck::k_crc_ragged, 1, 256, 0, 0, o, 3); }
 """

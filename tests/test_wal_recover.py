@@ -1,0 +1,198 @@
+"""WAL recovery in one device pass (mck_wal_recover_batch / mck_wal_recover,
+row a11): every physical record's CRC32C (db/log_reader.cc:512-525) and the
+XXH3_64bits record_checksum of every logical record ReadRecord returns
+(:107-110 for one fragment, hashed in place by the same kernel; :128-158 for
+fragmented records, gathered and hashed on the same stream) -- what
+DBImpl::RecoverLogFiles asks for (db/db_impl/db_impl_open.cc:1217-1221).
+
+Checked against the CPU oracle (util/xxhash.cc's XXH3_64bits restated,
+pinned by the reference's own vectors) and against mck_wal_verify_batch's
+per-block results for the same images (the CRC half must not change).  The
+reader's own semantics (log_test.cc's cases) run through mck_wal_recover in
+test_wal_reader.py::test_log_reader_cases_on_device."""
+import numpy as np
+import pytest
+
+from formats import K_BLOCK, WalWriter
+
+LOG = 77
+kTolerate, kAbsolute, kPIT, kSkipAny = 0, 1, 2, 3
+
+
+def _payload(rng, n):
+    return rng.integers(0, 256, size=n, dtype=np.uint8).tobytes()
+
+
+def _full_slots(w: WalWriter):
+    """{(block, k): (file offset of header, payload length)} of every
+    full-type physical record, k = its index among the block's full records."""
+    out, cnt = {}, {}
+    for off, t, n in w.records:
+        if t in (1, 5):
+            b = off // K_BLOCK
+            k = cnt.get(b, 0)
+            cnt[b] = k + 1
+            out[(b, k)] = (off, n)
+    return out
+
+
+# payload lengths around the XXH3 length classes (16, 128, 240), the 1 KiB
+# segment / 64-byte stripe grid and the wave unit (4 segments), and the
+# largest one-block record (32761 / 32757 bytes)
+EDGE_LENS = [0, 1, 3, 4, 8, 9, 16, 17, 128, 129, 239, 240, 241, 255, 256, 257, 1023, 1024, 1025, 1087, 1088,
+             1089, 2047, 2048, 3071, 3072, 4095, 4096, 4097, 4160, 5120, 8191, 8192, 8193, 16383, 16384,
+             16385, 20000, 32761]
+
+
+def _image(oracle, recycle, lens, seed):
+    rng = np.random.default_rng(seed)
+    w = WalWriter(oracle, log_number=LOG, recycle=recycle)
+    recs = []
+    for n in lens:
+        p = _payload(rng, n)
+        w.add_record(p)
+        recs.append(p)
+    return w, recs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True])
+def test_recover_batch_equals_verify_and_oracle(gpu, oracle, recycle):
+    """Per-block results identical to mck_wal_verify_batch; the hash of the
+    k-th full record of block b at slot b * S + k equals the oracle's XXH3 of
+    its payload, for every edge length at many block offsets."""
+    import speedb_amd as S
+    torch = gpu
+    rng = np.random.default_rng(5)
+    lens = EDGE_LENS * 3 + [int(x) for x in rng.integers(0, 40000, size=60)]
+    rng.shuffle(lens)
+    w, _ = _image(oracle, recycle, lens, 11)
+    img = bytes(w.buf)
+    d = torch.frombuffer(bytearray(img + bytes(64)), dtype=torch.uint8).cuda()
+    ver = S.wal_verify_batch(d, len(img), LOG).cpu().numpy()
+    slots = 64
+    res, h = S.wal_recover_batch(d, len(img), LOG, slots_per_block=slots)
+    assert (res.cpu().numpy() == ver).all()
+    assert (ver[:, 1] == 0).all()
+    hv = h.cpu().numpy().view(np.uint64)
+    full = _full_slots(w)
+    assert full and max(k for _, k in full) < slots
+    for (b, k), (off, n) in full.items():
+        hs = 11 if recycle else 7
+        assert int(hv[b * slots + k]) == oracle.XXH3(img[off + hs:off + hs + n]), (b, k, n)
+
+
+@pytest.mark.gpu
+def test_recover_batch_dense_slots_and_caps(gpu, oracle):
+    """slot_base: record k of block b at slot_base[b] + k, only for k <
+    slot_base[b + 1] - slot_base[b] (nothing is written past a block's cap:
+    the guard words survive); CRC only when no hash array is given."""
+    import speedb_amd as S
+    torch = gpu
+    rng = np.random.default_rng(9)
+    lens = [int(x) for x in rng.integers(0, 3000, size=400)]
+    w, _ = _image(oracle, False, lens, 3)
+    img = bytes(w.buf)
+    d = torch.frombuffer(bytearray(img + bytes(64)), dtype=torch.uint8).cuda()
+    full = _full_slots(w)
+    nb = (len(img) + K_BLOCK - 1) // K_BLOCK
+    counts = np.zeros(nb, np.int64)
+    for (b, k) in full:
+        counts[b] = max(counts[b], k + 1)
+    caps = np.maximum(counts - (np.arange(nb) % 3), 0)  # some blocks get fewer slots than records
+    base = np.zeros(nb + 1, np.int64)
+    base[1:] = np.cumsum(caps)
+    guard = 0x5A5A5A5A5A5A5A5A - (1 << 64)
+    hashes = torch.full((int(base[-1]) + 8,), guard, dtype=torch.int64, device="cuda")
+    res, h = S.wal_recover_batch(d, len(img), LOG, slot_base=torch.from_numpy(base).cuda(), hashes=hashes)
+    hv = h.cpu().numpy().view(np.uint64)
+    seen = set()
+    for (b, k), (off, n) in full.items():
+        if k < caps[b]:
+            assert int(hv[base[b] + k]) == oracle.XXH3(img[off + 7:off + 7 + n])
+            seen.add(int(base[b] + k))
+    assert len(seen) == int(base[-1])
+    assert (hv[int(base[-1]):] == np.uint64(guard & ((1 << 64) - 1))).all()
+    res2, none = S.wal_recover_batch(d, len(img), LOG)
+    assert none is None and (res2.cpu().numpy() == res.cpu().numpy()).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True])
+def test_recover_corrupt_records(gpu, oracle, recycle):
+    """A flipped payload byte in a full record stops its block there (as
+    ReadPhysicalRecord's kBadRecordChecksum drops the rest of the block);
+    the records before it in the block keep their hashes; mck_wal_recover's
+    walk then matches mck_wal_read_records over the same verdicts, with a
+    checksum for every record it returns."""
+    import speedb_amd as S
+    torch = gpu
+    rng = np.random.default_rng(21)
+    lens = [int(x) for x in rng.integers(100, 6000, size=300)]
+    w, _ = _image(oracle, recycle, lens, 8)
+    img = bytearray(w.buf)
+    hs = 11 if recycle else 7
+    fulls = [(o, n) for o, t, n in w.records if t in (1, 5) and n > 20]
+    for o, n in fulls[5::37]:
+        img[o + hs + n // 2] ^= 0x10
+    img = bytes(img)
+    d = torch.frombuffer(bytearray(img + bytes(64)), dtype=torch.uint8).cuda()
+    ver = S.wal_verify_batch(d, len(img), LOG).cpu().numpy()
+    res, h = S.wal_recover_batch(d, len(img), LOG, slots_per_block=32)
+    assert (res.cpu().numpy() == ver).all() and (ver[:, 1] == 1).any()
+    for mode in (kTolerate, kAbsolute, kPIT, kSkipAny):
+        r = S.WalRecover(img, LOG, mode)
+        plan = S.wal_read_records(img, LOG, mode, ver)
+        assert r.message == plan.message and r.dropped_bytes == plan.dropped_bytes
+        recs = r.Records()
+        assert len(recs) == len(plan.rec_lengths)
+        assert [int(x) for x in r.record_checksums] == [oracle.XXH3(x) for x in recs]
+        assert r.info.host_walks == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recycle", [False, True])
+def test_wal_recover_mixed_records_at_scale(gpu, oracle, recycle):
+    """A group-commit-shaped log written by the device writer (records of
+    100 B - 4 KiB, the realistic mix the bench times): every record and
+    every record_checksum bit-exact, the one-fragment records hashed in the
+    recover pass, the block-straddling ones gathered."""
+    import speedb_amd as S
+    torch = gpu
+    rng = np.random.default_rng(31)
+    n = 40000
+    lens = rng.integers(100, 4097, size=n).astype(np.int64)
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum(lens)[:-1]
+    src = torch.randint(0, 256, (int(lens.sum()) + 64,), dtype=torch.uint8, device="cuda")
+    log = S.WalBatchWriter(LOG, recycle_log_files=recycle).AddRecords(src, offs, lens)
+    img = bytes(log.cpu().numpy().tobytes())
+    dev = torch.zeros(len(img) + 64, dtype=torch.uint8, device="cuda")
+    dev[:len(img)] = log
+    r = S.WalRecover(img, LOG, kTolerate, wal_dev=dev)
+    host_src = src.cpu().numpy().tobytes()
+    want = [host_src[o:o + k] for o, k in zip(offs, lens)]
+    got = r.Records()
+    assert got == want and r.dropped_bytes == 0
+    assert [int(x) for x in r.record_checksums] == [oracle.XXH3(x) for x in want]
+    assert r.info.in_place + r.info.gathered == n and r.info.gathered > 0 and r.info.in_place > 0
+    assert r.info.host_walks == 1
+
+
+@pytest.mark.gpu
+def test_recover_configs3_shape(gpu, oracle):
+    """configs[3]'s layout (one kFullType 32761-byte record per 32 KiB
+    block), more blocks than the grid has waves: every block's hash at slot
+    b equals the oracle's XXH3 of its payload, verify results all OK."""
+    import speedb_amd as S
+    from speedb_amd import workloads as W
+    torch = gpu
+    im = W.WalImage(6000, "cuda", seed=4, log_number=LOG)
+    res, h = S.wal_recover_batch(im.data, im.nbytes, LOG, slots_per_block=1)
+    r = res.cpu().numpy()
+    assert (r[:, 0] == 1).all() and (r[:, 1] == 0).all()
+    host = im.data[:im.nbytes].cpu().numpy().reshape(-1, K_BLOCK)
+    hv = h.cpu().numpy().view(np.uint64)
+    for b in range(im.nblocks):
+        assert int(hv[b]) == oracle.XXH3(host[b, 7:].tobytes()), b
+    torch.cuda.synchronize()
