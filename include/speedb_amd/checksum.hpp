@@ -22,6 +22,7 @@
 #include <memory>
 #include <stdexcept>
 #include <string>
+#include <string_view>
 #include <vector>
 
 #include "mck.h"
@@ -282,6 +283,124 @@ inline uint32_t PhysicalRecordCrc(RecordType t, const char* payload, size_t n, u
   crc = crc32c::Crc32cCombine(crc, payload_crc, n);
   return crc32c::Mask(crc);
 }
+
+// include/rocksdb/options.h:383-420
+enum class WALRecoveryMode : char {
+  kTolerateCorruptedTailRecords = MCK_WAL_kTolerateCorruptedTailRecords,
+  kAbsoluteConsistency = MCK_WAL_kAbsoluteConsistency,
+  kPointInTimeRecovery = MCK_WAL_kPointInTimeRecovery,
+  kSkipAnyCorruptedRecords = MCK_WAL_kSkipAnyCorruptedRecords,
+};
+
+// log::Reader::ReadRecord (db/log_reader.cc:69-321) as DBImpl::RecoverLogFiles
+// drives it (db/db_impl/db_impl_open.cc:1204-1221: records until false, each
+// with its XXH3 record_checksum), over the engine's one-pass recovery
+// (mck_wal_recover): Recover() runs the device pass and the reader's walk for
+// the whole log once; ReadRecord() then hands out the records in order, with
+// the reporter's Corruption(bytes, status) calls made inside the ReadRecord
+// call where the reference makes them (mck_wal_recovery_report_positions).
+// A record is a view into the caller's host image (one fragment) or
+// reassembled into *scratch (fragmented), as the reference returns it.
+class RecoveryReader {
+ public:
+  class Reporter {  // log::Reader::Reporter (db/log_reader.h:41-48)
+   public:
+    virtual ~Reporter() {}
+    virtual void Corruption(size_t bytes, const Status& status) = 0;
+  };
+  RecoveryReader(Reporter* reporter, uint64_t log_num) : reporter_(reporter), log_num_(log_num) {}
+  ~RecoveryReader() { mck_wal_recovery_free(rec_); }
+  RecoveryReader(const RecoveryReader&) = delete;
+  void operator=(const RecoveryReader&) = delete;
+
+  // The whole log: wal_host (the file's bytes) and the same nbytes at
+  // wal_dev (device memory, readable 16 bytes past nbytes).
+  Status Recover(const char* wal_host, const void* wal_dev, uint64_t nbytes, WALRecoveryMode mode,
+                 mck_stream_t stream = nullptr) {
+    mck_wal_recovery_free(rec_);
+    rec_ = nullptr;
+    host_ = wal_host;
+    mode_ = mode;
+    next_ = next_report_ = 0;
+    int rc = mck_wal_recover(wal_host, wal_dev, nbytes, static_cast<uint32_t>(log_num_), static_cast<int>(mode),
+                             stream, &rec_);
+    if (rc) return FromRc(rc, "mck_wal_recover");
+    mck_wal_read_out o{};
+    o.struct_size = sizeof(o);
+    if ((rc = mck_wal_recovery_read_out(rec_, &o))) return FromRc(rc, "mck_wal_recovery_read_out");
+    frags_.resize(o.nfrags);
+    roff_.resize(o.nrecords);
+    rlen_.resize(o.nrecords);
+    rfile_.resize(o.nrecords);
+    reports_.resize(o.nreports);
+    report_pos_.resize(o.nreports);
+    o.frags = frags_.data();
+    o.frag_cap = frags_.size();
+    o.rec_offsets = roff_.data();
+    o.rec_lengths = rlen_.data();
+    o.rec_file_offsets = rfile_.data();
+    o.rec_cap = roff_.size();
+    o.reports = reports_.data();
+    o.report_cap = reports_.size();
+    if ((rc = mck_wal_recovery_read_out(rec_, &o))) return FromRc(rc, "mck_wal_recovery_read_out");
+    if ((rc = mck_wal_recovery_report_positions(rec_, report_pos_.data(), report_pos_.size())))
+      return FromRc(rc, "mck_wal_recovery_report_positions");
+    if ((rc = mck_wal_recovery_get_info(rec_, &info_))) return FromRc(rc, "mck_wal_recovery_get_info");
+    checksums_.assign(roff_.size(), 0);
+    if (info_.has_checksums && (rc = mck_wal_recovery_checksums(rec_, checksums_.data(), checksums_.size())))
+      return FromRc(rc, "mck_wal_recovery_checksums");
+    return Status::OK();
+  }
+
+  // record_checksum: XXH3_64bits of the record (compressed logs: unset, the
+  // reference hashes the decompressed record).  mode must be Recover()'s.
+  bool ReadRecord(std::string_view* record, std::string* scratch,
+                  WALRecoveryMode mode = WALRecoveryMode::kTolerateCorruptedTailRecords,
+                  uint64_t* record_checksum = nullptr) {
+    scratch->clear();
+    *record = std::string_view();
+    if (mode != mode_) throw std::invalid_argument("RecoveryReader: the recovery mode of Recover() is fixed");
+    ForwardReports(next_);
+    if (next_ >= roff_.size()) return false;
+    const size_t r = next_++;
+    size_t f = frag_idx_;
+    while (f < frags_.size() && frags_[f].dst_off < roff_[r]) f++;
+    size_t e = f;
+    while (e < frags_.size() && (frags_[e].dst_off < roff_[r] + rlen_[r] || (e == f && rlen_[r] == 0))) e++;
+    frag_idx_ = e;
+    if (e - f == 1) {  // one fragment: a view of the image
+      *record = std::string_view(host_ + frags_[f].src_off, frags_[f].length);
+    } else {
+      for (size_t k = f; k < e; k++) scratch->append(host_ + frags_[k].src_off, frags_[k].length);
+      *record = std::string_view(*scratch);
+    }
+    last_record_offset_ = rfile_[r];
+    if (record_checksum && info_.has_checksums) *record_checksum = checksums_[r];
+    return true;
+  }
+  uint64_t LastRecordOffset() const { return last_record_offset_; }
+  const mck_wal_recovery_info& info() const { return info_; }
+
+ private:
+  void ForwardReports(size_t upto) {
+    for (; next_report_ < reports_.size() && report_pos_[next_report_] <= upto; next_report_++)
+      if (reporter_)
+        reporter_->Corruption(static_cast<size_t>(reports_[next_report_].bytes),
+                              Status::Corruption(mck_wal_reason_string(reports_[next_report_].reason)));
+  }
+  Reporter* reporter_;
+  uint64_t log_num_;
+  const char* host_ = nullptr;
+  WALRecoveryMode mode_ = WALRecoveryMode::kTolerateCorruptedTailRecords;
+  mck_wal_recovery* rec_ = nullptr;
+  mck_wal_recovery_info info_{};
+  std::vector<mck_wal_fragment> frags_;
+  std::vector<uint64_t> roff_, rfile_, checksums_, report_pos_;
+  std::vector<uint32_t> rlen_;
+  std::vector<mck_wal_report> reports_;
+  size_t next_ = 0, next_report_ = 0, frag_idx_ = 0;
+  uint64_t last_record_offset_ = 0;
+};
 }  // namespace log
 
 // util/hash.h:45 NPHash64 / util/hash.cc:81 Hash64 -- XXPH3 on the GPU

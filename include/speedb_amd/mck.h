@@ -455,6 +455,13 @@ int mck_wal_recovery_get_info(const mck_wal_recovery* r, mck_wal_recovery_info* 
  * cap >= ceil(nbytes / 32768). */
 int mck_wal_recovery_block_results(const mck_wal_recovery* r, mck_wal_block_result* results,
                                    uint64_t cap);
+/* Where each report of mck_wal_recovery_read_out falls in the record stream:
+ * positions[i] = the records returned before report i, i.e. the reader's
+ * Reporter::Corruption call for it happens inside the ReadRecord call that
+ * returns record positions[i] (== nrecords: the final call, which returns
+ * false).  cap >= nreports.  What a log::Reader::Reporter adapter needs to
+ * replay the reports in the reference's order (integration/rocksdb_adapters.h). */
+int mck_wal_recovery_report_positions(const mck_wal_recovery* r, uint64_t* positions, uint64_t cap);
 void mck_wal_recovery_free(mck_wal_recovery* r);
 
 /* Text of a MCK_WAL_R_* reason ("checksum mismatch", "unknown record type

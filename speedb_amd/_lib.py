@@ -157,6 +157,7 @@ SIGNATURES = [
     ("mck_wal_recovery_checksums", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("mck_wal_recovery_get_info", ctypes.c_int, [vp, vp]),
     ("mck_wal_recovery_block_results", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
+    ("mck_wal_recovery_report_positions", ctypes.c_int, [vp, vp, ctypes.c_uint64]),
     ("mck_wal_recovery_free", None, [vp]),
     ("mck_wal_tail_create", ctypes.c_int, [ctypes.c_uint32, vp]),
     ("mck_wal_tail_destroy", None, [vp]),

@@ -137,8 +137,13 @@ struct WalReader {
 
   void report(uint64_t off, uint64_t bytes, int reason) {
     reports.push_back(mck_wal_report{off, bytes, reason, 0});
+    if (records_so_far) report_pos.push_back(records_so_far->size());
     dropped += bytes;
   }
+  // per report: the records returned before it (the ReadRecord call that
+  // reported it returns record report_pos[i], or false at the end)
+  const std::vector<uint64_t>* records_so_far = nullptr;
+  std::vector<uint64_t> report_pos;
   bool strict() const {  // kAbsoluteConsistency / kPointInTimeRecovery
     return mode == MCK_WAL_kAbsoluteConsistency || mode == MCK_WAL_kPointInTimeRecovery;
   }
@@ -276,6 +281,7 @@ namespace mck_walk {
 int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recovery_mode,
              const mck_wal_block_result* verified, bool count_full, WalWalk& W) {
   WalReader R{d, nbytes, log_number, recovery_mode, verified};
+  R.records_so_far = &W.roff;
   if (count_full) {
     W.full_counts.assign((nbytes + MCK_WAL_kBlockSize - 1) / MCK_WAL_kBlockSize, 0u);
     R.full_counts = &W.full_counts;
@@ -452,6 +458,7 @@ int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recover
   W.rfrag.push_back(fr.size());
   W.records_bytes = dst;
   W.reports = std::move(R.reports);
+  W.report_pos = std::move(R.report_pos);
   W.dropped = R.dropped;
   W.end_offset = R.end_of_buffer_offset - R.buf_size;
   W.compression = compression;

@@ -21,6 +21,7 @@ struct WalWalk {
   std::vector<uint64_t> rfrag;  // record r's fragments: fr[rfrag[r] .. rfrag[r + 1])
   std::vector<uint32_t> full_counts;  // per block (count_full)
   std::vector<mck_wal_report> reports;
+  std::vector<uint64_t> report_pos;  // per report: records returned before it
   uint64_t dropped = 0, end_offset = 0, records_bytes = 0;
   uint32_t compression = 0;
   std::vector<mck_wal_fragment> stream;

@@ -314,5 +314,15 @@ extern "C" int mck_wal_recovery_block_results(const mck_wal_recovery* r, mck_wal
   return MCK_OK;
 }
 
+extern "C" int mck_wal_recovery_report_positions(const mck_wal_recovery* r, uint64_t* positions, uint64_t cap) {
+  mck_internal_set_error("");
+  if (!r || (!positions && !r->W.report_pos.empty()) || cap < r->W.report_pos.size()) {
+    mck_internal_set_error("recovery / positions is NULL or the capacity is too small");
+    return MCK_EINVAL;
+  }
+  if (!r->W.report_pos.empty()) memcpy(positions, r->W.report_pos.data(), r->W.report_pos.size() * 8);
+  return MCK_OK;
+}
+
 extern "C" void mck_wal_recovery_free(mck_wal_recovery* r) { delete r; }
 

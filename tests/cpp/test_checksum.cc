@@ -225,6 +225,94 @@ TEST(Log, PhysicalRecordCrc) {
   }
 }
 
+// log::Writer restated on the host (db/log_writer.cc:79-175, 263-311; legacy
+// headers), CRCs from the mirror's PhysicalRecordCrc.
+static void LogWrite(std::string* log, uint32_t* block_offset, const std::string& rec) {
+  size_t left = rec.size(), ptr = 0;
+  bool begin = true;
+  do {
+    const uint32_t leftover = log::kBlockSize - *block_offset;
+    if (leftover < (uint32_t)log::kHeaderSize) {
+      log->append(leftover, '\0');
+      *block_offset = 0;
+    }
+    const size_t avail = log::kBlockSize - *block_offset - log::kHeaderSize;
+    const size_t frag = left < avail ? left : avail;
+    const bool end = left == frag;
+    const log::RecordType t = begin && end ? log::kFullType : begin ? log::kFirstType
+                              : end ? log::kLastType : log::kMiddleType;
+    const uint32_t crc = log::PhysicalRecordCrc(t, rec.data() + ptr, frag, 0);
+    char h[7] = {(char)crc, (char)(crc >> 8), (char)(crc >> 16), (char)(crc >> 24), (char)(frag & 0xff),
+                 (char)(frag >> 8), (char)t};
+    log->append(h, 7);
+    log->append(rec.data() + ptr, frag);
+    *block_offset += 7 + (uint32_t)frag;
+    ptr += frag;
+    left -= frag;
+    begin = false;
+  } while (left > 0);
+}
+struct CountingReporter : log::RecoveryReader::Reporter {
+  size_t dropped = 0;
+  std::string message;
+  void Corruption(size_t bytes, const Status& s) override {
+    dropped += bytes;
+    message += s.ToString();
+  }
+};
+static std::string BigString(const std::string& part, size_t n) {  // db/log_test.cc:23-33
+  std::string r;
+  while (r.size() < n) r += part;
+  r.resize(n);
+  return r;
+}
+// db/log_test.cc:342-350 Fragmentation and :513-521 ChecksumMismatch through
+// the one-pass recovery reader, each record with its XXH3 record_checksum.
+TEST(Log, RecoveryReader) {
+  auto run = [](const std::string& img, CountingReporter* rep, std::vector<std::string>* out,
+                std::vector<uint64_t>* sums) {
+    void* d = nullptr;
+    EXPECT_EQ(hipMalloc(&d, img.size() + 64), hipSuccess);
+    EXPECT_EQ(hipMemcpy(d, img.data(), img.size(), hipMemcpyHostToDevice), hipSuccess);
+    log::RecoveryReader reader(rep, 0);
+    EXPECT_TRUE(reader.Recover(img.data(), d, img.size(), log::WALRecoveryMode::kTolerateCorruptedTailRecords).ok());
+    std::string_view rec;
+    std::string scratch;
+    uint64_t sum = 0;
+    while (reader.ReadRecord(&rec, &scratch, log::WALRecoveryMode::kTolerateCorruptedTailRecords, &sum)) {
+      out->emplace_back(rec);
+      sums->push_back(sum);
+    }
+    (void)hipFree(d);
+  };
+  {
+    std::string img;
+    uint32_t bo = 0;
+    const std::vector<std::string> want = {"small", BigString("medium", 50000), BigString("large", 100000)};
+    for (const auto& r : want) LogWrite(&img, &bo, r);
+    CountingReporter rep;
+    std::vector<std::string> got;
+    std::vector<uint64_t> sums;
+    run(img, &rep, &got, &sums);
+    EXPECT_TRUE(got == want);
+    EXPECT_EQ(rep.dropped, 0u);
+    for (size_t i = 0; i < got.size() && i < sums.size(); i++) EXPECT_EQ(sums[i], XXH3_64bits(want[i].data(), want[i].size()));
+  }
+  {
+    std::string img;
+    uint32_t bo = 0;
+    LogWrite(&img, &bo, "foooooo");
+    img[0] = static_cast<char>(img[0] + 14);  // IncrementByte(0, 14)
+    CountingReporter rep;
+    std::vector<std::string> got;
+    std::vector<uint64_t> sums;
+    run(img, &rep, &got, &sums);
+    EXPECT_TRUE(got.empty());
+    EXPECT_EQ(rep.dropped, 14u);
+    EXPECT_TRUE(rep.message.find("checksum mismatch") != std::string::npos);
+  }
+}
+
 // util/hash_test.cc:162-228 (a sample of Hash64SmallValueSchema)
 TEST(HashTest, Hash64SmallValueSchema) {
   EXPECT_EQ(Hash64("", 0, 0), uint64_t{5999572062939766020u});
@@ -532,6 +620,7 @@ int main(int argc, char** argv) {
   RUN(BuiltinChecksumTest, ChecksumSchemas);
   RUN(BlockChecksum, VerifyScalarAndBatched);
   RUN(Log, PhysicalRecordCrc);
+  RUN(Log, RecoveryReader);
   RUN(HashTest, Hash64SmallValueSchema);
   RUN(KvChecksum, ScalarChainEqualsBatch);
   RUN(FileChecksum, Crc32cGenerator);
