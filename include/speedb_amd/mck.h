@@ -290,26 +290,39 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes,
                          uint32_t log_number, mck_wal_block_result* results,
                          mck_stream_t stream);
 
-/* WAL recovery's device pass (db/log_reader.cc:69-584 with a record_checksum,
- * as DBImpl::RecoverLogFiles asks for it, db/db_impl/db_impl_open.cc:1217-1221):
- * ONE read of the image gives mck_wal_verify_batch's per-block results AND
- * the XXH3_64bits of every single-fragment record -- kFullType /
- * kRecyclableFullType, whose record_checksum ReadRecord computes over the
- * fragment in place (:107-110) -- in walk order per block: the k-th
- * full-type record of block b (counting every full-type record the block's
- * walk passes, before its stop) goes to record_hashes[base_b + k] if k <
- * cap_b, with
- *   base_b = slot_base[b], cap_b = slot_base[b + 1] - slot_base[b]
- *            (slot_base: device array [nblocks + 1], e.g. the prefix sum of
- *            the full records per block of a host plan -- mck_wal_recover),
- *   or, slot_base NULL: base_b = b * slots_per_block, cap_b = slots_per_block.
- * record_hashes NULL: the CRC verify alone.  Multi-fragment records
- * (kFirst..kLast) are not hashed here (their bytes are not contiguous):
- * mck_wal_gather_batch + mck_xxh3_64_batch. */
-int mck_wal_recover_batch(const void* wal, uint64_t nbytes, uint32_t log_number,
-                          mck_wal_block_result* results, const uint64_t* slot_base,
-                          uint32_t slots_per_block, uint64_t* record_hashes,
+/* WAL recovery's device pass (DBImpl::RecoverLogFiles reads every record with
+ * a record_checksum, db/db_impl/db_impl_open.cc:1217-1221): for every
+ * physical record of a host plan of the log, its CRC32C verdict
+ * (ReadPhysicalRecord, db/log_reader.cc:512-525) and -- from the SAME read of
+ * its bytes -- the XXH3_64bits of its payload when asked (ReadRecord's
+ * record_checksum of a one-fragment record is the fragment's XXH3,
+ * :107-110).  The plan is what the reader's header walk yields
+ * (mck_wal_recover builds it): per record the payload offset in the image,
+ * its type, its length and the header's stored (masked) CRC. */
+typedef struct mck_wal_rec_desc {
+  uint32_t payload_off_lo; /* payload offset in the image, bits 0-31        */
+  uint32_t hi;             /* bits 0-15: payload offset bits 32-47;
+                              bits 16-23: record type (db/log_format.h);
+                              bit 24: hash the payload (XXH3_64bits)      */
+  uint32_t length;         /* payload bytes                               */
+  uint32_t stored_crc;     /* the header's masked CRC (LE32 at the header) */
+} mck_wal_rec_desc;
+#define MCK_WAL_REC_HASH (1u << 24)
+/* wal: the image in device memory (readable 16 bytes past its end);
+ * recs: device array [count], in file order; crc_ok[i] = 1 when
+ * Mask(Extend(type_crc[+log number], payload)) equals the stored CRC, else
+ * 0; record_hashes[i] = XXH3_64bits(payload) of every record flagged
+ * MCK_WAL_REC_HASH (others untouched).  Device arrays [count]. */
+int mck_wal_recover_batch(const void* wal, const mck_wal_rec_desc* recs, uint32_t count,
+                          uint32_t log_number, uint8_t* crc_ok, uint64_t* record_hashes,
                           mck_stream_t stream);
+/* Host: the plan of a WAL image in host memory -- every physical record of
+ * every 32 KiB block, each block walked from offset 0 as ReadPhysicalRecord
+ * parses it (the records any reader of the log can reach), in file order,
+ * MCK_WAL_REC_HASH set on the full-type ones (kFullType /
+ * kRecyclableFullType).  out NULL: *count only. */
+int mck_wal_plan_records(const void* wal, uint64_t nbytes, uint32_t log_number,
+                         mck_wal_rec_desc* out, uint64_t cap, uint64_t* count);
 
 /* ---- log::Reader, the whole log (db/log_reader.cc:69-584) ----------------- */
 

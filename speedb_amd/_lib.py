@@ -149,8 +149,8 @@ SIGNATURES = [
     ("mck_wal_gather_batch", ctypes.c_int, [vp, vp, ctypes.c_uint32, vp, vp]),
     ("mck_wal_read_records", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, vp, vp]),
     ("mck_wal_reason_string", ctypes.c_char_p, [ctypes.c_int]),
-    ("mck_wal_recover_batch", ctypes.c_int,
-     [vp, ctypes.c_uint64, ctypes.c_uint32, vp, vp, ctypes.c_uint32, vp, vp]),
+    ("mck_wal_recover_batch", ctypes.c_int, [vp, vp, ctypes.c_uint32, ctypes.c_uint32, vp, vp, vp]),
+    ("mck_wal_plan_records", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint32, vp, ctypes.c_uint64, vp]),
     ("mck_wal_recover", ctypes.c_int,
      [vp, vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, vp, vp]),
     ("mck_wal_recovery_read_out", ctypes.c_int, [vp, vp]),

@@ -346,26 +346,34 @@ def wal_verify_batch(wal, nbytes: Optional[int] = None, log_number: int = 0, str
     return res
 
 
-def wal_recover_batch(wal, nbytes: Optional[int] = None, log_number: int = 0, slot_base=None,
-                      slots_per_block: int = 0, hashes=None, stream=None, out=None):
-    """mck_wal_recover_batch: the per-block verify results (as
-    wal_verify_batch) and, in the same read, the XXH3_64bits of every
-    full-type record: record k of block b at hashes[slot_base[b] + k] (k <
-    slot_base[b + 1] - slot_base[b]) or, without slot_base, at
-    hashes[b * slots_per_block + k].  Returns (results, hashes)."""
+def wal_plan_records(wal: bytes, log_number: int = 0):
+    """mck_wal_plan_records: every physical record of a host WAL image as a
+    numpy uint32 [count, 4] array of mck_wal_rec_desc (payload offset low,
+    offset high | type << 16 | MCK_WAL_REC_HASH, length, stored CRC)."""
+    import numpy as np
+    buf = bytes(wal)
+    n = ctypes.c_uint64()
+    check(lib.mck_wal_plan_records(buf, len(buf), log_number & 0xFFFFFFFF, None, 0, ctypes.byref(n)),
+          "mck_wal_plan_records")
+    out = np.zeros((max(n.value, 1), 4), dtype=np.uint32)
+    check(lib.mck_wal_plan_records(buf, len(buf), log_number & 0xFFFFFFFF, out.ctypes.data, n.value,
+                                   ctypes.byref(n)), "mck_wal_plan_records")
+    return out[:n.value]
+
+
+def wal_recover_batch(wal, recs, log_number: int = 0, ok=None, hashes=None, stream=None):
+    """mck_wal_recover_batch: for every record of a plan (``recs``: a device
+    int32/uint32 tensor [count, 4] of mck_wal_rec_desc, e.g. from
+    wal_plan_records), its CRC verdict (uint8 [count], 1 = holds) and, for
+    the records flagged MCK_WAL_REC_HASH, the XXH3_64bits of its payload
+    (int64 [count]) -- one read of the image.  Returns (ok, hashes)."""
     torch = _torch()
-    if nbytes is None:
-        nbytes = wal.numel()
-    nblocks = (nbytes + 32767) // 32768
-    res = out if out is not None else torch.empty((nblocks, 4), dtype=torch.int32, device=wal.device)
-    if hashes is None and (slot_base is not None or slots_per_block):
-        n = int(slot_base[-1].item()) if slot_base is not None else nblocks * slots_per_block
-        hashes = torch.zeros(max(n, 1), dtype=torch.int64, device=wal.device)
-    check(lib.mck_wal_recover_batch(wal.data_ptr(), nbytes, log_number & 0xFFFFFFFF, res.data_ptr(),
-                                    slot_base.data_ptr() if slot_base is not None else None, slots_per_block,
-                                    hashes.data_ptr() if hashes is not None else None, _stream(stream)),
-          "mck_wal_recover_batch")
-    return res, hashes
+    n = int(recs.shape[0])
+    ok = ok if ok is not None else torch.zeros(max(n, 1), dtype=torch.uint8, device=wal.device)
+    hashes = hashes if hashes is not None else torch.zeros(max(n, 1), dtype=torch.int64, device=wal.device)
+    check(lib.mck_wal_recover_batch(wal.data_ptr(), recs.data_ptr(), n, log_number & 0xFFFFFFFF, ok.data_ptr(),
+                                    hashes.data_ptr(), _stream(stream)), "mck_wal_recover_batch")
+    return ok[:n], hashes[:n]
 
 
 def np_hash64_batch(spans: Spans, seed: int = 0, out=None, stream=None):
@@ -1006,7 +1014,7 @@ class FragmentBufferedReader:
 
 __all__ += ["wal_plan", "WalBatchWriter", "mck_wal_fragment", "wal_list_records", "WalReadRecords",
             "WALRecoveryMode", "wal_read_records", "WalReadPlan", "WalRecover", "WalRecovery",
-            "FragmentBufferedReader", "wal_recover_batch", "mck_wal_recovery_info"]
+            "FragmentBufferedReader", "wal_recover_batch", "wal_plan_records", "mck_wal_recovery_info"]
 
 
 # ---------------------------------------------------------------------------

@@ -875,36 +875,26 @@ int mck_wal_verify_batch(const void* wal, uint64_t nbytes, uint32_t log_number, 
   return MCK_OK;
 }
 
-// One device pass of WAL recovery (mck_walrec.hpp): the verify results of
-// mck_wal_verify_batch plus the XXH3 record checksum of every full-type
-// record, hashed in place from the same read.
-int mck_wal_recover_batch(const void* wal, uint64_t nbytes, uint32_t log_number, mck_wal_block_result* results,
-                          const uint64_t* slot_base, uint32_t slots_per_block, uint64_t* record_hashes,
-                          mck_stream_t stream) {
+// One device pass of WAL recovery (mck_walrec.hpp): the CRC verdict of every
+// physical record of a host plan and, from the same registers, the XXH3
+// record checksum of the one-fragment records.
+int mck_wal_recover_batch(const void* wal, const mck_wal_rec_desc* recs, uint32_t count, uint32_t log_number,
+                          uint8_t* crc_ok, uint64_t* record_hashes, mck_stream_t stream) {
   t_err[0] = 0;
-  if (!nbytes) return MCK_OK;
-  if (!wal || !results) {
-    set_err("wal / results is NULL");
-    return MCK_EINVAL;
-  }
-  if (record_hashes && !slot_base && !slots_per_block) {
-    set_err("record_hashes needs slot_base or slots_per_block");
-    return MCK_EINVAL;
-  }
-  const uint64_t nb64 = (nbytes + 32767) / 32768;
-  if (nb64 > 0xFFFFFFFFull) {
-    set_err("WAL image too large");
+  static_assert(sizeof(mck_wal_rec_desc) == sizeof(WalRecDesc), "layout");
+  if (!count) return MCK_OK;
+  if (!wal || !recs || !crc_ok || !record_hashes) {
+    set_err("wal / recs / crc_ok / record_hashes is NULL");
     return MCK_EINVAL;
   }
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
-  if (int rc = ensure_lds(k_wal_recover<true>, dev)) return rc;
-  const uint32_t nblocks = (uint32_t)nb64;
-  const uint32_t wpb = kWalRecThreads / 64;
-  const uint32_t grid = std::min<uint32_t>(ncu, (nblocks + wpb - 1) / wpb);
-  hipLaunchKernelGGL(k_wal_recover<true>, dim3(grid), dim3(kWalRecThreads), kCrcLdsBytes,
-                     reinterpret_cast<hipStream_t>(stream), static_cast<const uint8_t*>(wal), nbytes, log_number,
-                     reinterpret_cast<WalResult*>(results), nblocks, record_hashes, slot_base, slots_per_block);
+  if (int rc = ensure_lds(k_wal_recover, dev)) return rc;
+  const uint32_t grid = std::min<uint32_t>(ncu, (count + 63) / 64);
+  const WrArgs a{static_cast<const uint8_t*>(wal), reinterpret_cast<const WalRecDesc*>(recs), count, crc_ok,
+                 record_hashes};
+  hipLaunchKernelGGL(k_wal_recover, dim3(grid), dim3(1024), kCrcLdsBytes, reinterpret_cast<hipStream_t>(stream), a,
+                     wal_type_crcs(log_number));
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }

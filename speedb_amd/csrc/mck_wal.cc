@@ -216,15 +216,7 @@ struct WalReader {
         buf_size = 0;
         return kBadRecordChecksum;
       }
-      if (type == 1 || type == 5) {  // a full-type record: its slot in the block (mck_wal_recover)
-        const uint64_t blk = buf_off / MCK_WAL_kBlockSize;
-        if (blk != full_blk) {
-          full_blk = blk;
-          full_k = 0;
-        }
-        last_full_k = full_k++;
-        if (full_counts) (*full_counts)[blk]++;
-      }
+      last_hoff = buf_off;  // (mck_wal_recover: the record's physical record)
       *frag_off = buf_off + hs;
       *frag_len = length;
       buf_off += hs + length;
@@ -234,12 +226,7 @@ struct WalReader {
     }
   }
   bool read_ok = false;  // the last read_physical returned a record
-  // full-type records (kFullType / kRecyclableFullType) returned per block, in
-  // walk order: the device's recover pass hashes them in the same order
-  // (k_wal_recover), so record k of block b is slot (b, k)
-  uint64_t full_blk = ~0ull;
-  uint32_t full_k = 0, last_full_k = 0;
-  std::vector<uint32_t>* full_counts = nullptr;  // per block (optional)
+  uint64_t last_hoff = 0;  // header offset of the last record read_physical returned
 };
 
 }  // namespace
@@ -279,13 +266,9 @@ namespace mck_walk {
 // log::Reader (checksum = true) reading the whole image: ReadRecord until it
 // returns false, over the device's verdicts (NULL = trust every CRC).
 int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recovery_mode,
-             const mck_wal_block_result* verified, bool count_full, WalWalk& W) {
+             const mck_wal_block_result* verified, WalWalk& W) {
   WalReader R{d, nbytes, log_number, recovery_mode, verified};
   R.records_so_far = &W.roff;
-  if (count_full) {
-    W.full_counts.assign((nbytes + MCK_WAL_kBlockSize - 1) / MCK_WAL_kBlockSize, 0u);
-    R.full_counts = &W.full_counts;
-  }
   TsRecorder ts;
   std::vector<mck_wal_fragment>& fr = W.fr;
   std::vector<uint64_t>& roff = W.roff;
@@ -322,14 +305,13 @@ int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recover
     cur_file = file_off;
     scratch_append(off, len, type);
   };
-  auto emit = [&](uint64_t blk, uint32_t k) {  // ReadRecord returns *record = scratch
+  auto emit = [&](uint64_t hoff) {  // ReadRecord returns *record = scratch
     for (size_t j = cur_first_frag; j < fr.size(); j++)
       if (fr_sidx[j] != ~0ull) stream[fr_sidx[j]].dst_off = j;
     roff.push_back(cur_start);
     rlen.push_back((uint32_t)(dst - cur_start));
     rfile.push_back(cur_file);
-    W.rblk.push_back(blk);
-    W.rk.push_back(k);
+    W.rhoff.push_back(hoff);
     W.rfrag.push_back(cur_first_frag);
     cur_start = dst;
     cur_first_frag = fr.size();
@@ -355,7 +337,7 @@ int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recover
       if (t == 1 || t == 5) {  // kFullType
         if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_PARTIAL_WITHOUT_END_1);
         scratch_assign(foff, flen, (uint8_t)t, phys);
-        emit(R.full_blk, R.last_full_k);
+        emit(R.last_hoff);
         break;
       } else if (t == 2 || t == 6) {  // kFirstType
         if (in_fragmented_record && scratch_size()) R.report(phys, scratch_size(), MCK_WAL_R_PARTIAL_WITHOUT_END_2);
@@ -371,7 +353,7 @@ int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recover
           R.report(phys, flen, MCK_WAL_R_MISSING_START_2);
         } else {
           scratch_append(foff, flen, (uint8_t)t);
-          emit(~0ull, 0u);
+          emit(~0ull);
           break;
         }
       } else if (t == (int)kSetCompressionType) {  // :167-188
@@ -531,16 +513,102 @@ int check_read_args(const void* wal, uint64_t nbytes, int recovery_mode, const m
   }
   return MCK_OK;
 }
+// k_wal_verify's per-block walk (mck_kernels.hpp wal_parse) on the host,
+// without the CRCs: a < 7-byte rest is the block trailer (at the end of the
+// file: a truncated header), a recyclable header needs 11 bytes, a record of
+// another log, a length past the block and a zero-length kZeroType stop it.
+void wal_block_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, std::vector<PhysRec>& phys,
+                    std::vector<BlockStop>& stops) {
+  const uint64_t nb = (nbytes + MCK_WAL_kBlockSize - 1) / MCK_WAL_kBlockSize;
+  stops.resize(nb);
+  phys.reserve(phys.size() + nb);
+  for (uint64_t b = 0; b < nb; b++) {
+    const uint64_t base = b * MCK_WAL_kBlockSize;
+    const uint32_t size = (uint32_t)std::min<uint64_t>(MCK_WAL_kBlockSize, nbytes - base);
+    const bool last = nbytes - base <= MCK_WAL_kBlockSize;
+    BlockStop& st = stops[b];
+    st.first = phys.size();
+    st.status = MCK_WAL_OK;
+    uint32_t pos = 0;
+    for (;;) {
+      const uint32_t left = size - pos;
+      const uint8_t* h = d + base + pos;
+      if (left < MCK_WAL_kHeaderSize) {
+        if (last && left > 0) st.status = MCK_WAL_BAD_HEADER;
+        break;
+      }
+      const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
+      const uint32_t type = h[6];
+      uint32_t hs = MCK_WAL_kHeaderSize;
+      if ((type >= 5 && type <= 8) || type == 11) {
+        hs = MCK_WAL_kRecyclableHeaderSize;
+        if (left < hs) {
+          if (last) st.status = MCK_WAL_BAD_HEADER;
+          break;
+        }
+        const uint32_t ln = (uint32_t)h[7] | ((uint32_t)h[8] << 8) | ((uint32_t)h[9] << 16) | ((uint32_t)h[10] << 24);
+        if (ln != log_number) {
+          st.status = MCK_WAL_OLD_RECORD;
+          break;
+        }
+      }
+      if (hs + length > left) {
+        st.status = MCK_WAL_BAD_LENGTH;
+        break;
+      }
+      if (type == 0 && length == 0) {
+        st.status = MCK_WAL_ZERO_RECORD;
+        break;
+      }
+      const uint32_t stored = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+      phys.push_back(PhysRec{base + pos, length, (uint8_t)hs, (uint8_t)type, stored});
+      pos += hs + length;
+    }
+    st.count = (uint32_t)(phys.size() - st.first);
+    st.pos = pos;
+  }
+}
+
 }  // namespace mck_walk
 
 using namespace mck_walk;
+
+extern "C" int mck_wal_plan_records(const void* wal, uint64_t nbytes, uint32_t log_number, mck_wal_rec_desc* out,
+                                    uint64_t cap, uint64_t* count) {
+  mck_internal_set_error("");
+  if ((!wal && nbytes) || !count) {
+    mck_internal_set_error("wal / count is NULL");
+    return MCK_EINVAL;
+  }
+  if (nbytes >> 48) {
+    mck_internal_set_error("WAL image too large (payload offsets are 48-bit)");
+    return MCK_EINVAL;
+  }
+  std::vector<PhysRec> phys;
+  std::vector<BlockStop> stops;
+  wal_block_walk(static_cast<const uint8_t*>(wal), nbytes, log_number, phys, stops);
+  *count = phys.size();
+  if (!out) return MCK_OK;
+  if (cap < phys.size()) {
+    mck_internal_set_error("out capacity too small");
+    return MCK_EINVAL;
+  }
+  for (size_t i = 0; i < phys.size(); i++) {
+    const PhysRec& p = phys[i];
+    const uint64_t po = p.hoff + p.hsize;
+    const bool full = p.type == 1 || p.type == 5;
+    out[i] = mck_wal_rec_desc{(uint32_t)po, (uint32_t)(po >> 32) | ((uint32_t)p.type << 16) | (full ? MCK_WAL_REC_HASH : 0u),
+                              p.length, p.stored};
+  }
+  return MCK_OK;
+}
 
 extern "C" int mck_wal_read_records(const void* wal, uint64_t nbytes, uint32_t log_number, int recovery_mode,
                                     const mck_wal_block_result* verified, mck_wal_read_out* out) {
   mck_internal_set_error("");
   if (int rc = check_read_args(wal, nbytes, recovery_mode, out)) return rc;
   WalWalk W;
-  if (int rc = wal_walk(static_cast<const uint8_t*>(wal), nbytes, log_number, recovery_mode, verified, false, W)) {
+  if (int rc = wal_walk(static_cast<const uint8_t*>(wal), nbytes, log_number, recovery_mode, verified, W)) {
     mck_internal_set_error("verify results do not match the WAL image (a record the device did not reach)");
     return rc;
   }

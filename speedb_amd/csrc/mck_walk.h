@@ -16,10 +16,8 @@ struct WalWalk {
   std::vector<mck_wal_fragment> fr;
   std::vector<uint64_t> roff, rfile;
   std::vector<uint32_t> rlen;
-  std::vector<uint64_t> rblk;  // full-type record: its physical record's block; ~0 = multi-fragment
-  std::vector<uint32_t> rk;    // ... and its index among the block's full-type records
+  std::vector<uint64_t> rhoff;  // one-fragment record: its physical record's header offset; ~0 = fragmented
   std::vector<uint64_t> rfrag;  // record r's fragments: fr[rfrag[r] .. rfrag[r + 1])
-  std::vector<uint32_t> full_counts;  // per block (count_full)
   std::vector<mck_wal_report> reports;
   std::vector<uint64_t> report_pos;  // per report: records returned before it
   uint64_t dropped = 0, end_offset = 0, records_bytes = 0;
@@ -28,10 +26,28 @@ struct WalWalk {
 };
 
 // log::Reader (checksum = true) reading the whole image: ReadRecord until it
-// returns false, over the device's verdicts (NULL = trust every CRC);
-// count_full fills full_counts (full-type records per block).
+// returns false, over the device's verdicts (NULL = trust every CRC).
 int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recovery_mode,
-             const mck_wal_block_result* verified, bool count_full, WalWalk& W);
+             const mck_wal_block_result* verified, WalWalk& W);
+
+// Every physical record of every 32 KiB block, each block walked on its own
+// from offset 0 as ReadPhysicalRecord parses it (db/log_reader.cc:450-584;
+// k_wal_verify's walk): the records a reader can reach, whatever it drops.
+struct PhysRec {
+  uint64_t hoff;    // header offset
+  uint32_t length;  // payload bytes
+  uint8_t hsize;    // 7 or 11
+  uint8_t type;
+  uint32_t stored;  // the header's masked CRC
+};
+struct BlockStop {  // where the block's walk stopped, and why (MCK_WAL_* status)
+  uint64_t first;   // its first record in the list
+  uint32_t count;   // its records
+  uint32_t pos;     // stop position in the block
+  int32_t status;
+};
+void wal_block_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, std::vector<PhysRec>& phys,
+                    std::vector<BlockStop>& stops);
 // mck_wal_read_out (caller arrays, *_cap sizes) from a walk
 int wal_copy_out(const WalWalk& W, mck_wal_read_out* out);
 // argument checks of the read-out entry points (struct_size, mode)

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime_api.h>
 #include <string.h>
 
+#include <algorithm>
 #include <chrono>
 #include <new>
 #include <vector>
@@ -82,7 +83,7 @@ struct MultiPlan {
 MultiPlan multi_plan(const WalWalk& W) {
   MultiPlan M;
   for (size_t r = 0; r < W.roff.size(); r++) {
-    if (W.rblk[r] != ~0ull) continue;  // one fragment: hashed in place
+    if (W.rhoff[r] != ~0ull) continue;  // one fragment: hashed in place
     M.recs.push_back(r);
     M.offs.push_back(M.bytes);
     M.lens.push_back(W.rlen[r]);
@@ -124,6 +125,28 @@ size_t multi_bytes(const MultiPlan& M) {
 }
 }  // namespace
 
+// The per-block results (mck_wal_verify_batch's) the walk over verdicts
+// consumes, from the block walk and the device's per-record verdicts: a
+// block stops at its first record whose CRC fails, else where its walk did.
+static void block_results(const std::vector<PhysRec>& phys, const std::vector<BlockStop>& stops,
+                          const std::vector<uint8_t>& ok, uint64_t nbytes, std::vector<mck_wal_block_result>& res) {
+  res.resize(stops.size());
+  for (size_t b = 0; b < stops.size(); b++) {
+    const BlockStop& st = stops[b];
+    const uint64_t base = b * (uint64_t)MCK_WAL_kBlockSize;
+    const uint32_t size = (uint32_t)std::min<uint64_t>(MCK_WAL_kBlockSize, nbytes - base);
+    mck_wal_block_result r{st.count, st.status, st.status ? st.pos : size, st.pos};
+    for (uint32_t j = 0; j < st.count; j++) {
+      if (!ok[st.first + j]) {
+        const uint32_t h = (uint32_t)(phys[st.first + j].hoff - base);
+        r = mck_wal_block_result{j, MCK_WAL_BAD_CHECKSUM, h, h};
+        break;
+      }
+    }
+    res[b] = r;
+  }
+}
+
 extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64_t nbytes, uint32_t log_number,
                                int recovery_mode, mck_stream_t stream, mck_wal_recovery** out) {
   mck_internal_set_error("");
@@ -136,9 +159,8 @@ extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64
     mck_internal_set_error("unknown WALRecoveryMode");
     return MCK_EINVAL;
   }
-  const uint64_t nblocks = (nbytes + MCK_WAL_kBlockSize - 1) / MCK_WAL_kBlockSize;
-  if (nblocks > 0xFFFFFFFFull) {
-    mck_internal_set_error("WAL image too large");
+  if (nbytes >> 48) {
+    mck_internal_set_error("WAL image too large (payload offsets are 48-bit)");
     return MCK_EINVAL;
   }
   mck_wal_recovery* R = new (std::nothrow) mck_wal_recovery();
@@ -149,41 +171,55 @@ extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64
   const uint8_t* d = static_cast<const uint8_t*>(wal_host);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   double t0 = now_s();
-  // 1. the plan
+  // 1. the plan: every physical record (the block walk) and the reader's
+  //    walk with every CRC trusted
+  std::vector<PhysRec> phys;
+  std::vector<BlockStop> stops;
+  wal_block_walk(d, nbytes, log_number, phys, stops);
+  if (phys.size() > 0xFFFFFFFFull) {
+    delete R;
+    mck_internal_set_error("more than 2^32 physical records");
+    return MCK_EINVAL;
+  }
+  const uint32_t np = (uint32_t)phys.size();
   WalWalk plan;
-  if (int rc = wal_walk(d, nbytes, log_number, recovery_mode, nullptr, true, plan)) {
+  if (int rc = wal_walk(d, nbytes, log_number, recovery_mode, nullptr, plan)) {
     delete R;
     return rc;
   }
-  std::vector<uint64_t> base(nblocks + 1, 0);
-  for (uint64_t b = 0; b < nblocks; b++) base[b + 1] = base[b] + plan.full_counts[b];
-  const uint64_t nfull = base[nblocks];
+  std::vector<mck_wal_rec_desc> desc(np);
+  for (uint32_t i = 0; i < np; i++) {
+    const PhysRec& p = phys[i];
+    const uint64_t po = p.hoff + p.hsize;
+    const bool full = p.type == 1 || p.type == 5;
+    desc[i] = mck_wal_rec_desc{(uint32_t)po, (uint32_t)(po >> 32) | ((uint32_t)p.type << 16) | (full ? MCK_WAL_REC_HASH : 0u),
+                               p.length, p.stored};
+  }
   const MultiPlan M = plan.compression ? MultiPlan{} : multi_plan(plan);
   R->info.walk_seconds = now_s() - t0;
   R->info.host_walks = 1;
   // 2. the device pass (+ the multi-fragment records), one readback
   t0 = now_s();
-  std::vector<mck_wal_block_result> res(nblocks);
-  std::vector<uint64_t> hashes(nfull), mhash(M.recs.size());
+  std::vector<uint8_t> ok(np);
+  std::vector<uint64_t> hashes(np), mhash(M.recs.size());
   int rc = MCK_OK;
   {
     DevArena A{st};
-    const size_t need = DevArena::need(nblocks, sizeof(mck_wal_block_result)) + DevArena::need(nblocks + 1, 8) +
-                        DevArena::need(nfull, 8) + multi_bytes(M);
-    if (nblocks && !(rc = A.reserve(need))) {
-      auto* d_res = A.take<mck_wal_block_result>(nblocks);
-      auto* d_base = A.take<uint64_t>(nblocks + 1);
-      auto* d_hash = A.take<uint64_t>(nfull);
+    const size_t need = DevArena::need(np, sizeof(mck_wal_rec_desc)) + DevArena::need(np, 1) +
+                        DevArena::need(np, 8) + multi_bytes(M);
+    if (np && !(rc = A.reserve(need))) {
+      auto* d_desc = A.take<mck_wal_rec_desc>(np);
+      auto* d_ok = A.take<uint8_t>(np);
+      auto* d_hash = A.take<uint64_t>(np);
       uint64_t* d_mh = nullptr;
-      if (hipMemcpyAsync(d_base, base.data(), (nblocks + 1) * 8, hipMemcpyHostToDevice, st)) {
-        mck_internal_set_error("hipMemcpyAsync failed (slot bases)");
+      if (hipMemcpyAsync(d_desc, desc.data(), (size_t)np * sizeof(mck_wal_rec_desc), hipMemcpyHostToDevice, st)) {
+        mck_internal_set_error("hipMemcpyAsync failed (record plan)");
         rc = MCK_EHIP;
       }
-      if (!rc)
-        rc = mck_wal_recover_batch(wal_dev, nbytes, log_number, d_res, d_base, 0, nfull ? d_hash : nullptr, stream);
+      if (!rc) rc = mck_wal_recover_batch(wal_dev, d_desc, np, log_number, d_ok, d_hash, stream);
       if (!rc) rc = launch_multi(wal_dev, M, A, &d_mh, st);
-      if (!rc && (hipMemcpyAsync(res.data(), d_res, nblocks * sizeof(mck_wal_block_result), hipMemcpyDeviceToHost, st) ||
-                  (nfull && hipMemcpyAsync(hashes.data(), d_hash, nfull * 8, hipMemcpyDeviceToHost, st)) ||
+      if (!rc && (hipMemcpyAsync(ok.data(), d_ok, np, hipMemcpyDeviceToHost, st) ||
+                  hipMemcpyAsync(hashes.data(), d_hash, (size_t)np * 8, hipMemcpyDeviceToHost, st) ||
                   (d_mh && hipMemcpyAsync(mhash.data(), d_mh, mhash.size() * 8, hipMemcpyDeviceToHost, st)))) {
         mck_internal_set_error("hipMemcpyAsync failed (recover results)");
         rc = MCK_EHIP;
@@ -199,9 +235,10 @@ extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64
     delete R;
     return rc;
   }
+  block_results(phys, stops, ok, nbytes, R->blocks);
   // 3. a failed checksum changes the walk: walk again over the verdicts
   bool bad = false;
-  for (uint64_t b = 0; b < nblocks && !bad; b++) bad = res[b].status == MCK_WAL_BAD_CHECKSUM;
+  for (uint32_t i = 0; i < np && !bad; i++) bad = !ok[i];
   WalWalk& W = R->W;
   const MultiPlan* MP = &M;
   MultiPlan M2;
@@ -210,11 +247,11 @@ extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64
     W = std::move(plan);
   } else {
     t0 = now_s();
-    rc = wal_walk(d, nbytes, log_number, recovery_mode, res.data(), false, W);
+    rc = wal_walk(d, nbytes, log_number, recovery_mode, R->blocks.data(), W);
     R->info.walk_seconds += now_s() - t0;
     R->info.host_walks = 2;
     if (rc) {
-      mck_internal_set_error("verify results do not match the WAL image (a record the device did not reach)");
+      mck_internal_set_error("recover: the walk over the verdicts reached a record the block walk did not");
       delete R;
       return rc;
     }
@@ -241,22 +278,23 @@ extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64
     }
   }
   const std::vector<uint64_t>& mh = bad ? mhash2 : mhash;
-  R->blocks = std::move(res);
-  // 4. every record's checksum
+  // 4. every record's checksum: a one-fragment record's from its physical
+  //    record (records come in file order: one forward cursor)
   const size_t nr = W.roff.size();
   R->info.nrecords = nr;
   R->info.has_checksums = W.compression ? 0u : 1u;
   if (!W.compression) {
     R->checksums.assign(nr, 0);
+    uint32_t cur = 0;
     for (size_t r = 0; r < nr; r++) {
-      if (W.rblk[r] == ~0ull) continue;
-      const uint64_t b = W.rblk[r];
-      if (W.rk[r] >= base[b + 1] - base[b]) {  // cannot happen: the plan counted every one
-        mck_internal_set_error("recover: a full record outside its block's slots");
+      if (W.rhoff[r] == ~0ull) continue;
+      while (cur < np && phys[cur].hoff < W.rhoff[r]) cur++;
+      if (cur >= np || phys[cur].hoff != W.rhoff[r]) {  // cannot happen: the block walk lists every record
+        mck_internal_set_error("recover: a record outside the block walk");
         delete R;
         return MCK_EINVAL;
       }
-      R->checksums[r] = hashes[base[b] + W.rk[r]];
+      R->checksums[r] = hashes[cur];
       R->info.in_place++;
     }
     for (size_t j = 0; j < MP->recs.size(); j++) R->checksums[MP->recs[j]] = mh[j];

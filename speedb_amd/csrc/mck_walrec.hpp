@@ -1,291 +1,388 @@
 // mck_walrec.hpp -- WAL recovery in one device pass (round 6): every physical
-// record's CRC32C (ReadPhysicalRecord, db/log_reader.cc:450-584) and, from
-// the same read of the image, the XXH3_64bits record checksum of every
-// single-fragment record (ReadRecord's kFullType case, :95-116 -- the
-// logical record IS the fragment, hashed in place, :107-110).
+// record's CRC32C (ReadPhysicalRecord, db/log_reader.cc:512-525) and, from
+// the SAME registers, the XXH3_64bits record_checksum of every
+// single-fragment record (ReadRecord's kFullType case, :95-116: the logical
+// record IS the fragment, :107-110).
 //
-// The walk is k_wal_verify's (one wave per 32 KiB block, a wave's blocks
-// form one record pipeline, the next block's first round loaded with the
-// last one of a record that ends its block).  A kFullType /
-// kRecyclableFullType record of more than 240 bytes is also hashed by the
-// XXH3 wave layout (x3w_*, mck_xxh.hpp) in lockstep with its CRC rounds, one
-// iteration behind: iteration m runs CRC round m (4 KiB, end-anchored) and
-// XXH3 unit m - 1 (4 KiB, start-anchored).  Unit m - 1 lies in CRC windows
-// m - 1 and m, whose loads were issued before it, so its loads are L2 hits on
-// lines the CRC loads brought in (no second HBM read), and they are issued
-// before the CRC prefetch of window m + 1, so waiting for them never waits
-// for the prefetch (vmcnt retires in order).  Shorter full records take the
-// short classes (xxh3_short) on one lane after the CRC, from L2.
+// Input: the host plan of the log (mck_wal_recover's walk, mck_walk.h): one
+// 16-byte descriptor per physical record -- payload offset, type, length,
+// the header's stored CRC.  The header walk is the host's (it reads the
+// headers anyway to hand the records out), so the device only hashes.
 //
-// Output per block: mck_wal_block_result (as k_wal_verify), and the hashes
-// of the block's full-type records, in walk order: record k of block b at
-// x3[base_b + k] for k < cap_b, with base_b = slot_base[b] and cap_b =
-// slot_base[b + 1] - base_b (a dense array: the host's plan counted the full
-// records of every block, mck_wal_recover) or, without slot_base, base_b =
-// b * nslots and cap_b = nslots.  The host walk (mck_wal.cc) counts the full
-// records it reads per block to find a record's slot; multi-fragment records
-// are hashed by a gather + XXH3 batch.
+// Layout: the CRC row driver's (16-lane rows, one record per row, records
+// taken from an LDS ticket), but with the round grid anchored at the
+// payload START (a0 = payload & ~3): row round k covers [a0 + 1024 k, +1024),
+// lane c the 64-byte chunk a0 + 1024 k + 64 c.  That grid is XXH3's: round k
+// is segment k (1 KiB = 16 stripes of 64 B, util/xxhash.h:5141-5171) and
+// lane c's chunk holds stripe c shifted by b = payload & 3 bytes, so the
+// stripe is the chunk funnel-shifted with one more dword (the next chunk's
+// first, loaded beside the chunk).  Per round a lane folds its chunk into the
+// CRC (the 4-byte table step) and its stripe into XXH3's 8 accumulator
+// terms; a reduce-scatter over the row leaves accumulator a's segment sum in
+// lanes a and a + 8, which keep accumulator a and scramble it after every
+// full segment.  One read of the log, no second pass, no record copies.
+//
+// The CRC covers [type][log number if recyclable][payload] as
+// EmitPhysicalRecord does (db/log_writer.cc:281-298): the type (and log
+// number) bytes are the row's init state (type_crc, as the writer's), the
+// payload is the span.  With the start-anchored grid the last round ends
+// past the record: lanes past its last byte keep their previous state and
+// shift it by one more row round, and the sum is un-shifted by the < 64
+// bytes after the end (the lane-final tables shift by any 64 j, j < 64).
 #pragma once
 #include "mck_kernels.hpp"
 
 namespace mck {
 
-// per-wave 1 KiB XXH3 exchange buffer (x3w_fold's tx), in the LDS bytes the
-// wave-driver CRC image leaves free below the step tables
-constexpr uint32_t kLdsWalX3 = kLdsLowEnd;
-static_assert(kLdsWalX3 + 16 * 1024 <= kLdsStep, "16 waves x 1 KiB below the step tables");
+// == mck_wal_rec_desc (mck.h)
+struct WalRecDesc {
+  uint32_t off_lo;  // payload offset in the image, bits 0-31
+  uint32_t hi;      // bits 0-15: payload offset bits 32-47; 16-23: record type; 24: hash the record
+  uint32_t len;     // payload bytes
+  uint32_t stored;  // the header's masked CRC (LE32)
+};
+static_assert(sizeof(WalRecDesc) == 16, "descriptor");
 
-// the XXH3 wave layout's per-lane constants (X3Row, ~50 VGPRs if kept in
-// registers beside the CRC pipeline's): one copy per lane index in LDS,
-// written once per workgroup, read inside each fold (only the fields the
-// fold uses are loaded); the loads' address math needs only the lane's
-// indices (x3_row_idx)
-constexpr uint32_t kLdsWalX3Row = kLdsWalX3 + 16 * 1024;
-static_assert(kLdsWalX3Row + 64 * sizeof(X3Row) <= kLdsStep, "X3Row per lane below the step tables");
-static_assert(sizeof(X3Row) % 8 == 0, "X3Row as u64 words");
-__device__ __forceinline__ X3Row x3_row_lds() {
-  X3Row X;
-  uint64_t* d = reinterpret_cast<uint64_t*>(&X);
-  const uint32_t off = kLdsWalX3Row + (uint32_t)sizeof(X3Row) * (threadIdx.x & 63);
-#pragma unroll
-  for (uint32_t i = 0; i < sizeof(X3Row) / 8; i++) d[i] = *lds_p64(off + 8 * i);
-  return X;
-}
-__device__ __forceinline__ void x3_row_lds_store() {
-  if (threadIdx.x < 64) {
-    const X3Row X = x3_row(0);
-    const uint64_t* s = reinterpret_cast<const uint64_t*>(&X);
-#pragma unroll
-    for (uint32_t i = 0; i < sizeof(X3Row) / 8; i++)
-      *lds_p64(kLdsWalX3Row + (uint32_t)sizeof(X3Row) * threadIdx.x + 8 * i) = s[i];
-  }
-}
-__device__ __forceinline__ X3Row x3_row_idx() {
-  X3Row X{};
-  X.lane = threadIdx.x & 63;
-  X.row = X.lane >> 4;
-  X.j = X.lane & 15;
-  X.q = X.j & 3;
-  X.st4 = X.j >> 2;
-  X.role = X.lane >> 5;
-  return X;
-}
+// LDS: the row drivers' image (crc_fill_rows: wave image + row gap maps,
+// row_init_tables: typed init + masks), then this kernel's descriptor cache,
+// ticket and the XXH3 secret words.
+constexpr uint32_t kWrDescCache = 1400;
+constexpr uint32_t kLdsWrDesc = kLdsRowDesc;
+constexpr uint32_t kLdsWrTicket = kLdsWrDesc + 16 * kWrDescCache;
+constexpr uint32_t kLdsWrSecret = kLdsWrTicket + 64;  // 25 u64 words of XXH3_kSecret
+static_assert(kLdsWrSecret + 8 * 25 <= kLdsRowMaskHead, "below the row mask tables");
 
-// CRC image fill for any workgroup size (crc_fill_lds assumes kCrcBlock
-// threads): once per persistent workgroup
-__device__ __forceinline__ void crc_fill_lds_any(uint8_t* lds, const CrcTables* __restrict__ g) {
-  uint4* l4 = reinterpret_cast<uint4*>(lds + kLdsStep);
-  for (uint32_t i = threadIdx.x; i < 4096; i += blockDim.x) {
-    const uint32_t x = g->step[(i >> 2) & 3][i >> 4];
-    l4[i] = make_uint4(x, x, x, x);
-  }
-  const uint4* lo = reinterpret_cast<const uint4*>(&g->lane_final[0][0][0]);
-  uint4* dlo = reinterpret_cast<uint4*>(lds + kLdsFinal);
-  for (uint32_t i = threadIdx.x; i < (uint32_t)kFillLow; i += blockDim.x) dlo[i] = lo[i];
-  const uint4* us = reinterpret_cast<const uint4*>(&g->unshift[0][0][0]);
-  uint4* dus = reinterpret_cast<uint4*>(lds + kLdsUnshift);
-  for (uint32_t i = threadIdx.x; i < (uint32_t)kFillUnshift; i += blockDim.x) dus[i] = us[i];
-}
-
-// finish() target of the XXH3 wave fold: slot k of the current block
-struct OpWalX3 {
-  uint64_t* out;  // x3 + block * nslots
-  typedef NoPre Pre;
-  __device__ void finish(uint32_t k, uint64_t h, const Pre& = Pre{}) const { out[k] = h; }
+struct WrOp {  // row_init_tables' interface (typed init = type_crc[t] with the log number)
+  WalTypeCrcs tc;
+  static constexpr bool kTypedInit = true;
+  __device__ uint32_t typed_init(uint32_t t) const { return tc.v[t & 15]; }
 };
 
-// An interior unit k (k + 1 < units: four full segments, loads x3w_round_load)
-// folded into the lane's accumulator: x3w_fold's round part with every
-// segment scrambled.
-__device__ __forceinline__ void x3w_interior(const X3WSpan& sp, X3RoundLoads R, uint64_t& a, uint64_t* tx) {
-  const X3Row X = x3_row_lds();
-  uint64_t c0, c1;
-  x3w_round_sums<false>(sp, R, X, c0, c1);
-  if (X.st4 == 0) {
-    tx[4 * X.q + X.row] = c0;
-    tx[64 + 4 * X.q + X.row] = c1;
+// A row's record and round (the derived geometry is recomputed where it is
+// used: the row state stays at 7 VGPRs, three copies of it are live).
+struct WrRow {
+  uint64_t P;        // payload address
+  uint32_t len;      // payload bytes
+  uint32_t k;        // current round
+  uint32_t i;        // record index
+  uint32_t stored;   // the header's masked CRC
+  uint32_t th;       // type | hash << 8 (hash 1: XXH3 by stripes, len > 240; 2: short XXH3; 0: none)
+  __device__ uint64_t a0() const { return P & ~3ull; }  // the grid
+  __device__ uint32_t b() const { return (uint32_t)P & 3u; }
+  __device__ uint32_t type() const { return th & 0xFFu; }
+  __device__ uint32_t hash() const { return th >> 8; }
+  __device__ uint32_t R() const {  // rounds
+    const uint32_t cover = len + b();
+    return cover ? (cover + 1023) >> 10 : 1u;
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-  const ulonglong2* tr = reinterpret_cast<const ulonglong2*>(tx + 64 * X.role + 4 * X.q);
-  const ulonglong2 t01 = tr[0], t23 = tr[1];
-  a = xxh3_scramble(a + t01.x, X.ksw);
-  a = xxh3_scramble(a + t01.y, X.ksw);
-  a = xxh3_scramble(a + t23.x, X.ksw);
-  a = xxh3_scramble(a + t23.y, X.ksw);
+  // XXH3 long loop (util/xxhash.h:5141-5171; len > 240 here): full
+  // segments, stripes of the partial one
+  __device__ uint32_t nb() const { return (len - 1) >> 10; }
+  __device__ uint32_t nst() const { return ((len - 1) & 1023u) >> 6; }
+};
+__device__ __forceinline__ WrRow wr_row(const uint4& d, uint32_t i, uint64_t base) {
+  WrRow r;
+  r.P = base + ((uint64_t)d.x | ((uint64_t)(d.y & 0xFFFFu) << 32));
+  r.len = d.z;
+  r.stored = d.w;
+  const uint32_t h = (d.y >> 24) & 1u;
+  r.th = ((d.y >> 16) & 0xFFu) | ((h ? (r.len > 240 ? 1u : 2u) : 0u) << 8);
+  r.k = 0;
+  r.i = i;
+  return r;
+}
+__device__ __forceinline__ WrRow wr_sel(bool a, const WrRow& x, const WrRow& y) {
+  WrRow r;
+  r.P = a ? x.P : y.P;
+  r.len = a ? x.len : y.len;
+  r.k = a ? x.k : y.k;
+  r.i = a ? x.i : y.i;
+  r.stored = a ? x.stored : y.stored;
+  r.th = a ? x.th : y.th;
+  return r;
 }
 
-// x3: NULL = CRC only (k_wal_verify's output).
-// T: transposed CRC loads (non-temporal) as k_wal_verify<true>; the XXH3
-// re-reads use the default policy.
-constexpr int kWalRecThreads = 512;  // 8 waves per CU: 256 VGPRs each
-template <bool T>
-__global__ __launch_bounds__(kWalRecThreads) void k_wal_recover(const uint8_t* wal, uint64_t nbytes, uint32_t log_number,
-                                                      WalResult* res, uint32_t nblocks, uint64_t* x3,
-                                                      const uint64_t* slot_base, uint32_t nslots) {
+// A row round's loads: lane c's chunk, the dword after it (the stripe's
+// last b bytes), and -- when the round is the record's XXH3 merge round
+// (segment nb) -- lanes 0-7's 8-byte word of the last stripe (at len - 64,
+// util/xxhash.h:5160-5165), as three dwords covering it.  Every piece past
+// the record reads the zero piece instead (a piece at x < end ends at most
+// 15 bytes past it: the image is readable 16 bytes past nbytes).
+struct WrLoads {
+  Chunk ch;
+  uint32_t e;
+  uint32_t l0, l1, l2;
+};
+__device__ __forceinline__ WrLoads wr_load(const WrRow& r, uint32_t c, uint64_t zp) {
+  WrLoads L;
+  const uint64_t cb = r.a0() + 1024ull * r.k + 64ull * c;
+  const uint64_t end = r.P + r.len;
+#pragma unroll
+  for (int j = 0; j < 4; j++) L.ch.v[j] = span_load16<false>(cb + 16 * j < end ? cb + 16 * j : zp);
+  L.e = gload4(cb + 64 < end ? cb + 64 : zp);
+  const bool ls = r.hash() == 1u && r.k == r.nb() && c < 8;
+  const uint64_t w = end - 64 + 8ull * c;  // word c of the last stripe
+  const uint64_t w4 = w & ~3ull;
+  L.l0 = gload4(ls ? w4 : zp);
+  L.l1 = gload4(ls ? w4 + 4 : zp);
+  L.l2 = gload4(ls && w4 + 8 < end ? w4 + 8 : zp);
+  return L;
+}
+
+__device__ __forceinline__ uint32_t abyte(uint32_t hi, uint32_t lo, uint32_t s) {
+  return __builtin_amdgcn_alignbyte(hi, lo, s);
+}
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v) {
+  return ((uint64_t)dpp32<CTRL>((uint32_t)(v >> 32)) << 32) | dpp32<CTRL>((uint32_t)v);
+}
+constexpr int kDppHalfMirror = 0x141, kDppQuadXor1 = 0xB1, kDppQuadXor2 = 0x4E, kDppRowRor8 = 0x128,
+              kDppRowRor4 = 0x124;
+__device__ __forceinline__ uint64_t sel64(bool a, uint64_t x, uint64_t y) { return a ? x : y; }
+
+// Sum of A[lane & 7] over the 16 lanes of each row (a reduce-scatter: A[0..7]
+// are this lane's terms of the 8 accumulators).  Partners c ^ 7 (half
+// mirror), c ^ 2, c ^ 1 split the accumulator index bit by bit, then the two
+// halves add (c ^ 8).
+__device__ __forceinline__ uint64_t wr_row_reduce(const uint64_t (&A)[8], uint32_t c) {
+  const bool b2 = (c & 4u) != 0, b1 = (c & 2u) != 0, b0 = (c & 1u) != 0;
+  uint64_t B[4];
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    const uint64_t send = sel64(b2, A[j], A[4 + j]);
+    const uint64_t keep = sel64(b2, A[4 + j], A[j]);
+    B[j] = keep + dpp_u64<kDppHalfMirror>(send);
+  }
+  uint64_t C[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++) {
+    const uint64_t send = sel64(b1, B[j], B[2 + j]);
+    const uint64_t keep = sel64(b1, B[2 + j], B[j]);
+    C[j] = keep + dpp_u64<kDppQuadXor2>(send);
+  }
+  const uint64_t send = sel64(b0, C[0], C[1]);
+  const uint64_t keep = sel64(b0, C[1], C[0]);
+  uint64_t D = keep + dpp_u64<kDppQuadXor1>(send);
+  return D + dpp_u64<kDppRowRor8>(D);
+}
+
+__device__ __forceinline__ uint64_t lds_sec(uint32_t w) { return *lds_p64(kLdsWrSecret + 8 * w); }
+
+// Per-lane XXH3 constants: lane c keeps accumulator a = c & 7.
+struct WrX3 {
+  uint64_t init;  // XXH3_INIT_ACC[a]
+  uint64_t ks;    // scramble secret (offset 128 + 8 a)
+  uint64_t kl;    // last-stripe secret (offset 121 + 8 a)
+  uint64_t km;    // merge secret (offset 11 + 8 a)
+};
+__device__ __forceinline__ WrX3 wr_x3(uint32_t c) {
+  const uint32_t a = c & 7u;
+  WrX3 X;
+  const uint64_t ia[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+  X.init = ia[0];
+#pragma unroll
+  for (int k = 1; k < 8; k++) X.init = a == (uint32_t)k ? ia[k] : X.init;
+  X.ks = sec64(128 + 8 * (int)a);
+  X.kl = sec64(121 + 8 * (int)a);
+  X.km = sec64(11 + 8 * (int)a);
+  return X;
+}
+
+// One row round of XXH3: stripe c of segment k (lane c's chunk shifted by b,
+// the extra dword e) into acc.  Returns the record's hash in lane 0 of the
+// row at its merge round (valid where `merge`).
+__device__ __forceinline__ uint64_t wr_x3_round(const WrRow& r, const WrLoads& L, uint32_t c, const WrX3& X,
+                                                uint64_t& acc, bool act, bool& merge) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(&L.ch.v[0]);
+  const uint32_t nb = r.nb(), b = r.b();
+  const bool valid = act && (r.k < nb || (r.k == nb && c < r.nst()));
+  uint64_t W[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    const uint32_t lo = abyte(w[2 * q + 1], w[2 * q], b);
+    const uint32_t hi = abyte(2 * q + 2 < 16 ? w[2 * q + 2] : L.e, w[2 * q + 1], b);
+    W[q] = ((uint64_t)hi << 32) | lo;
+  }
+  uint64_t A[8];
+#pragma unroll
+  for (int q = 0; q < 8; q++) {
+    // v0.8.1: acc[q] += lo32(d ^ s) * hi32(d ^ s); acc[q ^ 1] += d
+    const uint64_t t = mul32to64(W[q] ^ lds_sec(c + q)) + W[q ^ 1];
+    A[q] = valid ? t : 0ull;
+  }
+  const uint64_t S = wr_row_reduce(A, c);
+  acc += act ? S : 0ull;
+  const bool full = act && r.k < nb;
+  acc = full ? xxh3_scramble(acc, X.ks) : acc;
+  merge = act && r.k == nb;
+  uint64_t h = 0;
+  if (wave_any(merge)) {
+    // the last stripe (util/xxhash.h:5160-5165): lane a < 8 holds its word a
+    const uint32_t s = (uint32_t)(r.P + r.len - 64 + 8 * (c & 7u)) & 3u;
+    const uint64_t lw = ((uint64_t)abyte(L.l2, L.l1, s) << 32) | abyte(L.l1, L.l0, s);
+    const uint64_t lx = dpp_u64<kDppQuadXor1>(lw);  // word a ^ 1
+    const uint64_t tl = mul32to64(lw ^ X.kl) + lx;
+    // lanes 0-7 hold accumulator a = c; lanes 8-15 the same sums (copies)
+    const uint64_t am = acc + (c < 8 ? tl : dpp_u64<kDppRowRor8>(tl));
+    // merge (util/xxhash.h:5182-5206): pairs (2i, 2i + 1) in lanes 2i, 2i + 1
+    const uint64_t mine = am ^ X.km;
+    const uint64_t odd = dpp_u64<kDppQuadXor1>(mine);
+    uint64_t m = (c & 1u) ? 0ull : mul128_fold64(mine, odd);
+    m += dpp_u64<kDppQuadXor2>(m);  // lanes 0 + 2, 4 + 6
+    m += dpp_u64<kDppRowRor4>(m);   // (0 + 2) + (4 + 6) in lane 0
+    h = xxh3_avalanche((uint64_t)r.len * P64_1 + m);
+  }
+  return h;
+}
+
+// One row round of the CRC: lane c's chunk into the lane's state (the row
+// driver's 4-byte table step), the record's init injected at lane 0 of
+// round 0, the bytes before the payload zeroed; in the record's last round
+// the lanes past its last byte keep their state.  Returns the state.
+__device__ __forceinline__ uint32_t wr_crc_round(uint32_t s, const WrRow& r, Chunk ch, uint32_t c,
+                                                 const CrcLane& L, bool act) {
+  const bool first = r.k == 0, last = r.k + 1 == r.R();
+  const uint32_t b = r.b();
+  uint32_t* w = reinterpret_cast<uint32_t*>(&ch.v[0]);
+  // first round, lane 0: the b bytes before the payload are zeros
+  if (first && c == 0) w[0] &= 0xFFFFFFFFu << (8 * b);
+  // last round: lane e keeps the first kb bytes of its chunk
+  const uint32_t E = r.len + b - 1024 * r.k;  // bytes of the round in the record (1..1024)
+  const uint32_t e = (E - 1) >> 6, kb = E - 64 * e;
+  if (last && c == e) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      const int kq = (int)kb - 4 * q;
+      w[q] = kq >= 4 ? w[q] : kq <= 0 ? 0u : w[q] & (0xFFFFFFFFu >> (8 * (4 - kq)));
+    }
+  }
+  uint32_t x = 0;
+  if (wave_any(!first)) x = crc_nibmap(row_gap_off<16>(), s);
+  x = first ? (c == 0 ? *lds_p32(kLdsRowInj + 4 * ((r.type() & 15u) * 64 + b)) : 0u) : x;
+  x ^= w[0];
+#pragma unroll
+  for (int k = 0; k < 16; k++) x = crc_step4x(x, L, k < 15 ? w[k + 1] : 0u);
+  return (act && !(last && c > e)) ? x : s;
+}
+
+// The record's CRC (Extend(type_crc, payload)) from the last round's states.
+__device__ __forceinline__ uint32_t wr_crc_finish(uint32_t s, const WrRow& r, uint32_t c) {
+  const uint32_t E = r.len + r.b() - 1024 * (r.R() - 1);
+  const uint32_t e = (E - 1) >> 6, kb = E - 64 * e;
+  // to the end of chunk e: lanes c <= e (this round) by 64 (e - c), lanes
+  // past e (the previous round) by 64 (16 + e - c)
+  const uint32_t j = c <= e ? e - c : 16 + e - c;
+  uint32_t p = row_xor32<16>(crc_lane_final4(s, (63u - j) << 2));
+  if (wave_any(kb != 64)) p = crc_unshift(64 - kb, p);
+  const uint32_t init = *lds_p32(kLdsRowInit + 4 * (r.type() & 15u));
+  return r.len == 0 ? init : ~p;
+}
+
+__device__ __forceinline__ uint4 wr_desc(uint32_t t, uint32_t share) {
+  const span_u32x4 v = *reinterpret_cast<__attribute__((address_space(3))) const span_u32x4*>(
+      static_cast<size_t>(kLdsWrDesc + 16 * (t < share ? t : 0)));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint32_t wr_ticket(bool take) {
+  uint32_t t = 0;
+  if ((threadIdx.x & 15) == 0 && take)
+    t = __hip_atomic_fetch_add(lds_p32(kLdsWrTicket), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((threadIdx.x & 48u) << 2), (int)t);
+}
+
+struct WrArgs {
+  const uint8_t* wal;
+  const WalRecDesc* recs;
+  uint32_t count;
+  uint8_t* ok;       // per record: 1 = the CRC holds
+  uint64_t* x3;      // per record: XXH3_64bits of its payload (hashed records)
+};
+
+// A window of the workgroup's records [w0, w0 + n): staged, then the rows loop.
+__device__ __forceinline__ void wr_rows_loop(const WrArgs& a, uint32_t w0, uint32_t n, const CrcLane& L,
+                                             const WrX3& X) {
+  const uint32_t c = threadIdx.x & 15u;
+  const uint64_t zp = reinterpret_cast<uint64_t>(&g_crc_tables.zero16[0]);
+  const uint64_t base = reinterpret_cast<uint64_t>(a.wal);
+  uint32_t t = wr_ticket(true);
+  bool live = t < n;
+  WrRow A = wr_row(wr_desc(t, n), w0 + (live ? t : 0), base);
+  WrLoads LA = wr_load(A, c, zp);
+  uint32_t nt = wr_ticket(true);
+  uint4 nd = wr_desc(nt, n);
+  uint32_t s = 0;
+  uint64_t acc = X.init;
+  while (wave_any(live)) {
+    const bool last = A.k + 1 == A.R();
+    const bool go = live && (!last || nt < n);
+    const bool sw = go && last;
+    WrRow B = A;
+    B.k = A.k + 1;
+    const WrRow N = wr_row(nd, w0 + (nt < n ? nt : 0), base);
+    B = wr_sel(sw, N, B);
+    const WrLoads LB = wr_load(B, c, zp);
+    if (wave_any(sw)) {
+      const uint32_t tk = wr_ticket(sw);
+      if (sw) {
+        nt = tk;
+        nd = wr_desc(tk, n);
+      }
+    }
+    // this round: CRC, then XXH3 from the same registers
+    s = wr_crc_round(s, A, LA.ch, c, L, live);
+    bool merge = false;
+    const bool xa = live && A.hash() == 1u && A.k <= A.nb();
+    uint64_t h = 0;
+    if (wave_any(xa)) h = wr_x3_round(A, LA, c, X, acc, xa, merge);
+    if (wave_any(live && last)) {
+      const uint32_t crc = wr_crc_finish(s, A, c);
+      if (live && last && c == 0) {
+        a.ok[A.i] = crc_mask(crc) == A.stored ? 1 : 0;
+        if (A.hash() == 2u) a.x3[A.i] = xxh3_short(reinterpret_cast<const uint8_t*>(A.P), A.len);
+      }
+      s = (live && last) ? 0u : s;
+    }
+    if (merge && c == 0) a.x3[A.i] = h;
+    if (merge || (live && last)) acc = X.init;
+    live = go;
+    A = B;
+    LA = LB;
+  }
+}
+
+// Workgroup b: a byte-balanced contiguous share of the records, in windows
+// of kWrDescCache staged in LDS.
+struct WrOffs {
+  const WalRecDesc* recs;
+  __device__ uint64_t off(uint32_t i) const {
+    const uint4 d = reinterpret_cast<const uint4*>(recs)[i];
+    return (uint64_t)d.x | ((uint64_t)(d.y & 0xFFFFu) << 32);
+  }
+};
+__global__ __launch_bounds__(1024) void k_wal_recover(WrArgs a, WalTypeCrcs tc) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  crc_fill_lds_any(lds, &g_crc_tables);
-  x3_row_lds_store();
+  asm volatile("" ::"v"((uint32_t)(size_t)lds));
+  uint32_t lo, hi;
+  share_by_bytes(WrOffs{a.recs}, 0u, a.count, a.count / gridDim.x + 1, lds_p32(kLdsWrTicket + 8), &lo, &hi,
+                 [&](uint32_t i) { return a.recs[i].len; });
+  crc_fill_rows(lds, &g_crc_tables);
+  if (threadIdx.x < 25) *lds_p64(kLdsWrSecret + 8 * threadIdx.x) = kXxh3SecretW.w[threadIdx.x];
   __syncthreads();
+  row_init_tables(WrOp{tc});
   const CrcLane L = crc_lane();
-  const X3Row XI = x3_row_idx();
-  uint64_t* tx = reinterpret_cast<uint64_t*>(lds + kLdsWalX3 + 1024u * (threadIdx.x >> 6));
-  const uint32_t wpb = blockDim.x >> 6;
-  const uint32_t nw = gridDim.x * wpb;
-  // block k's slots (wave-uniform: the loads go through the scalar cache)
-  auto slots_of = [&](uint32_t k, uint64_t& base, uint32_t& cap) {
-    if (!x3) {
-      base = 0;
-      cap = 0;
-    } else if (slot_base) {
-      base = slot_base[k];
-      cap = (uint32_t)(slot_base[k + 1] - base);
-    } else {
-      base = (uint64_t)k * nslots;
-      cap = nslots;
+  const WrX3 X = wr_x3(threadIdx.x & 15u);
+  const uint32_t n = hi - lo;
+  for (uint32_t w0 = 0; w0 < n; w0 += kWrDescCache) {
+    const uint32_t wn = n - w0 < kWrDescCache ? n - w0 : kWrDescCache;
+    __syncthreads();  // (the init tables are built / every row is done with the previous window)
+    for (uint32_t t = threadIdx.x; t < wn; t += blockDim.x) {
+      const uint4 d = reinterpret_cast<const uint4*>(a.recs)[lo + w0 + t];
+      *reinterpret_cast<__attribute__((address_space(3))) span_u32x4*>(static_cast<size_t>(kLdsWrDesc + 16 * t)) =
+          span_u32x4{d.x, d.y, d.z, d.w};
     }
-  };
-  uint32_t cb = __builtin_amdgcn_readfirstlane(blockIdx.x * wpb + (threadIdx.x >> 6));
-  if (cb >= nblocks) return;
-  auto block_size = [&](uint32_t k) {
-    const uint64_t rem = nbytes - (uint64_t)k * 32768;
-    return rem < 32768 ? (uint32_t)rem : 32768u;
-  };
-  auto last_block = [&](uint32_t k) { return nbytes - (uint64_t)k * 32768 <= 32768; };
-  auto emit = [&](uint32_t k, uint32_t ok, int32_t status, uint32_t pos) {
-    if ((threadIdx.x & 63) == 0) {
-      WalResult o;
-      o.records_ok = ok;
-      o.status = status;
-      o.stop_offset = status ? pos : block_size(k);
-      o.bytes_ok = pos;
-      res[k] = o;
-    }
-  };
-  // a block's first record from the 16-byte vector load h of its start
-  // (w1: header bytes 4-7 -- length, type, first log-number byte)
-  auto parse_first = [&](uint32_t k, const uint4& h) {
-    const uint32_t w1 = rfl_u32(h.y);
-    return wal_parse(block_size(k), last_block(k), log_number, w1,
-                     [&] { return (w1 >> 24) | (rfl_u32(h.z) << 8); });
-  };
-  uint32_t cpos = 0, cok = 0, kf = 0;  // record offset, records verified before it, full records before it
-  uint64_t xbase;
-  uint32_t xcap;
-  slots_of(cb, xbase, xcap);
-  uint4 hb = wal_hdr16(wal, cb);
-  bool seek = true;
-  WalRec rec{};
-  uint32_t stored = 0, type = 0;
-  CrcSpan sp = crc_span(wal, 0, 0u);
-  Chunk cur{};
-  for (;;) {
-    if (seek) {
-      for (;;) {  // finish blocks until a record to hash
-        const uint32_t left = block_size(cb) - cpos;
-        const uint8_t* h = wal + (uint64_t)cb * 32768 + cpos;
-        uint32_t w1 = 0;
-        if (cpos == 0) {
-          w1 = rfl_u32(hb.y);
-          rec = parse_first(cb, hb);
-          stored = rfl_u32(hb.x);
-        } else {
-          if (left >= 7) {
-            stored = rfl_u32(rd32_bytes(h));
-            w1 = rfl_u32((uint32_t)h[4] | ((uint32_t)h[5] << 8) | ((uint32_t)h[6] << 16));
-          }
-          rec = wal_parse(left, last_block(cb), log_number, w1, [&] { return rfl_u32(rd32_bytes(h + 7)); });
-        }
-        type = (w1 >> 16) & 0xFFu;
-        if (rec.go) break;
-        emit(cb, cok, rec.status, cpos);
-        cb += nw;
-        if (cb >= nblocks) return;
-        cpos = 0;
-        cok = 0;
-        kf = 0;
-        slots_of(cb, xbase, xcap);
-        hb = wal_hdr16(wal, cb);
-      }
-      sp = crc_span(wal + (uint64_t)cb * 32768 + cpos + 6, rec.length + rec.hsize - 6, 0u);
-      cur = crc_load_chunk<T>(sp, sp.rounds - 1, L);
-    }
-    const uint32_t size = block_size(cb);
-    const uint32_t e = cpos + rec.hsize + rec.length;
-    const uint32_t nb = cb + nw;
-    const bool spec = size - e < 7 && nb < nblocks;
-    const uint4 hn = wal_hdr16(wal, spec ? nb : cb);
-    WalRec nrec = rec;
-    auto next_span = [&] {
-      return nrec.go ? crc_span(wal + (uint64_t)nb * 32768 + 6, nrec.length + nrec.hsize - 6, 0u)
-                     : crc_span(wal + (uint64_t)nb * 32768, 0, 0u);
-    };
-    // the record's XXH3 (ReadRecord's record_checksum of a one-fragment record)
-    const bool full = type == 1u || type == 5u;
-    const bool slot = full && kf < xcap;
-    const OpWalX3 xop{x3 + xbase};
-    const uint64_t xptr = sp.ptr + rec.hsize - 6;  // the payload
-    const uint32_t xlen = rec.length;
-    const X3WSpan xs = x3w_span<false>(xptr, xlen, kf);
-    const uint32_t units = (slot && xlen > 240) ? xs.units : 0u;
-    const uint32_t iters = (uint32_t)sp.rounds > units ? (uint32_t)sp.rounds : units + 1;
-    uint64_t a = x3_row_lds().iw;
-    uint32_t s = 0;
-    for (uint32_t m = 0; m < iters; m++) {  // wave-uniform
-      const int r = sp.rounds - 1 - (int)m;    // CRC round (< 0: XXH3 only)
-      const bool xu = m >= 1 && m <= units;     // XXH3 unit m - 1
-      const bool xl = xu && m == units;         // ... the last one
-      // XXH3 loads first (L2), then the CRC load of the next window (or of
-      // the next block's first round with this record's last iteration)
-      X3RoundLoads R{};
-      X3WLoads XL{};
-      if (xu && !xl) R = x3w_round_load<false>(xs, m - 1, XI);
-      if (xl) XL = x3w_load<false>(xs, m - 1, XI);
-      Chunk nxt;
-      if (r > 0) {
-        nxt = crc_load_chunk<T>(sp, r - 1, L);
-      } else if (m + 1 == iters && spec) {
-        nrec = parse_first(nb, hn);
-        const CrcSpan nsp = next_span();
-        nxt = crc_load_chunk<T>(nsp, nsp.rounds - 1, L);
-      }
-      if (r >= 0) {
-        if (T && !(sp.mini && r == sp.rounds - 1)) row_transpose(cur);  // wave-uniform
-        s = crc_round(s, cur, sp, r, L);
-      }
-      if (r > 0 || (m + 1 == iters && spec)) cur = nxt;
-      if (xu && !xl) x3w_interior(xs, R, a, tx);
-      if (xl) x3w_fold<OpWalX3, false>(xop, xs, m - 1, XL, x3_row_lds(), a, NoPre{}, tx);
-    }
-    const bool pass = crc_mask(rfl_u32(crc_finish(s, sp, L))) == stored;
-    if (pass && slot && xlen <= 240 && (threadIdx.x & 63) == 0)
-      xop.finish(kf, xxh3_short(reinterpret_cast<const uint8_t*>(xptr), xlen));
-    if (!pass) {
-      emit(cb, cok, 1, cpos);  // kBadRecordChecksum
-    } else if (size - e < 7) {
-      emit(cb, cok + 1, last_block(cb) && size > e ? 5 : 0, e);
-    } else {  // the next record of the same block
-      cok++;
-      kf += full ? 1u : 0u;
-      cpos = e;
-      seek = true;
-      continue;
-    }
-    if (nb >= nblocks) return;
-    cb = nb;
-    cpos = 0;
-    cok = 0;
-    kf = 0;
-    slots_of(cb, xbase, xcap);
-    hb = spec ? hn : wal_hdr16(wal, cb);
-    seek = !(spec && nrec.go);
-    if (!seek) {  // pipelined: the record's first round is in cur
-      rec = nrec;
-      sp = next_span();
-      stored = rfl_u32(hn.x);
-      type = (rfl_u32(hn.y) >> 16) & 0xFFu;
-    }
+    if (threadIdx.x == 0) *lds_p32(kLdsWrTicket) = 0;
+    __syncthreads();
+    wr_rows_loop(a, lo + w0, wn, L, X);
   }
 }
 

@@ -55,12 +55,35 @@ def _image(oracle, recycle, lens, seed):
     return w, recs
 
 
+def _plan(S, torch, img):
+    plan = S.wal_plan_records(img, LOG)
+    return plan, torch.from_numpy(plan.view(np.int32)).cuda()
+
+
+def test_plan_records_lists_every_physical_record(oracle):
+    """mck_wal_plan_records (host) = the writer's physical records: payload
+    offset, type, length, stored CRC, the hash flag on full types."""
+    import speedb_amd as S
+    for recycle in (False, True):
+        w, _ = _image(oracle, recycle, EDGE_LENS, 2)
+        img = bytes(w.buf)
+        plan = S.wal_plan_records(img, LOG)
+        hs = 11 if recycle else 7
+        assert len(plan) == len(w.records)
+        for (off, t, n), d in zip(w.records, plan):
+            assert int(d[0]) | ((int(d[1]) & 0xFFFF) << 32) == off + hs
+            assert (int(d[1]) >> 16) & 0xFF == t and int(d[2]) == n
+            assert int(d[3]) == int.from_bytes(img[off:off + 4], "little")
+            assert bool(int(d[1]) & (1 << 24)) == (t in (1, 5))
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("recycle", [False, True])
-def test_recover_batch_equals_verify_and_oracle(gpu, oracle, recycle):
-    """Per-block results identical to mck_wal_verify_batch; the hash of the
-    k-th full record of block b at slot b * S + k equals the oracle's XXH3 of
-    its payload, for every edge length at many block offsets."""
+def test_recover_batch_equals_oracle(gpu, oracle, recycle):
+    """Every physical record's CRC verdict holds and every full record's hash
+    equals the oracle's XXH3 of its payload, for the edge lengths (XXH3's
+    length classes, the 1 KiB segment / 64-B stripe grid, the last round's
+    lane boundaries) at every payload alignment the headers produce."""
     import speedb_amd as S
     torch = gpu
     rng = np.random.default_rng(5)
@@ -68,53 +91,44 @@ def test_recover_batch_equals_verify_and_oracle(gpu, oracle, recycle):
     rng.shuffle(lens)
     w, _ = _image(oracle, recycle, lens, 11)
     img = bytes(w.buf)
-    d = torch.frombuffer(bytearray(img + bytes(64)), dtype=torch.uint8).cuda()
-    ver = S.wal_verify_batch(d, len(img), LOG).cpu().numpy()
-    slots = 64
-    res, h = S.wal_recover_batch(d, len(img), LOG, slots_per_block=slots)
-    assert (res.cpu().numpy() == ver).all()
-    assert (ver[:, 1] == 0).all()
+    # exactly 16 bytes of slack past the image (mck.h: readable 16 B past nbytes)
+    d = torch.frombuffer(bytearray(img + bytes(16)), dtype=torch.uint8).cuda()
+    plan, dp = _plan(S, torch, img)
+    ok, h = S.wal_recover_batch(d, dp, LOG)
+    assert (ok.cpu().numpy() == 1).all()
     hv = h.cpu().numpy().view(np.uint64)
-    full = _full_slots(w)
-    assert full and max(k for _, k in full) < slots
-    for (b, k), (off, n) in full.items():
-        hs = 11 if recycle else 7
-        assert int(hv[b * slots + k]) == oracle.XXH3(img[off + hs:off + hs + n]), (b, k, n)
+    hs = 11 if recycle else 7
+    for k, (off, t, n) in enumerate(w.records):
+        if t in (1, 5):
+            assert int(hv[k]) == oracle.XXH3(img[off + hs:off + hs + n]), (k, n, (off + hs) & 3)
 
 
 @pytest.mark.gpu
-def test_recover_batch_dense_slots_and_caps(gpu, oracle):
-    """slot_base: record k of block b at slot_base[b] + k, only for k <
-    slot_base[b + 1] - slot_base[b] (nothing is written past a block's cap:
-    the guard words survive); CRC only when no hash array is given."""
+def test_recover_batch_every_alignment_and_length(gpu, oracle):
+    """Payloads of 0..1100 B and around 2-4 KiB at all four dword
+    alignments, packed back to back in one image (legacy and recyclable
+    headers mixed): verdicts all hold and every hash matches."""
     import speedb_amd as S
     torch = gpu
-    rng = np.random.default_rng(9)
-    lens = [int(x) for x in rng.integers(0, 3000, size=400)]
-    w, _ = _image(oracle, False, lens, 3)
-    img = bytes(w.buf)
-    d = torch.frombuffer(bytearray(img + bytes(64)), dtype=torch.uint8).cuda()
-    full = _full_slots(w)
-    nb = (len(img) + K_BLOCK - 1) // K_BLOCK
-    counts = np.zeros(nb, np.int64)
-    for (b, k) in full:
-        counts[b] = max(counts[b], k + 1)
-    caps = np.maximum(counts - (np.arange(nb) % 3), 0)  # some blocks get fewer slots than records
-    base = np.zeros(nb + 1, np.int64)
-    base[1:] = np.cumsum(caps)
-    guard = 0x5A5A5A5A5A5A5A5A
-    hashes = torch.full((int(base[-1]) + 8,), guard, dtype=torch.int64, device="cuda")
-    res, h = S.wal_recover_batch(d, len(img), LOG, slot_base=torch.from_numpy(base).cuda(), hashes=hashes)
-    hv = h.cpu().numpy().view(np.uint64)
-    seen = set()
-    for (b, k), (off, n) in full.items():
-        if k < caps[b]:
-            assert int(hv[base[b] + k]) == oracle.XXH3(img[off + 7:off + 7 + n])
-            seen.add(int(base[b] + k))
-    assert len(seen) == int(base[-1])
-    assert (hv[int(base[-1]):] == np.uint64(guard)).all()
-    res2, none = S.wal_recover_batch(d, len(img), LOG)
-    assert none is None and (res2.cpu().numpy() == res.cpu().numpy()).all()
+    rng = np.random.default_rng(77)
+    lens = list(range(0, 1100, 7)) + [int(x) for x in rng.integers(1900, 4300, size=80)]
+    rng.shuffle(lens)
+    w = WalWriter(oracle, log_number=LOG, recycle=False)
+    w2 = WalWriter(oracle, log_number=LOG, recycle=True)
+    for n in lens:
+        p = _payload(rng, n)
+        (w if n % 2 else w2).add_record(p)
+    for ww in (w, w2):
+        img = bytes(ww.buf)
+        d = torch.frombuffer(bytearray(img + bytes(16)), dtype=torch.uint8).cuda()
+        plan, dp = _plan(S, torch, img)
+        ok, h = S.wal_recover_batch(d, dp, LOG)
+        assert (ok.cpu().numpy() == 1).all()
+        hv = h.cpu().numpy().view(np.uint64)
+        hs = 11 if ww.recycle else 7
+        for k, (off, t, n) in enumerate(ww.records):
+            if t in (1, 5):
+                assert int(hv[k]) == oracle.XXH3(img[off + hs:off + hs + n]), (k, n)
 
 
 @pytest.mark.gpu
@@ -138,8 +152,13 @@ def test_recover_corrupt_records(gpu, oracle, recycle):
     img = bytes(img)
     d = torch.frombuffer(bytearray(img + bytes(64)), dtype=torch.uint8).cuda()
     ver = S.wal_verify_batch(d, len(img), LOG).cpu().numpy()
-    res, h = S.wal_recover_batch(d, len(img), LOG, slots_per_block=32)
-    assert (res.cpu().numpy() == ver).all() and (ver[:, 1] == 1).any()
+    assert (ver[:, 1] == 1).any()
+    plan, dp = _plan(S, torch, img)
+    ok, _ = S.wal_recover_batch(d, dp, LOG)
+    bad = {o + hs + n // 2 for o, n in fulls[5::37]}
+    want_ok = [0 if any(p <= x < p + n for x in bad) else 1
+               for p, n in ((int(r[0]) | ((int(r[1]) & 0xFFFF) << 32), int(r[2])) for r in plan)]
+    assert ok.cpu().numpy().tolist() == want_ok
     for mode in (kTolerate, kAbsolute, kPIT, kSkipAny):
         r = S.WalRecover(img, LOG, mode)
         plan = S.wal_read_records(img, LOG, mode, ver)
@@ -148,6 +167,9 @@ def test_recover_corrupt_records(gpu, oracle, recycle):
         assert len(recs) == len(plan.rec_lengths)
         assert [int(x) for x in r.record_checksums] == [oracle.XXH3(x) for x in recs]
         assert r.info.host_walks == 2
+        # the per-block verdicts derived from the per-record ones are the
+        # device walk's (mck_wal_verify_batch)
+        assert (r.blocks.numpy() == ver).all()
 
 
 @pytest.mark.gpu
@@ -182,17 +204,18 @@ def test_wal_recover_mixed_records_at_scale(gpu, oracle, recycle):
 @pytest.mark.gpu
 def test_recover_configs3_shape(gpu, oracle):
     """configs[3]'s layout (one kFullType 32761-byte record per 32 KiB
-    block), more blocks than the grid has waves: every block's hash at slot
-    b equals the oracle's XXH3 of its payload, verify results all OK."""
+    block, payloads at offset 7 of their block), more records than the grid
+    has rows: every verdict holds, every hash equals the oracle's."""
     import speedb_amd as S
     from speedb_amd import workloads as W
     torch = gpu
     im = W.WalImage(6000, "cuda", seed=4, log_number=LOG)
-    res, h = S.wal_recover_batch(im.data, im.nbytes, LOG, slots_per_block=1)
-    r = res.cpu().numpy()
-    assert (r[:, 0] == 1).all() and (r[:, 1] == 0).all()
-    host = im.data[:im.nbytes].cpu().numpy().reshape(-1, K_BLOCK)
+    host = im.data[:im.nbytes].cpu().numpy()
+    plan, dp = _plan(S, torch, host.tobytes())
+    assert len(plan) == im.nblocks
+    ok, h = S.wal_recover_batch(im.data, dp, LOG)
+    assert (ok.cpu().numpy() == 1).all()
     hv = h.cpu().numpy().view(np.uint64)
+    blocks = host.reshape(-1, K_BLOCK)
     for b in range(im.nblocks):
-        assert int(hv[b]) == oracle.XXH3(host[b, 7:].tobytes()), b
-    torch.cuda.synchronize()
+        assert int(hv[b]) == oracle.XXH3(blocks[b, 7:].tobytes()), b
