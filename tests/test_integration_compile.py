@@ -30,6 +30,14 @@ int main() {
   mck_sst_footer sf{};
   uint64_t n = 0;
   (void)mck_sst_list_blocks_uncompress(nullptr, 0, &A::UncompressWithReference, &uc, &sf, nullptr, 0, &n);
+  A::GpuLogRecoveryReader reader(nullptr, 7);
+  (void)reader.Recover(nullptr, nullptr, 0, ROCKSDB_NAMESPACE::WALRecoveryMode::kPointInTimeRecovery);
+  ROCKSDB_NAMESPACE::Slice rec;
+  std::string scratch;
+  uint64_t sum = 0;
+  (void)reader.ReadRecord(&rec, &scratch, ROCKSDB_NAMESPACE::WALRecoveryMode::kPointInTimeRecovery, &sum);
+  std::vector<std::array<char, 5>> tr;
+  (void)A::ComputeBlockTrailers(ROCKSDB_NAMESPACE::kCRC32c, 0, nullptr, 0, hs, {}, &tr);
   return g ? 0 : 1;
 }
 """
@@ -51,6 +59,31 @@ def _compile(tmp_path, header_text=None):
 def test_adapters_compile_against_reference_headers(tmp_path):
     r = _compile(tmp_path)
     assert r.returncode == 0, r.stderr[-4000:]
+
+
+# one drift per pin: the edited header must fail with that pin's message
+DRIFTS = [
+    ("MCK_WAL_kPointInTimeRecovery &&", "MCK_WAL_kSkipAnyCorruptedRecords &&", "WALRecoveryMode values differ"),
+    ("rdb::log::kBlockSize == MCK_WAL_kBlockSize", "rdb::log::kBlockSize == 2 * MCK_WAL_kBlockSize",
+     "WAL block / header sizes differ"),
+    ("(int)rdb::log::kLastType == speedb_amd::log::kLastType", "(int)rdb::log::kLastType == speedb_amd::log::kMiddleType",
+     "WAL record types differ"),
+    ("void(size_t, const rdb::Status&)>::value", "void(uint32_t, const rdb::Status&)>::value",
+     "Reporter::Corruption signature drifted"),
+    ("bool(rdb::Slice*, std::string*, rdb::WALRecoveryMode, uint64_t*)>::value",
+     "bool(rdb::Slice*, std::string*, rdb::WALRecoveryMode, uint32_t*)>::value", "ReadRecord signature drifted"),
+    ("rdb::BlockBasedTable::kBlockTrailerSize == 5", "rdb::BlockBasedTable::kBlockTrailerSize == 4",
+     "block trailer is [type][LE32]"),
+]
+
+
+@pytest.mark.parametrize("old,new,msg", DRIFTS, ids=[d[2].split()[0] + "_" + str(i) for i, d in enumerate(DRIFTS)])
+def test_wal_and_trailer_pins_bite(tmp_path, old, new, msg):
+    src = open(os.path.join(REPO, "integration", "rocksdb_adapters.h")).read()
+    drift = src.replace(old, new, 1)
+    assert drift != src, old
+    r = _compile(tmp_path, drift)
+    assert r.returncode != 0 and msg in r.stderr, r.stderr[-2000:]
 
 
 def test_signature_drift_fails(tmp_path):
