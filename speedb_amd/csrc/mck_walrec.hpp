@@ -43,20 +43,28 @@ struct WalRecDesc {
 };
 static_assert(sizeof(WalRecDesc) == 16, "descriptor");
 
-// LDS: the row drivers' image (crc_fill_rows: wave image + row gap maps,
-// row_init_tables: typed init + masks), then this kernel's descriptor cache,
-// ticket and the XXH3 secret words.
-constexpr uint32_t kWrDescCache = 1400;
-constexpr uint32_t kLdsWrDesc = kLdsRowDesc;
+// LDS: the row drivers' image (crc_fill_rows: wave image + row gap maps),
+// then this kernel's init tables (every type byte 0-255: a corrupt record's
+// type byte is CRC'd as it is, "unknown record type" comes after the CRC),
+// descriptor cache, ticket and the XXH3 secret words.
+constexpr uint32_t kLdsWrInj = kLdsRowInj;                   // [256][4] u32: unshift(~init_t, b)
+constexpr uint32_t kLdsWrInit = kLdsWrInj + 4096;            // [256] u32: init_t
+constexpr uint32_t kWrDescCache = 1300;
+constexpr uint32_t kLdsWrDesc = kLdsWrInit + 1024;
 constexpr uint32_t kLdsWrTicket = kLdsWrDesc + 16 * kWrDescCache;
 constexpr uint32_t kLdsWrSecret = kLdsWrTicket + 64;  // 25 u64 words of XXH3_kSecret
-static_assert(kLdsWrSecret + 8 * 25 <= kLdsRowMaskHead, "below the row mask tables");
+static_assert(kLdsWrSecret + 8 * 25 <= kLdsStep, "below the step tables");
 
-struct WrOp {  // row_init_tables' interface (typed init = type_crc[t] with the log number)
-  WalTypeCrcs tc;
-  static constexpr bool kTypedInit = true;
-  __device__ uint32_t typed_init(uint32_t t) const { return tc.v[t & 15]; }
-};
+// The CRC init of a record of type t: type_crc[t] (+ the log number for the
+// recyclable types, db/log_writer.cc:48-51, 281-289) for the 16 codes the
+// host table holds, Value(&t, 1) beyond; and the same un-shifted by b < 4
+// bytes (the lane-0 injection).  After crc_fill_rows' barrier.
+__device__ __forceinline__ void wr_init_tables(const WalTypeCrcs& tc) {
+  const uint32_t t = threadIdx.x >> 2, b = threadIdx.x & 3u;  // 1024 threads = 256 x 4
+  const uint32_t init = t < 16 ? tc.v[t] : crc_extend_byte(0u, (uint8_t)t);
+  *lds_p32(kLdsWrInj + 4 * threadIdx.x) = crc_unshift(b, ~init);
+  if (b == 0) *lds_p32(kLdsWrInit + 4 * t) = init;
+}
 
 // A row's record and round (the derived geometry is recomputed where it is
 // used: the row state stays at 7 VGPRs, three copies of it are live).
@@ -222,8 +230,11 @@ __device__ __forceinline__ uint64_t wr_x3_round(const WrRow& r, const WrLoads& L
     const uint64_t lw = ((uint64_t)abyte(L.l2, L.l1, s) << 32) | abyte(L.l1, L.l0, s);
     const uint64_t lx = dpp_u64<kDppQuadXor1>(lw);  // word a ^ 1
     const uint64_t tl = mul32to64(lw ^ X.kl) + lx;
-    // lanes 0-7 hold accumulator a = c; lanes 8-15 the same sums (copies)
-    const uint64_t am = acc + (c < 8 ? tl : dpp_u64<kDppRowRor8>(tl));
+    // lanes 0-7 hold accumulator a = c; lanes 8-15 the same sums (copies).
+    // (the DPP result taken before the ?: -- inside it clang branches, and
+    // the move would read the masked-off lanes 0-7 as zeros)
+    const uint64_t tl8 = dpp_u64<kDppRowRor8>(tl);
+    const uint64_t am = acc + (c < 8 ? tl : tl8);
     // merge (util/xxhash.h:5182-5206): pairs (2i, 2i + 1) in lanes 2i, 2i + 1
     const uint64_t mine = am ^ X.km;
     const uint64_t odd = dpp_u64<kDppQuadXor1>(mine);
@@ -258,7 +269,7 @@ __device__ __forceinline__ uint32_t wr_crc_round(uint32_t s, const WrRow& r, Chu
   }
   uint32_t x = 0;
   if (wave_any(!first)) x = crc_nibmap(row_gap_off<16>(), s);
-  x = first ? (c == 0 ? *lds_p32(kLdsRowInj + 4 * ((r.type() & 15u) * 64 + b)) : 0u) : x;
+  x = first ? (c == 0 ? *lds_p32(kLdsWrInj + 4 * (r.type() * 4 + b)) : 0u) : x;
   x ^= w[0];
 #pragma unroll
   for (int k = 0; k < 16; k++) x = crc_step4x(x, L, k < 15 ? w[k + 1] : 0u);
@@ -274,8 +285,7 @@ __device__ __forceinline__ uint32_t wr_crc_finish(uint32_t s, const WrRow& r, ui
   const uint32_t j = c <= e ? e - c : 16 + e - c;
   uint32_t p = row_xor32<16>(crc_lane_final4(s, (63u - j) << 2));
   if (wave_any(kb != 64)) p = crc_unshift(64 - kb, p);
-  const uint32_t init = *lds_p32(kLdsRowInit + 4 * (r.type() & 15u));
-  return r.len == 0 ? init : ~p;
+  return r.len == 0 ? *lds_p32(kLdsWrInit + 4 * r.type()) : ~p;
 }
 
 __device__ __forceinline__ uint4 wr_desc(uint32_t t, uint32_t share) {
@@ -368,7 +378,7 @@ __global__ __launch_bounds__(1024) void k_wal_recover(WrArgs a, WalTypeCrcs tc) 
   crc_fill_rows(lds, &g_crc_tables);
   if (threadIdx.x < 25) *lds_p64(kLdsWrSecret + 8 * threadIdx.x) = kXxh3SecretW.w[threadIdx.x];
   __syncthreads();
-  row_init_tables(WrOp{tc});
+  wr_init_tables(tc);
   const CrcLane L = crc_lane();
   const WrX3 X = wr_x3(threadIdx.x & 15u);
   const uint32_t n = hi - lo;
