@@ -501,8 +501,8 @@ def make_workload(args, dev, rank, world):
         # what recovery must move: the log once, the 16-B plan entry, the
         # 1-B verdict and the 8-B record_checksum of every physical record
         w.alg_bytes = nbytes + nphys * (16 + 1 + 8)
-        w.kernel = ("mck::k_wal_recover" if not nm else
-                    "mck::k_wal_recover + k_wal_gather + mck::k_xxh3 (whole step)")
+        w.kernel = ("mck::k_wal_recover<true>" if not nm else
+                    "mck::k_wal_recover<true> + k_wal_gather + mck::k_xxh3 (whole step)")
         shape = ("one kFullType 32761-B record per 32 KiB block (BASELINE.json configs[3] layout)"
                  if args.walrec_shape == "full32k" else
                  f"{nrec} records of 100-4096 B (device writer), {nm} of them block-straddling (gathered + hashed)")

@@ -889,12 +889,15 @@ int mck_wal_recover_batch(const void* wal, const mck_wal_rec_desc* recs, uint32_
   }
   int dev, ncu;
   if (int rc = current_device(&dev, &ncu)) return rc;
-  if (int rc = ensure_lds(k_wal_recover, dev)) return rc;
   const uint32_t grid = std::min<uint32_t>(ncu, (count + 63) / 64);
   const WrArgs a{static_cast<const uint8_t*>(wal), reinterpret_cast<const WalRecDesc*>(recs), count, crc_ok,
                  record_hashes};
-  hipLaunchKernelGGL(k_wal_recover, dim3(grid), dim3(1024), kCrcLdsBytes, reinterpret_cast<hipStream_t>(stream), a,
-                     wal_type_crcs(log_number));
+  // (round 6 A/B: the rows loop unrolled twice, its rows and loads swapping
+  // register names, 0.640 / 0.317 of peak on the 32 KiB / 100 B - 4 KiB logs
+  // against 0.629 / 0.313 copying them every round; profiles/r6/walrec_ab/)
+  if (int rc = ensure_lds(k_wal_recover<true>, dev)) return rc;
+  hipLaunchKernelGGL(k_wal_recover<true>, dim3(grid), dim3(1024), kCrcLdsBytes, reinterpret_cast<hipStream_t>(stream),
+                     a, wal_type_crcs(log_number));
   MCK_HIP(hipGetLastError());
   return MCK_OK;
 }

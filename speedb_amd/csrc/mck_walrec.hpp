@@ -121,19 +121,25 @@ struct WrLoads {
   uint32_t e;
   uint32_t l0, l1, l2;
 };
-__device__ __forceinline__ WrLoads wr_load(const WrRow& r, uint32_t c, uint64_t zp) {
+__device__ __forceinline__ WrLoads wr_load(const WrRow& r, uint32_t c) {
   WrLoads L;
-  const uint64_t cb = r.a0() + 1024ull * r.k + 64ull * c;
-  const uint64_t end = r.P + r.len;
+  // offsets from the grid base a0; a piece past the record reads the
+  // record's last dword instead (clamped: one v_min per address, no 64-bit
+  // compare-and-select), whose data the rounds mask out
+  const uint64_t a0 = r.a0();
+  const uint32_t cover = r.len + r.b();
+  const uint32_t lim = cover ? (cover - 1) & ~3u : 0u;  // the last dword of the record (or its start)
+  const uint32_t cb = 1024u * r.k + 64u * c;
 #pragma unroll
-  for (int j = 0; j < 4; j++) L.ch.v[j] = span_load16<false>(cb + 16 * j < end ? cb + 16 * j : zp);
-  L.e = gload4(cb + 64 < end ? cb + 64 : zp);
+  for (int j = 0; j < 4; j++) L.ch.v[j] = span_load16<false>(a0 + min(cb + 16u * j, lim));
+  L.e = gload4(a0 + min(cb + 64u, lim));
+  // the last stripe's word c (lanes 0-7), as the three dwords covering it;
+  // other lanes and rounds read the record's first dword
   const bool ls = r.hash() == 1u && r.k == r.nb() && c < 8;
-  const uint64_t w = end - 64 + 8ull * c;  // word c of the last stripe
-  const uint64_t w4 = w & ~3ull;
-  L.l0 = gload4(ls ? w4 : zp);
-  L.l1 = gload4(ls ? w4 + 4 : zp);
-  L.l2 = gload4(ls && w4 + 8 < end ? w4 + 8 : zp);
+  const uint32_t w4 = ls ? (cover - 64 + 8 * c) & ~3u : 0u;
+  L.l0 = gload4(a0 + w4);
+  L.l1 = gload4(a0 + min(w4 + 4, lim));
+  L.l2 = gload4(a0 + min(w4 + 8, lim));
   return L;
 }
 
@@ -176,24 +182,26 @@ __device__ __forceinline__ uint64_t wr_row_reduce(const uint64_t (&A)[8], uint32
 
 __device__ __forceinline__ uint64_t lds_sec(uint32_t w) { return *lds_p64(kLdsWrSecret + 8 * w); }
 
-// Per-lane XXH3 constants: lane c keeps accumulator a = c & 7.
+// Per-lane XXH3 constants: lane c keeps accumulator a = c & 7.  Only the
+// scramble secret stays in registers; XXH3_INIT_ACC and the last-stripe /
+// merge secrets (once per record) are read from LDS where they are used.
+constexpr uint32_t kLdsWrInitAcc = kLdsWrSecret + 8 * 25;  // [8] u64 XXH3_INIT_ACC
+static_assert(kLdsWrInitAcc + 64 <= kLdsStep, "below the step tables");
 struct WrX3 {
-  uint64_t init;  // XXH3_INIT_ACC[a]
-  uint64_t ks;    // scramble secret (offset 128 + 8 a)
-  uint64_t kl;    // last-stripe secret (offset 121 + 8 a)
-  uint64_t km;    // merge secret (offset 11 + 8 a)
+  uint64_t ks;  // scramble secret (offset 128 + 8 a)
+  __device__ uint64_t init(uint32_t c) const { return *lds_p64(kLdsWrInitAcc + 8 * (c & 7u)); }
 };
 __device__ __forceinline__ WrX3 wr_x3(uint32_t c) {
-  const uint32_t a = c & 7u;
   WrX3 X;
-  const uint64_t ia[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
-  X.init = ia[0];
-#pragma unroll
-  for (int k = 1; k < 8; k++) X.init = a == (uint32_t)k ? ia[k] : X.init;
-  X.ks = sec64(128 + 8 * (int)a);
-  X.kl = sec64(121 + 8 * (int)a);
-  X.km = sec64(11 + 8 * (int)a);
+  X.ks = sec64(128 + 8 * (int)(c & 7u));
   return X;
+}
+// 8 secret bytes at byte offset 8 w + B, 0 < B < 8 (the merge secrets at
+// 11 + 8 a = 8 (1 + a) + 3, the last stripe's at 121 + 8 a = 8 (15 + a) + 1)
+template <int B>
+__device__ __forceinline__ uint64_t lds_sec_at(uint32_t w) {
+  const uint64_t lo = *lds_p64(kLdsWrSecret + 8 * w), hi = *lds_p64(kLdsWrSecret + 8 * w + 8);
+  return (lo >> (8 * B)) | (hi << (64 - 8 * B));
 }
 
 // One row round of XXH3: stripe c of segment k (lane c's chunk shifted by b,
@@ -203,7 +211,6 @@ __device__ __forceinline__ uint64_t wr_x3_round(const WrRow& r, const WrLoads& L
                                                 uint64_t& acc, bool act, bool& merge) {
   const uint32_t* w = reinterpret_cast<const uint32_t*>(&L.ch.v[0]);
   const uint32_t nb = r.nb(), b = r.b();
-  const bool valid = act && (r.k < nb || (r.k == nb && c < r.nst()));
   uint64_t W[8];
 #pragma unroll
   for (int q = 0; q < 8; q++) {
@@ -215,8 +222,14 @@ __device__ __forceinline__ uint64_t wr_x3_round(const WrRow& r, const WrLoads& L
 #pragma unroll
   for (int q = 0; q < 8; q++) {
     // v0.8.1: acc[q] += lo32(d ^ s) * hi32(d ^ s); acc[q ^ 1] += d
-    const uint64_t t = mul32to64(W[q] ^ lds_sec(c + q)) + W[q ^ 1];
-    A[q] = valid ? t : 0ull;
+    A[q] = mul32to64(W[q] ^ lds_sec(c + q)) + W[q ^ 1];
+  }
+  // only the partial segment's stripes past nst drop out (a row that does
+  // not hash this round reduces garbage into its own sum, unused)
+  if (wave_any(act && r.k == nb)) {
+    const bool valid = r.k < nb || c < r.nst();
+#pragma unroll
+    for (int q = 0; q < 8; q++) A[q] = valid ? A[q] : 0ull;
   }
   const uint64_t S = wr_row_reduce(A, c);
   acc += act ? S : 0ull;
@@ -229,14 +242,14 @@ __device__ __forceinline__ uint64_t wr_x3_round(const WrRow& r, const WrLoads& L
     const uint32_t s = (uint32_t)(r.P + r.len - 64 + 8 * (c & 7u)) & 3u;
     const uint64_t lw = ((uint64_t)abyte(L.l2, L.l1, s) << 32) | abyte(L.l1, L.l0, s);
     const uint64_t lx = dpp_u64<kDppQuadXor1>(lw);  // word a ^ 1
-    const uint64_t tl = mul32to64(lw ^ X.kl) + lx;
+    const uint64_t tl = mul32to64(lw ^ lds_sec_at<1>(15 + (c & 7u))) + lx;  // offset 121 + 8 a
     // lanes 0-7 hold accumulator a = c; lanes 8-15 the same sums (copies).
     // (the DPP result taken before the ?: -- inside it clang branches, and
     // the move would read the masked-off lanes 0-7 as zeros)
     const uint64_t tl8 = dpp_u64<kDppRowRor8>(tl);
     const uint64_t am = acc + (c < 8 ? tl : tl8);
     // merge (util/xxhash.h:5182-5206): pairs (2i, 2i + 1) in lanes 2i, 2i + 1
-    const uint64_t mine = am ^ X.km;
+    const uint64_t mine = am ^ lds_sec_at<3>(1 + (c & 7u));  // offset 11 + 8 a
     const uint64_t odd = dpp_u64<kDppQuadXor1>(mine);
     uint64_t m = (c & 1u) ? 0ull : mul128_fold64(mine, odd);
     m += dpp_u64<kDppQuadXor2>(m);  // lanes 0 + 2, 4 + 6
@@ -309,54 +322,83 @@ struct WrArgs {
 };
 
 // A window of the workgroup's records [w0, w0 + n): staged, then the rows loop.
+struct WrCtx {
+  const WrArgs& a;
+  uint32_t w0, n, c;
+  uint64_t base;
+  const CrcLane& L;
+  const WrX3& X;
+};
+// One iteration: round A.k of A's record (loads LA) is hashed while B -- the
+// row's next round or its next record's first -- is set up and loaded.
+// Returns whether any row goes on.
+__device__ __forceinline__ bool wr_step(const WrCtx& x, const WrRow& A, const WrLoads& LA, bool live, WrRow& B,
+                                        WrLoads& LB, bool& blive, uint32_t& nt, uint4& nd, uint32_t& s,
+                                        uint64_t& acc) {
+  const uint32_t c = x.c;
+  const bool last = A.k + 1 == A.R();
+  const bool go = live && (!last || nt < x.n);
+  const bool sw = go && last;
+  B = A;
+  B.k = A.k + 1;
+  const WrRow N = wr_row(nd, x.w0 + (nt < x.n ? nt : 0), x.base);
+  B = wr_sel(sw, N, B);
+  LB = wr_load(B, c);
+  if (wave_any(sw)) {
+    const uint32_t tk = wr_ticket(sw);
+    if (sw) {
+      nt = tk;
+      nd = wr_desc(tk, x.n);
+    }
+  }
+  // this round: CRC, then XXH3 from the same registers
+  s = wr_crc_round(s, A, LA.ch, c, x.L, live);
+  bool merge = false;
+  const bool xa = live && A.hash() == 1u && A.k <= A.nb();
+  uint64_t h = 0;
+  if (wave_any(xa)) h = wr_x3_round(A, LA, c, x.X, acc, xa, merge);
+  if (wave_any(live && last)) {
+    const uint32_t crc = wr_crc_finish(s, A, c);
+    if (live && last && c == 0) {
+      x.a.ok[A.i] = crc_mask(crc) == A.stored ? 1 : 0;
+      if (A.hash() == 2u) x.a.x3[A.i] = xxh3_short(reinterpret_cast<const uint8_t*>(A.P), A.len);
+    }
+    s = (live && last) ? 0u : s;
+  }
+  if (merge && c == 0) x.a.x3[A.i] = h;
+  if (merge || (live && last)) acc = x.X.init(c);
+  blive = go;
+  return wave_any(go);
+}
+
+// A window of the workgroup's records [w0, w0 + n) (staged), the rows loop
+// unrolled twice so the two iterations' rows and loads swap register names
+// instead of being copied every round.
+template <bool U2>
 __device__ __forceinline__ void wr_rows_loop(const WrArgs& a, uint32_t w0, uint32_t n, const CrcLane& L,
                                              const WrX3& X) {
   const uint32_t c = threadIdx.x & 15u;
-  const uint64_t zp = reinterpret_cast<uint64_t>(&g_crc_tables.zero16[0]);
-  const uint64_t base = reinterpret_cast<uint64_t>(a.wal);
+  const WrCtx x{a, w0, n, c, reinterpret_cast<uint64_t>(a.wal), L, X};
   uint32_t t = wr_ticket(true);
-  bool live = t < n;
-  WrRow A = wr_row(wr_desc(t, n), w0 + (live ? t : 0), base);
-  WrLoads LA = wr_load(A, c, zp);
+  bool la = t < n, lb = false;
+  WrRow A = wr_row(wr_desc(t, n), w0 + (la ? t : 0), x.base), B;
+  WrLoads LA = wr_load(A, c), LB;
   uint32_t nt = wr_ticket(true);
   uint4 nd = wr_desc(nt, n);
   uint32_t s = 0;
-  uint64_t acc = X.init;
-  while (wave_any(live)) {
-    const bool last = A.k + 1 == A.R();
-    const bool go = live && (!last || nt < n);
-    const bool sw = go && last;
-    WrRow B = A;
-    B.k = A.k + 1;
-    const WrRow N = wr_row(nd, w0 + (nt < n ? nt : 0), base);
-    B = wr_sel(sw, N, B);
-    const WrLoads LB = wr_load(B, c, zp);
-    if (wave_any(sw)) {
-      const uint32_t tk = wr_ticket(sw);
-      if (sw) {
-        nt = tk;
-        nd = wr_desc(tk, n);
-      }
+  uint64_t acc = X.init(c);
+  if (!wave_any(la)) return;
+  if constexpr (U2) {
+    for (;;) {
+      if (!wr_step(x, A, LA, la, B, LB, lb, nt, nd, s, acc)) break;
+      if (!wr_step(x, B, LB, lb, A, LA, la, nt, nd, s, acc)) break;
     }
-    // this round: CRC, then XXH3 from the same registers
-    s = wr_crc_round(s, A, LA.ch, c, L, live);
-    bool merge = false;
-    const bool xa = live && A.hash() == 1u && A.k <= A.nb();
-    uint64_t h = 0;
-    if (wave_any(xa)) h = wr_x3_round(A, LA, c, X, acc, xa, merge);
-    if (wave_any(live && last)) {
-      const uint32_t crc = wr_crc_finish(s, A, c);
-      if (live && last && c == 0) {
-        a.ok[A.i] = crc_mask(crc) == A.stored ? 1 : 0;
-        if (A.hash() == 2u) a.x3[A.i] = xxh3_short(reinterpret_cast<const uint8_t*>(A.P), A.len);
-      }
-      s = (live && last) ? 0u : s;
+  } else {
+    while (wr_step(x, A, LA, la, B, LB, lb, nt, nd, s, acc)) {
+      A = B;
+      LA = LB;
+      la = lb;
     }
-    if (merge && c == 0) a.x3[A.i] = h;
-    if (merge || (live && last)) acc = X.init;
-    live = go;
-    A = B;
-    LA = LB;
   }
 }
 
@@ -369,6 +411,7 @@ struct WrOffs {
     return (uint64_t)d.x | ((uint64_t)(d.y & 0xFFFFu) << 32);
   }
 };
+template <bool U2>
 __global__ __launch_bounds__(1024) void k_wal_recover(WrArgs a, WalTypeCrcs tc) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   asm volatile("" ::"v"((uint32_t)(size_t)lds));
@@ -377,6 +420,12 @@ __global__ __launch_bounds__(1024) void k_wal_recover(WrArgs a, WalTypeCrcs tc) 
                  [&](uint32_t i) { return a.recs[i].len; });
   crc_fill_rows(lds, &g_crc_tables);
   if (threadIdx.x < 25) *lds_p64(kLdsWrSecret + 8 * threadIdx.x) = kXxh3SecretW.w[threadIdx.x];
+  if (threadIdx.x >= 32 && threadIdx.x < 40) {  // XXH3_INIT_ACC (util/xxhash.h:5208-5209)
+    const uint32_t q = threadIdx.x - 32;
+    const uint64_t ia = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_1 : q == 2 ? P64_2 : q == 3 ? P64_3
+                      : q == 4 ? P64_4 : q == 5 ? (uint64_t)P32_2 : q == 6 ? P64_5 : (uint64_t)P32_1;
+    *lds_p64(kLdsWrInitAcc + 8 * q) = ia;
+  }
   __syncthreads();
   wr_init_tables(tc);
   const CrcLane L = crc_lane();
@@ -392,7 +441,7 @@ __global__ __launch_bounds__(1024) void k_wal_recover(WrArgs a, WalTypeCrcs tc) 
     }
     if (threadIdx.x == 0) *lds_p32(kLdsWrTicket) = 0;
     __syncthreads();
-    wr_rows_loop(a, lo + w0, wn, L, X);
+    wr_rows_loop<U2>(a, lo + w0, wn, L, X);
   }
 }
 
