@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/speedb_amd/mck.h"
@@ -187,6 +188,10 @@ struct WalReader {
         if (!read_more(drop_size, &r)) return r;
         continue;
       }
+      if (phys && !phys->empty()) {  // the headers ahead are known: fetch them while this one is parsed
+        while (pcur + 1 < phys->size() && (*phys)[pcur].hoff < buf_off) pcur++;
+        __builtin_prefetch(d + (*phys)[std::min<size_t>(pcur + 16, phys->size() - 1)].hoff);
+      }
       const uint8_t* h = d + buf_off;
       const uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
       const uint32_t type = header_type(h);
@@ -227,6 +232,9 @@ struct WalReader {
   }
   bool read_ok = false;  // the last read_physical returned a record
   uint64_t last_hoff = 0;  // header offset of the last record read_physical returned
+  // the block walk's records (optional): their headers are prefetched ahead
+  const std::vector<mck_walk::PhysRec>* phys = nullptr;
+  size_t pcur = 0;
 };
 
 }  // namespace
@@ -266,9 +274,18 @@ namespace mck_walk {
 // log::Reader (checksum = true) reading the whole image: ReadRecord until it
 // returns false, over the device's verdicts (NULL = trust every CRC).
 int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recovery_mode,
-             const mck_wal_block_result* verified, WalWalk& W) {
+             const mck_wal_block_result* verified, WalWalk& W, const std::vector<PhysRec>* phys) {
   WalReader R{d, nbytes, log_number, recovery_mode, verified};
   R.records_so_far = &W.roff;
+  R.phys = phys;
+  if (phys) {  // about one record per physical record
+    W.fr.reserve(phys->size());
+    W.roff.reserve(phys->size());
+    W.rlen.reserve(phys->size());
+    W.rfile.reserve(phys->size());
+    W.rhoff.reserve(phys->size());
+    W.rfrag.reserve(phys->size() + 1);
+  }
   TsRecorder ts;
   std::vector<mck_wal_fragment>& fr = W.fr;
   std::vector<uint64_t>& roff = W.roff;
@@ -517,12 +534,13 @@ int check_read_args(const void* wal, uint64_t nbytes, int recovery_mode, const m
 // without the CRCs: a < 7-byte rest is the block trailer (at the end of the
 // file: a truncated header), a recyclable header needs 11 bytes, a record of
 // another log, a length past the block and a zero-length kZeroType stop it.
-void wal_block_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, std::vector<PhysRec>& phys,
-                    std::vector<BlockStop>& stops) {
-  const uint64_t nb = (nbytes + MCK_WAL_kBlockSize - 1) / MCK_WAL_kBlockSize;
-  stops.resize(nb);
-  phys.reserve(phys.size() + nb);
-  for (uint64_t b = 0; b < nb; b++) {
+namespace {
+// Blocks [b0, b1) of the walk into phys / stops[b0 .. b1) (stops[b].first
+// relative to this range's first record).
+void block_walk_range(const uint8_t* d, uint64_t nbytes, uint32_t log_number, uint64_t b0, uint64_t b1,
+                      std::vector<PhysRec>& phys, BlockStop* stops) {
+  phys.reserve(phys.size() + (b1 - b0));
+  for (uint64_t b = b0; b < b1; b++) {
     const uint64_t base = b * MCK_WAL_kBlockSize;
     const uint32_t size = (uint32_t)std::min<uint64_t>(MCK_WAL_kBlockSize, nbytes - base);
     const bool last = nbytes - base <= MCK_WAL_kBlockSize;
@@ -566,6 +584,41 @@ void wal_block_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, std:
     }
     st.count = (uint32_t)(phys.size() - st.first);
     st.pos = pos;
+  }
+}
+}  // namespace
+
+// k_wal_verify's per-block walk (mck_kernels.hpp wal_parse) on the host,
+// without the CRCs: a < 7-byte rest is the block trailer (at the end of the
+// file: a truncated header), a recyclable header needs 11 bytes, a record of
+// another log, a length past the block and a zero-length kZeroType stop it.
+// Blocks are independent: a large log is walked by several threads (each
+// header is a cache miss one hop after the last -- the walk is memory-latency
+// bound, not compute bound), their lists concatenated in file order.
+void wal_block_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, std::vector<PhysRec>& phys,
+                    std::vector<BlockStop>& stops) {
+  const uint64_t nb = (nbytes + MCK_WAL_kBlockSize - 1) / MCK_WAL_kBlockSize;
+  stops.resize(nb);
+  const uint64_t hw = std::max<unsigned>(1u, std::thread::hardware_concurrency());
+  const uint64_t T = std::min<uint64_t>(std::min<uint64_t>(hw, 16), nb / 256 + 1);
+  if (T <= 1) {
+    phys.clear();
+    block_walk_range(d, nbytes, log_number, 0, nb, phys, stops.data());
+    return;
+  }
+  std::vector<std::vector<PhysRec>> part(T);
+  std::vector<std::thread> th;
+  for (uint64_t t = 0; t < T; t++)
+    th.emplace_back([&, t] { block_walk_range(d, nbytes, log_number, nb * t / T, nb * (t + 1) / T, part[t], stops.data()); });
+  for (auto& x : th) x.join();
+  uint64_t total = 0;
+  for (const auto& p : part) total += p.size();
+  phys.clear();
+  phys.reserve(total);
+  for (uint64_t t = 0; t < T; t++) {
+    const uint64_t off = phys.size();
+    for (uint64_t b = nb * t / T; b < nb * (t + 1) / T; b++) stops[b].first += off;
+    phys.insert(phys.end(), part[t].begin(), part[t].end());
   }
 }
 

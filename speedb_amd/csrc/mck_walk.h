@@ -25,11 +25,6 @@ struct WalWalk {
   std::vector<mck_wal_fragment> stream;
 };
 
-// log::Reader (checksum = true) reading the whole image: ReadRecord until it
-// returns false, over the device's verdicts (NULL = trust every CRC).
-int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recovery_mode,
-             const mck_wal_block_result* verified, WalWalk& W);
-
 // Every physical record of every 32 KiB block, each block walked on its own
 // from offset 0 as ReadPhysicalRecord parses it (db/log_reader.cc:450-584;
 // k_wal_verify's walk): the records a reader can reach, whatever it drops.
@@ -48,6 +43,13 @@ struct BlockStop {  // where the block's walk stopped, and why (MCK_WAL_* status
 };
 void wal_block_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, std::vector<PhysRec>& phys,
                     std::vector<BlockStop>& stops);
+// log::Reader (checksum = true) reading the whole image: ReadRecord until it
+// returns false, over the device's verdicts (NULL = trust every CRC).
+// phys (optional): the block walk's records of the same image (their headers
+// are prefetched ahead of the walk).
+int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recovery_mode,
+             const mck_wal_block_result* verified, WalWalk& W, const std::vector<PhysRec>* phys = nullptr);
+
 // mck_wal_read_out (caller arrays, *_cap sizes) from a walk
 int wal_copy_out(const WalWalk& W, mck_wal_read_out* out);
 // argument checks of the read-out entry points (struct_size, mode)

@@ -183,7 +183,7 @@ extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64
   }
   const uint32_t np = (uint32_t)phys.size();
   WalWalk plan;
-  if (int rc = wal_walk(d, nbytes, log_number, recovery_mode, nullptr, plan)) {
+  if (int rc = wal_walk(d, nbytes, log_number, recovery_mode, nullptr, plan, &phys)) {
     delete R;
     return rc;
   }
@@ -247,7 +247,7 @@ extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64
     W = std::move(plan);
   } else {
     t0 = now_s();
-    rc = wal_walk(d, nbytes, log_number, recovery_mode, R->blocks.data(), W);
+    rc = wal_walk(d, nbytes, log_number, recovery_mode, R->blocks.data(), W, &phys);
     R->info.walk_seconds += now_s() - t0;
     R->info.host_walks = 2;
     if (rc) {
