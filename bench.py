@@ -149,6 +149,8 @@ def parse():
     p.add_argument("--span-min", type=int, default=100, help="smallest span (walrec, ragged)")
     p.add_argument("--span-max", type=int, default=1100, help="largest span (walrec, ragged)")
     p.add_argument("--span-bytes", type=int, default=1 << 30, help="span bytes per GPU (walrec, ragged)")
+    p.add_argument("--ragged-hash", choices=["crc32c", "xxh3"], default="crc32c",
+                   help="ragged: the checksum (xxh3: XXH3_64bits per span, mck_xxh3_64_batch)")
     p.add_argument("--host-blocks", type=int, default=2_500_000,
                    help="pinned 4300-B blocks per GPU (host; configs[4]'s 8-GPU share)")
     p.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -589,32 +591,42 @@ def make_workload(args, dev, rank, world):
         data = W.rand_bytes(int(offs[-1] + lens[-1]) + 64, dev, 801 + rank)
         sp = S.Spans(data, count, offsets=torch.from_numpy(offs).to(dev),
                      lengths=torch.from_numpy(lens.astype(np.int32)).to(dev))
-        out = torch.empty(count, dtype=torch.int32, device=dev)
+        x3 = args.workload == "ragged" and args.ragged_hash == "xxh3"
+        out = torch.empty(count, dtype=torch.int64 if x3 else torch.int32, device=dev)
         if args.workload == "walrec":
             types = torch.from_numpy(rng.choice([1, 2, 3, 4], size=count).astype(np.uint8)).to(dev)
             w.step = lambda: S.wal_record_crc_batch(sp, types, 7, out=out, stream=stream)
             w.kernel = _ragged("mck::OpCrcWal", float(lens.mean()))
             w.desc = (f"WAL record CRCs (EmitPhysicalRecord, db/log_writer.cc:263-311): {count} records of "
                       f"{args.span_min}-{args.span_max} B per GPU at any byte offset, mck_wal_record_crc_batch")
+        elif x3:
+            w.step = lambda: S.xxh3_64_batch(sp, out=out, stream=stream)
+            w.kernel = "mck::k_xxh3_wave<mck::OpX3Value>"
+            w.desc = (f"xxh3_64_batch over {count} ragged spans of {args.span_min}-{args.span_max} B per GPU "
+                      "(explicit offsets/lengths)")
         else:
             w.step = lambda: S.crc32c_batch(sp, out=out, stream=stream)
             w.kernel = _ragged("mck::OpCrcValueZ", float(lens.mean()))
             w.desc = (f"crc32c_batch over {count} ragged spans of {args.span_min}-{args.span_max} B per GPU "
                       "(explicit offsets/lengths)")
         w.span_bytes = int(lens.sum())
-        # span bytes + 8 B offset + 4 B length + 4 B out (+1 B type)
-        w.alg_bytes = int(lens.sum()) + count * (16 + (1 if args.workload == "walrec" else 0))
+        # span bytes + 8 B offset + 4 B length + 4 B out (8 B for XXH3) (+1 B type)
+        w.alg_bytes = int(lens.sum()) + count * (16 + (1 if args.workload == "walrec" else 0) + (4 if x3 else 0))
         w.cfg = {"spans_per_gpu": count, "span_min": args.span_min, "span_max": args.span_max}
+        if x3:
+            w.cfg["hash"] = "xxh3"
 
         def check():
             idx = np.random.default_rng(rank).choice(count, size=256, replace=False)
             hd = data.cpu().numpy()
-            res = out.cpu().numpy().view(np.uint32)
+            res = out.cpu().numpy().view(np.uint64 if x3 else np.uint32)
             tys = types.cpu().numpy() if args.workload == "walrec" else None
             ok = True
             for k in idx:
                 b = hd[offs[k]:offs[k] + lens[k]].tobytes()
-                if args.workload == "walrec":
+                if x3:
+                    want = S.XXH3_64bits(b)
+                elif args.workload == "walrec":
                     want = S.crc32c.Mask(S.crc32c.Extend(S.crc32c.Value(bytes([int(tys[k])])), b))
                 else:
                     want = S.crc32c.Value(b)

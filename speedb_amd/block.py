@@ -186,13 +186,15 @@ def VerifyBlockProtectionInfo(blocks: Spans, prot: BlockProtection, stored=None,
     mismatch_count int32[1]) laid out by ``prot.key_base`` -- the protect-time
     index, as the iterators index kv_checksum_ (block.h:623) -- and, with
     ``return_status``, the walk's per-block status (int32 [count] device; None
-    for the two-pass verify, which has none).
+    for protection built by the two-pass pair, which has no walk).
 
     A block that no longer walks (bad header, entry or restart array) or now
     holds another number of entries has ALL of its keys flagged -- the
     iterator's CorruptionError (block.h:559-565) -- and no other block's keys
     move.  A block the one-pass walk cannot park (kSlotOverflow) sends the
-    whole batch to the two-pass verify."""
+    batch's entries to the two-pass verify; the walk's layout verdicts still
+    flag whole blocks and come back as the status, so a block's verdict does
+    not depend on whether another block of the batch overflowed."""
     torch = _torch()
     dev = blocks.base.device
     stored = prot.kv_checksum if stored is None else stored
@@ -208,18 +210,31 @@ def VerifyBlockProtectionInfo(blocks: Spans, prot: BlockProtection, stored=None,
                                                    work.data_ptr(), stored.data_ptr(), mismatch.data_ptr(),
                                                    count.data_ptr(), _stream(stream)),
               "mck_block_kv_verify_blocks_batch")
-        if not bool((status[:n] == int(BlockStatus.kSlotOverflow)).any().item()):
+        overflow = status[:n] == int(BlockStatus.kSlotOverflow)
+        if not bool(overflow.any().item()):
             out = (mismatch[:prot.total_keys], count)
             return out + (status[:n],) if return_status else out
-        count.zero_()  # a block outgrew its slots: the two-pass verify decides the batch
+        # a block outgrew its slots: the two-pass verify decides the entries,
+        # and the walk's layout verdicts (which the two-pass verify, reading
+        # the protect-time restart array, cannot see) still flag whole blocks
+        walk_bad = (status[:n] != int(BlockStatus.kOk)) & ~overflow
+        count.zero_()
     work = _work(prot.total_keys, prot.total_key_bytes, dev)
     check(lib.mck_block_kv_verify_batch(int(prot.kind), ctypes.byref(s), prot.protection_bytes_per_key,
                                         prot.key_base.data_ptr(), prot.arena_base.data_ptr(),
                                         prot.restart_interval.data_ptr(), prot.total_keys,
                                         work.data_ptr(), stored.data_ptr(), mismatch.data_ptr(),
                                         count.data_ptr(), _stream(stream)), "mck_block_kv_verify_batch")
-    out = (mismatch[:prot.total_keys], count)
-    return out + (None,) if return_status else out
+    mm = mismatch[:prot.total_keys]
+    walk_status = None
+    if prot.slot_cap and prot.total_keys <= n * prot.slot_cap:  # the fallback: keep the walk's verdicts
+        walk_status = status[:n]
+        per_block = prot.key_base[1:n + 1] - prot.key_base[:n]
+        bad_keys = torch.repeat_interleave(walk_bad, per_block.to(torch.int64), output_size=prot.total_keys)
+        mm |= bad_keys.to(torch.uint8)
+        count.copy_(mm.sum(dtype=torch.int32).reshape(1))
+    out = (mm, count)
+    return out + (walk_status,) if return_status else out
 
 
 def PerKVChecksumStatus(prot: BlockProtection, mismatch, entry_offsets: Optional[list] = None,

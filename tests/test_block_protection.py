@@ -550,6 +550,48 @@ def test_block_protection_verify_corrupt_block_data(gpu, p):
 
 
 @pytest.mark.gpu
+def test_block_protection_verify_overflow_fallback_keeps_walk(gpu):
+    """a block that outgrows the one-pass slots at VERIFY time
+    sends the batch's entries to the two-pass verify.  A neighbour whose
+    restart point moved must still have all of its keys flagged and its
+    layout status returned -- the verdict of one block does not depend on
+    whether another block of the batch overflowed."""
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    rnd = random.Random(77)
+    blocks = [build_block(data_block(rnd, rnd.randrange(8, 30), 4, 0, 60), 4) for _ in range(40)]
+    grow, moved = 7, 21
+    base, offs, lens = _pack(torch, blocks, random.Random(3))
+    spans = speedb_amd.Spans(base, len(blocks), offs, lens)
+    prot = B.InitializeBlockProtectionInfoOnePass(DATA, spans, 8, slot_cap=32, arena_cap=512)
+    assert prot.status.cpu().tolist() == [OK] * len(blocks)
+    kb = prot.key_base.cpu().tolist()
+    bad = list(blocks)
+    bad[grow] = build_block(data_block(rnd, 90, 4, 0, 60), 4)  # 90 entries > slot_cap
+    b = bytearray(blocks[moved])
+    nr = struct.unpack("<I", b[-4:])[0]
+    assert nr > 1
+    ro = len(b) - 4 * (nr + 1)
+    r1 = struct.unpack("<I", b[ro + 4:ro + 8])[0]
+    b[ro + 4:ro + 8] = struct.pack("<I", r1 + 1)
+    bad[moved] = bytes(b)
+    base2, offs2, lens2 = _pack(torch, bad, random.Random(3))
+    spans2 = speedb_amd.Spans(base2, len(bad), offs2, lens2)
+    mism, cnt, st = B.VerifyBlockProtectionInfo(spans2, prot, return_status=True)
+    assert st is not None
+    sts = st.cpu().tolist()
+    assert sts[grow] == B.BlockStatus.kSlotOverflow
+    assert sts[moved] not in (OK, B.BlockStatus.kSlotOverflow)
+    flagged = set(torch.nonzero(mism).flatten().cpu().tolist())
+    assert set(range(kb[moved], kb[moved + 1])) <= flagged
+    assert flagged <= set(range(kb[moved], kb[moved + 1])) | set(range(kb[grow], kb[grow + 1]))
+    assert int(cnt.item()) == len(flagged)
+    msgs = dict(B.PerKVChecksumStatus(prot, mism, status=st))
+    assert moved in msgs and "per key-value" not in msgs[moved].message
+
+
+@pytest.mark.gpu
 def test_block_protection_empty_and_all_bad(gpu):
     import speedb_amd
     from speedb_amd import block as B
