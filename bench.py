@@ -1133,13 +1133,17 @@ def main():
             "kernel": w.kernel, "kernel_avg_ms": round(kern_ms, 4),
             "alg_bytes_per_launch": int(w.alg_bytes),
         }
-        tf = os.path.join(REPO, "profiles", f"traffic_{args.workload}.json")
-        if os.path.exists(tf):
+        # the tracked PMC traffic of this exact workload, config and kernel
+        # (profiles/traffic_*.json, one file per profiled shape)
+        import glob
+        for tf in sorted(glob.glob(os.path.join(REPO, "profiles", "traffic_*.json"))):
             with open(tf) as f:
                 tr = json.load(f)
-            if tr.get("config") == w.cfg and tr.get("kernel") == w.kernel:
+            if (tr.get("workload", args.workload) == args.workload and tr.get("config") == w.cfg
+                    and tr.get("kernel") == w.kernel):
                 roof["traffic"] = tr["hbm_bytes_per_launch"]
                 roof["traffic_source"] = os.path.relpath(tf, REPO)
+                break
     cpu = None
     if (rank == 0 and world == 1 and args.cpu_seconds > 0 and not args.no_verify
             and args.workload in ("crc32c", "xxh3")):

@@ -2,7 +2,7 @@
 """Turn a run_profile.sh output directory into the per-launch HBM traffic
 figure bench.py reports as roofline.traffic.
 
-  python profiles/pmc_to_traffic.py gpurun_out/prof_<tag> <workload>
+  python profiles/pmc_to_traffic.py gpurun_out/prof_<tag> <workload> [<shape name>]
 
 Reads the bench JSON line of the trace pass (kernel names + config), the
 kernel-trace stats (average duration of those kernels), and the FETCH_SIZE /
@@ -117,7 +117,10 @@ def main():
                   + "; separate --pmc passes with --kernel-trace only"
                   + ("; per full resident pass (dispatch_scale = mean dispatch / full pass)" if scale != 1.0 else ""),
     }
-    dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"traffic_{workload}.json")
+    # (argv[3]: the file's shape name when a workload has several profiled
+    # shapes -- bench.py matches a file by workload, config and kernel)
+    name = sys.argv[3] if len(sys.argv) > 3 else workload
+    dst = os.path.join(os.path.dirname(os.path.abspath(__file__)), f"traffic_{name}.json")
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
         f.write("\n")

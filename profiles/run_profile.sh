@@ -20,6 +20,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$out/pmc_write" 
 if [ "${PROFILE_SQ:-0}" = 1 ]; then
   timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY --kernel-trace -d "$out/pmc_sq" -o pmc --output-format csv -- python3 bench.py $args > "$out/bench_sq.txt" 2>&1
 fi
-python3 profiles/pmc_to_traffic.py "$out" "$wl" > "$out/traffic.json"
-cp profiles/traffic_${wl}.json "$out/" 2>/dev/null || true
+tn=${TRAFFIC_NAME:-$wl}
+python3 profiles/pmc_to_traffic.py "$out" "$wl" "$tn" > "$out/traffic.json"
+cp profiles/traffic_${tn}.json "$out/" 2>/dev/null || true
 echo "profile done: $out"

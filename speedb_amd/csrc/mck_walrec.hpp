@@ -359,9 +359,13 @@ __device__ __forceinline__ bool wr_step(const WrCtx& x, const WrRow& A, const Wr
   if (wave_any(xa)) h = wr_x3_round(A, LA, c, x.X, acc, xa, merge);
   if (wave_any(live && last)) {
     const uint32_t crc = wr_crc_finish(s, A, c);
-    if (live && last && c == 0) {
-      x.a.ok[A.i] = crc_mask(crc) == A.stored ? 1 : 0;
-      if (A.hash() == 2u) x.a.x3[A.i] = xxh3_short(reinterpret_cast<const uint8_t*>(A.P), A.len);
+    if (live && last && c == 0) x.a.ok[A.i] = crc_mask(crc) == A.stored ? 1 : 0;
+    // a record of <= 240 bytes: its XXH3 on the row, one window per lane
+    // (x3s_row_hash; the small classes on lane 0)
+    const bool sh = live && last && A.hash() == 2u;
+    if (wave_any(sh)) {
+      const uint64_t h2 = x3s_hash_row<false>(A.P, sh ? A.len : 0u, 0);  // (other rows: an empty span)
+      if (sh && c == 0) x.a.x3[A.i] = h2;
     }
     s = (live && last) ? 0u : s;
   }

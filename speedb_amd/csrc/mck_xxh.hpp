@@ -394,6 +394,171 @@ __device__ __forceinline__ X3Row x3_row(uint64_t seed) {
   return X;
 }
 
+// ---- short spans (n <= 240) on 16-lane rows (round 6) ---------------------
+// XXH3_64bits and XXPH3 for 17 <= n <= 240 (util/xxhash.h:4060-4130,
+// util/xxph3.h:1112-1147) are sums of independent mix16 terms -- a 16-byte
+// window of the input against a 16-byte secret window -- under one or two
+// avalanches.  Lane j of a row takes one window:
+//   n <= 128: m = ceil(n / 32) pairs; lanes j < m the front windows 16 j
+//     (secret 32 j), lanes 8 <= j < 8 + m the back windows n - 16 (j - 7)
+//     (secret 32 (j - 8) + 16); h = avalanche(n P1 + sum of all)
+//   n > 128: lanes j < 8 the windows 16 j (secret 16 j): S0; lanes
+//     8 <= j < n / 16 the windows 16 j (secret 16 (j - 8) + 3) and lane 15
+//     the last window n - 16 (secret 119): S1;
+//     h = avalanche(avalanche(n P1 + S0) + S1)
+// S0 and S1 sit in the two half-rows in both classes, so one 3-step half-row
+// sum and one row_ror 8 give both.  A row hashes a short span with one
+// coalesced 16-byte load per lane where one lane used to walk up to 15
+// windows alone while its wave waited.  n <= 16 (one or two loads, the
+// small classes): lane 0 of the row, as before.
+struct X3Short {
+  uint64_t a0, a1;  // lane j's secret words for n <= 128
+  uint64_t b0, b1;  // ... for n > 128
+};
+// (the short classes key mix16 with secret + seed / secret - seed,
+// util/xxph3.h:1644 -- not the custom secret of the long loop; seed 0 for XXH3)
+__device__ __forceinline__ X3Short x3s_keys(uint32_t j, uint64_t seed) {
+  const int sa = 32 * (int)(j & 3u) + (j < 8 ? 0 : 16);
+  const int sb = j < 8 ? 16 * (int)j : j < 15 ? 16 * (int)(j - 8) + 3 : 119;
+  X3Short K;
+  K.a0 = sec64(sa) + seed;
+  K.a1 = sec64(sa + 8) - seed;
+  K.b0 = sec64(sb) + seed;
+  K.b1 = sec64(sb + 8) - seed;
+  return K;
+}
+// lane j's window offset in a span of 17 <= n <= 240 bytes, and whether the
+// lane has one
+__device__ __forceinline__ uint32_t x3s_off(uint32_t n, uint32_t j, bool& has) {
+  if (n <= 128) {
+    has = (j & 7u) < ((n + 31) >> 5);
+    return j < 8 ? 16 * j : n - 16 * (j - 7);
+  }
+  has = j < 8 || j < (n >> 4) || j == 15;
+  return j == 15 ? n - 16 : 16 * j;
+}
+// the small classes (n <= 16) of XXH3 / XXPH3, one lane
+template <bool PREVIEW>
+__device__ __forceinline__ uint64_t x3_small(const uint8_t* in, uint64_t len, uint64_t seed) {
+  if constexpr (PREVIEW) {
+    if (len > 8) {
+      const uint64_t lo = rd64(in) ^ (sec64(0) + seed), hi = rd64(in + len - 8) ^ (sec64(8) - seed);
+      return xxph3_avalanche(len + (lo + hi) + mul128_fold64(lo, hi));
+    }
+    if (len >= 4) return xxph3_4to8(rd32(in), rd32(in + len - 4), len, seed);
+    if (len) return xxph3_1to3(in[0], in[len >> 1], in[len - 1], len, seed);
+    return mul128_fold64(seed + sec64(0), P64_2);
+  } else {
+    if (len > 8) {
+      const uint64_t bf1 = sec64(24) ^ sec64(32), bf2 = sec64(40) ^ sec64(48);
+      const uint64_t lo = rd64(in) ^ bf1, hi = rd64(in + len - 8) ^ bf2;
+      return xxh3_avalanche(len + __builtin_bswap64(lo) + hi + mul128_fold64(lo, hi));
+    }
+    if (len >= 4) {
+      const uint64_t in1 = rd32(in), in2 = rd32(in + len - 4);
+      const uint64_t bf = sec64(8) ^ sec64(16);
+      return xxh3_rrmxmx((in2 + (in1 << 32)) ^ bf, len);
+    }
+    if (len) {
+      const uint32_t c1 = in[0], c2 = in[len >> 1], c3 = in[len - 1];
+      const uint32_t comb = (c1 << 16) | (c2 << 24) | c3 | ((uint32_t)len << 8);
+      return xxh64_avalanche((uint64_t)comb ^ (uint64_t)(sec32(0) ^ sec32(4)));
+    }
+    return xxh64_avalanche(sec64(56) ^ sec64(64));
+  }
+}
+// The row's hash of a 17..240-byte span from lane j's window d (has: the
+// lane holds one); valid in lanes 0-7 of the row.  Every lane of the row
+// must be active (DPP).
+template <bool PREVIEW>
+__device__ __forceinline__ uint64_t x3s_row_hash(uint32_t n, const uint4& d, bool has, const X3Short& K) {
+  const bool mid = n <= 128;
+  const uint64_t lo = ((uint64_t)d.y << 32) | d.x, hi = ((uint64_t)d.w << 32) | d.z;
+  const uint64_t v = has ? mul128_fold64(lo ^ (mid ? K.a0 : K.b0), hi ^ (mid ? K.a1 : K.b1)) : 0ull;
+  uint64_t t = quad_sum(v);
+  t += dpp64<0x141>(t);                      // half mirror: the half-row's sum
+  const uint64_t u = dpp64<0x128>(t);        // row_ror 8: the other half's
+  const uint64_t a = (uint64_t)n * P64_1 + t;
+  if constexpr (PREVIEW) return mid ? xxph3_avalanche(a + u) : xxph3_avalanche(xxph3_avalanche(a) + u);
+  else return mid ? xxh3_avalanche(a + u) : xxh3_avalanche(xxh3_avalanche(a) + u);
+}
+
+// A row's span of n <= 240 bytes at ptr, called by the row's 16 lanes
+// together: its hash in lane 0 (out of line: the row loops that meet an
+// occasional short span keep their registers -- inlined, per-KV protection's
+// verify kernel went from 128 to 144 VGPRs)
+template <bool PREVIEW>
+__device__ __noinline__ uint64_t x3s_hash_row(uint64_t ptr, uint64_t n, uint64_t seed) {
+  const uint32_t j = threadIdx.x & 15u;
+  bool has;
+  const uint32_t o = x3s_off((uint32_t)n, j, has);
+  has = has && n > 16;
+  const uint4 d = gload16u(has ? ptr + o : ptr & ~15ull);
+  const uint64_t h = x3s_row_hash<PREVIEW>((uint32_t)n, d, has, x3s_keys(j, seed));
+  return n <= 16 && j == 0 ? x3_small<PREVIEW>(reinterpret_cast<const uint8_t*>(ptr), n, seed) : h;
+}
+
+// Every short span (n <= 240) among slots t0, t0 + rows, ... < n of a row,
+// U spans per row in flight, the next group's descriptors loaded while the
+// current one is hashed.  slot(t, &len, &off) -> span index.  Lane u of the
+// row finishes span u of a group (U <= 8).  Wave-uniform: every lane calls
+// it with the same n and rows.
+// (kl: the 16 lanes' keys in LDS, read where they are used -- the caller's
+// row-loop constants stay live across this pass; nullptr: in registers)
+template <class Op, bool PREVIEW, int U, class Slot>
+__device__ __forceinline__ void x3_short_rows(const Op& op, uint32_t t0, uint32_t n, uint32_t rows, uint64_t seed,
+                                              Slot&& slot, const X3Short* kl = nullptr) {
+  static_assert(U <= 8, "lanes 0-7 hold the hashes");
+  if (n == 0) return;
+  const uint32_t j = threadIdx.x & 15u;
+  const X3Short Kr = kl ? X3Short{} : x3s_keys(j, seed);
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  uint32_t len[U], idx[U];
+  uint64_t off[U];
+  auto fetch = [&](uint32_t t) {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t tt = t + rows * (uint32_t)u;
+      idx[u] = slot(tt < n ? tt : n - 1, len[u], off[u]);
+      len[u] = tt < n ? len[u] : 0xFFFFFFFFu;  // past the slots: not short
+    }
+  };
+  fetch(t0);
+  for (uint32_t t = t0; __any(t < n); t += rows * U) {
+    bool sh[U], has[U];
+    uint4 d[U];
+    uint32_t ln[U], ix[U];
+    uint64_t ptr[U];
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      ln[u] = len[u];
+      ix[u] = idx[u];
+      ptr[u] = base + off[u];
+      sh[u] = ln[u] <= 240u;
+      any |= sh[u];
+    }
+    if (__any(any)) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const uint32_t o = x3s_off(ln[u], j, has[u]);
+        has[u] = has[u] && sh[u] && ln[u] > 16u;
+        d[u] = gload16u(has[u] ? ptr[u] + o : ptr[u] & ~15ull);  // (idle: the span's 16-byte line)
+      }
+    }
+    fetch(t + rows * U);  // (past n: clamped slots, flagged not short)
+    if (__any(any)) {
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        uint64_t h = x3s_row_hash<PREVIEW>(ln[u], d[u], has[u], kl ? kl[j] : Kr);
+        if (sh[u] && ln[u] <= 16u && j == (uint32_t)u)
+          h = x3_small<PREVIEW>(reinterpret_cast<const uint8_t*>(ptr[u]), ln[u], seed);
+        if (sh[u] && j == (uint32_t)u) op.finish(ix[u], h);
+      }
+    }
+  }
+}
+
 // One row's span in progress.
 struct X3Span {
   uint64_t ptr, len;
@@ -407,6 +572,20 @@ struct X3Span {
   uint64_t pl = 0, po = 0;
   uint32_t pi = ~0u;
 };
+
+// A row's long span (n > 240) from its start.
+template <bool PREVIEW>
+__device__ __forceinline__ void x3_span_start(X3Span& rs, uint64_t ptr, uint64_t len, uint32_t i) {
+  rs.ptr = ptr;
+  rs.len = len;
+  // XXH3 util/xxhash.h:5141-5171; XXPH3 util/xxph3.h:1516-1543
+  const uint64_t body = PREVIEW ? len : len - 1;
+  rs.nb = (uint32_t)(body / 1024);
+  rs.nst = (uint32_t)((body - 1024ull * rs.nb) / 64);
+  rs.tail = PREVIEW ? (len & 63) != 0 : true;
+  rs.g = 0;
+  rs.i = i;
+}
 
 // Advance the row to its next long span (hashing short ones -- n <= 240 --
 // on the row's first lane on the way).  Op: base(), off(i), hlen(i),
@@ -432,20 +611,19 @@ __device__ __forceinline__ bool x3_next_long(const Op& op, uint32_t i, uint32_t 
         rs.pl = op.hlen(pj);
         rs.po = op.off(pj);
       }
-      rs.ptr = ptr;
-      rs.len = len;
-      // XXH3 util/xxhash.h:5141-5171; XXPH3 util/xxph3.h:1516-1543
-      const uint64_t body = PREVIEW ? len : len - 1;
-      rs.nb = (uint32_t)(body / 1024);
-      rs.nst = (uint32_t)((body - 1024ull * rs.nb) / 64);
-      rs.tail = PREVIEW ? (len & 63) != 0 : true;
-      rs.g = 0;
-      rs.i = i;
+      x3_span_start<PREVIEW>(rs, ptr, len, i);
       return true;
     }
-    if (!SKIP_SHORT && X.j == 0) {
-      const uint8_t* p = reinterpret_cast<const uint8_t*>(ptr);
-      op.finish(i, PREVIEW ? xxph3_short(p, len, X.seed) : xxh3_short(p, len));
+    if constexpr (!SKIP_SHORT) {
+      if constexpr (PREVIEW) {
+        // XXPH3 (k_xph3): lane 0 of the row -- short values are rare there,
+        // and the row call cost per-KV protection's verify kernel its fourth
+        // wave per SIMD (128 -> 130 VGPRs)
+        if (X.j == 0) op.finish(i, xxph3_short(reinterpret_cast<const uint8_t*>(ptr), len, X.seed));
+      } else {  // the whole row: one window per lane
+        const uint64_t h = x3s_hash_row<false>(ptr, len, 0);
+        if (X.j == 0) op.finish(i, h);
+      }
     }
   }
   return false;
@@ -885,6 +1063,8 @@ struct X3Lds {
   uint32_t done[kX3DescCache];     // pieces of span t chained so far
   uint32_t wsum[kX3MaxWaves];
   uint32_t ctr;
+  uint32_t lists[2][4];  // rows share, by window parity: short count, long count, long ticket
+  X3Short skeys[16];     // rows share: x3_short_rows' keys of row lane j
   ulonglong2 acc[kX3DescCache][4];                       // span t's accumulators, pair q
   ulonglong2 csum[kX3MaxWaves][4 * kX3PieceRounds][4];  // a wave's parked C_g, pair q
 };
@@ -994,7 +1174,10 @@ __device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, c
 // wave units win (2000-4000 B 0.636 vs 0.590, SST-sized 4 KiB + jitter
 // 0.733 vs 0.628; microbench/x3_width.py, profiles/r5/x3_width/).  Chosen
 // per workgroup from a sample of its share's lengths, as crc_share_long.
-constexpr uint32_t kX3RowsMin = 256, kX3RowsMax = 2560;  // mean span bytes
+// (round 6: no lower bound -- below 256 B the wave units padded every
+// 241-600-byte span to a 4 KiB round: ragged 100-300 B ran at 0.136; the
+// rows share hashes the short spans on rows, x3_short_rows)
+constexpr uint32_t kX3RowsMin = 0, kX3RowsMax = 2560;  // mean span bytes
 template <class Op>
 __device__ __forceinline__ bool x3_share_rows(const Op& op, uint32_t lo, uint32_t hi) {
   const uint32_t n = hi - lo, lane = threadIdx.x & 63;
@@ -1003,6 +1186,82 @@ __device__ __forceinline__ bool x3_share_rows(const Op& op, uint32_t lo, uint32_
   if (lane < m) len = op.hlen(lo + (uint32_t)((uint64_t)lane * n / m));
   for (int d = 32; d >= 1; d >>= 1) len += __shfl_xor(len, d, 64);
   return m != 0 && len >= (uint64_t)kX3RowsMin * m && len < (uint64_t)kX3RowsMax * m;
+}
+
+// The rows share (spans averaging < 2.5 KiB, round 6): windows of
+// blockDim spans, staged in LDS and split into a short list (<= 240 B,
+// hashed first by x3_short_rows, four per row in flight) and a long list the
+// rows draw from by LDS ticket -- balanced inside the workgroup, where the
+// static row stride left a row that drew short or small spans idle.  Each
+// thread loads the next window's descriptor while the current window runs.
+// (Round 6 first ran the short spans as a separate pass over the share's
+// global descriptors: ragged 241-600 B fell from 0.363 to 0.316, every
+// slot costing the rows a dependent descriptor load.)
+template <class Op, bool PREVIEW>
+__device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t lo, uint32_t hi, const X3Row& X,
+                                              uint64_t seed) {
+  const uint32_t n = hi - lo, W = blockDim.x, t = threadIdx.x;
+  const uint32_t rows = W >> 4, row = t >> 4, j = t & 15u;
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  uint32_t nlen = 0;
+  uint64_t noff = 0;
+  if (t < n) {
+    nlen = (uint32_t)op.hlen(lo + t);
+    noff = op.off(lo + t);
+  }
+  if (t < 8) (&s.lists[0][0])[t] = 0;
+  if (t < 16) s.skeys[t] = x3s_keys(t, seed);
+  uint32_t par = 0;
+  for (uint32_t w0 = 0; w0 < n; w0 += W, par ^= 1u) {
+    const uint32_t wn = n - w0 < W ? n - w0 : W;
+    uint32_t* L = &s.lists[par][0];
+    __syncthreads();  // (the previous window's rows are done with its lists; the counters are zero)
+    s.off[t] = noff;
+    s.len[t] = nlen;
+    const bool in = t < wn, sh = in && nlen <= 240u, lg = in && nlen > 240u;
+    const uint64_t ms = __ballot(sh), ml = __ballot(lg);
+    const uint32_t lane = t & 63u;
+    uint32_t bs = 0, bl = 0;
+    if (lane == 0) {
+      if (ms) bs = atomicAdd(&L[0], (uint32_t)__popcll(ms));
+      if (ml) bl = atomicAdd(&L[1], (uint32_t)__popcll(ml));
+    }
+    bs = __shfl(bs, 0, 64);
+    bl = __shfl(bl, 0, 64);
+    const uint64_t below = (1ull << lane) - 1;
+    if (sh) s.pre[bs + (uint32_t)__popcll(ms & below)] = t;
+    if (lg) s.done[bl + (uint32_t)__popcll(ml & below)] = t;
+    if (t < 4) s.lists[par ^ 1u][t] = 0;  // the next window's counters
+    __syncthreads();
+    // the next window's descriptors, in flight while this one runs
+    {
+      const uint32_t k = w0 + W + t;
+      if (k < n) {
+        nlen = (uint32_t)op.hlen(lo + k);
+        noff = op.off(lo + k);
+      }
+    }
+    const uint32_t wb = lo + w0, nshort = L[0], nlong = L[1];
+    x3_short_rows<Op, PREVIEW, 4>(op, row, nshort, rows, seed, [&](uint32_t q, uint32_t& len, uint64_t& off) {
+      const uint32_t k = s.pre[q];
+      len = s.len[k];
+      off = s.off[k];
+      return wb + k;
+    }, s.skeys);
+    auto next = [&](X3Span& r) {
+      uint32_t tk = 0;
+      if (j == 0) tk = atomicAdd(&L[2], 1u);
+      tk = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((t & 0x30u) << 2), (int)tk);
+      if (tk >= nlong) return false;
+      const uint32_t k = s.done[tk];
+      x3_span_start<PREVIEW>(r, base + s.off[k], s.len[k], wb + k);
+      return true;
+    };
+    // idle rows keep loading from a valid address: the batch's base
+    X3Span rs{base, 0, 0, 0, 0, 0, false};
+    const bool act = next(rs);
+    xxh3_rows_loop<Op, PREVIEW>(op, X, rs, act, next);
+  }
 }
 
 // Workgroup b's share: a byte-balanced contiguous range (share_by_bytes),
@@ -1020,21 +1279,7 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
                  [&](uint32_t i) { return (uint32_t)op.off(i) ^ (uint32_t)op.hlen(i); },
                  [&] { X = x3_row(seed); });
   if (x3_share_rows(op, lo, hi)) {  // workgroup-uniform
-    const uint64_t base = reinterpret_cast<uint64_t>(op.base());
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {  // short spans, one per lane
-      const uint64_t len = op.hlen(i);
-      if (len <= 240) {
-        const uint8_t* p = reinterpret_cast<const uint8_t*>(base + op.off(i));
-        op.finish(i, PREVIEW ? xxph3_short(p, len, seed) : xxh3_short(p, len));
-      }
-    }
-    const uint32_t rows = wpb * 4, row = wid * 4 + (uint32_t)X.row;
-    // idle rows keep loading from a valid address: the batch's base
-    X3Span rs{base, 0, 0, 0, 0, 0, false};
-    const bool act = x3_next_long<Op, PREVIEW, true>(op, lo + row, hi, rows, X, rs);
-    xxh3_rows_loop<Op, PREVIEW>(op, X, rs, act, [&](X3Span& r) {
-      return x3_next_long<Op, PREVIEW, true>(op, r.i + rows, hi, rows, X, r);
-    });
+    x3_rows_share<Op, PREVIEW>(op, s, lo, hi, X, seed);
     return;
   }
   const uint32_t start = lo, stride = 1, n = hi - lo;
@@ -1075,7 +1320,7 @@ __device__ __forceinline__ void xxh3_wave_driver(const Op& op, uint32_t count, u
     if (threadIdx.x == 0) s.pre[wn] = carry;
     __syncthreads();
     // short spans (<= 240 bytes: the three small-input classes) first, one
-    // per lane -- outside the pipelined loop
+    // per lane -- outside the pipelined loop (spans of KiBs: few are short)
     const uint64_t base = reinterpret_cast<uint64_t>(op.base());
     for (uint32_t t = threadIdx.x; t < wn; t += blockDim.x) {
       const uint64_t len = s.len[t];
