@@ -864,10 +864,28 @@ def make_workload(args, dev, rank, world):
             return {"value": round(n * block / (ms * 1e-3) / 2**30, 2), "unit": "GiB/s",
                     "blocks": n, "kernel_ms": round(ms, 4), "agrees_with_host_path": ok}
 
+        def h2d_only():
+            # the PCIe leg alone: the same pinned bytes copied H2D in the
+            # pipeline's 256 MiB chunks, two device buffers alternating
+            chunk = 256 << 20
+            bufs = [torch.empty(chunk, dtype=torch.uint8, device=dev) for _ in range(2)]
+            tot = count * block
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            for k, o in enumerate(range(0, tot, chunk)):
+                n = min(chunk, tot - o)
+                bufs[k & 1][:n].copy_(hbuf[o:o + n], non_blocking=True)
+            torch.cuda.synchronize(dev)
+            dt = time.perf_counter() - t0
+            del bufs
+            return {"GBps": round(tot / dt / 1e9, 2), "GiBps": round(tot / dt / 2**30, 2), "seconds": round(dt, 4)}
+
         def check():
             # host-pipeline results == the device-resident kernel's on the
-            # same blocks (all of the 4 GiB slice), and its rate
+            # same blocks (all of the 4 GiB slice), and its rate; the H2D
+            # copy alone for the overlap figure
             w.device_only = device_only()
+            w.h2d_only = h2d_only()
             return w.device_only["agrees_with_host_path"]
         w.check = check
     return w
@@ -1168,6 +1186,15 @@ def main():
         }
         if getattr(w, "device_only", None):
             line["device_only"] = w.device_only
+        if getattr(w, "h2d_only", None) and args.host_ndev <= 0:
+            # overlap: the share of the shorter leg (copy or kernel) hidden
+            # under the other in the copy-inclusive step
+            t_step = wall / args.steps
+            t_h2d = w.h2d_only["seconds"]
+            t_kern = w.span_bytes / (w.device_only["value"] * 2**30)
+            hidden = (t_h2d + t_kern - t_step) / min(t_h2d, t_kern)
+            line["h2d_only"] = dict(w.h2d_only, overlap_fraction=round(max(0.0, min(1.0, hidden)), 3),
+                                    kernel_seconds_at_device_rate=round(t_kern, 4))
         if getattr(w, "end_to_end", None):
             line["end_to_end"] = w.end_to_end
         print(json.dumps(line))

@@ -12,5 +12,5 @@ csrc = os.path.join(REPO, "speedb_amd", "csrc")
 subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-fPIC", "-shared",
                        "-Wall", "-Wno-unused-function"] + ["-D" + d for d in defs] +
                       ["-o", out] + [os.path.join(csrc, f) for f in
-                                     ("mck_engine.hip", "mck_sst.cc", "mck_blob.cc", "mck_wal.cc")])
+                                     ("mck_engine.hip", "mck_sst.cc", "mck_blob.cc", "mck_wal.cc", "mck_walrec.cc")])
 print(out)

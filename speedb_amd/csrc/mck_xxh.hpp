@@ -427,6 +427,19 @@ __device__ __forceinline__ X3Short x3s_keys(uint32_t j, uint64_t seed) {
   K.b1 = sec64(sb + 8) - seed;
   return K;
 }
+// The 16 bytes at any byte address from dword-aligned loads (a 16-byte
+// load at a byte-misaligned address runs far below rate): the dwords at
+// a & ~3 and the next one, funnel-shifted.  Reads at most 3 bytes past
+// a + 16, inside the dword holding byte a + 15 (s = 0: the last dword of the
+// window again).
+__device__ __forceinline__ uint4 load16_realign(uint64_t a) {
+  const uint64_t a4 = a & ~3ull;
+  const uint32_t s = (uint32_t)a & 3u;
+  const uint4 u = span_load16<false>(a4);
+  const uint32_t e = gload4(a4 + (s ? 16u : 12u));
+  return make_uint4(__builtin_amdgcn_alignbyte(u.y, u.x, s), __builtin_amdgcn_alignbyte(u.z, u.y, s),
+                    __builtin_amdgcn_alignbyte(u.w, u.z, s), __builtin_amdgcn_alignbyte(e, u.w, s));
+}
 // lane j's window offset in a span of 17 <= n <= 240 bytes, and whether the
 // lane has one
 __device__ __forceinline__ uint32_t x3s_off(uint32_t n, uint32_t j, bool& has) {
@@ -493,7 +506,7 @@ __device__ __noinline__ uint64_t x3s_hash_row(uint64_t ptr, uint64_t n, uint64_t
   bool has;
   const uint32_t o = x3s_off((uint32_t)n, j, has);
   has = has && n > 16;
-  const uint4 d = gload16u(has ? ptr + o : ptr & ~15ull);
+  const uint4 d = load16_realign(has ? ptr + o : ptr & ~15ull);
   const uint64_t h = x3s_row_hash<PREVIEW>((uint32_t)n, d, has, x3s_keys(j, seed));
   return n <= 16 && j == 0 ? x3_small<PREVIEW>(reinterpret_cast<const uint8_t*>(ptr), n, seed) : h;
 }
@@ -543,7 +556,7 @@ __device__ __forceinline__ void x3_short_rows(const Op& op, uint32_t t0, uint32_
       for (int u = 0; u < U; u++) {
         const uint32_t o = x3s_off(ln[u], j, has[u]);
         has[u] = has[u] && sh[u] && ln[u] > 16u;
-        d[u] = gload16u(has[u] ? ptr[u] + o : ptr[u] & ~15ull);  // (idle: the span's 16-byte line)
+        d[u] = load16_realign(has[u] ? ptr[u] + o : ptr[u] & ~15ull);  // (idle: the span's 16-byte line)
       }
     }
     fetch(t + rows * U);  // (past n: clamped slots, flagged not short)
@@ -1174,10 +1187,12 @@ __device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, c
 // wave units win (2000-4000 B 0.636 vs 0.590, SST-sized 4 KiB + jitter
 // 0.733 vs 0.628; microbench/x3_width.py, profiles/r5/x3_width/).  Chosen
 // per workgroup from a sample of its share's lengths, as crc_share_long.
-// (round 6: no lower bound -- below 256 B the wave units padded every
-// 241-600-byte span to a 4 KiB round: ragged 100-300 B ran at 0.136; the
-// rows share hashes the short spans on rows, x3_short_rows)
-constexpr uint32_t kX3RowsMin = 0, kX3RowsMax = 2560;  // mean span bytes
+// (round 6: from a 160-byte mean -- below 256 B the wave units padded every
+// 241-600-byte span to a 4 KiB round: ragged 100-300 B ran at 0.136, 0.264
+// in the rows share, x3_rows_share; shares of mostly <= 240-byte spans stay
+// on the wave units' one-span-per-lane short loop: 16-240 B 0.243 there,
+// 0.228 in the rows share; profiles/r6/x3short/)
+constexpr uint32_t kX3RowsMin = 160, kX3RowsMax = 2560;  // mean span bytes
 template <class Op>
 __device__ __forceinline__ bool x3_share_rows(const Op& op, uint32_t lo, uint32_t hi) {
   const uint32_t n = hi - lo, lane = threadIdx.x & 63;
@@ -1188,6 +1203,9 @@ __device__ __forceinline__ bool x3_share_rows(const Op& op, uint32_t lo, uint32_
   return m != 0 && len >= (uint64_t)kX3RowsMin * m && len < (uint64_t)kX3RowsMax * m;
 }
 
+#ifndef X3S_U
+#define X3S_U 2
+#endif
 // The rows share (spans averaging < 2.5 KiB, round 6): windows of
 // blockDim spans, staged in LDS and split into a short list (<= 240 B,
 // hashed first by x3_short_rows, four per row in flight) and a long list the
@@ -1242,7 +1260,7 @@ __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t l
       }
     }
     const uint32_t wb = lo + w0, nshort = L[0], nlong = L[1];
-    x3_short_rows<Op, PREVIEW, 4>(op, row, nshort, rows, seed, [&](uint32_t q, uint32_t& len, uint64_t& off) {
+    x3_short_rows<Op, PREVIEW, X3S_U>(op, row, nshort, rows, seed, [&](uint32_t q, uint32_t& len, uint64_t& off) {
       const uint32_t k = s.pre[q];
       len = s.len[k];
       off = s.off[k];
@@ -1260,6 +1278,10 @@ __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t l
     // idle rows keep loading from a valid address: the batch's base
     X3Span rs{base, 0, 0, 0, 0, 0, false};
     const bool act = next(rs);
+    // (round 6 measured the row loop's constants re-read from LDS after the
+    // short pass, so that more short spans per row fit in flight: slower at
+    // every shape, and 4 or 8 spans per row slower than 2 -- 16-240 B 0.240
+    // with 2, 0.203 with 4, 0.097 with 8)
     xxh3_rows_loop<Op, PREVIEW>(op, X, rs, act, next);
   }
 }
