@@ -1206,6 +1206,9 @@ __device__ __forceinline__ bool x3_share_rows(const Op& op, uint32_t lo, uint32_
 #ifndef X3S_U
 #define X3S_U 2
 #endif
+#ifndef X3S_WIN
+#define X3S_WIN 1024
+#endif
 // The rows share (spans averaging < 2.5 KiB, round 6): windows of
 // blockDim spans, staged in LDS and split into a short list (<= 240 B,
 // hashed first by x3_short_rows, four per row in flight) and a long list the
@@ -1215,15 +1218,31 @@ __device__ __forceinline__ bool x3_share_rows(const Op& op, uint32_t lo, uint32_
 // (Round 6 first ran the short spans as a separate pass over the share's
 // global descriptors: ragged 241-600 B fell from 0.363 to 0.316, every
 // slot costing the rows a dependent descriptor load.)
+// The rows share's hashes park in LDS (slot of the window) and thread t
+// finishes window slot t after both passes: one coalesced output write per
+// window instead of an 8-byte store per span from whichever row finished it
+// (XXH3 100-300 B: WRITE_SIZE 0.215 x the algorithmic bytes, six times the
+// 8-byte outputs, before).
+template <class Op>
+struct X3ParkOp {
+  const Op& op;
+  uint64_t* hv;
+  uint32_t wb;
+  __device__ const uint8_t* base() const { return op.base(); }
+  __device__ uint64_t off(uint32_t i) const { return op.off(i); }
+  __device__ uint64_t hlen(uint32_t i) const { return op.hlen(i); }
+  __device__ void finish(uint32_t i, uint64_t h) const { hv[i - wb] = h; }
+};
 template <class Op, bool PREVIEW>
 __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t lo, uint32_t hi, const X3Row& X,
                                               uint64_t seed) {
-  const uint32_t n = hi - lo, W = blockDim.x, t = threadIdx.x;
-  const uint32_t rows = W >> 4, row = t >> 4, j = t & 15u;
+  // window W spans (<= blockDim.x; threads t >= W stage nothing)
+  const uint32_t n = hi - lo, W = X3S_WIN < blockDim.x ? X3S_WIN : blockDim.x, t = threadIdx.x;
+  const uint32_t rows = blockDim.x >> 4, row = t >> 4, j = t & 15u;
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   uint32_t nlen = 0;
   uint64_t noff = 0;
-  if (t < n) {
+  if (t < W && t < n) {
     nlen = (uint32_t)op.hlen(lo + t);
     noff = op.off(lo + t);
   }
@@ -1234,8 +1253,10 @@ __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t l
     const uint32_t wn = n - w0 < W ? n - w0 : W;
     uint32_t* L = &s.lists[par][0];
     __syncthreads();  // (the previous window's rows are done with its lists; the counters are zero)
-    s.off[t] = noff;
-    s.len[t] = nlen;
+    if (t < W) {
+      s.off[t] = noff;
+      s.len[t] = nlen;
+    }
     const bool in = t < wn, sh = in && nlen <= 240u, lg = in && nlen > 240u;
     const uint64_t ms = __ballot(sh), ml = __ballot(lg);
     const uint32_t lane = t & 63u;
@@ -1254,13 +1275,15 @@ __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t l
     // the next window's descriptors, in flight while this one runs
     {
       const uint32_t k = w0 + W + t;
-      if (k < n) {
+      if (t < W && k < n) {
         nlen = (uint32_t)op.hlen(lo + k);
         noff = op.off(lo + k);
       }
     }
     const uint32_t wb = lo + w0, nshort = L[0], nlong = L[1];
-    x3_short_rows<Op, PREVIEW, X3S_U>(op, row, nshort, rows, seed, [&](uint32_t q, uint32_t& len, uint64_t& off) {
+    uint64_t* hv = reinterpret_cast<uint64_t*>(&s.acc[0][0]);  // (the piece path's accumulators, unused here)
+    const X3ParkOp<Op> pop{op, hv, wb};
+    x3_short_rows<X3ParkOp<Op>, PREVIEW, X3S_U>(pop, row, nshort, rows, seed, [&](uint32_t q, uint32_t& len, uint64_t& off) {
       const uint32_t k = s.pre[q];
       len = s.len[k];
       off = s.off[k];
@@ -1282,7 +1305,9 @@ __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t l
     // short pass, so that more short spans per row fit in flight: slower at
     // every shape, and 4 or 8 spans per row slower than 2 -- 16-240 B 0.240
     // with 2, 0.203 with 4, 0.097 with 8)
-    xxh3_rows_loop<Op, PREVIEW>(op, X, rs, act, next);
+    xxh3_rows_loop<X3ParkOp<Op>, PREVIEW>(pop, X, rs, act, next);
+    __syncthreads();
+    if (t < wn) op.finish(wb + t, hv[t]);
   }
 }
 
