@@ -1017,6 +1017,13 @@ int mck_test_set_crc_driver(int driver, int interleaved);
  * uniform batches, a wave per span for ragged ones), 1 = a wave per span,
  * 2 = 16-lane rows.  Production code never calls it. */
 int mck_test_set_xxh3_driver(int driver);
+/* Test hook (host only): mck_wal_recover's plan walk from the block walk's
+ * list (wal_walk_fast) against the reader's walk over the image, both with
+ * every CRC trusted.  1 = the list walk ran and every output (fragments,
+ * records, offsets, reports, end offset) equals the reader's; 0 = it
+ * declined (the reader's walk is then the plan); -1 = they differ.
+ * Production code never calls it. */
+int mck_test_wal_walk_fast(const void* wal, uint64_t nbytes, uint32_t log_number);
 
 #ifdef __cplusplus
 }

@@ -50,6 +50,14 @@ void wal_block_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, std:
 int wal_walk(const uint8_t* d, uint64_t nbytes, uint32_t log_number, int recovery_mode,
              const mck_wal_block_result* verified, WalWalk& W, const std::vector<PhysRec>* phys = nullptr);
 
+// The same walk (verified = NULL) from the block walk's list alone, without
+// reading the image again, when the log holds nothing the list does not
+// describe: every block walked to its end (MCK_WAL_OK), only the full /
+// first / middle / last types in a well-formed order.  Returns false (W
+// untouched) otherwise; the caller then runs wal_walk.
+bool wal_walk_fast(uint64_t nbytes, const std::vector<PhysRec>& phys, const std::vector<BlockStop>& stops,
+                   WalWalk& W);
+
 // mck_wal_read_out (caller arrays, *_cap sizes) from a walk
 int wal_copy_out(const WalWalk& W, mck_wal_read_out* out);
 // argument checks of the read-out entry points (struct_size, mode)

@@ -6,7 +6,9 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <new>
+#include <thread>
 #include <vector>
 
 #include "../../include/speedb_amd/mck.h"
@@ -183,17 +185,41 @@ extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64
   }
   const uint32_t np = (uint32_t)phys.size();
   WalWalk plan;
-  if (int rc = wal_walk(d, nbytes, log_number, recovery_mode, nullptr, plan, &phys)) {
-    delete R;
-    return rc;
+  if (!wal_walk_fast(nbytes, phys, stops, plan)) {  // (the list walk declines: the reader's walk)
+    if (int rc = wal_walk(d, nbytes, log_number, recovery_mode, nullptr, plan, &phys)) {
+      delete R;
+      return rc;
+    }
   }
-  std::vector<mck_wal_rec_desc> desc(np);
-  for (uint32_t i = 0; i < np; i++) {
-    const PhysRec& p = phys[i];
-    const uint64_t po = p.hoff + p.hsize;
-    const bool full = p.type == 1 || p.type == 5;
-    desc[i] = mck_wal_rec_desc{(uint32_t)po, (uint32_t)(po >> 32) | ((uint32_t)p.type << 16) | (full ? MCK_WAL_REC_HASH : 0u),
-                               p.length, p.stored};
+  // the device plan, one descriptor per physical record (ranges over
+  // threads: the array's first-touch page faults dominate its build)
+  std::unique_ptr<mck_wal_rec_desc[]> desc(new (std::nothrow) mck_wal_rec_desc[np ? np : 1]);  // (no zeroing pass)
+  if (!desc) {
+    delete R;
+    mck_internal_set_error("out of memory");
+    return MCK_ENOMEM;
+  }
+  {
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const uint32_t T = std::min<uint32_t>(std::min<uint32_t>(hw, 16), np / 65536 + 1);
+    auto fill = [&](uint32_t lo, uint32_t hi) {
+      for (uint32_t i = lo; i < hi; i++) {
+        const PhysRec& p = phys[i];
+        const uint64_t po = p.hoff + p.hsize;
+        const bool full = p.type == 1 || p.type == 5;
+        desc[i] = mck_wal_rec_desc{(uint32_t)po,
+                                   (uint32_t)(po >> 32) | ((uint32_t)p.type << 16) | (full ? MCK_WAL_REC_HASH : 0u),
+                                   p.length, p.stored};
+      }
+    };
+    if (T <= 1) {
+      fill(0, np);
+    } else {
+      std::vector<std::thread> th;
+      for (uint32_t k = 0; k < T; k++)
+        th.emplace_back(fill, (uint32_t)((uint64_t)np * k / T), (uint32_t)((uint64_t)np * (k + 1) / T));
+      for (auto& x : th) x.join();
+    }
   }
   const MultiPlan M = plan.compression ? MultiPlan{} : multi_plan(plan);
   R->info.walk_seconds = now_s() - t0;
@@ -212,7 +238,7 @@ extern "C" int mck_wal_recover(const void* wal_host, const void* wal_dev, uint64
       auto* d_ok = A.take<uint8_t>(np);
       auto* d_hash = A.take<uint64_t>(np);
       uint64_t* d_mh = nullptr;
-      if (hipMemcpyAsync(d_desc, desc.data(), (size_t)np * sizeof(mck_wal_rec_desc), hipMemcpyHostToDevice, st)) {
+      if (hipMemcpyAsync(d_desc, desc.get(), (size_t)np * sizeof(mck_wal_rec_desc), hipMemcpyHostToDevice, st)) {
         mck_internal_set_error("hipMemcpyAsync failed (record plan)");
         rc = MCK_EHIP;
       }
