@@ -134,11 +134,14 @@ __device__ __forceinline__ WrLoads wr_load(const WrRow& r, uint32_t c) {
   for (int j = 0; j < 4; j++) L.ch.v[j] = span_load16<false>(a0 + min(cb + 16u * j, lim));
   L.e = gload4(a0 + min(cb + 64u, lim));
   // the last stripe's word c (lanes 0-7), as the three dwords covering it;
-  // other lanes and rounds read their own chunk's first dword (round 6:
-  // they read the record's FIRST dword, whose line was long evicted after
-  // round 0 -- one more line per row round, FETCH 1.109 x at 32 KiB records)
+  // other lanes and rounds read the round's first dword -- one address per
+  // row, in the line lane 0's chunk load fetches (round 6: the record's
+  // first dword, long evicted after round 0, cost a line per row round,
+  // FETCH 1.109 x at 32 KiB records; each lane's own chunk instead put 16
+  // lines per row on the texture addresser for each of the three loads:
+  // 0.667 -> 0.470 of peak)
   const bool ls = r.hash() == 1u && r.k == r.nb() && c < 8;
-  const uint32_t w4 = ls ? (cover - 64 + 8 * c) & ~3u : min(cb, lim);
+  const uint32_t w4 = ls ? (cover - 64 + 8 * c) & ~3u : min(1024u * r.k, lim);
   L.l0 = gload4(a0 + w4);
   L.l1 = gload4(a0 + min(w4 + 4, lim));
   L.l2 = gload4(a0 + min(w4 + 8, lim));
