@@ -89,11 +89,23 @@ uint32_t mck_context_modifier(uint32_t base_context_checksum, uint64_t offset);
  * small synchronous calls and routes only batch-shaped callers to family 2.
  *
  * Error behaviour: the reference functions have no failure channel
- * (util/crc32c.h:26, include/rocksdb/file_checksum.h:47-49), so the plain
- * shims return 0 on ANY error and set mck_last_error() -- in particular
- * when mck_device_count() == 0 or a HIP call fails.  A caller that must not
- * mistake an error for a checksum uses the *_r variants, which return 0 /
- * MCK_E* and write the result through `out`. */
+ * (util/crc32c.h:26, include/rocksdb/file_checksum.h:47-49), so a plain
+ * shim cannot return an error.  By default it FAILS LOUDLY: on any error --
+ * in particular when mck_device_count() == 0 or a HIP call fails -- it
+ * prints mck_last_error() to stderr and aborts, so a call site re-pointed at
+ * a shim never stores a wrong checksum.  mck_set_shim_error_policy (or the
+ * environment variable SPEEDB_AMD_SHIM_ERRORS=zero, read once) selects the
+ * round-5 behaviour instead: return 0 with mck_last_error() set.  A caller
+ * that must handle errors uses the *_r variants, which return 0 / MCK_E*
+ * and write the result through `out`. */
+#define MCK_SHIM_ERRORS_ABORT 0 /* default: message to stderr, abort()      */
+#define MCK_SHIM_ERRORS_ZERO 1  /* return 0, mck_last_error() set            */
+/* Called (when set) with the error message before the policy applies --
+ * e.g. a maintainer's logger. */
+typedef void (*mck_shim_error_handler)(const char* message, void* arg);
+/* Process-wide; returns the previous policy, or MCK_EINVAL for an unknown
+ * one. */
+int mck_set_shim_error_policy(int policy, mck_shim_error_handler handler, void* arg);
 /* util/crc32c.h:26 Extend, :35 Value */
 uint32_t mck_crc32c_extend(uint32_t init_crc, const void* data, size_t n);
 uint32_t mck_crc32c_value(const void* data, size_t n);

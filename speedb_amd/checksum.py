@@ -99,6 +99,17 @@ def _checked(v):
     return v
 
 
+def _scalar(fn, ctype, *args):
+    """A scalar call through its *_r variant (the plain shims abort on a
+    device error by default, mck_set_shim_error_policy): the result, or
+    RuntimeError with mck_last_error()."""
+    out = ctype(0)
+    rc = fn(*args, ctypes.byref(out))
+    if rc != 0:
+        raise RuntimeError(f"speedb_amd: {_err()} ({rc})")
+    return out.value
+
+
 # ---------------------------------------------------------------------------
 # scalar API (util/crc32c.h, util/xxhash.h, table/format.cc)
 # ---------------------------------------------------------------------------
@@ -110,12 +121,12 @@ class crc32c:  # noqa: N801 -- mirrors the reference's namespace
     @staticmethod
     def Extend(init_crc: int, data) -> int:
         b, n = _buf(data)
-        return _checked(lib.mck_crc32c_extend(init_crc & 0xFFFFFFFF, b, n))
+        return _scalar(lib.mck_crc32c_extend_r, ctypes.c_uint32, init_crc & 0xFFFFFFFF, b, n)
 
     @staticmethod
     def Value(data) -> int:
         b, n = _buf(data)
-        return _checked(lib.mck_crc32c_value(b, n))
+        return _scalar(lib.mck_crc32c_value_r, ctypes.c_uint32, b, n)
 
     @staticmethod
     def Mask(crc: int) -> int:
@@ -132,26 +143,26 @@ class crc32c:  # noqa: N801 -- mirrors the reference's namespace
 
 def XXH3_64bits(data) -> int:
     b, n = _buf(data)
-    return _checked(lib.mck_xxh3_64(b, n))
+    return _scalar(lib.mck_xxh3_64_r, ctypes.c_uint64, b, n)
 
 
 def ComputeBuiltinChecksum(checksum_type: int, data) -> int:
     b, n = _buf(data)
-    return _checked(lib.mck_builtin_checksum(int(checksum_type), b, n))
+    return _scalar(lib.mck_builtin_checksum_r, ctypes.c_uint32, int(checksum_type), b, n)
 
 
 def ComputeBuiltinChecksumWithLastByte(checksum_type: int, data, last_byte) -> int:
     b, n = _buf(data)
     if isinstance(last_byte, int):
         last_byte = bytes([last_byte & 0xFF])
-    return _checked(lib.mck_builtin_checksum_with_last_byte(int(checksum_type), b, n, last_byte))
+    return _scalar(lib.mck_builtin_checksum_with_last_byte_r, ctypes.c_uint32, int(checksum_type), b, n, last_byte)
 
 
 def NPHash64(data, seed: int = 0) -> int:
     """util/hash.h:45 NPHash64 == util/hash.cc:81 Hash64: XXPH3 (the XXH3
     preview), seeded -- computed on the GPU."""
     b, n = _buf(data)
-    return _checked(lib.mck_np_hash64(b, n, seed & 0xFFFFFFFFFFFFFFFF))
+    return _scalar(lib.mck_np_hash64_r, ctypes.c_uint64, b, n, seed & 0xFFFFFFFFFFFFFFFF)
 
 
 Hash64 = NPHash64

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -1120,36 +1121,85 @@ int mck_np_hash64_r(const void* data, size_t n, uint64_t seed, uint64_t* out) {
   return scalar_u64(1, data, n, seed, out);
 }
 
-// The signature-compatible shims: 0 (and mck_last_error()) on any error.
+// The signature-compatible shims.  The reference functions cannot fail, so
+// an error is either fatal (default: a re-pointed call site must not store
+// a wrong checksum) or 0 with mck_last_error() set (MCK_SHIM_ERRORS_ZERO,
+// or SPEEDB_AMD_SHIM_ERRORS=zero).
+namespace {
+std::atomic<int> g_shim_policy{-1};  // -1: not read from the environment yet
+std::atomic<mck_shim_error_handler> g_shim_handler{nullptr};
+std::atomic<void*> g_shim_arg{nullptr};
+int shim_policy() {
+  int p = g_shim_policy.load(std::memory_order_acquire);
+  if (p < 0) {
+    const char* e = getenv("SPEEDB_AMD_SHIM_ERRORS");
+    const int env = (e && (strcmp(e, "zero") == 0 || strcmp(e, "0") == 0)) ? MCK_SHIM_ERRORS_ZERO : MCK_SHIM_ERRORS_ABORT;
+    int expected = -1;
+    g_shim_policy.compare_exchange_strong(expected, env, std::memory_order_acq_rel);
+    p = g_shim_policy.load(std::memory_order_acquire);
+  }
+  return p;
+}
+// the failure path of a plain shim: the handler, then abort or 0
+void shim_error(int rc, const char* fn) {
+  char msg[512];
+  snprintf(msg, sizeof msg, "speedb_amd: %s failed (%d): %s", fn, rc, mck_last_error());
+  if (mck_shim_error_handler h = g_shim_handler.load(std::memory_order_acquire))
+    h(msg, g_shim_arg.load(std::memory_order_acquire));
+  if (shim_policy() == MCK_SHIM_ERRORS_ABORT) {
+    fprintf(stderr, "%s\n(the reference function has no error channel; use the *_r variant or "
+                    "SPEEDB_AMD_SHIM_ERRORS=zero)\n", msg);
+    fflush(stderr);
+    abort();
+  }
+}
+uint32_t shim_u32(int rc, uint32_t v, const char* fn) {
+  if (rc == MCK_OK) return v;
+  shim_error(rc, fn);
+  return 0;
+}
+uint64_t shim_u64(int rc, uint64_t v, const char* fn) {
+  if (rc == MCK_OK) return v;
+  shim_error(rc, fn);
+  return 0;
+}
+}  // namespace
+
+int mck_set_shim_error_policy(int policy, mck_shim_error_handler handler, void* arg) {
+  if (policy != MCK_SHIM_ERRORS_ABORT && policy != MCK_SHIM_ERRORS_ZERO) {
+    set_err("unknown shim error policy %d", policy);
+    return MCK_EINVAL;
+  }
+  const int prev = shim_policy();
+  g_shim_arg.store(arg, std::memory_order_release);
+  g_shim_handler.store(handler, std::memory_order_release);
+  g_shim_policy.store(policy, std::memory_order_release);
+  return prev;
+}
 uint32_t mck_crc32c_extend(uint32_t init_crc, const void* data, size_t n) {
   uint32_t v = 0;
-  (void)mck_crc32c_extend_r(init_crc, data, n, &v);
-  return v;
+  return shim_u32(mck_crc32c_extend_r(init_crc, data, n, &v), v, "mck_crc32c_extend");
 }
 uint32_t mck_crc32c_value(const void* data, size_t n) {
   uint32_t v = 0;
-  (void)mck_crc32c_value_r(data, n, &v);
-  return v;
+  return shim_u32(mck_crc32c_value_r(data, n, &v), v, "mck_crc32c_value");
 }
 uint32_t mck_builtin_checksum(int type, const void* data, size_t n) {
   uint32_t v = 0;
-  (void)mck_builtin_checksum_r(type, data, n, &v);
-  return v;
+  return shim_u32(mck_builtin_checksum_r(type, data, n, &v), v, "mck_builtin_checksum");
 }
 uint32_t mck_builtin_checksum_with_last_byte(int type, const void* data, size_t n, char last_byte) {
   uint32_t v = 0;
-  (void)mck_builtin_checksum_with_last_byte_r(type, data, n, last_byte, &v);
-  return v;
+  return shim_u32(mck_builtin_checksum_with_last_byte_r(type, data, n, last_byte, &v), v,
+                     "mck_builtin_checksum_with_last_byte");
 }
 uint64_t mck_xxh3_64(const void* data, size_t n) {
   uint64_t v = 0;
-  (void)mck_xxh3_64_r(data, n, &v);
-  return v;
+  return shim_u64(mck_xxh3_64_r(data, n, &v), v, "mck_xxh3_64");
 }
 uint64_t mck_np_hash64(const void* data, size_t n, uint64_t seed) {
   uint64_t v = 0;
-  (void)mck_np_hash64_r(data, n, seed, &v);
-  return v;
+  return shim_u64(mck_np_hash64_r(data, n, seed, &v), v, "mck_np_hash64");
 }
 int mck_np_hash64_batch(const mck_spans* spans, uint64_t seed, uint64_t* out, mck_stream_t stream) {
   t_err[0] = 0;

@@ -82,8 +82,13 @@ def test_data_shims_fail_cleanly_without_gpu():
     if torch.cuda.is_available():
         pytest.skip("GPU present")
     from speedb_amd import _lib
-    assert _lib.lib.mck_crc32c_value(b"abc", 3) == 0
-    assert _lib.lib.mck_last_error() != b""
+    prev = _lib.lib.mck_set_shim_error_policy(1, None, None)  # MCK_SHIM_ERRORS_ZERO
+    try:
+        assert _lib.lib.mck_crc32c_value(b"abc", 3) == 0
+        assert _lib.lib.mck_last_error() != b""
+    finally:
+        _lib.lib.mck_set_shim_error_policy(prev, None, None)
+    assert _lib.lib.mck_set_shim_error_policy(7, None, None) == -1  # unknown policy
     # the error-returning variants report it
     out32, out64 = ctypes.c_uint32(7), ctypes.c_uint64(7)
     assert _lib.lib.mck_crc32c_value_r(b"abc", 3, ctypes.byref(out32)) < 0 and out32.value == 0
@@ -133,3 +138,29 @@ def test_statistics_without_device():
     assert set(st) == {"BLOCK_CHECKSUM_COMPUTE_COUNT", "BLOCK_CHECKSUM_MISMATCH_COUNT", "batches", "spans",
                        "bytes_known"}
     assert all(v >= 0 for v in st.values())
+
+
+def test_plain_shim_error_fails_loudly_by_default(tmp_path):
+    """ADVICE/VERDICT r5: a plain shim (no error channel, like the reference
+    function it replaces) must not hand a re-pointed call site a silent 0 --
+    by default it prints the error and aborts; SPEEDB_AMD_SHIM_ERRORS=zero
+    (or mck_set_shim_error_policy) restores return-0.  Without a GPU the
+    device call fails, which is the error exercised here."""
+    import os
+    import subprocess
+    import sys
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    code = ("from speedb_amd import _lib\n"
+            "v = _lib.lib.mck_crc32c_value(b'abc', 3)\n"
+            "print('returned', v)\n")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=repo)
+    env.pop("SPEEDB_AMD_SHIM_ERRORS", None)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode != 0 and "returned" not in r.stdout
+    assert "mck_crc32c_value failed" in r.stderr and "_r variant" in r.stderr
+    env["SPEEDB_AMD_SHIM_ERRORS"] = "zero"
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0 and "returned 0" in r.stdout
