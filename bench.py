@@ -149,6 +149,8 @@ def parse():
     p.add_argument("--span-min", type=int, default=100, help="smallest span (walrec, ragged)")
     p.add_argument("--span-max", type=int, default=1100, help="largest span (walrec, ragged)")
     p.add_argument("--span-bytes", type=int, default=1 << 30, help="span bytes per GPU (walrec, ragged)")
+    p.add_argument("--span-align", type=int, default=1,
+                   help="ragged: span starts rounded up to this multiple (128: no cache line shared by two spans)")
     p.add_argument("--ragged-hash", choices=["crc32c", "xxh3"], default="crc32c",
                    help="ragged: the checksum (xxh3: XXH3_64bits per span, mck_xxh3_64_batch)")
     p.add_argument("--host-blocks", type=int, default=2_500_000,
@@ -585,6 +587,8 @@ def make_workload(args, dev, rank, world):
         # walrec: a WAL payload follows its 7-byte header (+ trailer gaps):
         # records at any byte offset; ragged: spans back to back
         step = lens + (7 + gaps if args.workload == "walrec" else 0)
+        if args.workload == "ragged" and args.span_align > 1:  # each span's slot rounded up
+            step = (step + args.span_align - 1) // args.span_align * args.span_align
         offs = np.zeros(n_est, dtype=np.int64)
         offs[1:] = np.cumsum(step)[:-1]
         count = n_est
@@ -615,6 +619,8 @@ def make_workload(args, dev, rank, world):
         w.cfg = {"spans_per_gpu": count, "span_min": args.span_min, "span_max": args.span_max}
         if x3:
             w.cfg["hash"] = "xxh3"
+        if args.workload == "ragged" and args.span_align > 1:
+            w.cfg["span_align"] = args.span_align
 
         def check():
             idx = np.random.default_rng(rank).choice(count, size=256, replace=False)
