@@ -518,13 +518,18 @@ __device__ __noinline__ uint64_t x3s_hash_row(uint64_t ptr, uint64_t n, uint64_t
 // it with the same n and rows.
 // (kl: the 16 lanes' keys in LDS, read where they are used -- the caller's
 // row-loop constants stay live across this pass; nullptr: in registers)
-template <class Op, bool PREVIEW, int U, class Slot>
+// (KLDS is a template flag, not a null test: a runtime choice between the
+// LDS keys and a register copy had the compiler take the copy's address --
+// a scratch store of 32 bytes per lane per iteration, WRITE 4.6 x the
+// outputs at 100-300 B)
+template <class Op, bool PREVIEW, int U, bool KLDS = false, class Slot>
 __device__ __forceinline__ void x3_short_rows(const Op& op, uint32_t t0, uint32_t n, uint32_t rows, uint64_t seed,
                                               Slot&& slot, const X3Short* kl = nullptr) {
   static_assert(U <= 8, "lanes 0-7 hold the hashes");
   if (n == 0) return;
   const uint32_t j = threadIdx.x & 15u;
-  const X3Short Kr = kl ? X3Short{} : x3s_keys(j, seed);
+  X3Short Kr{};
+  if constexpr (!KLDS) Kr = x3s_keys(j, seed);
   const uint64_t base = reinterpret_cast<uint64_t>(op.base());
   uint32_t len[U], idx[U];
   uint64_t off[U];
@@ -561,9 +566,14 @@ __device__ __forceinline__ void x3_short_rows(const Op& op, uint32_t t0, uint32_
     }
     fetch(t + rows * U);  // (past n: clamped slots, flagged not short)
     if (__any(any)) {
+      X3Short K;
+      if constexpr (KLDS)
+        K = kl[j];
+      else
+        K = Kr;
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        uint64_t h = x3s_row_hash<PREVIEW>(ln[u], d[u], has[u], kl ? kl[j] : Kr);
+        uint64_t h = x3s_row_hash<PREVIEW>(ln[u], d[u], has[u], K);
         if (sh[u] && ln[u] <= 16u && j == (uint32_t)u)
           h = x3_small<PREVIEW>(reinterpret_cast<const uint8_t*>(ptr[u]), ln[u], seed);
         if (sh[u] && j == (uint32_t)u) op.finish(ix[u], h);
@@ -1283,7 +1293,7 @@ __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t l
     const uint32_t wb = lo + w0, nshort = L[0], nlong = L[1];
     uint64_t* hv = reinterpret_cast<uint64_t*>(&s.acc[0][0]);  // (the piece path's accumulators, unused here)
     const X3ParkOp<Op> pop{op, hv, wb};
-    x3_short_rows<X3ParkOp<Op>, PREVIEW, X3S_U>(pop, row, nshort, rows, seed, [&](uint32_t q, uint32_t& len, uint64_t& off) {
+    x3_short_rows<X3ParkOp<Op>, PREVIEW, X3S_U, true>(pop, row, nshort, rows, seed, [&](uint32_t q, uint32_t& len, uint64_t& off) {
       const uint32_t k = s.pre[q];
       len = s.len[k];
       off = s.off[k];
