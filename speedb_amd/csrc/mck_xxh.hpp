@@ -1088,6 +1088,7 @@ struct X3Lds {
   uint32_t ctr;
   uint32_t lists[2][4];  // rows share, by window parity: short count, long count, long ticket
   X3Short skeys[16];     // rows share: x3_short_rows' keys of row lane j
+  uint64_t sec[24];      // rows share: XXH3_kSecret as words (x3_mid_quads)
   ulonglong2 acc[kX3DescCache][4];                       // span t's accumulators, pair q
   ulonglong2 csum[kX3MaxWaves][4 * kX3PieceRounds][4];  // a wave's parked C_g, pair q
 };
@@ -1197,12 +1198,16 @@ __device__ __forceinline__ void xxh3_piece_loop(const Op& op, X3FeedPieces& f, c
 // wave units win (2000-4000 B 0.636 vs 0.590, SST-sized 4 KiB + jitter
 // 0.733 vs 0.628; microbench/x3_width.py, profiles/r5/x3_width/).  Chosen
 // per workgroup from a sample of its share's lengths, as crc_share_long.
-// (round 6: from a 160-byte mean -- below 256 B the wave units padded every
-// 241-600-byte span to a 4 KiB round: ragged 100-300 B ran at 0.136, 0.264
-// in the rows share, x3_rows_share; shares of mostly <= 240-byte spans stay
-// on the wave units' one-span-per-lane short loop: 16-240 B 0.243 there,
-// 0.228 in the rows share; profiles/r6/x3short/)
-constexpr uint32_t kX3RowsMin = 160, kX3RowsMax = 2560;  // mean span bytes
+// (round 6: no lower bound -- below 256 B the wave units padded every
+// 241-600-byte span to a 4 KiB round: ragged 100-300 B ran at 0.136; the
+// rows share with short spans on lane quads (x3_short_quads) and 241..512-
+// byte spans on lane quads (x3_mid_quads) runs 100-300 B at 0.41 and
+// 16-240 B at 0.445, against 0.243 on the wave units' one-span-per-lane
+// short loop; profiles/r6/x3short/)
+#ifndef X3_ROWS_MIN
+#define X3_ROWS_MIN 0u
+#endif
+constexpr uint32_t kX3RowsMin = X3_ROWS_MIN, kX3RowsMax = 2560;  // mean span bytes
 template <class Op>
 __device__ __forceinline__ bool x3_share_rows(const Op& op, uint32_t lo, uint32_t hi) {
   const uint32_t n = hi - lo, lane = threadIdx.x & 63;
@@ -1213,8 +1218,112 @@ __device__ __forceinline__ bool x3_share_rows(const Op& op, uint32_t lo, uint32_
   return m != 0 && len >= (uint64_t)kX3RowsMin * m && len < (uint64_t)kX3RowsMax * m;
 }
 
+// Short spans (<= 240 B) on lane quads: lane q of a quad takes windows q,
+// q + 4, q + 8, q + 12 of x3s_off's sixteen (four loads), the quad sums
+// S0 (windows < 8) and S1 with two quad_sum -- four spans per row per
+// iteration where x3_short_rows hashed one per row slot.  Keys from LDS.
+template <class Op, class Slot>
+__device__ __forceinline__ void x3_short_quads(const Op& op, uint32_t n, const X3Short* kl, Slot&& slot) {
+  if (n == 0) return;
+  const uint32_t qd = threadIdx.x >> 2, nq = blockDim.x >> 2, q = threadIdx.x & 3u;
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  for (uint32_t t = qd; __any(t < n); t += nq) {
+    const bool act = t < n;
+    uint32_t len;
+    uint64_t off;
+    const uint32_t idx = slot(act ? t : n - 1, len, off);
+    const uint64_t ptr = base + off;
+    uint4 d[4];
+    bool has[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t o = x3s_off(len, q + 4 * (uint32_t)k, has[k]);
+      has[k] = has[k] && act && len > 16;
+      d[k] = load16_realign(has[k] ? ptr + o : ptr & ~15ull);
+    }
+    const bool mid = len <= 128;
+    uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const X3Short K = kl[q + 4 * k];
+      const uint64_t lo = ((uint64_t)d[k].y << 32) | d[k].x, hi = ((uint64_t)d[k].w << 32) | d[k].z;
+      const uint64_t v = has[k] ? mul128_fold64(lo ^ (mid ? K.a0 : K.b0), hi ^ (mid ? K.a1 : K.b1)) : 0ull;
+      if (k < 2)
+        s0 += v;
+      else
+        s1 += v;
+    }
+    s0 = quad_sum(s0);
+    s1 = quad_sum(s1);
+    const uint64_t a = (uint64_t)len * P64_1 + s0;
+    uint64_t h = mid ? xxh3_avalanche(a + s1) : xxh3_avalanche(xxh3_avalanche(a) + s1);
+    if (act && q == 0) {
+      if (len <= 16) h = x3_small<false>(reinterpret_cast<const uint8_t*>(ptr), len, 0);
+      op.finish(idx, h);
+    }
+  }
+}
+
+// ---- spans of 241..1024 bytes on lane quads (round 6) ----------------------
+// XXH3_64bits of 240 < n <= 1024 (util/xxhash.h:5141-5227 with no full
+// block: nbStripes = (n - 1) / 64 stripes of the one partial segment, the
+// last stripe at n - 64, the merge) needs no scramble, so a span is FOUR
+// lanes: lane q of the quad keeps accumulators 2q, 2q + 1 and reads bytes
+// [16 q, 16 q + 16) of every stripe (the quad reads each 64-byte stripe
+// whole), four stripes per iteration.  The 16-lane row loop spent a whole
+// 1 KiB iteration on such a span (a 280-byte span filled 27 % of it); four
+// spans per row now share one.  Stripe secrets from the LDS copy (word
+// s + 2 q of stripe s).
+template <class Op, class Slot>
+__device__ __forceinline__ void x3_mid_quads(const Op& op, uint32_t n, const X3Row& X, const uint64_t* lsec,
+                                             Slot&& slot) {
+  if (n == 0) return;
+  const uint32_t qd = threadIdx.x >> 2, nq = blockDim.x >> 2, q = threadIdx.x & 3u;
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  for (uint32_t t = qd; __any(t < n); t += nq) {
+    const bool act = t < n;
+    uint32_t len;
+    uint64_t off;
+    const uint32_t idx = slot(act ? t : n - 1, len, off);
+    const uint64_t ptr = base + off;
+    const uint32_t nst = act ? (len - 1) >> 6 : 0u;  // 240 < len <= 1024: no full segment
+    uint64_t a0 = X.i0, a1 = X.i1;
+    for (uint32_t g = 0; __any(4 * g < nst); g++) {
+      uint4 d[4];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t st = 4 * g + (uint32_t)k;
+        d[k] = load16_realign(st < nst ? ptr + 64 * st + 16 * q : ptr & ~15ull);
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        const uint32_t st = 4 * g + (uint32_t)k;
+        if (st < nst) {  // v0.8.1: acc[i] += data[i ^ 1] + lo32(d ^ s) * hi32(d ^ s)
+          const uint64_t d0 = ((uint64_t)d[k].y << 32) | d[k].x, d1 = ((uint64_t)d[k].w << 32) | d[k].z;
+          a0 += d1 + mul32to64(d0 ^ lsec[st + 2 * q]);
+          a1 += d0 + mul32to64(d1 ^ lsec[st + 2 * q + 1]);
+        }
+      }
+    }
+    // the last stripe (secret 121 + 16 q) and the merge (secret 11 + 16 q)
+    const uint4 dl = load16_realign(act ? ptr + len - 64 + 16 * q : ptr & ~15ull);
+    const uint64_t l0 = ((uint64_t)dl.y << 32) | dl.x, l1 = ((uint64_t)dl.w << 32) | dl.z;
+    a0 += l1 + mul32to64(l0 ^ X.kl0);
+    a1 += l0 + mul32to64(l1 ^ X.kl1);
+    const uint64_t m = quad_sum(mul128_fold64(a0 ^ X.km0, a1 ^ X.km1));
+    const uint64_t h = xxh3_avalanche((uint64_t)len * P64_1 + m);
+    if (act && q == 0) op.finish(idx, h);
+  }
+}
+
 #ifndef X3S_U
 #define X3S_U 2
+#endif
+#ifndef X3S_MIDMAX
+#define X3S_MIDMAX 512u
+#endif
+#ifndef X3S_QUADS
+#define X3S_QUADS 1
 #endif
 #ifndef X3S_WIN
 #define X3S_WIN 1024
@@ -1258,6 +1367,9 @@ __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t l
   }
   if (t < 8) (&s.lists[0][0])[t] = 0;
   if (t < 16) s.skeys[t] = x3s_keys(t, seed);
+  if (t < 24) s.sec[t] = sec64(8 * (int)t);
+  // the mid list lives past the parked hashes in the piece path's accumulators
+  uint32_t* const mlist = reinterpret_cast<uint32_t*>(&s.acc[0][0]) + 2 * kX3DescCache;
   uint32_t par = 0;
   for (uint32_t w0 = 0; w0 < n; w0 += W, par ^= 1u) {
     const uint32_t wn = n - w0 < W ? n - w0 : W;
@@ -1267,18 +1379,23 @@ __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t l
       s.off[t] = noff;
       s.len[t] = nlen;
     }
-    const bool in = t < wn, sh = in && nlen <= 240u, lg = in && nlen > 240u;
-    const uint64_t ms = __ballot(sh), ml = __ballot(lg);
+    // short (<= 240), mid (<= 1024: x3_mid_quads), long (the row loop)
+    const bool in = t < wn, sh = in && nlen <= 240u, md = in && nlen > 240u && nlen <= X3S_MIDMAX,
+               lg = in && nlen > X3S_MIDMAX;
+    const uint64_t ms = __ballot(sh), mm = __ballot(md), ml = __ballot(lg);
     const uint32_t lane = t & 63u;
-    uint32_t bs = 0, bl = 0;
+    uint32_t bs = 0, bm = 0, bl = 0;
     if (lane == 0) {
       if (ms) bs = atomicAdd(&L[0], (uint32_t)__popcll(ms));
       if (ml) bl = atomicAdd(&L[1], (uint32_t)__popcll(ml));
+      if (mm) bm = atomicAdd(&L[3], (uint32_t)__popcll(mm));
     }
     bs = __shfl(bs, 0, 64);
+    bm = __shfl(bm, 0, 64);
     bl = __shfl(bl, 0, 64);
     const uint64_t below = (1ull << lane) - 1;
     if (sh) s.pre[bs + (uint32_t)__popcll(ms & below)] = t;
+    if (md) mlist[bm + (uint32_t)__popcll(mm & below)] = t;
     if (lg) s.done[bl + (uint32_t)__popcll(ml & below)] = t;
     if (t < 4) s.lists[par ^ 1u][t] = 0;  // the next window's counters
     __syncthreads();
@@ -1293,12 +1410,22 @@ __device__ __forceinline__ void x3_rows_share(const Op& op, X3Lds& s, uint32_t l
     const uint32_t wb = lo + w0, nshort = L[0], nlong = L[1];
     uint64_t* hv = reinterpret_cast<uint64_t*>(&s.acc[0][0]);  // (the piece path's accumulators, unused here)
     const X3ParkOp<Op> pop{op, hv, wb};
-    x3_short_rows<X3ParkOp<Op>, PREVIEW, X3S_U, true>(pop, row, nshort, rows, seed, [&](uint32_t q, uint32_t& len, uint64_t& off) {
+    auto sslot = [&](uint32_t q, uint32_t& len, uint64_t& off) {
       const uint32_t k = s.pre[q];
       len = s.len[k];
       off = s.off[k];
       return wb + k;
-    }, s.skeys);
+    };
+    if constexpr (X3S_QUADS && !PREVIEW)
+      x3_short_quads(pop, nshort, s.skeys, sslot);
+    else
+      x3_short_rows<X3ParkOp<Op>, PREVIEW, X3S_U, true>(pop, row, nshort, rows, seed, sslot, s.skeys);
+    x3_mid_quads(pop, L[3], X, s.sec, [&](uint32_t q, uint32_t& len, uint64_t& off) {
+      const uint32_t k = mlist[q];
+      len = s.len[k];
+      off = s.off[k];
+      return wb + k;
+    });
     auto next = [&](X3Span& r) {
       uint32_t tk = 0;
       if (j == 0) tk = atomicAdd(&L[2], 1u);
