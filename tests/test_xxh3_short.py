@@ -4,8 +4,11 @@ a half-row reduction replace the one-lane walk of util/xxhash.h:3990-4130
 (XXPH3: util/xxph3.h:1086-1147).  Every length 0..260 at every start
 alignment, on each driver that hashes short spans:
 
-* the wave kernel's piece path (ragged batch, short spans staged in LDS),
-* the wave kernel's rows share (ragged batch averaging 256 B - 2.5 KiB),
+* the wave kernel's rows share (ragged batches averaging < 2.5 KiB): short
+  spans and 241..512-byte spans on lane quads (x3_short_quads,
+  x3_mid_quads), longer ones on the row loop,
+* the wave kernel's piece path (shares averaging >= 2.5 KiB; short spans
+  one per lane),
 * the rows kernel (uniform batches, x3_next_long),
 * k_xph3 (NPHash64 batches, seeded XXPH3),
 * k_wal_recover (records of <= 240 B hashed at their last round).
@@ -59,7 +62,8 @@ def _all_short():
 @pytest.mark.parametrize("driver", [0, 1, 2])
 def test_xxh3_short_every_length_alignment(gpu, oracle, driver):
     """driver 0: the engine's choice (a ragged batch of mostly short spans:
-    the wave kernel's piece path), 1: the wave kernel, 2: the rows kernel."""
+    the wave kernel's rows share, lane quads), 1: the wave kernel, 2: the
+    rows kernel."""
     import speedb_amd as S
     from speedb_amd._lib import lib
     torch = gpu
@@ -152,3 +156,21 @@ def test_wal_recover_every_short_record(gpu, oracle):
         bad = [(n, (off + hs) & 3) for k, (off, t, n) in enumerate(w.records)
                if t in (1, 5) and int(hv[k]) != oracle.XXH3(img[off + hs:off + hs + n])]
         assert not bad, bad[:10]
+
+
+def test_xxh3_short_in_piece_path(gpu, oracle):
+    """Shares averaging >= 2.5 KiB run on the wave units (the piece path),
+    whose short spans are hashed one per lane before the pieces: every
+    length 0..260 between 6-9 KiB spans, each span bit-exact."""
+    import speedb_amd as S
+    torch = gpu
+    rnd = random.Random(61)
+    lens = []
+    for n in range(261):
+        lens += [n, rnd.randrange(6000, 9000)]
+    host, dev, offs = _pack(torch, 67, lens)
+    sp = _spans(torch, S, dev, offs, lens)
+    got = S.xxh3_64_batch(sp).cpu().numpy().view(np.uint64)
+    bad = [(lens[i], offs[i] % 16) for i in range(len(lens))
+           if int(got[i]) != oracle.XXH3(host[offs[i]:offs[i] + lens[i]])]
+    assert not bad, bad[:10]
