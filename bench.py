@@ -324,9 +324,10 @@ def make_workload(args, dev, rank, world):
         else:
             w.step = lambda: S.xxh3_64_batch(spans, out=out64, stream=stream)
             # uniform batches of >= 3 KiB spans (and >= 16 per CU) run on the
-            # wave kernel since round 5 (mck_engine.hip kX3UniformWaveMin)
+            # wave kernel since round 5 (mck_engine.hip kX3UniformWaveMin),
+            # those of <= 512 B since round 6 (lane quads, X3_UNIFORM_QUAD_MAX)
             ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-            w.kernel = ("mck::k_xxh3_wave<mck::OpX3Value>" if block >= 3072 and count >= 16 * ncu
+            w.kernel = ("mck::k_xxh3_wave<mck::OpX3Value>" if (block >= 3072 or block <= 512) and count >= 16 * ncu
                         else "mck::k_xxh3<mck::OpX3Value>")
             w.alg_bytes = count * (block + 8)
         w.span_bytes = count * block

@@ -301,6 +301,9 @@ std::atomic<int> g_x3_force{0};
 // uniform.txt: 4 KiB 0.827 vs 0.761 on rows, 16 KiB 0.801 vs 0.685; 1-2 KiB
 // stay on rows, 0.774-0.815 vs 0.721-0.768).
 constexpr uint32_t kX3UniformWaveMin = 3072;
+#ifndef X3_UNIFORM_QUAD_MAX
+#define X3_UNIFORM_QUAD_MAX 512u
+#endif
 template <class Op>
 int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform, uint32_t uniform_len = 0) {
   if (!count) return MCK_OK;
@@ -309,6 +312,10 @@ int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform, uint
   if (rc) return rc;
   // (small batches keep the rows kernel: no share search in their latency)
   if (uniform && uniform_len >= kX3UniformWaveMin && count >= 16u * (uint32_t)ncu) uniform = false;
+  // uniform spans of <= 512 bytes too: the wave kernel's rows share hashes
+  // them four per row on lane quads (x3_short_quads / x3_mid_quads), the
+  // rows kernel one per row
+  if (uniform && uniform_len <= X3_UNIFORM_QUAD_MAX && count >= 16u * (uint32_t)ncu) uniform = false;
   const int force = g_x3_force.load(std::memory_order_relaxed);
   if (force) uniform = force == 2;
   if (!uniform) {
