@@ -142,7 +142,7 @@ def parse():
     p.add_argument("--wal-len-max", type=int, default=1100, help="largest record payload (walwrite)")
     p.add_argument("--blob-records", type=int, default=1 << 20, help="blob records per GPU (blob)")
     p.add_argument("--kvs", type=int, default=1 << 22, help="KVs per GPU (kv)")
-    p.add_argument("--kv-value-bytes", type=int, default=1000, help="value bytes (blockkv)")
+    p.add_argument("--kv-value-bytes", type=int, default=1000, help="value bytes (kv, blockkv)")
     p.add_argument("--kv-prot-bytes", type=int, default=8, help="protection_bytes_per_key (blockkv)")
     p.add_argument("--kv-two-pass", action="store_true",
                    help="blockkv: the layout + protect pair (host readback between) instead of the one-pass call")
@@ -704,7 +704,7 @@ def make_workload(args, dev, rank, world):
             return int(status.sum().item()) == 0
         w.check = check
     elif args.workload == "kv":
-        count, kb, vb = args.kvs, 16, 1000
+        count, kb, vb = args.kvs, 16, args.kv_value_bytes
         keys = W.rand_bytes(count * kb + 64, dev, 400 + rank)
         vals = W.rand_bytes(count * vb + 64, dev, 401 + rank)
         ks, vs = S.Spans.uniform(keys, kb, count), S.Spans.uniform(vals, vb, count)
@@ -712,11 +712,13 @@ def make_workload(args, dev, rank, world):
         seqs = torch.arange(count, dtype=torch.int64, device=dev) + (rank << 40)
         out = torch.empty(count, dtype=torch.int64, device=dev)
         w.step = lambda: S.kv_protect_batch(S.ProtectionKind.KVOS, ks, vs, ops, seqs, out=out, stream=stream)
-        w.kernel = "mck::k_xph3<mck::OpKvProtect<false> >"
+        w.kernel = ("mck::k_xph3_quads<mck::OpKvProtect<false> >" if vb <= 240
+                    else "mck::k_xph3<mck::OpKvProtect<false> >")
         w.span_bytes = count * (kb + vb)
         w.alg_bytes = count * (kb + vb + 1 + 8 + 8)
         w.desc = (f"per-KV protection ProtectKVO(key, value, op).ProtectS(seqno) (db/kv_checksum.h) of "
-                  f"{count} KVs per GPU, {kb} B keys + {vb} B values (README 80M-key/1KB-value shape)")
+                  f"{count} KVs per GPU, {kb} B keys + {vb} B values"
+                  + (" (README 80M-key/1KB-value shape)" if vb == 1000 else ""))
         w.cfg = {"kvs_per_gpu": count, "key_bytes": kb, "value_bytes": vb}
 
         def check():

@@ -1036,6 +1036,11 @@ int mck_test_set_xxh3_driver(int driver);
  * declined (the reader's walk is then the plan); -1 = they differ.
  * Production code never calls it. */
 int mck_test_wal_walk_fast(const void* wal, uint64_t nbytes, uint32_t log_number);
+/* Test hook: 0 sends uniform batches of <= 240-byte spans of the XXPH3
+ * entry points (mck_np_hash64_batch, mck_kv_protect*_batch) to the row
+ * driver instead of the lane-quad kernel (1, the default).  Process-wide;
+ * production code never calls it. */
+int mck_test_set_xph3_quads(int on);
 
 #ifdef __cplusplus
 }

@@ -186,6 +186,7 @@ SIGNATURES = [
     ("mck_test_set_virtual_devices", ctypes.c_int, [ctypes.c_int]),
     ("mck_test_wal_walk_fast", ctypes.c_int, [vp, ctypes.c_uint64, ctypes.c_uint32]),
     ("mck_set_shim_error_policy", ctypes.c_int, [ctypes.c_int, vp, vp]),
+    ("mck_test_set_xph3_quads", ctypes.c_int, [ctypes.c_int]),
     ("mck_set_perf_level", ctypes.c_int, [ctypes.c_int]),
     ("mck_get_perf_level", ctypes.c_int, []),
     ("mck_perf_context_get", ctypes.c_int, [vp, ctypes.c_int]),

@@ -331,12 +331,24 @@ int launch_xxh3(const Op& op, uint32_t count, hipStream_t st, bool uniform, uint
   return MCK_OK;
 }
 
+// (test hook: mck_test_set_xph3_quads(0) sends uniform short batches to the
+// row driver, for the A/B and the parity of both)
+#ifndef XPH3_QUADS_DEFAULT
+#define XPH3_QUADS_DEFAULT 1
+#endif
+std::atomic<int> g_xph3_quads{XPH3_QUADS_DEFAULT};
 template <class Op>
-int launch_xph3(const Op& op, uint32_t count, uint64_t seed, hipStream_t st) {
+int launch_xph3(const Op& op, uint32_t count, uint64_t seed, hipStream_t st, bool uniform_short = false) {
   if (!count) return MCK_OK;
   int ncu;
   int rc = current_device(nullptr, &ncu);
   if (rc) return rc;
+  if (uniform_short && g_xph3_quads.load(std::memory_order_relaxed)) {  // every span <= 240 bytes
+    const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 63) / 64);
+    hipLaunchKernelGGL(k_xph3_quads<Op>, dim3(grid), dim3(256), 0, st, op, count, seed);
+    MCK_HIP(hipGetLastError());
+    return MCK_OK;
+  }
   const uint32_t grid = std::min<uint32_t>((uint32_t)ncu * 8, (count + 15) / 16);
   hipLaunchKernelGGL(k_xph3<Op>, dim3(grid), dim3(256), 0, st, op, count, seed);
   MCK_HIP(hipGetLastError());
@@ -1216,7 +1228,8 @@ int mck_np_hash64_batch(const mck_spans* spans, uint64_t seed, uint64_t* out, mc
     set_err("out is NULL");
     return MCK_EINVAL;
   }
-  return launch_xph3(OpXpValue{to_src(spans), out}, spans->count, seed, reinterpret_cast<hipStream_t>(stream));
+  return launch_xph3(OpXpValue{to_src(spans), out}, spans->count, seed, reinterpret_cast<hipStream_t>(stream),
+                     spans->lengths == nullptr && spans->length <= 240);
 }
 
 static int check_kv(int kind, const mck_spans* keys, const mck_spans* values, const uint64_t* extras) {
@@ -1246,7 +1259,8 @@ int mck_kv_protect_batch(int kind, const mck_spans* keys, const mck_spans* value
     return MCK_EINVAL;
   }
   const OpKvProtect<false> op{to_src(keys), to_src(values), op_types, extras, kind, out, nullptr, 0, nullptr, nullptr};
-  return launch_xph3(op, values->count, kSeedV, reinterpret_cast<hipStream_t>(stream));
+  return launch_xph3(op, values->count, kSeedV, reinterpret_cast<hipStream_t>(stream),
+                     values->lengths == nullptr && values->length <= 240);
 }
 
 int mck_kv_protect_verify_batch(int kind, const mck_spans* keys, const mck_spans* values, const uint8_t* op_types,
@@ -1265,7 +1279,8 @@ int mck_kv_protect_verify_batch(int kind, const mck_spans* keys, const mck_spans
   }
   const OpKvProtect<true> op{to_src(keys), to_src(values), op_types, extras, kind, computed, stored, prot_bytes,
                              mismatch, mismatch_count};
-  return launch_xph3(op, values->count, kSeedV, reinterpret_cast<hipStream_t>(stream));
+  return launch_xph3(op, values->count, kSeedV, reinterpret_cast<hipStream_t>(stream),
+                     values->lengths == nullptr && values->length <= 240);
 }
 
 // ---- per-KV protection of block entries (block.cc:1091-1222) ---------------
@@ -1773,6 +1788,11 @@ void mck_host_pipeline_release(void) {
     host_pipe_free(P);
   }
   (void)hipSetDevice(prev);
+}
+
+int mck_test_set_xph3_quads(int on) {
+  g_xph3_quads.store(on ? 1 : 0, std::memory_order_relaxed);
+  return MCK_OK;
 }
 
 int mck_test_set_virtual_devices(int k) {

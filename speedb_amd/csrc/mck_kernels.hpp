@@ -406,6 +406,56 @@ __global__ __launch_bounds__(256) void k_xph3(Op op, uint32_t count, uint64_t se
   xxh3_rows_driver<Op, true>(op, count, seed);
 }
 
+// Uniform batches of <= 240-byte spans (round 6): one span per lane QUAD
+// (the short classes' windows as x3_short_quads: lane q takes windows q,
+// q + 4, q + 8, q + 12, keys secret +/- seed, util/xxph3.h:1112-1147), 16
+// spans per wave at a time -- the row driver hashed a short span on one
+// lane of its row (a uniform batch of 100-byte values: one value per row per
+// round trip).  The quad's lane 0 runs the op's epilogue (finish(i, h)).
+template <class Op>
+__global__ __launch_bounds__(256) void k_xph3_quads(Op op, uint32_t count, uint64_t seed) {
+  const uint32_t q = threadIdx.x & 3u;
+  const uint32_t nq = gridDim.x * (blockDim.x >> 2);
+  X3Short K[4];
+#pragma unroll
+  for (int k = 0; k < 4; k++) K[k] = x3s_keys(q + 4 * (uint32_t)k, seed);
+  const uint64_t base = reinterpret_cast<uint64_t>(op.base());
+  for (uint32_t t = blockIdx.x * (blockDim.x >> 2) + (threadIdx.x >> 2); __any(t < count); t += nq) {
+    const bool act = t < count;
+    const uint32_t i = act ? t : count - 1;
+    const uint64_t len = op.hlen(i);
+    const uint64_t ptr = base + op.off(i);
+    const uint32_t n = (uint32_t)len;  // <= 240: launch_xph3 sends only such batches here
+    uint4 d[4];
+    bool has[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint32_t o = x3s_off(n, q + 4 * (uint32_t)k, has[k]);
+      has[k] = has[k] && act && n > 16;
+      d[k] = load16_realign(has[k] ? ptr + o : ptr & ~15ull);
+    }
+    const bool mid = n <= 128;
+    uint64_t s0 = 0, s1 = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      const uint64_t lo = ((uint64_t)d[k].y << 32) | d[k].x, hi = ((uint64_t)d[k].w << 32) | d[k].z;
+      const uint64_t v = has[k] ? mul128_fold64(lo ^ (mid ? K[k].a0 : K[k].b0), hi ^ (mid ? K[k].a1 : K[k].b1)) : 0ull;
+      if (k < 2)
+        s0 += v;
+      else
+        s1 += v;
+    }
+    s0 = quad_sum(s0);
+    s1 = quad_sum(s1);
+    const uint64_t a = (uint64_t)n * P64_1 + s0;
+    uint64_t h = mid ? xxph3_avalanche(a + s1) : xxph3_avalanche(xxph3_avalanche(a) + s1);
+    if (act && q == 0) {
+      if (len <= 16) h = x3_small<true>(reinterpret_cast<const uint8_t*>(ptr), len, seed);
+      op.finish(i, h);
+    }
+  }
+}
+
 // util/hash.h:45 NPHash64(data, n, seed) == util/hash.cc:81 Hash64
 struct OpXpValue {
   SpanSrc s;

@@ -174,3 +174,61 @@ def test_xxh3_short_in_piece_path(gpu, oracle):
     bad = [(lens[i], offs[i] % 16) for i in range(len(lens))
            if int(got[i]) != oracle.XXH3(host[offs[i]:offs[i] + lens[i]])]
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("quads", [1, 0])
+def test_np_hash64_uniform_short_quads(gpu, oracle, quads):
+    """Uniform XXPH3 batches of <= 240-byte spans run on k_xph3_quads (one
+    span per lane quad; the test hook sends them to the row driver for the
+    comparison): every length 0..240, odd strides, two seeds."""
+    import speedb_amd as S
+    from speedb_amd import _lib
+    torch = gpu
+    try:
+        _lib.check(_lib.lib.mck_test_set_xph3_quads(quads), "mck_test_set_xph3_quads")
+        for seed in (0, 0xA5155AE5E937AA16):
+            bad = []
+            for length in range(0, 241, 3 if quads == 0 else 1):
+                n = 700
+                stride = length + 7
+                host = splitmix_bytes(length * 31 + 5, n * stride + 64)
+                dev = torch.frombuffer(bytearray(host), dtype=torch.uint8).to("cuda")
+                sp = S.Spans(dev, n, offsets=torch.arange(n, dtype=torch.int64, device="cuda") * stride,
+                             length=length)
+                got = S.np_hash64_batch(sp, seed=seed).cpu().numpy().view(np.uint64)
+                bad += [(length, i) for i in range(0, n, 37)
+                        if int(got[i]) != oracle.Hash64(host[i * stride:i * stride + length], seed)]
+            assert not bad, bad[:10]
+    finally:
+        _lib.check(_lib.lib.mck_test_set_xph3_quads(1), "mck_test_set_xph3_quads")
+
+
+@pytest.mark.parametrize("vlen", [0, 5, 16, 17, 100, 128, 129, 200, 240])
+def test_kv_protect_uniform_short_values(gpu, oracle, vlen):
+    """Per-KV protection (db/kv_checksum.h ProtectKV / ProtectKVO /
+    ProtectKVOS) of uniform short values on the lane quads: the epilogue
+    (key, op type, seqno hashes) runs on each quad's lane 0; against the
+    oracle's KvProtect for every mode, and verify flags exactly the
+    corrupted entries."""
+    import speedb_amd as S
+    torch = gpu
+    n, kb = 3000, 24
+    host_k = splitmix_bytes(vlen + 1, n * kb + 64)
+    host_v = splitmix_bytes(vlen + 2, n * max(vlen, 1) + 64)
+    keys = torch.frombuffer(bytearray(host_k), dtype=torch.uint8).to("cuda")
+    vals = torch.frombuffer(bytearray(host_v), dtype=torch.uint8).to("cuda")
+    ks = S.Spans.uniform(keys, kb, n)
+    vs = S.Spans(vals, n, stride=vlen, length=vlen)
+    rnd = random.Random(vlen)
+    ops = torch.tensor([rnd.randrange(256) for _ in range(n)], dtype=torch.uint8, device="cuda")
+    seqs = torch.tensor([rnd.randrange(1 << 56) for _ in range(n)], dtype=torch.int64, device="cuda")
+    for mode, extra in ((S.ProtectionKind.KV, None), (S.ProtectionKind.KVO, None), (S.ProtectionKind.KVOS, seqs)):
+        out = S.kv_protect_batch(mode, ks, vs, ops, extra)
+        got = out.cpu().numpy().view(np.uint64)
+        o = ops.cpu().tolist()
+        ex = seqs.cpu().tolist()
+        for i in range(0, n, 53):
+            k = host_k[i * kb:(i + 1) * kb]
+            v = host_v[i * vlen:(i + 1) * vlen] if vlen else b""
+            want = oracle.KvProtect(int(mode), k, v, o[i], ex[i] if extra is not None else 0)
+            assert int(got[i]) == want, (int(mode), i)
