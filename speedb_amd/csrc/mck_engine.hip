@@ -559,6 +559,11 @@ int blk_kv(int kind, const mck_spans* blocks, uint32_t prot_bytes, const uint64_
 }
 
 // ---- one pass: k_block_kv_walk + scan + k_block_kv_flush + long values -----
+// (MCK_BLK_WALK_PAD: dynamic LDS added to the walk's launch, an occupancy
+// A/B knob for variant builds; the product build adds none)
+#ifndef MCK_BLK_WALK_PAD
+#define MCK_BLK_WALK_PAD 0
+#endif
 template <int KIND>
 struct BlkWalkT {
   template <class... A>
@@ -666,7 +671,7 @@ int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32
   MCK_HIP(hipMemsetAsync(w.flag, 0, 4, st));
   // (the walk's key buffers + entry windows, 73 KiB static, already hold it
   // at two workgroups per CU: no pad)
-  if (int rc = launch_blk<BlkWalkT>(kind, n, st, n, 0, to_src(blocks), n, slot_cap, w.arena, arena_cap,
+  if (int rc = launch_blk<BlkWalkT>(kind, n, st, n, (size_t)MCK_BLK_WALK_PAD, to_src(blocks), n, slot_cap, w.arena, arena_cap,
                                     w.slot_h, w.slot_m, w.blk_long, kb, ab, restart_interval, status, w.flag))
     return rc;
   const uint32_t tiles = (uint32_t)blk_tiles(n);
@@ -1445,6 +1450,7 @@ struct HostPipe {
   std::mutex mu;
   size_t cap = 0;          // chunk bytes per slot
   uint32_t max_spans = 0;  // descriptor/result entries per slot
+  int dev = -1;            // device the buffers and streams were built on
   HostSlot slot[kHostSlots];
 };
 static HostPipe g_host[kMaxDev];
@@ -1465,15 +1471,24 @@ static void host_pipe_free(HostPipe& p) {
   }
   p.cap = 0;
   p.max_spans = 0;
+  p.dev = -1;
 }
 
 // Make the pipeline hold at least cap chunk bytes and max_spans entries per
 // slot.  On failure everything is freed (no partial state survives).
-static int host_pipe_reserve(HostPipe& p, size_t cap, uint32_t max_spans) {
-  if (p.cap >= cap && p.max_spans >= max_spans && p.slot[0].st) return MCK_OK;
+static int host_pipe_reserve(HostPipe& p, int dev, size_t cap, uint32_t max_spans) {
+  if (p.dev == dev && p.cap >= cap && p.max_spans >= max_spans && p.slot[0].st) return MCK_OK;
   cap = std::max(cap, p.cap);
   max_spans = std::max(max_spans, p.max_spans);
+  if (p.dev >= 0 && p.dev != dev) {
+    // a pipe built on another device (the virtual-devices hook maps pipe
+    // indices to device 0) is freed on that device, then rebuilt on dev
+    (void)hipSetDevice(p.dev);
+    host_pipe_free(p);
+    (void)hipSetDevice(dev);
+  }
   host_pipe_free(p);
+  p.dev = dev;
   hipError_t e = hipSuccess;
   const char* what = "";
   auto ok = [&](hipError_t r, const char* w) {
@@ -1523,7 +1538,7 @@ static int run_device_share(int dev, int pipe, const HostJob& J, uint32_t lo, ui
   const uint32_t max_spans = (uint32_t)std::min<uint64_t>(hi - lo, 1u << 20);
   HostPipe& P = g_host[pipe];
   std::lock_guard<std::mutex> lock(P.mu);
-  if ((rc = host_pipe_reserve(P, cap, max_spans))) return rc;
+  if ((rc = host_pipe_reserve(P, dev, cap, max_spans))) return rc;
   const size_t res_sz = J.kind == MCK_kXXH3 ? 8 : 4;
   auto drain = [&](HostSlot& s) -> int {
     if (!s.n) return MCK_OK;
@@ -1778,13 +1793,13 @@ int mck_test_set_crc_driver(int driver, int interleaved) {
 void mck_host_pipeline_release(void) {
   int prev = 0;
   (void)hipGetDevice(&prev);
-  const bool virt = g_virtual_devs.load(std::memory_order_relaxed) > 0;
   for (int d = 0; d < kMaxDev; d++) {
     HostPipe& P = g_host[d];
     std::lock_guard<std::mutex> lock(P.mu);
     if (!P.slot[0].st && !P.cap) continue;
-    // (pipes of virtual devices live on device 0)
-    if (hipSetDevice(virt ? 0 : d) != hipSuccess) continue;
+    // each pipe is freed on the device it was built on (pipes of virtual
+    // devices live on device 0, a caller's own device's pipe on that device)
+    if (P.dev < 0 || hipSetDevice(P.dev) != hipSuccess) continue;
     host_pipe_free(P);
   }
   (void)hipSetDevice(prev);
