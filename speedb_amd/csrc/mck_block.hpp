@@ -894,6 +894,15 @@ __host__ __device__ __forceinline__ uint32_t blk_long_words(uint32_t slot_cap) {
 // (144 B: 16-byte aligned, conflict-free b128 stores; 16 B of pad for the
 // unaligned reads at the row end).
 constexpr uint32_t kBlkWin = 128, kBlkWinRow = 36;
+// MCK_BLK_SLOT_NT: the walk's slot stores non-temporal (A/B knob: a lane's
+// partly written slot line otherwise sits in L2 for ~16 entries beside the
+// window lines the next entry re-reads)
+#ifndef MCK_BLK_SLOT_NT
+#define MCK_BLK_SLOT_NT 0
+#endif
+#ifndef MCK_BLK_RS_CACHE
+#define MCK_BLK_RS_CACHE 0
+#endif
 __device__ __forceinline__ uint4 lds_row_u4(const uint32_t* w, uint32_t o) {  // 16 bytes at byte o
   const uint32_t i = o >> 2, sb = o & 3u;
   const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2], d3 = w[i + 3], d4 = w[i + 4];
@@ -974,6 +983,7 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
   int st = kBlkOk;
   BlkHdr h{0, 0, false};
   bool active = false;
+  uint32_t rs1 = 0, rs2 = 0, rs3 = 0;  // restart points 1..3 (MCK_BLK_RS_CACHE)
   if (in) {
     h = rd_header(rd, n64);
     if (!h.ok) {
@@ -986,6 +996,11 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
         uint32_t x[4];
 #pragma unroll
         for (int j = 0; j < 4; j++) x[j] = r0 + j < h.nr ? rd.u32(h.ro + 4 * (r0 + j)) : 0u;
+        if (MCK_BLK_RS_CACHE && r0 == 0) {
+          rs1 = x[1];
+          rs2 = x[2];
+          rs3 = x[3];
+        }
 #pragma unroll
         for (int j = 0; j < 4; j++) {
           const uint32_t r = r0 + j;
@@ -1009,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
   uint32_t p = 0, idx = 0, interval = 0, in_cur = 0, r = 0, kl = 0;
   // restart point r and, loaded one restart ahead, r + 1
   uint32_t next = active ? rd.u32(ro) : 0u;
-  uint32_t nextn = active && nr > 1 ? rd.u32(ro + 4) : 0xFFFFFFFFu;
+  uint32_t nextn = active && nr > 1 ? (MCK_BLK_RS_CACHE ? rs1 : rd.u32(ro + 4)) : 0xFFFFFFFFu;
   uint64_t kbytes = 0;
   // the next entry, one entry ahead: its window (octet loads, wnx) when
   // [p, p + 128) lies in the block, else its first 16 bytes (U, uok)
@@ -1049,7 +1064,10 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
         in_cur = 0;
         r++;
         next = nextn;
-        nextn = r + 1 < nr ? rd.u32(ro + 4 * (r + 1)) : 0xFFFFFFFFu;
+        // (the restart array's line is long gone from L2 by now: points 1..3
+        // come from the header pass's registers)
+        nextn = r + 1 < nr ? (MCK_BLK_RS_CACHE && r + 1 <= 3 ? (r == 1 ? rs2 : rs3) : rd.u32(ro + 4 * (r + 1)))
+                           : 0xFFFFFFFFu;
       }
       const uint4 Uc = wok ? lds_row_u4(s_win[threadIdx.x], 0) : U;
       bool fast = false;
@@ -1150,12 +1168,17 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
         else
           hv ^= xp_short(rd, v, vl, kSeedV);
       }
-      if (idx & 1)  // entries idx - 1, idx as one 16-byte store (half the divergent stores)
-        *reinterpret_cast<__attribute__((address_space(1))) span_u32x4*>(
-            reinterpret_cast<uint64_t>(slot_h + sbase + idx - 1)) =
-            span_u32x4{(uint32_t)pend, (uint32_t)(pend >> 32), (uint32_t)hv, (uint32_t)(hv >> 32)};
-      else if (v + vl >= ro)  // the block's last entry, even
+      if (idx & 1) {  // entries idx - 1, idx as one 16-byte store (half the divergent stores)
+        const span_u32x4 pr{(uint32_t)pend, (uint32_t)(pend >> 32), (uint32_t)hv, (uint32_t)(hv >> 32)};
+        auto* dst = reinterpret_cast<__attribute__((address_space(1))) span_u32x4*>(
+            reinterpret_cast<uint64_t>(slot_h + sbase + idx - 1));
+        if constexpr (MCK_BLK_SLOT_NT)
+          __builtin_nontemporal_store(pr, dst);
+        else
+          *dst = pr;
+      } else if (v + vl >= ro) {  // the block's last entry, even
         slot_h[sbase + idx] = hv;
+      }
       pend = hv;
       if (lng) {
         slot_m[sbase + idx] = (uint64_t)v << 32 | vl;
