@@ -879,6 +879,24 @@ __host__ __device__ __forceinline__ uint32_t blk_slot_stride(uint32_t slot_cap) 
 __host__ __device__ __forceinline__ uint32_t blk_long_words(uint32_t slot_cap) {
   return (blk_slot_stride(slot_cap) + 31) / 32;
 }
+// Where entry e of block b's slot lives.  MCK_BLK_SLOT_T (round 6): the 64
+// blocks of a wave (b >> 6; the walk's lane is b & 63) keep entry e side by
+// side, so the walk's per-entry store -- every active lane is at the same
+// entry index -- is one coalesced 512-byte row per wave; block-major slots
+// (b * stride + e) were 16-byte pair stores, 64 lines per instruction, each
+// line completed over ~16 entries: 0.62 GB written for 0.28 GB of slots at
+// 100-B values and a partly written line per lane in L2 beside the window
+// lines the walk re-reads.  The slot area holds count rounded up to 64.
+#ifndef MCK_BLK_SLOT_T
+#define MCK_BLK_SLOT_T 1
+#endif
+__host__ __device__ __forceinline__ uint64_t blk_slot_at(uint32_t b, uint32_t e, uint32_t stride) {
+  if (MCK_BLK_SLOT_T) return ((uint64_t)(b >> 6) * stride + e) * 64 + (b & 63);
+  return (uint64_t)b * stride + e;
+}
+__host__ __device__ __forceinline__ uint64_t blk_slot_count(uint32_t count) {
+  return MCK_BLK_SLOT_T ? ((uint64_t)count + 63) & ~63ull : count;
+}
 
 // ---- entry windows (round 5) ----------------------------------------------
 // The walk's divergent loads -- each entry's 16-byte head (U), its key's
@@ -901,7 +919,7 @@ constexpr uint32_t kBlkWin = 128, kBlkWinRow = 36;
 #define MCK_BLK_SLOT_NT 0
 #endif
 #ifndef MCK_BLK_RS_CACHE
-#define MCK_BLK_RS_CACHE 0
+#define MCK_BLK_RS_CACHE 1
 #endif
 __device__ __forceinline__ uint4 lds_row_u4(const uint32_t* w, uint32_t o) {  // 16 bytes at byte o
   const uint32_t i = o >> 2, sb = o & 3u;
@@ -1017,7 +1035,8 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
   uint8_t* const gkey = arena + (uint64_t)(in ? b : 0) * arena_cap;
   bool global_key = false;
   const uint64_t oklo = sec64(16 * (int)(lane & 7)) + kSeedV, okhi = sec64(16 * (int)(lane & 7) + 8) - kSeedV;
-  const uint64_t sbase = (uint64_t)(in ? b : 0) * blk_slot_stride(slot_cap);
+  const uint32_t sstride = blk_slot_stride(slot_cap);
+  const uint64_t sbase = (uint64_t)(in ? b : 0) * sstride;
   uint64_t pend = 0;  // the lane's even entry, stored with the odd one after it
   uint32_t lmask = 0;  // long entries of the current 32
   uint32_t* const lwords = blk_long + (uint64_t)(in ? b : 0) * blk_long_words(slot_cap);
@@ -1168,7 +1187,9 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
         else
           hv ^= xp_short(rd, v, vl, kSeedV);
       }
-      if (idx & 1) {  // entries idx - 1, idx as one 16-byte store (half the divergent stores)
+      if (MCK_BLK_SLOT_T) {
+        slot_h[blk_slot_at(b, idx, sstride)] = hv;
+      } else if (idx & 1) {  // entries idx - 1, idx as one 16-byte store (half the divergent stores)
         const span_u32x4 pr{(uint32_t)pend, (uint32_t)(pend >> 32), (uint32_t)hv, (uint32_t)(hv >> 32)};
         auto* dst = reinterpret_cast<__attribute__((address_space(1))) span_u32x4*>(
             reinterpret_cast<uint64_t>(slot_h + sbase + idx - 1));
@@ -1181,7 +1202,7 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
       }
       pend = hv;
       if (lng) {
-        slot_m[sbase + idx] = (uint64_t)v << 32 | vl;
+        slot_m[MCK_BLK_SLOT_T ? blk_slot_at(b, idx, sstride) : sbase + idx] = (uint64_t)v << 32 | vl;
         lmask |= 1u << (idx & 31);
       }
       if ((idx & 31) == 31 || v + vl >= ro) {
@@ -1213,15 +1234,14 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
 // key): thread t moves slot pair t of the flattened slot array, 4 pairs per
 // thread (a wave per block ran into the dispatcher: 0.27 ms at 1M blocks).
 template <bool VERIFY>
-__device__ __forceinline__ void blk_flush_one(SpanSrc blocks, uint32_t stride, uint32_t j, const uint64_t* slot_h,
+__device__ __forceinline__ void blk_flush_one(SpanSrc blocks, uint32_t stride, uint32_t b, uint32_t i,
+                                              const uint64_t* slot_h,
                                               const uint64_t* slot_m, const uint32_t* blk_long,
                                               const uint64_t* key_base, const uint64_t* prot_base, uint64_t kcap,
                                               uint32_t prot_bytes, bool p8, uint8_t* enc,
                                               const uint8_t* stored, uint8_t* mismatch, uint32_t* mismatch_count,
                                               uint64_t* long_off, uint32_t* long_len, uint64_t* long_part,
                                               bool batch_long) {
-  const uint32_t hs = stride >> 1;
-  const uint32_t b = j / hs, i = 2 * (j - b * hs);
   uint64_t k0 = ldg_u64(key_base, b);
   const uint64_t cnt = ldg_u64(key_base, b + 1) - k0;
   if (i >= cnt) return;
@@ -1232,10 +1252,14 @@ __device__ __forceinline__ void blk_flush_one(SpanSrc blocks, uint32_t stride, u
     k0 = ldg_u64(prot_base, b);
     if (ldg_u64(prot_base, b + 1) - k0 != cnt || k0 > kcap || cnt > kcap - k0) return;
   }
-  const uint64_t s0 = (uint64_t)b * stride + i;
+  const uint64_t s0 = blk_slot_at(b, i, stride);
+  const uint64_t s1 = blk_slot_at(b, i + 1, stride);
   const bool two = i + 1 < cnt;
   uint64_t h[2];
-  if (two) {
+  if (MCK_BLK_SLOT_T) {
+    h[0] = slot_h[s0];
+    h[1] = two ? slot_h[s1] : 0;
+  } else if (two) {
     const span_u32x4 v = *reinterpret_cast<__attribute__((address_space(1))) const span_u32x4*>(
         reinterpret_cast<uint64_t>(slot_h + s0));
     h[0] = (uint64_t)v.y << 32 | v.x;
@@ -1251,7 +1275,7 @@ __device__ __forceinline__ void blk_flush_one(SpanSrc blocks, uint32_t stride, u
   for (int e = 0; e < 2; e++) {
     if (e == 1 && !two) break;
     const uint64_t k = k0 + i + e;
-    const uint64_t m = (lm >> e) & 1u ? slot_m[s0 + e] : 0ull;  // (unwritten for short values)
+    const uint64_t m = (lm >> e) & 1u ? slot_m[e ? s1 : s0] : 0ull;  // (unwritten for short values)
     const uint32_t vl = (uint32_t)m;
     if (batch_long) long_len[k] = vl;  // (no long value in the batch: the sweep exits on the flag)
     if (vl) {
@@ -1283,15 +1307,37 @@ __global__ __launch_bounds__(256) void k_block_kv_flush(SpanSrc blocks, uint32_t
                                                         uint64_t* long_part, const uint32_t* long_flag) {
   const bool p8 = prot_bytes == 8 && (reinterpret_cast<uint64_t>(enc) & 7) == 0;
   const bool batch_long = *long_flag != 0;
+  const uint32_t hs = stride >> 1;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (MCK_BLK_SLOT_T) {
+    // wave-interleaved slots: lane l of a wave takes block 64 c + l, the
+    // wave's q-th group of 4 pairs (entries 8 q .. 8 q + 7): every slot load
+    // reads one contiguous 512-byte row, and the 4 waves of a workgroup write
+    // 32 consecutive entries (two whole output lines) of each of 64 blocks
+    const uint32_t nb = npairs / hs, qn = (hs + 3) >> 2;
+    const uint64_t r = t >> 6;
+    const uint32_t q = (uint32_t)(r % qn);
+    const uint64_t b = (r / qn) * 64 + (t & 63);
+    if (b >= nb) return;
+#pragma unroll
+    for (uint32_t u = 0; u < 4; u++) {
+      const uint32_t pi = 4 * q + u;
+      if (pi < hs)
+        blk_flush_one<VERIFY>(blocks, stride, (uint32_t)b, 2 * pi, slot_h, slot_m, blk_long, key_base, prot_base,
+                              kcap, prot_bytes, p8, enc, stored, mismatch, mismatch_count, long_off, long_len,
+                              long_part, batch_long);
+    }
+    return;
+  }
   const uint32_t g = gridDim.x * blockDim.x;
-  const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
 #pragma unroll
   for (uint32_t u = 0; u < 4; u++) {
     const uint64_t j = t + (uint64_t)u * g;
-    if (j < npairs)
-      blk_flush_one<VERIFY>(blocks, stride, (uint32_t)j, slot_h, slot_m, blk_long, key_base, prot_base, kcap,
-                            prot_bytes, p8, enc, stored, mismatch, mismatch_count, long_off, long_len, long_part,
-                            batch_long);
+    if (j < npairs) {
+      const uint32_t b = (uint32_t)(j / hs), i = 2 * (uint32_t)(j - (uint64_t)b * hs);
+      blk_flush_one<VERIFY>(blocks, stride, b, i, slot_h, slot_m, blk_long, key_base, prot_base, kcap, prot_bytes,
+                            p8, enc, stored, mismatch, mismatch_count, long_off, long_len, long_part, batch_long);
+    }
   }
 }
 

@@ -597,7 +597,7 @@ BlkBlocksWork blk_blocks_work(void* work, uint32_t count, uint32_t slot_cap, uin
   o += up(16 * blk_tiles(count) + 64);
   r.flag = reinterpret_cast<uint32_t*>(w + o);
   o += 256;
-  const uint64_t S = (uint64_t)count * blk_slot_stride(slot_cap);
+  const uint64_t S = blk_slot_count(count) * blk_slot_stride(slot_cap);
   r.slot_h = reinterpret_cast<uint64_t*>(w + o);
   o += up(8 * S);
   r.slot_m = reinterpret_cast<uint64_t*>(w + o);
@@ -655,7 +655,7 @@ int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32
     set_err("restart_interval/status/work/out is NULL");
     return MCK_EINVAL;
   }
-  if (slot_cap == 0 || (uint64_t)n * blk_slot_stride(slot_cap) > 0xFFFFFFFFull) {
+  if (slot_cap == 0 || blk_slot_count(n) * blk_slot_stride(slot_cap) > 0xFFFFFFFFull) {
     set_err("slot_cap must be >= 1 with count * slot_cap < 2^32 (got %u x %u)", n, slot_cap);
     return MCK_EINVAL;
   }
@@ -682,7 +682,10 @@ int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32
   if (int rc = current_device(nullptr, &ncu)) return rc;
   const uint32_t stride = blk_slot_stride(slot_cap);
   const uint32_t npairs = n * (stride / 2);
-  const uint32_t fgrid = (uint32_t)(((uint64_t)npairs + 4 * 256 - 1) / (4 * 256));  // 4 pairs per thread
+  // 4 pairs per thread (wave-interleaved slots: a thread per block and
+  // group of 4 pairs, blocks in whole 64-block chunks)
+  const uint64_t fthreads = MCK_BLK_SLOT_T ? blk_slot_count(n) * ((stride / 2 + 3) / 4) : ((uint64_t)npairs + 3) / 4;
+  const uint32_t fgrid = (uint32_t)((fthreads + 255) / 256);
   const uint64_t kcap = verify ? total_keys : K;
   const uint64_t* const kidx = verify ? prot_base : kb;  // the index the outputs are laid out by
   if (verify) {
