@@ -1310,23 +1310,22 @@ __global__ __launch_bounds__(256) void k_block_kv_flush(SpanSrc blocks, uint32_t
   const uint32_t hs = stride >> 1;
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (MCK_BLK_SLOT_T) {
-    // wave-interleaved slots: lane l of a wave takes block 64 c + l, the
-    // wave's q-th group of 4 pairs (entries 8 q .. 8 q + 7): every slot load
-    // reads one contiguous 512-byte row, and the 4 waves of a workgroup write
-    // 32 consecutive entries (two whole output lines) of each of 64 blocks
-    const uint32_t nb = npairs / hs, qn = (hs + 3) >> 2;
-    const uint64_t r = t >> 6;
-    const uint32_t q = (uint32_t)(r % qn);
-    const uint64_t b = (r / qn) * 64 + (t & 63);
-    if (b >= nb) return;
-#pragma unroll
-    for (uint32_t u = 0; u < 4; u++) {
-      const uint32_t pi = 4 * q + u;
-      if (pi < hs)
-        blk_flush_one<VERIFY>(blocks, stride, (uint32_t)b, 2 * pi, slot_h, slot_m, blk_long, key_base, prot_base,
-                              kcap, prot_bytes, p8, enc, stored, mismatch, mismatch_count, long_off, long_len,
-                              long_part, batch_long);
-    }
+    // wave-interleaved slots: workgroup c flushes the 64-block chunk c, its
+    // threads striding over the chunk's pairs block-major (consecutive
+    // threads, consecutive pairs of one block: coalesced output writes);
+    // every slot line (16 blocks' entry e) is read by this workgroup alone,
+    // so once from HBM (a pair per thread across workgroups split the lines
+    // over XCDs: 0.59 GB fetched for 0.28; lane-per-block writes scattered
+    // 16-byte pieces: 1.43 GB written for 0.28)
+    const uint32_t nb = npairs / hs, per = 64 * hs;
+    for (uint32_t c = blockIdx.x; (uint64_t)c * 64 < nb; c += gridDim.x)
+      for (uint32_t jl = threadIdx.x; jl < per; jl += blockDim.x) {
+        const uint32_t b = c * 64 + jl / hs;
+        if (b >= nb) break;
+        blk_flush_one<VERIFY>(blocks, stride, b, 2 * (jl % hs), slot_h, slot_m, blk_long, key_base, prot_base, kcap,
+                              prot_bytes, p8, enc, stored, mismatch, mismatch_count, long_off, long_len, long_part,
+                              batch_long);
+      }
     return;
   }
   const uint32_t g = gridDim.x * blockDim.x;

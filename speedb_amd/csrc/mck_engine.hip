@@ -682,10 +682,9 @@ int blk_kv_blocks(int kind, const mck_spans* blocks, uint32_t prot_bytes, uint32
   if (int rc = current_device(nullptr, &ncu)) return rc;
   const uint32_t stride = blk_slot_stride(slot_cap);
   const uint32_t npairs = n * (stride / 2);
-  // 4 pairs per thread (wave-interleaved slots: a thread per block and
-  // group of 4 pairs, blocks in whole 64-block chunks)
-  const uint64_t fthreads = MCK_BLK_SLOT_T ? blk_slot_count(n) * ((stride / 2 + 3) / 4) : ((uint64_t)npairs + 3) / 4;
-  const uint32_t fgrid = (uint32_t)((fthreads + 255) / 256);
+  // 4 pairs per thread (wave-interleaved slots: a workgroup per 64-block
+  // chunk)
+  const uint32_t fgrid = MCK_BLK_SLOT_T ? (uint32_t)((n + 63) / 64) : (uint32_t)(((uint64_t)npairs + 1023) / 1024);
   const uint64_t kcap = verify ? total_keys : K;
   const uint64_t* const kidx = verify ? prot_base : kb;  // the index the outputs are laid out by
   if (verify) {
