@@ -14,6 +14,7 @@ B="timeout -k 10 240 python -u bench.py"
 $B > $O/crc32c.json || exit 1
 for wl in xxh3 sst wal kv file walwrite blob blockkv walrec; do $B --workload $wl --cpu-seconds 0 > $O/$wl.json || exit 1; done
 $B --workload blockkv --kv-value-bytes 100 --cpu-seconds 0 > $O/blockkv100.json || exit 1
+$B --workload kv --kv-value-bytes 100 --cpu-seconds 0 > $O/kv100.json || exit 1
 $B --workload ragged --span-min 100 --span-max 300 --cpu-seconds 0 > $O/r100.json || exit 1
 $B --workload ragged --span-min 4100 --span-max 4400 --cpu-seconds 0 > $O/r4100.json || exit 1
 $B --workload crc32c --blocks 1000000 --block-bytes 4300 --cpu-seconds 0 > $O/u4300.json || exit 1

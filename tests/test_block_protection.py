@@ -430,6 +430,35 @@ def test_block_protection_one_pass_equals_two_pass_many(gpu):
         assert torch.nonzero(mism).flatten().cpu().tolist() == bad
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("count", [1, 63, 64, 65, 129, 200])
+def test_block_protection_one_pass_chunk_edges(gpu, count):
+    """The one-pass walk keeps its slots interleaved by wave (entry e of a
+    wave's 64 blocks side by side, blk_slot_at) and the flush takes a
+    workgroup per 64-block chunk: batches of 1 block, around one and two
+    chunks, and a ragged last chunk agree with the two-pass pair on every
+    status, key base and checksum byte (blocks of 1..40 entries, restart
+    intervals 1..16, so walks end at different iterations)."""
+    import speedb_amd
+    from speedb_amd import block as B
+    torch = gpu
+    rnd = random.Random(count)
+    blocks = []
+    for i in range(count):
+        ri = rnd.choice((1, 3, 16))
+        blocks.append(build_block(data_block(rnd, rnd.randrange(1, 41), ri, 0, 130 if i % 5 else 400), ri))
+    base, offs, lens = _pack(torch, blocks, rnd)
+    spans = speedb_amd.Spans(base, len(blocks), offs, lens)
+    for p in (1, 8):
+        one = B.InitializeBlockProtectionInfoOnePass(DATA, spans, p, slot_cap=64, arena_cap=512)
+        two = B.InitializeBlockProtectionInfo(DATA, spans, p, one_pass=False)
+        assert one.status.cpu().tolist() == two.status.cpu().tolist()
+        assert one.key_base.cpu().tolist() == two.key_base.cpu().tolist()
+        assert torch.equal(one.kv_checksum, two.kv_checksum)
+        mism, cnt = B.VerifyBlockProtectionInfo(spans, one, one.kv_checksum.clone())
+        assert int(cnt.item()) == 0
+
+
 def _corrupt_cases(rnd, blocks):
     """Block-data corruptions: (block index, new bytes, whole)
     -- whole: the block no longer walks to its protect-time entry count, so
