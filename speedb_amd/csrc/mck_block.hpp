@@ -1188,7 +1188,10 @@ __global__ __launch_bounds__(256) void k_block_kv_walk(SpanSrc blocks, uint32_t 
           hv ^= xp_short(rd, v, vl, kSeedV);
       }
       if (MCK_BLK_SLOT_T) {
-        slot_h[blk_slot_at(b, idx, sstride)] = hv;
+        if constexpr (MCK_BLK_SLOT_NT)  // (whole rows: streamed out, not parked in L2)
+          __builtin_nontemporal_store(hv, &slot_h[blk_slot_at(b, idx, sstride)]);
+        else
+          slot_h[blk_slot_at(b, idx, sstride)] = hv;
       } else if (idx & 1) {  // entries idx - 1, idx as one 16-byte store (half the divergent stores)
         const span_u32x4 pr{(uint32_t)pend, (uint32_t)(pend >> 32), (uint32_t)hv, (uint32_t)(hv >> 32)};
         auto* dst = reinterpret_cast<__attribute__((address_space(1))) span_u32x4*>(
